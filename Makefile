@@ -1,0 +1,34 @@
+# Build of the MI355X topic-routing engine (gfx950 only) and its test oracle.
+#   emqx_amd/libtopicmatch.so  product: C-ABI + HIP kernels (hipcc, gfx950)
+#   emqx_amd/libtmwork.so      synthetic workload generator (bench/test input)
+#   oracle/liboracle.so        CPU restatement of the reference (checker only)
+HIPCC   ?= /opt/rocm/bin/hipcc
+ARCH    ?= gfx950
+CC      ?= gcc
+HIPFLAGS = --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -Wall -Wno-unused-result
+BUILD   := build
+
+all: emqx_amd/libtopicmatch.so emqx_amd/libtmwork.so oracle/liboracle.so
+
+$(BUILD):
+	mkdir -p $(BUILD)
+
+$(BUILD)/kernels.o: emqx_amd/csrc/kernels.hip emqx_amd/csrc/kernels.h emqx_amd/csrc/image.h | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(BUILD)/engine.o: emqx_amd/csrc/engine.cpp emqx_amd/csrc/kernels.h emqx_amd/csrc/image.h include/topicmatch.h | $(BUILD)
+	$(HIPCC) -O3 -fPIC -std=c++17 -Wall -c $< -o $@
+
+emqx_amd/libtopicmatch.so: $(BUILD)/kernels.o $(BUILD)/engine.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -o $@
+
+emqx_amd/libtmwork.so: emqx_amd/csrc/workload.c
+	$(CC) -O2 -fPIC -shared -Wall $< -o $@ -lm
+
+oracle/liboracle.so: oracle/o1_trie.c
+	$(CC) -O2 -fPIC -shared -Wall $< -o $@ -lpthread
+
+clean:
+	rm -rf $(BUILD) emqx_amd/libtopicmatch.so emqx_amd/libtmwork.so oracle/liboracle.so
+
+.PHONY: all clean

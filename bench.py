@@ -1,0 +1,191 @@
+"""bench.py — topic matches/sec at 10M wildcard filters on MI355X.
+
+One step = one batch of publish topics (bytes + offsets already resident in
+HBM) through the whole hot path of emqx_trie:match/1: device tokenizer
+(emqx_topic:words/1), NFA walk, CSR emission of the ordered match lists.
+
+Workload: 10M distinct wildcard filters (8 levels max,
+p+ 0.20, p# 0.05, Zipf(1.0) words over 16/64/256/1024/4096x4), replicated on
+every GPU; each rank matches its own batch of 8-level topics (weak scaling,
+no collective on the data path).  `value` = topics matched per second over all
+ranks (max-over-ranks step time).
+
+Run: python bench.py [--gpus N --steps K --warmup W]
+     torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from emqx_amd import Engine  # noqa: E402
+from emqx_amd import workload as W  # noqa: E402
+
+METRIC = "topic matches/sec (whole node) at 10M wildcard filters; % HBM roofline"
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak, /opt/skills/guides/MI355X_MICROARCH.md
+
+
+def log(*a):
+    print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", type=int, default=3, help="SURVEY §8(d) config (3 = the metric's)")
+    ap.add_argument("--filters", type=int, default=None, help="override filter count")
+    ap.add_argument("--topics", type=int, default=2_000_000, help="topics per GPU per step")
+    ap.add_argument("--cpu-sample", type=int, default=200_000, help="topics timed on the host (0 = skip)")
+    ap.add_argument("--cpu-threads", type=int, default=None)
+    ap.add_argument("--check", type=int, default=20_000, help="topics checked bit-exactly vs the oracle")
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    if world > 1:
+        dist.init_process_group("nccl" if torch.cuda.is_available() else "gloo")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    cfg = W.CONFIGS[a.config]
+    n_filters = a.filters or cfg["filters"]
+    t0 = time.time()
+    fb, fo = W.filters(a.config, n=n_filters)
+    log("rank %d: generated %d filters (%.1f MB) in %.1fs" % (rank, n_filters, fo[-1] / 1e6, time.time() - t0))
+    t0 = time.time()
+    eng = Engine(device=local, filters_hint=n_filters)
+    eng.insert_many(fb, fo)
+    eng.commit()
+    log("rank %d: trie built + committed in %.1fs: %d filters, %d nodes, image %.2f GB" % (
+        rank, time.time() - t0, eng.filter_count, eng.node_count, eng.image_bytes / 1e9))
+
+    tb, to = W.topics(a.config, n=a.topics, stream=rank)
+    n = len(to) - 1
+    nbytes = int(to[-1])
+    d_b = torch.from_numpy(tb).to(dev)
+    d_o = torch.from_numpy(to.view(np.int64)).to(dev)
+    d_c = torch.empty(n, dtype=torch.int32, device=dev)
+    d_oo = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    d_t = torch.zeros(1, dtype=torch.int64, device=dev)
+    st = torch.cuda.current_stream(dev)
+
+    # size the output from one counting pass (untimed), with exact stats
+    eng.set_stats(True)
+    eng.match_batch_device(d_b, d_o, n, nbytes, d_c, d_oo, None, 0, d_t, stream=st)
+    torch.cuda.synchronize(dev)
+    stats = eng.last_stats()
+    eng.set_stats(False)
+    total = int(d_t.item())
+    cap = total + 1024
+    d_i = torch.empty(cap, dtype=torch.int32, device=dev)
+
+    def step():
+        eng.match_batch_device(d_b, d_o, n, nbytes, d_c, d_oo, d_i, cap, d_t, stream=st)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+
+    # ---- timed region: K steps, kernel events recorded on the launch stream
+    eng.set_timing(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t_start = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t_start
+    kms = eng.last_kernel_times()
+    eng.set_timing(False)
+    if world > 1:
+        tt = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    assert int(d_t.item()) == total, "match total changed between steps"
+
+    # ---- bit-exact spot check of this rank's batch against the oracle
+    check_ok = None
+    o1 = None
+    cpu = None
+    if rank == 0 and (a.check > 0 or (world == 1 and a.cpu_sample > 0)):
+        from oracle import O1   # checker / CPU baseline only
+        t0 = time.time()
+        o1 = O1(n_filters)
+        o1.insert_many(fb, fo)
+        log("oracle O1 built in %.1fs (%d nodes)" % (time.time() - t0, o1.node_count))
+        threads = a.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count())
+        if a.check > 0:
+            k = min(a.check, n)
+            ksub = to[: k + 1]
+            oc, oo, oi = o1.match_ids(tb, ksub, threads=threads)
+            dc = d_c[:k].cpu().numpy().view(np.uint32)
+            doo = d_oo[: k + 1].cpu().numpy().view(np.uint64)
+            di = d_i[: int(doo[-1])].cpu().numpy().view(np.uint32)
+            check_ok = bool(np.array_equal(dc, oc) and np.array_equal(doo, oo) and np.array_equal(di, oi))
+            log("bit-exact check of %d topics vs O1: %s" % (k, check_ok))
+        if world == 1 and a.cpu_sample > 0:
+            k = min(a.cpu_sample, n)
+            secs, m, e = o1.match_batch(tb, to[: k + 1], threads=threads)
+            cpu = {"value": k / secs, "unit": "topics/s", "cores": threads, "kind": "port",
+                   "sample": "%d topics of the same batch against the same 10M-filter trie, C restatement "
+                             "of emqx_trie (string-path ids, ETS-like tables), %d pthreads, %.1f s" % (k, threads, secs)}
+            log("cpu baseline: %.0f topics/s on %d threads" % (k / secs, threads))
+
+    if rank == 0:
+        topics_per_s = n * a.steps * world / dt
+        levels = stats["levels"]
+        B = 8 * levels + 16 * stats["edge_reads"] + 4 * stats["matches"]   # SURVEY §8(d), per launch
+        walk_ms = kms.get("match_emit", 0.0)
+        achieved = B / (walk_ms * 1e-3) / 1e9 if walk_ms > 0 else None
+        out = {
+            "metric": METRIC,
+            "value": topics_per_s,
+            "unit": "topics/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": dt / a.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic",
+            "config": {"workload": "C%d: %d distinct wildcard filters replicated per GPU, %d-level topics, "
+                                   "%d topics per GPU per step" % (a.config, n_filters, cfg["levels"], n),
+                       "filters": n_filters, "topics_per_gpu_step": n, "levels": cfg["levels"],
+                       "parallelism": "replicated trie x %d, topic batches sharded by rank" % world},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": None,
+                         "kernel": "tm_match<EMIT> (NFA walk + ordered emission)",
+                         "algorithmic_bytes_per_launch": B,
+                         "per_topic": {"n": levels / n, "E": stats["edge_reads"] / n, "M": stats["matches"] / n}},
+            "cpu_baseline": cpu,
+            "kernel_ms": kms,
+            "filter_hits_per_s": stats["matches"] * a.steps * world / dt,
+            "parity_check": check_ok,
+        }
+        print(json.dumps(out), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,110 @@
+"""ctypes binding of libtopicmatch (include/topicmatch.h).
+
+This is the Python analogue of the reference-side NIF binding
+(emqx_amd/csrc/emqx_trie_nif.c).  Loading fails loudly when
+the in-tree library has not been built: there is no CPU fallback for the
+match path.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libtopicmatch.so")
+
+TM_OK, TM_EINVAL, TM_ENOSPC, TM_EDEVICE, TM_ENOMEM, TM_ENOENT, TM_ERANGE = 0, -1, -2, -3, -4, -5, -6
+TM_NO_FILTER = 0xFFFFFFFF
+
+c_u8p = ctypes.POINTER(ctypes.c_uint8)
+c_u32p = ctypes.POINTER(ctypes.c_uint32)
+c_u64p = ctypes.POINTER(ctypes.c_uint64)
+
+
+class TmConfig(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int32), ("reserved0", ctypes.c_uint32),
+                ("filters_hint", ctypes.c_uint64), ("batch_topics", ctypes.c_uint64),
+                ("batch_bytes", ctypes.c_uint64)]
+
+
+class TmNodeInfo(ctypes.Structure):
+    _fields_ = [("edge_count", ctypes.c_uint32), ("filter_id", ctypes.c_uint32)]
+
+
+class TmBatchStats(ctypes.Structure):
+    _fields_ = [("topics", ctypes.c_uint64), ("levels", ctypes.c_uint64),
+                ("visits", ctypes.c_uint64), ("edge_reads", ctypes.c_uint64),
+                ("matches", ctypes.c_uint64)]
+
+
+# (name, restype, argtypes) — every symbol include/topicmatch.h declares
+SIGNATURES = [
+    ("tm_open", ctypes.c_int, [ctypes.POINTER(TmConfig), ctypes.POINTER(ctypes.c_void_p)]),
+    ("tm_close", None, [ctypes.c_void_p]),
+    ("tm_strerror", ctypes.c_char_p, [ctypes.c_int]),
+    ("tm_last_error", ctypes.c_char_p, [ctypes.c_void_p]),
+    ("tm_insert", ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint32]),
+    ("tm_insert_batch", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32]),
+    ("tm_delete", ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint32]),
+    ("tm_lookup", ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.POINTER(TmNodeInfo)]),
+    ("tm_commit", ctypes.c_int, [ctypes.c_void_p, c_u64p]),
+    ("tm_filter_count", ctypes.c_uint64, [ctypes.c_void_p]),
+    ("tm_node_count", ctypes.c_uint64, [ctypes.c_void_p]),
+    ("tm_image_bytes", ctypes.c_uint64, [ctypes.c_void_p]),
+    ("tm_filter_bytes", ctypes.c_void_p, [ctypes.c_void_p, ctypes.c_uint32, c_u32p]),
+    ("tm_match_batch", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                      c_u64p]),
+    ("tm_match_batch_device", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                             ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                             ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]),
+    ("tm_set_stats", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    ("tm_last_stats", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(TmBatchStats)]),
+    ("tm_set_timing", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    ("tm_last_kernel_times", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_char_p),
+                                            ctypes.POINTER(ctypes.c_float), ctypes.c_int]),
+    ("tm_topic_match", ctypes.c_int, [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_uint32]),
+    ("tm_topic_wildcard", ctypes.c_int, [ctypes.c_char_p, ctypes.c_uint32]),
+    ("tm_topic_parse", ctypes.c_int, [ctypes.c_char_p, ctypes.c_uint32, ctypes.POINTER(ctypes.c_void_p), c_u32p,
+                                      ctypes.POINTER(ctypes.c_void_p), c_u32p]),
+    ("tm_build_info", ctypes.c_char_p, []),
+]
+
+_lib = None
+
+
+class TopicMatchError(RuntimeError):
+    def __init__(self, code, msg=""):
+        self.code = code
+        super().__init__("%s (%d)%s" % (_strerror(code), code, (": " + msg) if msg else ""))
+
+
+def _strerror(code):
+    try:
+        return load().tm_strerror(code).decode()
+    except Exception:  # pragma: no cover
+        return "status"
+
+
+def load():
+    """Load libtopicmatch.so from the package directory (never from a
+    site-packages copy) and bind every exported symbol.  Raises ImportError
+    if it was not built — the match path has no fallback."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    # torch wheels bundle their own libamdhip64.so.7; when torch is present,
+    # load it first so this library binds to the SAME HIP runtime (one HSA
+    # context per process, device pointers and streams shared with torch).
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
+    if not os.path.exists(LIB_PATH):
+        raise ImportError("libtopicmatch.so not built at %s: run `make` (or __graft_entry__.build()); "
+                          "the HIP match path has no CPU fallback" % LIB_PATH)
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, res, args in SIGNATURES:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib

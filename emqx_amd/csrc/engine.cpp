@@ -1,0 +1,1032 @@
+// engine.cpp — host side of libtopicmatch: the C-ABI (include/topicmatch.h),
+// the subscription-trie host mirror with emqx_trie's bookkeeping, the word
+// dictionary, and the HBM image it commits to the device.
+//
+// Reference semantics (vus520/emqx @ 3.0-rc.3):
+//   insert/1      src/emqx_trie.erl:62-73, add_path/1 :104-117
+//   delete/1      src/emqx_trie.erl:88-96, delete_path/1 :149-163
+//   lookup/1      src/emqx_trie.erl:83-84
+//   match/1       src/emqx_trie.erl:77-79, 121-145 (device: kernels.hip)
+//   words/1       src/emqx_topic.erl:141-147 (device tokenizer)
+//   match/2, wildcard/1, parse/1,2   src/emqx_topic.erl:41-75, 180-200
+//
+// The host mirror IS the host copy of the device image (image.h): inserts and
+// deletes patch it in place and mark 64 KiB pages dirty; tm_commit uploads
+// the dirty pages (or the whole table after a resize) on the engine stream.
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/topicmatch.h"
+#include "image.h"
+#include "kernels.h"
+
+using namespace tmx;
+
+namespace {
+
+constexpr size_t PAGE_ELEMS = 4096;  // 4096 x 16 B = 64 KiB dirty granule
+
+struct DevError : std::runtime_error {
+    using std::runtime_error::runtime_error;
+};
+struct ArgError : std::runtime_error {
+    using std::runtime_error::runtime_error;
+};
+struct RangeError : std::runtime_error {
+    using std::runtime_error::runtime_error;
+};
+
+#define HIPCHK(x)                                                                       \
+    do {                                                                                \
+        hipError_t _e = (x);                                                            \
+        if (_e != hipSuccess)                                                           \
+            throw DevError(std::string(#x) + ": " + hipGetErrorString(_e));             \
+    } while (0)
+
+// ---- word hashing, identical to the device tokenizer (image.h) --------------
+uint64_t word_hash(const uint8_t* p, uint32_t len) {
+    uint64_t h = 0x243F6A8885A308D3ULL;
+    for (uint32_t i = 0; i < len; i += 8) {
+        uint32_t k = std::min<uint32_t>(8, len - i);
+        uint64_t c = 0;
+        std::memcpy(&c, p + i, k);  // little-endian host (x86_64)
+        h = word_hash_step(h, c);
+    }
+    return word_hash_final(h, len);
+}
+
+size_t next_pow2(size_t x) {
+    size_t p = 1;
+    while (p < x) p <<= 1;
+    return p;
+}
+
+// dirty-page bitmap over a table of 16 B elements
+struct Dirty {
+    std::vector<uint8_t> pages;
+    bool all = true;  // whole table must be (re)uploaded
+    void mark(size_t idx) {
+        size_t pg = idx / PAGE_ELEMS;
+        if (pg >= pages.size()) pages.resize(pg + 1, 0);
+        pages[pg] = 1;
+    }
+    void clear() {
+        std::fill(pages.begin(), pages.end(), 0);
+        all = false;
+    }
+};
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    // grow to at least `need` bytes (contents not preserved); true if reallocated
+    bool ensure(size_t need, double slack = 1.25) {
+        if (need <= bytes && p) return false;
+        release();
+        size_t want = std::max<size_t>(256, (size_t)(need * slack));
+        hipError_t e = hipMalloc(&p, want);
+        if (e != hipSuccess) {
+            p = nullptr;
+            throw DevError(std::string("hipMalloc(") + std::to_string(want) + "): " + hipGetErrorString(e));
+        }
+        bytes = want;
+        return true;
+    }
+    template <class T>
+    T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+struct NodeAux {
+    uint32_t parent;      // parent node id (root: NODE_NONE)
+    uint32_t word;        // word by which the parent reaches it (id, WORD_PLUS, WORD_HASH)
+    uint32_t edge_count;  // #trie_node.edge_count
+    uint32_t lit_count;   // literal children (HAS_LIT flag <=> lit_count > 0)
+};
+
+struct FilterRec {
+    uint64_t off;   // into filter arena
+    uint32_t len;
+    uint32_t node;  // NODE_NONE when the id is free
+};
+
+struct KTimes {
+    const char* name;
+    hipEvent_t a, b;
+};
+constexpr int N_KERNEL_SLOTS = 4;   // tokenize, match_count, scan, match_emit
+
+}  // namespace
+
+struct tm_engine {
+    std::recursive_mutex mu;
+    int device = -1;
+    hipStream_t stream = nullptr;
+    std::string last_error;
+    uint64_t epoch = 0;
+
+    // ---- word dictionary (host copy of dict/word_arena/word_off) ----
+    std::vector<DictSlot> dict;
+    size_t dict_used = 0;
+    std::vector<uint8_t> word_arena;   // 8-aligned, zero-padded words
+    std::vector<uint32_t> word_off;
+    Dirty dict_dirty;
+    size_t arena_uploaded = 0, woff_uploaded = 0;
+
+    // ---- trie mirror / image ----
+    std::vector<Node> nodes;
+    std::vector<NodeAux> aux;
+    std::vector<uint32_t> free_nodes;
+    size_t live_nodes = 0;
+    std::vector<EdgeSlot> edges;
+    size_t edge_used = 0;
+    Dirty node_dirty, edge_dirty;
+
+    // ---- filter registry ----
+    std::vector<uint8_t> filter_arena;
+    std::vector<FilterRec> filters;
+    std::vector<uint32_t> free_filters;
+    size_t live_filters = 0;
+
+    // ---- device image ----
+    DevBuf d_nodes, d_edges, d_dict, d_arena, d_woff;
+    bool dev_dirty = true;
+
+    // ---- match workspace ----
+    DevBuf w_bytes, w_off, w_words, w_meta, w_counts, w_outoff, w_ids, w_scan, w_total, w_path, w_stats;
+    hipEvent_t last_match_done = nullptr;
+    bool match_in_flight = false;
+    bool stats_enabled = false, timing_enabled = false;
+    tm_batch_stats last_stats{};
+    // per-batch event records, accumulated until tm_last_kernel_times()
+    std::vector<KTimes> ev_pool;          // recycled events
+    std::vector<KTimes> ev_pending;       // recorded, not yet read
+    KTimes ev_cur[N_KERNEL_SLOTS];
+    bool ev_open[N_KERNEL_SLOTS] = {false, false, false, false};
+
+    // scratch for words of one filter
+    std::vector<uint32_t> tmp_words;
+
+    tm_engine() {
+        dict.assign(1024, DictSlot{0, WORD_NONE, 0});
+        nodes.reserve(1024);
+        edges.assign(1024, EdgeSlot{EDGE_EMPTY, 0, 0, 0});
+        new_node(NODE_NONE, NODE_NONE);  // root = 0
+    }
+
+    // ------------------------------------------------------------------
+    // dictionary
+    uint32_t dict_find(const uint8_t* p, uint32_t len, uint64_t h) const {
+        size_t mask = dict.size() - 1;
+        for (size_t s = h & mask;; s = (s + 1) & mask) {
+            const DictSlot& d = dict[s];
+            if (d.word == WORD_NONE) return WORD_NONE;
+            if (d.hash == h && d.len == len && std::memcmp(&word_arena[word_off[d.word]], p, len) == 0)
+                return d.word;
+        }
+    }
+    void dict_place(uint64_t h, uint32_t id, uint32_t len) {
+        size_t mask = dict.size() - 1;
+        size_t s = h & mask;
+        while (dict[s].word != WORD_NONE) s = (s + 1) & mask;
+        dict[s] = DictSlot{h, id, len};
+        dict_dirty.mark(s);
+    }
+    void dict_grow() {
+        std::vector<DictSlot> old;
+        old.swap(dict);
+        dict.assign(old.size() * 2, DictSlot{0, WORD_NONE, 0});
+        for (const DictSlot& d : old)
+            if (d.word != WORD_NONE) dict_place(d.hash, d.word, d.len);
+        dict_dirty.all = true;
+    }
+    // word id of a level (interning it when `intern`)
+    uint32_t word_id(const uint8_t* p, uint32_t len, bool intern) {
+        if (len == 1 && p[0] == '+') return WORD_PLUS;
+        if (len == 1 && p[0] == '#') return WORD_HASH;
+        uint64_t h = word_hash(p, len);
+        uint32_t id = dict_find(p, len, h);
+        if (id != WORD_NONE || !intern) return id;
+        if (word_off.size() >= WORD_MAX) throw RangeError("word dictionary full");
+        id = (uint32_t)word_off.size();
+        size_t off = word_arena.size();
+        if (off > 0xFFFFFFF0ull) throw RangeError("word arena exceeds 4 GiB");
+        size_t padded = (len + 7) & ~size_t(7);
+        if (padded == 0) padded = 8;  // the empty word still owns one zero chunk
+        word_arena.resize(off + padded, 0);
+        if (len) std::memcpy(&word_arena[off], p, len);
+        word_off.push_back((uint32_t)off);
+        if ((dict_used + 1) * 2 > dict.size()) dict_grow();
+        dict_place(h, id, len);
+        ++dict_used;
+        return id;
+    }
+    // emqx_topic:words/1 (src/emqx_topic.erl:141-147): split on every '/',
+    // N slashes -> N+1 levels, empty levels kept.
+    bool split_words(const uint8_t* p, uint32_t len, bool intern) {
+        tmp_words.clear();
+        uint32_t s = 0;
+        for (uint32_t i = 0; i <= len; ++i) {
+            if (i == len || p[i] == '/') {
+                uint32_t w = word_id(p + s, i - s, intern);
+                if (w == WORD_NONE) return false;  // cannot be on any trie path
+                tmp_words.push_back(w);
+                s = i + 1;
+            }
+        }
+        return true;
+    }
+
+    // ------------------------------------------------------------------
+    // edges (open addressing, linear probing over 16 B slots from the home
+    // bucket's first slot; backward-shift deletion keeps probes tombstone-free)
+    size_t edge_find_slot(uint32_t parent, uint32_t word) const {
+        size_t mask = edges.size() - 1;
+        for (size_t s = edge_home(parent, word, mask);; s = (s + 1) & mask) {
+            const EdgeSlot& e = edges[s];
+            if (e.parent == EDGE_EMPTY) return SIZE_MAX;
+            if (e.parent == parent && e.word == word) return s;
+        }
+    }
+    void edge_place(const EdgeSlot& x) {
+        size_t mask = edges.size() - 1;
+        size_t s = edge_home(x.parent, x.word, mask);
+        while (edges[s].parent != EDGE_EMPTY) s = (s + 1) & mask;
+        edges[s] = x;
+        edge_dirty.mark(s);
+    }
+    void edge_grow() {
+        std::vector<EdgeSlot> old;
+        old.swap(edges);
+        edges.assign(old.size() * 2, EdgeSlot{EDGE_EMPTY, 0, 0, 0});
+        for (const EdgeSlot& e : old)
+            if (e.parent != EDGE_EMPTY) edge_place(e);
+        edge_dirty.all = true;
+    }
+    void edge_insert(uint32_t parent, uint32_t word, uint32_t child) {
+        if ((edge_used + 1) * 2 > edges.size()) edge_grow();
+        edge_place(EdgeSlot{parent, word, child, 0});
+        ++edge_used;
+    }
+    void edge_erase(uint32_t parent, uint32_t word) {
+        size_t i = edge_find_slot(parent, word);
+        if (i == SIZE_MAX) return;
+        size_t mask = edges.size() - 1;
+        size_t j = i;
+        for (;;) {
+            j = (j + 1) & mask;
+            if (edges[j].parent == EDGE_EMPTY) break;
+            size_t k = edge_home(edges[j].parent, edges[j].word, mask);
+            bool move = (i <= j) ? (k <= i || k > j) : (k <= i && k > j);
+            if (move) {
+                edges[i] = edges[j];
+                edge_dirty.mark(i);
+                i = j;
+            }
+        }
+        edges[i] = EdgeSlot{EDGE_EMPTY, 0, 0, 0};
+        edge_dirty.mark(i);
+        --edge_used;
+    }
+
+    // ------------------------------------------------------------------
+    // nodes
+    uint32_t new_node(uint32_t parent, uint32_t word) {
+        uint32_t id;
+        if (!free_nodes.empty()) {
+            id = free_nodes.back();
+            free_nodes.pop_back();
+        } else {
+            if (nodes.size() >= NODE_NONE) throw RangeError("trie exceeds 2^30-1 nodes");
+            id = (uint32_t)nodes.size();
+            nodes.push_back(Node{});
+            aux.push_back(NodeAux{});
+        }
+        nodes[id] = Node{NODE_NONE, NODE_NONE, FILTER_NONE, FILTER_NONE};
+        aux[id] = NodeAux{parent, word, 0, 0};
+        node_dirty.mark(id);
+        ++live_nodes;
+        return id;
+    }
+    uint32_t child(uint32_t v, uint32_t w) const {
+        if (w == WORD_PLUS) return nodes[v].plus & NODE_MASK;
+        if (w == WORD_HASH) return nodes[v].hash;
+        if (!(nodes[v].plus & HAS_LIT)) return NODE_NONE;
+        size_t s = edge_find_slot(v, w);
+        return s == SIZE_MAX ? NODE_NONE : edges[s].child;
+    }
+    // add_path/1 (emqx_trie.erl:104-117) for one (Node, Word, Child) triple:
+    // a new edge bumps the parent's edge_count.
+    uint32_t child_or_create(uint32_t v, uint32_t w) {
+        uint32_t c = child(v, w);
+        if (c != NODE_NONE) return c;
+        c = new_node(v, w);
+        if (w == WORD_PLUS) {
+            nodes[v].plus = (nodes[v].plus & HAS_LIT) | c;
+        } else if (w == WORD_HASH) {
+            nodes[v].hash = c;
+        } else {
+            edge_insert(v, w, c);
+            aux[v].lit_count++;
+            nodes[v].plus |= HAS_LIT;
+        }
+        aux[v].edge_count++;
+        node_dirty.mark(v);
+        return c;
+    }
+    void unlink_child(uint32_t c) {
+        uint32_t v = aux[c].parent, w = aux[c].word;
+        if (w == WORD_PLUS) {
+            nodes[v].plus = (nodes[v].plus & HAS_LIT) | NODE_NONE;
+        } else if (w == WORD_HASH) {
+            nodes[v].hash = NODE_NONE;
+            nodes[v].hash_filter = FILTER_NONE;
+        } else {
+            edge_erase(v, w);
+            if (--aux[v].lit_count == 0) nodes[v].plus &= ~HAS_LIT;
+        }
+        aux[v].edge_count--;
+        node_dirty.mark(v);
+        nodes[c] = Node{NODE_NONE, NODE_NONE, FILTER_NONE, FILTER_NONE};
+        aux[c] = NodeAux{NODE_NONE, 0, 0, 0};
+        node_dirty.mark(c);
+        free_nodes.push_back(c);
+        --live_nodes;
+    }
+    uint32_t walk(const std::vector<uint32_t>& ws) const {
+        uint32_t v = ROOT;
+        for (uint32_t w : ws) {
+            v = child(v, w);
+            if (v == NODE_NONE) return NODE_NONE;
+        }
+        return v;
+    }
+    // set/clear #trie_node.topic of node c (and the inline copy in the parent
+    // when c is a '#' child)
+    void set_topic(uint32_t c, uint32_t fid) {
+        nodes[c].self_filter = fid;
+        node_dirty.mark(c);
+        if (aux[c].word == WORD_HASH && aux[c].parent != NODE_NONE) {
+            nodes[aux[c].parent].hash_filter = fid;
+            node_dirty.mark(aux[c].parent);
+        }
+    }
+
+    // ------------------------------------------------------------------
+    // filters
+    uint32_t new_filter(const uint8_t* p, uint32_t len, uint32_t node) {
+        uint32_t id;
+        if (!free_filters.empty()) {
+            id = free_filters.back();
+            free_filters.pop_back();
+        } else {
+            if (filters.size() >= 0xFFFFFFF0ull) throw RangeError("filter ids exhausted");
+            id = (uint32_t)filters.size();
+            filters.push_back(FilterRec{});
+        }
+        uint64_t off = filter_arena.size();
+        filter_arena.insert(filter_arena.end(), p, p + len);
+        filters[id] = FilterRec{off, len, node};
+        ++live_filters;
+        return id;
+    }
+    void free_filter(uint32_t id) {
+        filters[id].node = NODE_NONE;
+        free_filters.push_back(id);
+        --live_filters;
+    }
+
+    // emqx_trie:insert/1 (src/emqx_trie.erl:62-73)
+    void insert(const uint8_t* p, uint32_t len) {
+        split_words(p, len, true);
+        uint32_t v = ROOT;
+        for (uint32_t w : tmp_words) v = child_or_create(v, w);
+        if (nodes[v].self_filter == FILTER_NONE) set_topic(v, new_filter(p, len, v));
+        dev_dirty = true;
+    }
+
+    // emqx_trie:delete/1 (src/emqx_trie.erl:88-96) + delete_path/1 (:149-163)
+    void remove(const uint8_t* p, uint32_t len) {
+        if (!split_words(p, len, false)) return;  // [] -> ok
+        uint32_t v = walk(tmp_words);
+        if (v == NODE_NONE) return;               // [] -> ok
+        uint32_t fid = nodes[v].self_filter;
+        if (fid != FILTER_NONE) {
+            set_topic(v, FILTER_NONE);
+            free_filter(fid);
+        }
+        if (aux[v].edge_count == 0) {
+            // [#trie_node{edge_count = 0}] -> delete node, then walk up removing
+            // nodes whose edge_count drops to 0 with topic = undefined
+            for (;;) {
+                uint32_t parent = aux[v].parent;
+                unlink_child(v);
+                if (parent == ROOT || aux[parent].edge_count != 0 ||
+                    nodes[parent].self_filter != FILTER_NONE)
+                    break;
+                v = parent;
+            }
+        }
+        dev_dirty = true;
+    }
+
+    // ------------------------------------------------------------------
+    // device image
+    struct Guard {
+        int prev = -1;
+        explicit Guard(int dev) {
+            (void)hipGetDevice(&prev);
+            HIPCHK(hipSetDevice(dev));
+        }
+        ~Guard() {
+            if (prev >= 0) (void)hipSetDevice(prev);
+        }
+    };
+
+    ImageView view() const {
+        ImageView im;
+        im.nodes = d_nodes.as<const Node>();
+        im.edges = d_edges.as<const EdgeSlot>();
+        im.edge_slot_mask = edges.size() - 1;
+        im.dict = d_dict.as<const DictSlot>();
+        im.dict_slot_mask = dict.size() - 1;
+        im.word_arena = d_arena.as<const uint8_t>();
+        im.word_off = d_woff.as<const uint32_t>();
+        return im;
+    }
+
+    template <class T>
+    void upload_table(DevBuf& buf, const std::vector<T>& host, Dirty& dirty, size_t dev_elems_min) {
+        size_t need = std::max(host.size(), dev_elems_min) * sizeof(T);
+        bool re = buf.ensure(need);
+        if (re || dirty.all) {
+            HIPCHK(hipMemcpyAsync(buf.p, host.data(), host.size() * sizeof(T), hipMemcpyHostToDevice, stream));
+        } else {
+            size_t np = dirty.pages.size();
+            for (size_t pg = 0; pg < np;) {
+                if (!dirty.pages[pg]) { ++pg; continue; }
+                size_t q = pg;
+                while (q < np && dirty.pages[q]) ++q;
+                size_t a = pg * PAGE_ELEMS, b = std::min(host.size(), q * PAGE_ELEMS);
+                if (a < b)
+                    HIPCHK(hipMemcpyAsync(buf.as<T>() + a, host.data() + a, (b - a) * sizeof(T),
+                                          hipMemcpyHostToDevice, stream));
+                pg = q;
+            }
+        }
+        dirty.clear();
+    }
+
+    void wait_matches() {
+        if (match_in_flight) {
+            HIPCHK(hipEventSynchronize(last_match_done));
+            match_in_flight = false;
+        }
+    }
+
+    void commit() {
+        if (device < 0) {
+            ++epoch;
+            dev_dirty = false;
+            return;
+        }
+        if (!dev_dirty && d_nodes.p) return;
+        Guard g(device);
+        wait_matches();  // never patch the image under a running walk
+        upload_table(d_nodes, nodes, node_dirty, 0);
+        upload_table(d_edges, edges, edge_dirty, 0);
+        upload_table(d_dict, dict, dict_dirty, 0);
+        // append-only arrays: upload the new tail (or all after a realloc)
+        {
+            bool re = d_arena.ensure(std::max<size_t>(word_arena.size(), 8) + 16);
+            size_t from = re ? 0 : arena_uploaded;
+            if (word_arena.size() > from)
+                HIPCHK(hipMemcpyAsync(d_arena.as<uint8_t>() + from, word_arena.data() + from,
+                                      word_arena.size() - from, hipMemcpyHostToDevice, stream));
+            arena_uploaded = word_arena.size();
+        }
+        {
+            bool re = d_woff.ensure(std::max<size_t>(word_off.size(), 1) * 4);
+            size_t from = re ? 0 : woff_uploaded;
+            if (word_off.size() > from)
+                HIPCHK(hipMemcpyAsync(d_woff.as<uint32_t>() + from, word_off.data() + from,
+                                      (word_off.size() - from) * 4, hipMemcpyHostToDevice, stream));
+            woff_uploaded = word_off.size();
+        }
+        HIPCHK(hipStreamSynchronize(stream));
+        dev_dirty = false;
+        ++epoch;
+    }
+
+    // ------------------------------------------------------------------
+    // the match pipeline on device buffers (all stream-ordered on st)
+    KTimes take_event(const char* name) {
+        KTimes k{name, nullptr, nullptr};
+        if (!ev_pool.empty()) {
+            k = ev_pool.back();
+            ev_pool.pop_back();
+            k.name = name;
+        } else {
+            HIPCHK(hipEventCreate(&k.a));
+            HIPCHK(hipEventCreate(&k.b));
+        }
+        return k;
+    }
+    void timed(hipStream_t st, const char* name, int idx) {
+        if (!timing_enabled) return;
+        ev_cur[idx] = take_event(name);
+        ev_open[idx] = true;
+        HIPCHK(hipEventRecord(ev_cur[idx].a, st));
+    }
+    void timed_end(hipStream_t st, int idx) {
+        if (!timing_enabled || !ev_open[idx]) return;
+        HIPCHK(hipEventRecord(ev_cur[idx].b, st));
+        ev_pending.push_back(ev_cur[idx]);
+        ev_open[idx] = false;
+    }
+
+    void ensure_workspace(uint32_t n, uint64_t nbytes, bool want_path) {
+        w_words.ensure((nbytes + n + 1) * 4);
+        w_meta.ensure((size_t)(n + 1) * 4);
+        w_scan.ensure(scan_tmp_elems(n) * 8 + 8);
+        w_total.ensure(64);
+        w_stats.ensure(64);
+        if (want_path) w_path.ensure((nbytes + 2ull * n + 2) * 4);
+    }
+
+    // phase A: tokenize + count + scan
+    void run_count(const uint8_t* bytes, const uint64_t* off, uint32_t n, uint64_t nbytes, uint32_t* counts,
+                   uint64_t* out_off, uint64_t* total, hipStream_t st) {
+        ensure_workspace(n, nbytes, true);
+        ImageView im = view();
+        uint32_t* words = w_words.as<uint32_t>();
+        uint32_t* meta = w_meta.as<uint32_t>();
+        timed(st, "tokenize", 0);
+        HIPCHK(launch_tokenize(im, bytes, off, n, words, meta, st));
+        timed_end(st, 0);
+        timed(st, "match_count", 1);
+        HIPCHK(launch_match(TM_MODE_COUNT, false, im, off, n, words, meta, counts, nullptr, nullptr, 0,
+                            w_path.as<uint32_t>(), nullptr, st));
+        HIPCHK(launch_match(TM_MODE_COUNT, true, im, off, n, words, meta, counts, nullptr, nullptr, 0,
+                            w_path.as<uint32_t>(), nullptr, st));
+        timed_end(st, 1);
+        timed(st, "scan", 2);
+        HIPCHK(launch_scan(counts, n, out_off, total, w_scan.as<uint64_t>(), st));
+        timed_end(st, 2);
+        if (stats_enabled) {
+            HIPCHK(hipMemsetAsync(w_stats.p, 0, 64, st));
+            unsigned long long* sp = w_stats.as<unsigned long long>();
+            // the STATS walk re-counts; it writes counts again (same values)
+            HIPCHK(launch_match(TM_MODE_STATS, false, im, off, n, words, meta, counts, nullptr, nullptr, 0,
+                                w_path.as<uint32_t>(), sp, st));
+            HIPCHK(launch_match(TM_MODE_STATS, true, im, off, n, words, meta, counts, nullptr, nullptr, 0,
+                                w_path.as<uint32_t>(), sp, st));
+        }
+    }
+    // phase B: emit ids in reference order at the scanned offsets
+    void run_emit(const uint64_t* off, uint32_t n, const uint64_t* out_off, uint32_t* ids, uint64_t cap,
+                  hipStream_t st) {
+        ImageView im = view();
+        timed(st, "match_emit", 3);
+        HIPCHK(launch_match(TM_MODE_EMIT, false, im, off, n, w_words.as<uint32_t>(), w_meta.as<uint32_t>(),
+                            nullptr, out_off, ids, cap, w_path.as<uint32_t>(), nullptr, st));
+        HIPCHK(launch_match(TM_MODE_EMIT, true, im, off, n, w_words.as<uint32_t>(), w_meta.as<uint32_t>(),
+                            nullptr, out_off, ids, cap, w_path.as<uint32_t>(), nullptr, st));
+        timed_end(st, 3);
+    }
+    void finish_batch(hipStream_t st, uint32_t n) {
+        if (!last_match_done) HIPCHK(hipEventCreateWithFlags(&last_match_done, hipEventDisableTiming));
+        HIPCHK(hipEventRecord(last_match_done, st));
+        match_in_flight = true;
+        last_stats = tm_batch_stats{};
+        last_stats.topics = n;
+    }
+    void collect_stats() {
+        if (!stats_enabled || !w_stats.p) return;
+        unsigned long long h[4] = {0, 0, 0, 0};
+        HIPCHK(hipMemcpy(h, w_stats.p, sizeof(h), hipMemcpyDeviceToHost));
+        last_stats.levels = h[0];
+        last_stats.visits = h[1];
+        last_stats.edge_reads = h[2];
+        last_stats.matches = h[3];
+    }
+};
+
+// ---------------------------------------------------------------------------
+namespace {
+
+template <class F>
+int guarded(tm_engine* e, F&& f) {
+    if (!e) return TM_EINVAL;
+    std::lock_guard<std::recursive_mutex> lk(e->mu);
+    try {
+        return f();
+    } catch (const ArgError& x) {
+        e->last_error = x.what();
+        return TM_EINVAL;
+    } catch (const RangeError& x) {
+        e->last_error = x.what();
+        return TM_ERANGE;
+    } catch (const DevError& x) {
+        e->last_error = x.what();
+        return TM_EDEVICE;
+    } catch (const std::bad_alloc&) {
+        e->last_error = "out of host memory";
+        return TM_ENOMEM;
+    } catch (const std::exception& x) {
+        e->last_error = x.what();
+        return TM_EDEVICE;
+    } catch (...) {
+        e->last_error = "unknown failure";
+        return TM_EDEVICE;
+    }
+}
+
+// emqx_topic:words/1 over a byte string, into (start, len) pairs
+inline void split_levels(const uint8_t* p, uint32_t len, std::vector<std::pair<uint32_t, uint32_t>>& out) {
+    out.clear();
+    uint32_t s = 0;
+    for (uint32_t i = 0; i <= len; ++i)
+        if (i == len || p[i] == '/') {
+            out.emplace_back(s, i - s);
+            s = i + 1;
+        }
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* tm_build_info(void) { return "libtopicmatch gfx950 (CDNA4) HIP; image v1 (node16/edge16x4/dict16)"; }
+
+const char* tm_strerror(int code) {
+    switch (code) {
+        case TM_OK: return "ok";
+        case TM_EINVAL: return "invalid argument";
+        case TM_ENOSPC: return "output buffer too small";
+        case TM_EDEVICE: return "device unavailable or HIP error";
+        case TM_ENOMEM: return "out of memory";
+        case TM_ENOENT: return "no such trie node";
+        case TM_ERANGE: return "capacity exceeded";
+        default: return "unknown status";
+    }
+}
+
+const char* tm_last_error(tm_engine* e) { return e ? e->last_error.c_str() : "null engine"; }
+
+int tm_open(const tm_config* cfg, tm_engine** out) {
+    if (!out) return TM_EINVAL;
+    *out = nullptr;
+    tm_engine* e = nullptr;
+    try {
+        e = new tm_engine();
+    } catch (...) {
+        return TM_ENOMEM;
+    }
+    int dev = cfg ? cfg->device : -1;
+    if (cfg && cfg->filters_hint) {
+        size_t nodes_hint = (size_t)cfg->filters_hint * 3;
+        e->nodes.reserve(nodes_hint);
+        e->aux.reserve(nodes_hint);
+        e->edges.assign(next_pow2(nodes_hint * 2), EdgeSlot{EDGE_EMPTY, 0, 0, 0});
+    }
+    if (dev >= 0) {
+        int ndev = 0;
+        hipError_t err = hipGetDeviceCount(&ndev);
+        if (err != hipSuccess || dev >= ndev) {
+            delete e;
+            return TM_EDEVICE;
+        }
+        int prev = -1;
+        (void)hipGetDevice(&prev);
+        if (hipSetDevice(dev) != hipSuccess ||
+            hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
+            delete e;
+            return TM_EDEVICE;
+        }
+        if (prev >= 0) (void)hipSetDevice(prev);
+        e->device = dev;
+    }
+    *out = e;
+    return TM_OK;
+}
+
+void tm_close(tm_engine* e) {
+    if (!e) return;
+    if (e->device >= 0) {
+        (void)hipSetDevice(e->device);
+        if (e->stream) (void)hipStreamSynchronize(e->stream);
+        for (DevBuf* b : {&e->d_nodes, &e->d_edges, &e->d_dict, &e->d_arena, &e->d_woff, &e->w_bytes, &e->w_off,
+                          &e->w_words, &e->w_meta, &e->w_counts, &e->w_outoff, &e->w_ids, &e->w_scan, &e->w_total,
+                          &e->w_path, &e->w_stats})
+            b->release();
+        for (auto* v : {&e->ev_pool, &e->ev_pending})
+            for (auto& k : *v) {
+                (void)hipEventDestroy(k.a);
+                (void)hipEventDestroy(k.b);
+            }
+        if (e->last_match_done) (void)hipEventDestroy(e->last_match_done);
+        if (e->stream) (void)hipStreamDestroy(e->stream);
+    }
+    delete e;
+}
+
+int tm_insert(tm_engine* e, const uint8_t* filter, uint32_t len) {
+    if (!filter && len) return TM_EINVAL;
+    return guarded(e, [&] {
+        e->insert(filter, len);
+        return TM_OK;
+    });
+}
+
+int tm_insert_batch(tm_engine* e, const uint8_t* bytes, const uint64_t* off, uint32_t n) {
+    if (n && (!bytes || !off)) return TM_EINVAL;
+    return guarded(e, [&] {
+        for (uint32_t i = 0; i < n; ++i) {
+            if (off[i + 1] < off[i] || off[i + 1] - off[i] > 0xFFFFFFFFull) throw ArgError("bad offsets");
+            e->insert(bytes + off[i], (uint32_t)(off[i + 1] - off[i]));
+        }
+        return TM_OK;
+    });
+}
+
+int tm_delete(tm_engine* e, const uint8_t* filter, uint32_t len) {
+    if (!filter && len) return TM_EINVAL;
+    return guarded(e, [&] {
+        e->remove(filter, len);
+        return TM_OK;
+    });
+}
+
+int tm_lookup(tm_engine* e, const uint8_t* node_id, uint32_t len, tm_node_info* out) {
+    if ((!node_id && len) || !out) return TM_EINVAL;
+    return guarded(e, [&] {
+        if (!e->split_words(node_id, len, false)) return TM_ENOENT;
+        uint32_t v = e->walk(e->tmp_words);
+        if (v == NODE_NONE) return TM_ENOENT;
+        out->edge_count = e->aux[v].edge_count;
+        out->filter_id = e->nodes[v].self_filter;
+        return TM_OK;
+    });
+}
+
+int tm_commit(tm_engine* e, uint64_t* epoch_out) {
+    return guarded(e, [&] {
+        e->commit();
+        if (epoch_out) *epoch_out = e->epoch;
+        return TM_OK;
+    });
+}
+
+uint64_t tm_filter_count(tm_engine* e) { return e ? e->live_filters : 0; }
+uint64_t tm_node_count(tm_engine* e) { return e ? e->live_nodes : 0; }
+uint64_t tm_image_bytes(tm_engine* e) {
+    if (!e) return 0;
+    return e->nodes.size() * sizeof(Node) + e->edges.size() * sizeof(EdgeSlot) + e->dict.size() * sizeof(DictSlot) +
+           e->word_arena.size() + e->word_off.size() * 4;
+}
+
+const uint8_t* tm_filter_bytes(tm_engine* e, uint32_t fid, uint32_t* len) {
+    if (!e || fid >= e->filters.size() || e->filters[fid].node == NODE_NONE) {
+        if (len) *len = 0;
+        return nullptr;
+    }
+    if (len) *len = e->filters[fid].len;
+    return e->filter_arena.data() + e->filters[fid].off;
+}
+
+int tm_match_batch(tm_engine* e, const uint8_t* topic_bytes, const uint64_t* topic_off, uint32_t n,
+                   uint32_t* out_count, uint64_t* out_off, uint32_t* out_ids, uint64_t out_cap,
+                   uint64_t* out_needed) {
+    if (!topic_off || !out_off || (n && (!out_count)) || (out_cap && !out_ids)) return TM_EINVAL;
+    return guarded(e, [&]() -> int {
+        if (e->device < 0) {
+            e->last_error = "engine is host-only (device = -1): the match path runs on the GPU only";
+            return TM_EDEVICE;
+        }
+        for (uint32_t i = 0; i < n; ++i)
+            if (topic_off[i + 1] < topic_off[i]) throw ArgError("topic offsets not monotone");
+        uint64_t base = topic_off[0], nbytes = topic_off[n] - base;
+        if (n && nbytes && !topic_bytes) throw ArgError("null topic bytes");
+        if (n == 0) {
+            out_off[0] = 0;
+            if (out_needed) *out_needed = 0;
+            return TM_OK;
+        }
+        e->commit();
+        tm_engine::Guard g(e->device);
+        hipStream_t st = e->stream;
+        e->w_bytes.ensure(nbytes + 16);
+        e->w_off.ensure((size_t)(n + 1) * 8);
+        e->w_counts.ensure((size_t)n * 4 + 4);
+        e->w_outoff.ensure((size_t)(n + 1) * 8);
+        std::vector<uint64_t> rel(topic_off, topic_off + n + 1);
+        for (auto& x : rel) x -= base;
+        if (nbytes)
+            HIPCHK(hipMemcpyAsync(e->w_bytes.p, topic_bytes + base, nbytes, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(e->w_off.p, rel.data(), (n + 1) * 8, hipMemcpyHostToDevice, st));
+        uint64_t* d_total = e->w_total.as<uint64_t>();
+        e->ensure_workspace(n, nbytes, true);
+        d_total = e->w_total.as<uint64_t>();
+        e->run_count(e->w_bytes.as<uint8_t>(), e->w_off.as<uint64_t>(), n, nbytes, e->w_counts.as<uint32_t>(),
+                     e->w_outoff.as<uint64_t>(), d_total, st);
+        uint64_t total = 0;
+        HIPCHK(hipMemcpyAsync(&total, d_total, 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        uint64_t cap = std::min(total, out_cap);
+        if (cap) {
+            e->w_ids.ensure(cap * 4);
+            e->run_emit(e->w_off.as<uint64_t>(), n, e->w_outoff.as<uint64_t>(), e->w_ids.as<uint32_t>(), cap, st);
+        }
+        e->finish_batch(st, n);
+        HIPCHK(hipMemcpyAsync(out_count, e->w_counts.p, (size_t)n * 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(out_off, e->w_outoff.p, (size_t)(n + 1) * 8, hipMemcpyDeviceToHost, st));
+        if (cap) HIPCHK(hipMemcpyAsync(out_ids, e->w_ids.p, cap * 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        e->match_in_flight = false;
+        e->collect_stats();
+        if (out_needed) *out_needed = total;
+        return total > out_cap ? TM_ENOSPC : TM_OK;
+    });
+}
+
+int tm_match_batch_device(tm_engine* e, const uint8_t* d_bytes, const uint64_t* d_off, uint32_t n,
+                          uint64_t topic_bytes, uint32_t* d_count, uint64_t* d_out_off, uint32_t* d_ids,
+                          uint64_t out_cap, uint64_t* d_total, void* hip_stream) {
+    if (!d_off || !d_out_off || !d_total || (n && !d_count) || (out_cap && !d_ids)) return TM_EINVAL;
+    return guarded(e, [&]() -> int {
+        if (e->device < 0) {
+            e->last_error = "engine is host-only (device = -1): the match path runs on the GPU only";
+            return TM_EDEVICE;
+        }
+        e->commit();
+        tm_engine::Guard g(e->device);
+        hipStream_t st = hip_stream ? (hipStream_t)hip_stream : e->stream;
+        if (n == 0) {
+            HIPCHK(hipMemsetAsync(d_out_off, 0, 8, st));
+            HIPCHK(hipMemsetAsync(d_total, 0, 8, st));
+            return TM_OK;
+        }
+        e->run_count(d_bytes, d_off, n, topic_bytes, d_count, d_out_off, d_total, st);
+        if (out_cap) e->run_emit(d_off, n, d_out_off, d_ids, out_cap, st);
+        e->finish_batch(st, n);
+        if (e->stats_enabled) {
+            HIPCHK(hipStreamSynchronize(st));
+            e->match_in_flight = false;
+            e->collect_stats();
+        }
+        return TM_OK;
+    });
+}
+
+int tm_set_stats(tm_engine* e, int enable) {
+    return guarded(e, [&] {
+        e->stats_enabled = enable != 0;
+        return TM_OK;
+    });
+}
+
+int tm_last_stats(tm_engine* e, tm_batch_stats* out) {
+    if (!out) return TM_EINVAL;
+    return guarded(e, [&] {
+        *out = e->last_stats;
+        return TM_OK;
+    });
+}
+
+int tm_set_timing(tm_engine* e, int enable) {
+    return guarded(e, [&] {
+        e->timing_enabled = enable != 0;
+        return TM_OK;
+    });
+}
+
+int tm_last_kernel_times(tm_engine* e, const char** names, float* ms, int cap) {
+    return guarded(e, [&]() -> int {
+        if (e->ev_pending.empty()) return 0;
+        tm_engine::Guard g(e->device);
+        // average per batch of each kernel stage over every batch recorded
+        // since the previous call
+        std::vector<const char*> order;
+        std::vector<double> sum;
+        std::vector<int> cnt;
+        for (auto& t : e->ev_pending) {
+            HIPCHK(hipEventSynchronize(t.b));
+            float v = 0.f;
+            HIPCHK(hipEventElapsedTime(&v, t.a, t.b));
+            size_t i = 0;
+            while (i < order.size() && std::strcmp(order[i], t.name) != 0) ++i;
+            if (i == order.size()) {
+                order.push_back(t.name);
+                sum.push_back(0.0);
+                cnt.push_back(0);
+            }
+            sum[i] += v;
+            cnt[i] += 1;
+            e->ev_pool.push_back(t);
+        }
+        e->ev_pending.clear();
+        int k = 0;
+        for (size_t i = 0; i < order.size() && k < cap; ++i, ++k) {
+            if (names) names[k] = order[i];
+            if (ms) ms[k] = (float)(sum[i] / cnt[i]);
+        }
+        return k;
+    });
+}
+
+// ---- pure topic algebra ----------------------------------------------------
+
+// emqx_topic:match/2, binary/binary clause (src/emqx_topic.erl:56-61) then the
+// word-list clauses (:62-75)
+int tm_topic_match(const uint8_t* name, uint32_t nlen, const uint8_t* filt, uint32_t flen) {
+    if ((!name && nlen) || (!filt && flen)) return 0;
+    if (nlen > 0 && name[0] == '$' && flen > 0 && (filt[0] == '+' || filt[0] == '#')) return 0;
+    std::vector<std::pair<uint32_t, uint32_t>> nw, fw;
+    split_levels(name, nlen, nw);
+    split_levels(filt, flen, fw);
+    auto is = [](const uint8_t* p, std::pair<uint32_t, uint32_t> w, char c) {
+        return w.second == 1 && p[w.first] == (uint8_t)c;
+    };
+    size_t i = 0, j = 0;
+    for (;;) {
+        if (i == nw.size() && j == fw.size()) return 1;          // match([], [])
+        if (j < fw.size() && i < nw.size()) {
+            auto a = nw[i], b = fw[j];
+            // match([H|T1], [H|T2]) — equal words (atoms compare equal too)
+            if (a.second == b.second && std::memcmp(name + a.first, filt + b.first, a.second) == 0) {
+                ++i, ++j;
+                continue;
+            }
+            if (is(filt, b, '+')) {                              // match([_|T1], ['+'|T2])
+                ++i, ++j;
+                continue;
+            }
+        }
+        if (j + 1 == fw.size() && is(filt, fw[j], '#')) return 1;  // match(_, ['#'])
+        return 0;
+    }
+}
+
+int tm_topic_wildcard(const uint8_t* topic, uint32_t len) {
+    if (!topic && len) return 0;
+    std::vector<std::pair<uint32_t, uint32_t>> w;
+    split_levels(topic, len, w);
+    for (auto x : w)
+        if (x.second == 1 && (topic[x.first] == '+' || topic[x.first] == '#')) return 1;
+    return 0;
+}
+
+// emqx_topic:parse/1,2 (src/emqx_topic.erl:180-200)
+int tm_topic_parse(const uint8_t* t, uint32_t len, const uint8_t** inner, uint32_t* inner_len,
+                   const uint8_t** group, uint32_t* group_len) {
+    if ((!t && len) || !inner || !inner_len || !group || !group_len) return TM_EINVAL;
+    static const uint8_t kQueue[] = "$queue";
+    auto starts = [&](const uint8_t* p, uint32_t n, const char* pre) {
+        size_t k = std::strlen(pre);
+        return n >= k && std::memcmp(p, pre, k) == 0;
+    };
+    const uint8_t* p = t;
+    uint32_t n = len;
+    bool shared = false;
+    *group = nullptr;
+    *group_len = 0;
+    if (starts(p, n, "$queue/")) {
+        p += 7, n -= 7;
+        *group = kQueue;
+        *group_len = 6;
+        shared = true;
+        if (starts(p, n, "$queue/") || starts(p, n, "$share/")) return TM_EINVAL;  // nested share
+    } else if (starts(p, n, "$share/")) {
+        const uint8_t* q = p + 7;
+        uint32_t m = n - 7;
+        const uint8_t* slash = (const uint8_t*)std::memchr(q, '/', m);
+        if (!slash) return TM_EINVAL;  // [<<>>] or [_]
+        uint32_t glen = (uint32_t)(slash - q);
+        for (uint32_t i = 0; i < glen; ++i)
+            if (q[i] == '+' || q[i] == '#') return TM_EINVAL;
+        *group = q;
+        *group_len = glen;
+        p = slash + 1;
+        n = m - glen - 1;
+        shared = true;
+    }
+    (void)shared;
+    *inner = p;
+    *inner_len = n;
+    return TM_OK;
+}
+
+}  // extern "C"

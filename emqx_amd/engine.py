@@ -1,0 +1,183 @@
+"""Python handle on one libtopicmatch engine (one engine per GPU).
+
+Thin wrapper over the C-ABI: numpy arrays for host batches, torch tensors
+(or raw device pointers) for HBM-resident batches.  No matching logic lives
+here; every match runs in the HIP kernels of emqx_amd/csrc/kernels.hip.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib as L
+
+
+def pack(strings):
+    """Concatenate byte strings -> (bytes ndarray u8, offsets ndarray u64)."""
+    bs = [s if isinstance(s, (bytes, bytearray)) else s.encode() for s in strings]
+    off = np.zeros(len(bs) + 1, dtype=np.uint64)
+    if bs:
+        off[1:] = np.cumsum([len(b) for b in bs], dtype=np.uint64)
+    buf = np.frombuffer(b"".join(bs) + b"\0" * 8, dtype=np.uint8)
+    return buf, off
+
+
+def _ptr(a):
+    return ctypes.c_void_p(a.ctypes.data) if a is not None else None
+
+
+class Engine:
+    """One subscription trie + its HBM image on `device` (-1 = host-only:
+    insert/delete/lookup work, matching raises TM_EDEVICE)."""
+
+    def __init__(self, device=0, filters_hint=0, batch_topics=0, batch_bytes=0):
+        self.lib = L.load()
+        cfg = L.TmConfig(device, 0, filters_hint, batch_topics, batch_bytes)
+        h = ctypes.c_void_p()
+        rc = self.lib.tm_open(ctypes.byref(cfg), ctypes.byref(h))
+        if rc != L.TM_OK:
+            raise L.TopicMatchError(rc, "tm_open(device=%d)" % device)
+        self.h = h
+        self.device = device
+
+    # -- lifetime ---------------------------------------------------------
+    def close(self):
+        if self.h:
+            self.lib.tm_close(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc, what):
+        if rc != L.TM_OK:
+            raise L.TopicMatchError(rc, "%s: %s" % (what, self.lib.tm_last_error(self.h).decode()))
+        return rc
+
+    # -- emqx_trie:insert/1, delete/1, lookup/1 ---------------------------
+    def insert(self, filt: bytes):
+        return self._check(self.lib.tm_insert(self.h, filt, len(filt)), "tm_insert")
+
+    def insert_many(self, buf, off):
+        n = len(off) - 1
+        buf = np.ascontiguousarray(buf, dtype=np.uint8)
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        return self._check(self.lib.tm_insert_batch(self.h, _ptr(buf), _ptr(off), n), "tm_insert_batch")
+
+    def delete(self, filt: bytes):
+        return self._check(self.lib.tm_delete(self.h, filt, len(filt)), "tm_delete")
+
+    def lookup(self, node_id: bytes):
+        """[] or [(edge_count, topic_bytes_or_None)] like emqx_trie:lookup/1"""
+        info = L.TmNodeInfo()
+        rc = self.lib.tm_lookup(self.h, node_id, len(node_id), ctypes.byref(info))
+        if rc == L.TM_ENOENT:
+            return []
+        self._check(rc, "tm_lookup")
+        topic = None if info.filter_id == L.TM_NO_FILTER else self.filter_bytes(info.filter_id)
+        return [(info.edge_count, topic)]
+
+    def commit(self):
+        ep = ctypes.c_uint64()
+        self._check(self.lib.tm_commit(self.h, ctypes.byref(ep)), "tm_commit")
+        return ep.value
+
+    def filter_bytes(self, fid: int) -> bytes:
+        n = ctypes.c_uint32()
+        p = self.lib.tm_filter_bytes(self.h, fid, ctypes.byref(n))
+        if not p:
+            raise KeyError(fid)
+        return ctypes.string_at(p, n.value)
+
+    @property
+    def filter_count(self):
+        return self.lib.tm_filter_count(self.h)
+
+    @property
+    def node_count(self):
+        return self.lib.tm_node_count(self.h)
+
+    @property
+    def image_bytes(self):
+        return self.lib.tm_image_bytes(self.h)
+
+    # -- emqx_trie:match/1 over a batch ------------------------------------
+    def match_batch(self, buf, off, out_cap=None):
+        """Host batch -> (counts u32[n], offsets u64[n+1], filter ids u32[total])."""
+        buf = np.ascontiguousarray(buf, dtype=np.uint8)
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        n = len(off) - 1
+        counts = np.zeros(max(n, 1), dtype=np.uint32)
+        offs = np.zeros(n + 1, dtype=np.uint64)
+        cap = 1 << 16 if out_cap is None else out_cap
+        while True:
+            ids = np.zeros(max(cap, 1), dtype=np.uint32)
+            needed = ctypes.c_uint64()
+            rc = self.lib.tm_match_batch(self.h, _ptr(buf), _ptr(off), n, _ptr(counts), _ptr(offs), _ptr(ids),
+                                         cap, ctypes.byref(needed))
+            if rc == L.TM_ENOSPC and out_cap is None:
+                cap = int(needed.value)
+                continue
+            self._check(rc, "tm_match_batch")
+            return counts[:n], offs, ids[: int(needed.value)]
+
+    def match(self, topics):
+        """list of topics -> list of lists of filter bytes, reference order."""
+        buf, off = pack(topics)
+        counts, offs, ids = self.match_batch(buf, off)
+        names = {}
+        out = []
+        for t in range(len(topics)):
+            row = []
+            for fid in ids[int(offs[t]): int(offs[t]) + int(counts[t])]:
+                fid = int(fid)
+                if fid not in names:
+                    names[fid] = self.filter_bytes(fid)
+                row.append(names[fid])
+            out.append(row)
+        return out
+
+    def match_batch_device(self, d_bytes, d_off, n, topic_bytes, d_counts, d_offs, d_ids, out_cap, d_total,
+                           stream=None):
+        """All arguments are device pointers (ints) or torch tensors; stream-
+        ordered, no synchronisation."""
+        def p(x):
+            if x is None:
+                return None
+            if hasattr(x, "data_ptr"):
+                return ctypes.c_void_p(x.data_ptr())
+            return ctypes.c_void_p(int(x))
+        st = None
+        if stream is not None:
+            st = ctypes.c_void_p(stream if isinstance(stream, int) else stream.cuda_stream)
+        rc = self.lib.tm_match_batch_device(self.h, p(d_bytes), p(d_off), n, topic_bytes, p(d_counts), p(d_offs),
+                                            p(d_ids), out_cap, p(d_total), st)
+        return self._check(rc, "tm_match_batch_device")
+
+    # -- instrumentation ----------------------------------------------------
+    def set_stats(self, on=True):
+        self._check(self.lib.tm_set_stats(self.h, 1 if on else 0), "tm_set_stats")
+
+    def last_stats(self):
+        s = L.TmBatchStats()
+        self._check(self.lib.tm_last_stats(self.h, ctypes.byref(s)), "tm_last_stats")
+        return {k: getattr(s, k) for k, _ in s._fields_}
+
+    def set_timing(self, on=True):
+        self._check(self.lib.tm_set_timing(self.h, 1 if on else 0), "tm_set_timing")
+
+    def last_kernel_times(self):
+        names = (ctypes.c_char_p * 16)()
+        ms = (ctypes.c_float * 16)()
+        k = self.lib.tm_last_kernel_times(self.h, names, ms, 16)
+        if k < 0:
+            self._check(k, "tm_last_kernel_times")
+        return {names[i].decode(): ms[i] for i in range(k)}

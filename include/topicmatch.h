@@ -1,0 +1,161 @@
+/*
+ * topicmatch.h — C-ABI of libtopicmatch, the MI355X topic-routing engine that sits
+ * behind EMQ X's publish path (emqx_trie:match/1, emqx_topic:words/1 + match/2,
+ * emqx_router:match_routes/1).
+ *
+ * Every entry point replaces one reference interface; the citation is the Erlang
+ * function (file:line in vus520/emqx @ 3.0-rc.3) whose semantics it reproduces.
+ * No torch types, no C++ types: plain pointers, sizes and int status codes.
+ * No exception ever crosses this boundary.
+ *
+ * Ownership: input buffers are borrowed for the duration of the call only.
+ * Output buffers are caller-allocated. Filter bytes returned by
+ * tm_filter_bytes() stay engine-owned and valid until that filter is deleted
+ * and the next tm_commit().
+ *
+ * Threading: every call on one engine is serialised by the engine (single
+ * writer; matches read a committed snapshot).  Different engines are
+ * independent (one engine per GPU is the multi-GPU model).
+ */
+#ifndef TOPICMATCH_H
+#define TOPICMATCH_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ------------------------------------------------------- */
+#define TM_OK        0
+#define TM_EINVAL   -1   /* bad argument (NIF: enif_make_badarg)              */
+#define TM_ENOSPC   -2   /* output buffer too small; *out_needed says how big */
+#define TM_EDEVICE  -3   /* no GPU / HIP error / engine opened host-only      */
+#define TM_ENOMEM   -4   /* host or device allocation failed                  */
+#define TM_ENOENT   -5   /* tm_lookup: no such trie node                      */
+#define TM_ERANGE   -6   /* image would exceed 2^30 nodes / 2^32 filters       */
+
+#define TM_NO_FILTER 0xFFFFFFFFu
+
+typedef struct tm_engine tm_engine;
+
+/* mnesia(boot) analogue: src/emqx_trie.erl:38-48 creates the two ram_copies
+ * tables; here the engine holds the host mirror and the HBM image. */
+typedef struct tm_config {
+    int32_t  device;          /* HIP device ordinal; -1 = host-only engine       */
+    uint32_t reserved0;
+    uint64_t filters_hint;    /* expected filter count (pre-sizes tables)        */
+    uint64_t batch_topics;    /* workspace hint: topics per match batch          */
+    uint64_t batch_bytes;     /* workspace hint: topic bytes per match batch     */
+} tm_config;
+
+/* #trie_node{node_id, edge_count, topic} — include/emqx.hrl:100-105 */
+typedef struct tm_node_info {
+    uint32_t edge_count;      /* distinct child words ('+', '#' included)        */
+    uint32_t filter_id;       /* TM_NO_FILTER when topic = undefined             */
+} tm_node_info;
+
+/* batch statistics of the last match (for the roofline accounting) */
+typedef struct tm_batch_stats {
+    uint64_t topics;          /* n                                               */
+    uint64_t levels;          /* sum n_t                                         */
+    uint64_t visits;          /* trie nodes visited by the NFA walk (frontier)   */
+    uint64_t edge_reads;      /* E = mnesia:read(?TRIE,...) calls the reference  */
+                              /*     would make (emqx_trie.erl:132,141)          */
+    uint64_t matches;         /* sum M_t                                         */
+} tm_batch_stats;
+
+/* engine lifetime ------------------------------------------------------------ */
+int  tm_open(const tm_config* cfg, tm_engine** out);
+void tm_close(tm_engine* e);
+const char* tm_strerror(int code);
+const char* tm_last_error(tm_engine* e);  /* text of the last failure on e */
+
+/* emqx_trie:insert/1 — src/emqx_trie.erl:62-73 (+ add_path/1 :104-117).
+ * Idempotent. Any byte string is accepted (the reference does not validate
+ * inside the trie; validation happens at emqx_topic:validate/2). */
+int tm_insert(tm_engine* e, const uint8_t* filter, uint32_t len);
+
+/* Bulk form of tm_insert over n concatenated filters ([off[i], off[i+1])),
+ * the router's batch add (src/emqx_router.erl:148-163 per route). Stops at
+ * the first failure and returns its code. */
+int tm_insert_batch(tm_engine* e, const uint8_t* bytes, const uint64_t* off, uint32_t n);
+
+/* emqx_trie:delete/1 — src/emqx_trie.erl:88-96 (+ delete_path/1 :149-163).
+ * Unknown filter = no-op (TM_OK). */
+int tm_delete(tm_engine* e, const uint8_t* filter, uint32_t len);
+
+/* emqx_trie:lookup/1 — src/emqx_trie.erl:83-84.  node_id is the full path
+ * binary (emqx_topic:join of the words).  TM_ENOENT when the node is absent. */
+int tm_lookup(tm_engine* e, const uint8_t* node_id, uint32_t len, tm_node_info* out);
+
+/* Publish pending deltas to the HBM image (mnesia transaction commit,
+ * src/emqx_router.erl:264-268).  tm_match_* commit implicitly. */
+int tm_commit(tm_engine* e, uint64_t* epoch_out);
+
+/* number of filters currently in the trie (nodes with topic =/= undefined) */
+uint64_t tm_filter_count(tm_engine* e);
+/* trie nodes / literal edges of the image (for sizing reports) */
+uint64_t tm_node_count(tm_engine* e);
+uint64_t tm_image_bytes(tm_engine* e);
+
+/* filter id -> filter bytes (the #trie_node.topic binary) */
+const uint8_t* tm_filter_bytes(tm_engine* e, uint32_t filter_id, uint32_t* len);
+
+/* emqx_trie:match/1 over a batch — src/emqx_trie.erl:77-79, 121-145, with
+ * emqx_topic:words/1 (src/emqx_topic.erl:141-147) done on the device.
+ * Topics are concatenated in topic_bytes; topic t is
+ * [topic_off[t], topic_off[t+1]).  Output is CSR: the match list of topic t is
+ * out_filter_id[out_off[t] .. out_off[t]+out_count[t]), in exactly the order
+ * emqx_trie:match/1 returns it.  out_off has n+1 entries.
+ * If the total exceeds out_cap: TM_ENOSPC, *out_needed = total, counts and
+ * offsets are still filled.  Host buffers; the call synchronises. */
+int tm_match_batch(tm_engine* e, const uint8_t* topic_bytes, const uint64_t* topic_off,
+                   uint32_t n, uint32_t* out_count, uint64_t* out_off,
+                   uint32_t* out_filter_id, uint64_t out_cap, uint64_t* out_needed);
+
+/* Same, with every buffer device-resident (HBM) and stream-ordered on
+ * `hip_stream` (a hipStream_t; NULL = the engine's stream).  Does not
+ * synchronise.  *d_total (device) receives the match total; ids past out_cap
+ * are dropped (the caller compares *d_total with out_cap).  d_topic_off must
+ * have n+1 entries and topic_bytes = d_topic_off[n] - d_topic_off[0] (sizes
+ * the engine's workspace without a device read).  Calls on one engine must
+ * be issued on one stream.  This is the entry a pipelined batcher and the
+ * bench use. */
+int tm_match_batch_device(tm_engine* e, const uint8_t* d_topic_bytes, const uint64_t* d_topic_off,
+                          uint32_t n, uint64_t topic_bytes, uint32_t* d_out_count,
+                          uint64_t* d_out_off, uint32_t* d_out_filter_id, uint64_t out_cap,
+                          uint64_t* d_total, void* hip_stream);
+
+/* Counters of the last batch (visits, reference edge reads, matches).  Costs
+ * one extra device pass; enable with tm_set_stats(e, 1) before the batch. */
+int tm_set_stats(tm_engine* e, int enable);
+int tm_last_stats(tm_engine* e, tm_batch_stats* out);
+
+/* Per-kernel device times (ms), measured with hipEvents recorded around each
+ * kernel stage on the stream the stage ran on; enable with tm_set_timing(e, 1).
+ * Returns, per stage, the average over every batch since the previous call
+ * (synchronising on those events).  names[i] point at static strings.
+ * Returns the number of entries. */
+int tm_set_timing(tm_engine* e, int enable);
+int tm_last_kernel_times(tm_engine* e, const char** names, float* ms, int cap);
+
+/* ---- pure topic algebra (no engine) ----------------------------------------
+ * emqx_topic:match/2 (binary, binary) — src/emqx_topic.erl:56-75.  1 / 0. */
+int tm_topic_match(const uint8_t* name, uint32_t nlen, const uint8_t* filt, uint32_t flen);
+/* emqx_topic:wildcard/1 — src/emqx_topic.erl:41-50.  1 / 0. */
+int tm_topic_wildcard(const uint8_t* topic, uint32_t len);
+/* emqx_topic:parse/1 — src/emqx_topic.erl:180-200.  Strips "$queue/" and
+ * "$share/<group>/".  On success *inner points into `topic`, *group into
+ * `topic` (or NULL when not shared; "$queue" for $queue/).  TM_EINVAL on the
+ * reference's {invalid_topic, _} errors. */
+int tm_topic_parse(const uint8_t* topic, uint32_t len, const uint8_t** inner, uint32_t* inner_len,
+                   const uint8_t** group, uint32_t* group_len);
+
+/* library identity: "gfx950" build tag, for loaders that must fail loudly */
+const char* tm_build_info(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TOPICMATCH_H */

@@ -1,0 +1,220 @@
+"""Parity of the HIP path (tokenizer + NFA walk + CSR emission on gfx950)
+against the oracle, through the C-ABI.  Bit-exact: same filters, same order.
+
+    - the reference's KATs (tests/golden/kat_*.json) on the device
+    - the committed O1 vectors (random tries, '$' rule, empty levels, literal
+      '+'/'#' topic levels, >32-level topics that take the long-path kernel)
+    - C1 at full size and C2 at full size (1M filters x 1M topics) vs O1 by id
+    - C5 (16 levels, '#'-heavy, $SYS, $share) on a sample
+    - subscribe/unsubscribe deltas between batches, ENOSPC, the device API
+"""
+import random
+
+import numpy as np
+import pytest
+
+from emqx_amd import Engine, _lib, pack
+from emqx_amd import emqx_topic as T
+from emqx_amd import workload as W
+from emqx_amd.emqx_router import Router
+from oracle import O1, pytrie
+
+pytestmark = pytest.mark.gpu
+L1 = "latin-1"
+
+
+def b(x):
+    return x.encode(L1)
+
+
+@pytest.fixture
+def eng(gpu_device):
+    e = Engine(device=gpu_device)
+    yield e
+    e.close()
+
+
+def test_kat_trie_on_device(gpu_device, golden):
+    for kat in golden["kat_trie"]:
+        e = Engine(device=gpu_device)
+        for op, arg in kat["ops"]:
+            getattr(e, op)(b(arg))
+        for kind, arg, exp in kat["checks"]:
+            if kind == "match":
+                assert [x.decode(L1) for x in e.match([b(arg)])[0]] == exp, (kat["name"], arg)
+            elif kind == "match_len":
+                assert len(e.match([b(arg)])[0]) == exp
+            elif kind == "lookup":
+                got = [[ec, None if t is None else t.decode(L1)] for ec, t in e.lookup(b(arg))]
+                assert got == exp
+        e.close()
+
+
+def test_kat_client_on_device(gpu_device, golden):
+    for case in golden["kat_client"]["cases"]:
+        e = Engine(device=gpu_device)
+        for f in case["subs"]:
+            e.insert(b(f))
+        assert sorted(x.decode() for x in e.match([b(case["pub"])])[0]) == sorted(case["set"])
+        e.close()
+
+
+def test_kat_router_match_routes_on_device(gpu_device, golden):
+    for kat in golden["kat_router"]:
+        r = Router(Engine(device=gpu_device), node="node")
+        for topic, dest in kat["add"]:
+            r.add_route(b(topic), dest)
+        got = sorted([x.topic.decode(), x.dest] for x in r.match_routes(b(kat["topic"])))
+        assert got == kat["sorted"]
+        if "then_del" in kat:
+            for topic, dest in kat["then_del"]:
+                r.del_route(b(topic), dest)
+            got = sorted([x.topic.decode(), x.dest] for x in r.match_routes(b(kat["topic"])))
+            assert got == kat["sorted_after"]
+        r.engine.close()
+
+
+def test_o1_vectors_on_device(gpu_device, golden):
+    for vec in golden["o1_vectors"]:
+        e = Engine(device=gpu_device)
+        for f in vec["filters"]:
+            e.insert(b(f))
+        topics = [b(r["topic"]) for r in vec["topics"]]
+        got = e.match(topics)
+        for row, g in zip(vec["topics"], got):
+            assert [x.decode(L1) for x in g] == row["match"], (vec["name"], row["topic"])
+        e.close()
+
+
+def test_single_topic_batches(eng, golden):
+    vec = golden["o1_vectors"][-1]
+    for f in vec["filters"]:
+        eng.insert(b(f))
+    for row in vec["topics"][:20]:
+        assert [x.decode(L1) for x in eng.match([b(row["topic"])])[0]] == row["match"]
+
+
+def _by_id(o1, eng, tb, to, threads=16):
+    ec, eo, ei = eng.match_batch(tb, to)
+    oc, oo, oi = o1.match_ids(tb, to, threads=threads)
+    assert np.array_equal(ec, oc)
+    assert np.array_equal(eo, oo)
+    assert np.array_equal(ei, oi)
+    return ec
+
+
+def test_c1_full_vs_o1(eng):
+    fb, fo = W.filters(1)
+    o1 = O1()
+    o1.insert_many(fb, fo)
+    eng.insert_many(fb, fo)
+    tb, to = W.topics(1)
+    counts = _by_id(o1, eng, tb, to)
+    assert counts.sum() > 0
+
+
+def test_c2_full_vs_o1(gpu_device):
+    fb, fo = W.filters(2)
+    o1 = O1(len(fo))
+    o1.insert_many(fb, fo)
+    e = Engine(device=gpu_device, filters_hint=len(fo) - 1)
+    e.insert_many(fb, fo)
+    tb, to = W.topics(2)
+    counts = _by_id(o1, e, tb, to)
+    assert counts.mean() > 1
+    e.close()
+
+
+def test_c5_sample_vs_o1(gpu_device):
+    fb, fo = W.filters(5, n=200_000)
+    raw = W.unpack(fb, fo)
+    inner = [T.parse(f)[0] for f in raw]     # the trie sees the inner filter (emqx_topic.erl:189-197)
+    ib, io = pack(inner)
+    o1 = O1(len(io))
+    o1.insert_many(ib, io)
+    e = Engine(device=gpu_device, filters_hint=len(io) - 1)
+    e.insert_many(ib, io)
+    tb, to = W.topics(5, n=5000)
+    counts = _by_id(o1, e, tb, to)
+    assert counts.max() >= 1000              # adversarial fan-out reached
+    e.close()
+
+
+def test_deltas_between_batches(eng):
+    rng = random.Random(77)
+    py = pytrie.Trie()
+    pool = ["/".join(rng.choice(["a", "b", "+", "", "$x"]) for _ in range(rng.randint(1, 5))) +
+            rng.choice(["", "/#"]) for _ in range(300)]
+    topics = ["/".join(rng.choice(["a", "b", "", "$x", "c"]) for _ in range(rng.randint(1, 6))) for _ in range(200)]
+    for rnd in range(8):
+        for _ in range(60):
+            f = b(rng.choice(pool))
+            if rng.random() < 0.65:
+                eng.insert(f)
+                py.insert(f)
+            else:
+                eng.delete(f)
+                py.delete(f)
+        got = eng.match([b(t) for t in topics])
+        for t, g in zip(topics, got):
+            assert g == py.match(b(t)), (rnd, t)
+
+
+def test_enospc_reports_needed(eng):
+    for f in [b"#", b"+/#", b"+/+/#", b"a/#"]:
+        eng.insert(f)
+    buf, off = pack([b"a/b/c", b"a/x"])
+    with pytest.raises(_lib.TopicMatchError) as ei:
+        eng.match_batch(buf, off, out_cap=2)
+    assert ei.value.code == _lib.TM_ENOSPC
+    c, o, ids = eng.match_batch(buf, off)
+    assert list(c) == [4, 3] and int(o[-1]) == 7
+
+
+def test_empty_batch_and_empty_topic(eng):
+    eng.insert(b"#")
+    eng.insert(b"+")
+    buf, off = pack([])
+    c, o, ids = eng.match_batch(buf, off)
+    assert len(c) == 0 and list(o) == [0] and len(ids) == 0
+    assert eng.match([b""]) == [[b"+", b"#"]]
+
+
+def test_device_api_with_torch(gpu_device):
+    import torch
+    fb, fo = W.filters(1)
+    e = Engine(device=gpu_device)
+    e.insert_many(fb, fo)
+    tb, to = W.topics(1, n=20000)
+    hc, ho, hi = e.match_batch(tb, to)
+    dev = torch.device("cuda", gpu_device)
+    d_b = torch.from_numpy(tb).to(dev)
+    d_o = torch.from_numpy(to.view(np.int64)).to(dev)
+    n = len(to) - 1
+    d_c = torch.zeros(n, dtype=torch.int32, device=dev)
+    d_oo = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    d_i = torch.zeros(len(hi) + 16, dtype=torch.int32, device=dev)
+    d_t = torch.zeros(1, dtype=torch.int64, device=dev)
+    st = torch.cuda.current_stream(dev)
+    e.match_batch_device(d_b, d_o, n, int(to[-1]), d_c, d_oo, d_i, len(hi) + 16, d_t, stream=st)
+    torch.cuda.synchronize(dev)
+    assert int(d_t.item()) == len(hi)
+    assert np.array_equal(d_c.cpu().numpy().view(np.uint32), hc)
+    assert np.array_equal(d_oo.cpu().numpy().view(np.uint64), ho)
+    assert np.array_equal(d_i.cpu().numpy().view(np.uint32)[: len(hi)], hi)
+    e.close()
+
+
+def test_stats_edge_reads_match_oracle(gpu_device, golden):
+    """device-side E (reference edge reads) equals O1's count"""
+    vec = next(v for v in golden["o1_vectors"] if v["name"] == "c1_mini")
+    e = Engine(device=gpu_device)
+    for f in vec["filters"]:
+        e.insert(b(f))
+    e.set_stats(True)
+    buf, off = pack([b(r["topic"]) for r in vec["topics"]])
+    e.match_batch(buf, off)
+    st = e.last_stats()
+    assert st["edge_reads"] == sum(r["edge_reads"] for r in vec["topics"])
+    assert st["matches"] == sum(len(r["match"]) for r in vec["topics"])
+    e.close()
