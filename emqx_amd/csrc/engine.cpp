@@ -17,6 +17,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <new>
@@ -165,7 +166,10 @@ struct tm_engine {
     bool dev_dirty = true;
 
     // ---- match workspace ----
-    DevBuf w_bytes, w_off, w_words, w_meta, w_counts, w_outoff, w_ids, w_scan, w_total, w_path, w_stats;
+    DevBuf w_bytes, w_off, w_words, w_meta, w_counts, w_outoff, w_ids, w_scan, w_total, w_path, w_stats, w_stage,
+        w_ws;
+    bool twopass = false;     // TM_WALK=twopass: count walk + scan + emit walk (A/B only)
+    uint32_t stage_k = 128;   // TM_STAGE_K: ids staged per lane before a re-walk
     hipEvent_t last_match_done = nullptr;
     bool match_in_flight = false;
     bool stats_enabled = false, timing_enabled = false;
@@ -180,6 +184,11 @@ struct tm_engine {
     std::vector<uint32_t> tmp_words;
 
     tm_engine() {
+        if (const char* v = std::getenv("TM_WALK")) twopass = std::strcmp(v, "twopass") == 0;
+        if (const char* v = std::getenv("TM_STAGE_K")) {
+            long k = std::atol(v);
+            if (k >= 1 && k <= 4096) stage_k = (uint32_t)k;
+        }
         dict.assign(1024, DictSlot{0, WORD_NONE, 0});
         nodes.reserve(1024);
         edges.assign(1024, EdgeSlot{EDGE_EMPTY, 0, 0, 0});
@@ -309,7 +318,7 @@ struct tm_engine {
             id = free_nodes.back();
             free_nodes.pop_back();
         } else {
-            if (nodes.size() >= NODE_NONE) throw RangeError("trie exceeds 2^30-1 nodes");
+            if (nodes.size() >= NODE_NONE) throw RangeError("trie exceeds 2^29-1 nodes");
             id = (uint32_t)nodes.size();
             nodes.push_back(Node{});
             aux.push_back(NodeAux{});
@@ -557,54 +566,64 @@ struct tm_engine {
         ev_open[idx] = false;
     }
 
-    void ensure_workspace(uint32_t n, uint64_t nbytes, bool want_path) {
+    void ensure_workspace(uint32_t n, uint64_t nbytes) {
         w_words.ensure((nbytes + n + 1) * 4);
-        w_meta.ensure((size_t)(n + 1) * 4);
-        w_scan.ensure(scan_tmp_elems(n) * 8 + 8);
+        w_path.ensure((nbytes + 2ull * n + 2) * 4);
         w_total.ensure(64);
         w_stats.ensure(64);
-        if (want_path) w_path.ensure((nbytes + 2ull * n + 2) * 4);
+        if (twopass) {
+            w_meta.ensure((size_t)(n + 1) * 4);
+            w_scan.ensure(scan_tmp_elems(n) * 8 + 8);
+        } else {
+            w_stage.ensure(fused_stage_elems(n, stage_k) * 4);
+            w_ws.ensure(fused_ws_words(n) * 8);
+        }
     }
 
-    // phase A: tokenize + count + scan
-    void run_count(const uint8_t* bytes, const uint64_t* off, uint32_t n, uint64_t nbytes, uint32_t* counts,
-                   uint64_t* out_off, uint64_t* total, hipStream_t st) {
-        ensure_workspace(n, nbytes, true);
+    // the whole hot path of one batch, stream-ordered on st: CSR of ordered
+    // filter ids (ids past cap are dropped; *total always exact)
+    void run_batch(const uint8_t* bytes, const uint64_t* off, uint32_t n, uint64_t nbytes, uint32_t* counts,
+                   uint64_t* out_off, uint32_t* ids, uint64_t cap, uint64_t* total, hipStream_t st) {
+        ensure_workspace(n, nbytes);
         ImageView im = view();
         uint32_t* words = w_words.as<uint32_t>();
+        uint32_t* path = w_path.as<uint32_t>();
+        unsigned long long* sp = w_stats.as<unsigned long long>();
+        if (stats_enabled) HIPCHK(hipMemsetAsync(w_stats.p, 0, 64, st));
+        if (!twopass) {
+            timed(st, "match_fused", 0);
+            HIPCHK(launch_fused(stats_enabled, im, bytes, off, n, words, path, w_stage.as<uint32_t>(), stage_k,
+                                counts, out_off, ids, cap, total, w_ws.as<unsigned long long>(), sp, st));
+            timed_end(st, 0);
+            return;
+        }
         uint32_t* meta = w_meta.as<uint32_t>();
         timed(st, "tokenize", 0);
         HIPCHK(launch_tokenize(im, bytes, off, n, words, meta, st));
         timed_end(st, 0);
         timed(st, "match_count", 1);
-        HIPCHK(launch_match(TM_MODE_COUNT, false, im, off, n, words, meta, counts, nullptr, nullptr, 0,
-                            w_path.as<uint32_t>(), nullptr, st));
-        HIPCHK(launch_match(TM_MODE_COUNT, true, im, off, n, words, meta, counts, nullptr, nullptr, 0,
-                            w_path.as<uint32_t>(), nullptr, st));
+        int cmode = stats_enabled ? TM_MODE_STATS : TM_MODE_COUNT;
+        HIPCHK(launch_match(cmode, false, im, off, n, words, meta, counts, nullptr, nullptr, 0, path, sp, st));
+        HIPCHK(launch_match(cmode, true, im, off, n, words, meta, counts, nullptr, nullptr, 0, path, sp, st));
         timed_end(st, 1);
         timed(st, "scan", 2);
         HIPCHK(launch_scan(counts, n, out_off, total, w_scan.as<uint64_t>(), st));
         timed_end(st, 2);
-        if (stats_enabled) {
-            HIPCHK(hipMemsetAsync(w_stats.p, 0, 64, st));
-            unsigned long long* sp = w_stats.as<unsigned long long>();
-            // the STATS walk re-counts; it writes counts again (same values)
-            HIPCHK(launch_match(TM_MODE_STATS, false, im, off, n, words, meta, counts, nullptr, nullptr, 0,
-                                w_path.as<uint32_t>(), sp, st));
-            HIPCHK(launch_match(TM_MODE_STATS, true, im, off, n, words, meta, counts, nullptr, nullptr, 0,
-                                w_path.as<uint32_t>(), sp, st));
+        if (cap) {
+            timed(st, "match_emit", 3);
+            HIPCHK(launch_match(TM_MODE_EMIT, false, im, off, n, words, meta, nullptr, out_off, ids, cap, path,
+                                nullptr, st));
+            HIPCHK(launch_match(TM_MODE_EMIT, true, im, off, n, words, meta, nullptr, out_off, ids, cap, path,
+                                nullptr, st));
+            timed_end(st, 3);
         }
     }
-    // phase B: emit ids in reference order at the scanned offsets
-    void run_emit(const uint64_t* off, uint32_t n, const uint64_t* out_off, uint32_t* ids, uint64_t cap,
-                  hipStream_t st) {
-        ImageView im = view();
-        timed(st, "match_emit", 3);
-        HIPCHK(launch_match(TM_MODE_EMIT, false, im, off, n, w_words.as<uint32_t>(), w_meta.as<uint32_t>(),
-                            nullptr, out_off, ids, cap, w_path.as<uint32_t>(), nullptr, st));
-        HIPCHK(launch_match(TM_MODE_EMIT, true, im, off, n, w_words.as<uint32_t>(), w_meta.as<uint32_t>(),
-                            nullptr, out_off, ids, cap, w_path.as<uint32_t>(), nullptr, st));
-        timed_end(st, 3);
+    // look-back spin guard of the fused kernel (never expected to trip)
+    void check_fused_error() {
+        if (twopass || !w_ws.p) return;
+        unsigned long long err = 0;
+        HIPCHK(hipMemcpy(&err, w_ws.as<unsigned long long>() + 1, 8, hipMemcpyDeviceToHost));
+        if (err) throw DevError("fused match: look-back spin limit exceeded");
     }
     void finish_batch(hipStream_t st, uint32_t n) {
         if (!last_match_done) HIPCHK(hipEventCreateWithFlags(&last_match_done, hipEventDisableTiming));
@@ -837,19 +856,25 @@ int tm_match_batch(tm_engine* e, const uint8_t* topic_bytes, const uint64_t* top
         if (nbytes)
             HIPCHK(hipMemcpyAsync(e->w_bytes.p, topic_bytes + base, nbytes, hipMemcpyHostToDevice, st));
         HIPCHK(hipMemcpyAsync(e->w_off.p, rel.data(), (n + 1) * 8, hipMemcpyHostToDevice, st));
+        e->ensure_workspace(n, nbytes);
         uint64_t* d_total = e->w_total.as<uint64_t>();
-        e->ensure_workspace(n, nbytes, true);
-        d_total = e->w_total.as<uint64_t>();
-        e->run_count(e->w_bytes.as<uint8_t>(), e->w_off.as<uint64_t>(), n, nbytes, e->w_counts.as<uint32_t>(),
-                     e->w_outoff.as<uint64_t>(), d_total, st);
+        // ids go to an engine buffer sized from the previous batch; grow and
+        // rerun only when a batch needs more (the total is always exact)
+        uint64_t want = std::max<uint64_t>(e->w_ids.bytes / 4, std::min<uint64_t>(out_cap, (uint64_t)n * 16 + 1024));
+        e->w_ids.ensure(want * 4, 1.0);
+        uint64_t icap = e->w_ids.bytes / 4;
         uint64_t total = 0;
-        HIPCHK(hipMemcpyAsync(&total, d_total, 8, hipMemcpyDeviceToHost, st));
-        HIPCHK(hipStreamSynchronize(st));
-        uint64_t cap = std::min(total, out_cap);
-        if (cap) {
-            e->w_ids.ensure(cap * 4);
-            e->run_emit(e->w_off.as<uint64_t>(), n, e->w_outoff.as<uint64_t>(), e->w_ids.as<uint32_t>(), cap, st);
+        for (int pass = 0; pass < 2; ++pass) {
+            e->run_batch(e->w_bytes.as<uint8_t>(), e->w_off.as<uint64_t>(), n, nbytes, e->w_counts.as<uint32_t>(),
+                         e->w_outoff.as<uint64_t>(), e->w_ids.as<uint32_t>(), icap, d_total, st);
+            HIPCHK(hipMemcpyAsync(&total, d_total, 8, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipStreamSynchronize(st));
+            e->check_fused_error();
+            if (total <= icap || total > out_cap) break;
+            e->w_ids.ensure(total * 4, 1.25);
+            icap = e->w_ids.bytes / 4;
         }
+        uint64_t cap = std::min(total, out_cap);
         e->finish_batch(st, n);
         HIPCHK(hipMemcpyAsync(out_count, e->w_counts.p, (size_t)n * 4, hipMemcpyDeviceToHost, st));
         HIPCHK(hipMemcpyAsync(out_off, e->w_outoff.p, (size_t)(n + 1) * 8, hipMemcpyDeviceToHost, st));
@@ -879,8 +904,7 @@ int tm_match_batch_device(tm_engine* e, const uint8_t* d_bytes, const uint64_t* 
             HIPCHK(hipMemsetAsync(d_total, 0, 8, st));
             return TM_OK;
         }
-        e->run_count(d_bytes, d_off, n, topic_bytes, d_count, d_out_off, d_total, st);
-        if (out_cap) e->run_emit(d_off, n, d_out_off, d_ids, out_cap, st);
+        e->run_batch(d_bytes, d_off, n, topic_bytes, d_count, d_out_off, d_ids, out_cap, d_total, st);
         e->finish_batch(st, n);
         if (e->stats_enabled) {
             HIPCHK(hipStreamSynchronize(st));

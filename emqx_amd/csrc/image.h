@@ -25,8 +25,8 @@
 namespace tmx {
 
 constexpr uint32_t ROOT       = 0u;
-constexpr uint32_t NODE_MASK  = 0x3FFFFFFFu;   // node ids are 30-bit
-constexpr uint32_t NODE_NONE  = 0x3FFFFFFFu;
+constexpr uint32_t NODE_MASK  = 0x1FFFFFFFu;   // node ids are 29-bit (walk path packs 3 flag bits)
+constexpr uint32_t NODE_NONE  = 0x1FFFFFFFu;
 constexpr uint32_t HAS_LIT    = 0x80000000u;   // nodes[].plus bit31: has literal children
 constexpr uint32_t FILTER_NONE = 0xFFFFFFFFu;
 

@@ -18,6 +18,12 @@ hipError_t launch_match(int mode, bool long_topics, const ImageView& im, const u
                         const uint64_t* out_off, uint32_t* out, uint64_t out_cap,
                         uint32_t* path_scratch, unsigned long long* stats, hipStream_t st);
 size_t scan_tmp_elems(uint32_t n);
+size_t fused_ws_words(uint32_t n);
+size_t fused_stage_elems(uint32_t n, uint32_t K);
+hipError_t launch_fused(bool stats_mode, const ImageView& im, const uint8_t* bytes, const uint64_t* off,
+                        uint32_t n, uint32_t* words, uint32_t* path_scratch, uint32_t* stage, uint32_t K,
+                        uint32_t* counts, uint64_t* out_off, uint32_t* out, uint64_t out_cap, uint64_t* total,
+                        unsigned long long* ws, unsigned long long* stats, hipStream_t st);
 hipError_t launch_scan(const uint32_t* counts, uint32_t n, uint64_t* out_off, uint64_t* total,
                        uint64_t* tmp, hipStream_t st);
 

@@ -33,7 +33,7 @@ extern "C" {
 #define TM_EDEVICE  -3   /* no GPU / HIP error / engine opened host-only      */
 #define TM_ENOMEM   -4   /* host or device allocation failed                  */
 #define TM_ENOENT   -5   /* tm_lookup: no such trie node                      */
-#define TM_ERANGE   -6   /* image would exceed 2^30 nodes / 2^32 filters       */
+#define TM_ERANGE   -6   /* image would exceed 2^29-1 nodes / 2^32 filters       */
 
 #define TM_NO_FILTER 0xFFFFFFFFu
 
