@@ -48,6 +48,10 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=200_000, help="topics timed on the host (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=None)
     ap.add_argument("--check", type=int, default=20_000, help="topics checked bit-exactly vs the oracle")
+    ap.add_argument("--walk", default=None, help="walk variant (lane|tile256|tile512|tile1024|twopass)")
+    ap.add_argument("--ab", default=None, help="comma list of walk variants timed interleaved (extra report)")
+    ap.add_argument("--stage-k", type=int, default=None)
+    ap.add_argument("--layout", type=int, default=None, help="1 = DFS relayout on commit (default), 0 = off")
     return ap.parse_args()
 
 
@@ -68,6 +72,12 @@ def main():
     log("rank %d: generated %d filters (%.1f MB) in %.1fs" % (rank, n_filters, fo[-1] / 1e6, time.time() - t0))
     t0 = time.time()
     eng = Engine(device=local, filters_hint=n_filters)
+    if a.walk:
+        eng.set_walk(a.walk)
+    if a.stage_k:
+        eng.set_option("stage_k", a.stage_k)
+    if a.layout is not None:
+        eng.set_option("layout", a.layout)
     eng.insert_many(fb, fo)
     eng.commit()
     log("rank %d: trie built + committed in %.1fs: %d filters, %d nodes, image %.2f GB" % (
@@ -91,6 +101,10 @@ def main():
     eng.set_stats(False)
     total = int(d_t.item())
     cap = total + 1024
+    fan = np.sort(d_c.cpu().numpy().view(np.uint32))
+    fanout = {"mean": float(fan.mean()), "p50": int(fan[len(fan) // 2]), "p90": int(fan[int(len(fan) * 0.9)]),
+              "p99": int(fan[int(len(fan) * 0.99)]), "max": int(fan[-1])}
+    log("fan-out per topic: %s" % fanout)
     d_i = torch.empty(cap, dtype=torch.int32, device=dev)
 
     def step():
@@ -99,6 +113,25 @@ def main():
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize(dev)
+
+    if a.ab:
+        # interleaved A/B of walk variants on the same image and batch
+        # (rounds x variants, one process: methodology rule 24)
+        res = {v: [] for v in a.ab.split(",")}
+        for _ in range(5):
+            for v in res:
+                eng.set_walk(v)
+                step()
+                torch.cuda.synchronize(dev)
+                t1 = time.perf_counter()
+                for _ in range(3):
+                    step()
+                torch.cuda.synchronize(dev)
+                res[v].append((time.perf_counter() - t1) / 3 * 1e3)
+                assert int(d_t.item()) == total
+        log("A/B ms/step (median, min): " + ", ".join(
+            "%s %.2f/%.2f" % (v, sorted(x)[len(x) // 2], min(x)) for v, x in res.items()))
+        eng.set_walk(a.walk or "queue")
 
     # ---- timed region: K steps, kernel events recorded on the launch stream
     eng.set_timing(True)
@@ -155,7 +188,7 @@ def main():
         B = 8 * levels + 16 * stats["edge_reads"] + 4 * stats["matches"]   # SURVEY §8(d), per launch
         # dominant kernel = the longest stage (the fused walk; the emit walk
         # of the two-pass A/B variant); B is what one launch of it processes
-        kname = max(kms, key=kms.get) if kms else None
+        kname = max(kms, key=kms.get) if kms else None   # "walk" for the default queue pipeline
         walk_ms = kms.get(kname, 0.0) if kname else 0.0
         achieved = B / (walk_ms * 1e-3) / 1e9 if walk_ms > 0 else None
         out = {
@@ -177,7 +210,8 @@ def main():
                        "parallelism": "replicated trie x %d, topic batches sharded by rank" % world},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": None,
-                         "kernel": {"match_fused": "tm_match_fused (tokenize + NFA walk + look-back CSR)",
+                         "kernel": {"walk": "tm_walk_queue (globally balanced NFA walk)",
+                                    "match_fused": "tm_match_fused/lane (tokenize + NFA walk + look-back CSR)",
                                     "match_emit": "tm_match<EMIT> (two-pass emit walk)"}.get(kname, kname),
                          "kernel_ms": walk_ms,
                          "algorithmic_bytes_per_launch": B,
@@ -185,6 +219,7 @@ def main():
             "cpu_baseline": cpu,
             "kernel_ms": kms,
             "filter_hits_per_s": stats["matches"] * a.steps * world / dt,
+            "fanout": fanout,
             "parity_check": check_ok,
         }
         print(json.dumps(out), flush=True)

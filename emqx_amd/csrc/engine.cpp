@@ -33,7 +33,7 @@ using namespace tmx;
 
 namespace {
 
-constexpr size_t PAGE_ELEMS = 4096;  // 4096 x 16 B = 64 KiB dirty granule
+constexpr size_t PAGE_ELEMS = 4096;  // dirty granule: 4096 elements (64 KiB of 16 B slots, 128 KiB of nodes)
 
 struct DevError : std::runtime_error {
     using std::runtime_error::runtime_error;
@@ -114,7 +114,7 @@ struct NodeAux {
     uint32_t parent;      // parent node id (root: NODE_NONE)
     uint32_t word;        // word by which the parent reaches it (id, WORD_PLUS, WORD_HASH)
     uint32_t edge_count;  // #trie_node.edge_count
-    uint32_t lit_count;   // literal children (HAS_LIT flag <=> lit_count > 0)
+    uint32_t lit_count;   // literal children (HAS_LIT flag <=> lit_count > 0; LIT_TABLE once > INLINE_LIT)
 };
 
 struct FilterRec {
@@ -164,12 +164,16 @@ struct tm_engine {
     // ---- device image ----
     DevBuf d_nodes, d_edges, d_dict, d_arena, d_woff;
     bool dev_dirty = true;
+    int layout_mode = 1;              // option "layout": 0 off, 1 auto, 2 every commit (tests)
+    size_t created_since_layout = 0;  // nodes created since the last relayout
 
     // ---- match workspace ----
     DevBuf w_bytes, w_off, w_words, w_meta, w_counts, w_outoff, w_ids, w_scan, w_total, w_path, w_stats, w_stage,
         w_ws;
     bool twopass = false;     // TM_WALK=twopass: count walk + scan + emit walk (A/B only)
-    uint32_t stage_k = 128;   // TM_STAGE_K: ids staged per lane before a re-walk
+    int variant = TM_VARIANT_QUEUE;    // TM_WALK=lane|tile256|tile512|tile1024|queue
+    uint32_t stage_k = 512;   // TM_STAGE_K: ids staged per topic before a re-walk (rows are
+                              // written sparsely: HBM footprint, not traffic)
     hipEvent_t last_match_done = nullptr;
     bool match_in_flight = false;
     bool stats_enabled = false, timing_enabled = false;
@@ -184,10 +188,17 @@ struct tm_engine {
     std::vector<uint32_t> tmp_words;
 
     tm_engine() {
-        if (const char* v = std::getenv("TM_WALK")) twopass = std::strcmp(v, "twopass") == 0;
+        if (const char* v = std::getenv("TM_WALK")) {
+            twopass = std::strcmp(v, "twopass") == 0;
+            if (!std::strcmp(v, "lane")) variant = TM_VARIANT_LANE;
+            if (!std::strcmp(v, "tile256")) variant = TM_VARIANT_TILE256;
+            if (!std::strcmp(v, "tile512")) variant = TM_VARIANT_TILE512;
+            if (!std::strcmp(v, "tile1024")) variant = TM_VARIANT_TILE1024;
+            if (!std::strcmp(v, "queue")) variant = TM_VARIANT_QUEUE;
+        }
         if (const char* v = std::getenv("TM_STAGE_K")) {
             long k = std::atol(v);
-            if (k >= 1 && k <= 4096) stage_k = (uint32_t)k;
+            if (k >= 4 && k <= 4096 && !(k & 3)) stage_k = (uint32_t)k;
         }
         dict.assign(1024, DictSlot{0, WORD_NONE, 0});
         nodes.reserve(1024);
@@ -323,18 +334,72 @@ struct tm_engine {
             nodes.push_back(Node{});
             aux.push_back(NodeAux{});
         }
-        nodes[id] = Node{NODE_NONE, NODE_NONE, FILTER_NONE, FILTER_NONE};
+        nodes[id] = empty_node();
         aux[id] = NodeAux{parent, word, 0, 0};
         node_dirty.mark(id);
         ++live_nodes;
+        ++created_since_layout;
         return id;
     }
+    static Node empty_node() {
+        Node x;
+        x.plus = NODE_NONE;
+        x.hash = NODE_NONE;
+        x.hash_filter = FILTER_NONE;
+        x.self_filter = FILTER_NONE;
+        for (int i = 0; i < INLINE_LIT; ++i) {
+            x.lw[i] = WORD_NONE;
+            x.lc[i] = NODE_NONE;
+        }
+        return x;
+    }
     uint32_t child(uint32_t v, uint32_t w) const {
-        if (w == WORD_PLUS) return nodes[v].plus & NODE_MASK;
-        if (w == WORD_HASH) return nodes[v].hash;
-        if (!(nodes[v].plus & HAS_LIT)) return NODE_NONE;
+        const Node& x = nodes[v];
+        if (w == WORD_PLUS) return x.plus & NODE_MASK;
+        if (w == WORD_HASH) return x.hash;
+        if (!(x.plus & HAS_LIT)) return NODE_NONE;
+        if (!(x.plus & LIT_TABLE)) {
+            for (int i = 0; i < INLINE_LIT; ++i)
+                if (x.lw[i] == w) return x.lc[i];
+            return NODE_NONE;
+        }
         size_t s = edge_find_slot(v, w);
         return s == SIZE_MAX ? NODE_NONE : edges[s].child;
+    }
+    // literal child add / remove, keeping "LIT_TABLE set => every literal
+    // edge of v is in edges[], else all are inline"
+    void lit_add(uint32_t v, uint32_t w, uint32_t c) {
+        Node& x = nodes[v];
+        if (!(x.plus & LIT_TABLE)) {
+            for (int i = 0; i < INLINE_LIT; ++i)
+                if (x.lw[i] == WORD_NONE) {
+                    x.lw[i] = w;
+                    x.lc[i] = c;
+                    x.plus |= HAS_LIT;
+                    return;
+                }
+            for (int i = 0; i < INLINE_LIT; ++i) {  // spill the inline pairs to the table
+                edge_insert(v, x.lw[i], x.lc[i]);
+                x.lw[i] = WORD_NONE;
+                x.lc[i] = NODE_NONE;
+            }
+            nodes[v].plus |= LIT_TABLE;
+        }
+        edge_insert(v, w, c);
+        nodes[v].plus |= HAS_LIT;
+    }
+    void lit_remove(uint32_t v, uint32_t w) {
+        Node& x = nodes[v];
+        if (x.plus & LIT_TABLE) {
+            edge_erase(v, w);
+        } else {
+            for (int i = 0; i < INLINE_LIT; ++i)
+                if (x.lw[i] == w) {
+                    x.lw[i] = WORD_NONE;
+                    x.lc[i] = NODE_NONE;
+                }
+        }
+        if (--aux[v].lit_count == 0) nodes[v].plus &= ~PLUS_FLAGS;
     }
     // add_path/1 (emqx_trie.erl:104-117) for one (Node, Word, Child) triple:
     // a new edge bumps the parent's edge_count.
@@ -343,13 +408,12 @@ struct tm_engine {
         if (c != NODE_NONE) return c;
         c = new_node(v, w);
         if (w == WORD_PLUS) {
-            nodes[v].plus = (nodes[v].plus & HAS_LIT) | c;
+            nodes[v].plus = (nodes[v].plus & PLUS_FLAGS) | c;
         } else if (w == WORD_HASH) {
             nodes[v].hash = c;
         } else {
-            edge_insert(v, w, c);
+            lit_add(v, w, c);
             aux[v].lit_count++;
-            nodes[v].plus |= HAS_LIT;
         }
         aux[v].edge_count++;
         node_dirty.mark(v);
@@ -358,17 +422,16 @@ struct tm_engine {
     void unlink_child(uint32_t c) {
         uint32_t v = aux[c].parent, w = aux[c].word;
         if (w == WORD_PLUS) {
-            nodes[v].plus = (nodes[v].plus & HAS_LIT) | NODE_NONE;
+            nodes[v].plus = (nodes[v].plus & PLUS_FLAGS) | NODE_NONE;
         } else if (w == WORD_HASH) {
             nodes[v].hash = NODE_NONE;
             nodes[v].hash_filter = FILTER_NONE;
         } else {
-            edge_erase(v, w);
-            if (--aux[v].lit_count == 0) nodes[v].plus &= ~HAS_LIT;
+            lit_remove(v, w);
         }
         aux[v].edge_count--;
         node_dirty.mark(v);
-        nodes[c] = Node{NODE_NONE, NODE_NONE, FILTER_NONE, FILTER_NONE};
+        nodes[c] = empty_node();
         aux[c] = NodeAux{NODE_NONE, 0, 0, 0};
         node_dirty.mark(c);
         free_nodes.push_back(c);
@@ -452,6 +515,83 @@ struct tm_engine {
     }
 
     // ------------------------------------------------------------------
+    // DFS-preorder relayout: renumber the live nodes so that every subtree is
+    // a contiguous id range and a node's first child (its '+' child when it
+    // has one: the branch the walk takes first) directly follows it — two
+    // 32 B records share a 64 B line, and topics with a common prefix walk a
+    // compact region.  Deleted ids are dropped (compaction).  Filter ids are
+    // unchanged.
+    void relayout() {
+        const size_t N = nodes.size();
+        // literal children per node (inline pairs or table edges), CSR
+        std::vector<uint32_t> start(N + 1, 0);
+        for (size_t v = 0; v < N; ++v) {
+            if (aux[v].parent == NODE_NONE && v != ROOT) continue;  // free slot
+            if ((nodes[v].plus & HAS_LIT) && !(nodes[v].plus & LIT_TABLE))
+                for (int i = 0; i < INLINE_LIT; ++i) start[v + 1] += nodes[v].lw[i] != WORD_NONE;
+        }
+        for (const EdgeSlot& e : edges)
+            if (e.parent != EDGE_EMPTY) start[e.parent + 1]++;
+        for (size_t v = 0; v < N; ++v) start[v + 1] += start[v];
+        std::vector<uint32_t> kids(start[N]);
+        {
+            std::vector<uint32_t> fill(start.begin(), start.end() - 1);
+            for (size_t v = 0; v < N; ++v) {
+                if (aux[v].parent == NODE_NONE && v != ROOT) continue;
+                if ((nodes[v].plus & HAS_LIT) && !(nodes[v].plus & LIT_TABLE))
+                    for (int i = 0; i < INLINE_LIT; ++i)
+                        if (nodes[v].lw[i] != WORD_NONE) kids[fill[v]++] = nodes[v].lc[i];
+            }
+            for (const EdgeSlot& e : edges)
+                if (e.parent != EDGE_EMPTY) kids[fill[e.parent]++] = e.child;
+        }
+        // preorder: v, '+' subtree, literal subtrees, '#' subtree
+        std::vector<uint32_t> newid(N, NODE_NONE), order;
+        order.reserve(live_nodes);
+        std::vector<uint32_t> stack;
+        stack.push_back(ROOT);
+        while (!stack.empty()) {
+            uint32_t v = stack.back();
+            stack.pop_back();
+            newid[v] = (uint32_t)order.size();
+            order.push_back(v);
+            if (nodes[v].hash != NODE_NONE) stack.push_back(nodes[v].hash);
+            for (uint32_t k = start[v + 1]; k > start[v]; --k) stack.push_back(kids[k - 1]);
+            uint32_t pc = nodes[v].plus & NODE_MASK;
+            if (pc != NODE_NONE) stack.push_back(pc);
+        }
+        std::vector<uint32_t>().swap(kids);
+        std::vector<uint32_t>().swap(start);
+        auto remap = [&](uint32_t id) { return id == NODE_NONE ? NODE_NONE : newid[id]; };
+        std::vector<Node> nn(order.size());
+        std::vector<NodeAux> na(order.size());
+        for (size_t i = 0; i < order.size(); ++i) {
+            Node x = nodes[order[i]];
+            x.plus = (x.plus & PLUS_FLAGS) | remap(x.plus & NODE_MASK);
+            x.hash = remap(x.hash);
+            for (int k = 0; k < INLINE_LIT; ++k) x.lc[k] = remap(x.lc[k]);
+            nn[i] = x;
+            NodeAux a = aux[order[i]];
+            a.parent = remap(a.parent);
+            na[i] = a;
+        }
+        // literal edge table with the new ids
+        std::vector<EdgeSlot> old;
+        old.swap(edges);
+        edges.assign(old.size(), EdgeSlot{EDGE_EMPTY, 0, 0, 0});
+        for (const EdgeSlot& e : old)
+            if (e.parent != EDGE_EMPTY) edge_place(EdgeSlot{newid[e.parent], e.word, newid[e.child], 0});
+        for (FilterRec& f : filters)
+            if (f.node != NODE_NONE) f.node = newid[f.node];
+        nodes.swap(nn);
+        aux.swap(na);
+        free_nodes.clear();
+        created_since_layout = 0;
+        node_dirty.all = true;
+        edge_dirty.all = true;
+    }
+
+    // ------------------------------------------------------------------
     // device image
     struct Guard {
         int prev = -1;
@@ -505,7 +645,13 @@ struct tm_engine {
         }
     }
 
+    void maybe_relayout() {
+        if (layout_mode == 2 || (layout_mode == 1 && live_nodes >= 4096 && created_since_layout * 4 >= live_nodes))
+            relayout();
+    }
+
     void commit() {
+        if (dev_dirty || !d_nodes.p) maybe_relayout();
         if (device < 0) {
             ++epoch;
             dev_dirty = false;
@@ -574,6 +720,11 @@ struct tm_engine {
         if (twopass) {
             w_meta.ensure((size_t)(n + 1) * 4);
             w_scan.ensure(scan_tmp_elems(n) * 8 + 8);
+        } else if (variant == TM_VARIANT_QUEUE) {
+            w_meta.ensure((size_t)(n + 1) * 4);
+            w_scan.ensure(scan_tmp_elems(n) * 8 + 8);
+            w_stage.ensure(((size_t)n * stage_k + 1) * 4);
+            w_ws.ensure(64);
         } else {
             w_stage.ensure(fused_stage_elems(n, stage_k) * 4);
             w_ws.ensure(fused_ws_words(n) * 8);
@@ -590,9 +741,26 @@ struct tm_engine {
         uint32_t* path = w_path.as<uint32_t>();
         unsigned long long* sp = w_stats.as<unsigned long long>();
         if (stats_enabled) HIPCHK(hipMemsetAsync(w_stats.p, 0, 64, st));
+        if (!twopass && variant == TM_VARIANT_QUEUE) {
+            static const char* kStage[4] = {"tokenize", "walk", "scan", "copy_out"};
+            hipEvent_t marks[8];
+            if (timing_enabled)
+                for (int i = 0; i < 4; ++i) {
+                    ev_cur[i] = take_event(kStage[i]);
+                    marks[2 * i] = ev_cur[i].a;
+                    marks[2 * i + 1] = ev_cur[i].b;
+                }
+            HIPCHK(launch_queue(stats_enabled, im, bytes, off, n, words, w_meta.as<uint32_t>(), path,
+                                w_stage.as<uint32_t>(), stage_k, counts, out_off, ids, cap, total,
+                                w_scan.as<uint64_t>(), w_ws.as<unsigned long long>(), sp, st,
+                                timing_enabled ? marks : nullptr));
+            if (timing_enabled)
+                for (int i = 0; i < 4; ++i) ev_pending.push_back(ev_cur[i]);
+            return;
+        }
         if (!twopass) {
             timed(st, "match_fused", 0);
-            HIPCHK(launch_fused(stats_enabled, im, bytes, off, n, words, path, w_stage.as<uint32_t>(), stage_k,
+            HIPCHK(launch_fused(variant, stats_enabled, im, bytes, off, n, words, path, w_stage.as<uint32_t>(), stage_k,
                                 counts, out_off, ids, cap, total, w_ws.as<unsigned long long>(), sp, st));
             timed_end(st, 0);
             return;
@@ -620,7 +788,7 @@ struct tm_engine {
     }
     // look-back spin guard of the fused kernel (never expected to trip)
     void check_fused_error() {
-        if (twopass || !w_ws.p) return;
+        if (twopass || variant == TM_VARIANT_QUEUE || !w_ws.p) return;
         unsigned long long err = 0;
         HIPCHK(hipMemcpy(&err, w_ws.as<unsigned long long>() + 1, 8, hipMemcpyDeviceToHost));
         if (err) throw DevError("fused match: look-back spin limit exceeded");
@@ -688,7 +856,7 @@ inline void split_levels(const uint8_t* p, uint32_t len, std::vector<std::pair<u
 
 extern "C" {
 
-const char* tm_build_info(void) { return "libtopicmatch gfx950 (CDNA4) HIP; image v1 (node16/edge16x4/dict16)"; }
+const char* tm_build_info(void) { return "libtopicmatch gfx950 (CDNA4) HIP; image v2 (node32+2 inline/edge16x4/dict16)"; }
 
 const char* tm_strerror(int code) {
     switch (code) {
@@ -719,7 +887,8 @@ int tm_open(const tm_config* cfg, tm_engine** out) {
         size_t nodes_hint = (size_t)cfg->filters_hint * 3;
         e->nodes.reserve(nodes_hint);
         e->aux.reserve(nodes_hint);
-        e->edges.assign(next_pow2(nodes_hint * 2), EdgeSlot{EDGE_EMPTY, 0, 0, 0});
+        // only wide nodes (> INLINE_LIT literal children) use the edge table
+        e->edges.assign(next_pow2(nodes_hint / 2), EdgeSlot{EDGE_EMPTY, 0, 0, 0});
     }
     if (dev >= 0) {
         int ndev = 0;
@@ -912,6 +1081,29 @@ int tm_match_batch_device(tm_engine* e, const uint8_t* d_bytes, const uint64_t* 
             e->collect_stats();
         }
         return TM_OK;
+    });
+}
+
+int tm_set_option(tm_engine* e, const char* name, int64_t value) {
+    if (!name) return TM_EINVAL;
+    return guarded(e, [&]() -> int {
+        if (!std::strcmp(name, "walk")) {
+            if (value < 0 || value > 5) return TM_EINVAL;
+            e->twopass = value == 4;
+            if (value != 4) e->variant = (int)value;
+            return TM_OK;
+        }
+        if (!std::strcmp(name, "layout")) {
+            if (value < 0 || value > 2) return TM_EINVAL;
+            e->layout_mode = (int)value;
+            return TM_OK;
+        }
+        if (!std::strcmp(name, "stage_k")) {
+            if (value < 4 || value > 4096 || (value & 3)) return TM_EINVAL;
+            e->stage_k = (uint32_t)value;
+            return TM_OK;
+        }
+        return TM_EINVAL;
     });
 }
 

@@ -8,14 +8,17 @@
 // with node ids = full path binaries.  Here node ids are dense u32 and words
 // are interned u32, so every probe is a fixed-size integer compare:
 //
-//   nodes[]  16 B per node: the '+' edge and the '#' edge are ARRAY READS
-//            (fields of the parent), the filter ending at the node and the
-//            filter ending at its '#' child are carried inline, so the
-//            reference's 'match_#'/2 (emqx_trie.erl:140-145) costs nothing
-//            beyond the node read.
-//   edges[]  literal edges only, open addressing, 16 B slots grouped in
-//            64 B buckets (one HBM burst), linear probing over slots from the
-//            home bucket's first slot, load <= 1/2.
+//   nodes[]  32 B per node (half an HBM burst): the '+' edge and the '#'
+//            edge are ARRAY READS (fields of the parent), the filter ending at
+//            the node and the filter ending at its '#' child are carried
+//            inline, so the reference's 'match_#'/2 (emqx_trie.erl:140-145)
+//            costs nothing beyond the node read; up to INLINE_LIT literal
+//            children live in the record too, so the deep, narrow part of the
+//            trie (most of the walk) needs no hash probe at all.
+//   edges[]  literal edges of the wide nodes (> INLINE_LIT literal
+//            children, flag LIT_TABLE), open addressing, 16 B slots grouped
+//            in 64 B buckets (one HBM burst), linear probing over slots from
+//            the home bucket's first slot, load <= 1/2.
 //   dict[]   word dictionary: 64-bit hash -> word id, byte-verified against
 //            the word arena, so tokenisation is collision-free (no hash-only
 //            identity).
@@ -28,6 +31,9 @@ constexpr uint32_t ROOT       = 0u;
 constexpr uint32_t NODE_MASK  = 0x1FFFFFFFu;   // node ids are 29-bit (walk path packs 3 flag bits)
 constexpr uint32_t NODE_NONE  = 0x1FFFFFFFu;
 constexpr uint32_t HAS_LIT    = 0x80000000u;   // nodes[].plus bit31: has literal children
+constexpr uint32_t LIT_TABLE  = 0x40000000u;   // nodes[].plus bit30: they live in edges[] (else inline)
+constexpr uint32_t PLUS_FLAGS = HAS_LIT | LIT_TABLE;
+constexpr int      INLINE_LIT = 2;             // literal children kept in the node record
 constexpr uint32_t FILTER_NONE = 0xFFFFFFFFu;
 
 // token ids produced by the tokenizer (emqx_topic:words/1 + word/1)
@@ -39,11 +45,13 @@ constexpr uint32_t WORD_MAX   = 0xFFFFFFF0u;   // interned ids are < WORD_MAX
 constexpr uint32_t EDGE_EMPTY = 0xFFFFFFFFu;   // slot.parent of an empty slot
 constexpr int      SLOTS_PER_BUCKET = 4;       // 4 x 16 B = 64 B
 
-struct alignas(16) Node {
-    uint32_t plus;         // '+' child node id (| HAS_LIT flag), NODE_NONE if none
+struct alignas(32) Node {
+    uint32_t plus;         // '+' child node id | HAS_LIT | LIT_TABLE, NODE_NONE if none
     uint32_t hash;         // '#' child node id, NODE_NONE if none
     uint32_t hash_filter;  // filter id of the '#' child (its topic), FILTER_NONE if none
     uint32_t self_filter;  // filter id ending at this node, FILTER_NONE if topic = undefined
+    uint32_t lw[INLINE_LIT];  // inline literal children: word ids (WORD_NONE = empty slot)
+    uint32_t lc[INLINE_LIT];  //   and child node ids; unused when LIT_TABLE is set
 };
 
 struct alignas(16) EdgeSlot {

@@ -162,6 +162,14 @@ class Engine:
                                             p(d_ids), out_cap, p(d_total), st)
         return self._check(rc, "tm_match_batch_device")
 
+    WALKS = {"lane": 0, "tile256": 1, "tile512": 2, "tile1024": 3, "twopass": 4, "queue": 5}
+
+    def set_option(self, name: str, value: int):
+        self._check(self.lib.tm_set_option(self.h, name.encode(), int(value)), "tm_set_option(%s)" % name)
+
+    def set_walk(self, walk: str):
+        self.set_option("walk", self.WALKS[walk])
+
     # -- instrumentation ----------------------------------------------------
     def set_stats(self, on=True):
         self._check(self.lib.tm_set_stats(self.h, 1 if on else 0), "tm_set_stats")

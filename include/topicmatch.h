@@ -127,6 +127,17 @@ int tm_match_batch_device(tm_engine* e, const uint8_t* d_topic_bytes, const uint
                           uint64_t* d_out_off, uint32_t* d_out_filter_id, uint64_t out_cap,
                           uint64_t* d_total, void* hip_stream);
 
+/* Engine knobs (the app-env analogue of SURVEY §5 config):
+ *   "walk"     5 = queue (default: tokenize, globally balanced walk, scan,
+ *              coalesced copy-out), 0 = lane-per-topic fused, 1/2/3 = tiled
+ *              fused (256/512/1024 topics per tile), 4 = two-pass
+ *   "layout"   1 = renumber nodes in DFS preorder on commit once >= 1/4 of
+ *              the live nodes are new (default), 0 = keep insertion order,
+ *              2 = renumber on every commit
+ *   "stage_k"  ids staged per topic before a fan-out re-walk (4..4096, % 4 == 0)
+ * TM_EINVAL for unknown names / values. */
+int tm_set_option(tm_engine* e, const char* name, int64_t value);
+
 /* Counters of the last batch (visits, reference edge reads, matches).  Costs
  * one extra device pass; enable with tm_set_stats(e, 1) before the batch. */
 int tm_set_stats(tm_engine* e, int enable);

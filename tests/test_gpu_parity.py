@@ -140,7 +140,9 @@ def test_c5_sample_vs_o1(gpu_device):
     e.close()
 
 
-def test_deltas_between_batches(eng):
+@pytest.mark.parametrize("layout", [0, 2])
+def test_deltas_between_batches(eng, layout):
+    eng.set_option("layout", layout)
     rng = random.Random(77)
     py = pytrie.Trie()
     pool = ["/".join(rng.choice(["a", "b", "+", "", "$x"]) for _ in range(rng.randint(1, 5))) +
@@ -168,7 +170,7 @@ def test_enospc_reports_needed(eng):
         eng.match_batch(buf, off, out_cap=2)
     assert ei.value.code == _lib.TM_ENOSPC
     c, o, ids = eng.match_batch(buf, off)
-    assert list(c) == [4, 3] and int(o[-1]) == 7
+    assert list(c) == [4, 4] and int(o[-1]) == 8   # "+/+/#" matches a/x: "#" takes zero levels
 
 
 def test_empty_batch_and_empty_topic(eng):
@@ -217,4 +219,28 @@ def test_stats_edge_reads_match_oracle(gpu_device, golden):
     st = e.last_stats()
     assert st["edge_reads"] == sum(r["edge_reads"] for r in vec["topics"])
     assert st["matches"] == sum(len(r["match"]) for r in vec["topics"])
+    e.close()
+
+
+@pytest.mark.parametrize("walk", ["queue", "lane", "tile256", "tile512", "tile1024", "twopass"])
+def test_every_walk_variant_bit_exact(gpu_device, golden, walk):
+    """each kernel variant (A/B knobs) against the committed vectors and C1"""
+    for vec in golden["o1_vectors"]:
+        e = Engine(device=gpu_device)
+        e.set_walk(walk)
+        e.set_option("stage_k", 4)          # force the fan-out re-walk path too
+        for f in vec["filters"]:
+            e.insert(b(f))
+        got = e.match([b(r["topic"]) for r in vec["topics"]])
+        for row, g in zip(vec["topics"], got):
+            assert [x.decode(L1) for x in g] == row["match"], (walk, vec["name"], row["topic"])
+        e.close()
+    fb, fo = W.filters(1)
+    o1 = O1()
+    o1.insert_many(fb, fo)
+    e = Engine(device=gpu_device)
+    e.set_walk(walk)
+    e.insert_many(fb, fo)
+    tb, to = W.topics(1, n=30000)
+    _by_id(o1, e, tb, to)
     e.close()

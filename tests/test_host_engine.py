@@ -137,3 +137,29 @@ def test_router_kat_host_side(golden):
                 r.del_route(b(topic), dest)
             node, exp = kat["lookup_after"]
             assert r.engine.lookup(b(node)) == exp
+
+
+def test_relayout_preserves_bookkeeping():
+    """DFS-preorder relayout on every commit (layout=2) keeps emqx_trie's
+    bookkeeping (edge_count, topic) and the filter ids intact"""
+    rng = random.Random(31)
+    for _ in range(25):
+        e, py = kat_engine(), pytrie.Trie()
+        e.set_option("layout", 2)
+        pool = [b"/".join(rng.choice([b"a", b"b", b"", b"+", b"#", b"$x", b"c", b"d", b"e"])
+                          for _ in range(rng.randint(1, 6))) for _ in range(rng.randint(5, 120))]
+        for step in range(300):
+            f = rng.choice(pool)
+            if rng.random() < 0.6:
+                e.insert(f)
+                py.insert(f)
+            else:
+                e.delete(f)
+                py.delete(f)
+            if step % 37 == 0:
+                e.commit()
+        e.commit()
+        for f in pool:
+            for nid in _prefixes(f):
+                assert e.lookup(nid) == py.lookup(nid), nid
+        e.close()
