@@ -32,3 +32,11 @@ clean:
 	rm -rf $(BUILD) emqx_amd/libtopicmatch.so emqx_amd/libtmwork.so oracle/liboracle.so
 
 .PHONY: all clean
+
+# Erlang NIF shim (needs OTP's erl_nif.h; not present in this image):
+#   make nif ERL_INCLUDE=/usr/lib/erlang/usr/include
+nif: emqx_amd/libtopicmatch.so
+	@test -n "$(ERL_INCLUDE)" || (echo "set ERL_INCLUDE to the directory holding erl_nif.h" && false)
+	$(CC) -O2 -fPIC -shared -I$(ERL_INCLUDE) emqx_amd/csrc/emqx_trie_nif.c -Lemqx_amd -ltopicmatch \
+	  -Wl,-rpath,'$$ORIGIN' -o emqx_amd/emqx_trie_nif.so
+.PHONY: nif

@@ -27,6 +27,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from emqx_amd import Engine  # noqa: E402
+from emqx_amd import multi  # noqa: E402
 from emqx_amd import workload as W  # noqa: E402
 
 METRIC = "topic matches/sec (whole node) at 10M wildcard filters; % HBM roofline"
@@ -57,9 +58,7 @@ def parse():
 
 def main():
     a = parse()
-    rank = int(os.environ.get("RANK", 0))
-    world = int(os.environ.get("WORLD_SIZE", 1))
-    local = int(os.environ.get("LOCAL_RANK", 0))
+    rank, world, local = multi.env_rank()
     if world > 1:
         dist.init_process_group("nccl" if torch.cuda.is_available() else "gloo")
     torch.cuda.set_device(local)
@@ -83,7 +82,7 @@ def main():
     log("rank %d: trie built + committed in %.1fs: %d filters, %d nodes, image %.2f GB" % (
         rank, time.time() - t0, eng.filter_count, eng.node_count, eng.image_bytes / 1e9))
 
-    tb, to = W.topics(a.config, n=a.topics, stream=rank)
+    tb, to = W.topics(a.config, n=a.topics, stream=multi.topic_stream(rank))
     n = len(to) - 1
     nbytes = int(to[-1])
     d_b = torch.from_numpy(tb).to(dev)
@@ -133,24 +132,12 @@ def main():
             "%s %.2f/%.2f" % (v, sorted(x)[len(x) // 2], min(x)) for v, x in res.items()))
         eng.set_walk(a.walk or "queue")
 
-    # ---- timed region: K steps, kernel events recorded on the launch stream
+    # ---- timed region: K steps, kernel events recorded on the launch stream;
+    # barrier + sync on both sides, max over ranks (emqx_amd/multi.py)
     eng.set_timing(True)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t_start = time.perf_counter()
-    for _ in range(a.steps):
-        step()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t_start
+    dt = multi.timed_region(step, a.steps, lambda: torch.cuda.synchronize(dev))
     kms = eng.last_kernel_times()
     eng.set_timing(False)
-    if world > 1:
-        tt = torch.tensor([dt], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
     assert int(d_t.item()) == total, "match total changed between steps"
 
     # ---- bit-exact spot check of this rank's batch against the oracle

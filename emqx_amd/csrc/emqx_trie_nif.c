@@ -1,0 +1,229 @@
+/*
+ * emqx_trie_nif.c — Erlang NIF binding of libtopicmatch (include/topicmatch.h):
+ * the reference-side drop-in for emqx_trie:match/1 and the trie deltas.
+ * Built only where OTP's erl_nif.h is available (`make nif ERL_INCLUDE=...`);
+ * this image has no Erlang runtime.  The Erlang wrapper that loads it is in
+ * INTEGRATION.md.
+ *
+ *   emqx_trie_nif:open(Device)                -> {ok, Engine} | {error, Reason}
+ *   emqx_trie_nif:insert(Engine, Filter)      -> ok          emqx_trie:insert/1  (src/emqx_trie.erl:62-73)
+ *   emqx_trie_nif:delete(Engine, Filter)      -> ok          emqx_trie:delete/1  (src/emqx_trie.erl:88-96)
+ *   emqx_trie_nif:lookup(Engine, NodeId)      -> [] | [{EdgeCount, Topic | undefined}]
+ *                                                           emqx_trie:lookup/1  (src/emqx_trie.erl:83-84)
+ *   emqx_trie_nif:commit(Engine)              -> {ok, Epoch} (transaction commit -> HBM image)
+ *   emqx_trie_nif:match(Engine, Topic)        -> [Filter]    emqx_trie:match/1   (src/emqx_trie.erl:77-79)
+ *   emqx_trie_nif:match_many(Engine, [Topic]) -> [[Filter]]  one GPU batch for many publishes
+ *
+ * Conventions: bad input -> badarg; engine errors ->
+ * {error, Atom}; the engine handle is a resource; GPU calls run on dirty IO
+ * schedulers so a batch never blocks a normal scheduler.
+ */
+#include <erl_nif.h>
+#include <string.h>
+
+#include "../../include/topicmatch.h"
+
+static ErlNifResourceType* ENGINE_RT = NULL;
+
+typedef struct {
+    tm_engine* e;
+    ErlNifMutex* mu;
+} engine_res;
+
+static ERL_NIF_TERM atom(ErlNifEnv* env, const char* name) {
+    ERL_NIF_TERM a;
+    if (enif_make_existing_atom(env, name, &a, ERL_NIF_LATIN1)) return a;
+    return enif_make_atom(env, name);
+}
+
+static ERL_NIF_TERM error_tuple(ErlNifEnv* env, int code) {
+    const char* why = "device";
+    switch (code) {
+        case TM_EINVAL: why = "einval"; break;
+        case TM_ENOSPC: why = "enospc"; break;
+        case TM_ENOMEM: why = "enomem"; break;
+        case TM_ERANGE: why = "erange"; break;
+        default: why = "edevice"; break;
+    }
+    return enif_make_tuple2(env, atom(env, "error"), atom(env, why));
+}
+
+static void engine_dtor(ErlNifEnv* env, void* obj) {
+    (void)env;
+    engine_res* r = (engine_res*)obj;
+    if (r->e) tm_close(r->e);
+    if (r->mu) enif_mutex_destroy(r->mu);
+}
+
+static int load(ErlNifEnv* env, void** priv, ERL_NIF_TERM info) {
+    (void)priv;
+    (void)info;
+    ENGINE_RT = enif_open_resource_type(env, NULL, "tm_engine", engine_dtor, ERL_NIF_RT_CREATE, NULL);
+    return ENGINE_RT ? 0 : -1;
+}
+
+static int get_engine(ErlNifEnv* env, ERL_NIF_TERM t, engine_res** out) {
+    return enif_get_resource(env, t, ENGINE_RT, (void**)out) && (*out)->e != NULL;
+}
+
+static ERL_NIF_TERM nif_open(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    int dev;
+    if (argc != 1 || !enif_get_int(env, argv[0], &dev)) return enif_make_badarg(env);
+    tm_config cfg;
+    memset(&cfg, 0, sizeof(cfg));
+    cfg.device = dev;
+    engine_res* r = (engine_res*)enif_alloc_resource(ENGINE_RT, sizeof(engine_res));
+    r->e = NULL;
+    r->mu = enif_mutex_create("tm_engine");
+    int rc = tm_open(&cfg, &r->e);
+    if (rc != TM_OK) {
+        enif_release_resource(r);
+        return error_tuple(env, rc);
+    }
+    ERL_NIF_TERM term = enif_make_resource(env, r);
+    enif_release_resource(r);
+    return enif_make_tuple2(env, atom(env, "ok"), term);
+}
+
+static ERL_NIF_TERM nif_filter_op(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[], int is_insert) {
+    engine_res* r;
+    ErlNifBinary b;
+    if (argc != 2 || !get_engine(env, argv[0], &r) || !enif_inspect_binary(env, argv[1], &b))
+        return enif_make_badarg(env);
+    enif_mutex_lock(r->mu);
+    int rc = is_insert ? tm_insert(r->e, b.data, (uint32_t)b.size) : tm_delete(r->e, b.data, (uint32_t)b.size);
+    enif_mutex_unlock(r->mu);
+    return rc == TM_OK ? atom(env, "ok") : error_tuple(env, rc);
+}
+
+static ERL_NIF_TERM nif_insert(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    return nif_filter_op(env, argc, argv, 1);
+}
+static ERL_NIF_TERM nif_delete(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    return nif_filter_op(env, argc, argv, 0);
+}
+
+static ERL_NIF_TERM filter_binary(ErlNifEnv* env, tm_engine* e, uint32_t fid) {
+    uint32_t len = 0;
+    const uint8_t* p = tm_filter_bytes(e, fid, &len);
+    ERL_NIF_TERM bin;
+    unsigned char* d = enif_make_new_binary(env, len, &bin);
+    if (len) memcpy(d, p, len);
+    return bin;
+}
+
+static ERL_NIF_TERM nif_lookup(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    engine_res* r;
+    ErlNifBinary b;
+    if (argc != 2 || !get_engine(env, argv[0], &r) || !enif_inspect_binary(env, argv[1], &b))
+        return enif_make_badarg(env);
+    tm_node_info info;
+    enif_mutex_lock(r->mu);
+    int rc = tm_lookup(r->e, b.data, (uint32_t)b.size, &info);
+    ERL_NIF_TERM res;
+    if (rc == TM_ENOENT) {
+        res = enif_make_list(env, 0);
+    } else if (rc != TM_OK) {
+        res = error_tuple(env, rc);
+    } else {
+        ERL_NIF_TERM topic = info.filter_id == TM_NO_FILTER ? atom(env, "undefined")
+                                                             : filter_binary(env, r->e, info.filter_id);
+        res = enif_make_list1(env, enif_make_tuple2(env, enif_make_uint(env, info.edge_count), topic));
+    }
+    enif_mutex_unlock(r->mu);
+    return res;
+}
+
+static ERL_NIF_TERM nif_commit(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    engine_res* r;
+    if (argc != 1 || !get_engine(env, argv[0], &r)) return enif_make_badarg(env);
+    uint64_t epoch = 0;
+    enif_mutex_lock(r->mu);
+    int rc = tm_commit(r->e, &epoch);
+    enif_mutex_unlock(r->mu);
+    if (rc != TM_OK) return error_tuple(env, rc);
+    return enif_make_tuple2(env, atom(env, "ok"), enif_make_uint64(env, epoch));
+}
+
+/* match over a list of topic binaries -> list of lists (reference order) */
+static ERL_NIF_TERM match_list(ErlNifEnv* env, engine_res* r, ERL_NIF_TERM list, unsigned n, int single) {
+    ErlNifBinary* bins = (ErlNifBinary*)enif_alloc(sizeof(ErlNifBinary) * (n ? n : 1));
+    uint64_t* off = (uint64_t*)enif_alloc(sizeof(uint64_t) * (n + 1));
+    ERL_NIF_TERM head, tail = list;
+    uint64_t total_bytes = 0;
+    for (unsigned i = 0; i < n; ++i) {
+        if (!enif_get_list_cell(env, tail, &head, &tail) || !enif_inspect_binary(env, head, &bins[i])) {
+            enif_free(bins);
+            enif_free(off);
+            return enif_make_badarg(env);
+        }
+        total_bytes += bins[i].size;
+    }
+    uint8_t* buf = (uint8_t*)enif_alloc(total_bytes + 8);
+    off[0] = 0;
+    for (unsigned i = 0; i < n; ++i) {
+        memcpy(buf + off[i], bins[i].data, bins[i].size);
+        off[i + 1] = off[i] + bins[i].size;
+    }
+    uint32_t* counts = (uint32_t*)enif_alloc(sizeof(uint32_t) * (n ? n : 1));
+    uint64_t* out_off = (uint64_t*)enif_alloc(sizeof(uint64_t) * (n + 1));
+    uint64_t cap = (uint64_t)n * 32 + 64, need = 0;
+    uint32_t* ids = (uint32_t*)enif_alloc(sizeof(uint32_t) * cap);
+    enif_mutex_lock(r->mu);
+    int rc = tm_match_batch(r->e, buf, off, n, counts, out_off, ids, cap, &need);
+    if (rc == TM_ENOSPC) {
+        enif_free(ids);
+        cap = need;
+        ids = (uint32_t*)enif_alloc(sizeof(uint32_t) * (cap ? cap : 1));
+        rc = tm_match_batch(r->e, buf, off, n, counts, out_off, ids, cap, &need);
+    }
+    ERL_NIF_TERM res;
+    if (rc != TM_OK) {
+        res = error_tuple(env, rc);
+    } else {
+        ERL_NIF_TERM* rows = (ERL_NIF_TERM*)enif_alloc(sizeof(ERL_NIF_TERM) * (n ? n : 1));
+        for (unsigned i = 0; i < n; ++i) {
+            uint32_t c = counts[i];
+            ERL_NIF_TERM* cells = (ERL_NIF_TERM*)enif_alloc(sizeof(ERL_NIF_TERM) * (c ? c : 1));
+            for (uint32_t k = 0; k < c; ++k) cells[k] = filter_binary(env, r->e, ids[out_off[i] + k]);
+            rows[i] = enif_make_list_from_array(env, cells, c);
+            enif_free(cells);
+        }
+        res = single ? rows[0] : enif_make_list_from_array(env, rows, n);
+        enif_free(rows);
+    }
+    enif_mutex_unlock(r->mu);
+    enif_free(ids);
+    enif_free(out_off);
+    enif_free(counts);
+    enif_free(buf);
+    enif_free(off);
+    enif_free(bins);
+    return res;
+}
+
+static ERL_NIF_TERM nif_match(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    engine_res* r;
+    if (argc != 2 || !get_engine(env, argv[0], &r) || !enif_is_binary(env, argv[1])) return enif_make_badarg(env);
+    return match_list(env, r, enif_make_list1(env, argv[1]), 1, 1);
+}
+
+static ERL_NIF_TERM nif_match_many(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    engine_res* r;
+    unsigned n;
+    if (argc != 2 || !get_engine(env, argv[0], &r) || !enif_get_list_length(env, argv[1], &n))
+        return enif_make_badarg(env);
+    return match_list(env, r, argv[1], n, 0);
+}
+
+static ErlNifFunc funcs[] = {
+    {"open", 1, nif_open, 0},
+    {"insert", 2, nif_insert, 0},
+    {"delete", 2, nif_delete, 0},
+    {"lookup", 2, nif_lookup, 0},
+    {"commit", 1, nif_commit, ERL_NIF_DIRTY_JOB_IO_BOUND},
+    {"match", 2, nif_match, ERL_NIF_DIRTY_JOB_IO_BOUND},
+    {"match_many", 2, nif_match_many, ERL_NIF_DIRTY_JOB_IO_BOUND},
+};
+
+ERL_NIF_INIT(emqx_trie_nif, funcs, load, NULL, NULL, NULL)

@@ -1,0 +1,63 @@
+"""Multi-GPU plumbing of the topic-routing engine (one process per GPU).
+
+The hot path shards by publish topic: every GPU holds a full replica of the
+trie image (10M filters are ~1 GB of HBM of the 288 GB) and matches its own
+topic batches, so the data path needs NO collective (SURVEY.md §8(e),
+"replicated").  torch.distributed (RCCL on ROCm, gloo on CPU) is used only
+for the control plane around a measured region: a barrier, and the max of
+the per-rank step times.
+
+The sharded-filter mode of config C4 (filters partitioned by root word, match
+sets all-gathered over xGMI) is a next-round item; `root_shard` below is its
+partition function, kept here so the C-ABI and tests can already use it.
+"""
+import os
+import time
+import zlib
+
+
+def env_rank():
+    """(rank, world, local_rank) from the torchrun environment"""
+    return (int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1)),
+            int(os.environ.get("LOCAL_RANK", 0)))
+
+
+def topic_stream(rank: int) -> int:
+    """independent synthetic topic stream per rank (weak scaling)"""
+    return rank
+
+
+def timed_region(step, steps: int, sync, group=None):
+    """Run `steps` calls of step() bracketed by barrier + device sync on both
+    sides; returns the MAX over ranks of the wall time (seconds)."""
+    import torch
+    import torch.distributed as dist
+    dist_on = dist.is_available() and dist.is_initialized()
+    if dist_on:
+        dist.barrier(group=group)
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    sync()
+    if dist_on:
+        dist.barrier(group=group)
+    dt = time.perf_counter() - t0
+    if dist_on:
+        dev = torch.device("cuda", torch.cuda.current_device()) \
+            if dist.get_backend(group) == "nccl" else torch.device("cpu")
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+        dt = float(t.item())
+    return dt
+
+
+def root_shard(filt: bytes, shards: int) -> int:
+    """Shard of a filter in the sharded (C4) layout: filters whose root word
+    is literal go to hash(root) mod shards; root '+' / '#' filters are spread
+    by a hash of the whole filter (every shard then also walks its root
+    wildcard part for each topic: match(T, F) = U_s match(T, F_s))."""
+    root = filt.split(b"/", 1)[0]
+    if root in (b"+", b"#"):
+        return zlib.crc32(filt) % shards
+    return zlib.crc32(root) % shards

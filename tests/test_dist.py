@@ -1,0 +1,68 @@
+"""The N>1 control plane on CPU: two gloo ranks run the bench's timed region
+(barrier, per-rank steps, max over ranks) and its per-rank topic streams.
+The data path has no collective (replicated trie, topic-sharded batches)."""
+import os
+import socket
+import sys
+
+import numpy as np
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    sys.path.insert(0, ROOT)
+    import time
+
+    import torch.distributed as dist
+    from emqx_amd import multi
+    from emqx_amd import workload as W
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    r, w, lr = multi.env_rank()
+    # each rank's step sleeps a different time: the reported time is the max
+    delay = 0.02 * (rank + 1)
+    dt = multi.timed_region(lambda: time.sleep(delay), 3, lambda: None)
+    tb, to = W.topics(1, n=500, stream=multi.topic_stream(r))
+    q.put((rank, r, w, dt, tb[:int(to[-1])].tobytes()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_timed_region_and_streams():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (r0, rr0, w0, dt0, b0), (r1, rr1, w1, dt1, b1) = res
+    assert (rr0, rr1, w0, w1) == (0, 1, 2, 2)
+    assert abs(dt0 - dt1) < 1e-9            # both ranks report the same max
+    assert dt0 >= 3 * 0.04                  # the slower rank's time
+    assert b0 != b1                         # independent topic streams
+
+
+def test_root_shard_partition():
+    sys.path.insert(0, ROOT)
+    from emqx_amd import multi
+    fs = [b"a/+", b"a/b/#", b"+/x", b"#", b"b/c", b"a", b"+/+/#"]
+    for s in (1, 2, 8):
+        shards = [multi.root_shard(f, s) for f in fs]
+        assert all(0 <= x < s for x in shards)
+        assert multi.root_shard(b"a/+", s) == multi.root_shard(b"a/b/#", s)   # same literal root
+    assert np.unique([multi.root_shard(b"+/%d" % i, 8) for i in range(200)]).size == 8
