@@ -46,12 +46,14 @@ def parse():
     ap.add_argument("--config", type=int, default=3, help="SURVEY §8(d) config (3 = the metric's)")
     ap.add_argument("--filters", type=int, default=None, help="override filter count")
     ap.add_argument("--topics", type=int, default=2_000_000, help="topics per GPU per step")
-    ap.add_argument("--cpu-sample", type=int, default=200_000, help="topics timed on the host (0 = skip)")
+    ap.add_argument("--cpu-sample", type=int, default=1_500_000, help="topics timed on the host (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=None)
     ap.add_argument("--check", type=int, default=20_000, help="topics checked bit-exactly vs the oracle")
-    ap.add_argument("--walk", default=None, help="walk variant (lane|tile256|tile512|tile1024|twopass)")
+    ap.add_argument("--walk", default=None, help="walk variant (queue|queue_xcd)")
     ap.add_argument("--ab", default=None, help="comma list of walk variants timed interleaved (extra report)")
     ap.add_argument("--stage-k", type=int, default=None)
+    ap.add_argument("--presort", action="store_true",
+                    help="EXPERIMENT: sort the batch by topic bytes on the host before upload (untimed)")
     ap.add_argument("--layout", type=int, default=None, help="1 = DFS relayout on commit (default), 0 = off")
     return ap.parse_args()
 
@@ -85,6 +87,15 @@ def main():
     tb, to = W.topics(a.config, n=a.topics, stream=multi.topic_stream(rank))
     n = len(to) - 1
     nbytes = int(to[-1])
+    if a.presort:
+        ts = [bytes(tb[to[i]:to[i + 1]]) for i in range(n)]
+        ts.sort()
+        lens = np.fromiter((len(t) for t in ts), dtype=np.uint64, count=n)
+        to = np.zeros(n + 1, dtype=np.uint64)
+        np.cumsum(lens, out=to[1:])
+        tb = np.frombuffer(b"".join(ts), dtype=np.uint8).copy()
+        del ts
+        log("presorted %d topics (experiment, untimed)" % n)
     d_b = torch.from_numpy(tb).to(dev)
     d_o = torch.from_numpy(to.view(np.int64)).to(dev)
     d_c = torch.empty(n, dtype=torch.int32, device=dev)
@@ -173,9 +184,9 @@ def main():
         topics_per_s = n * a.steps * world / dt
         levels = stats["levels"]
         B = 8 * levels + 16 * stats["edge_reads"] + 4 * stats["matches"]   # SURVEY §8(d), per launch
-        # dominant kernel = the longest stage (the fused walk; the emit walk
-        # of the two-pass A/B variant); B is what one launch of it processes
-        kname = max(kms, key=kms.get) if kms else None   # "walk" for the default queue pipeline
+        # dominant kernel = the longest stage (the walk); B is what one launch
+        # of it processes
+        kname = max(kms, key=kms.get) if kms else None
         walk_ms = kms.get(kname, 0.0) if kname else 0.0
         achieved = B / (walk_ms * 1e-3) / 1e9 if walk_ms > 0 else None
         out = {
@@ -197,12 +208,12 @@ def main():
                        "parallelism": "replicated trie x %d, topic batches sharded by rank" % world},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": None,
-                         "kernel": {"walk": "tm_walk_queue (globally balanced NFA walk)",
-                                    "match_fused": "tm_match_fused/lane (tokenize + NFA walk + look-back CSR)",
-                                    "match_emit": "tm_match<EMIT> (two-pass emit walk)"}.get(kname, kname),
+                         "kernel": {"walk": "tm_walk_queue (balanced NFA walk, one 16 B node-half load per step)"
+                                    }.get(kname, kname),
                          "kernel_ms": walk_ms,
                          "algorithmic_bytes_per_launch": B,
-                         "per_topic": {"n": levels / n, "E": stats["edge_reads"] / n, "M": stats["matches"] / n}},
+                         "per_topic": {"n": levels / n, "E": stats["edge_reads"] / n, "M": stats["matches"] / n,
+                                       "visits": stats["visits"] / n}},
             "cpu_baseline": cpu,
             "kernel_ms": kms,
             "filter_hits_per_s": stats["matches"] * a.steps * world / dt,

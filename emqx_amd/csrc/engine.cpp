@@ -114,7 +114,7 @@ struct NodeAux {
     uint32_t parent;      // parent node id (root: NODE_NONE)
     uint32_t word;        // word by which the parent reaches it (id, WORD_PLUS, WORD_HASH)
     uint32_t edge_count;  // #trie_node.edge_count
-    uint32_t lit_count;   // literal children (HAS_LIT flag <=> lit_count > 0; LIT_TABLE once > INLINE_LIT)
+    uint32_t lit_count;   // literal children (inline when 1, LW_TABLE once 2 or more)
 };
 
 struct FilterRec {
@@ -127,7 +127,7 @@ struct KTimes {
     const char* name;
     hipEvent_t a, b;
 };
-constexpr int N_KERNEL_SLOTS = 4;   // tokenize, match_count, scan, match_emit
+constexpr int N_KERNEL_SLOTS = 4;   // tokenize, walk, scan, copy_out
 
 }  // namespace
 
@@ -164,14 +164,13 @@ struct tm_engine {
     // ---- device image ----
     DevBuf d_nodes, d_edges, d_dict, d_arena, d_woff;
     bool dev_dirty = true;
+    int xcdq = 0;                     // option "xcdq": per-XCD dequeue ranges in the queue walk
     int layout_mode = 1;              // option "layout": 0 off, 1 auto, 2 every commit (tests)
     size_t created_since_layout = 0;  // nodes created since the last relayout
 
     // ---- match workspace ----
-    DevBuf w_bytes, w_off, w_words, w_meta, w_counts, w_outoff, w_ids, w_scan, w_total, w_path, w_stats, w_stage,
+    DevBuf w_twords, w_bytes, w_off, w_words, w_meta, w_counts, w_outoff, w_ids, w_scan, w_total, w_path, w_stats, w_stage,
         w_ws;
-    bool twopass = false;     // TM_WALK=twopass: count walk + scan + emit walk (A/B only)
-    int variant = TM_VARIANT_QUEUE;    // TM_WALK=lane|tile256|tile512|tile1024|queue
     uint32_t stage_k = 512;   // TM_STAGE_K: ids staged per topic before a re-walk (rows are
                               // written sparsely: HBM footprint, not traffic)
     hipEvent_t last_match_done = nullptr;
@@ -182,20 +181,12 @@ struct tm_engine {
     std::vector<KTimes> ev_pool;          // recycled events
     std::vector<KTimes> ev_pending;       // recorded, not yet read
     KTimes ev_cur[N_KERNEL_SLOTS];
-    bool ev_open[N_KERNEL_SLOTS] = {false, false, false, false};
 
     // scratch for words of one filter
     std::vector<uint32_t> tmp_words;
 
     tm_engine() {
-        if (const char* v = std::getenv("TM_WALK")) {
-            twopass = std::strcmp(v, "twopass") == 0;
-            if (!std::strcmp(v, "lane")) variant = TM_VARIANT_LANE;
-            if (!std::strcmp(v, "tile256")) variant = TM_VARIANT_TILE256;
-            if (!std::strcmp(v, "tile512")) variant = TM_VARIANT_TILE512;
-            if (!std::strcmp(v, "tile1024")) variant = TM_VARIANT_TILE1024;
-            if (!std::strcmp(v, "queue")) variant = TM_VARIANT_QUEUE;
-        }
+        if (const char* v = std::getenv("TM_XCDQ")) xcdq = std::atoi(v) ? 1 : 0;
         if (const char* v = std::getenv("TM_STAGE_K")) {
             long k = std::atol(v);
             if (k >= 4 && k <= 4096 && !(k & 3)) stage_k = (uint32_t)k;
@@ -296,7 +287,7 @@ struct tm_engine {
         edge_dirty.all = true;
     }
     void edge_insert(uint32_t parent, uint32_t word, uint32_t child) {
-        if ((edge_used + 1) * 2 > edges.size()) edge_grow();
+        if ((edge_used + 1) * 4 > edges.size()) edge_grow();
         edge_place(EdgeSlot{parent, word, child, 0});
         ++edge_used;
     }
@@ -344,62 +335,52 @@ struct tm_engine {
     static Node empty_node() {
         Node x;
         x.plus = NODE_NONE;
-        x.hash = NODE_NONE;
         x.hash_filter = FILTER_NONE;
+        x.lw = WORD_NONE;
+        x.lc = NODE_NONE;
         x.self_filter = FILTER_NONE;
-        for (int i = 0; i < INLINE_LIT; ++i) {
-            x.lw[i] = WORD_NONE;
-            x.lc[i] = NODE_NONE;
-        }
+        x.hash_filter2 = FILTER_NONE;
+        x.hash = NODE_NONE;
+        x.pad = 0;
         return x;
     }
     uint32_t child(uint32_t v, uint32_t w) const {
         const Node& x = nodes[v];
-        if (w == WORD_PLUS) return x.plus & NODE_MASK;
+        if (w == WORD_PLUS) return x.plus;
         if (w == WORD_HASH) return x.hash;
-        if (!(x.plus & HAS_LIT)) return NODE_NONE;
-        if (!(x.plus & LIT_TABLE)) {
-            for (int i = 0; i < INLINE_LIT; ++i)
-                if (x.lw[i] == w) return x.lc[i];
-            return NODE_NONE;
-        }
+        if (x.lw == w) return x.lc;
+        if (x.lw != LW_TABLE) return NODE_NONE;
         size_t s = edge_find_slot(v, w);
         return s == SIZE_MAX ? NODE_NONE : edges[s].child;
     }
-    // literal child add / remove, keeping "LIT_TABLE set => every literal
-    // edge of v is in edges[], else all are inline"
+    // literal child add / remove: one literal child lives inline (lw, lc);
+    // from the second on, all of them live in edges[] (lw = LW_TABLE)
     void lit_add(uint32_t v, uint32_t w, uint32_t c) {
         Node& x = nodes[v];
-        if (!(x.plus & LIT_TABLE)) {
-            for (int i = 0; i < INLINE_LIT; ++i)
-                if (x.lw[i] == WORD_NONE) {
-                    x.lw[i] = w;
-                    x.lc[i] = c;
-                    x.plus |= HAS_LIT;
-                    return;
-                }
-            for (int i = 0; i < INLINE_LIT; ++i) {  // spill the inline pairs to the table
-                edge_insert(v, x.lw[i], x.lc[i]);
-                x.lw[i] = WORD_NONE;
-                x.lc[i] = NODE_NONE;
-            }
-            nodes[v].plus |= LIT_TABLE;
+        if (x.lw == WORD_NONE) {
+            x.lw = w;
+            x.lc = c;
+            return;
+        }
+        if (x.lw != LW_TABLE) {  // spill the inline pair to the table
+            edge_insert(v, x.lw, x.lc);
+            nodes[v].lw = LW_TABLE;
+            nodes[v].lc = NODE_NONE;
         }
         edge_insert(v, w, c);
-        nodes[v].plus |= HAS_LIT;
     }
     void lit_remove(uint32_t v, uint32_t w) {
         Node& x = nodes[v];
-        if (x.plus & LIT_TABLE) {
+        if (x.lw == LW_TABLE) {
             edge_erase(v, w);
-        } else {
-            for (int i = 0; i < INLINE_LIT; ++i)
-                if (x.lw[i] == w) {
-                    x.lw[i] = WORD_NONE;
-                    x.lc[i] = NODE_NONE;
-                }
+        } else if (x.lw == w) {
+            x.lw = WORD_NONE;
+            x.lc = NODE_NONE;
         }
-        if (--aux[v].lit_count == 0) nodes[v].plus &= ~PLUS_FLAGS;
+        if (--aux[v].lit_count == 0) {
+            nodes[v].lw = WORD_NONE;
+            nodes[v].lc = NODE_NONE;
+        }
     }
     // add_path/1 (emqx_trie.erl:104-117) for one (Node, Word, Child) triple:
     // a new edge bumps the parent's edge_count.
@@ -408,9 +389,10 @@ struct tm_engine {
         if (c != NODE_NONE) return c;
         c = new_node(v, w);
         if (w == WORD_PLUS) {
-            nodes[v].plus = (nodes[v].plus & PLUS_FLAGS) | c;
+            nodes[v].plus = c;
         } else if (w == WORD_HASH) {
             nodes[v].hash = c;
+            edge_insert(v, WORD_HASH, c);
         } else {
             lit_add(v, w, c);
             aux[v].lit_count++;
@@ -422,10 +404,12 @@ struct tm_engine {
     void unlink_child(uint32_t c) {
         uint32_t v = aux[c].parent, w = aux[c].word;
         if (w == WORD_PLUS) {
-            nodes[v].plus = (nodes[v].plus & PLUS_FLAGS) | NODE_NONE;
+            nodes[v].plus = NODE_NONE;
         } else if (w == WORD_HASH) {
             nodes[v].hash = NODE_NONE;
             nodes[v].hash_filter = FILTER_NONE;
+            nodes[v].hash_filter2 = FILTER_NONE;
+            edge_erase(v, WORD_HASH);
         } else {
             lit_remove(v, w);
         }
@@ -452,6 +436,7 @@ struct tm_engine {
         node_dirty.mark(c);
         if (aux[c].word == WORD_HASH && aux[c].parent != NODE_NONE) {
             nodes[aux[c].parent].hash_filter = fid;
+            nodes[aux[c].parent].hash_filter2 = fid;
             node_dirty.mark(aux[c].parent);
         }
     }
@@ -516,36 +501,33 @@ struct tm_engine {
 
     // ------------------------------------------------------------------
     // DFS-preorder relayout: renumber the live nodes so that every subtree is
-    // a contiguous id range and a node's first child (its '+' child when it
-    // has one: the branch the walk takes first) directly follows it — two
-    // 32 B records share a 64 B line, and topics with a common prefix walk a
-    // compact region.  Deleted ids are dropped (compaction).  Filter ids are
-    // unchanged.
+    // a contiguous id range and a node's first child in walk order (its
+    // literal children, then its '+' child: the walk runs in the reference's
+    // discovery order) directly follows it, two 32 B records to a 64 B line;
+    // topics with a common prefix walk a compact region.  Deleted ids are
+    // dropped (compaction).  Filter ids are unchanged.
     void relayout() {
         const size_t N = nodes.size();
-        // literal children per node (inline pairs or table edges), CSR
+        // literal children per node (inline or table edges), CSR
         std::vector<uint32_t> start(N + 1, 0);
         for (size_t v = 0; v < N; ++v) {
             if (aux[v].parent == NODE_NONE && v != ROOT) continue;  // free slot
-            if ((nodes[v].plus & HAS_LIT) && !(nodes[v].plus & LIT_TABLE))
-                for (int i = 0; i < INLINE_LIT; ++i) start[v + 1] += nodes[v].lw[i] != WORD_NONE;
+            if (nodes[v].lw != WORD_NONE && nodes[v].lw != LW_TABLE) start[v + 1]++;
         }
         for (const EdgeSlot& e : edges)
-            if (e.parent != EDGE_EMPTY) start[e.parent + 1]++;
+            if (e.parent != EDGE_EMPTY && e.word != WORD_HASH) start[e.parent + 1]++;
         for (size_t v = 0; v < N; ++v) start[v + 1] += start[v];
         std::vector<uint32_t> kids(start[N]);
         {
             std::vector<uint32_t> fill(start.begin(), start.end() - 1);
             for (size_t v = 0; v < N; ++v) {
                 if (aux[v].parent == NODE_NONE && v != ROOT) continue;
-                if ((nodes[v].plus & HAS_LIT) && !(nodes[v].plus & LIT_TABLE))
-                    for (int i = 0; i < INLINE_LIT; ++i)
-                        if (nodes[v].lw[i] != WORD_NONE) kids[fill[v]++] = nodes[v].lc[i];
+                if (nodes[v].lw != WORD_NONE && nodes[v].lw != LW_TABLE) kids[fill[v]++] = nodes[v].lc;
             }
             for (const EdgeSlot& e : edges)
-                if (e.parent != EDGE_EMPTY) kids[fill[e.parent]++] = e.child;
+                if (e.parent != EDGE_EMPTY && e.word != WORD_HASH) kids[fill[e.parent]++] = e.child;
         }
-        // preorder: v, '+' subtree, literal subtrees, '#' subtree
+        // preorder: v, literal subtrees, '+' subtree, '#' subtree
         std::vector<uint32_t> newid(N, NODE_NONE), order;
         order.reserve(live_nodes);
         std::vector<uint32_t> stack;
@@ -556,9 +538,8 @@ struct tm_engine {
             newid[v] = (uint32_t)order.size();
             order.push_back(v);
             if (nodes[v].hash != NODE_NONE) stack.push_back(nodes[v].hash);
+            if (nodes[v].plus != NODE_NONE) stack.push_back(nodes[v].plus);
             for (uint32_t k = start[v + 1]; k > start[v]; --k) stack.push_back(kids[k - 1]);
-            uint32_t pc = nodes[v].plus & NODE_MASK;
-            if (pc != NODE_NONE) stack.push_back(pc);
         }
         std::vector<uint32_t>().swap(kids);
         std::vector<uint32_t>().swap(start);
@@ -567,15 +548,15 @@ struct tm_engine {
         std::vector<NodeAux> na(order.size());
         for (size_t i = 0; i < order.size(); ++i) {
             Node x = nodes[order[i]];
-            x.plus = (x.plus & PLUS_FLAGS) | remap(x.plus & NODE_MASK);
+            x.plus = remap(x.plus);
             x.hash = remap(x.hash);
-            for (int k = 0; k < INLINE_LIT; ++k) x.lc[k] = remap(x.lc[k]);
+            if (x.lw != WORD_NONE && x.lw != LW_TABLE) x.lc = remap(x.lc);
             nn[i] = x;
             NodeAux a = aux[order[i]];
             a.parent = remap(a.parent);
             na[i] = a;
         }
-        // literal edge table with the new ids
+        // edge table with the new ids
         std::vector<EdgeSlot> old;
         old.swap(edges);
         edges.assign(old.size(), EdgeSlot{EDGE_EMPTY, 0, 0, 0});
@@ -699,36 +680,16 @@ struct tm_engine {
         }
         return k;
     }
-    void timed(hipStream_t st, const char* name, int idx) {
-        if (!timing_enabled) return;
-        ev_cur[idx] = take_event(name);
-        ev_open[idx] = true;
-        HIPCHK(hipEventRecord(ev_cur[idx].a, st));
-    }
-    void timed_end(hipStream_t st, int idx) {
-        if (!timing_enabled || !ev_open[idx]) return;
-        HIPCHK(hipEventRecord(ev_cur[idx].b, st));
-        ev_pending.push_back(ev_cur[idx]);
-        ev_open[idx] = false;
-    }
-
     void ensure_workspace(uint32_t n, uint64_t nbytes) {
+        w_twords.ensure((size_t)(n + 1) * WREG * 4);
         w_words.ensure((nbytes + n + 1) * 4);
         w_path.ensure((nbytes + 2ull * n + 2) * 4);
         w_total.ensure(64);
         w_stats.ensure(64);
-        if (twopass) {
-            w_meta.ensure((size_t)(n + 1) * 4);
-            w_scan.ensure(scan_tmp_elems(n) * 8 + 8);
-        } else if (variant == TM_VARIANT_QUEUE) {
-            w_meta.ensure((size_t)(n + 1) * 4);
-            w_scan.ensure(scan_tmp_elems(n) * 8 + 8);
-            w_stage.ensure(((size_t)n * stage_k + 1) * 4);
-            w_ws.ensure(64);
-        } else {
-            w_stage.ensure(fused_stage_elems(n, stage_k) * 4);
-            w_ws.ensure(fused_ws_words(n) * 8);
-        }
+        w_meta.ensure((size_t)(n + 1) * 4);
+        w_scan.ensure(scan_tmp_elems(n) * 8 + 8);
+        w_stage.ensure(((size_t)n * stage_k + 4) * 4);
+        w_ws.ensure(QWS_BYTES);
     }
 
     // the whole hot path of one batch, stream-ordered on st: CSR of ordered
@@ -737,61 +698,28 @@ struct tm_engine {
                    uint64_t* out_off, uint32_t* ids, uint64_t cap, uint64_t* total, hipStream_t st) {
         ensure_workspace(n, nbytes);
         ImageView im = view();
-        uint32_t* words = w_words.as<uint32_t>();
-        uint32_t* path = w_path.as<uint32_t>();
         unsigned long long* sp = w_stats.as<unsigned long long>();
         if (stats_enabled) HIPCHK(hipMemsetAsync(w_stats.p, 0, 64, st));
-        if (!twopass && variant == TM_VARIANT_QUEUE) {
-            static const char* kStage[4] = {"tokenize", "walk", "scan", "copy_out"};
-            hipEvent_t marks[8];
-            if (timing_enabled)
-                for (int i = 0; i < 4; ++i) {
-                    ev_cur[i] = take_event(kStage[i]);
-                    marks[2 * i] = ev_cur[i].a;
-                    marks[2 * i + 1] = ev_cur[i].b;
-                }
-            HIPCHK(launch_queue(stats_enabled, im, bytes, off, n, words, w_meta.as<uint32_t>(), path,
-                                w_stage.as<uint32_t>(), stage_k, counts, out_off, ids, cap, total,
-                                w_scan.as<uint64_t>(), w_ws.as<unsigned long long>(), sp, st,
-                                timing_enabled ? marks : nullptr));
-            if (timing_enabled)
-                for (int i = 0; i < 4; ++i) ev_pending.push_back(ev_cur[i]);
-            return;
-        }
-        if (!twopass) {
-            timed(st, "match_fused", 0);
-            HIPCHK(launch_fused(variant, stats_enabled, im, bytes, off, n, words, path, w_stage.as<uint32_t>(), stage_k,
-                                counts, out_off, ids, cap, total, w_ws.as<unsigned long long>(), sp, st));
-            timed_end(st, 0);
-            return;
-        }
-        uint32_t* meta = w_meta.as<uint32_t>();
-        timed(st, "tokenize", 0);
-        HIPCHK(launch_tokenize(im, bytes, off, n, words, meta, st));
-        timed_end(st, 0);
-        timed(st, "match_count", 1);
-        int cmode = stats_enabled ? TM_MODE_STATS : TM_MODE_COUNT;
-        HIPCHK(launch_match(cmode, false, im, off, n, words, meta, counts, nullptr, nullptr, 0, path, sp, st));
-        HIPCHK(launch_match(cmode, true, im, off, n, words, meta, counts, nullptr, nullptr, 0, path, sp, st));
-        timed_end(st, 1);
-        timed(st, "scan", 2);
-        HIPCHK(launch_scan(counts, n, out_off, total, w_scan.as<uint64_t>(), st));
-        timed_end(st, 2);
-        if (cap) {
-            timed(st, "match_emit", 3);
-            HIPCHK(launch_match(TM_MODE_EMIT, false, im, off, n, words, meta, nullptr, out_off, ids, cap, path,
-                                nullptr, st));
-            HIPCHK(launch_match(TM_MODE_EMIT, true, im, off, n, words, meta, nullptr, out_off, ids, cap, path,
-                                nullptr, st));
-            timed_end(st, 3);
-        }
-    }
-    // look-back spin guard of the fused kernel (never expected to trip)
-    void check_fused_error() {
-        if (twopass || variant == TM_VARIANT_QUEUE || !w_ws.p) return;
-        unsigned long long err = 0;
-        HIPCHK(hipMemcpy(&err, w_ws.as<unsigned long long>() + 1, 8, hipMemcpyDeviceToHost));
-        if (err) throw DevError("fused match: look-back spin limit exceeded");
+        static const char* kStage[4] = {"tokenize", "walk", "scan", "copy_out"};
+        hipEvent_t marks[8];
+        if (timing_enabled)
+            for (int i = 0; i < 4; ++i) {
+                ev_cur[i] = take_event(kStage[i]);
+                marks[2 * i] = ev_cur[i].a;
+                marks[2 * i + 1] = ev_cur[i].b;
+            }
+        QueueBufs qb;
+        qb.twords = w_twords.as<uint32_t>();
+        qb.words = w_words.as<uint32_t>();
+        qb.meta = w_meta.as<uint32_t>();
+        qb.path = w_path.as<uint32_t>();
+        qb.stage = w_stage.as<uint32_t>();
+        qb.scan_tmp = w_scan.as<uint64_t>();
+        qb.ws = w_ws.as<unsigned long long>();
+        HIPCHK(launch_queue(stats_enabled, xcdq != 0, im, bytes, off, n, qb, stage_k, counts, out_off, ids, cap,
+                            total, sp, st, timing_enabled ? marks : nullptr));
+        if (timing_enabled)
+            for (int i = 0; i < 4; ++i) ev_pending.push_back(ev_cur[i]);
     }
     void finish_batch(hipStream_t st, uint32_t n) {
         if (!last_match_done) HIPCHK(hipEventCreateWithFlags(&last_match_done, hipEventDisableTiming));
@@ -887,8 +815,8 @@ int tm_open(const tm_config* cfg, tm_engine** out) {
         size_t nodes_hint = (size_t)cfg->filters_hint * 3;
         e->nodes.reserve(nodes_hint);
         e->aux.reserve(nodes_hint);
-        // only wide nodes (> INLINE_LIT literal children) use the edge table
-        e->edges.assign(next_pow2(nodes_hint / 2), EdgeSlot{EDGE_EMPTY, 0, 0, 0});
+        // wide nodes' literal edges and '#' edges use the table (load <= 1/4)
+        e->edges.assign(next_pow2(nodes_hint), EdgeSlot{EDGE_EMPTY, 0, 0, 0});
     }
     if (dev >= 0) {
         int ndev = 0;
@@ -1038,7 +966,6 @@ int tm_match_batch(tm_engine* e, const uint8_t* topic_bytes, const uint64_t* top
                          e->w_outoff.as<uint64_t>(), e->w_ids.as<uint32_t>(), icap, d_total, st);
             HIPCHK(hipMemcpyAsync(&total, d_total, 8, hipMemcpyDeviceToHost, st));
             HIPCHK(hipStreamSynchronize(st));
-            e->check_fused_error();
             if (total <= icap || total > out_cap) break;
             e->w_ids.ensure(total * 4, 1.25);
             icap = e->w_ids.bytes / 4;
@@ -1087,10 +1014,9 @@ int tm_match_batch_device(tm_engine* e, const uint8_t* d_bytes, const uint64_t* 
 int tm_set_option(tm_engine* e, const char* name, int64_t value) {
     if (!name) return TM_EINVAL;
     return guarded(e, [&]() -> int {
-        if (!std::strcmp(name, "walk")) {
-            if (value < 0 || value > 5) return TM_EINVAL;
-            e->twopass = value == 4;
-            if (value != 4) e->variant = (int)value;
+        if (!std::strcmp(name, "xcdq")) {
+            if (value < 0 || value > 1) return TM_EINVAL;
+            e->xcdq = (int)value;
             return TM_OK;
         }
         if (!std::strcmp(name, "layout")) {

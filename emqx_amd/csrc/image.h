@@ -8,17 +8,18 @@
 // with node ids = full path binaries.  Here node ids are dense u32 and words
 // are interned u32, so every probe is a fixed-size integer compare:
 //
-//   nodes[]  32 B per node (half an HBM burst): the '+' edge and the '#'
-//            edge are ARRAY READS (fields of the parent), the filter ending at
-//            the node and the filter ending at its '#' child are carried
-//            inline, so the reference's 'match_#'/2 (emqx_trie.erl:140-145)
-//            costs nothing beyond the node read; up to INLINE_LIT literal
-//            children live in the record too, so the deep, narrow part of the
-//            trie (most of the walk) needs no hash probe at all.
-//   edges[]  literal edges of the wide nodes (> INLINE_LIT literal
-//            children, flag LIT_TABLE), open addressing, 16 B slots grouped
-//            in 64 B buckets (one HBM burst), linear probing over slots from
-//            the home bucket's first slot, load <= 1/2.
+//   nodes[]  32 B per node in two 16 B halves, so every step of the walk is
+//            ONE 16 B load: a visit with topic words left reads the inner
+//            half {'+' child, '#' filter, one inline literal child (word,
+//            child)}, a visit at the topic's last level reads the leaf half
+//            {filter ending here, '#' filter}.  The '+' edge and the '#' edge
+//            are fields of the parent, the filter ending at the '#' child is
+//            carried inline (the reference's 'match_#'/2, emqx_trie.erl:140-145,
+//            costs nothing beyond the visit's own load).
+//   edges[]  literal edges of the wide nodes (>= 2 literal children, lw =
+//            LW_TABLE) and the '#' children (word WORD_HASH, only looked up
+//            for the out-of-domain topic level "#"): open addressing, 16 B
+//            slots, linear probing slot by slot from the home slot, load <= 1/4.
 //   dict[]   word dictionary: 64-bit hash -> word id, byte-verified against
 //            the word arena, so tokenisation is collision-free (no hash-only
 //            identity).
@@ -30,10 +31,7 @@ namespace tmx {
 constexpr uint32_t ROOT       = 0u;
 constexpr uint32_t NODE_MASK  = 0x1FFFFFFFu;   // node ids are 29-bit (walk path packs 3 flag bits)
 constexpr uint32_t NODE_NONE  = 0x1FFFFFFFu;
-constexpr uint32_t HAS_LIT    = 0x80000000u;   // nodes[].plus bit31: has literal children
-constexpr uint32_t LIT_TABLE  = 0x40000000u;   // nodes[].plus bit30: they live in edges[] (else inline)
-constexpr uint32_t PLUS_FLAGS = HAS_LIT | LIT_TABLE;
-constexpr int      INLINE_LIT = 2;             // literal children kept in the node record
+constexpr uint32_t LW_TABLE   = 0xFFFFFFFCu;   // nodes[].lw: literal children live in edges[]
 constexpr uint32_t FILTER_NONE = 0xFFFFFFFFu;
 
 // token ids produced by the tokenizer (emqx_topic:words/1 + word/1)
@@ -43,16 +41,20 @@ constexpr uint32_t WORD_HASH  = 0xFFFFFFFDu;   // level == "#"  (atom '#')
 constexpr uint32_t WORD_MAX   = 0xFFFFFFF0u;   // interned ids are < WORD_MAX
 
 constexpr uint32_t EDGE_EMPTY = 0xFFFFFFFFu;   // slot.parent of an empty slot
-constexpr int      SLOTS_PER_BUCKET = 4;       // 4 x 16 B = 64 B
 
 struct alignas(32) Node {
-    uint32_t plus;         // '+' child node id | HAS_LIT | LIT_TABLE, NODE_NONE if none
-    uint32_t hash;         // '#' child node id, NODE_NONE if none
+    // inner half: read by a visit with words left (level r < n)
+    uint32_t plus;         // '+' child node id, NODE_NONE if none
     uint32_t hash_filter;  // filter id of the '#' child (its topic), FILTER_NONE if none
+    uint32_t lw;           // word of the single literal child, WORD_NONE if none, LW_TABLE if >= 2
+    uint32_t lc;           // that child's node id
+    // leaf half: read by a visit at the topic's last level (r == n)
     uint32_t self_filter;  // filter id ending at this node, FILTER_NONE if topic = undefined
-    uint32_t lw[INLINE_LIT];  // inline literal children: word ids (WORD_NONE = empty slot)
-    uint32_t lc[INLINE_LIT];  //   and child node ids; unused when LIT_TABLE is set
+    uint32_t hash_filter2; // = hash_filter
+    uint32_t hash;         // '#' child node id, NODE_NONE if none
+    uint32_t pad;
 };
+static_assert(sizeof(Node) == 32, "node record is two 16 B halves");
 
 struct alignas(16) EdgeSlot {
     uint32_t parent;       // EDGE_EMPTY when free
@@ -96,9 +98,9 @@ TM_HD uint64_t edge_hash(uint32_t parent, uint32_t word) {
     return fmix64(((uint64_t)parent << 32) | word);
 }
 
-// first slot of the home bucket of key (parent, word)
+// home slot of key (parent, word)
 TM_HD uint64_t edge_home(uint32_t parent, uint32_t word, uint64_t slot_mask) {
-    return (edge_hash(parent, word) * SLOTS_PER_BUCKET) & slot_mask;
+    return edge_hash(parent, word) & slot_mask;
 }
 
 // word hash: 8-byte little-endian chunks folded with a multiply-xorshift; the

@@ -5,39 +5,31 @@
 #include <stdint.h>
 #include "image.h"
 
-#define TM_MODE_COUNT 0
-#define TM_MODE_EMIT 1
-#define TM_MODE_STATS 2
-
-// fused-kernel variants (A/B; TM_WALK env in the engine)
-#define TM_VARIANT_LANE 0
-#define TM_VARIANT_TILE256 1
-#define TM_VARIANT_TILE512 2
-#define TM_VARIANT_TILE1024 3
-#define TM_VARIANT_QUEUE 5
-
 namespace tmx {
 
-// marks: 8 events, [2i] before / [2i+1] after stage i (tokenize, walk, scan, copy-out), or null
-hipError_t launch_queue(bool stats_mode, const ImageView& im, const uint8_t* bytes, const uint64_t* off,
-                        uint32_t n, uint32_t* words, uint32_t* meta, uint32_t* path_scratch, uint32_t* stage,
-                        uint32_t K, uint32_t* counts, uint64_t* out_off, uint32_t* out, uint64_t out_cap,
-                        uint64_t* total, uint64_t* scan_tmp, unsigned long long* ws, unsigned long long* stats,
+constexpr uint32_t WREG = 16;        // topic levels kept in VGPRs / LDS path slots; longer
+                                     // topics keep their path in global scratch
+constexpr size_t QWS_BYTES = 1024;   // queue heads: 8 ranges x 128 B
+
+// per-batch device workspace of the queue pipeline
+struct QueueBufs {
+    uint32_t* twords;     // n x WREG word ids (levels < WREG)
+    uint32_t* words;      // levels >= WREG of long topics, at (byte offset + topic index)
+    uint32_t* meta;       // n: levels | long << 30 | dollar << 31
+    uint32_t* path;       // global path of long topics, at (byte offset + 2 x topic index)
+    uint32_t* stage;      // n x K: first K ids of each topic (written from the row's end)
+    uint64_t* scan_tmp;   // scan_tmp_elems(n)
+    unsigned long long* ws;   // QWS_BYTES of queue heads
+};
+
+// tokenize -> NFA walk -> scan -> copy-out, all on st.  marks: 8 events,
+// [2i] before / [2i+1] after stage i, or null.  out_cap == 0: counts and
+// offsets only.  stats (5 x u64, zeroed by the caller) is filled when
+// stats_mode: levels, visits, edge reads, matches.
+hipError_t launch_queue(bool stats_mode, bool xcdq, const ImageView& im, const uint8_t* bytes, const uint64_t* off,
+                        uint32_t n, const QueueBufs& qb, uint32_t K, uint32_t* counts, uint64_t* out_off,
+                        uint32_t* out, uint64_t out_cap, uint64_t* total, unsigned long long* stats,
                         hipStream_t st, hipEvent_t* marks);
-hipError_t launch_tokenize(const ImageView& im, const uint8_t* bytes, const uint64_t* off, uint32_t n,
-                           uint32_t* words, uint32_t* meta, hipStream_t st);
-hipError_t launch_match(int mode, bool long_topics, const ImageView& im, const uint64_t* off, uint32_t n,
-                        const uint32_t* words, const uint32_t* meta, uint32_t* counts,
-                        const uint64_t* out_off, uint32_t* out, uint64_t out_cap,
-                        uint32_t* path_scratch, unsigned long long* stats, hipStream_t st);
 size_t scan_tmp_elems(uint32_t n);
-size_t fused_ws_words(uint32_t n);
-size_t fused_stage_elems(uint32_t n, uint32_t K);
-hipError_t launch_fused(int variant, bool stats_mode, const ImageView& im, const uint8_t* bytes, const uint64_t* off,
-                        uint32_t n, uint32_t* words, uint32_t* path_scratch, uint32_t* stage, uint32_t K,
-                        uint32_t* counts, uint64_t* out_off, uint32_t* out, uint64_t out_cap, uint64_t* total,
-                        unsigned long long* ws, unsigned long long* stats, hipStream_t st);
-hipError_t launch_scan(const uint32_t* counts, uint32_t n, uint64_t* out_off, uint64_t* total,
-                       uint64_t* tmp, hipStream_t st);
 
 }  // namespace tmx

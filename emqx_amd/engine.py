@@ -162,13 +162,15 @@ class Engine:
                                             p(d_ids), out_cap, p(d_total), st)
         return self._check(rc, "tm_match_batch_device")
 
-    WALKS = {"lane": 0, "tile256": 1, "tile512": 2, "tile1024": 3, "twopass": 4, "queue": 5}
+    # walk variants (A/B knobs of tm_walk_queue): one global dequeue head, or
+    # per-XCD heads over contiguous ranges of the batch
+    WALKS = {"queue": 0, "queue_xcd": 1}
 
     def set_option(self, name: str, value: int):
         self._check(self.lib.tm_set_option(self.h, name.encode(), int(value)), "tm_set_option(%s)" % name)
 
     def set_walk(self, walk: str):
-        self.set_option("walk", self.WALKS[walk])
+        self.set_option("xcdq", self.WALKS[walk])
 
     # -- instrumentation ----------------------------------------------------
     def set_stats(self, on=True):

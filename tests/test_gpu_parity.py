@@ -222,7 +222,7 @@ def test_stats_edge_reads_match_oracle(gpu_device, golden):
     e.close()
 
 
-@pytest.mark.parametrize("walk", ["queue", "lane", "tile256", "tile512", "tile1024", "twopass"])
+@pytest.mark.parametrize("walk", ["queue", "queue_xcd"])
 def test_every_walk_variant_bit_exact(gpu_device, golden, walk):
     """each kernel variant (A/B knobs) against the committed vectors and C1"""
     for vec in golden["o1_vectors"]:

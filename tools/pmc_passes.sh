@@ -1,18 +1,22 @@
 #!/bin/bash
-# PMC passes over the C3 bench (one counter group per rocprofv3 run, per the
-# gfx950 slot limits in /opt/skills/guides/MI355X_MICROARCH.md).  Output:
-# gpurun_out/pmc/<pass>/...counter_collection.csv
-set -e
+# PMC passes over the bench (one counter group per rocprofv3 run, within the
+# gfx950 per-block slot limits of /opt/skills/guides/MI355X_MICROARCH.md).
+# Output: gpurun_out/${PMC_DIR:-pmc}/<pass>/run_counter_collection.csv, then a
+# per-kernel summary (tools/pmc_summary.py) in gpurun_out/${PMC_DIR}/summary.json
+set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
+D=gpurun_out/${PMC_DIR:-pmc}
 ARGS="--steps 3 --warmup 1 --cpu-sample 0 --check 0 ${BENCH_ARGS}"
 run() {
   name=$1; shift
-  mkdir -p gpurun_out/pmc/$name
-  timeout -k 10 240 rocprofv3 --pmc "$@" --output-format csv -d gpurun_out/pmc/$name -o run -- python3 bench.py $ARGS > gpurun_out/pmc/$name/log.txt 2>&1
+  mkdir -p $D/$name
+  timeout -s KILL 180 rocprofv3 --pmc "$@" --output-format csv -d $D/$name -o run -- python3 bench.py $ARGS > $D/$name/log.txt 2>&1
 }
-run fetch FETCH_SIZE
-run write WRITE_SIZE
-run tcc TCC_HIT_sum TCC_MISS_sum
-run sq SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY
-run tcp TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum
+run fetch FETCH_SIZE && \
+run write WRITE_SIZE && \
+run tcc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum && \
+run sq SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_BUSY_CYCLES && \
+run tcp TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCP_TCC_WRITE_REQ_sum TCP_TOTAL_READ_sum && \
+run ta TA_TA_BUSY_sum TA_BUFFER_READ_WAVEFRONTS_sum && \
+python3 tools/pmc_summary.py $D > $D/summary.json
