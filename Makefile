@@ -5,7 +5,8 @@
 HIPCC   ?= /opt/rocm/bin/hipcc
 ARCH    ?= gfx950
 CC      ?= gcc
-HIPFLAGS = --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -Wall -Wno-unused-result
+TMDEFS  ?=
+HIPFLAGS = --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -Wall -Wno-unused-result $(TMDEFS)
 BUILD   := build
 
 all: emqx_amd/libtopicmatch.so emqx_amd/libtmwork.so oracle/liboracle.so
@@ -17,7 +18,7 @@ $(BUILD)/kernels.o: emqx_amd/csrc/kernels.hip emqx_amd/csrc/kernels.h emqx_amd/c
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(BUILD)/engine.o: emqx_amd/csrc/engine.cpp emqx_amd/csrc/kernels.h emqx_amd/csrc/image.h include/topicmatch.h | $(BUILD)
-	$(HIPCC) -O3 -fPIC -std=c++17 -Wall -c $< -o $@
+	$(HIPCC) -O3 -fPIC -std=c++17 -Wall $(TMDEFS) -c $< -o $@
 
 emqx_amd/libtopicmatch.so: $(BUILD)/kernels.o $(BUILD)/engine.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -o $@

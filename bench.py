@@ -52,6 +52,8 @@ def parse():
     ap.add_argument("--walk", default=None, help="walk variant (queue|queue_xcd)")
     ap.add_argument("--ab", default=None, help="comma list of walk variants timed interleaved (extra report)")
     ap.add_argument("--stage-k", type=int, default=None)
+    ap.add_argument("--lib", default=None, help="EXPERIMENT: alternative build of libtopicmatch.so (A/B of build options)")
+    ap.add_argument("--hist", action="store_true", help="log per-level visit/probe histogram (diagnostic)")
     ap.add_argument("--presort", action="store_true",
                     help="EXPERIMENT: sort the batch by topic bytes on the host before upload (untimed)")
     ap.add_argument("--layout", type=int, default=None, help="1 = DFS relayout on commit (default), 0 = off")
@@ -60,6 +62,9 @@ def parse():
 
 def main():
     a = parse()
+    if a.lib:
+        from emqx_amd import _lib
+        _lib.LIB_PATH = os.path.abspath(a.lib)
     rank, world, local = multi.env_rank()
     if world > 1:
         dist.init_process_group("nccl" if torch.cuda.is_available() else "gloo")
@@ -108,6 +113,12 @@ def main():
     eng.match_batch_device(d_b, d_o, n, nbytes, d_c, d_oo, None, 0, d_t, stream=st)
     torch.cuda.synchronize(dev)
     stats = eng.last_stats()
+    if a.hist:
+        import ctypes
+        h = (ctypes.c_uint64 * 48)()
+        eng.lib.tm_debug_hist(eng.h, h, 48)
+        for k, name in enumerate(["visits", "probe_loads", "failed_probes"]):
+            log("per-level %s per topic: %s" % (name, [round(h[16 * k + l] / n, 2) for l in range(16)]))
     eng.set_stats(False)
     total = int(d_t.item())
     cap = total + 1024
@@ -128,9 +139,17 @@ def main():
         # interleaved A/B of walk variants on the same image and batch
         # (rounds x variants, one process: methodology rule 24)
         res = {v: [] for v in a.ab.split(",")}
+
+        def configure(v):   # "walk[@option=value[@...]]"
+            parts = v.split("@")
+            eng.set_walk(parts[0])
+            eng.set_option("walk_bpc", 0)
+            for kv in parts[1:]:
+                k, x = kv.split("=")
+                eng.set_option(k, int(x))
         for _ in range(5):
             for v in res:
-                eng.set_walk(v)
+                configure(v)
                 step()
                 torch.cuda.synchronize(dev)
                 t1 = time.perf_counter()
@@ -141,7 +160,7 @@ def main():
                 assert int(d_t.item()) == total
         log("A/B ms/step (median, min): " + ", ".join(
             "%s %.2f/%.2f" % (v, sorted(x)[len(x) // 2], min(x)) for v, x in res.items()))
-        eng.set_walk(a.walk or "queue")
+        configure(a.walk or "queue")
 
     # ---- timed region: K steps, kernel events recorded on the launch stream;
     # barrier + sync on both sides, max over ranks (emqx_amd/multi.py)
@@ -213,7 +232,8 @@ def main():
                          "kernel_ms": walk_ms,
                          "algorithmic_bytes_per_launch": B,
                          "per_topic": {"n": levels / n, "E": stats["edge_reads"] / n, "M": stats["matches"] / n,
-                                       "visits": stats["visits"] / n}},
+                                       "visits": stats["visits"] / n, "leaf_visits": stats["leaf_visits"] / n,
+                                       "probe_loads": stats["probe_loads"] / n}},
             "cpu_baseline": cpu,
             "kernel_ms": kms,
             "filter_hits_per_s": stats["matches"] * a.steps * world / dt,

@@ -32,7 +32,8 @@ class TmNodeInfo(ctypes.Structure):
 class TmBatchStats(ctypes.Structure):
     _fields_ = [("topics", ctypes.c_uint64), ("levels", ctypes.c_uint64),
                 ("visits", ctypes.c_uint64), ("edge_reads", ctypes.c_uint64),
-                ("matches", ctypes.c_uint64)]
+                ("matches", ctypes.c_uint64), ("leaf_visits", ctypes.c_uint64),
+                ("probe_loads", ctypes.c_uint64)]
 
 
 # (name, restype, argtypes) — every symbol include/topicmatch.h declares

@@ -110,11 +110,18 @@ struct DevBuf {
     T* as() const { return reinterpret_cast<T*>(p); }
 };
 
+constexpr EdgeSlot empty_slot() {
+    EdgeSlot e{};
+    e.parent = EDGE_EMPTY;
+    return e;
+}
+constexpr EdgeSlot kEmptySlot = empty_slot();
+
 struct NodeAux {
     uint32_t parent;      // parent node id (root: NODE_NONE)
     uint32_t word;        // word by which the parent reaches it (id, WORD_PLUS, WORD_HASH)
     uint32_t edge_count;  // #trie_node.edge_count
-    uint32_t lit_count;   // literal children (inline when 1, LW_TABLE once 2 or more)
+    uint32_t lit_count;   // literal children (inline when 1, WIDE + edges[] once 2 or more)
 };
 
 struct FilterRec {
@@ -164,7 +171,8 @@ struct tm_engine {
     // ---- device image ----
     DevBuf d_nodes, d_edges, d_dict, d_arena, d_woff;
     bool dev_dirty = true;
-    int xcdq = 0;                     // option "xcdq": per-XCD dequeue ranges in the queue walk
+    uint32_t walk_bpc = 0;            // option "walk_bpc": walk blocks per CU (0 = full occupancy)
+    int xcdq = 1;                     // option "xcdq": per-XCD dequeue ranges in the queue walk (default on)
     int layout_mode = 1;              // option "layout": 0 off, 1 auto, 2 every commit (tests)
     size_t created_since_layout = 0;  // nodes created since the last relayout
 
@@ -193,7 +201,7 @@ struct tm_engine {
         }
         dict.assign(1024, DictSlot{0, WORD_NONE, 0});
         nodes.reserve(1024);
-        edges.assign(1024, EdgeSlot{EDGE_EMPTY, 0, 0, 0});
+        edges.assign(1024, kEmptySlot);
         new_node(NODE_NONE, NODE_NONE);  // root = 0
     }
 
@@ -281,15 +289,43 @@ struct tm_engine {
     void edge_grow() {
         std::vector<EdgeSlot> old;
         old.swap(edges);
-        edges.assign(old.size() * 2, EdgeSlot{EDGE_EMPTY, 0, 0, 0});
+        edges.assign(old.size() * 2, kEmptySlot);
         for (const EdgeSlot& e : old)
             if (e.parent != EDGE_EMPTY) edge_place(e);
         edge_dirty.all = true;
     }
+    EdgeSlot slot_for(uint32_t parent, uint32_t word, uint32_t child) const {
+        const Node& c = nodes[child];
+        EdgeSlot e{};
+        e.parent = parent;
+        e.word = word;
+        e.child = child;
+        e.plus = c.plus;
+#if TM_SLOT_RECORD
+        e.hash_filter = c.hash_filter;
+        e.lw = c.lw;
+        e.lc = c.lc;
+        e.self_filter = c.self_filter;
+#endif
+        return e;
+    }
     void edge_insert(uint32_t parent, uint32_t word, uint32_t child) {
         if ((edge_used + 1) * 4 > edges.size()) edge_grow();
-        edge_place(EdgeSlot{parent, word, child, 0});
+        edge_place(slot_for(parent, word, child));
         ++edge_used;
+    }
+    // node x changed: mark its page and refresh the copy of its record in
+    // its parent's edge slot (when it is a table child)
+    void touched(uint32_t x) {
+        node_dirty.mark(x);
+        if (!SLOT_RECORD) return;
+        const uint32_t p = aux[x].parent, w = aux[x].word;
+        if (p == NODE_NONE || w == WORD_PLUS) return;
+        if (w != WORD_HASH && !(nodes[p].plus & WIDE)) return;
+        const size_t s = edge_find_slot(p, w);
+        if (s == SIZE_MAX) return;
+        edges[s] = slot_for(p, w, x);
+        edge_dirty.mark(s);
     }
     void edge_erase(uint32_t parent, uint32_t word) {
         size_t i = edge_find_slot(parent, word);
@@ -307,7 +343,7 @@ struct tm_engine {
                 i = j;
             }
         }
-        edges[i] = EdgeSlot{EDGE_EMPTY, 0, 0, 0};
+        edges[i] = kEmptySlot;
         edge_dirty.mark(i);
         --edge_used;
     }
@@ -346,38 +382,50 @@ struct tm_engine {
     }
     uint32_t child(uint32_t v, uint32_t w) const {
         const Node& x = nodes[v];
-        if (w == WORD_PLUS) return x.plus;
+        if (w == WORD_PLUS) return x.plus & NODE_MASK;
         if (w == WORD_HASH) return x.hash;
-        if (x.lw == w) return x.lc;
-        if (x.lw != LW_TABLE) return NODE_NONE;
+        if (!(x.plus & WIDE)) return x.lw == w ? x.lc : NODE_NONE;
         size_t s = edge_find_slot(v, w);
         return s == SIZE_MAX ? NODE_NONE : edges[s].child;
     }
     // literal child add / remove: one literal child lives inline (lw, lc);
-    // from the second on, all of them live in edges[] (lw = LW_TABLE)
+    // from the second on, all of them live in edges[] (WIDE), and lw:lc
+    // hold a Bloom mask of their words (a superset after deletes; rebuilt
+    // exactly on relayout)
+    static void bloom_add(Node& x, uint32_t w) {
+        const uint64_t b = word_bloom(w);
+        x.lw |= (uint32_t)b;
+        x.lc |= (uint32_t)(b >> 32);
+    }
     void lit_add(uint32_t v, uint32_t w, uint32_t c) {
         Node& x = nodes[v];
-        if (x.lw == WORD_NONE) {
-            x.lw = w;
-            x.lc = c;
-            return;
-        }
-        if (x.lw != LW_TABLE) {  // spill the inline pair to the table
-            edge_insert(v, x.lw, x.lc);
-            nodes[v].lw = LW_TABLE;
-            nodes[v].lc = NODE_NONE;
+        if (!(x.plus & WIDE)) {
+            if (x.lw == WORD_NONE) {
+                x.lw = w;
+                x.lc = c;
+                return;
+            }
+            edge_insert(v, x.lw, x.lc);  // spill the inline pair to the table
+            Node& y = nodes[v];
+            const uint32_t w0 = y.lw;
+            y.plus |= WIDE;
+            y.lw = 0;
+            y.lc = 0;
+            bloom_add(y, w0);
         }
         edge_insert(v, w, c);
+        bloom_add(nodes[v], w);
     }
     void lit_remove(uint32_t v, uint32_t w) {
         Node& x = nodes[v];
-        if (x.lw == LW_TABLE) {
+        if (x.plus & WIDE) {
             edge_erase(v, w);
         } else if (x.lw == w) {
             x.lw = WORD_NONE;
             x.lc = NODE_NONE;
         }
         if (--aux[v].lit_count == 0) {
+            nodes[v].plus &= ~WIDE;
             nodes[v].lw = WORD_NONE;
             nodes[v].lc = NODE_NONE;
         }
@@ -389,7 +437,7 @@ struct tm_engine {
         if (c != NODE_NONE) return c;
         c = new_node(v, w);
         if (w == WORD_PLUS) {
-            nodes[v].plus = c;
+            nodes[v].plus = (nodes[v].plus & WIDE) | c;
         } else if (w == WORD_HASH) {
             nodes[v].hash = c;
             edge_insert(v, WORD_HASH, c);
@@ -398,13 +446,13 @@ struct tm_engine {
             aux[v].lit_count++;
         }
         aux[v].edge_count++;
-        node_dirty.mark(v);
+        touched(v);
         return c;
     }
     void unlink_child(uint32_t c) {
         uint32_t v = aux[c].parent, w = aux[c].word;
         if (w == WORD_PLUS) {
-            nodes[v].plus = NODE_NONE;
+            nodes[v].plus = (nodes[v].plus & WIDE) | NODE_NONE;
         } else if (w == WORD_HASH) {
             nodes[v].hash = NODE_NONE;
             nodes[v].hash_filter = FILTER_NONE;
@@ -414,7 +462,7 @@ struct tm_engine {
             lit_remove(v, w);
         }
         aux[v].edge_count--;
-        node_dirty.mark(v);
+        touched(v);
         nodes[c] = empty_node();
         aux[c] = NodeAux{NODE_NONE, 0, 0, 0};
         node_dirty.mark(c);
@@ -433,11 +481,11 @@ struct tm_engine {
     // when c is a '#' child)
     void set_topic(uint32_t c, uint32_t fid) {
         nodes[c].self_filter = fid;
-        node_dirty.mark(c);
+        touched(c);
         if (aux[c].word == WORD_HASH && aux[c].parent != NODE_NONE) {
             nodes[aux[c].parent].hash_filter = fid;
             nodes[aux[c].parent].hash_filter2 = fid;
-            node_dirty.mark(aux[c].parent);
+            touched(aux[c].parent);
         }
     }
 
@@ -512,7 +560,7 @@ struct tm_engine {
         std::vector<uint32_t> start(N + 1, 0);
         for (size_t v = 0; v < N; ++v) {
             if (aux[v].parent == NODE_NONE && v != ROOT) continue;  // free slot
-            if (nodes[v].lw != WORD_NONE && nodes[v].lw != LW_TABLE) start[v + 1]++;
+            if (!(nodes[v].plus & WIDE) && nodes[v].lw != WORD_NONE) start[v + 1]++;
         }
         for (const EdgeSlot& e : edges)
             if (e.parent != EDGE_EMPTY && e.word != WORD_HASH) start[e.parent + 1]++;
@@ -522,7 +570,7 @@ struct tm_engine {
             std::vector<uint32_t> fill(start.begin(), start.end() - 1);
             for (size_t v = 0; v < N; ++v) {
                 if (aux[v].parent == NODE_NONE && v != ROOT) continue;
-                if (nodes[v].lw != WORD_NONE && nodes[v].lw != LW_TABLE) kids[fill[v]++] = nodes[v].lc;
+                if (!(nodes[v].plus & WIDE) && nodes[v].lw != WORD_NONE) kids[fill[v]++] = nodes[v].lc;
             }
             for (const EdgeSlot& e : edges)
                 if (e.parent != EDGE_EMPTY && e.word != WORD_HASH) kids[fill[e.parent]++] = e.child;
@@ -538,7 +586,7 @@ struct tm_engine {
             newid[v] = (uint32_t)order.size();
             order.push_back(v);
             if (nodes[v].hash != NODE_NONE) stack.push_back(nodes[v].hash);
-            if (nodes[v].plus != NODE_NONE) stack.push_back(nodes[v].plus);
+            if ((nodes[v].plus & NODE_MASK) != NODE_NONE) stack.push_back(nodes[v].plus & NODE_MASK);
             for (uint32_t k = start[v + 1]; k > start[v]; --k) stack.push_back(kids[k - 1]);
         }
         std::vector<uint32_t>().swap(kids);
@@ -548,9 +596,10 @@ struct tm_engine {
         std::vector<NodeAux> na(order.size());
         for (size_t i = 0; i < order.size(); ++i) {
             Node x = nodes[order[i]];
-            x.plus = remap(x.plus);
+            x.plus = (x.plus & WIDE) | remap(x.plus & NODE_MASK);
             x.hash = remap(x.hash);
-            if (x.lw != WORD_NONE && x.lw != LW_TABLE) x.lc = remap(x.lc);
+            if (x.plus & WIDE) x.lw = x.lc = 0;   // Bloom rebuilt exactly below
+            else if (x.lw != WORD_NONE) x.lc = remap(x.lc);
             nn[i] = x;
             NodeAux a = aux[order[i]];
             a.parent = remap(a.parent);
@@ -559,12 +608,14 @@ struct tm_engine {
         // edge table with the new ids
         std::vector<EdgeSlot> old;
         old.swap(edges);
-        edges.assign(old.size(), EdgeSlot{EDGE_EMPTY, 0, 0, 0});
+        edges.assign(old.size(), kEmptySlot);
         for (const EdgeSlot& e : old)
-            if (e.parent != EDGE_EMPTY) edge_place(EdgeSlot{newid[e.parent], e.word, newid[e.child], 0});
+            if (e.parent != EDGE_EMPTY && e.word != WORD_HASH) bloom_add(nn[newid[e.parent]], e.word);
+        nodes.swap(nn);
+        for (const EdgeSlot& e : old)
+            if (e.parent != EDGE_EMPTY) edge_place(slot_for(newid[e.parent], e.word, newid[e.child]));
         for (FilterRec& f : filters)
             if (f.node != NODE_NONE) f.node = newid[f.node];
-        nodes.swap(nn);
         aux.swap(na);
         free_nodes.clear();
         created_since_layout = 0;
@@ -685,7 +736,7 @@ struct tm_engine {
         w_words.ensure((nbytes + n + 1) * 4);
         w_path.ensure((nbytes + 2ull * n + 2) * 4);
         w_total.ensure(64);
-        w_stats.ensure(64);
+        w_stats.ensure(STATS_BYTES);
         w_meta.ensure((size_t)(n + 1) * 4);
         w_scan.ensure(scan_tmp_elems(n) * 8 + 8);
         w_stage.ensure(((size_t)n * stage_k + 4) * 4);
@@ -699,7 +750,7 @@ struct tm_engine {
         ensure_workspace(n, nbytes);
         ImageView im = view();
         unsigned long long* sp = w_stats.as<unsigned long long>();
-        if (stats_enabled) HIPCHK(hipMemsetAsync(w_stats.p, 0, 64, st));
+        if (stats_enabled) HIPCHK(hipMemsetAsync(w_stats.p, 0, STATS_BYTES, st));
         static const char* kStage[4] = {"tokenize", "walk", "scan", "copy_out"};
         hipEvent_t marks[8];
         if (timing_enabled)
@@ -717,7 +768,7 @@ struct tm_engine {
         qb.scan_tmp = w_scan.as<uint64_t>();
         qb.ws = w_ws.as<unsigned long long>();
         HIPCHK(launch_queue(stats_enabled, xcdq != 0, im, bytes, off, n, qb, stage_k, counts, out_off, ids, cap,
-                            total, sp, st, timing_enabled ? marks : nullptr));
+                            total, sp, st, timing_enabled ? marks : nullptr, walk_bpc));
         if (timing_enabled)
             for (int i = 0; i < 4; ++i) ev_pending.push_back(ev_cur[i]);
     }
@@ -730,12 +781,14 @@ struct tm_engine {
     }
     void collect_stats() {
         if (!stats_enabled || !w_stats.p) return;
-        unsigned long long h[4] = {0, 0, 0, 0};
+        unsigned long long h[6] = {0, 0, 0, 0, 0, 0};
         HIPCHK(hipMemcpy(h, w_stats.p, sizeof(h), hipMemcpyDeviceToHost));
         last_stats.levels = h[0];
         last_stats.visits = h[1];
         last_stats.edge_reads = h[2];
         last_stats.matches = h[3];
+        last_stats.leaf_visits = h[4];
+        last_stats.probe_loads = h[5];
     }
 };
 
@@ -816,7 +869,7 @@ int tm_open(const tm_config* cfg, tm_engine** out) {
         e->nodes.reserve(nodes_hint);
         e->aux.reserve(nodes_hint);
         // wide nodes' literal edges and '#' edges use the table (load <= 1/4)
-        e->edges.assign(next_pow2(nodes_hint), EdgeSlot{EDGE_EMPTY, 0, 0, 0});
+        e->edges.assign(next_pow2(nodes_hint), kEmptySlot);
     }
     if (dev >= 0) {
         int ndev = 0;
@@ -1011,9 +1064,25 @@ int tm_match_batch_device(tm_engine* e, const uint8_t* d_bytes, const uint64_t* 
     });
 }
 
+// diagnostics (not part of include/topicmatch.h): the last stats-mode
+// batch's per-level histogram [visits, probe loads, failed probes] x 16
+extern "C" int tm_debug_hist(tm_engine* e, uint64_t* out, int n) {
+    if (!e || !out || n > 48) return TM_EINVAL;
+    return guarded(e, [&]() -> int {
+        if (!e->w_stats.p) return TM_EINVAL;
+        HIPCHK(hipMemcpy(out, e->w_stats.as<uint64_t>() + 8, (size_t)n * 8, hipMemcpyDeviceToHost));
+        return TM_OK;
+    });
+}
+
 int tm_set_option(tm_engine* e, const char* name, int64_t value) {
     if (!name) return TM_EINVAL;
     return guarded(e, [&]() -> int {
+        if (!std::strcmp(name, "walk_bpc")) {
+            if (value < 0 || value > 64) return TM_EINVAL;
+            e->walk_bpc = (uint32_t)value;
+            return TM_OK;
+        }
         if (!std::strcmp(name, "xcdq")) {
             if (value < 0 || value > 1) return TM_EINVAL;
             e->xcdq = (int)value;

@@ -11,15 +11,18 @@
 //   nodes[]  32 B per node in two 16 B halves, so every step of the walk is
 //            ONE 16 B load: a visit with topic words left reads the inner
 //            half {'+' child, '#' filter, one inline literal child (word,
-//            child)}, a visit at the topic's last level reads the leaf half
+//            child) or, for a WIDE node, a 64-bit Bloom mask of its literal
+//            children's words that rejects most absent words without a probe},
+//            a visit at the topic's last level reads the leaf half
 //            {filter ending here, '#' filter}.  The '+' edge and the '#' edge
 //            are fields of the parent, the filter ending at the '#' child is
 //            carried inline (the reference's 'match_#'/2, emqx_trie.erl:140-145,
 //            costs nothing beyond the visit's own load).
-//   edges[]  literal edges of the wide nodes (>= 2 literal children, lw =
-//            LW_TABLE) and the '#' children (word WORD_HASH, only looked up
+//   edges[]  literal edges of the wide nodes (>= 2 literal children, WIDE
+//            flag) and the '#' children (word WORD_HASH, only looked up
 //            for the out-of-domain topic level "#"): open addressing, 16 B
-//            slots, linear probing slot by slot from the home slot, load <= 1/4.
+//            slots (key + child id; see TM_SLOT_RECORD), linear probing slot
+//            by slot from the home slot, load <= 1/4.
 //   dict[]   word dictionary: 64-bit hash -> word id, byte-verified against
 //            the word arena, so tokenisation is collision-free (no hash-only
 //            identity).
@@ -31,7 +34,8 @@ namespace tmx {
 constexpr uint32_t ROOT       = 0u;
 constexpr uint32_t NODE_MASK  = 0x1FFFFFFFu;   // node ids are 29-bit (walk path packs 3 flag bits)
 constexpr uint32_t NODE_NONE  = 0x1FFFFFFFu;
-constexpr uint32_t LW_TABLE   = 0xFFFFFFFCu;   // nodes[].lw: literal children live in edges[]
+constexpr uint32_t WIDE       = 0x80000000u;   // nodes[].plus bit 31: >= 2 literal children, all in
+                                               // edges[]; lw:lc then hold a 64-bit Bloom mask of their words
 constexpr uint32_t FILTER_NONE = 0xFFFFFFFFu;
 
 // token ids produced by the tokenizer (emqx_topic:words/1 + word/1)
@@ -44,10 +48,10 @@ constexpr uint32_t EDGE_EMPTY = 0xFFFFFFFFu;   // slot.parent of an empty slot
 
 struct alignas(32) Node {
     // inner half: read by a visit with words left (level r < n)
-    uint32_t plus;         // '+' child node id, NODE_NONE if none
+    uint32_t plus;         // '+' child node id (NODE_NONE if none) | WIDE
     uint32_t hash_filter;  // filter id of the '#' child (its topic), FILTER_NONE if none
-    uint32_t lw;           // word of the single literal child, WORD_NONE if none, LW_TABLE if >= 2
-    uint32_t lc;           // that child's node id
+    uint32_t lw;           // narrow: word of the single literal child (WORD_NONE if none); WIDE: Bloom bits 0-31
+    uint32_t lc;           // narrow: that child's node id; WIDE: Bloom bits 32-63
     // leaf half: read by a visit at the topic's last level (r == n)
     uint32_t self_filter;  // filter id ending at this node, FILTER_NONE if topic = undefined
     uint32_t hash_filter2; // = hash_filter
@@ -56,12 +60,29 @@ struct alignas(32) Node {
 };
 static_assert(sizeof(Node) == 32, "node record is two 16 B halves");
 
-struct alignas(16) EdgeSlot {
+// Edge slot layout (build-time A/B, TM_SLOT_RECORD):
+//   0: 16 B {parent, word, child, child.plus}: the probe finds the child id,
+//      the child's visit loads its node half;
+//   1: 32 B, second half {child.hash_filter, child.lw, child.lc,
+//      child.self_filter}: the probe that finds the edge also delivers the
+//      child's record (same 64 B sector), at twice the table footprint.
+#ifndef TM_SLOT_RECORD
+#define TM_SLOT_RECORD 0
+#endif
+constexpr bool SLOT_RECORD = TM_SLOT_RECORD != 0;
+struct alignas(SLOT_RECORD ? 32 : 16) EdgeSlot {
     uint32_t parent;       // EDGE_EMPTY when free
     uint32_t word;
     uint32_t child;
-    uint32_t pad;
+    uint32_t plus;         // child's record ...
+#if TM_SLOT_RECORD
+    uint32_t hash_filter;
+    uint32_t lw;
+    uint32_t lc;
+    uint32_t self_filter;
+#endif
 };
+static_assert(sizeof(EdgeSlot) == (SLOT_RECORD ? 32 : 16), "edge slot is one or two 16 B halves");
 
 struct alignas(16) DictSlot {
     uint64_t hash;         // 64-bit word hash (0 reserved for empty)
@@ -96,6 +117,12 @@ TM_HD uint64_t fmix64(uint64_t k) {
 
 TM_HD uint64_t edge_hash(uint32_t parent, uint32_t word) {
     return fmix64(((uint64_t)parent << 32) | word);
+}
+
+// Bloom bits of a literal word in a WIDE node's mask (2 of 64)
+TM_HD uint64_t word_bloom(uint32_t w) {
+    const uint64_t h = fmix64(0x9E3779B97F4A7C15ULL ^ w);
+    return (1ull << (h & 63)) | (1ull << ((h >> 6) & 63));
 }
 
 // home slot of key (parent, word)

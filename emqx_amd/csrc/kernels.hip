@@ -150,29 +150,52 @@ tm_tokenize(ImageView im, const uint8_t* __restrict__ bytes, const uint64_t* __r
 }
 
 // ---------------------------------------------------------------------------
+// The child found by a probe, with its record when the edge table delivered
+// it: the inner half {plus, hash_filter, lw, lc} and the filter ending at
+// the child.
+struct Hit {
+    uint32_t child;
+    uint32_t plus, hf, lw, lc, sf;   // (no HIP vector type here: its union
+    bool have;                       // layout sends the struct to scratch)
+};
+
 // literal (or '#') edge (v, w) in the edge table: linear probing, one 16 B
-// slot per load (load factor <= 1/4: ~1.2 loads per hit)
-__device__ __forceinline__ uint32_t probe_edge(const ImageView& im, uint32_t v, uint32_t w) {
+// key half per slot (load factor <= 1/4: ~1.2 loads per hit); on a hit the
+// slot's second half completes the child's record
+template <bool STATS>
+__device__ __forceinline__ Hit probe_edge(const ImageView& im, uint32_t v, uint32_t w, uint64_t& loads) {
     uint64_t s = edge_home(v, w, im.edge_slot_mask);
     for (;;) {
-        const uint4 e = *reinterpret_cast<const uint4*>(im.edges + s);
-        if (e.x == v && e.y == w) return e.z;
-        if (e.x == EDGE_EMPTY) return NODE_NONE;
+        const uint4* slot = reinterpret_cast<const uint4*>(im.edges + s);
+        const uint4 e = slot[0];
+        if (STATS) ++loads;
+        if (e.x == v && e.y == w) {
+            if (!SLOT_RECORD) return Hit{e.z, 0, 0, 0, 0, 0, false};
+            const uint4 d = slot[1];   // same 32 B: hash_filter, lw, lc, self_filter
+            return Hit{e.z, e.w, d.x, d.y, d.z, d.w, true};
+        }
+        if (e.x == EDGE_EMPTY) return Hit{NODE_NONE, 0, 0, 0, 0, 0, false};
         s = (s + 1) & im.edge_slot_mask;
     }
 }
 
-// child of v by topic word w, given v's inner half q.  WORD_PLUS / WORD_HASH
-// reproduce the reference for the out-of-domain topic levels "+" / "#": the
-// fold over [W, '+'] at emqx_trie.erl:131-136 follows the '+' / '#' edge.
-__device__ __forceinline__ uint32_t lit_child(const ImageView& im, uint32_t v, const uint4& q, uint32_t w) {
+// child of v by topic word w, given v's inner half {plus, lw, lc}.
+// WORD_PLUS / WORD_HASH reproduce the reference for the out-of-domain topic
+// levels "+" / "#": the fold over [W, '+'] at emqx_trie.erl:131-136 follows
+// the '+' / '#' edge.
+template <bool STATS>
+__device__ __forceinline__ Hit lit_child(const ImageView& im, uint32_t v, uint32_t plus, uint32_t lw, uint32_t lc,
+                                         uint32_t w, uint64_t& loads) {
+    const Hit none{NODE_NONE, 0, 0, 0, 0, 0, false};
     if (w < WORD_MAX) {
-        if (q.z == w) return q.w;
-        return q.z == LW_TABLE ? probe_edge(im, v, w) : NODE_NONE;
+        if (!(plus & WIDE)) return Hit{lw == w ? lc : NODE_NONE, 0, 0, 0, 0, 0, false};
+        const uint64_t b = word_bloom(w);
+        const uint64_t mask = ((uint64_t)lc << 32) | lw;
+        return (mask & b) == b ? probe_edge<STATS>(im, v, w, loads) : none;
     }
-    if (w == WORD_PLUS) return q.x;
-    if (w == WORD_HASH) return probe_edge(im, v, WORD_HASH);
-    return NODE_NONE;   // WORD_NONE: bytes no filter contains
+    if (w == WORD_PLUS) return Hit{plus & NODE_MASK, 0, 0, 0, 0, 0, false};
+    if (w == WORD_HASH) return probe_edge<STATS>(im, v, WORD_HASH, loads);
+    return none;   // WORD_NONE: bytes no filter contains
 }
 
 __device__ __forceinline__ uint4 load_half(const ImageView& im, uint32_t v, bool leaf) {
@@ -190,20 +213,24 @@ __device__ __forceinline__ uint4 load_half(const ImageView& im, uint32_t v, bool
 // literal subtree below it runs; a step visits one node with one 16 B load
 // and then either descends or pops to the deepest pending '+' child.
 struct WalkStats {
-    uint64_t visits = 0, edge_reads = 0;
+    uint64_t visits = 0, edge_reads = 0, leaf_visits = 0, probe_loads = 0;
+    unsigned long long* hist = nullptr;   // STATS diagnostics: [visits, probe loads, failed probes] x 16 levels
 };
+constexpr int HIST_OFF = 8;   // hist = stats + HIST_OFF
 
 struct Cursor {
-    uint32_t v, r, n, r0;
+    uint32_t v, r, n, r0;   // node to visit next and its level; topic levels; start level
 };
 
-// topic words in VGPRs (n <= WREG): dynamic index by a select chain
+// topic words in VGPRs (n <= WREG): dynamic index by AND-masks (a select
+// chain or tree over the array gets turned back into a private-memory array
+// indexed by r, i.e. scratch loads, by the compiler)
 struct RegWords {
     uint32_t w[WREG];
     __device__ __forceinline__ uint32_t operator()(uint32_t r) const {
-        uint32_t x = w[0];
+        uint32_t x = 0;
 #pragma unroll
-        for (uint32_t k = 1; k < WREG; ++k) x = r == k ? w[k] : x;
+        for (uint32_t k = 0; k < WREG; ++k) x |= w[k] & (0u - (uint32_t)(r == k));
         return x;
     }
 };
@@ -227,7 +254,8 @@ struct GlobalPath {
 // starts at node <<W0>>, skipping root's '#' and '+' edges.  false: nothing
 // to walk.
 template <class Words>
-__device__ __forceinline__ bool walk_begin(const ImageView& im, Cursor& c, uint32_t n, bool dollar, const Words& W) {
+__device__ __forceinline__ bool walk_begin(const ImageView& im, Cursor& c, uint32_t n, bool dollar, const Words& W,
+                                           WalkStats& st) {
     c.n = n;
     if (!dollar) {
         c.v = ROOT;
@@ -235,35 +263,66 @@ __device__ __forceinline__ bool walk_begin(const ImageView& im, Cursor& c, uint3
         return true;
     }
     const uint4 q = load_half(im, ROOT, false);
-    c.v = lit_child(im, ROOT, q, W(0));
+    c.v = lit_child<false>(im, ROOT, q.x, q.z, q.w, W(0), st.probe_loads).child;
     c.r = c.r0 = 1;
     return c.v != NODE_NONE;
 }
 
-// one step; true when the topic's walk is complete
+// one step; true when the topic's walk is complete.  A step loads ONE node
+// half; a literal child found through the edge table arrives with its record
+// (EdgeSlot), so it is visited in the same step, and so on down a chain of
+// table children, until a child needs its own load or the walk pops.
 template <bool STATS, class Path, class Words, class Emit>
 __device__ __forceinline__ bool walk_step(const ImageView& im, Cursor& c, Path path, const Words& W, Emit& emit,
                                           WalkStats& st) {
-    const uint32_t v = c.v, r = c.r;
-    const bool leaf = r == c.n;
-    const uint4 q = load_half(im, v, leaf);
-    if (STATS) {
-        ++st.visits;
-        st.edge_reads += leaf ? 1 : 3;   // 'match_#' (:141) + fold over [W, '+'] (:132)
-    }
-    if (q.y != FILTER_NONE) emit(q.y);   // 'match_#': the '#' filter (both halves carry it)
-    uint32_t next = NODE_NONE;
-    if (leaf) {
-        if (q.x != FILTER_NONE) emit(q.x);   // the node's own filter (mnesia:read of the node, :128)
-    } else {
-        const uint32_t lc = lit_child(im, v, q, W(r));
-        path(r) = lc != NODE_NONE ? q.x : NODE_NONE;
-        next = lc != NODE_NONE ? lc : q.x;
-    }
-    if (next != NODE_NONE) {
-        c.v = next;
-        c.r = r + 1;
-        return false;
+    uint32_t v = c.v, r = c.r;
+    bool leaf = r == c.n;
+    const uint4 h = load_half(im, v, leaf);   // inner {plus, hf, lw, lc} / leaf {sf, hf, hash, pad}
+    uint32_t plus = h.x, hf = h.y, lw = h.z, lc = h.w, sf = h.x;
+    for (;;) {
+        if (STATS) {
+            ++st.visits;
+            st.edge_reads += leaf ? 1 : 3;   // 'match_#' (:141) + fold over [W, '+'] (:132)
+            st.leaf_visits += leaf ? 1 : 0;
+        }
+        if (hf != FILTER_NONE) emit(hf);     // 'match_#': the '#' filter
+        if (leaf) {
+            if (sf != FILTER_NONE) emit(sf);   // the node's own filter (mnesia:read of the node, :128)
+            break;
+        }
+        const uint64_t pl0 = st.probe_loads;
+        const Hit g = lit_child<STATS>(im, v, plus, lw, lc, W(r), st.probe_loads);
+        if (STATS && st.hist) {
+            const uint32_t lv = r < 15 ? r : 15;
+            atomicAdd(st.hist + lv, 1ull);
+            if (st.probe_loads != pl0) atomicAdd(st.hist + 16 + lv, (unsigned long long)(st.probe_loads - pl0));
+            if (st.probe_loads != pl0 && g.child == NODE_NONE) atomicAdd(st.hist + 32 + lv, 1ull);
+        }
+        const uint32_t pc = plus & NODE_MASK;
+        if (g.child != NODE_NONE) {   // literal subtree first, '+' child pending at level r
+            path(r) = pc;
+            v = g.child;
+            ++r;
+            if (!g.have) {
+                c.v = v;
+                c.r = r;
+                return false;
+            }
+            plus = g.plus;
+            hf = g.hf;
+            lw = g.lw;
+            lc = g.lc;
+            sf = g.sf;
+            leaf = r == c.n;
+            continue;
+        }
+        if (pc != NODE_NONE) {        // no literal child: straight into the '+' subtree
+            path(r) = NODE_NONE;
+            c.v = pc;
+            c.r = r + 1;
+            return false;
+        }
+        break;
     }
     for (uint32_t k = r; k > c.r0;) {   // pop to the deepest pending '+' child
         --k;
@@ -282,7 +341,7 @@ template <bool STATS, class Path, class Words, class Emit>
 __device__ __forceinline__ void walk(const ImageView& im, uint32_t n, bool dollar, Path path, const Words& W,
                                      Emit& emit, WalkStats& st) {
     Cursor c;
-    if (!walk_begin(im, c, n, dollar, W)) return;
+    if (!walk_begin(im, c, n, dollar, W, st)) return;
     while (!walk_step<STATS>(im, c, path, W, emit, st)) {
     }
 }
@@ -324,12 +383,12 @@ struct TailEmit {
 };
 
 template <bool STATS>
-__device__ __forceinline__ void wave_stats_add(unsigned long long* stats, uint64_t a, uint64_t b, uint64_t c,
-                                               uint64_t d) {
+__device__ __forceinline__ void wave_stats_add(unsigned long long* stats, uint64_t lev, uint64_t matches,
+                                               const WalkStats& st) {
     if (!STATS) return;
-    uint64_t v[4] = {a, b, c, d};
+    uint64_t v[6] = {lev, st.visits, st.edge_reads, matches, st.leaf_visits, st.probe_loads};
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < 6; ++k) {
         uint64_t x = v[k];
         for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
         if ((threadIdx.x & 63) == 0 && x) atomicAdd(stats + k, (unsigned long long)x);
@@ -376,6 +435,7 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
     Cursor cur;
     RowEmit em{nullptr, K, 0, make_uint4(0, 0, 0, 0)};
     WalkStats st;
+    if (STATS) st.hist = stats + HIST_OFF;
     uint64_t lev_sum = 0, match_sum = 0;
     for (;;) {
         const bool need = (my == NO_TOPIC) && !drained;
@@ -445,12 +505,12 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
                                 rw.w[4 * k + 3] = x.w;
                             }
                         }
-                        go = walk_begin(im, cur, nl, dollar, rw);
+                        go = walk_begin(im, cur, nl, dollar, rw, st);
                     } else {
                         const uint64_t b = off[i] - off[0];
                         mw = MemWords{tw, words + b + i};
                         gp.base = gpath + b + 2ull * i;
-                        go = walk_begin(im, cur, nl, dollar, mw);
+                        go = walk_begin(im, cur, nl, dollar, mw, st);
                     }
                     if (go) my = i;
                     else counts[i] = 0;
@@ -480,7 +540,7 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
             my = NO_TOPIC;
         }
     }
-    wave_stats_add<STATS>(stats, lev_sum, st.visits, st.edge_reads, match_sum);
+    wave_stats_add<STATS>(stats, lev_sum, match_sum, st);
 }
 
 // tm_copy_out: per 256 topics, the block's output range is copied from the
@@ -595,11 +655,12 @@ static inline uint32_t div_up(uint64_t a, uint64_t b) { return (uint32_t)((a + b
 
 // one resident wave set: blocks per CU at full occupancy x CUs
 template <typename Kern>
-static uint32_t resident_grid(Kern k, uint32_t n_tiles) {
+static uint32_t resident_grid(Kern k, uint32_t n_tiles, uint32_t cap_per_cu = 0) {
     int dev = 0, cus = 256, per = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k, BLOCK, 0);
+    if (cap_per_cu && per > (int)cap_per_cu) per = (int)cap_per_cu;
     uint32_t g = (uint32_t)((per > 0 ? per : 1) * (cus > 0 ? cus : 1));
     return g < n_tiles ? g : n_tiles;
 }
@@ -618,7 +679,7 @@ static hipError_t launch_scan(const uint32_t* counts, uint32_t n, uint64_t* out_
 hipError_t launch_queue(bool stats_mode, bool xcdq, const ImageView& im, const uint8_t* bytes, const uint64_t* off,
                         uint32_t n, const QueueBufs& qb, uint32_t K, uint32_t* counts, uint64_t* out_off,
                         uint32_t* out, uint64_t out_cap, uint64_t* total, unsigned long long* stats,
-                        hipStream_t st, hipEvent_t* marks) {
+                        hipStream_t st, hipEvent_t* marks, uint32_t walk_blocks_per_cu) {
     auto mark = [&](int i) {
         if (marks) (void)hipEventRecord(marks[i], st);
     };
@@ -636,7 +697,7 @@ hipError_t launch_queue(bool stats_mode, bool xcdq, const ImageView& im, const u
     hipLaunchKernelGGL(tm_tokenize, g, blk, 0, st, im, bytes, off, n, qb.twords, qb.words, qb.meta);
     mark(1);
     mark(2);
-    const uint32_t wg = resident_grid(tm_walk_queue<false, false>, div_up(n, 64));
+    const uint32_t wg = resident_grid(tm_walk_queue<false, false>, div_up(n, 64), walk_blocks_per_cu);
 #define TM_Q(S, X)                                                                                              \
     hipLaunchKernelGGL((tm_walk_queue<S, X>), dim3(wg), blk, 0, st, im, off, n, qb.twords, qb.words, qb.meta, \
                        qb.path, qb.stage, K, counts, qb.ws, stats)

@@ -63,6 +63,8 @@ typedef struct tm_batch_stats {
     uint64_t edge_reads;      /* E = mnesia:read(?TRIE,...) calls the reference  */
                               /*     would make (emqx_trie.erl:132,141)          */
     uint64_t matches;         /* sum M_t                                         */
+    uint64_t leaf_visits;     /* visits at the topic's last level (leaf half)    */
+    uint64_t probe_loads;     /* 16 B edge-table slot loads (wide nodes, '#')    */
 } tm_batch_stats;
 
 /* engine lifetime ------------------------------------------------------------ */
