@@ -110,6 +110,8 @@ def main():
 
     # size the output from one counting pass (untimed), with exact stats
     eng.set_stats(True)
+    if a.hist:
+        eng.set_option("hist", 1)
     eng.match_batch_device(d_b, d_o, n, nbytes, d_c, d_oo, None, 0, d_t, stream=st)
     torch.cuda.synchronize(dev)
     stats = eng.last_stats()
@@ -208,6 +210,15 @@ def main():
         kname = max(kms, key=kms.get) if kms else None
         walk_ms = kms.get(kname, 0.0) if kname else 0.0
         achieved = B / (walk_ms * 1e-3) / 1e9 if walk_ms > 0 else None
+        # HBM traffic of the walk from the committed PMC passes of this same
+        # workload (tools/pmc_passes.sh -> tools/traffic.py); null otherwise
+        traffic = None
+        tpath = os.path.join(ROOT, "profiles", "traffic_c%d.json" % a.config)
+        if os.path.exists(tpath) and kname == "walk":
+            tj = json.load(open(tpath))
+            tc = tj.get("config") or {}
+            if tc.get("filters") == n_filters and tc.get("topics_per_gpu_step") == n and tc.get("levels") == cfg["levels"]:
+                traffic = tj["traffic_bytes_per_launch"] / (walk_ms * 1e-3) / 1e9
         out = {
             "metric": METRIC,
             "value": topics_per_s,
@@ -226,7 +237,9 @@ def main():
                        "filters": n_filters, "topics_per_gpu_step": n, "levels": cfg["levels"],
                        "parallelism": "replicated trie x %d, topic batches sharded by rank" % world},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": None,
+                         "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
+                         "traffic_source": ("FETCH_SIZE+WRITE_SIZE per launch, profiles/traffic_c%d.json, over this "
+                                            "run's walk time" % a.config) if traffic else None,
                          "kernel": {"walk": "tm_walk_queue (balanced NFA walk, one 16 B node-half load per step)"
                                     }.get(kname, kname),
                          "kernel_ms": walk_ms,

@@ -171,6 +171,7 @@ struct tm_engine {
     // ---- device image ----
     DevBuf d_nodes, d_edges, d_dict, d_arena, d_woff;
     bool dev_dirty = true;
+    int hist_enabled = 0;             // option "hist": per-level histogram in stats mode (diagnostic, slow)
     uint32_t walk_bpc = 0;            // option "walk_bpc": walk blocks per CU (0 = full occupancy)
     int xcdq = 1;                     // option "xcdq": per-XCD dequeue ranges in the queue walk (default on)
     int layout_mode = 1;              // option "layout": 0 off, 1 auto, 2 every commit (tests)
@@ -768,7 +769,7 @@ struct tm_engine {
         qb.scan_tmp = w_scan.as<uint64_t>();
         qb.ws = w_ws.as<unsigned long long>();
         HIPCHK(launch_queue(stats_enabled, xcdq != 0, im, bytes, off, n, qb, stage_k, counts, out_off, ids, cap,
-                            total, sp, st, timing_enabled ? marks : nullptr, walk_bpc));
+                            total, sp, st, timing_enabled ? marks : nullptr, walk_bpc, hist_enabled != 0));
         if (timing_enabled)
             for (int i = 0; i < 4; ++i) ev_pending.push_back(ev_cur[i]);
     }
@@ -1078,6 +1079,10 @@ extern "C" int tm_debug_hist(tm_engine* e, uint64_t* out, int n) {
 int tm_set_option(tm_engine* e, const char* name, int64_t value) {
     if (!name) return TM_EINVAL;
     return guarded(e, [&]() -> int {
+        if (!std::strcmp(name, "hist")) {
+            e->hist_enabled = value != 0;
+            return TM_OK;
+        }
         if (!std::strcmp(name, "walk_bpc")) {
             if (value < 0 || value > 64) return TM_EINVAL;
             e->walk_bpc = (uint32_t)value;

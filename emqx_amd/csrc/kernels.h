@@ -30,7 +30,7 @@ struct QueueBufs {
 hipError_t launch_queue(bool stats_mode, bool xcdq, const ImageView& im, const uint8_t* bytes, const uint64_t* off,
                         uint32_t n, const QueueBufs& qb, uint32_t K, uint32_t* counts, uint64_t* out_off,
                         uint32_t* out, uint64_t out_cap, uint64_t* total, unsigned long long* stats,
-                        hipStream_t st, hipEvent_t* marks, uint32_t walk_blocks_per_cu = 0);
+                        hipStream_t st, hipEvent_t* marks, uint32_t walk_blocks_per_cu = 0, bool hist = false);
 size_t scan_tmp_elems(uint32_t n);
 
 }  // namespace tmx

@@ -419,7 +419,8 @@ __global__ void __launch_bounds__(BLOCK)
 tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const uint32_t* __restrict__ twords,
               const uint32_t* __restrict__ words, const uint32_t* __restrict__ meta, uint32_t* __restrict__ gpath,
               uint32_t* __restrict__ stage, uint32_t K, uint32_t* __restrict__ counts,
-              unsigned long long* __restrict__ ws, unsigned long long* __restrict__ stats) {
+              unsigned long long* __restrict__ ws, unsigned long long* __restrict__ stats,
+              unsigned long long* __restrict__ hist) {
     __shared__ uint32_t lds_path[WREG * BLOCK];
     const uint32_t lane = threadIdx.x & 63;
     const LdsPath lp{lds_path + threadIdx.x};
@@ -435,7 +436,7 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
     Cursor cur;
     RowEmit em{nullptr, K, 0, make_uint4(0, 0, 0, 0)};
     WalkStats st;
-    if (STATS) st.hist = stats + HIST_OFF;
+    if (STATS) st.hist = hist;
     uint64_t lev_sum = 0, match_sum = 0;
     for (;;) {
         const bool need = (my == NO_TOPIC) && !drained;
@@ -679,7 +680,7 @@ static hipError_t launch_scan(const uint32_t* counts, uint32_t n, uint64_t* out_
 hipError_t launch_queue(bool stats_mode, bool xcdq, const ImageView& im, const uint8_t* bytes, const uint64_t* off,
                         uint32_t n, const QueueBufs& qb, uint32_t K, uint32_t* counts, uint64_t* out_off,
                         uint32_t* out, uint64_t out_cap, uint64_t* total, unsigned long long* stats,
-                        hipStream_t st, hipEvent_t* marks, uint32_t walk_blocks_per_cu) {
+                        hipStream_t st, hipEvent_t* marks, uint32_t walk_blocks_per_cu, bool hist) {
     auto mark = [&](int i) {
         if (marks) (void)hipEventRecord(marks[i], st);
     };
@@ -700,7 +701,7 @@ hipError_t launch_queue(bool stats_mode, bool xcdq, const ImageView& im, const u
     const uint32_t wg = resident_grid(tm_walk_queue<false, false>, div_up(n, 64), walk_blocks_per_cu);
 #define TM_Q(S, X)                                                                                              \
     hipLaunchKernelGGL((tm_walk_queue<S, X>), dim3(wg), blk, 0, st, im, off, n, qb.twords, qb.words, qb.meta, \
-                       qb.path, qb.stage, K, counts, qb.ws, stats)
+                       qb.path, qb.stage, K, counts, qb.ws, stats, hist ? stats + HIST_OFF : nullptr)
     if (stats_mode) {
         if (xcdq) TM_Q(true, true); else TM_Q(true, false);
     } else {

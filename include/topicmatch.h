@@ -130,9 +130,10 @@ int tm_match_batch_device(tm_engine* e, const uint8_t* d_topic_bytes, const uint
                           uint64_t* d_total, void* hip_stream);
 
 /* Engine knobs (the app-env analogue of SURVEY §5 config):
- *   "walk"     5 = queue (default: tokenize, globally balanced walk, scan,
- *              coalesced copy-out), 0 = lane-per-topic fused, 1/2/3 = tiled
- *              fused (256/512/1024 topics per tile), 4 = two-pass
+ *   "xcdq"     1 = per-XCD dequeue heads over contiguous ranges of the batch
+ *              (default), 0 = one global head
+ *   "walk_bpc" walk workgroups per CU, 0 = full occupancy (default)
+ *   "hist"     1 = per-level visit/probe histogram in stats mode (diagnostic)
  *   "layout"   1 = renumber nodes in DFS preorder on commit once >= 1/4 of
  *              the live nodes are new (default), 0 = keep insertion order,
  *              2 = renumber on every commit

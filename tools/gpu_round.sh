@@ -1,6 +1,7 @@
 #!/bin/bash
-# One GPU call: parity tests, smoke, default bench line, rocprofv3 kernel trace.
-# Every GPU step has its own time limit; steps are chained with &&.
+# One GPU call: parity tests, smoke, default bench line, rocprofv3 kernel
+# trace, PMC passes.  Every GPU step has its own time limit; steps are
+# chained with &&.  TAG names the output directory under gpurun_out/.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
@@ -9,4 +10,5 @@ mkdir -p $OUT
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 && \
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 && \
 timeout -k 10 400 python -u bench.py ${BENCH_ARGS} > $OUT/bench.json 2> $OUT/bench.log && \
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --steps 10 --warmup 2 --cpu-sample 0 --check 0 ${BENCH_ARGS} > $OUT/prof_bench.json 2> $OUT/prof_bench.log
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --steps 10 --warmup 2 --cpu-sample 0 --check 0 ${BENCH_ARGS} > $OUT/prof_bench.json 2> $OUT/prof_bench.log && \
+PMC_DIR=${TAG:-run}/pmc ./tools/pmc_passes.sh

@@ -1,0 +1,37 @@
+"""Per-launch HBM traffic of the dominant kernel from a PMC pass directory
+(tools/pmc_passes.sh): FETCH_SIZE + WRITE_SIZE of tm_walk_queue, as the
+`roofline.traffic` figure bench.py reports.
+
+Units and corrections (/opt/skills/guides/MI355X_MICROARCH.md, HBM section):
+FETCH_SIZE/WRITE_SIZE are in KB.  The guide's x2 correction is for wide
+coalesced streaming reads; the walk's reads are random 16 B gathers, which
+profiles/ubench/gather_rates.txt calibrates at exactly one 64 B TCC_EA0_RDREQ
+(= 64 B of FETCH_SIZE) per L2-missing access, so FETCH_SIZE is taken as is.
+
+usage: python tools/traffic.py gpurun_out/pmc_x profiles/traffic_c3.json
+"""
+import json
+import subprocess
+import sys
+
+src, dst = sys.argv[1], sys.argv[2]
+summ = json.load(open(src + "/summary.json"))
+w = summ["tm_walk_queue"]
+log = open(src + "/fetch/log.txt").read().splitlines()
+line = next((json.loads(x) for x in log if x.startswith("{")), None)
+cfg = line["config"] if line else None
+rev = subprocess.run(["git", "rev-parse", "--short", "HEAD"], capture_output=True, text=True).stdout.strip()
+out = {
+    "kernel": "tm_walk_queue",
+    "config": cfg,
+    "fetch_bytes_per_launch": w["FETCH_SIZE"] * 1024.0,
+    "write_bytes_per_launch": w["WRITE_SIZE"] * 1024.0,
+    "traffic_bytes_per_launch": (w["FETCH_SIZE"] + w["WRITE_SIZE"]) * 1024.0,
+    "l2_hit_rate": w["TCC_HIT_sum"] / (w["TCC_HIT_sum"] + w["TCC_MISS_sum"]),
+    "ea_read_requests_per_launch": w.get("TCC_EA0_RDREQ_sum"),
+    "correction": "none: random 16 B gathers, 1 EA read request = 64 B (profiles/ubench/gather_rates.txt)",
+    "source": src,
+    "build": rev,
+}
+json.dump(out, open(dst, "w"), indent=1)
+print(json.dumps(out, indent=1))
