@@ -20,7 +20,10 @@ $(BUILD)/kernels.o: emqx_amd/csrc/kernels.hip emqx_amd/csrc/kernels.h emqx_amd/c
 $(BUILD)/engine.o: emqx_amd/csrc/engine.cpp emqx_amd/csrc/kernels.h emqx_amd/csrc/image.h include/topicmatch.h | $(BUILD)
 	$(HIPCC) -O3 -fPIC -std=c++17 -Wall $(TMDEFS) -c $< -o $@
 
-emqx_amd/libtopicmatch.so: $(BUILD)/kernels.o $(BUILD)/engine.o
+$(BUILD)/shard.o: emqx_amd/csrc/shard.hip emqx_amd/csrc/kernels.h emqx_amd/csrc/image.h | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+emqx_amd/libtopicmatch.so: $(BUILD)/kernels.o $(BUILD)/shard.o $(BUILD)/engine.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -o $@
 
 emqx_amd/libtmwork.so: emqx_amd/csrc/workload.c

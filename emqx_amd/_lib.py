@@ -44,6 +44,9 @@ SIGNATURES = [
     ("tm_last_error", ctypes.c_char_p, [ctypes.c_void_p]),
     ("tm_insert", ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint32]),
     ("tm_insert_batch", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32]),
+    ("tm_shard_of", ctypes.c_uint32, [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint32]),
+    ("tm_insert_batch_shard", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                             ctypes.c_uint32, ctypes.c_uint32]),
     ("tm_delete", ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint32]),
     ("tm_lookup", ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.POINTER(TmNodeInfo)]),
     ("tm_commit", ctypes.c_int, [ctypes.c_void_p, c_u64p]),
@@ -59,6 +62,14 @@ SIGNATURES = [
                                              ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]),
     ("tm_set_option", ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int64]),
     ("tm_set_stats", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    ("tm_match_batch_device_keys", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                                   ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                   ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                                   ctypes.c_void_p]),
+    ("tm_shard_merge", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p,
+                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                      ctypes.c_void_p]),
     ("tm_last_stats", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(TmBatchStats)]),
     ("tm_set_timing", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     ("tm_last_kernel_times", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_char_p),

@@ -178,7 +178,7 @@ struct tm_engine {
     size_t created_since_layout = 0;  // nodes created since the last relayout
 
     // ---- match workspace ----
-    DevBuf w_twords, w_bytes, w_off, w_words, w_meta, w_counts, w_outoff, w_ids, w_scan, w_total, w_path, w_stats, w_stage,
+    DevBuf w_kstage, w_mpre, w_mscan, w_twords, w_bytes, w_off, w_words, w_meta, w_counts, w_outoff, w_ids, w_scan, w_total, w_path, w_stats, w_stage,
         w_ws;
     uint32_t stage_k = 512;   // TM_STAGE_K: ids staged per topic before a re-walk (rows are
                               // written sparsely: HBM footprint, not traffic)
@@ -747,8 +747,10 @@ struct tm_engine {
     // the whole hot path of one batch, stream-ordered on st: CSR of ordered
     // filter ids (ids past cap are dropped; *total always exact)
     void run_batch(const uint8_t* bytes, const uint64_t* off, uint32_t n, uint64_t nbytes, uint32_t* counts,
-                   uint64_t* out_off, uint32_t* ids, uint64_t cap, uint64_t* total, hipStream_t st) {
+                   uint64_t* out_off, uint32_t* ids, uint64_t cap, uint64_t* total, hipStream_t st,
+                   uint64_t* keys = nullptr) {
         ensure_workspace(n, nbytes);
+        if (keys) w_kstage.ensure(((size_t)n * stage_k + 4) * 8);
         ImageView im = view();
         unsigned long long* sp = w_stats.as<unsigned long long>();
         if (stats_enabled) HIPCHK(hipMemsetAsync(w_stats.p, 0, STATS_BYTES, st));
@@ -766,9 +768,10 @@ struct tm_engine {
         qb.meta = w_meta.as<uint32_t>();
         qb.path = w_path.as<uint32_t>();
         qb.stage = w_stage.as<uint32_t>();
+        qb.kstage = keys ? w_kstage.as<uint64_t>() : nullptr;
         qb.scan_tmp = w_scan.as<uint64_t>();
         qb.ws = w_ws.as<unsigned long long>();
-        HIPCHK(launch_queue(stats_enabled, xcdq != 0, im, bytes, off, n, qb, stage_k, counts, out_off, ids, cap,
+        HIPCHK(launch_queue(stats_enabled, xcdq != 0, im, bytes, off, n, qb, stage_k, counts, out_off, ids, keys, cap,
                             total, sp, st, timing_enabled ? marks : nullptr, walk_bpc, hist_enabled != 0));
         if (timing_enabled)
             for (int i = 0; i < 4; ++i) ev_pending.push_back(ev_cur[i]);
@@ -932,6 +935,32 @@ int tm_insert_batch(tm_engine* e, const uint8_t* bytes, const uint64_t* off, uin
     });
 }
 
+uint32_t tm_shard_of(const uint8_t* filter, uint32_t len, uint32_t n_shards) {
+    if (n_shards <= 1 || (!filter && len)) return 0;
+    // the root level decides (filters under one literal root share a shard);
+    // root '+' / '#' filters are spread over all shards by their whole bytes
+    uint32_t root = 0;
+    while (root < len && filter[root] != '/') ++root;
+    const bool wild = root == 1 && (filter[0] == '+' || filter[0] == '#');
+    const uint32_t hl = wild ? len : root;
+    uint64_t h = 0xcbf29ce484222325ULL;   // FNV-1a 64
+    for (uint32_t i = 0; i < hl; ++i) h = (h ^ filter[i]) * 0x100000001b3ULL;
+    return (uint32_t)(fmix64(h) % n_shards);
+}
+
+int tm_insert_batch_shard(tm_engine* e, const uint8_t* bytes, const uint64_t* off, uint32_t n, uint32_t n_shards,
+                          uint32_t shard) {
+    if ((n && (!bytes || !off)) || n_shards == 0 || shard >= n_shards) return TM_EINVAL;
+    return guarded(e, [&] {
+        for (uint32_t i = 0; i < n; ++i) {
+            if (off[i + 1] < off[i] || off[i + 1] - off[i] > 0xFFFFFFFFull) throw ArgError("bad offsets");
+            const uint32_t len = (uint32_t)(off[i + 1] - off[i]);
+            if (tm_shard_of(bytes + off[i], len, n_shards) == shard) e->insert(bytes + off[i], len);
+        }
+        return TM_OK;
+    });
+}
+
 int tm_delete(tm_engine* e, const uint8_t* filter, uint32_t len) {
     if (!filter && len) return TM_EINVAL;
     return guarded(e, [&] {
@@ -1037,9 +1066,49 @@ int tm_match_batch(tm_engine* e, const uint8_t* topic_bytes, const uint64_t* top
     });
 }
 
+static int match_device(tm_engine* e, const uint8_t* d_bytes, const uint64_t* d_off, uint32_t n,
+                        uint64_t topic_bytes, uint32_t* d_count, uint64_t* d_out_off, uint32_t* d_ids,
+                        uint64_t* d_keys, uint64_t out_cap, uint64_t* d_total, void* hip_stream);
+
 int tm_match_batch_device(tm_engine* e, const uint8_t* d_bytes, const uint64_t* d_off, uint32_t n,
                           uint64_t topic_bytes, uint32_t* d_count, uint64_t* d_out_off, uint32_t* d_ids,
                           uint64_t out_cap, uint64_t* d_total, void* hip_stream) {
+    return match_device(e, d_bytes, d_off, n, topic_bytes, d_count, d_out_off, d_ids, nullptr, out_cap, d_total,
+                        hip_stream);
+}
+
+int tm_match_batch_device_keys(tm_engine* e, const uint8_t* d_bytes, const uint64_t* d_off, uint32_t n,
+                               uint64_t topic_bytes, uint32_t* d_count, uint64_t* d_out_off, uint32_t* d_ids,
+                               uint64_t* d_keys, uint64_t out_cap, uint64_t* d_total, void* hip_stream) {
+    if (out_cap && !d_keys) return TM_EINVAL;
+    return match_device(e, d_bytes, d_off, n, topic_bytes, d_count, d_out_off, d_ids, d_keys, out_cap, d_total,
+                        hip_stream);
+}
+
+int tm_shard_merge(tm_engine* e, uint32_t n_shards, uint32_t m, const uint32_t* d_counts,
+                   const uint64_t* d_src_base, const uint32_t* d_ids, const uint64_t* d_keys, uint32_t* d_out_count,
+                   uint64_t* d_out_off, uint32_t* d_out_gid, uint64_t out_cap, uint64_t* d_total, void* hip_stream) {
+    if (n_shards == 0 || n_shards > MAX_SHARDS || !d_out_off || !d_total) return TM_EINVAL;
+    if (m && (!d_counts || !d_src_base || !d_out_count)) return TM_EINVAL;
+    if (out_cap && (!d_ids || !d_keys || !d_out_gid)) return TM_EINVAL;
+    return guarded(e, [&]() -> int {
+        if (e->device < 0) {
+            e->last_error = "engine is host-only (device = -1): the merge runs on the GPU only";
+            return TM_EDEVICE;
+        }
+        tm_engine::Guard g(e->device);
+        hipStream_t st = hip_stream ? (hipStream_t)hip_stream : e->stream;
+        e->w_mpre.ensure(((size_t)n_shards * (m + 1) + 1) * 8);
+        e->w_mscan.ensure(scan_tmp_elems(m) * 8 + 8);
+        HIPCHK(launch_shard_merge(n_shards, m, d_counts, d_src_base, d_ids, d_keys, d_out_count, d_out_off, d_out_gid,
+                                  out_cap, d_total, e->w_mpre.as<uint64_t>(), e->w_mscan.as<uint64_t>(), st));
+        return TM_OK;
+    });
+}
+
+static int match_device(tm_engine* e, const uint8_t* d_bytes, const uint64_t* d_off, uint32_t n,
+                        uint64_t topic_bytes, uint32_t* d_count, uint64_t* d_out_off, uint32_t* d_ids,
+                        uint64_t* d_keys, uint64_t out_cap, uint64_t* d_total, void* hip_stream) {
     if (!d_off || !d_out_off || !d_total || (n && !d_count) || (out_cap && !d_ids)) return TM_EINVAL;
     return guarded(e, [&]() -> int {
         if (e->device < 0) {
@@ -1054,7 +1123,7 @@ int tm_match_batch_device(tm_engine* e, const uint8_t* d_bytes, const uint64_t* 
             HIPCHK(hipMemsetAsync(d_total, 0, 8, st));
             return TM_OK;
         }
-        e->run_batch(d_bytes, d_off, n, topic_bytes, d_count, d_out_off, d_ids, out_cap, d_total, st);
+        e->run_batch(d_bytes, d_off, n, topic_bytes, d_count, d_out_off, d_ids, out_cap, d_total, st, d_keys);
         e->finish_batch(st, n);
         if (e->stats_enabled) {
             HIPCHK(hipStreamSynchronize(st));

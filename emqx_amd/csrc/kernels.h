@@ -19,6 +19,7 @@ struct QueueBufs {
     uint32_t* meta;       // n: levels | long << 30 | dollar << 31
     uint32_t* path;       // global path of long topics, at (byte offset + 2 x topic index)
     uint32_t* stage;      // n x K: first K ids of each topic (written from the row's end)
+    uint64_t* kstage;     // n x K order keys (sharded mode), or null
     uint64_t* scan_tmp;   // scan_tmp_elems(n)
     unsigned long long* ws;   // QWS_BYTES of queue heads
 };
@@ -27,10 +28,26 @@ struct QueueBufs {
 // [2i] before / [2i+1] after stage i, or null.  out_cap == 0: counts and
 // offsets only.  stats (6 x u64, zeroed by the caller) is filled when
 // stats_mode: levels, visits, edge reads, matches, leaf visits, probe loads.
+// qb.kstage != null: sharded mode, the order key of every id goes to out_keys
 hipError_t launch_queue(bool stats_mode, bool xcdq, const ImageView& im, const uint8_t* bytes, const uint64_t* off,
                         uint32_t n, const QueueBufs& qb, uint32_t K, uint32_t* counts, uint64_t* out_off,
-                        uint32_t* out, uint64_t out_cap, uint64_t* total, unsigned long long* stats,
-                        hipStream_t st, hipEvent_t* marks, uint32_t walk_blocks_per_cu = 0, bool hist = false);
+                        uint32_t* out, uint64_t* out_keys, uint64_t out_cap, uint64_t* total,
+                        unsigned long long* stats, hipStream_t st, hipEvent_t* marks, uint32_t walk_blocks_per_cu = 0,
+                        bool hist = false);
 size_t scan_tmp_elems(uint32_t n);
+// exclusive scan of n u32 counts -> out_off[n+1] (u64), *total (tmp: scan_tmp_elems(n))
+hipError_t launch_scan(const uint32_t* counts, uint32_t n, uint64_t* out_off, uint64_t* total, uint64_t* tmp,
+                       hipStream_t st);
+
+// Sharded mode (shard.hip): merge per-topic match lists of S filter shards
+// for m topics.  counts [S][m]; source s's items start at src_base[s] of
+// ids / keys and are CSR-ordered by topic, each list in descending key order.
+// Output: counts[m], offsets[m+1], global ids (local * S + s) in descending
+// key order = emqx_trie:match/1 order.  pre: S*(m+1) u64, tmp: scan_tmp_elems(m).
+constexpr uint32_t MAX_SHARDS = 8;
+hipError_t launch_shard_merge(uint32_t S, uint32_t m, const uint32_t* counts, const uint64_t* src_base,
+                              const uint32_t* ids, const uint64_t* keys, uint32_t* out_count, uint64_t* out_off,
+                              uint32_t* out_gid, uint64_t out_cap, uint64_t* total, uint64_t* pre, uint64_t* tmp,
+                              hipStream_t st);
 
 }  // namespace tmx

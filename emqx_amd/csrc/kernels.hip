@@ -220,7 +220,23 @@ constexpr int HIST_OFF = 8;   // hist = stats + HIST_OFF
 
 struct Cursor {
     uint32_t v, r, n, r0;   // node to visit next and its level; topic levels; start level
+    uint64_t key;           // KEYS: fold branches taken above level r (rank_sym)
 };
+
+// Order keys (sharded mode).  Every match of a topic is identified by the
+// branches the reference's fold took to discover it: at level i 'match_#'
+// (0), the topic word's edge (1) or the '+' edge (2), and for a node's own
+// filter at the last level n an end mark (1).  Discovery order is ascending
+// lexicographic order of these sequences (emqx_trie.erl:127-145; SURVEY
+// Appendix A.3), so packing them 2 bits per level from the top of a u64
+// makes a key whose DESCENDING order is the reference's output order, and
+// per-shard lists merge by key.  Levels >= 32 do not fit (keys saturate).
+__device__ __forceinline__ uint64_t rank_sym(uint32_t level, uint64_t s) {
+    return level < 32 ? s << (62 - 2 * level) : 0ull;
+}
+__device__ __forceinline__ uint64_t rank_prefix(uint64_t key, uint32_t level) {   // symbols of levels < level
+    return level == 0 ? 0ull : level >= 32 ? key : key & (~0ull << (64 - 2 * level));
+}
 
 // topic words in VGPRs (n <= WREG): dynamic index by AND-masks (a select
 // chain or tree over the array gets turned back into a private-memory array
@@ -257,11 +273,13 @@ template <class Words>
 __device__ __forceinline__ bool walk_begin(const ImageView& im, Cursor& c, uint32_t n, bool dollar, const Words& W,
                                            WalkStats& st) {
     c.n = n;
+    c.key = 0;
     if (!dollar) {
         c.v = ROOT;
         c.r = c.r0 = 0;
         return true;
     }
+    c.key = rank_sym(0, 1);
     const uint4 q = load_half(im, ROOT, false);
     c.v = lit_child<false>(im, ROOT, q.x, q.z, q.w, W(0), st.probe_loads).child;
     c.r = c.r0 = 1;
@@ -272,10 +290,11 @@ __device__ __forceinline__ bool walk_begin(const ImageView& im, Cursor& c, uint3
 // half; a literal child found through the edge table arrives with its record
 // (EdgeSlot), so it is visited in the same step, and so on down a chain of
 // table children, until a child needs its own load or the walk pops.
-template <bool STATS, class Path, class Words, class Emit>
+template <bool STATS, bool KEYS, class Path, class Words, class Emit>
 __device__ __forceinline__ bool walk_step(const ImageView& im, Cursor& c, Path path, const Words& W, Emit& emit,
                                           WalkStats& st) {
     uint32_t v = c.v, r = c.r;
+    uint64_t key = KEYS ? c.key : 0ull;
     bool leaf = r == c.n;
     const uint4 h = load_half(im, v, leaf);   // inner {plus, hf, lw, lc} / leaf {sf, hf, hash, pad}
     uint32_t plus = h.x, hf = h.y, lw = h.z, lc = h.w, sf = h.x;
@@ -285,9 +304,9 @@ __device__ __forceinline__ bool walk_step(const ImageView& im, Cursor& c, Path p
             st.edge_reads += leaf ? 1 : 3;   // 'match_#' (:141) + fold over [W, '+'] (:132)
             st.leaf_visits += leaf ? 1 : 0;
         }
-        if (hf != FILTER_NONE) emit(hf);     // 'match_#': the '#' filter
+        if (hf != FILTER_NONE) emit(hf, key);   // 'match_#': the '#' filter
         if (leaf) {
-            if (sf != FILTER_NONE) emit(sf);   // the node's own filter (mnesia:read of the node, :128)
+            if (sf != FILTER_NONE) emit(sf, KEYS ? key | rank_sym(r, 1) : 0ull);   // the node's own filter (:128)
             break;
         }
         const uint64_t pl0 = st.probe_loads;
@@ -302,10 +321,12 @@ __device__ __forceinline__ bool walk_step(const ImageView& im, Cursor& c, Path p
         if (g.child != NODE_NONE) {   // literal subtree first, '+' child pending at level r
             path(r) = pc;
             v = g.child;
+            if (KEYS) key |= rank_sym(r, 1);
             ++r;
             if (!g.have) {
                 c.v = v;
                 c.r = r;
+                if (KEYS) c.key = key;
                 return false;
             }
             plus = g.plus;
@@ -320,6 +341,7 @@ __device__ __forceinline__ bool walk_step(const ImageView& im, Cursor& c, Path p
             path(r) = NODE_NONE;
             c.v = pc;
             c.r = r + 1;
+            if (KEYS) c.key = key | rank_sym(r, 2);
             return false;
         }
         break;
@@ -331,28 +353,33 @@ __device__ __forceinline__ bool walk_step(const ImageView& im, Cursor& c, Path p
             path(k) = NODE_NONE;
             c.v = p;
             c.r = k + 1;
+            if (KEYS) c.key = rank_prefix(key, k) | rank_sym(k, 2);
             return false;
         }
     }
     return true;
 }
 
-template <bool STATS, class Path, class Words, class Emit>
+template <bool STATS, bool KEYS, class Path, class Words, class Emit>
 __device__ __forceinline__ void walk(const ImageView& im, uint32_t n, bool dollar, Path path, const Words& W,
                                      Emit& emit, WalkStats& st) {
     Cursor c;
     if (!walk_begin(im, c, n, dollar, W, st)) return;
-    while (!walk_step<STATS>(im, c, path, W, emit, st)) {
+    while (!walk_step<STATS, KEYS>(im, c, path, W, emit, st)) {
     }
 }
 
 // discovery k of a topic goes to stage row slot K-1-k (k < K), 4 ids per
-// 16 B store; the row's last `count` slots are then the output in order
+// 16 B store; the row's last `count` slots are then the output in order.
+// KEYS: its order key to the same slot of the topic's key row.
+template <bool KEYS>
 struct RowEmit {
     uint32_t* row;
+    uint64_t* krow;
     uint32_t K, cnt;
     uint4 buf;
-    __device__ __forceinline__ void operator()(uint32_t f) {
+    __device__ __forceinline__ void operator()(uint32_t f, uint64_t key) {
+        if (KEYS && cnt < K) krow[K - 1 - cnt] = key;
         if (cnt < K) {
             const uint32_t s = cnt & 3u;
             buf.w = s == 0 ? f : buf.w;
@@ -368,15 +395,20 @@ struct RowEmit {
     }
 };
 // re-walk of a topic with total > K ids: discovery k >= K goes to output
-// position total-1-k
+// position total-1-k (KEYS: with its key)
+template <bool KEYS>
 struct TailEmit {
     uint32_t* out;
+    uint64_t* kout;
     uint64_t base, cap;
     uint32_t K, total, cnt;
-    __device__ __forceinline__ void operator()(uint32_t f) {
+    __device__ __forceinline__ void operator()(uint32_t f, uint64_t key) {
         if (cnt >= K && cnt < total) {
             const uint64_t p = base + (total - 1 - cnt);
-            if (p < cap) out[p] = f;
+            if (p < cap) {
+                out[p] = f;
+                if (KEYS) kout[p] = key;
+            }
         }
         ++cnt;
     }
@@ -414,11 +446,11 @@ constexpr uint32_t QCHUNK = 64;
 constexpr uint32_t QRANGES = 8;
 constexpr uint32_t NO_TOPIC = 0xFFFFFFFFu;
 
-template <bool STATS, bool XCDQ>
+template <bool STATS, bool XCDQ, bool KEYS>
 __global__ void __launch_bounds__(BLOCK)
 tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const uint32_t* __restrict__ twords,
               const uint32_t* __restrict__ words, const uint32_t* __restrict__ meta, uint32_t* __restrict__ gpath,
-              uint32_t* __restrict__ stage, uint32_t K, uint32_t* __restrict__ counts,
+              uint32_t* __restrict__ stage, uint64_t* __restrict__ kstage, uint32_t K, uint32_t* __restrict__ counts,
               unsigned long long* __restrict__ ws, unsigned long long* __restrict__ stats,
               unsigned long long* __restrict__ hist) {
     __shared__ uint32_t lds_path[WREG * BLOCK];
@@ -434,7 +466,7 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
     uint32_t my = NO_TOPIC;
     bool is_long = false, drained = false;
     Cursor cur;
-    RowEmit em{nullptr, K, 0, make_uint4(0, 0, 0, 0)};
+    RowEmit<KEYS> em{nullptr, nullptr, K, 0, make_uint4(0, 0, 0, 0)};
     WalkStats st;
     if (STATS) st.hist = hist;
     uint64_t lev_sum = 0, match_sum = 0;
@@ -492,6 +524,7 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
                     lev_sum += nl;
                     is_long = (mt & MLONG) != 0;
                     em.row = stage + (uint64_t)i * K;
+                    if (KEYS) em.krow = kstage + (uint64_t)i * K;
                     em.cnt = 0;
                     const uint32_t* tw = twords + (uint64_t)i * WREG;
                     bool go;
@@ -532,8 +565,8 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
         }
         if (__all(my == NO_TOPIC && drained)) break;
         if (my == NO_TOPIC) continue;
-        const bool fin = is_long ? walk_step<STATS>(im, cur, gp, mw, em, st)
-                                 : walk_step<STATS>(im, cur, lp, rw, em, st);
+        const bool fin = is_long ? walk_step<STATS, KEYS>(im, cur, gp, mw, em, st)
+                                 : walk_step<STATS, KEYS>(im, cur, lp, rw, em, st);
         if (fin) {
             em.flush();
             counts[my] = em.cnt;
@@ -548,11 +581,13 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
 // stage rows with coalesced writes (output index -> topic by binary search of
 // the block's inclusive prefix); output j of a topic with c ids is row slot
 // K-c+j; a topic with c > K re-walks and writes its first c-K outputs.
+template <bool KEYS>
 __global__ void __launch_bounds__(BLOCK)
 tm_copy_out(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const uint32_t* __restrict__ twords,
             const uint32_t* __restrict__ words, const uint32_t* __restrict__ meta, uint32_t* __restrict__ gpath,
-            const uint32_t* __restrict__ stage, uint32_t K, const uint32_t* __restrict__ counts,
-            const uint64_t* __restrict__ out_off, uint32_t* __restrict__ out, uint64_t out_cap) {
+            const uint32_t* __restrict__ stage, const uint64_t* __restrict__ kstage, uint32_t K,
+            const uint32_t* __restrict__ counts, const uint64_t* __restrict__ out_off, uint32_t* __restrict__ out,
+            uint64_t* __restrict__ kout, uint64_t out_cap) {
     __shared__ uint32_t lds_path[WREG * BLOCK];
     __shared__ uint32_t lds_inc[BLOCK];
     __shared__ uint64_t lds_scan[BLOCK / 64];
@@ -574,19 +609,22 @@ tm_copy_out(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const ui
         const uint32_t k = (uint32_t)(j - prev);
         const uint32_t ct = lds_inc[lo] - prev;
         const int64_t slot = (int64_t)K - (int64_t)ct + (int64_t)k;
-        if (slot >= 0 && base + j < out_cap) out[base + j] = stage[(uint64_t)(t0 + lo) * K + (uint64_t)slot];
+        if (slot >= 0 && base + j < out_cap) {
+            out[base + j] = stage[(uint64_t)(t0 + lo) * K + (uint64_t)slot];
+            if (KEYS) kout[base + j] = kstage[(uint64_t)(t0 + lo) * K + (uint64_t)slot];
+        }
     }
     if (threadIdx.x < tn && c > K) {   // fan-out beyond the stage row: walk again, write the head
         const uint32_t t = t0 + threadIdx.x;
         const uint32_t mt = meta[t];
         const uint64_t b = off[t] - off[0];
         const MemWords mw{twords + (uint64_t)t * WREG, words + b + t};
-        TailEmit em{out, base + ex, out_cap, K, c, 0};
+        TailEmit<KEYS> em{out, kout, base + ex, out_cap, K, c, 0};
         WalkStats s2;
         if (mt & MLONG)
-            walk<false>(im, mt & MN, (mt & MDOLLAR) != 0, GlobalPath{gpath + b + 2ull * t}, mw, em, s2);
+            walk<false, KEYS>(im, mt & MN, (mt & MDOLLAR) != 0, GlobalPath{gpath + b + 2ull * t}, mw, em, s2);
         else
-            walk<false>(im, mt & MN, (mt & MDOLLAR) != 0, LdsPath{lds_path + threadIdx.x}, mw, em, s2);
+            walk<false, KEYS>(im, mt & MN, (mt & MDOLLAR) != 0, LdsPath{lds_path + threadIdx.x}, mw, em, s2);
     }
 }
 
@@ -668,8 +706,8 @@ static uint32_t resident_grid(Kern k, uint32_t n_tiles, uint32_t cap_per_cu = 0)
 
 size_t scan_tmp_elems(uint32_t n) { return div_up(n ? n : 1, SCAN_TILE); }
 
-static hipError_t launch_scan(const uint32_t* counts, uint32_t n, uint64_t* out_off, uint64_t* total,
-                              uint64_t* tmp, hipStream_t st) {
+hipError_t launch_scan(const uint32_t* counts, uint32_t n, uint64_t* out_off, uint64_t* total, uint64_t* tmp,
+                       hipStream_t st) {
     uint32_t tiles = div_up(n, SCAN_TILE);
     hipLaunchKernelGGL(tm_scan_reduce, dim3(tiles), dim3(BLOCK), 0, st, counts, n, tmp);
     hipLaunchKernelGGL(tm_scan_tiles, dim3(1), dim3(BLOCK), 0, st, tmp, tiles);
@@ -679,8 +717,9 @@ static hipError_t launch_scan(const uint32_t* counts, uint32_t n, uint64_t* out_
 
 hipError_t launch_queue(bool stats_mode, bool xcdq, const ImageView& im, const uint8_t* bytes, const uint64_t* off,
                         uint32_t n, const QueueBufs& qb, uint32_t K, uint32_t* counts, uint64_t* out_off,
-                        uint32_t* out, uint64_t out_cap, uint64_t* total, unsigned long long* stats,
-                        hipStream_t st, hipEvent_t* marks, uint32_t walk_blocks_per_cu, bool hist) {
+                        uint32_t* out, uint64_t* out_keys, uint64_t out_cap, uint64_t* total,
+                        unsigned long long* stats, hipStream_t st, hipEvent_t* marks, uint32_t walk_blocks_per_cu,
+                        bool hist) {
     auto mark = [&](int i) {
         if (marks) (void)hipEventRecord(marks[i], st);
     };
@@ -698,14 +737,17 @@ hipError_t launch_queue(bool stats_mode, bool xcdq, const ImageView& im, const u
     hipLaunchKernelGGL(tm_tokenize, g, blk, 0, st, im, bytes, off, n, qb.twords, qb.words, qb.meta);
     mark(1);
     mark(2);
-    const uint32_t wg = resident_grid(tm_walk_queue<false, false>, div_up(n, 64), walk_blocks_per_cu);
-#define TM_Q(S, X)                                                                                              \
-    hipLaunchKernelGGL((tm_walk_queue<S, X>), dim3(wg), blk, 0, st, im, off, n, qb.twords, qb.words, qb.meta, \
-                       qb.path, qb.stage, K, counts, qb.ws, stats, hist ? stats + HIST_OFF : nullptr)
-    if (stats_mode) {
-        if (xcdq) TM_Q(true, true); else TM_Q(true, false);
+    const bool keys = qb.kstage != nullptr;
+    const uint32_t wg = resident_grid(tm_walk_queue<false, false, false>, div_up(n, 64), walk_blocks_per_cu);
+#define TM_Q(S, X, Y)                                                                                              \
+    hipLaunchKernelGGL((tm_walk_queue<S, X, Y>), dim3(wg), blk, 0, st, im, off, n, qb.twords, qb.words, qb.meta, \
+                       qb.path, qb.stage, qb.kstage, K, counts, qb.ws, stats, hist ? stats + HIST_OFF : nullptr)
+    if (keys) {
+        if (stats_mode) TM_Q(true, true, true); else TM_Q(false, true, true);
+    } else if (stats_mode) {
+        if (xcdq) TM_Q(true, true, false); else TM_Q(true, false, false);
     } else {
-        if (xcdq) TM_Q(false, true); else TM_Q(false, false);
+        if (xcdq) TM_Q(false, true, false); else TM_Q(false, false, false);
     }
 #undef TM_Q
     mark(3);
@@ -714,9 +756,14 @@ hipError_t launch_queue(bool stats_mode, bool xcdq, const ImageView& im, const u
     if (err != hipSuccess) return err;
     mark(5);
     mark(6);
-    if (out_cap)
-        hipLaunchKernelGGL(tm_copy_out, g, blk, 0, st, im, off, n, qb.twords, qb.words, qb.meta, qb.path, qb.stage,
-                           K, counts, out_off, out, out_cap);
+    if (out_cap) {
+        if (keys)
+            hipLaunchKernelGGL(tm_copy_out<true>, g, blk, 0, st, im, off, n, qb.twords, qb.words, qb.meta, qb.path,
+                               qb.stage, qb.kstage, K, counts, out_off, out, out_keys, out_cap);
+        else
+            hipLaunchKernelGGL(tm_copy_out<false>, g, blk, 0, st, im, off, n, qb.twords, qb.words, qb.meta, qb.path,
+                               qb.stage, nullptr, K, counts, out_off, out, nullptr, out_cap);
+    }
     mark(7);
     return hipGetLastError();
 }

@@ -7,13 +7,11 @@ topic batches, so the data path needs NO collective (SURVEY.md §8(e),
 for the control plane around a measured region: a barrier, and the max of
 the per-rank step times.
 
-The sharded-filter mode of config C4 (filters partitioned by root word, match
-sets all-gathered over xGMI) is a next-round item; `root_shard` below is its
-partition function, kept here so the C-ABI and tests can already use it.
+The sharded-filter mode of config C4 (filters partitioned by root level,
+per-shard match lists exchanged over xGMI with RCCL) lives in shard.py.
 """
 import os
 import time
-import zlib
 
 
 def env_rank():
@@ -50,14 +48,3 @@ def timed_region(step, steps: int, sync, group=None):
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
         dt = float(t.item())
     return dt
-
-
-def root_shard(filt: bytes, shards: int) -> int:
-    """Shard of a filter in the sharded (C4) layout: filters whose root word
-    is literal go to hash(root) mod shards; root '+' / '#' filters are spread
-    by a hash of the whole filter (every shard then also walks its root
-    wildcard part for each topic: match(T, F) = U_s match(T, F_s))."""
-    root = filt.split(b"/", 1)[0]
-    if root in (b"+", b"#"):
-        return zlib.crc32(filt) % shards
-    return zlib.crc32(root) % shards

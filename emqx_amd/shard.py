@@ -1,0 +1,110 @@
+"""Sharded mode of the topic-routing engine.
+
+When the filter set is partitioned over S GPUs (one process per GPU), every
+GPU holds the sub-trie of its shard (`tm_shard_of`: by root level, so one
+literal root's subtree is on one shard; root '+' / '#' filters are spread by
+their bytes).  A publish batch is broadcast to all ranks; each rank walks the
+WHOLE batch against its sub-trie (match(T, F) = U_s match(T, F_s)) with order
+keys (`tm_match_batch_device_keys`), then the ranks exchange per-topic lists
+so that rank r ends up owning the complete, ordered match lists of topic slice
+r:
+
+    counts  all_to_all_single (slice d of my counts -> rank d)
+    sizes   all_to_all_single (how many ids I send to each rank)
+    ids     all_to_all_single, uneven splits (RCCL over xGMI on the GPUs)
+    keys    all_to_all_single, uneven splits
+    merge   tm_shard_merge on the GPU: S key-ordered lists per topic ->
+            one list in emqx_trie:match/1 order, global ids local*S + s
+
+An all-to-all moves each id once, to the rank that owns its topic; an
+all-gather would move every id to every rank (S x the bytes) only for each
+rank to keep 1/S of them.  Ids are global: gid = local_id * S + shard.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib as L
+from .engine import Engine
+
+
+def shard_of(filt: bytes, n_shards: int) -> int:
+    return L.load().tm_shard_of(filt, len(filt), n_shards)
+
+
+def slices(n: int, n_shards: int):
+    """topic slice boundaries: rank r owns topics [b[r], b[r+1])"""
+    return [(d * n) // n_shards for d in range(n_shards + 1)]
+
+
+def _p(x):
+    if x is None:
+        return None
+    return ctypes.c_void_p(x.data_ptr() if hasattr(x, "data_ptr") else int(x))
+
+
+class ShardEngine(Engine):
+    """The engine of shard `shard` of `n_shards` (one per GPU)."""
+
+    def __init__(self, device, n_shards, shard, filters_hint=0):
+        if not 1 <= n_shards <= 8 or not 0 <= shard < n_shards:
+            raise ValueError("n_shards must be 1..8 and shard < n_shards")
+        super().__init__(device=device, filters_hint=filters_hint)
+        self.n_shards, self.shard = n_shards, shard
+
+    def insert_many(self, buf, off):
+        """insert the filters of [off[i], off[i+1]) that belong to this shard"""
+        n = len(off) - 1
+        buf = np.ascontiguousarray(buf, dtype=np.uint8)
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        return self._check(self.lib.tm_insert_batch_shard(self.h, buf.ctypes.data, off.ctypes.data, n,
+                                                          self.n_shards, self.shard), "tm_insert_batch_shard")
+
+    def match_keys_device(self, d_bytes, d_off, n, topic_bytes, d_counts, d_offs, d_ids, d_keys, out_cap, d_total,
+                          stream=None):
+        st = None if stream is None else ctypes.c_void_p(stream if isinstance(stream, int) else stream.cuda_stream)
+        rc = self.lib.tm_match_batch_device_keys(self.h, _p(d_bytes), _p(d_off), n, topic_bytes, _p(d_counts),
+                                                 _p(d_offs), _p(d_ids), _p(d_keys), out_cap, _p(d_total), st)
+        return self._check(rc, "tm_match_batch_device_keys")
+
+    def merge_device(self, m, d_counts, d_src_base, d_ids, d_keys, d_out_count, d_out_off, d_out_gid, out_cap,
+                     d_total, stream=None):
+        st = None if stream is None else ctypes.c_void_p(stream if isinstance(stream, int) else stream.cuda_stream)
+        rc = self.lib.tm_shard_merge(self.h, self.n_shards, m, _p(d_counts), _p(d_src_base), _p(d_ids), _p(d_keys),
+                                     _p(d_out_count), _p(d_out_off), _p(d_out_gid), out_cap, _p(d_total), st)
+        return self._check(rc, "tm_shard_merge")
+
+
+def exchange(counts, offs, ids, keys, n, n_shards, rank, group=None):
+    """All-to-all of one rank's keyed lists (torch tensors on the rank's
+    device: counts int32[n], offs int64[n+1], ids int32[>= total], keys
+    int64[>= total]) so that every rank receives, from every shard, the lists
+    of its own topic slice.  Returns (recv_counts int32[S*m] source-major,
+    src_base int64[S], recv_ids int32, recv_keys int64, m)."""
+    import torch
+    import torch.distributed as dist
+    b = slices(n, n_shards)
+    m = b[rank + 1] - b[rank]
+    dev = counts.device
+    in_splits = [b[d + 1] - b[d] for d in range(n_shards)]
+    recv_counts = torch.empty(n_shards * m, dtype=torch.int32, device=dev)
+    dist.all_to_all_single(recv_counts, counts[:n].contiguous(), output_split_sizes=[m] * n_shards,
+                           input_split_sizes=in_splits, group=group)
+    cut = offs[torch.tensor(b, device=dev)].cpu().tolist()     # CSR cut points of the S slices
+    send_items = [int(cut[d + 1] - cut[d]) for d in range(n_shards)]
+    sizes = torch.tensor(send_items, dtype=torch.int64, device=dev)
+    recv_sizes = torch.empty(n_shards, dtype=torch.int64, device=dev)
+    dist.all_to_all_single(recv_sizes, sizes, group=group)
+    recv_items = [int(x) for x in recv_sizes.cpu().tolist()]
+    tot = sum(recv_items)
+    recv_ids = torch.empty(max(tot, 1), dtype=torch.int32, device=dev)
+    recv_keys = torch.empty(max(tot, 1), dtype=torch.int64, device=dev)
+    lo, hi = int(cut[0]), int(cut[-1])
+    dist.all_to_all_single(recv_ids[:tot], ids[lo:hi].contiguous(), output_split_sizes=recv_items,
+                           input_split_sizes=send_items, group=group)
+    dist.all_to_all_single(recv_keys[:tot], keys[lo:hi].contiguous(), output_split_sizes=recv_items,
+                           input_split_sizes=send_items, group=group)
+    base = np.zeros(n_shards, dtype=np.int64)
+    base[1:] = np.cumsum(recv_items)[:-1]
+    src_base = torch.from_numpy(base).to(dev)
+    return recv_counts, src_base, recv_ids, recv_keys, m

@@ -83,6 +83,15 @@ int tm_insert(tm_engine* e, const uint8_t* filter, uint32_t len);
  * the first failure and returns its code. */
 int tm_insert_batch(tm_engine* e, const uint8_t* bytes, const uint64_t* off, uint32_t n);
 
+/* Sharded mode: the shard (0..n_shards-1) that owns a filter — by its root
+ * level, so a literal root's whole subtree lives on one shard; filters whose
+ * root is '+' or '#' are spread over all shards by their bytes. */
+uint32_t tm_shard_of(const uint8_t* filter, uint32_t len, uint32_t n_shards);
+
+/* tm_insert_batch restricted to the filters tm_shard_of assigns to `shard`. */
+int tm_insert_batch_shard(tm_engine* e, const uint8_t* bytes, const uint64_t* off, uint32_t n,
+                          uint32_t n_shards, uint32_t shard);
+
 /* emqx_trie:delete/1 — src/emqx_trie.erl:88-96 (+ delete_path/1 :149-163).
  * Unknown filter = no-op (TM_OK). */
 int tm_delete(tm_engine* e, const uint8_t* filter, uint32_t len);
@@ -128,6 +137,30 @@ int tm_match_batch_device(tm_engine* e, const uint8_t* d_topic_bytes, const uint
                           uint32_t n, uint64_t topic_bytes, uint32_t* d_out_count,
                           uint64_t* d_out_off, uint32_t* d_out_filter_id, uint64_t out_cap,
                           uint64_t* d_total, void* hip_stream);
+
+/* Sharded mode (the filter set partitioned over GPUs, see
+ * emqx_amd/shard.py).  Same as tm_match_batch_device on this engine's shard,
+ * plus d_out_key[i]: the order key of id i (2 bits per level for the branch
+ * the reference's fold took — 'match_#' 0, topic word 1, '+' 2 — and an end
+ * mark 1 for a node's own filter, packed from the top of a u64).  Each
+ * topic's ids come in descending key order, which is emqx_trie:match/1's
+ * order (emqx_trie.erl:127-145), so shards' lists merge by key.  Keys cover
+ * topics of up to 31 levels. */
+int tm_match_batch_device_keys(tm_engine* e, const uint8_t* d_topic_bytes, const uint64_t* d_topic_off,
+                               uint32_t n, uint64_t topic_bytes, uint32_t* d_out_count,
+                               uint64_t* d_out_off, uint32_t* d_out_filter_id, uint64_t* d_out_key,
+                               uint64_t out_cap, uint64_t* d_total, void* hip_stream);
+
+/* Merge, on e's GPU, the keyed lists of n_shards (<= 8) shards for m topics
+ * (after the all-to-all exchange): d_counts [n_shards][m]; shard s's ids and
+ * keys start at d_src_base[s] (device u64 array) and are CSR-ordered by
+ * topic.  Output: per-topic counts, offsets[m+1] and global filter ids
+ * local_id * n_shards + s, in emqx_trie:match/1 order; *d_total is exact, ids
+ * past out_cap are dropped.  Stream-ordered. */
+int tm_shard_merge(tm_engine* e, uint32_t n_shards, uint32_t m, const uint32_t* d_counts,
+                   const uint64_t* d_src_base, const uint32_t* d_ids, const uint64_t* d_keys,
+                   uint32_t* d_out_count, uint64_t* d_out_off, uint32_t* d_out_gid, uint64_t out_cap,
+                   uint64_t* d_total, void* hip_stream);
 
 /* Engine knobs (the app-env analogue of SURVEY §5 config):
  *   "xcdq"     1 = per-XCD dequeue heads over contiguous ranges of the batch

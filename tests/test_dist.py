@@ -55,14 +55,3 @@ def test_two_rank_timed_region_and_streams():
     assert abs(dt0 - dt1) < 1e-9            # both ranks report the same max
     assert dt0 >= 3 * 0.04                  # the slower rank's time
     assert b0 != b1                         # independent topic streams
-
-
-def test_root_shard_partition():
-    sys.path.insert(0, ROOT)
-    from emqx_amd import multi
-    fs = [b"a/+", b"a/b/#", b"+/x", b"#", b"b/c", b"a", b"+/+/#"]
-    for s in (1, 2, 8):
-        shards = [multi.root_shard(f, s) for f in fs]
-        assert all(0 <= x < s for x in shards)
-        assert multi.root_shard(b"a/+", s) == multi.root_shard(b"a/b/#", s)   # same literal root
-    assert np.unique([multi.root_shard(b"+/%d" % i, 8) for i in range(200)]).size == 8

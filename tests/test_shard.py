@@ -1,0 +1,105 @@
+"""Sharded mode on CPU: the partition function, and two
+gloo ranks running the all-to-all exchange of keyed per-shard lists
+(emqx_amd/shard.py) with per-shard O1 results; the merged lists must equal
+O1 over the whole filter set, in order.  This also checks that descending
+order key = emqx_trie:match/1 order."""
+import os
+import socket
+import sys
+
+import numpy as np
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_shard_of_partition():
+    from emqx_amd import shard
+    fs = [b"a/+", b"a/b/#", b"+/x", b"#", b"b/c", b"a", b"+/+/#", b"$SYS/#", b"", b"/a"]
+    for s in (1, 2, 3, 8):
+        owners = [shard.shard_of(f, s) for f in fs]
+        assert all(0 <= x < s for x in owners)
+        assert shard.shard_of(b"a/+", s) == shard.shard_of(b"a/b/#", s) == shard.shard_of(b"a", s)
+    # root wildcards spread over every shard
+    assert np.unique([shard.shard_of(b"+/%d" % i, 8) for i in range(400)]).size == 8
+    assert np.unique([shard.shard_of(b"#", 8)]).size == 1
+
+
+def _workload():
+    from emqx_amd import workload as W
+    fb, fo = W.filters(1, n=6000)
+    tb, to = W.topics(1, n=3000)
+    return W.unpack(fb, fo), W.unpack(tb, to)
+
+
+def _worker(rank, world, port, q):
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import torch
+    import torch.distributed as dist
+    from emqx_amd import shard
+    from emqx_amd.engine import pack
+    from oracle import O1
+    from shard_ref import merge_host, order_key
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    filters, topics = _workload()
+    mine, seen = [], set()
+    for f in filters:
+        if shard.shard_of(f, world) == rank and f not in seen:
+            seen.add(f)
+            mine.append(f)                  # local id = insertion sequence
+    o1 = O1()
+    fb, fo = pack(mine)
+    o1.insert_many(fb, fo)
+    tb, to = pack(topics)
+    counts, offs, ids = o1.match_ids(tb, to)
+    levels = [t.count(b"/") + 1 for t in topics]
+    keys = np.zeros(max(len(ids), 1), dtype=np.uint64)
+    for t in range(len(topics)):
+        for j in range(int(offs[t]), int(offs[t + 1])):
+            keys[j] = order_key(mine[ids[j]], levels[t])
+    rc, base, rid, rk, m = shard.exchange(
+        torch.from_numpy(counts.astype(np.int32)), torch.from_numpy(offs.astype(np.int64)),
+        torch.from_numpy(ids.astype(np.int32)), torch.from_numpy(keys.view(np.int64)), len(topics), world, rank)
+    merged = merge_host(rc.numpy(), base.numpy(), rid.numpy(), rk.numpy(), m, world)
+    # gid -> (shard, local) -> bytes: gather every shard's filter list
+    lists = [None] * world
+    dist.all_gather_object(lists, mine)
+    out = [[lists[g % world][g // world] for g in row] for row in merged]
+    q.put((rank, out))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_exchange_and_merge_equals_o1():
+    from emqx_amd.engine import pack
+    from oracle import O1
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    filters, topics = _workload()
+    o1 = O1()
+    fb, fo = pack(filters)
+    o1.insert_many(fb, fo)
+    want = [o1.match(t) for t in topics]
+    got = res[0] + res[1]
+    assert len(got) == len(topics)
+    assert sum(len(r) for r in want) > 1000
+    assert got == want
