@@ -45,7 +45,10 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", type=int, default=3, help="SURVEY §8(d) config (3 = the metric's)")
     ap.add_argument("--filters", type=int, default=None, help="override filter count")
-    ap.add_argument("--topics", type=int, default=2_000_000, help="topics per GPU per step")
+    ap.add_argument("--topics", type=int, default=None,
+                    help="topics per GPU per step (replicated, default 2M) / per batch (sharded, default: config's)")
+    ap.add_argument("--mode", choices=["replicated", "sharded"], default=None,
+                    help="replicated trie per GPU (default) or filter shards per GPU (default for --config 4)")
     ap.add_argument("--cpu-sample", type=int, default=1_500_000, help="topics timed on the host (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=None)
     ap.add_argument("--check", type=int, default=20_000, help="topics checked bit-exactly vs the oracle")
@@ -70,6 +73,12 @@ def main():
         dist.init_process_group("nccl" if torch.cuda.is_available() else "gloo")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    if (a.mode or ("sharded" if a.config == 4 else "replicated")) == "sharded":
+        main_sharded(a, rank, world, local, dev)
+        if world > 1:
+            dist.destroy_process_group()
+        return
+    a.topics = a.topics or 2_000_000
 
     cfg = W.CONFIGS[a.config]
     n_filters = a.filters or cfg["filters"]
@@ -257,6 +266,150 @@ def main():
     eng.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def main_sharded(a, rank, world, local, dev):
+    """Config C4: the filter set partitioned over the ranks by
+    literal-prefix (one shard per GPU).  Every rank holds the same topic batch,
+    walks it against its own sub-trie with order keys, then the ranks
+    exchange per-topic keyed lists (all-to-all, RCCL over xGMI) and each
+    merges the lists of its topic slice into emqx_trie:match/1 order on its
+    GPU.  One step = walk + exchange + merge of one batch; `value` = batch
+    topics / max-over-ranks step time (strong scaling: the batch and filter
+    set are fixed, N GPUs share them)."""
+    from emqx_amd import shard
+    S = world
+    cfg = W.CONFIGS[a.config]
+    n_filters = a.filters or cfg["filters"]
+    t0 = time.time()
+    fb, fo = W.filters(a.config, n=n_filters)
+    log("rank %d: generated %d filters (%.1f MB) in %.1fs" % (rank, n_filters, fo[-1] / 1e6, time.time() - t0))
+    t0 = time.time()
+    eng = shard.ShardEngine(local, S, rank, filters_hint=n_filters // S + 1)
+    eng.set_option("stage_k", a.stage_k or (512 if S == 1 else 128))   # per-shard fan-out is ~1/S
+    eng.insert_many(fb, fo)
+    eng.commit()
+    log("rank %d: shard %d/%d built + committed in %.1fs: %d filters, %d nodes, image %.2f GB" % (
+        rank, rank, S, time.time() - t0, eng.filter_count, eng.node_count, eng.image_bytes / 1e9))
+
+    n_topics = a.topics if a.topics else cfg["topics"]
+    tb, to = W.topics(a.config, n=n_topics, stream=0)     # the same batch on every shard
+    n = len(to) - 1
+    nbytes = int(to[-1])
+    d_b = torch.from_numpy(tb).to(dev)
+    d_o = torch.from_numpy(to.view(np.int64)).to(dev)
+    d_c = torch.empty(n, dtype=torch.int32, device=dev)
+    d_oo = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    d_t = torch.zeros(1, dtype=torch.int64, device=dev)
+    st = torch.cuda.current_stream(dev)
+
+    eng.set_stats(True)
+    eng.match_keys_device(d_b, d_o, n, nbytes, d_c, d_oo, None, None, 0, d_t, stream=st)
+    torch.cuda.synchronize(dev)
+    stats = eng.last_stats()
+    eng.set_stats(False)
+    total = int(d_t.item())
+    cap = total + 1024
+    d_i = torch.empty(cap, dtype=torch.int32, device=dev)
+    d_k = torch.empty(cap, dtype=torch.int64, device=dev)
+    b = shard.slices(n, S)
+    m = b[rank + 1] - b[rank]
+    # merge output: sized after one exchange (the received total is exact)
+    merged = {}
+
+    def walk():
+        eng.match_keys_device(d_b, d_o, n, nbytes, d_c, d_oo, d_i, d_k, cap, d_t, stream=st)
+
+    def exchange():
+        return shard.exchange(d_c, d_oo, d_i, d_k, n, S, rank)
+
+    def merge(x):
+        rc, base, rid, rk, mm = x
+        if "cap" not in merged:
+            merged["cap"] = max(int(rid.numel()), 1) + 1024
+            merged["c"] = torch.empty(max(mm, 1), dtype=torch.int32, device=dev)
+            merged["o"] = torch.empty(mm + 1, dtype=torch.int64, device=dev)
+            merged["g"] = torch.empty(merged["cap"], dtype=torch.int32, device=dev)
+            merged["t"] = torch.zeros(1, dtype=torch.int64, device=dev)
+        eng.merge_device(mm, rc, base, rid, rk, merged["c"], merged["o"], merged["g"], merged["cap"], merged["t"],
+                         stream=st)
+
+    def step():
+        walk()
+        merge(exchange())
+
+    for _ in range(max(a.warmup, 1)):
+        step()
+    torch.cuda.synchronize(dev)
+    eng.set_timing(True)
+    dt = multi.timed_region(step, a.steps, lambda: torch.cuda.synchronize(dev))
+    kms = eng.last_kernel_times()
+    eng.set_timing(False)
+    assert int(d_t.item()) == total, "match total changed between steps"
+    mtotal = int(merged["t"].item())
+
+    # phase breakdown (untimed extra loops): walk / exchange / merge
+    def phase(fn, k=3):
+        multi.timed_region(lambda: None, 1, lambda: torch.cuda.synchronize(dev))
+        t1 = time.perf_counter()
+        for _ in range(k):
+            fn()
+        torch.cuda.synchronize(dev)
+        return (time.perf_counter() - t1) / k * 1e3
+    x = exchange()
+    phases = {"walk_ms": phase(walk), "exchange_ms": phase(exchange), "merge_ms": phase(lambda: merge(x))}
+
+    check_ok = None
+    if rank == 0 and a.check > 0 and n_filters <= 20_000_000:
+        from oracle import O1   # checker only
+        threads = a.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count())
+        o1 = O1(n_filters)
+        o1.insert_many(fb, fo)
+        k = min(a.check, m)
+        oc, oo, oi = o1.match_ids(tb, to[: k + 1], threads=threads)
+        g2i = shard.gid_to_index(shard.shard_of_batch(fb, fo, S), S)
+        mo = merged["o"][: k + 1].cpu().numpy().view(np.uint64)
+        mg = merged["g"][: int(mo[-1])].cpu().numpy().view(np.uint32).astype(np.int64)
+        check_ok = bool(np.array_equal(mo, oo) and np.array_equal(g2i[mg], oi.astype(np.int64)))
+        log("bit-exact check of %d topics (rank 0 slice) vs O1: %s" % (k, check_ok))
+
+    levels = stats["levels"]
+    B = 8 * levels + 16 * stats["edge_reads"] + 4 * stats["matches"]
+    walk_ms = kms.get("walk", 0.0)
+    achieved = B / (walk_ms * 1e-3) / 1e9 if walk_ms > 0 else None
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": n * a.steps / dt,
+            "unit": "topics/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": dt / a.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic",
+            "config": {"workload": "C%d: %d distinct wildcard filters sharded by literal-prefix over %d GPU(s), "
+                                   "%d-level topics, one %d-topic batch per step" % (
+                                       a.config, n_filters, S, cfg["levels"], n),
+                       "filters": n_filters, "topics_per_step": n, "levels": cfg["levels"],
+                       "parallelism": "filter shards x %d, all-to-all of keyed match lists (RCCL), device merge"
+                                      % S},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": None,
+                         "kernel": "tm_walk_queue<KEYS> on rank 0's shard", "kernel_ms": walk_ms,
+                         "algorithmic_bytes_per_launch": B},
+            "cpu_baseline": None,
+            "kernel_ms": kms,
+            "phases_ms_rank0": phases,
+            "shard0": {"filters": eng.filter_count, "nodes": eng.node_count, "image_gb": eng.image_bytes / 1e9,
+                       "ids_walked": total, "ids_merged": mtotal},
+            "parity_check": check_ok,
+        }
+        print(json.dumps(out), flush=True)
+    eng.close()
 
 
 if __name__ == "__main__":

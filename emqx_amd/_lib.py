@@ -45,7 +45,9 @@ SIGNATURES = [
     ("tm_insert", ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint32]),
     ("tm_insert_batch", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32]),
     ("tm_shard_of", ctypes.c_uint32, [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint32]),
-    ("tm_insert_batch_shard", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+    ("tm_shard_of_batch", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
+                                         ctypes.c_void_p]),
+    ("tm_insert_batch_shard",ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
                                              ctypes.c_uint32, ctypes.c_uint32]),
     ("tm_delete", ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint32]),
     ("tm_lookup", ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.POINTER(TmNodeInfo)]),

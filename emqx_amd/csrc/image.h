@@ -92,7 +92,9 @@ struct alignas(16) DictSlot {
 
 // device-side view of one committed image (plain pointers into HBM)
 struct ImageView {
-    const Node*     nodes;
+    const uint8_t*  inner;             // inner half of node v at inner + (v << node_shift)
+    const uint8_t*  leaf;              // leaf half of node v at leaf + (v << node_shift)
+    uint32_t        node_shift;        // 5: interleaved 32 B records; 4: split arrays of 16 B halves
     const EdgeSlot* edges;
     uint64_t        edge_slot_mask;    // slots - 1 (power of two)
     const DictSlot* dict;

@@ -35,6 +35,8 @@ hipError_t launch_queue(bool stats_mode, bool xcdq, const ImageView& im, const u
                         unsigned long long* stats, hipStream_t st, hipEvent_t* marks, uint32_t walk_blocks_per_cu = 0,
                         bool hist = false);
 size_t scan_tmp_elems(uint32_t n);
+// split image (option "split"): n 32 B node records -> inner[n], leaf[n] 16 B halves
+hipError_t launch_split_nodes(const void* nodes, uint64_t n, void* inner, void* leaf, hipStream_t st);
 // exclusive scan of n u32 counts -> out_off[n+1] (u64), *total (tmp: scan_tmp_elems(n))
 hipError_t launch_scan(const uint32_t* counts, uint32_t n, uint64_t* out_off, uint64_t* total, uint64_t* tmp,
                        hipStream_t st);
@@ -43,7 +45,7 @@ hipError_t launch_scan(const uint32_t* counts, uint32_t n, uint64_t* out_off, ui
 // for m topics.  counts [S][m]; source s's items start at src_base[s] of
 // ids / keys and are CSR-ordered by topic, each list in descending key order.
 // Output: counts[m], offsets[m+1], global ids (local * S + s) in descending
-// key order = emqx_trie:match/1 order.  pre: S*(m+1) u64, tmp: scan_tmp_elems(m).
+// key order = emqx_trie:match/1 order.  pre: S*m+1 u64, tmp: scan_tmp_elems(S*m).
 constexpr uint32_t MAX_SHARDS = 8;
 hipError_t launch_shard_merge(uint32_t S, uint32_t m, const uint32_t* counts, const uint64_t* src_base,
                               const uint32_t* ids, const uint64_t* keys, uint32_t* out_count, uint64_t* out_off,

@@ -199,8 +199,7 @@ __device__ __forceinline__ Hit lit_child(const ImageView& im, uint32_t v, uint32
 }
 
 __device__ __forceinline__ uint4 load_half(const ImageView& im, uint32_t v, bool leaf) {
-    return *reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(im.nodes) + (uint64_t)v * sizeof(Node) +
-                                          (leaf ? 16u : 0u));
+    return *reinterpret_cast<const uint4*>((leaf ? im.leaf : im.inner) + ((uint64_t)v << im.node_shift));
 }
 
 // ---------------------------------------------------------------------------
@@ -702,6 +701,23 @@ static uint32_t resident_grid(Kern k, uint32_t n_tiles, uint32_t cap_per_cu = 0)
     if (cap_per_cu && per > (int)cap_per_cu) per = (int)cap_per_cu;
     uint32_t g = (uint32_t)((per > 0 ? per : 1) * (cus > 0 ? cus : 1));
     return g < n_tiles ? g : n_tiles;
+}
+
+// split image: node records -> separate arrays of inner and leaf halves
+__global__ void __launch_bounds__(BLOCK)
+tm_split_nodes(const uint4* __restrict__ nodes, uint64_t n, uint4* __restrict__ inner, uint4* __restrict__ leaf) {
+    for (uint64_t v = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; v < n; v += (uint64_t)gridDim.x * BLOCK) {
+        inner[v] = nodes[2 * v];
+        leaf[v] = nodes[2 * v + 1];
+    }
+}
+
+hipError_t launch_split_nodes(const void* nodes, uint64_t n, void* inner, void* leaf, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    const uint64_t blocks = (n + BLOCK - 1) / BLOCK;
+    hipLaunchKernelGGL(tm_split_nodes, dim3((uint32_t)(blocks < 8192 ? blocks : 8192)), dim3(BLOCK), 0, st,
+                       (const uint4*)nodes, n, (uint4*)inner, (uint4*)leaf);
+    return hipGetLastError();
 }
 
 size_t scan_tmp_elems(uint32_t n) { return div_up(n ? n : 1, SCAN_TILE); }

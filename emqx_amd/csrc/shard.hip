@@ -25,47 +25,102 @@ tm_shard_sum(uint32_t S, uint32_t m, const uint32_t* __restrict__ counts, uint32
     out_count[t] = c;
 }
 
-__global__ void __launch_bounds__(MBLOCK)
+// One wave per topic.  Item i of the topic's S concatenated lists (each in
+// descending key order) belongs to source s with ls[s] <= i < ls[s+1]; its
+// output position is its index in its own list plus, for every other list,
+// the number of keys greater than its own (binary search).  Keys of one
+// topic are distinct, so positions are a permutation.  The wave loads all
+// items of the topic at once (one round trip) into LDS, searches there, and
+// writes every id once; a topic beyond MCAP ids searches the lists in global
+// memory instead (L2-resident after the first touch).
+constexpr uint32_t MCAP = 512;   // ids of one topic staged in LDS (6 KB)
+
+template <class Keys>
+__device__ __forceinline__ uint32_t count_greater(const Keys& a, uint32_t len, uint64_t key) {
+    uint32_t lo = 0, hi = len;   // a[] descending: first index with a[i] <= key
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (a[mid] > key) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+__global__ void __launch_bounds__(64)
 tm_shard_merge(uint32_t S, uint32_t m, const uint32_t* __restrict__ counts, const uint64_t* __restrict__ src_base,
                const uint64_t* __restrict__ pre, const uint32_t* __restrict__ ids, const uint64_t* __restrict__ keys,
                const uint64_t* __restrict__ out_off, uint32_t* __restrict__ out_gid, uint64_t out_cap) {
-    const uint32_t t = blockIdx.x * MBLOCK + threadIdx.x;
-    if (t >= m) return;
-    // heads (next item) and ends of the S lists; head keys cached; unrolled
-    // over MAX_SHARDS so every array stays in VGPRs
-    uint64_t h[MAX_SHARDS], e[MAX_SHARDS], hk[MAX_SHARDS];
-#pragma unroll
-    for (uint32_t s = 0; s < MAX_SHARDS; ++s) {
-        h[s] = e[s] = 0;
-        hk[s] = 0;
-        if (s < S) {
-            h[s] = src_base[s] + pre[(uint64_t)s * (m + 1) + t];
-            e[s] = h[s] + counts[(uint64_t)s * m + t];
-            if (h[s] < e[s]) hk[s] = keys[h[s]];
+    __shared__ uint64_t lk[MCAP];
+    __shared__ uint32_t lg[MCAP];
+    const uint32_t lane = threadIdx.x;
+    for (uint32_t t = blockIdx.x; t < m; t += gridDim.x) {
+        // lane s < S: head of source s's list for t and its length
+        uint64_t hs = 0;
+        uint32_t cs = 0;
+        if (lane < S) {
+            cs = counts[(uint64_t)lane * m + t];
+            hs = src_base[lane] + pre[(uint64_t)lane * m + t] - pre[(uint64_t)lane * m];
         }
-    }
-    uint64_t o = out_off[t];
-    for (;;) {
-        uint32_t best = MAX_SHARDS;
-        uint64_t bk = 0;
+        // every source's (length, start in the topic, head) in registers of
+        // every lane, read while the whole wave is active
+        uint32_t ns[MAX_SHARDS], ls[MAX_SHARDS];
+        uint64_t hh[MAX_SHARDS];
+        uint32_t c = 0;
 #pragma unroll
         for (uint32_t s = 0; s < MAX_SHARDS; ++s) {
-            const bool live = h[s] < e[s];
-            if (live && (best == MAX_SHARDS || hk[s] > bk)) {   // keys of one topic are distinct
-                best = s;
-                bk = hk[s];
-            }
+            ns[s] = s < S ? (uint32_t)__shfl((int)cs, (int)s, 64) : 0u;
+            hh[s] = s < S ? (uint64_t)__shfl((long long)hs, (int)s, 64) : 0ull;
+            ls[s] = c;
+            c += ns[s];
         }
-        if (best == MAX_SHARDS) break;
+        const uint64_t o = out_off[t];
+        // item i -> (source s, index j in s's list, global position)
+        auto locate = [&](uint32_t i, uint32_t& s, uint32_t& j, uint64_t& g) {
+            s = 0;
+            j = i;
+            g = hh[0] + i;
 #pragma unroll
-        for (uint32_t s = 0; s < MAX_SHARDS; ++s) {
-            if (s == best) {
-                if (o < out_cap) out_gid[o] = ids[h[s]] * S + s;
-                ++h[s];
-                if (h[s] < e[s]) hk[s] = keys[h[s]];
+            for (uint32_t q = 1; q < MAX_SHARDS; ++q)
+                if (q < S && i >= ls[q]) {
+                    s = q;
+                    j = i - ls[q];
+                    g = hh[q] + j;
+                }
+        };
+        if (c <= MCAP) {
+            for (uint32_t i = lane; i < c; i += 64) {
+                uint32_t s, j;
+                uint64_t g;
+                locate(i, s, j, g);
+                lk[i] = keys[g];
+                lg[i] = ids[g] * S + s;
+            }
+            __syncthreads();
+            for (uint32_t i = lane; i < c; i += 64) {
+                uint32_t s, j;
+                uint64_t g;
+                locate(i, s, j, g);
+                const uint64_t key = lk[i];
+                uint32_t r = j;
+#pragma unroll
+                for (uint32_t s2 = 0; s2 < MAX_SHARDS; ++s2)
+                    if (s2 != s && ns[s2]) r += count_greater(lk + ls[s2], ns[s2], key);
+                if (o + r < out_cap) out_gid[o + r] = lg[i];
+            }
+            __syncthreads();
+        } else {
+            for (uint32_t i = lane; i < c; i += 64) {
+                uint32_t s, j;
+                uint64_t g;
+                locate(i, s, j, g);
+                const uint64_t key = keys[g];
+                uint32_t r = j;
+#pragma unroll
+                for (uint32_t s2 = 0; s2 < MAX_SHARDS; ++s2)
+                    if (s2 != s && ns[s2]) r += count_greater(keys + hh[s2], ns[s2], key);
+                if (o + r < out_cap) out_gid[o + r] = ids[g] * S + s;
             }
         }
-        ++o;
     }
 }
 
@@ -80,17 +135,16 @@ hipError_t launch_shard_merge(uint32_t S, uint32_t m, const uint32_t* counts, co
         hipError_t err = hipMemsetAsync(out_off, 0, 8, st);
         return err == hipSuccess ? hipMemsetAsync(total, 0, 8, st) : err;
     }
-    for (uint32_t s = 0; s < S; ++s) {
-        // per-source exclusive prefix of its counts (its total lands in pre's last slot)
-        uint64_t* p = pre + (uint64_t)s * (m + 1);
-        hipError_t err = launch_scan(counts + (uint64_t)s * m, m, p, p + m, tmp, st);
-        if (err != hipSuccess) return err;
-    }
-    hipLaunchKernelGGL(tm_shard_sum, dim3(mdiv_up(m, MBLOCK)), dim3(MBLOCK), 0, st, S, m, counts, out_count);
-    hipError_t err = launch_scan(out_count, m, out_off, total, tmp, st);
+    // exclusive prefix of all S x m counts, source-major: within source s,
+    // pre[s*m + t] - pre[s*m] is topic t's offset in s's block
+    hipError_t err = launch_scan(counts, S * m, pre, pre + (uint64_t)S * m, tmp, st);
     if (err != hipSuccess) return err;
-    hipLaunchKernelGGL(tm_shard_merge, dim3(mdiv_up(m, MBLOCK)), dim3(MBLOCK), 0, st, S, m, counts, src_base, pre,
-                       ids, keys, out_off, out_gid, out_cap);
+    hipLaunchKernelGGL(tm_shard_sum, dim3(mdiv_up(m, MBLOCK)), dim3(MBLOCK), 0, st, S, m, counts, out_count);
+    err = launch_scan(out_count, m, out_off, total, tmp, st);
+    if (err != hipSuccess) return err;
+    const uint32_t grid = m < 65536 ? m : 65536;
+    hipLaunchKernelGGL(tm_shard_merge, dim3(grid), dim3(64), 0, st, S, m, counts, src_base, pre, ids, keys, out_off,
+                       out_gid, out_cap);
     return hipGetLastError();
 }
 

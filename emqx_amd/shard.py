@@ -1,9 +1,9 @@
 """Sharded mode of the topic-routing engine.
 
 When the filter set is partitioned over S GPUs (one process per GPU), every
-GPU holds the sub-trie of its shard (`tm_shard_of`: by root level, so one
-literal root's subtree is on one shard; root '+' / '#' filters are spread by
-their bytes).  A publish batch is broadcast to all ranks; each rank walks the
+GPU holds the sub-trie of its shard (`tm_shard_of`: a hash of the filter's
+prefix through its second literal level, so Zipf-heavy root words and
+wildcard-led subtrees such as "+/+/..." spread over all shards).  A publish batch is broadcast to all ranks; each rank walks the
 WHOLE batch against its sub-trie (match(T, F) = U_s match(T, F_s)) with order
 keys (`tm_match_batch_device_keys`), then the ranks exchange per-topic lists
 so that rank r ends up owning the complete, ordered match lists of topic slice
@@ -30,6 +30,33 @@ from .engine import Engine
 
 def shard_of(filt: bytes, n_shards: int) -> int:
     return L.load().tm_shard_of(filt, len(filt), n_shards)
+
+
+def shard_of_batch(buf, off, n_shards: int):
+    """u32[n]: the shard of every filter of a packed batch"""
+    n = len(off) - 1
+    buf = np.ascontiguousarray(buf, dtype=np.uint8)
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    out = np.zeros(max(n, 1), dtype=np.uint32)
+    rc = L.load().tm_shard_of_batch(buf.ctypes.data, off.ctypes.data, n, n_shards, out.ctypes.data)
+    if rc != L.TM_OK:
+        raise L.TopicMatchError(rc, "tm_shard_of_batch")
+    return out[:n]
+
+
+def gid_to_index(owner, n_shards: int):
+    """For a DISTINCT filter list inserted shard by shard in list order (local
+    id = rank among the shard's filters): int64 array gid -> list index, with
+    gid = local * n_shards + shard."""
+    owner = np.asarray(owner, dtype=np.int64)
+    local = np.zeros(len(owner), dtype=np.int64)
+    for s in range(n_shards):
+        sel = np.nonzero(owner == s)[0]
+        local[sel] = np.arange(len(sel))
+    gid = local * n_shards + owner
+    out = np.full(int(gid.max()) + 1 if len(gid) else 0, -1, dtype=np.int64)
+    out[gid] = np.arange(len(owner))
+    return out
 
 
 def slices(n: int, n_shards: int):
@@ -86,6 +113,8 @@ def exchange(counts, offs, ids, keys, n, n_shards, rank, group=None):
     b = slices(n, n_shards)
     m = b[rank + 1] - b[rank]
     dev = counts.device
+    if n_shards == 1:      # one shard: its own lists are the whole result
+        return counts[:n], torch.zeros(1, dtype=torch.int64, device=dev), ids, keys, n
     in_splits = [b[d + 1] - b[d] for d in range(n_shards)]
     recv_counts = torch.empty(n_shards * m, dtype=torch.int32, device=dev)
     dist.all_to_all_single(recv_counts, counts[:n].contiguous(), output_split_sizes=[m] * n_shards,

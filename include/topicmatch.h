@@ -83,10 +83,16 @@ int tm_insert(tm_engine* e, const uint8_t* filter, uint32_t len);
  * the first failure and returns its code. */
 int tm_insert_batch(tm_engine* e, const uint8_t* bytes, const uint64_t* off, uint32_t n);
 
-/* Sharded mode: the shard (0..n_shards-1) that owns a filter — by its root
- * level, so a literal root's whole subtree lives on one shard; filters whose
- * root is '+' or '#' are spread over all shards by their bytes. */
+/* Sharded mode: the shard (0..n_shards-1) that owns a filter — by a hash of
+ * its prefix through the second literal (non '+'/'#') level, so every filter
+ * under one such prefix lives on one shard.  Any partition is correct (a
+ * match is a per-filter predicate, match(T, F) = U_s match(T, F_s)); this one
+ * keeps sub-tries disjoint below the prefix and spreads Zipf-heavy root words
+ * and wildcard-led subtrees over all shards. */
 uint32_t tm_shard_of(const uint8_t* filter, uint32_t len, uint32_t n_shards);
+
+/* tm_shard_of over a packed batch: out[i] = shard of filter [off[i], off[i+1]). */
+int tm_shard_of_batch(const uint8_t* bytes, const uint64_t* off, uint32_t n, uint32_t n_shards, uint32_t* out);
 
 /* tm_insert_batch restricted to the filters tm_shard_of assigns to `shard`. */
 int tm_insert_batch_shard(tm_engine* e, const uint8_t* bytes, const uint64_t* off, uint32_t n,

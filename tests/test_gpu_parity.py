@@ -222,24 +222,34 @@ def test_stats_edge_reads_match_oracle(gpu_device, golden):
     e.close()
 
 
-@pytest.mark.parametrize("walk", ["queue", "queue_xcd"])
-def test_every_walk_variant_bit_exact(gpu_device, golden, walk):
-    """each kernel variant (A/B knobs) against the committed vectors and C1"""
+VARIANTS = {"queue": {}, "queue_xcd": {}, "queue_xcd@nosplit@dfs": {"split": 0, "hot_levels": 0},
+            "queue_xcd@hot3": {"hot_levels": 3, "layout": 2}, "queue_xcd@nosplit@hot2": {"split": 0, "hot_levels": 2}}
+
+
+@pytest.mark.parametrize("variant", list(VARIANTS))
+def test_every_walk_variant_bit_exact(gpu_device, golden, variant):
+    """each kernel / image variant (A/B knobs) against the committed vectors and C1"""
+    walk = variant.split("@")[0]
+
+    def configure(e):
+        e.set_walk(walk)
+        for k, v in VARIANTS[variant].items():
+            e.set_option(k, v)
     for vec in golden["o1_vectors"]:
         e = Engine(device=gpu_device)
-        e.set_walk(walk)
+        configure(e)
         e.set_option("stage_k", 4)          # force the fan-out re-walk path too
         for f in vec["filters"]:
             e.insert(b(f))
         got = e.match([b(r["topic"]) for r in vec["topics"]])
         for row, g in zip(vec["topics"], got):
-            assert [x.decode(L1) for x in g] == row["match"], (walk, vec["name"], row["topic"])
+            assert [x.decode(L1) for x in g] == row["match"], (variant, vec["name"], row["topic"])
         e.close()
     fb, fo = W.filters(1)
     o1 = O1()
     o1.insert_many(fb, fo)
     e = Engine(device=gpu_device)
-    e.set_walk(walk)
+    configure(e)
     e.insert_many(fb, fo)
     tb, to = W.topics(1, n=30000)
     _by_id(o1, e, tb, to)

@@ -110,3 +110,18 @@ def test_sharded_kats(gpu_device, golden):
         filters = [f.encode("latin-1") for f in vec["filters"]]
         got = _run_sharded(filters, topics, 3)
         assert [[x.decode("latin-1") for x in row] for row in got] == [r["match"] for r in vec["topics"]], vec["name"]
+
+
+def test_sharded_topic_beyond_lds_merge(gpu_device):
+    """a topic with > 1024 matches (all 2^11 literal/'+' combinations of an
+    11-level topic, plus '#' prefixes) takes the merge's serial path"""
+    import itertools
+    words = [b"l%d" % i for i in range(11)]
+    filters = [b"/".join(w if bit else b"+" for w, bit in zip(words, bits))
+               for bits in itertools.product([0, 1], repeat=11)]
+    filters += [b"/".join(words[:k] + [b"#"]) for k in range(11)]
+    topics = [b"/".join(words), b"l0/l1/x", b"/".join(words[:5]), b"$SYS/l1"]
+    want = _o1(filters, topics)
+    assert len(want[0]) > 1024
+    for S in (2, 5):
+        assert _run_sharded(filters, topics, S, K=256) == want

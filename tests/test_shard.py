@@ -28,10 +28,18 @@ def test_shard_of_partition():
     for s in (1, 2, 3, 8):
         owners = [shard.shard_of(f, s) for f in fs]
         assert all(0 <= x < s for x in owners)
-        assert shard.shard_of(b"a/+", s) == shard.shard_of(b"a/b/#", s) == shard.shard_of(b"a", s)
-    # root wildcards spread over every shard
+        # one prefix through the 2nd literal level -> one shard
+        assert shard.shard_of(b"a/b/+", s) == shard.shard_of(b"a/b/#", s) == shard.shard_of(b"a/b", s)
+        assert shard.shard_of(b"+/b/c/d", s) == shard.shard_of(b"+/b/c/+", s) == shard.shard_of(b"+/b/c", s)
+        assert shard.shard_of(b"+/+/#", s) == shard.shard_of(b"+/+/#", s)
+    # root wildcards and one root's subtrees spread over every shard
     assert np.unique([shard.shard_of(b"+/%d" % i, 8) for i in range(400)]).size == 8
-    assert np.unique([shard.shard_of(b"#", 8)]).size == 1
+    assert np.unique([shard.shard_of(b"a/%d/#" % i, 8) for i in range(400)]).size == 8
+    assert np.unique([shard.shard_of(b"+/+/%d/x" % i, 8) for i in range(400)]).size == 8
+    from emqx_amd import workload as W
+    fb, fo = W.filters(4, n=200_000)
+    load = np.bincount(shard.shard_of_batch(fb, fo, 8), minlength=8) / 25_000
+    assert load.max() < 1.6, load
 
 
 def _workload():
