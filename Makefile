@@ -23,7 +23,10 @@ $(BUILD)/engine.o: emqx_amd/csrc/engine.cpp emqx_amd/csrc/kernels.h emqx_amd/csr
 $(BUILD)/shard.o: emqx_amd/csrc/shard.hip emqx_amd/csrc/kernels.h emqx_amd/csrc/image.h | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-emqx_amd/libtopicmatch.so: $(BUILD)/kernels.o $(BUILD)/shard.o $(BUILD)/engine.o
+$(BUILD)/routes.o: emqx_amd/csrc/routes.hip emqx_amd/csrc/kernels.h emqx_amd/csrc/image.h | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+emqx_amd/libtopicmatch.so: $(BUILD)/kernels.o $(BUILD)/shard.o $(BUILD)/routes.o $(BUILD)/engine.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -o $@
 
 emqx_amd/libtmwork.so: emqx_amd/csrc/workload.c

@@ -72,6 +72,21 @@ SIGNATURES = [
                                       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
                                       ctypes.c_void_p]),
+    ("tm_route_add", ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p,
+                                    ctypes.c_uint32]),
+    ("tm_route_del", ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p,
+                                    ctypes.c_uint32]),
+    ("tm_get_routes", ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_void_p,
+                                     ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]),
+    ("tm_route_count", ctypes.c_uint64, [ctypes.c_void_p]),
+    ("tm_dest_bytes", ctypes.c_void_p, [ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]),
+    ("tm_match_routes_batch", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                             ctypes.c_uint64, ctypes.c_void_p]),
+    ("tm_match_routes_batch_device", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                    ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p,
+                                                    ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                    ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]),
     ("tm_last_stats", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(TmBatchStats)]),
     ("tm_set_timing", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     ("tm_last_kernel_times", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_char_p),

@@ -23,6 +23,7 @@
 #include <new>
 #include <stdexcept>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/topicmatch.h"
@@ -30,6 +31,8 @@
 #include "kernels.h"
 
 using namespace tmx;
+
+extern "C" int tm_topic_wildcard(const uint8_t* topic, uint32_t len);
 
 namespace {
 
@@ -182,6 +185,18 @@ struct tm_engine {
     int split_halves = 1;             // option "split": walk reads separate inner / leaf half arrays
     bool split_stale = true;
     DevBuf d_inner, d_leaf;
+
+    // ---- route table: the emqx_route bag (src/emqx_router.erl:52-59) ----
+    std::unordered_map<std::string, uint32_t> dest_index;   // dest bytes -> dest id
+    std::vector<std::string> dest_names;
+    std::unordered_map<std::string, std::vector<uint32_t>> route_bag;   // topic -> dests, insertion order
+    size_t route_total = 0;
+    bool routes_dirty = true;         // the route image must be rebuilt at commit
+    DevBuf d_fr_off, d_fr_dest, d_ex_slots, d_ex_arena, d_ex_dest;
+    uint64_t ex_slot_mask = 0;
+    uint32_t fr_filters = 0;          // filter ids covered by fr_off
+    bool route_image = false;
+    DevBuf w_rexact, w_rscan, w_rids, w_rcounts, w_roff;
 
     // ---- match workspace ----
     DevBuf w_kstage, w_mpre, w_mscan, w_twords, w_bytes, w_off, w_words, w_meta, w_counts, w_outoff, w_ids, w_scan, w_total, w_path, w_stats, w_stage,
@@ -527,6 +542,7 @@ struct tm_engine {
         for (uint32_t w : tmp_words) v = child_or_create(v, w);
         if (nodes[v].self_filter == FILTER_NONE) set_topic(v, new_filter(p, len, v));
         dev_dirty = true;
+        routes_dirty = true;   // filter ids may have changed
     }
 
     // emqx_trie:delete/1 (src/emqx_trie.erl:88-96) + delete_path/1 (:149-163)
@@ -552,6 +568,131 @@ struct tm_engine {
             }
         }
         dev_dirty = true;
+        routes_dirty = true;
+    }
+
+    // ------------------------------------------------------------------
+    // routes (emqx_router.erl): add_route/del_route with the reference's
+    // trie bookkeeping, get_routes/1, and the route image match_routes/1 reads
+    uint32_t intern_dest(const uint8_t* d, uint32_t dlen) {
+        std::string k(reinterpret_cast<const char*>(d), dlen);
+        auto it = dest_index.find(k);
+        if (it != dest_index.end()) return it->second;
+        if (dest_names.size() >= 0xFFFFFFF0ull) throw RangeError("dest ids exhausted");
+        const uint32_t id = (uint32_t)dest_names.size();
+        dest_names.push_back(k);
+        dest_index.emplace(std::move(k), id);
+        return id;
+    }
+    // handle_cast({add_route, Route}) (:153-163) + add_trie_route/1 (:226-231)
+    void route_add(const uint8_t* t, uint32_t tlen, const uint8_t* d, uint32_t dlen) {
+        const uint32_t dest = intern_dest(d, dlen);
+        std::string key(reinterpret_cast<const char*>(t), tlen);
+        auto it = route_bag.find(key);
+        if (it != route_bag.end() &&
+            std::find(it->second.begin(), it->second.end(), dest) != it->second.end())
+            return;   // lists:member(Route, get_routes(Topic)) -> ok
+        const bool had = it != route_bag.end() && !it->second.empty();
+        if (tm_topic_wildcard(t, tlen) && !had) insert(t, tlen);   // mnesia:wread -> [] -> emqx_trie:insert
+        route_bag[key].push_back(dest);
+        ++route_total;
+        routes_dirty = true;
+    }
+    // handle_cast({del_route, Route}) (:165-187) + del_trie_route/1 (:252-260)
+    // or del_direct_route/1 (:240-241); the emqx_subscriber check (:179) is
+    // the broker's and stays in the caller
+    void route_del(const uint8_t* t, uint32_t tlen, const uint8_t* d, uint32_t dlen) {
+        auto di = dest_index.find(std::string(reinterpret_cast<const char*>(d), dlen));
+        if (di == dest_index.end()) return;
+        auto it = route_bag.find(std::string(reinterpret_cast<const char*>(t), tlen));
+        if (it == route_bag.end()) return;   // [] -> ok
+        std::vector<uint32_t>& bag = it->second;
+        auto pos = std::find(bag.begin(), bag.end(), di->second);
+        if (pos == bag.end()) return;        // delete_object of an absent route: no-op
+        const bool last = bag.size() == 1;
+        bag.erase(pos);
+        --route_total;
+        if (last) {
+            route_bag.erase(it);
+            if (tm_topic_wildcard(t, tlen)) remove(t, tlen);   // [Route] -> emqx_trie:delete(Topic)
+        }
+        routes_dirty = true;
+    }
+    const std::vector<uint32_t>* get_routes(const uint8_t* t, uint32_t tlen) const {
+        auto it = route_bag.find(std::string(reinterpret_cast<const char*>(t), tlen));
+        return it == route_bag.end() ? nullptr : &it->second;
+    }
+    // filter id of a trie filter (or FILTER_NONE)
+    uint32_t filter_of(const uint8_t* p, uint32_t len) {
+        if (!split_words(p, len, false)) return FILTER_NONE;
+        const uint32_t v = walk(tmp_words);
+        return v == NODE_NONE ? FILTER_NONE : nodes[v].self_filter;
+    }
+    // rebuild the route image: per-filter-id dest lists (CSR) and the
+    // exact-topic table over every topic with routes
+    void build_route_image() {
+        const uint32_t nf = (uint32_t)filters.size();
+        std::vector<uint32_t> fr_off(nf + 1, 0);
+        std::vector<std::pair<uint32_t, const std::vector<uint32_t>*>> by_fid;
+        by_fid.reserve(route_bag.size());
+        size_t cap = 16;
+        while (cap < route_bag.size() * 2) cap <<= 1;
+        std::vector<ExactSlot> slots(cap);
+        for (auto& x : slots) x = ExactSlot{0, 0, 0, 0, 0, 0};
+        std::vector<uint8_t> arena;
+        std::vector<uint32_t> ex_dest;
+        ex_dest.reserve(route_total);
+        for (const auto& kv : route_bag) {
+            const uint8_t* t = reinterpret_cast<const uint8_t*>(kv.first.data());
+            const uint32_t tlen = (uint32_t)kv.first.size();
+            if (tm_topic_wildcard(t, tlen)) {
+                const uint32_t fid = filter_of(t, tlen);
+                if (fid != FILTER_NONE) {
+                    fr_off[fid + 1] = (uint32_t)kv.second.size();
+                    by_fid.emplace_back(fid, &kv.second);
+                }
+            }
+            const uint64_t h = word_hash(t, tlen);
+            size_t sl = h & (cap - 1);
+            while (slots[sl].hash) sl = (sl + 1) & (cap - 1);
+            ExactSlot& e = slots[sl];
+            e.hash = h;
+            e.len = tlen;
+            e.count = (uint32_t)kv.second.size();
+            e.arena = arena.size();
+            e.dest_off = (uint32_t)ex_dest.size();
+            arena.resize(arena.size() + std::max<size_t>(8, (tlen + 7) & ~size_t(7)), 0);
+            if (tlen) std::memcpy(&arena[e.arena], t, tlen);
+            ex_dest.insert(ex_dest.end(), kv.second.begin(), kv.second.end());
+        }
+        for (uint32_t f = 0; f < nf; ++f) fr_off[f + 1] += fr_off[f];
+        std::vector<uint32_t> fr_dest(fr_off[nf]);
+        for (const auto& x : by_fid) std::copy(x.second->begin(), x.second->end(), fr_dest.begin() + fr_off[x.first]);
+        auto up = [&](DevBuf& b, const void* src, size_t bytes) {
+            b.ensure(std::max<size_t>(bytes, 16));
+            if (bytes) HIPCHK(hipMemcpyAsync(b.p, src, bytes, hipMemcpyHostToDevice, stream));
+        };
+        up(d_fr_off, fr_off.data(), fr_off.size() * 4);
+        up(d_fr_dest, fr_dest.data(), fr_dest.size() * 4);
+        up(d_ex_slots, slots.data(), slots.size() * sizeof(ExactSlot));
+        up(d_ex_arena, arena.data(), arena.size());
+        up(d_ex_dest, ex_dest.data(), ex_dest.size() * 4);
+        ex_slot_mask = cap - 1;
+        fr_filters = nf;
+        route_image = !route_bag.empty();
+        HIPCHK(hipStreamSynchronize(stream));   // host vectors die here
+        routes_dirty = false;
+    }
+    RouteView route_view() const {
+        RouteView rv;
+        rv.fr_off = d_fr_off.as<const uint32_t>();
+        rv.fr_dest = d_fr_dest.as<const uint32_t>();
+        rv.n_filters = route_image ? fr_filters : 0u;
+        rv.ex_slots = route_image ? d_ex_slots.as<const ExactSlot>() : nullptr;
+        rv.ex_slot_mask = ex_slot_mask;
+        rv.ex_arena = d_ex_arena.as<const uint8_t>();
+        rv.ex_dest = d_ex_dest.as<const uint32_t>();
+        return rv;
     }
 
     // ------------------------------------------------------------------
@@ -832,6 +973,40 @@ struct tm_engine {
         if (timing_enabled)
             for (int i = 0; i < 4; ++i) ev_pending.push_back(ev_cur[i]);
     }
+    // emqx_router:match_routes/1 over a device batch (stream-ordered except
+    // for one read of the match total that sizes the ids workspace)
+    void run_routes(const uint8_t* bytes, const uint64_t* off, uint32_t n, uint64_t nbytes, uint32_t* counts,
+                    uint64_t* out_off, uint32_t* src, uint32_t* dest, uint64_t cap, uint64_t* total,
+                    hipStream_t st) {
+        if (routes_dirty) {
+            if (route_bag.empty()) {
+                route_image = false;
+                routes_dirty = false;
+            } else {
+                build_route_image();
+            }
+        }
+        w_rcounts.ensure((size_t)n * 4 + 4);
+        w_roff.ensure((size_t)(n + 1) * 8);
+        uint64_t want = std::max<uint64_t>(w_rids.bytes / 4, (uint64_t)n * 16 + 1024);
+        w_rids.ensure(want * 4, 1.0);
+        uint64_t icap = w_rids.bytes / 4, ids_total = 0;
+        for (int pass = 0; pass < 2; ++pass) {
+            run_batch(bytes, off, n, nbytes, w_rcounts.as<uint32_t>(), w_roff.as<uint64_t>(), w_rids.as<uint32_t>(),
+                      icap, total, st);
+            HIPCHK(hipMemcpyAsync(&ids_total, total, 8, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipStreamSynchronize(st));
+            if (ids_total <= icap) break;
+            w_rids.ensure(ids_total * 4, 1.25);
+            icap = w_rids.bytes / 4;
+        }
+        w_rexact.ensure((size_t)n * 8 + 8);
+        w_rscan.ensure(scan_tmp_elems(n) * 8 + 8);
+        HIPCHK(launch_routes(route_view(), bytes, off, n, w_rcounts.as<uint32_t>(), w_roff.as<uint64_t>(),
+                             w_rids.as<uint32_t>(), w_rexact.as<uint2>(), counts, out_off, src, dest, cap, total,
+                             w_rscan.as<uint64_t>(), st));
+    }
+
     void finish_batch(hipStream_t st, uint32_t n) {
         if (!last_match_done) HIPCHK(hipEventCreateWithFlags(&last_match_done, hipEventDisableTiming));
         HIPCHK(hipEventRecord(last_match_done, st));
@@ -957,6 +1132,9 @@ void tm_close(tm_engine* e) {
     if (e->device >= 0) {
         (void)hipSetDevice(e->device);
         if (e->stream) (void)hipStreamSynchronize(e->stream);
+        for (DevBuf* b : {&e->d_fr_off, &e->d_fr_dest, &e->d_ex_slots, &e->d_ex_arena, &e->d_ex_dest, &e->w_rexact,
+                          &e->w_rscan, &e->w_rids, &e->w_rcounts, &e->w_roff})
+            b->release();
         for (DevBuf* b : {&e->d_nodes, &e->d_edges, &e->d_dict, &e->d_arena, &e->d_woff, &e->d_inner, &e->d_leaf,
                           &e->w_kstage, &e->w_mpre, &e->w_mscan, &e->w_twords, &e->w_bytes, &e->w_off, &e->w_words,
                           &e->w_meta, &e->w_counts, &e->w_outoff, &e->w_ids, &e->w_scan, &e->w_total, &e->w_path,
@@ -1147,6 +1325,133 @@ int tm_match_batch(tm_engine* e, const uint8_t* topic_bytes, const uint64_t* top
 static int match_device(tm_engine* e, const uint8_t* d_bytes, const uint64_t* d_off, uint32_t n,
                         uint64_t topic_bytes, uint32_t* d_count, uint64_t* d_out_off, uint32_t* d_ids,
                         uint64_t* d_keys, uint64_t out_cap, uint64_t* d_total, void* hip_stream);
+
+// ---- routes (emqx_router) ---------------------------------------------------
+int tm_route_add(tm_engine* e, const uint8_t* topic, uint32_t tlen, const uint8_t* dest, uint32_t dlen) {
+    if ((!topic && tlen) || (!dest && dlen)) return TM_EINVAL;
+    return guarded(e, [&] {
+        e->route_add(topic, tlen, dest, dlen);
+        return TM_OK;
+    });
+}
+
+int tm_route_del(tm_engine* e, const uint8_t* topic, uint32_t tlen, const uint8_t* dest, uint32_t dlen) {
+    if ((!topic && tlen) || (!dest && dlen)) return TM_EINVAL;
+    return guarded(e, [&] {
+        e->route_del(topic, tlen, dest, dlen);
+        return TM_OK;
+    });
+}
+
+int tm_get_routes(tm_engine* e, const uint8_t* topic, uint32_t tlen, uint32_t* out_dest, uint32_t cap,
+                  uint32_t* out_n) {
+    if ((!topic && tlen) || !out_n || (cap && !out_dest)) return TM_EINVAL;
+    return guarded(e, [&] {
+        const std::vector<uint32_t>* b = e->get_routes(topic, tlen);
+        const uint32_t k = b ? (uint32_t)b->size() : 0u;
+        *out_n = k;
+        for (uint32_t i = 0; i < k && i < cap; ++i) out_dest[i] = (*b)[i];
+        return k > cap ? TM_ENOSPC : TM_OK;
+    });
+}
+
+uint64_t tm_route_count(tm_engine* e) {
+    if (!e) return 0;
+    std::lock_guard<std::recursive_mutex> lk(e->mu);
+    return e->route_total;
+}
+
+const uint8_t* tm_dest_bytes(tm_engine* e, uint32_t dest_id, uint32_t* len) {
+    if (!e) return nullptr;
+    std::lock_guard<std::recursive_mutex> lk(e->mu);
+    if (dest_id >= e->dest_names.size()) return nullptr;
+    if (len) *len = (uint32_t)e->dest_names[dest_id].size();
+    return reinterpret_cast<const uint8_t*>(e->dest_names[dest_id].data());
+}
+
+int tm_match_routes_batch_device(tm_engine* e, const uint8_t* d_bytes, const uint64_t* d_off, uint32_t n,
+                                 uint64_t topic_bytes, uint32_t* d_count, uint64_t* d_out_off, uint32_t* d_src,
+                                 uint32_t* d_dest, uint64_t out_cap, uint64_t* d_total, void* hip_stream) {
+    if (!d_off || !d_out_off || !d_total || (n && !d_count) || (out_cap && (!d_src || !d_dest))) return TM_EINVAL;
+    return guarded(e, [&]() -> int {
+        if (e->device < 0) {
+            e->last_error = "engine is host-only (device = -1): match_routes runs on the GPU only";
+            return TM_EDEVICE;
+        }
+        e->commit();
+        tm_engine::Guard g(e->device);
+        hipStream_t st = hip_stream ? (hipStream_t)hip_stream : e->stream;
+        if (n == 0) {
+            HIPCHK(hipMemsetAsync(d_out_off, 0, 8, st));
+            HIPCHK(hipMemsetAsync(d_total, 0, 8, st));
+            return TM_OK;
+        }
+        e->run_routes(d_bytes, d_off, n, topic_bytes, d_count, d_out_off, d_src, d_dest, out_cap, d_total, st);
+        e->finish_batch(st, n);
+        return TM_OK;
+    });
+}
+
+int tm_match_routes_batch(tm_engine* e, const uint8_t* topic_bytes, const uint64_t* topic_off, uint32_t n,
+                          uint32_t* out_count, uint64_t* out_off, uint32_t* out_src, uint32_t* out_dest,
+                          uint64_t out_cap, uint64_t* out_needed) {
+    if (!topic_off || !out_off || (n && !out_count) || (out_cap && (!out_src || !out_dest))) return TM_EINVAL;
+    return guarded(e, [&]() -> int {
+        if (e->device < 0) {
+            e->last_error = "engine is host-only (device = -1): match_routes runs on the GPU only";
+            return TM_EDEVICE;
+        }
+        for (uint32_t i = 0; i < n; ++i)
+            if (topic_off[i + 1] < topic_off[i]) throw ArgError("topic offsets not monotone");
+        const uint64_t base = topic_off[0], nbytes = topic_off[n] - base;
+        if (n && nbytes && !topic_bytes) throw ArgError("null topic bytes");
+        if (n == 0) {
+            out_off[0] = 0;
+            if (out_needed) *out_needed = 0;
+            return TM_OK;
+        }
+        e->commit();
+        tm_engine::Guard g(e->device);
+        hipStream_t st = e->stream;
+        e->w_bytes.ensure(nbytes + 16);
+        e->w_off.ensure((size_t)(n + 1) * 8);
+        e->w_counts.ensure((size_t)n * 4 + 4);
+        e->w_outoff.ensure((size_t)(n + 1) * 8);
+        std::vector<uint64_t> rel(topic_off, topic_off + n + 1);
+        for (auto& x : rel) x -= base;
+        if (nbytes) HIPCHK(hipMemcpyAsync(e->w_bytes.p, topic_bytes + base, nbytes, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(e->w_off.p, rel.data(), (n + 1) * 8, hipMemcpyHostToDevice, st));
+        e->ensure_workspace(n, nbytes);
+        uint64_t* d_total = e->w_total.as<uint64_t>() + 1;
+        // routes into engine buffers sized from the previous batch; grow and
+        // rerun only when a batch needs more
+        uint64_t want = std::max<uint64_t>(e->w_ids.bytes / 8, std::min<uint64_t>(out_cap, (uint64_t)n * 16 + 1024));
+        e->w_ids.ensure(want * 8, 1.0);
+        uint64_t rcap = e->w_ids.bytes / 8, total = 0;
+        for (int pass = 0; pass < 2; ++pass) {
+            uint32_t* src = e->w_ids.as<uint32_t>();
+            e->run_routes(e->w_bytes.as<uint8_t>(), e->w_off.as<uint64_t>(), n, nbytes, e->w_counts.as<uint32_t>(),
+                          e->w_outoff.as<uint64_t>(), src, src + rcap, rcap, d_total, st);
+            HIPCHK(hipMemcpyAsync(&total, d_total, 8, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipStreamSynchronize(st));
+            if (total <= rcap || total > out_cap) break;
+            e->w_ids.ensure(total * 8, 1.25);
+            rcap = e->w_ids.bytes / 8;
+        }
+        const uint64_t cap = std::min(total, out_cap);
+        e->finish_batch(st, n);
+        HIPCHK(hipMemcpyAsync(out_count, e->w_counts.p, (size_t)n * 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(out_off, e->w_outoff.p, (size_t)(n + 1) * 8, hipMemcpyDeviceToHost, st));
+        if (cap) {
+            HIPCHK(hipMemcpyAsync(out_src, e->w_ids.p, cap * 4, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipMemcpyAsync(out_dest, e->w_ids.as<uint32_t>() + rcap, cap * 4, hipMemcpyDeviceToHost, st));
+        }
+        HIPCHK(hipStreamSynchronize(st));
+        e->match_in_flight = false;
+        if (out_needed) *out_needed = total;
+        return total > out_cap ? TM_ENOSPC : TM_OK;
+    });
+}
 
 int tm_match_batch_device(tm_engine* e, const uint8_t* d_bytes, const uint64_t* d_off, uint32_t n,
                           uint64_t topic_bytes, uint32_t* d_count, uint64_t* d_out_off, uint32_t* d_ids,

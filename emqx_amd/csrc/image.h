@@ -103,6 +103,33 @@ struct ImageView {
     const uint32_t* word_off;          // word id -> arena offset
 };
 
+// ---- route image (emqx_route bag, src/emqx_router.erl:52-59, 89-90) --------
+// Routes are (topic, dest) pairs; dests are interned to u32 ids.  The routes
+// of a trie filter are found by its filter id (CSR fr_off/fr_dest over filter
+// ids, bag insertion order); the routes of a literal topic (get_routes/1 of
+// the publish topic itself) through an exact-topic hash table whose keys are
+// verified byte for byte against the topic arena (8-aligned, zero padded).
+constexpr uint32_t TM_ROUTE_TOPIC_ID = 0xFFFFFFFFu;   // route source = the literal topic
+
+struct alignas(32) ExactSlot {
+    uint64_t hash;         // word_hash of the topic bytes (0 = empty slot)
+    uint32_t len;          // topic length
+    uint32_t count;        // routes of the topic
+    uint64_t arena;        // topic bytes in the arena
+    uint32_t dest_off;     // first route's dest in ex_dest[]
+    uint32_t pad;
+};
+
+struct RouteView {
+    const uint32_t*  fr_off;        // n_filters + 1
+    const uint32_t*  fr_dest;
+    uint32_t         n_filters;
+    const ExactSlot* ex_slots;      // null: no routes
+    uint64_t         ex_slot_mask;
+    const uint8_t*   ex_arena;
+    const uint32_t*  ex_dest;
+};
+
 // ---- hashing (identical on host and device) ---------------------------------
 #if defined(__HIPCC__)
 #define TM_HD __host__ __device__ __forceinline__

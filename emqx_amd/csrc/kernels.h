@@ -41,6 +41,15 @@ hipError_t launch_split_nodes(const void* nodes, uint64_t n, void* inner, void* 
 hipError_t launch_scan(const uint32_t* counts, uint32_t n, uint64_t* out_off, uint64_t* total, uint64_t* tmp,
                        hipStream_t st);
 
+// emqx_router:match_routes/1 expansion (routes.hip) of a batch's ordered
+// match lists: per topic its literal-topic routes, then each matched filter's
+// routes.  exact: n uint2, rcount: n u32, tmp: scan_tmp_elems(n).  out_cap
+// == 0: counts and offsets only.
+hipError_t launch_routes(const RouteView& rv, const uint8_t* bytes, const uint64_t* off, uint32_t n,
+                         const uint32_t* counts, const uint64_t* ids_off, const uint32_t* ids, uint2* exact,
+                         uint32_t* rcount, uint64_t* out_off, uint32_t* out_src, uint32_t* out_dest,
+                         uint64_t out_cap, uint64_t* total, uint64_t* scan_tmp, hipStream_t st);
+
 // Sharded mode (shard.hip): merge per-topic match lists of S filter shards
 // for m topics.  counts [S][m]; source s's items start at src_base[s] of
 // ids / keys and are CSR-ordered by topic, each list in descending key order.

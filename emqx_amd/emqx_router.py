@@ -1,5 +1,7 @@
 """emqx_router — route table + trie deltas + match_routes/1 (src/emqx_router.erl),
-same names and semantics, backed by the MI355X engine for the trie part.
+same names and semantics, backed by the MI355X engine: the emqx_route bag
+lives in the engine (tm_route_add/del, get_routes), and match_routes/1 runs
+on the GPU end to end (trie walk + route expansion, routes.hip).
 
     add_route(Topic[, Dest])   handle_cast add_route  :148-163, add_trie_route :226-231
     del_route(Topic[, Dest])   handle_cast del_route  :165-187, del_trie_route :252-260
@@ -8,74 +10,81 @@ same names and semantics, backed by the MI355X engine for the trie part.
     get_routes / has_routes / topics   :89-90, :107-108, :110-111
 
 Route = (topic, dest) mirrors #route{topic, dest} (include/emqx.hrl:84-87);
-the emqx_route bag keeps insertion order per topic like an ETS bag.
+dests are node names or {Group, Node} tuples, passed to the engine as opaque
+bytes (the NIF would pass term_to_binary) and decoded back here.
 """
 from collections import namedtuple
 
-from . import emqx_topic
-from .engine import Engine
+from .engine import Engine, pack
 
 Route = namedtuple("Route", "topic dest")
+
+
+def _enc(dest) -> bytes:
+    if isinstance(dest, tuple):
+        return b"\x01" + b"\x00".join(_enc(x) for x in dest)
+    if isinstance(dest, str):
+        return b"\x02" + dest.encode()
+    return b"\x03" + bytes(dest)
 
 
 class Router:
     def __init__(self, engine: Engine, node=b"emqx@127.0.0.1"):
         self.engine = engine
         self.node = node
-        self.routes = {}   # emqx_route bag: topic -> [dest]
+        self._dec = {}          # encoded dest -> dest object
+        self._topics = {}       # topics with routes (insertion order): mnesia:dirty_all_keys(?ROUTE)
+
+    def _dest(self, dest_id: int):
+        return self._dec[self.engine.dest_bytes(dest_id)]
 
     # get_routes/1 — :89-90
     def get_routes(self, topic: bytes):
-        return [Route(topic, d) for d in self.routes.get(topic, [])]
+        return [Route(topic, self._dest(d)) for d in self.engine.get_routes(topic)]
 
     def has_routes(self, topic: bytes) -> bool:
-        return topic in self.routes
+        return topic in self._topics
 
     def topics(self):
-        return list(self.routes.keys())
+        return list(self._topics)
 
     # handle_cast({add_route, Route}) — :153-163
     def add_route(self, topic: bytes, dest=None):
         dest = self.node if dest is None else dest
-        bag = self.routes.get(topic, [])
-        if dest in bag:
-            return "ok"
-        if emqx_topic.wildcard(topic):
-            # add_trie_route/1 — :226-231: insert into the trie only when the
-            # topic had no route yet
-            if not bag:
-                self.engine.insert(topic)
-        self.routes.setdefault(topic, []).append(dest)
+        e = _enc(dest)
+        self._dec[e] = dest
+        self.engine.route_add(topic, e)
+        self._topics[topic] = True
         return "ok"
 
     # handle_cast({del_route, Route}) — :165-187 + del_trie_route/1 :252-260
     def del_route(self, topic: bytes, dest=None):
         dest = self.node if dest is None else dest
-        bag = self.routes.get(topic)
-        if not bag or dest not in bag:
-            return "ok"
-        if emqx_topic.wildcard(topic) and bag == [dest]:
-            self.engine.delete(topic)   # last route of the filter: remove it from the trie
-        bag.remove(dest)
-        if not bag:
-            del self.routes[topic]
+        self.engine.route_del(topic, _enc(dest))
+        if not self.engine.get_routes(topic):
+            self._topics.pop(topic, None)
         return "ok"
 
     # match_routes/1 — :116-118
     def match_routes(self, topic: bytes):
-        matched = self.engine.match([topic])[0]
-        out = []
-        for to in [topic] + matched:
-            out.extend(self.get_routes(to))
-        return out
+        return self.match_routes_many([topic])[0]
 
     def match_routes_many(self, topics):
         """batched match_routes/1: one device batch for all topics"""
-        rows = self.engine.match(list(topics))
-        res = []
-        for t, matched in zip(topics, rows):
-            out = []
-            for to in [t] + matched:
-                out.extend(self.get_routes(to))
-            res.append(out)
+        topics = list(topics)
+        buf, off = pack(topics)
+        counts, offs, src, dst = self.engine.match_routes_batch(buf, off)
+        names, res = {}, []
+        for t, topic in enumerate(topics):
+            row = []
+            for k in range(int(offs[t]), int(offs[t]) + int(counts[t])):
+                s = int(src[k])
+                if s == Engine.TOPIC_ROUTE:
+                    to = topic
+                else:
+                    if s not in names:
+                        names[s] = self.engine.filter_bytes(s)
+                    to = names[s]
+                row.append(Route(to, self._dest(int(dst[k]))))
+            res.append(row)
         return res

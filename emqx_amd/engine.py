@@ -162,6 +162,75 @@ class Engine:
                                             p(d_ids), out_cap, p(d_total), st)
         return self._check(rc, "tm_match_batch_device")
 
+    # -- emqx_router: the route bag and match_routes/1 ----------------------
+    TOPIC_ROUTE = 0xFFFFFFFF    # route source = the publish topic itself
+
+    def route_add(self, topic: bytes, dest: bytes):
+        return self._check(self.lib.tm_route_add(self.h, topic, len(topic), dest, len(dest)), "tm_route_add")
+
+    def route_del(self, topic: bytes, dest: bytes):
+        return self._check(self.lib.tm_route_del(self.h, topic, len(topic), dest, len(dest)), "tm_route_del")
+
+    def get_routes(self, topic: bytes):
+        """dest ids of topic's routes, insertion order (get_routes/1)"""
+        n = ctypes.c_uint32()
+        cap = 16
+        while True:
+            out = np.zeros(cap, dtype=np.uint32)
+            rc = self.lib.tm_get_routes(self.h, topic, len(topic), out.ctypes.data, cap, ctypes.byref(n))
+            if rc == L.TM_ENOSPC:
+                cap = n.value
+                continue
+            self._check(rc, "tm_get_routes")
+            return [int(x) for x in out[: n.value]]
+
+    @property
+    def route_count(self):
+        return self.lib.tm_route_count(self.h)
+
+    def dest_bytes(self, dest_id: int) -> bytes:
+        n = ctypes.c_uint32()
+        p = self.lib.tm_dest_bytes(self.h, dest_id, ctypes.byref(n))
+        if not p:
+            raise KeyError(dest_id)
+        return ctypes.string_at(p, n.value)
+
+    def match_routes_batch(self, buf, off, out_cap=None):
+        """Host batch -> (counts u32[n], offsets u64[n+1], src u32[total],
+        dest u32[total]): emqx_router:match_routes/1 per topic, src =
+        TOPIC_ROUTE for the literal topic's routes, else the filter id."""
+        buf = np.ascontiguousarray(buf, dtype=np.uint8)
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        n = len(off) - 1
+        counts = np.zeros(max(n, 1), dtype=np.uint32)
+        offs = np.zeros(n + 1, dtype=np.uint64)
+        cap = 1 << 16 if out_cap is None else out_cap
+        while True:
+            src = np.zeros(max(cap, 1), dtype=np.uint32)
+            dst = np.zeros(max(cap, 1), dtype=np.uint32)
+            needed = ctypes.c_uint64()
+            rc = self.lib.tm_match_routes_batch(self.h, _ptr(buf), _ptr(off), n, _ptr(counts), _ptr(offs), _ptr(src),
+                                                _ptr(dst), cap, ctypes.byref(needed))
+            if rc == L.TM_ENOSPC and out_cap is None:
+                cap = int(needed.value)
+                continue
+            self._check(rc, "tm_match_routes_batch")
+            k = int(needed.value)
+            return counts[:n], offs, src[:k], dst[:k]
+
+    def match_routes_batch_device(self, d_bytes, d_off, n, topic_bytes, d_counts, d_offs, d_src, d_dest, out_cap,
+                                  d_total, stream=None):
+        def p(x):
+            if x is None:
+                return None
+            return ctypes.c_void_p(x.data_ptr() if hasattr(x, "data_ptr") else int(x))
+        st = None
+        if stream is not None:
+            st = ctypes.c_void_p(stream if isinstance(stream, int) else stream.cuda_stream)
+        rc = self.lib.tm_match_routes_batch_device(self.h, p(d_bytes), p(d_off), n, topic_bytes, p(d_counts),
+                                                   p(d_offs), p(d_src), p(d_dest), out_cap, p(d_total), st)
+        return self._check(rc, "tm_match_routes_batch_device")
+
     # walk variants (A/B knobs of tm_walk_queue): one global dequeue head, or
     # per-XCD heads over contiguous ranges of the batch
     WALKS = {"queue": 0, "queue_xcd": 1}

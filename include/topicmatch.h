@@ -168,6 +168,55 @@ int tm_shard_merge(tm_engine* e, uint32_t n_shards, uint32_t m, const uint32_t* 
                    uint32_t* d_out_count, uint64_t* d_out_off, uint32_t* d_out_gid, uint64_t out_cap,
                    uint64_t* d_total, void* hip_stream);
 
+/* ---- routes: the emqx_route bag and emqx_router:match_routes/1 -------------
+ * A route is (topic, dest) (#route{topic, dest}, include/emqx.hrl:84-87); dest
+ * is opaque bytes (the NIF passes term_to_binary(node() | {Group, node()})),
+ * interned to a dest id.  Routes of one topic keep insertion order (ETS bag). */
+
+/* emqx_router add_route — handle_cast({add_route, Route}) src/emqx_router.erl:153-163
+ * and add_trie_route/1 :226-231: an existing route is a no-op; a wildcard
+ * topic (emqx_topic:wildcard/1) enters the trie (tm_insert) when it had no
+ * route yet. */
+int tm_route_add(tm_engine* e, const uint8_t* topic, uint32_t tlen, const uint8_t* dest, uint32_t dlen);
+
+/* emqx_router del_route — handle_cast({del_route, Route}) :165-187,
+ * del_trie_route/1 :252-260, del_direct_route/1 :240-241: removes the route;
+ * a wildcard topic leaves the trie (tm_delete) with its last route.  An
+ * absent route is a no-op.  (The emqx_subscriber check at :179 belongs to the
+ * broker and stays with the caller.) */
+int tm_route_del(tm_engine* e, const uint8_t* topic, uint32_t tlen, const uint8_t* dest, uint32_t dlen);
+
+/* get_routes/1 — :89-90: the dest ids of topic's routes in insertion order;
+ * *out_n = their number (TM_ENOSPC when it exceeds cap). */
+int tm_get_routes(tm_engine* e, const uint8_t* topic, uint32_t tlen, uint32_t* out_dest, uint32_t cap,
+                  uint32_t* out_n);
+
+/* number of routes (ets:info(emqx_route, size), emqx_router_helper.erl:148-154) */
+uint64_t tm_route_count(tm_engine* e);
+
+/* dest id -> dest bytes (engine-owned) */
+const uint8_t* tm_dest_bytes(tm_engine* e, uint32_t dest_id, uint32_t* len);
+
+#define TM_ROUTE_TOPIC 0xFFFFFFFFu   /* route source: the publish topic itself */
+
+/* emqx_router:match_routes/1 — src/emqx_router.erl:116-118 — over a batch:
+ * routes of topic t are out_src/out_dest[out_off[t] .. +out_count[t]): first
+ * get_routes(Topic) of the literal topic (out_src = TM_ROUTE_TOPIC), then,
+ * for each filter emqx_trie:match/1 returns, in its order, that filter's
+ * routes (out_src = filter id).  Host buffers, synchronous; TM_ENOSPC /
+ * out_needed as tm_match_batch.  Trie walk and route expansion both run on
+ * the GPU (routes.hip). */
+int tm_match_routes_batch(tm_engine* e, const uint8_t* topic_bytes, const uint64_t* topic_off, uint32_t n,
+                          uint32_t* out_count, uint64_t* out_off, uint32_t* out_src, uint32_t* out_dest,
+                          uint64_t out_cap, uint64_t* out_needed);
+
+/* Same with device buffers on hip_stream (reads the match total once to size
+ * its workspace); *d_total = route total, routes past out_cap are dropped. */
+int tm_match_routes_batch_device(tm_engine* e, const uint8_t* d_topic_bytes, const uint64_t* d_topic_off,
+                                 uint32_t n, uint64_t topic_bytes, uint32_t* d_out_count, uint64_t* d_out_off,
+                                 uint32_t* d_out_src, uint32_t* d_out_dest, uint64_t out_cap, uint64_t* d_total,
+                                 void* hip_stream);
+
 /* Engine knobs (the app-env analogue of SURVEY §5 config):
  *   "xcdq"     1 = per-XCD dequeue heads over contiguous ranges of the batch
  *              (default), 0 = one global head

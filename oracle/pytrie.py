@@ -243,3 +243,38 @@ def match_routes(trie: Trie, routes: dict, topic: bytes):
     for to in [topic] + matched:
         out.extend((to, d) for d in routes.get(to, []))
     return out
+
+
+class RouteTable:
+    """emqx_router's route bag with its trie bookkeeping (TEST ORACLE):
+    handle_cast add_route (src/emqx_router.erl:153-163) + add_trie_route/1
+    (:226-231), handle_cast del_route (:165-187) + del_trie_route/1
+    (:252-260) / del_direct_route/1 (:240-241), get_routes/1 (:89-90)."""
+
+    def __init__(self):
+        self.trie = Trie()
+        self.routes = {}
+
+    def add_route(self, topic: bytes, dest):
+        bag = self.routes.get(topic, [])
+        if dest in bag:                       # lists:member(Route, get_routes(Topic))
+            return
+        if wildcard(topic) and not bag:       # mnesia:wread -> [] -> emqx_trie:insert
+            self.trie.insert(topic)
+        self.routes.setdefault(topic, []).append(dest)
+
+    def del_route(self, topic: bytes, dest):
+        bag = self.routes.get(topic)
+        if not bag or dest not in bag:        # [] -> ok / delete_object of an absent route
+            return
+        if wildcard(topic) and bag == [dest]:  # [Route] -> delete route and trie path
+            self.trie.delete(topic)
+        bag.remove(dest)
+        if not bag:
+            del self.routes[topic]
+
+    def get_routes(self, topic: bytes):
+        return list(self.routes.get(topic, []))
+
+    def match_routes(self, topic: bytes):
+        return match_routes(self.trie, self.routes, topic)
