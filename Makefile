@@ -26,8 +26,11 @@ $(BUILD)/shard.o: emqx_amd/csrc/shard.hip emqx_amd/csrc/kernels.h emqx_amd/csrc/
 $(BUILD)/routes.o: emqx_amd/csrc/routes.hip emqx_amd/csrc/kernels.h emqx_amd/csrc/image.h | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-emqx_amd/libtopicmatch.so: $(BUILD)/kernels.o $(BUILD)/shard.o $(BUILD)/routes.o $(BUILD)/engine.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -o $@
+$(BUILD)/batcher.o: emqx_amd/csrc/batcher.cpp include/topicmatch.h | $(BUILD)
+	$(CXX) -O2 -fPIC -std=c++17 -Wall -pthread -c $< -o $@
+
+emqx_amd/libtopicmatch.so: $(BUILD)/kernels.o $(BUILD)/shard.o $(BUILD)/routes.o $(BUILD)/engine.o $(BUILD)/batcher.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -pthread $^ -o $@
 
 emqx_amd/libtmwork.so: emqx_amd/csrc/workload.c
 	$(CC) -O2 -fPIC -shared -Wall $< -o $@ -lm

@@ -36,6 +36,19 @@ class TmBatchStats(ctypes.Structure):
                 ("probe_loads", ctypes.c_uint64)]
 
 
+class TmBatcherConfig(ctypes.Structure):
+    _fields_ = [("max_topics", ctypes.c_uint32), ("deadline_us", ctypes.c_uint32), ("max_bytes", ctypes.c_uint64),
+                ("flags", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+
+
+class TmBatcherStats(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_uint64) for k in ("batches", "topics", "results", "max_batch", "size_seals",
+                                               "deadline_seals", "failed_batches")]
+
+
+TM_BATCHER_ROUTES = 1
+DONE_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, c_u32p, c_u32p, ctypes.c_uint32)
+
 # (name, restype, argtypes) — every symbol include/topicmatch.h declares
 SIGNATURES = [
     ("tm_open", ctypes.c_int, [ctypes.POINTER(TmConfig), ctypes.POINTER(ctypes.c_void_p)]),
@@ -50,6 +63,7 @@ SIGNATURES = [
     ("tm_insert_batch_shard",ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
                                              ctypes.c_uint32, ctypes.c_uint32]),
     ("tm_delete", ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint32]),
+    ("tm_delete_batch", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32]),
     ("tm_lookup", ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.POINTER(TmNodeInfo)]),
     ("tm_commit", ctypes.c_int, [ctypes.c_void_p, c_u64p]),
     ("tm_filter_count", ctypes.c_uint64, [ctypes.c_void_p]),
@@ -74,6 +88,8 @@ SIGNATURES = [
                                       ctypes.c_void_p]),
     ("tm_route_add", ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p,
                                     ctypes.c_uint32]),
+    ("tm_route_add_batch", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                          ctypes.c_void_p, ctypes.c_uint32]),
     ("tm_route_del", ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p,
                                     ctypes.c_uint32]),
     ("tm_get_routes", ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_void_p,
@@ -87,6 +103,13 @@ SIGNATURES = [
                                                     ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p,
                                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                                     ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]),
+    ("tm_batcher_open", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(TmBatcherConfig),
+                                       ctypes.POINTER(ctypes.c_void_p)]),
+    ("tm_batcher_submit", ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint32, DONE_FN, ctypes.c_void_p,
+                                         c_u64p]),
+    ("tm_batcher_flush", ctypes.c_int, [ctypes.c_void_p]),
+    ("tm_batcher_get_stats", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(TmBatcherStats)]),
+    ("tm_batcher_close", None, [ctypes.c_void_p]),
     ("tm_last_stats", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(TmBatchStats)]),
     ("tm_set_timing", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     ("tm_last_kernel_times", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_char_p),

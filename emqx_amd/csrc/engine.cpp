@@ -1217,6 +1217,17 @@ int tm_insert_batch_shard(tm_engine* e, const uint8_t* bytes, const uint64_t* of
     });
 }
 
+int tm_delete_batch(tm_engine* e, const uint8_t* bytes, const uint64_t* off, uint32_t n) {
+    if (n && (!bytes || !off)) return TM_EINVAL;
+    return guarded(e, [&] {
+        for (uint32_t i = 0; i < n; ++i) {
+            if (off[i + 1] < off[i] || off[i + 1] - off[i] > 0xFFFFFFFFull) throw ArgError("bad offsets");
+            e->remove(bytes + off[i], (uint32_t)(off[i + 1] - off[i]));
+        }
+        return TM_OK;
+    });
+}
+
 int tm_delete(tm_engine* e, const uint8_t* filter, uint32_t len) {
     if (!filter && len) return TM_EINVAL;
     return guarded(e, [&] {
@@ -1331,6 +1342,21 @@ int tm_route_add(tm_engine* e, const uint8_t* topic, uint32_t tlen, const uint8_
     if ((!topic && tlen) || (!dest && dlen)) return TM_EINVAL;
     return guarded(e, [&] {
         e->route_add(topic, tlen, dest, dlen);
+        return TM_OK;
+    });
+}
+
+int tm_route_add_batch(tm_engine* e, const uint8_t* topics, const uint64_t* topic_off, const uint8_t* dests,
+                       const uint64_t* dest_off, uint32_t n) {
+    if (n && (!topics || !topic_off || !dests || !dest_off)) return TM_EINVAL;
+    return guarded(e, [&] {
+        for (uint32_t i = 0; i < n; ++i) {
+            if (topic_off[i + 1] < topic_off[i] || topic_off[i + 1] - topic_off[i] > 0xFFFFFFFFull ||
+                dest_off[i + 1] < dest_off[i] || dest_off[i + 1] - dest_off[i] > 0xFFFFFFFFull)
+                throw ArgError("bad offsets");
+            e->route_add(topics + topic_off[i], (uint32_t)(topic_off[i + 1] - topic_off[i]), dests + dest_off[i],
+                         (uint32_t)(dest_off[i + 1] - dest_off[i]));
+        }
         return TM_OK;
     });
 }

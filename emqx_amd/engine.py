@@ -75,6 +75,12 @@ class Engine:
     def delete(self, filt: bytes):
         return self._check(self.lib.tm_delete(self.h, filt, len(filt)), "tm_delete")
 
+    def delete_many(self, buf, off):
+        n = len(off) - 1
+        buf = np.ascontiguousarray(buf, dtype=np.uint8)
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        return self._check(self.lib.tm_delete_batch(self.h, _ptr(buf), _ptr(off), n), "tm_delete_batch")
+
     def lookup(self, node_id: bytes):
         """[] or [(edge_count, topic_bytes_or_None)] like emqx_trie:lookup/1"""
         info = L.TmNodeInfo()
@@ -167,6 +173,16 @@ class Engine:
 
     def route_add(self, topic: bytes, dest: bytes):
         return self._check(self.lib.tm_route_add(self.h, topic, len(topic), dest, len(dest)), "tm_route_add")
+
+    def route_add_many(self, tbuf, toff, dbuf, doff):
+        """route i = (topic i of (tbuf, toff), dest i of (dbuf, doff))"""
+        n = len(toff) - 1
+        tbuf = np.ascontiguousarray(tbuf, dtype=np.uint8)
+        toff = np.ascontiguousarray(toff, dtype=np.uint64)
+        dbuf = np.ascontiguousarray(dbuf, dtype=np.uint8)
+        doff = np.ascontiguousarray(doff, dtype=np.uint64)
+        return self._check(self.lib.tm_route_add_batch(self.h, _ptr(tbuf), _ptr(toff), _ptr(dbuf), _ptr(doff), n),
+                           "tm_route_add_batch")
 
     def route_del(self, topic: bytes, dest: bytes):
         return self._check(self.lib.tm_route_del(self.h, topic, len(topic), dest, len(dest)), "tm_route_del")

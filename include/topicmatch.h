@@ -102,6 +102,10 @@ int tm_insert_batch_shard(tm_engine* e, const uint8_t* bytes, const uint64_t* of
  * Unknown filter = no-op (TM_OK). */
 int tm_delete(tm_engine* e, const uint8_t* filter, uint32_t len);
 
+/* Bulk form of tm_delete over n concatenated filters (the router's batch
+ * delete, src/emqx_router.erl:243-250), applied in order. */
+int tm_delete_batch(tm_engine* e, const uint8_t* bytes, const uint64_t* off, uint32_t n);
+
 /* emqx_trie:lookup/1 — src/emqx_trie.erl:83-84.  node_id is the full path
  * binary (emqx_topic:join of the words).  TM_ENOENT when the node is absent. */
 int tm_lookup(tm_engine* e, const uint8_t* node_id, uint32_t len, tm_node_info* out);
@@ -179,6 +183,11 @@ int tm_shard_merge(tm_engine* e, uint32_t n_shards, uint32_t m, const uint32_t* 
  * route yet. */
 int tm_route_add(tm_engine* e, const uint8_t* topic, uint32_t tlen, const uint8_t* dest, uint32_t dlen);
 
+/* Bulk tm_route_add: route i = (topic [topic_off[i], topic_off[i+1]),
+ * dest [dest_off[i], dest_off[i+1])), applied in order. */
+int tm_route_add_batch(tm_engine* e, const uint8_t* topics, const uint64_t* topic_off, const uint8_t* dests,
+                       const uint64_t* dest_off, uint32_t n);
+
 /* emqx_router del_route — handle_cast({del_route, Route}) :165-187,
  * del_trie_route/1 :252-260, del_direct_route/1 :240-241: removes the route;
  * a wildcard topic leaves the trie (tm_delete) with its last route.  An
@@ -216,6 +225,43 @@ int tm_match_routes_batch_device(tm_engine* e, const uint8_t* d_topic_bytes, con
                                  uint32_t n, uint64_t topic_bytes, uint32_t* d_out_count, uint64_t* d_out_off,
                                  uint32_t* d_out_src, uint32_t* d_out_dest, uint64_t out_cap, uint64_t* d_total,
                                  void* hip_stream);
+
+/* ---- publish micro-batcher (emqx_amd/csrc/batcher.cpp) -----
+ * emqx_broker:publish/1 (src/emqx_broker.erl:148-157) matches one topic per
+ * call in the publisher's process.  The NIF instead submits the topic here
+ * and returns at once; a worker thread seals a batch at max_topics /
+ * max_bytes, or deadline_us after its first topic, runs it on the GPU
+ * (tm_match_batch, or tm_match_routes_batch with TM_BATCHER_ROUTES) and calls
+ * done() once per topic, in submission order, from the worker thread.  The
+ * id / dest arrays are valid only during the callback (the NIF copies them
+ * into a term and enif_send()s it).  status != TM_OK: ids are null. */
+#define TM_BATCHER_ROUTES 1u   /* results are match_routes/1 (src ids + dest ids) */
+
+typedef struct tm_batcher tm_batcher;
+typedef struct tm_batcher_config {
+    uint32_t max_topics;      /* seal at this many topics (0 = 65536)            */
+    uint32_t deadline_us;     /* seal this long after the first topic (0 = 200)  */
+    uint64_t max_bytes;       /* seal at this many topic bytes (0 = 64 MiB)      */
+    uint32_t flags;           /* TM_BATCHER_ROUTES                              */
+    uint32_t reserved;
+} tm_batcher_config;
+typedef struct tm_batcher_stats {
+    uint64_t batches, topics, results, max_batch;
+    uint64_t size_seals, deadline_seals, failed_batches;
+} tm_batcher_stats;
+/* ids: filter ids (match/1) or route sources (match_routes/1); dests: route
+ * dest ids or null; n: list length */
+typedef void (*tm_batch_done_fn)(void* ctx, uint64_t ticket, int status, const uint32_t* ids,
+                                 const uint32_t* dests, uint32_t n);
+
+int  tm_batcher_open(tm_engine* e, const tm_batcher_config* cfg, tm_batcher** out);
+int  tm_batcher_submit(tm_batcher* b, const uint8_t* topic, uint32_t len, tm_batch_done_fn done, void* ctx,
+                       uint64_t* ticket_out);
+/* seal the open batch and wait until every submitted topic has completed */
+int  tm_batcher_flush(tm_batcher* b);
+int  tm_batcher_get_stats(tm_batcher* b, tm_batcher_stats* out);
+/* flush, then stop the worker */
+void tm_batcher_close(tm_batcher* b);
 
 /* Engine knobs (the app-env analogue of SURVEY §5 config):
  *   "xcdq"     1 = per-XCD dequeue heads over contiguous ranges of the batch

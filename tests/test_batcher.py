@@ -1,0 +1,44 @@
+"""Micro-batcher plumbing on CPU (tm_batcher_*): a host-only engine cannot
+match, so every submitted topic must complete with TM_EDEVICE (the match
+path fails loudly, no CPU fallback); sealing by size and by deadline; flush
+and close with requests in flight."""
+import threading
+import time
+
+from emqx_amd import Engine, _lib
+from emqx_amd.batcher import Batcher
+
+
+def test_batcher_fails_loudly_without_gpu_and_seals():
+    e = Engine(device=-1)
+    e.insert(b"a/+")
+    b = Batcher(e, max_topics=100, deadline_us=300)
+    got = []
+    lock = threading.Lock()
+
+    def cb(status, ids, dests):
+        with lock:
+            got.append((status, ids))
+
+    def producer(k):
+        for i in range(250):
+            b.submit(b"a/%d" % (k * 1000 + i), cb)
+    ts = [threading.Thread(target=producer, args=(k,)) for k in range(4)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    b.flush()
+    assert len(got) == 1000
+    assert all(s == _lib.TM_EDEVICE and ids is None for s, ids in got)
+    st = b.stats()
+    assert st["topics"] == 1000 and st["failed_batches"] == st["batches"]
+    assert st["size_seals"] >= 9 and st["max_batch"] <= 100
+    b.submit(b"x", cb)           # a lone topic is sealed by the deadline, no flush
+    for _ in range(200):
+        if len(got) == 1001:
+            break
+        time.sleep(0.01)
+    assert len(got) == 1001 and b.stats()["deadline_seals"] >= 1
+    b.close()
+    e.close()
