@@ -9,7 +9,7 @@ TMDEFS  ?=
 HIPFLAGS = --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -Wall -Wno-unused-result $(TMDEFS)
 BUILD   := build
 
-all: emqx_amd/libtopicmatch.so emqx_amd/libtmwork.so oracle/liboracle.so
+all: emqx_amd/libtopicmatch.so emqx_amd/libtmwork.so oracle/liboracle.so tools/ubench/batcher_bench
 
 $(BUILD):
 	mkdir -p $(BUILD)
@@ -50,3 +50,7 @@ nif: emqx_amd/libtopicmatch.so
 	$(CC) -O2 -fPIC -shared -I$(ERL_INCLUDE) emqx_amd/csrc/emqx_trie_nif.c -Lemqx_amd -ltopicmatch \
 	  -Wl,-rpath,'$$ORIGIN' -o emqx_amd/emqx_trie_nif.so
 .PHONY: nif
+
+# micro-batcher benchmark (single-topic submits from producer threads)
+tools/ubench/batcher_bench: tools/ubench/batcher_bench.cpp emqx_amd/libtopicmatch.so emqx_amd/libtmwork.so include/topicmatch.h
+	$(CXX) -O2 -std=c++17 -pthread $< -Lemqx_amd -ltopicmatch -ltmwork -Wl,-rpath,'$$ORIGIN/../../emqx_amd' -o $@

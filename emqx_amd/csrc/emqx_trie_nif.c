@@ -13,6 +13,14 @@
  *   emqx_trie_nif:commit(Engine)              -> {ok, Epoch} (transaction commit -> HBM image)
  *   emqx_trie_nif:match(Engine, Topic)        -> [Filter]    emqx_trie:match/1   (src/emqx_trie.erl:77-79)
  *   emqx_trie_nif:match_many(Engine, [Topic]) -> [[Filter]]  one GPU batch for many publishes
+ *   emqx_trie_nif:match_async(Engine, Topic)  -> Ref; later {Ref, [Filter]} | {Ref, {error, R}}
+ *                                                           (micro-batched: tm_batcher_*, H5)
+ *   emqx_trie_nif:route_add(Engine, Topic, DestBin) -> ok   emqx_router add_route (src/emqx_router.erl:153-163)
+ *   emqx_trie_nif:route_del(Engine, Topic, DestBin) -> ok   emqx_router del_route (:165-187)
+ *   emqx_trie_nif:match_routes_async(Engine, Topic) -> Ref; later {Ref, [{To, DestBin}]}
+ *                                                           emqx_router:match_routes/1 (:116-118)
+ * DestBin is term_to_binary(Dest) (node() or {Group, node()}): opaque to the
+ * engine, binary_to_term'd by the Erlang wrapper.
  *
  * Conventions: bad input -> badarg; engine errors ->
  * {error, Atom}; the engine handle is a resource; GPU calls run on dirty IO
@@ -28,7 +36,18 @@ static ErlNifResourceType* ENGINE_RT = NULL;
 typedef struct {
     tm_engine* e;
     ErlNifMutex* mu;
+    tm_batcher* filters_b;   /* micro-batcher for match_async (emqx_trie:match/1)          */
+    tm_batcher* routes_b;    /* micro-batcher for match_routes_async (match_routes/1)      */
 } engine_res;
+
+/* one in-flight async request: where the reply goes */
+typedef struct {
+    ErlNifPid pid;
+    ErlNifEnv* env;      /* process-independent env holding Ref and the reply */
+    ERL_NIF_TERM ref;
+    engine_res* r;       /* kept alive until the reply is sent */
+    ERL_NIF_TERM topic;  /* copy of the topic (route source TM_ROUTE_TOPIC) */
+} async_req;
 
 static ERL_NIF_TERM atom(ErlNifEnv* env, const char* name) {
     ERL_NIF_TERM a;
@@ -51,6 +70,8 @@ static ERL_NIF_TERM error_tuple(ErlNifEnv* env, int code) {
 static void engine_dtor(ErlNifEnv* env, void* obj) {
     (void)env;
     engine_res* r = (engine_res*)obj;
+    if (r->filters_b) tm_batcher_close(r->filters_b);
+    if (r->routes_b) tm_batcher_close(r->routes_b);
     if (r->e) tm_close(r->e);
     if (r->mu) enif_mutex_destroy(r->mu);
 }
@@ -74,8 +95,17 @@ static ERL_NIF_TERM nif_open(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]
     cfg.device = dev;
     engine_res* r = (engine_res*)enif_alloc_resource(ENGINE_RT, sizeof(engine_res));
     r->e = NULL;
+    r->filters_b = r->routes_b = NULL;
     r->mu = enif_mutex_create("tm_engine");
     int rc = tm_open(&cfg, &r->e);
+    if (rc == TM_OK) {
+        /* batches sealed at 64K topics or 200 us after their first topic */
+        tm_batcher_config bc;
+        memset(&bc, 0, sizeof(bc));
+        rc = tm_batcher_open(r->e, &bc, &r->filters_b);
+        bc.flags = TM_BATCHER_ROUTES;
+        if (rc == TM_OK) rc = tm_batcher_open(r->e, &bc, &r->routes_b);
+    }
     if (rc != TM_OK) {
         enif_release_resource(r);
         return error_tuple(env, rc);
@@ -216,6 +246,89 @@ static ERL_NIF_TERM nif_match_many(ErlNifEnv* env, int argc, const ERL_NIF_TERM 
     return match_list(env, r, argv[1], n, 0);
 }
 
+/* ---- async (micro-batched) match: the batcher's worker thread calls back ---- */
+static void async_done(void* ctx, uint64_t ticket, int status, const uint32_t* ids, const uint32_t* dests,
+                       uint32_t n) {
+    (void)ticket;
+    async_req* q = (async_req*)ctx;
+    ErlNifEnv* env = q->env;
+    ERL_NIF_TERM res;
+    if (status != TM_OK) {
+        res = error_tuple(env, status);
+    } else {
+        ERL_NIF_TERM* cells = (ERL_NIF_TERM*)enif_alloc(sizeof(ERL_NIF_TERM) * (n ? n : 1));
+        for (uint32_t k = 0; k < n; ++k) {
+            ERL_NIF_TERM to = ids[k] == TM_ROUTE_TOPIC ? q->topic : filter_binary(env, q->r->e, ids[k]);
+            if (dests) {
+                uint32_t dl = 0;
+                const uint8_t* dp = tm_dest_bytes(q->r->e, dests[k], &dl);
+                ERL_NIF_TERM db;
+                unsigned char* d = enif_make_new_binary(env, dl, &db);
+                if (dl) memcpy(d, dp, dl);
+                cells[k] = enif_make_tuple2(env, to, db);
+            } else {
+                cells[k] = to;
+            }
+        }
+        res = enif_make_list_from_array(env, cells, n);
+        enif_free(cells);
+    }
+    enif_send(NULL, &q->pid, env, enif_make_tuple2(env, q->ref, res));
+    enif_free_env(env);
+    enif_release_resource(q->r);
+    enif_free(q);
+}
+
+static ERL_NIF_TERM submit_async(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[], int routes) {
+    engine_res* r;
+    ErlNifBinary b;
+    if (argc != 2 || !get_engine(env, argv[0], &r) || !enif_inspect_binary(env, argv[1], &b))
+        return enif_make_badarg(env);
+    async_req* q = (async_req*)enif_alloc(sizeof(async_req));
+    if (!q) return error_tuple(env, TM_ENOMEM);
+    q->env = enif_alloc_env();
+    ERL_NIF_TERM ref = enif_make_ref(env);
+    q->ref = enif_make_copy(q->env, ref);
+    q->topic = enif_make_copy(q->env, argv[1]);
+    q->r = r;
+    enif_self(env, &q->pid);
+    enif_keep_resource(r);
+    int rc = tm_batcher_submit(routes ? r->routes_b : r->filters_b, b.data, (uint32_t)b.size, async_done, q, NULL);
+    if (rc != TM_OK) {
+        enif_release_resource(r);
+        enif_free_env(q->env);
+        enif_free(q);
+        return error_tuple(env, rc);
+    }
+    return ref;   /* the caller blocks in receive {Ref, Result} */
+}
+
+static ERL_NIF_TERM nif_match_async(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    return submit_async(env, argc, argv, 0);
+}
+static ERL_NIF_TERM nif_match_routes_async(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    return submit_async(env, argc, argv, 1);
+}
+
+static ERL_NIF_TERM nif_route_op(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[], int add) {
+    engine_res* r;
+    ErlNifBinary t, d;
+    if (argc != 3 || !get_engine(env, argv[0], &r) || !enif_inspect_binary(env, argv[1], &t) ||
+        !enif_inspect_binary(env, argv[2], &d))
+        return enif_make_badarg(env);
+    enif_mutex_lock(r->mu);
+    int rc = add ? tm_route_add(r->e, t.data, (uint32_t)t.size, d.data, (uint32_t)d.size)
+                 : tm_route_del(r->e, t.data, (uint32_t)t.size, d.data, (uint32_t)d.size);
+    enif_mutex_unlock(r->mu);
+    return rc == TM_OK ? atom(env, "ok") : error_tuple(env, rc);
+}
+static ERL_NIF_TERM nif_route_add(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    return nif_route_op(env, argc, argv, 1);
+}
+static ERL_NIF_TERM nif_route_del(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    return nif_route_op(env, argc, argv, 0);
+}
+
 static ErlNifFunc funcs[] = {
     {"open", 1, nif_open, 0},
     {"insert", 2, nif_insert, 0},
@@ -224,6 +337,10 @@ static ErlNifFunc funcs[] = {
     {"commit", 1, nif_commit, ERL_NIF_DIRTY_JOB_IO_BOUND},
     {"match", 2, nif_match, ERL_NIF_DIRTY_JOB_IO_BOUND},
     {"match_many", 2, nif_match_many, ERL_NIF_DIRTY_JOB_IO_BOUND},
+    {"match_async", 2, nif_match_async, 0},                 /* returns at once: normal scheduler */
+    {"match_routes_async", 2, nif_match_routes_async, 0},
+    {"route_add", 3, nif_route_add, 0},
+    {"route_del", 3, nif_route_del, 0},
 };
 
 ERL_NIF_INIT(emqx_trie_nif, funcs, load, NULL, NULL, NULL)
