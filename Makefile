@@ -27,9 +27,12 @@ $(BUILD)/routes.o: emqx_amd/csrc/routes.hip emqx_amd/csrc/kernels.h emqx_amd/csr
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(BUILD)/batcher.o: emqx_amd/csrc/batcher.cpp include/topicmatch.h | $(BUILD)
-	$(CXX) -O2 -fPIC -std=c++17 -Wall -pthread -c $< -o $@
+	$(HIPCC) -O2 -fPIC -std=c++17 -Wall -pthread -c $< -o $@
 
-emqx_amd/libtopicmatch.so: $(BUILD)/kernels.o $(BUILD)/shard.o $(BUILD)/routes.o $(BUILD)/engine.o $(BUILD)/batcher.o
+$(BUILD)/acl.o: emqx_amd/csrc/acl.hip include/topicmatch.h | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+emqx_amd/libtopicmatch.so: $(BUILD)/kernels.o $(BUILD)/shard.o $(BUILD)/routes.o $(BUILD)/engine.o $(BUILD)/batcher.o $(BUILD)/acl.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -pthread $^ -o $@
 
 emqx_amd/libtmwork.so: emqx_amd/csrc/workload.c

@@ -66,6 +66,7 @@ SIGNATURES = [
     ("tm_delete_batch", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32]),
     ("tm_lookup", ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.POINTER(TmNodeInfo)]),
     ("tm_commit", ctypes.c_int, [ctypes.c_void_p, c_u64p]),
+    ("tm_engine_device", ctypes.c_int, [ctypes.c_void_p]),
     ("tm_filter_count", ctypes.c_uint64, [ctypes.c_void_p]),
     ("tm_node_count", ctypes.c_uint64, [ctypes.c_void_p]),
     ("tm_image_bytes", ctypes.c_uint64, [ctypes.c_void_p]),
@@ -110,6 +111,15 @@ SIGNATURES = [
     ("tm_batcher_flush", ctypes.c_int, [ctypes.c_void_p]),
     ("tm_batcher_get_stats", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(TmBatcherStats)]),
     ("tm_batcher_close", None, [ctypes.c_void_p]),
+    ("tm_acl_open", ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+    ("tm_acl_close", None, [ctypes.c_void_p]),
+    ("tm_acl_rule_begin", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_uint32]),
+    ("tm_acl_who", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_uint32,
+                                  ctypes.c_uint32]),
+    ("tm_acl_topic", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_uint32]),
+    ("tm_acl_rule_end", ctypes.c_int, [ctypes.c_void_p]),
+    ("tm_acl_rule_count", ctypes.c_int, [ctypes.c_void_p]),
+    ("tm_acl_check_batch", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32] + [ctypes.c_void_p] * 13),
     ("tm_last_stats", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(TmBatchStats)]),
     ("tm_set_timing", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     ("tm_last_kernel_times", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_char_p),

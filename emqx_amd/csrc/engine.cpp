@@ -203,6 +203,12 @@ struct tm_engine {
         w_ws;
     uint32_t stage_k = 512;   // TM_STAGE_K: ids staged per topic before a re-walk (rows are
                               // written sparsely: HBM footprint, not traffic)
+    uint32_t stage_k_min = 512;         // option "stage_k"
+    int stage_auto = 1;                 // option "stage_auto": grow K to the largest list seen (no re-walks)
+    uint64_t* h_maxc = nullptr;         // pinned: largest match count of the last walk
+    hipEvent_t maxc_ev = nullptr;
+    bool maxc_pending = false;
+    static constexpr size_t STAGE_BUDGET = 16ull << 30;  // stage-row footprint cap (bytes, of 288 GB HBM)
     hipEvent_t last_match_done = nullptr;
     bool match_in_flight = false;
     bool stats_enabled = false, timing_enabled = false;
@@ -219,7 +225,10 @@ struct tm_engine {
         if (const char* v = std::getenv("TM_XCDQ")) xcdq = std::atoi(v) ? 1 : 0;
         if (const char* v = std::getenv("TM_STAGE_K")) {
             long k = std::atol(v);
-            if (k >= 4 && k <= 4096 && !(k & 3)) stage_k = (uint32_t)k;
+            if (k >= 4 && k <= 4096 && !(k & 3)) {
+                stage_k = stage_k_min = (uint32_t)k;
+                stage_auto = 0;
+            }
         }
         dict.assign(1024, DictSlot{0, WORD_NONE, 0});
         nodes.reserve(1024);
@@ -943,9 +952,31 @@ struct tm_engine {
 
     // the whole hot path of one batch, stream-ordered on st: CSR of ordered
     // filter ids (ids past cap are dropped; *total always exact)
+    // stage rows sized to the largest list of the previous walk (read back
+    // asynchronously), within STAGE_BUDGET: fan-out beyond K costs a re-walk
+    void adapt_stage_k(uint32_t n, bool keys) {
+        if (!stage_auto || !maxc_pending || hipEventQuery(maxc_ev) != hipSuccess) return;
+        maxc_pending = false;
+        uint64_t want = stage_k_min;
+        while (want < *h_maxc && want < 4096) want <<= 1;
+        uint64_t k = stage_k;
+        const uint64_t per = (uint64_t)n * (keys ? 12 : 4);
+        while (k < want && per * (k << 1) <= STAGE_BUDGET) k <<= 1;
+        stage_k = (uint32_t)k;
+    }
+    void record_maxc(hipStream_t st) {
+        if (!stage_auto) return;
+        if (!h_maxc) HIPCHK(hipHostMalloc((void**)&h_maxc, 64, hipHostMallocDefault));
+        if (!maxc_ev) HIPCHK(hipEventCreateWithFlags(&maxc_ev, hipEventDisableTiming));
+        HIPCHK(hipMemcpyAsync(h_maxc, w_ws.as<uint64_t>() + QWS_MAXC, 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipEventRecord(maxc_ev, st));
+        maxc_pending = true;
+    }
+
     void run_batch(const uint8_t* bytes, const uint64_t* off, uint32_t n, uint64_t nbytes, uint32_t* counts,
                    uint64_t* out_off, uint32_t* ids, uint64_t cap, uint64_t* total, hipStream_t st,
                    uint64_t* keys = nullptr) {
+        adapt_stage_k(n, keys != nullptr);
         ensure_workspace(n, nbytes);
         if (keys) w_kstage.ensure(((size_t)n * stage_k + 4) * 8);
         ImageView im = view();
@@ -970,6 +1001,7 @@ struct tm_engine {
         qb.ws = w_ws.as<unsigned long long>();
         HIPCHK(launch_queue(stats_enabled, xcdq != 0, im, bytes, off, n, qb, stage_k, counts, out_off, ids, keys, cap,
                             total, sp, st, timing_enabled ? marks : nullptr, walk_bpc, hist_enabled != 0));
+        record_maxc(st);
         if (timing_enabled)
             for (int i = 0; i < 4; ++i) ev_pending.push_back(ev_cur[i]);
     }
@@ -1146,6 +1178,8 @@ void tm_close(tm_engine* e) {
                 (void)hipEventDestroy(k.b);
             }
         if (e->last_match_done) (void)hipEventDestroy(e->last_match_done);
+        if (e->maxc_ev) (void)hipEventDestroy(e->maxc_ev);
+        if (e->h_maxc) (void)hipHostFree(e->h_maxc);
         if (e->stream) (void)hipStreamDestroy(e->stream);
     }
     delete e;
@@ -1258,6 +1292,8 @@ int tm_commit(tm_engine* e, uint64_t* epoch_out) {
 
 uint64_t tm_filter_count(tm_engine* e) { return e ? e->live_filters : 0; }
 uint64_t tm_node_count(tm_engine* e) { return e ? e->live_nodes : 0; }
+int tm_engine_device(tm_engine* e) { return e ? e->device : -1; }
+
 uint64_t tm_image_bytes(tm_engine* e) {
     if (!e) return 0;
     return e->nodes.size() * sizeof(Node) + e->edges.size() * sizeof(EdgeSlot) + e->dict.size() * sizeof(DictSlot) +
@@ -1593,7 +1629,13 @@ int tm_set_option(tm_engine* e, const char* name, int64_t value) {
         }
         if (!std::strcmp(name, "stage_k")) {
             if (value < 4 || value > 4096 || (value & 3)) return TM_EINVAL;
-            e->stage_k = (uint32_t)value;
+            e->stage_k = e->stage_k_min = (uint32_t)value;
+            e->stage_auto = 0;   // an explicit K is kept (set "stage_auto" after it to grow from it)
+            return TM_OK;
+        }
+        if (!std::strcmp(name, "stage_auto")) {
+            if (value < 0 || value > 1) return TM_EINVAL;
+            e->stage_auto = (int)value;
             return TM_OK;
         }
         return TM_EINVAL;

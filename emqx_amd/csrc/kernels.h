@@ -10,6 +10,7 @@ namespace tmx {
 constexpr uint32_t WREG = 16;        // topic levels kept in VGPRs / LDS path slots; longer
                                      // topics keep their path in global scratch
 constexpr size_t QWS_BYTES = 1024;   // queue heads: 8 ranges x 128 B
+constexpr size_t QWS_MAXC = 120;     // u64 slot of ws: the batch's largest match count
 constexpr size_t STATS_BYTES = 512;  // 8 totals + per-level diagnostic histogram
 
 // per-batch device workspace of the queue pipeline

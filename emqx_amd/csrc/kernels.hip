@@ -469,6 +469,7 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
     WalkStats st;
     if (STATS) st.hist = hist;
     uint64_t lev_sum = 0, match_sum = 0;
+    uint32_t maxc = 0;                 // largest list of this lane's topics (stage-row sizing)
     for (;;) {
         const bool need = (my == NO_TOPIC) && !drained;
         const uint64_t m = __ballot(need);
@@ -570,9 +571,15 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
             em.flush();
             counts[my] = em.cnt;
             match_sum += em.cnt;
+            maxc = em.cnt > maxc ? em.cnt : maxc;
             my = NO_TOPIC;
         }
     }
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint32_t y = (uint32_t)__shfl_xor((int)maxc, o, 64);
+        maxc = y > maxc ? y : maxc;
+    }
+    if (lane == 0 && maxc) atomicMax(ws + QWS_MAXC, (unsigned long long)maxc);
     wave_stats_add<STATS>(stats, lev_sum, match_sum, st);
 }
 
@@ -598,7 +605,24 @@ tm_copy_out(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const ui
     lds_inc[threadIdx.x] = (uint32_t)(ex + c);
     __syncthreads();
     const uint64_t base = out_off[t0];
-    for (uint64_t j = threadIdx.x; j < agg; j += BLOCK) {
+    if (agg >= 64ull * tn) {
+        // high fan-out block: one wave per topic, its lanes stride the row
+        // (no per-id search); output j of a topic with ct ids is row slot
+        // K-ct+j, staged for j >= ct-K
+        const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+        for (uint32_t lt = w; lt < tn; lt += BLOCK / 64) {
+            const uint32_t prev = lt ? lds_inc[lt - 1] : 0u;
+            const uint32_t ct = lds_inc[lt] - prev;
+            const uint64_t ob = base + prev;
+            const uint64_t row = (uint64_t)(t0 + lt) * K + K - ct;   // + j: slot of output j
+            for (uint32_t j = (ct > K ? ct - K : 0u) + lane; j < ct; j += 64) {
+                if (ob + j < out_cap) {
+                    out[ob + j] = stage[row + j];
+                    if (KEYS) kout[ob + j] = kstage[row + j];
+                }
+            }
+        }
+    } else for (uint64_t j = threadIdx.x; j < agg; j += BLOCK) {
         uint32_t lo = 0, hi = tn - 1;
         while (lo < hi) {
             const uint32_t mid = (lo + hi) >> 1;

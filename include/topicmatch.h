@@ -114,6 +114,9 @@ int tm_lookup(tm_engine* e, const uint8_t* node_id, uint32_t len, tm_node_info* 
  * src/emqx_router.erl:264-268).  tm_match_* commit implicitly. */
 int tm_commit(tm_engine* e, uint64_t* epoch_out);
 
+/* HIP device ordinal of the engine (-1: host-only) */
+int tm_engine_device(tm_engine* e);
+
 /* number of filters currently in the trie (nodes with topic =/= undefined) */
 uint64_t tm_filter_count(tm_engine* e);
 /* trie nodes / literal edges of the image (for sizing reports) */
@@ -239,7 +242,7 @@ int tm_match_routes_batch_device(tm_engine* e, const uint8_t* d_topic_bytes, con
 
 typedef struct tm_batcher tm_batcher;
 typedef struct tm_batcher_config {
-    uint32_t max_topics;      /* seal at this many topics (0 = 65536)            */
+    uint32_t max_topics;      /* seal at this many pending topics (0 = 65536); a seal takes every pending topic */
     uint32_t deadline_us;     /* seal this long after the first topic (0 = 200)  */
     uint64_t max_bytes;       /* seal at this many topic bytes (0 = 64 MiB)      */
     uint32_t flags;           /* TM_BATCHER_ROUTES                              */
@@ -263,6 +266,52 @@ int  tm_batcher_get_stats(tm_batcher* b, tm_batcher_stats* out);
 /* flush, then stop the worker */
 void tm_batcher_close(tm_batcher* b);
 
+/* ---- batched ACL checks (emqx_amd/csrc/acl.hip) ---------------
+ * The internal ACL module (src/emqx_acl_internal.erl) keeps the compiled
+ * rules of etc/acl.conf and answers check_acl({Credentials, PubSub, Topic})
+ * with the first matching rule of that access type (match/3, :63-87).  A
+ * tm_acl holds the rules in order, built like emqx_access_rule:compile/1
+ * (src/emqx_access_rule.erl:38-75):
+ *   tm_acl_rule_begin(allow, access)   {allow|deny, Who, Access, Topics} / {allow|deny, all}
+ *   tm_acl_who(kind, arg, len, prefix) Who: all | {client, C} | {user, U} | {client, all} |
+ *                                      {user, all} | {ipaddr, "a.b.c.d[/n]"} (prefix = n, 0 = host);
+ *                                      {'and' | 'or', [...]}: AND/OR, the conditions, END
+ *   tm_acl_topic(eq, topic, len)       a topic filter, or {eq, Topic}; "%c"/"%u" levels make a
+ *                                      pattern (feed_var/3, :136-149)
+ *   tm_acl_rule_end()
+ * tm_acl_check_batch evaluates n checks on the GPU: out_result[i] = 1 allow,
+ * 0 deny, -1 nomatch (the module's ignore); out_rule[i] = index of the
+ * matching rule (or 0xFFFFFFFF).  Credentials: client id / username bytes
+ * with a defined flag (undefined = the atom), peer address 16 B per check
+ * with family 4 / 6 (0 = no peername); peers may be NULL.  Topics are
+ * matched as word lists (emqx_access_rule:match_topic/2: no '$' rule). */
+#define TM_ACL_ALL        0u   /* {allow|deny, all}: matches any check */
+#define TM_ACL_PUBLISH    1u
+#define TM_ACL_SUBSCRIBE  2u
+#define TM_ACL_PUBSUB     3u
+#define TM_ACL_WHO_ALL        0u
+#define TM_ACL_WHO_CLIENT     1u
+#define TM_ACL_WHO_USER       2u
+#define TM_ACL_WHO_CLIENT_ALL 3u
+#define TM_ACL_WHO_USER_ALL   4u
+#define TM_ACL_WHO_IPADDR     5u
+#define TM_ACL_WHO_AND        6u
+#define TM_ACL_WHO_OR         7u
+#define TM_ACL_WHO_END        8u
+typedef struct tm_acl tm_acl;
+int  tm_acl_open(int device, tm_acl** out);
+void tm_acl_close(tm_acl* a);
+int  tm_acl_rule_begin(tm_acl* a, int allow, uint32_t access);
+int  tm_acl_who(tm_acl* a, uint32_t kind, const uint8_t* arg, uint32_t len, uint32_t prefix);
+int  tm_acl_topic(tm_acl* a, int eq, const uint8_t* topic, uint32_t len);
+int  tm_acl_rule_end(tm_acl* a);
+int  tm_acl_rule_count(tm_acl* a);
+int  tm_acl_check_batch(tm_acl* a, uint32_t n, const uint8_t* access, const uint8_t* topics,
+                        const uint64_t* topic_off, const uint8_t* client_ids, const uint64_t* client_off,
+                        const uint8_t* client_defined, const uint8_t* usernames, const uint64_t* user_off,
+                        const uint8_t* user_defined, const uint8_t* peers, const uint8_t* peer_family,
+                        int8_t* out_result, uint32_t* out_rule);
+
 /* Engine knobs (the app-env analogue of SURVEY §5 config):
  *   "xcdq"     1 = per-XCD dequeue heads over contiguous ranges of the batch
  *              (default), 0 = one global head
@@ -271,7 +320,14 @@ void tm_batcher_close(tm_batcher* b);
  *   "layout"   1 = renumber nodes in DFS preorder on commit once >= 1/4 of
  *              the live nodes are new (default), 0 = keep insertion order,
  *              2 = renumber on every commit
- *   "stage_k"  ids staged per topic before a fan-out re-walk (4..4096, % 4 == 0)
+ *   "stage_k"  ids staged per topic before a fan-out re-walk (4..4096, % 4 == 0);
+ *              setting it fixes K (turns "stage_auto" off)
+ *   "stage_auto" 1 = grow K to the largest list of the previous walk, within
+ *              a 16 GiB stage footprint (default), 0 = fixed K
+ *   "split"    1 = walk reads separate inner / leaf half arrays (default),
+ *              0 = interleaved 32 B records
+ *   "hot_levels" depths laid out level by level first at relayout (0..16,
+ *              default 4; 0 = DFS preorder throughout); forces a relayout
  * TM_EINVAL for unknown names / values. */
 int tm_set_option(tm_engine* e, const char* name, int64_t value);
 

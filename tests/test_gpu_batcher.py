@@ -52,7 +52,7 @@ def test_batcher_results_equal_batch_api(gpu_device, routes):
     b.flush()
     st = b.stats()
     b.close()
-    assert st["topics"] == len(topics) and st["failed_batches"] == 0 and st["batches"] >= 14
+    assert st["topics"] == len(topics) and st["failed_batches"] == 0 and st["batches"] >= 5
     for t in range(len(topics)):
         ids, dests = got[t]
         assert [int(x) for x in want[t][0]] == ids, t

@@ -76,7 +76,7 @@ int main(int argc, char** argv) {
     bool first = true;
     for (uint32_t dl : deadlines) {
         tm_batcher_config bc{};
-        bc.max_topics = 262144;
+        bc.max_topics = 65536;
         bc.deadline_us = dl;
         tm_batcher* b;
         if (tm_batcher_open(e, &bc, &b) != TM_OK) return 1;
