@@ -7,9 +7,10 @@ ARCH    ?= gfx950
 CC      ?= gcc
 TMDEFS  ?=
 HIPFLAGS = --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -Wall -Wno-unused-result $(TMDEFS)
-BUILD   := build
+BUILD   ?= build
+LIBOUT  ?= emqx_amd/libtopicmatch.so
 
-all: emqx_amd/libtopicmatch.so emqx_amd/libtmwork.so oracle/liboracle.so tools/ubench/batcher_bench
+all: $(LIBOUT) emqx_amd/libtmwork.so oracle/liboracle.so tools/ubench/batcher_bench
 
 $(BUILD):
 	mkdir -p $(BUILD)
@@ -19,6 +20,13 @@ $(BUILD)/kernels.o: emqx_amd/csrc/kernels.hip emqx_amd/csrc/kernels.h emqx_amd/c
 
 $(BUILD)/engine.o: emqx_amd/csrc/engine.cpp emqx_amd/csrc/kernels.h emqx_amd/csrc/image.h include/topicmatch.h | $(BUILD)
 	$(HIPCC) -O3 -fPIC -std=c++17 -Wall $(TMDEFS) -c $< -o $@
+
+# A/B builds of compile-time variants: make variant TAG=x TMDEFS="-D..." ->
+# emqx_amd/variants/libtopicmatch_x.so (bench.py --lib)
+variant:
+	mkdir -p emqx_amd/variants
+	$(MAKE) BUILD=build_$(TAG) LIBOUT=emqx_amd/variants/libtopicmatch_$(TAG).so TMDEFS="$(TMDEFS)" emqx_amd/variants/libtopicmatch_$(TAG).so
+.PHONY: variant
 
 $(BUILD)/shard.o: emqx_amd/csrc/shard.hip emqx_amd/csrc/kernels.h emqx_amd/csrc/image.h | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
@@ -32,7 +40,7 @@ $(BUILD)/batcher.o: emqx_amd/csrc/batcher.cpp include/topicmatch.h | $(BUILD)
 $(BUILD)/acl.o: emqx_amd/csrc/acl.hip include/topicmatch.h | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-emqx_amd/libtopicmatch.so: $(BUILD)/kernels.o $(BUILD)/shard.o $(BUILD)/routes.o $(BUILD)/engine.o $(BUILD)/batcher.o $(BUILD)/acl.o
+$(LIBOUT): $(BUILD)/kernels.o $(BUILD)/shard.o $(BUILD)/routes.o $(BUILD)/engine.o $(BUILD)/batcher.o $(BUILD)/acl.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -pthread $^ -o $@
 
 emqx_amd/libtmwork.so: emqx_amd/csrc/workload.c

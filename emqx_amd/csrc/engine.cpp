@@ -161,9 +161,21 @@ struct tm_engine {
     std::vector<NodeAux> aux;
     std::vector<uint32_t> free_nodes;
     size_t live_nodes = 0;
-    std::vector<EdgeSlot> edges;
-    size_t edge_used = 0;
-    Dirty node_dirty, edge_dirty;
+    // literal / '#' edges: parents with id < hot_limit (the level-by-level
+    // laid-out top of the trie, depths < hot_edge_depth) keep theirs in a
+    // small `hot` table, so the probes every topic makes near the root hit a
+    // few MB instead of lines scattered over the whole table
+    struct EdgeTable {
+        std::vector<EdgeSlot> slots;
+        size_t used = 0;
+        Dirty dirty;
+    };
+    EdgeTable cold, hot;
+    uint32_t hot_limit = 0;
+    uint32_t hot_edge_depth = 0;      // option "hot_edges": parents of depth < D use `hot` (0 = off; A/B: no gain at C3)
+    Dirty node_dirty;
+    EdgeTable& tab(uint32_t parent) { return parent < hot_limit ? hot : cold; }
+    const EdgeTable& tab(uint32_t parent) const { return parent < hot_limit ? hot : cold; }
 
     // ---- filter registry ----
     std::vector<uint8_t> filter_arena;
@@ -172,7 +184,7 @@ struct tm_engine {
     size_t live_filters = 0;
 
     // ---- device image ----
-    DevBuf d_nodes, d_edges, d_dict, d_arena, d_woff;
+    DevBuf d_nodes, d_edges, d_hedges, d_dict, d_arena, d_woff;
     bool dev_dirty = true;
     int hist_enabled = 0;             // option "hist": per-level histogram in stats mode (diagnostic, slow)
     uint32_t walk_bpc = 0;            // option "walk_bpc": walk blocks per CU (0 = full occupancy)
@@ -232,7 +244,8 @@ struct tm_engine {
         }
         dict.assign(1024, DictSlot{0, WORD_NONE, 0});
         nodes.reserve(1024);
-        edges.assign(1024, kEmptySlot);
+        cold.slots.assign(1024, kEmptySlot);
+        hot.slots.assign(1024, kEmptySlot);
         new_node(NODE_NONE, NODE_NONE);  // root = 0
     }
 
@@ -303,6 +316,7 @@ struct tm_engine {
     // edges (open addressing, linear probing over 16 B slots from the home
     // bucket's first slot; backward-shift deletion keeps probes tombstone-free)
     size_t edge_find_slot(uint32_t parent, uint32_t word) const {
+        const std::vector<EdgeSlot>& edges = tab(parent).slots;
         size_t mask = edges.size() - 1;
         for (size_t s = edge_home(parent, word, mask);; s = (s + 1) & mask) {
             const EdgeSlot& e = edges[s];
@@ -310,20 +324,21 @@ struct tm_engine {
             if (e.parent == parent && e.word == word) return s;
         }
     }
-    void edge_place(const EdgeSlot& x) {
-        size_t mask = edges.size() - 1;
+    static void place_in(EdgeTable& t, const EdgeSlot& x) {
+        size_t mask = t.slots.size() - 1;
         size_t s = edge_home(x.parent, x.word, mask);
-        while (edges[s].parent != EDGE_EMPTY) s = (s + 1) & mask;
-        edges[s] = x;
-        edge_dirty.mark(s);
+        while (t.slots[s].parent != EDGE_EMPTY) s = (s + 1) & mask;
+        t.slots[s] = x;
+        t.dirty.mark(s);
     }
-    void edge_grow() {
+    void edge_place(const EdgeSlot& x) { place_in(tab(x.parent), x); }
+    static void edge_grow(EdgeTable& t) {
         std::vector<EdgeSlot> old;
-        old.swap(edges);
-        edges.assign(old.size() * 2, kEmptySlot);
+        old.swap(t.slots);
+        t.slots.assign(old.size() * 2, kEmptySlot);
         for (const EdgeSlot& e : old)
-            if (e.parent != EDGE_EMPTY) edge_place(e);
-        edge_dirty.all = true;
+            if (e.parent != EDGE_EMPTY) place_in(t, e);
+        t.dirty.all = true;
     }
     EdgeSlot slot_for(uint32_t parent, uint32_t word, uint32_t child) const {
         const Node& c = nodes[child];
@@ -341,9 +356,10 @@ struct tm_engine {
         return e;
     }
     void edge_insert(uint32_t parent, uint32_t word, uint32_t child) {
-        if ((edge_used + 1) * 4 > edges.size()) edge_grow();
-        edge_place(slot_for(parent, word, child));
-        ++edge_used;
+        EdgeTable& t = tab(parent);
+        if ((t.used + 1) * 4 > t.slots.size()) edge_grow(t);
+        place_in(t, slot_for(parent, word, child));
+        ++t.used;
     }
     // node x changed: mark its page and refresh the copy of its record in
     // its parent's edge slot (when it is a table child)
@@ -355,12 +371,15 @@ struct tm_engine {
         if (w != WORD_HASH && !(nodes[p].plus & WIDE)) return;
         const size_t s = edge_find_slot(p, w);
         if (s == SIZE_MAX) return;
-        edges[s] = slot_for(p, w, x);
-        edge_dirty.mark(s);
+        tab(p).slots[s] = slot_for(p, w, x);
+        tab(p).dirty.mark(s);
     }
     void edge_erase(uint32_t parent, uint32_t word) {
         size_t i = edge_find_slot(parent, word);
         if (i == SIZE_MAX) return;
+        EdgeTable& t = tab(parent);
+        std::vector<EdgeSlot>& edges = t.slots;
+        Dirty& edge_dirty = t.dirty;
         size_t mask = edges.size() - 1;
         size_t j = i;
         for (;;) {
@@ -376,7 +395,7 @@ struct tm_engine {
         }
         edges[i] = kEmptySlot;
         edge_dirty.mark(i);
-        --edge_used;
+        --t.used;
     }
 
     // ------------------------------------------------------------------
@@ -417,7 +436,7 @@ struct tm_engine {
         if (w == WORD_HASH) return x.hash;
         if (!(x.plus & WIDE)) return x.lw == w ? x.lc : NODE_NONE;
         size_t s = edge_find_slot(v, w);
-        return s == SIZE_MAX ? NODE_NONE : edges[s].child;
+        return s == SIZE_MAX ? NODE_NONE : tab(v).slots[s].child;
     }
     // literal child add / remove: one literal child lives inline (lw, lc);
     // from the second on, all of them live in edges[] (WIDE), and lw:lc
@@ -719,8 +738,9 @@ struct tm_engine {
             if (aux[v].parent == NODE_NONE && v != ROOT) continue;  // free slot
             if (!(nodes[v].plus & WIDE) && nodes[v].lw != WORD_NONE) start[v + 1]++;
         }
-        for (const EdgeSlot& e : edges)
-            if (e.parent != EDGE_EMPTY && e.word != WORD_HASH) start[e.parent + 1]++;
+        for (const EdgeTable* t : {&cold, &hot})
+            for (const EdgeSlot& e : t->slots)
+                if (e.parent != EDGE_EMPTY && e.word != WORD_HASH) start[e.parent + 1]++;
         for (size_t v = 0; v < N; ++v) start[v + 1] += start[v];
         std::vector<uint32_t> kids(start[N]);
         {
@@ -729,8 +749,9 @@ struct tm_engine {
                 if (aux[v].parent == NODE_NONE && v != ROOT) continue;
                 if (!(nodes[v].plus & WIDE) && nodes[v].lw != WORD_NONE) kids[fill[v]++] = nodes[v].lc;
             }
-            for (const EdgeSlot& e : edges)
-                if (e.parent != EDGE_EMPTY && e.word != WORD_HASH) kids[fill[e.parent]++] = e.child;
+            for (const EdgeTable* t : {&cold, &hot})
+                for (const EdgeSlot& e : t->slots)
+                    if (e.parent != EDGE_EMPTY && e.word != WORD_HASH) kids[fill[e.parent]++] = e.child;
         }
         // preorder: v, literal subtrees, '+' subtree, '#' subtree; with
         // hot_levels = H, depths 0..H first, level by level (each node's
@@ -744,6 +765,7 @@ struct tm_engine {
             if ((nodes[v].plus & NODE_MASK) != NODE_NONE) out.push_back(nodes[v].plus & NODE_MASK);
             if (nodes[v].hash != NODE_NONE) out.push_back(nodes[v].hash);
         };
+        uint32_t new_hot_limit = 0;
         if (hot_levels > 0) {
             std::vector<uint32_t> cur{ROOT}, next;
             for (uint32_t d = 0; d <= hot_levels && !cur.empty(); ++d) {
@@ -754,7 +776,9 @@ struct tm_engine {
                     children(v, next);
                 }
                 cur.swap(next);
+                if (d + 1 == hot_edge_depth) new_hot_limit = (uint32_t)order.size();   // depths < D
             }
+            if (hot_edge_depth > hot_levels + 1) new_hot_limit = (uint32_t)order.size();
             for (auto it = cur.rbegin(); it != cur.rend(); ++it) stack.push_back(*it);
         } else {
             stack.push_back(ROOT);
@@ -784,15 +808,27 @@ struct tm_engine {
             a.parent = remap(a.parent);
             na[i] = a;
         }
-        // edge table with the new ids
+        // edge tables with the new ids: parents below the new hot limit in `hot`
         std::vector<EdgeSlot> old;
-        old.swap(edges);
-        edges.assign(old.size(), kEmptySlot);
+        old.reserve(cold.used + hot.used);
+        for (EdgeTable* t : {&cold, &hot}) {
+            for (const EdgeSlot& e : t->slots)
+                if (e.parent != EDGE_EMPTY) old.push_back(e);
+            std::vector<EdgeSlot>().swap(t->slots);
+            t->used = 0;
+        }
         for (const EdgeSlot& e : old)
-            if (e.parent != EDGE_EMPTY && e.word != WORD_HASH) bloom_add(nn[newid[e.parent]], e.word);
+            if (e.word != WORD_HASH) bloom_add(nn[newid[e.parent]], e.word);
         nodes.swap(nn);
-        for (const EdgeSlot& e : old)
-            if (e.parent != EDGE_EMPTY) edge_place(slot_for(newid[e.parent], e.word, newid[e.child]));
+        hot_limit = new_hot_limit;
+        size_t nhot = 0;
+        for (const EdgeSlot& e : old) nhot += newid[e.parent] < hot_limit;
+        cold.slots.assign(std::max<size_t>(1024, next_pow2((old.size() - nhot) * 4 + 1)), kEmptySlot);
+        hot.slots.assign(std::max<size_t>(1024, next_pow2(nhot * 4 + 1)), kEmptySlot);
+        for (const EdgeSlot& e : old) {
+            edge_place(slot_for(newid[e.parent], e.word, newid[e.child]));
+            ++tab(newid[e.parent]).used;
+        }
         for (FilterRec& f : filters)
             if (f.node != NODE_NONE) f.node = newid[f.node];
         aux.swap(na);
@@ -800,7 +836,8 @@ struct tm_engine {
         created_since_layout = 0;
         force_relayout = false;
         node_dirty.all = true;
-        edge_dirty.all = true;
+        cold.dirty.all = true;
+        hot.dirty.all = true;
     }
 
     // ------------------------------------------------------------------
@@ -828,7 +865,10 @@ struct tm_engine {
             im.node_shift = 5;
         }
         im.edges = d_edges.as<const EdgeSlot>();
-        im.edge_slot_mask = edges.size() - 1;
+        im.edge_slot_mask = cold.slots.size() - 1;
+        im.hot_edges = d_hedges.as<const EdgeSlot>();
+        im.hot_slot_mask = hot.slots.size() - 1;
+        im.hot_limit = hot_limit;
         im.dict = d_dict.as<const DictSlot>();
         im.dict_slot_mask = dict.size() - 1;
         im.word_arena = d_arena.as<const uint8_t>();
@@ -890,7 +930,8 @@ struct tm_engine {
         Guard g(device);
         wait_matches();  // never patch the image under a running walk
         upload_table(d_nodes, nodes, node_dirty, 0);
-        upload_table(d_edges, edges, edge_dirty, 0);
+        upload_table(d_edges, cold.slots, cold.dirty, 0);
+        upload_table(d_hedges, hot.slots, hot.dirty, 0);
         upload_table(d_dict, dict, dict_dirty, 0);
         // append-only arrays: upload the new tail (or all after a realloc)
         {
@@ -1136,7 +1177,7 @@ int tm_open(const tm_config* cfg, tm_engine** out) {
         e->nodes.reserve(nodes_hint);
         e->aux.reserve(nodes_hint);
         // wide nodes' literal edges and '#' edges use the table (load <= 1/4)
-        e->edges.assign(next_pow2(nodes_hint), kEmptySlot);
+        e->cold.slots.assign(next_pow2(nodes_hint), kEmptySlot);
     }
     if (dev >= 0) {
         int ndev = 0;
@@ -1167,7 +1208,7 @@ void tm_close(tm_engine* e) {
         for (DevBuf* b : {&e->d_fr_off, &e->d_fr_dest, &e->d_ex_slots, &e->d_ex_arena, &e->d_ex_dest, &e->w_rexact,
                           &e->w_rscan, &e->w_rids, &e->w_rcounts, &e->w_roff})
             b->release();
-        for (DevBuf* b : {&e->d_nodes, &e->d_edges, &e->d_dict, &e->d_arena, &e->d_woff, &e->d_inner, &e->d_leaf,
+        for (DevBuf* b : {&e->d_nodes, &e->d_edges, &e->d_hedges, &e->d_dict, &e->d_arena, &e->d_woff, &e->d_inner, &e->d_leaf,
                           &e->w_kstage, &e->w_mpre, &e->w_mscan, &e->w_twords, &e->w_bytes, &e->w_off, &e->w_words,
                           &e->w_meta, &e->w_counts, &e->w_outoff, &e->w_ids, &e->w_scan, &e->w_total, &e->w_path,
                           &e->w_stats, &e->w_stage, &e->w_ws})
@@ -1296,7 +1337,8 @@ int tm_engine_device(tm_engine* e) { return e ? e->device : -1; }
 
 uint64_t tm_image_bytes(tm_engine* e) {
     if (!e) return 0;
-    return e->nodes.size() * sizeof(Node) + e->edges.size() * sizeof(EdgeSlot) + e->dict.size() * sizeof(DictSlot) +
+    return e->nodes.size() * sizeof(Node) + (e->cold.slots.size() + e->hot.slots.size()) * sizeof(EdgeSlot) +
+           e->dict.size() * sizeof(DictSlot) +
            e->word_arena.size() + e->word_off.size() * 4;
 }
 
@@ -1616,6 +1658,15 @@ int tm_set_option(tm_engine* e, const char* name, int64_t value) {
         if (!std::strcmp(name, "split")) {
             if (value < 0 || value > 1) return TM_EINVAL;
             e->split_halves = (int)value;
+            return TM_OK;
+        }
+        if (!std::strcmp(name, "hot_edges")) {
+            if (value < 0 || value > 16) return TM_EINVAL;
+            if ((uint32_t)value != e->hot_edge_depth) {
+                e->hot_edge_depth = (uint32_t)value;
+                e->force_relayout = true;
+                e->dev_dirty = true;
+            }
             return TM_OK;
         }
         if (!std::strcmp(name, "hot_levels")) {

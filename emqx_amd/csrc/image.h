@@ -97,6 +97,9 @@ struct ImageView {
     uint32_t        node_shift;        // 5: interleaved 32 B records; 4: split arrays of 16 B halves
     const EdgeSlot* edges;
     uint64_t        edge_slot_mask;    // slots - 1 (power of two)
+    const EdgeSlot* hot_edges;         // edges of parents with id < hot_limit
+    uint64_t        hot_slot_mask;
+    uint32_t        hot_limit;
     const DictSlot* dict;
     uint64_t        dict_slot_mask;
     const uint8_t*  word_arena;

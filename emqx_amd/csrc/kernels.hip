@@ -164,9 +164,12 @@ struct Hit {
 // slot's second half completes the child's record
 template <bool STATS>
 __device__ __forceinline__ Hit probe_edge(const ImageView& im, uint32_t v, uint32_t w, uint64_t& loads) {
-    uint64_t s = edge_home(v, w, im.edge_slot_mask);
+    const bool hot = v < im.hot_limit;   // the top of the trie: a small table of its own
+    const EdgeSlot* tab = hot ? im.hot_edges : im.edges;
+    const uint64_t mask = hot ? im.hot_slot_mask : im.edge_slot_mask;
+    uint64_t s = edge_home(v, w, mask);
     for (;;) {
-        const uint4* slot = reinterpret_cast<const uint4*>(im.edges + s);
+        const uint4* slot = reinterpret_cast<const uint4*>(tab + s);
         const uint4 e = slot[0];
         if (STATS) ++loads;
         if (e.x == v && e.y == w) {
@@ -175,7 +178,7 @@ __device__ __forceinline__ Hit probe_edge(const ImageView& im, uint32_t v, uint3
             return Hit{e.z, e.w, d.x, d.y, d.z, d.w, true};
         }
         if (e.x == EDGE_EMPTY) return Hit{NODE_NONE, 0, 0, 0, 0, 0, false};
-        s = (s + 1) & im.edge_slot_mask;
+        s = (s + 1) & mask;
     }
 }
 
