@@ -100,11 +100,11 @@ __device__ __forceinline__ uint64_t block_exclusive_scan(uint64_t x, uint64_t* l
     return wpre + inc - x;
 }
 
-// emqx_topic:words/1 of topic [b, e): word id of level k to tw[k] (k < WREG)
-// or lw[k] (k >= WREG); returns the number of levels (N slashes -> N+1
-// levels, empty levels kept)
+// emqx_topic:words/1 of topic [b, e): word id of level k to tw[k] (k < WREG,
+// registers: AND-mask updates, no dynamic index) or lw[k] (k >= WREG);
+// returns the number of levels (N slashes -> N+1 levels, empty levels kept)
 __device__ __forceinline__ uint32_t tokenize_topic(const ImageView& im, const uint8_t* bytes, uint64_t b,
-                                                   uint64_t e, uint32_t* tw, uint32_t* lw) {
+                                                   uint64_t e, uint32_t (&tw)[WREG], uint32_t* lw) {
     uint32_t lev = 0;
     uint64_t s = b;
     for (;;) {
@@ -128,8 +128,12 @@ __device__ __forceinline__ uint32_t tokenize_topic(const ImageView& im, const ui
         }
         if (!found) q = e;
         const uint32_t w = dict_lookup(im, bytes, s, (uint32_t)(q - s));
-        if (lev < WREG) tw[lev] = w;
-        else lw[lev] = w;
+        if (lev < WREG) {
+#pragma unroll
+            for (uint32_t k = 0; k < WREG; ++k) tw[k] = lev == k ? w : tw[k];
+        } else {
+            lw[lev] = w;
+        }
         ++lev;
         if (!found) return lev;
         s = q + 1;
@@ -144,7 +148,16 @@ tm_tokenize(ImageView im, const uint8_t* __restrict__ bytes, const uint64_t* __r
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n) return;
     const uint64_t b = off[t], e = off[t + 1];
-    const uint32_t lev = tokenize_topic(im, bytes, b, e, twords + (uint64_t)t * WREG, words + (b - off[0]) + t);
+    uint32_t tw[WREG];
+#pragma unroll
+    for (uint32_t k = 0; k < WREG; ++k) tw[k] = WORD_NONE;
+    const uint32_t lev = tokenize_topic(im, bytes, b, e, tw, words + (b - off[0]) + t);
+    // the row as four whole 16 B stores (per-level 4 B stores from 64 lanes
+    // to 64 rows were partial-line writes: read-modify-write traffic)
+    uint4* row = reinterpret_cast<uint4*>(twords + (uint64_t)t * WREG);
+#pragma unroll
+    for (uint32_t k = 0; k < WREG / 4; ++k)
+        row[k] = make_uint4(tw[4 * k], tw[4 * k + 1], tw[4 * k + 2], tw[4 * k + 3]);
     const uint32_t dollar = (e > b && bytes[b] == '$') ? 1u : 0u;
     meta[t] = lev | (dollar << 31) | (lev > WREG ? MLONG : 0u);
 }
@@ -380,8 +393,16 @@ struct RowEmit {
     uint64_t* krow;
     uint32_t K, cnt;
     uint4 buf;
+    uint64_t kb;   // KEYS: key of the last even discovery, stored with the next one (16 B)
     __device__ __forceinline__ void operator()(uint32_t f, uint64_t key) {
-        if (KEYS && cnt < K) krow[K - 1 - cnt] = key;
+        if (KEYS && cnt < K) {
+            if (!(cnt & 1u)) {
+                kb = key;
+            } else {   // slots K-2-(cnt-1) and K-1-(cnt-1): this key, then the even one
+                *reinterpret_cast<uint4*>(krow + K - 1 - cnt) =
+                    make_uint4((uint32_t)key, (uint32_t)(key >> 32), (uint32_t)kb, (uint32_t)(kb >> 32));
+            }
+        }
         if (cnt < K) {
             const uint32_t s = cnt & 3u;
             buf.w = s == 0 ? f : buf.w;
@@ -394,6 +415,7 @@ struct RowEmit {
     }
     __device__ __forceinline__ void flush() {
         if ((cnt & 3u) && cnt < K) *reinterpret_cast<uint4*>(row + K - 4 - (cnt & ~3u)) = buf;
+        if (KEYS && (cnt & 1u) && cnt <= K) krow[K - cnt] = kb;   // the unpaired last even discovery
     }
 };
 // re-walk of a topic with total > K ids: discovery k >= K goes to output
@@ -468,7 +490,7 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
     uint32_t my = NO_TOPIC;
     bool is_long = false, drained = false;
     Cursor cur;
-    RowEmit<KEYS> em{nullptr, nullptr, K, 0, make_uint4(0, 0, 0, 0)};
+    RowEmit<KEYS> em{nullptr, nullptr, K, 0, make_uint4(0, 0, 0, 0), 0ull};
     WalkStats st;
     if (STATS) st.hist = hist;
     uint64_t lev_sum = 0, match_sum = 0;
