@@ -52,6 +52,10 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=1_500_000, help="topics timed on the host (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=None)
     ap.add_argument("--check", type=int, default=20_000, help="topics checked bit-exactly vs the oracle")
+    ap.add_argument("--streams", type=int, default=3,
+                    help="streams the steps alternate over (batches overlap on the GPU; 1 = strictly serial)")
+    ap.add_argument("--roof-steps", type=int, default=5,
+                    help="serial steps after the timed region that time each kernel for the roofline")
     ap.add_argument("--walk", default=None, help="walk variant (queue|queue_xcd)")
     ap.add_argument("--ab", default=None, help="comma list of walk variants timed interleaved (extra report)")
     ap.add_argument("--stage-k", type=int, default=None)
@@ -139,8 +143,20 @@ def main():
     log("fan-out per topic: %s" % fanout)
     d_i = torch.empty(cap, dtype=torch.int32, device=dev)
 
+    # consecutive steps alternate over a.streams streams, each with its own
+    # output buffers: a batch's tokenizer / copy-out overlap its neighbours'
+    # walks (the engine rotates its per-batch workspace slots likewise)
+    lanes = [(st, d_c, d_oo, d_i, d_t)]
+    for _ in range(1, a.streams):
+        lanes.append((torch.cuda.Stream(device=dev), torch.empty_like(d_c), torch.empty_like(d_oo),
+                      torch.empty_like(d_i), torch.zeros_like(d_t)))
+    eng.set_option("slots", min(4, max(2, a.streams)))
+    k_step = [0]
+
     def step():
-        eng.match_batch_device(d_b, d_o, n, nbytes, d_c, d_oo, d_i, cap, d_t, stream=st)
+        s_, c_, oo_, i_, t_ = lanes[k_step[0] % len(lanes)]
+        k_step[0] += 1
+        eng.match_batch_device(d_b, d_o, n, nbytes, c_, oo_, i_, cap, t_, stream=s_)
 
     for _ in range(a.warmup):
         step()
@@ -175,11 +191,21 @@ def main():
 
     # ---- timed region: K steps, kernel events recorded on the launch stream;
     # barrier + sync on both sides, max over ranks (emqx_amd/multi.py)
-    eng.set_timing(True)
     dt = multi.timed_region(step, a.steps, lambda: torch.cuda.synchronize(dev))
+    assert int(d_t.item()) == total, "match total changed between steps"
+    # per-kernel durations for the roofline: with batches overlapping, a
+    # kernel's event interval also holds its neighbours' work, so the kernels
+    # are timed over a.roof_steps extra steps issued serially on one stream
+    torch.cuda.synchronize(dev)
+    eng.set_timing(True)
+    for _ in range(a.roof_steps):
+        eng.match_batch_device(d_b, d_o, n, nbytes, d_c, d_oo, d_i, cap, d_t, stream=st)
+    torch.cuda.synchronize(dev)
     kms = eng.last_kernel_times()
     eng.set_timing(False)
-    assert int(d_t.item()) == total, "match total changed between steps"
+    for _, c_, oo_, i_, t_ in lanes[1:]:   # overlapping batches: identical results in every lane
+        assert int(t_.item()) == total and torch.equal(c_, d_c) and torch.equal(oo_, d_oo) and \
+            torch.equal(i_[:total], d_i[:total]), "batches on different streams disagree"
 
     # ---- bit-exact spot check of this rank's batch against the oracle
     check_ok = None
@@ -242,7 +268,8 @@ def main():
             "dtype": "u32",
             "data": "synthetic",
             "config": {"workload": "C%d: %d distinct wildcard filters replicated per GPU, %d-level topics, "
-                                   "%d topics per GPU per step" % (a.config, n_filters, cfg["levels"], n),
+                                   "%d topics per GPU per step, steps alternating over %d streams" % (
+                                       a.config, n_filters, cfg["levels"], n, a.streams),
                        "filters": n_filters, "topics_per_gpu_step": n, "levels": cfg["levels"],
                        "parallelism": "replicated trie x %d, topic batches sharded by rank" % world},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -252,6 +279,8 @@ def main():
                          "kernel": {"walk": "tm_walk_queue (balanced NFA walk, one 16 B node-half load per step)"
                                     }.get(kname, kname),
                          "kernel_ms": walk_ms,
+                         "kernel_ms_source": "HIP events around each kernel on its stream, %d serial steps after "
+                                             "the timed region" % a.roof_steps,
                          "algorithmic_bytes_per_launch": B,
                          "per_topic": {"n": levels / n, "E": stats["edge_reads"] / n, "M": stats["matches"] / n,
                                        "visits": stats["visits"] / n, "leaf_visits": stats["leaf_visits"] / n,
@@ -341,11 +370,18 @@ def main_sharded(a, rank, world, local, dev):
     for _ in range(max(a.warmup, 1)):
         step()
     torch.cuda.synchronize(dev)
-    eng.set_timing(True)
     dt = multi.timed_region(step, a.steps, lambda: torch.cuda.synchronize(dev))
+    assert int(d_t.item()) == total, "match total changed between steps"
+    # per-kernel durations for the roofline: with batches overlapping, a
+    # kernel's event interval also holds its neighbours' work, so the kernels
+    # are timed over a.roof_steps extra steps issued serially on one stream
+    torch.cuda.synchronize(dev)
+    eng.set_timing(True)
+    for _ in range(a.roof_steps):
+        eng.match_batch_device(d_b, d_o, n, nbytes, d_c, d_oo, d_i, cap, d_t, stream=st)
+    torch.cuda.synchronize(dev)
     kms = eng.last_kernel_times()
     eng.set_timing(False)
-    assert int(d_t.item()) == total, "match total changed between steps"
     mtotal = int(merged["t"].item())
 
     # phase breakdown (untimed extra loops): walk / exchange / merge

@@ -211,18 +211,25 @@ struct tm_engine {
     DevBuf w_rexact, w_rscan, w_rids, w_rcounts, w_roff;
 
     // ---- match workspace ----
-    DevBuf w_kstage, w_mpre, w_mscan, w_twords, w_bytes, w_off, w_words, w_meta, w_counts, w_outoff, w_ids, w_scan, w_total, w_path, w_stats, w_stage,
-        w_ws;
+    DevBuf w_mpre, w_mscan, w_bytes, w_off, w_counts, w_outoff, w_ids, w_total;
+    // per-batch device workspace: consecutive batches rotate over `nslots`
+    // slots, so batches issued on different streams overlap on the GPU (the
+    // walk of one beside the tokenizer / copy-out of its neighbours); a
+    // slot's next user waits for its previous batch (hipStreamWaitEvent)
+    struct Slot {
+        DevBuf twords, words, path, meta, scan, stage, kstage, ws, stats;
+        uint64_t* h_maxc = nullptr;     // pinned: largest match count of the slot's last walk
+        hipEvent_t maxc_ev = nullptr, done = nullptr;
+        bool maxc_pending = false, used = false;
+    };
+    static constexpr int MAX_SLOTS = 4;
+    Slot slots[MAX_SLOTS];
+    int nslots = 2, next_slot = 0, last_slot = 0;   // option "slots"
     uint32_t stage_k = 512;   // TM_STAGE_K: ids staged per topic before a re-walk (rows are
                               // written sparsely: HBM footprint, not traffic)
     uint32_t stage_k_min = 512;         // option "stage_k"
     int stage_auto = 1;                 // option "stage_auto": grow K to the largest list seen (no re-walks)
-    uint64_t* h_maxc = nullptr;         // pinned: largest match count of the last walk
-    hipEvent_t maxc_ev = nullptr;
-    bool maxc_pending = false;
     static constexpr size_t STAGE_BUDGET = 16ull << 30;  // stage-row footprint cap (bytes, of 288 GB HBM)
-    hipEvent_t last_match_done = nullptr;
-    bool match_in_flight = false;
     bool stats_enabled = false, timing_enabled = false;
     tm_batch_stats last_stats{};
     // per-batch event records, accumulated until tm_last_kernel_times()
@@ -899,10 +906,8 @@ struct tm_engine {
     }
 
     void wait_matches() {
-        if (match_in_flight) {
-            HIPCHK(hipEventSynchronize(last_match_done));
-            match_in_flight = false;
-        }
+        for (Slot& w : slots)
+            if (w.used) HIPCHK(hipEventSynchronize(w.done));
     }
 
     void maybe_relayout() {
@@ -979,16 +984,18 @@ struct tm_engine {
         }
         return k;
     }
-    void ensure_workspace(uint32_t n, uint64_t nbytes) {
-        w_twords.ensure((size_t)(n + 1) * WREG * 4);
-        w_words.ensure((nbytes + n + 1) * 4);
-        w_path.ensure((nbytes + 2ull * n + 2) * 4);
-        w_total.ensure(64);
-        w_stats.ensure(STATS_BYTES);
-        w_meta.ensure((size_t)(n + 1) * 4);
-        w_scan.ensure(scan_tmp_elems(n) * 8 + 8);
-        w_stage.ensure(((size_t)n * stage_k + 4) * 4);
-        w_ws.ensure(QWS_BYTES);
+    void ensure_workspace(uint32_t n, uint64_t nbytes) { w_total.ensure(64); }
+    void ensure_slot(Slot& w, uint32_t n, uint64_t nbytes, bool keys) {
+        w.twords.ensure((size_t)(n + 1) * WREG * 4);
+        w.words.ensure((nbytes + n + 1) * 4);
+        w.path.ensure((nbytes + 2ull * n + 2) * 4);
+        w.stats.ensure(STATS_BYTES);
+        w.meta.ensure((size_t)(n + 1) * 4);
+        w.scan.ensure(scan_tmp_elems(n) * 8 + 8);
+        w.stage.ensure(((size_t)n * stage_k + 4) * 4);
+        if (keys) w.kstage.ensure(((size_t)n * stage_k + 4) * 8);
+        w.ws.ensure(QWS_BYTES);
+        if (!w.done) HIPCHK(hipEventCreateWithFlags(&w.done, hipEventDisableTiming));
     }
 
     // the whole hot path of one batch, stream-ordered on st: CSR of ordered
@@ -996,22 +1003,28 @@ struct tm_engine {
     // stage rows sized to the largest list of the previous walk (read back
     // asynchronously), within STAGE_BUDGET: fan-out beyond K costs a re-walk
     void adapt_stage_k(uint32_t n, bool keys) {
-        if (!stage_auto || !maxc_pending || hipEventQuery(maxc_ev) != hipSuccess) return;
-        maxc_pending = false;
+        if (!stage_auto) return;
+        uint64_t mc = 0;
+        for (Slot& w : slots) {
+            if (!w.maxc_pending || hipEventQuery(w.maxc_ev) != hipSuccess) continue;
+            w.maxc_pending = false;
+            mc = std::max<uint64_t>(mc, *w.h_maxc);
+        }
+        if (!mc) return;
         uint64_t want = stage_k_min;
-        while (want < *h_maxc && want < 4096) want <<= 1;
+        while (want < mc && want < 4096) want <<= 1;
         uint64_t k = stage_k;
         const uint64_t per = (uint64_t)n * (keys ? 12 : 4);
         while (k < want && per * (k << 1) <= STAGE_BUDGET) k <<= 1;
         stage_k = (uint32_t)k;
     }
-    void record_maxc(hipStream_t st) {
+    void record_maxc(Slot& w, hipStream_t st) {
         if (!stage_auto) return;
-        if (!h_maxc) HIPCHK(hipHostMalloc((void**)&h_maxc, 64, hipHostMallocDefault));
-        if (!maxc_ev) HIPCHK(hipEventCreateWithFlags(&maxc_ev, hipEventDisableTiming));
-        HIPCHK(hipMemcpyAsync(h_maxc, w_ws.as<uint64_t>() + QWS_MAXC, 8, hipMemcpyDeviceToHost, st));
-        HIPCHK(hipEventRecord(maxc_ev, st));
-        maxc_pending = true;
+        if (!w.h_maxc) HIPCHK(hipHostMalloc((void**)&w.h_maxc, 64, hipHostMallocDefault));
+        if (!w.maxc_ev) HIPCHK(hipEventCreateWithFlags(&w.maxc_ev, hipEventDisableTiming));
+        HIPCHK(hipMemcpyAsync(w.h_maxc, w.ws.as<uint64_t>() + QWS_MAXC, 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipEventRecord(w.maxc_ev, st));
+        w.maxc_pending = true;
     }
 
     void run_batch(const uint8_t* bytes, const uint64_t* off, uint32_t n, uint64_t nbytes, uint32_t* counts,
@@ -1019,10 +1032,15 @@ struct tm_engine {
                    uint64_t* keys = nullptr) {
         adapt_stage_k(n, keys != nullptr);
         ensure_workspace(n, nbytes);
-        if (keys) w_kstage.ensure(((size_t)n * stage_k + 4) * 8);
+        const int si = next_slot;
+        next_slot = (next_slot + 1) % nslots;
+        Slot& w = slots[si];
+        if (w.used) HIPCHK(hipStreamWaitEvent(st, w.done, 0));   // its previous batch, maybe on another stream
+        ensure_slot(w, n, nbytes, keys != nullptr);
+        last_slot = si;
         ImageView im = view();
-        unsigned long long* sp = w_stats.as<unsigned long long>();
-        if (stats_enabled) HIPCHK(hipMemsetAsync(w_stats.p, 0, STATS_BYTES, st));
+        unsigned long long* sp = w.stats.as<unsigned long long>();
+        if (stats_enabled) HIPCHK(hipMemsetAsync(w.stats.p, 0, STATS_BYTES, st));
         static const char* kStage[4] = {"tokenize", "walk", "scan", "copy_out"};
         hipEvent_t marks[8];
         if (timing_enabled)
@@ -1032,17 +1050,19 @@ struct tm_engine {
                 marks[2 * i + 1] = ev_cur[i].b;
             }
         QueueBufs qb;
-        qb.twords = w_twords.as<uint32_t>();
-        qb.words = w_words.as<uint32_t>();
-        qb.meta = w_meta.as<uint32_t>();
-        qb.path = w_path.as<uint32_t>();
-        qb.stage = w_stage.as<uint32_t>();
-        qb.kstage = keys ? w_kstage.as<uint64_t>() : nullptr;
-        qb.scan_tmp = w_scan.as<uint64_t>();
-        qb.ws = w_ws.as<unsigned long long>();
+        qb.twords = w.twords.as<uint32_t>();
+        qb.words = w.words.as<uint32_t>();
+        qb.meta = w.meta.as<uint32_t>();
+        qb.path = w.path.as<uint32_t>();
+        qb.stage = w.stage.as<uint32_t>();
+        qb.kstage = keys ? w.kstage.as<uint64_t>() : nullptr;
+        qb.scan_tmp = w.scan.as<uint64_t>();
+        qb.ws = w.ws.as<unsigned long long>();
         HIPCHK(launch_queue(stats_enabled, xcdq != 0, im, bytes, off, n, qb, stage_k, counts, out_off, ids, keys, cap,
                             total, sp, st, timing_enabled ? marks : nullptr, walk_bpc, hist_enabled != 0));
-        record_maxc(st);
+        record_maxc(w, st);
+        HIPCHK(hipEventRecord(w.done, st));
+        w.used = true;
         if (timing_enabled)
             for (int i = 0; i < 4; ++i) ev_pending.push_back(ev_cur[i]);
     }
@@ -1081,16 +1101,15 @@ struct tm_engine {
     }
 
     void finish_batch(hipStream_t st, uint32_t n) {
-        if (!last_match_done) HIPCHK(hipEventCreateWithFlags(&last_match_done, hipEventDisableTiming));
-        HIPCHK(hipEventRecord(last_match_done, st));
-        match_in_flight = true;
+        (void)st;
         last_stats = tm_batch_stats{};
         last_stats.topics = n;
     }
     void collect_stats() {
-        if (!stats_enabled || !w_stats.p) return;
+        const DevBuf& ws = slots[last_slot].stats;
+        if (!stats_enabled || !ws.p) return;
         unsigned long long h[6] = {0, 0, 0, 0, 0, 0};
-        HIPCHK(hipMemcpy(h, w_stats.p, sizeof(h), hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(h, ws.p, sizeof(h), hipMemcpyDeviceToHost));
         last_stats.levels = h[0];
         last_stats.visits = h[1];
         last_stats.edge_reads = h[2];
@@ -1209,18 +1228,21 @@ void tm_close(tm_engine* e) {
                           &e->w_rscan, &e->w_rids, &e->w_rcounts, &e->w_roff})
             b->release();
         for (DevBuf* b : {&e->d_nodes, &e->d_edges, &e->d_hedges, &e->d_dict, &e->d_arena, &e->d_woff, &e->d_inner, &e->d_leaf,
-                          &e->w_kstage, &e->w_mpre, &e->w_mscan, &e->w_twords, &e->w_bytes, &e->w_off, &e->w_words,
-                          &e->w_meta, &e->w_counts, &e->w_outoff, &e->w_ids, &e->w_scan, &e->w_total, &e->w_path,
-                          &e->w_stats, &e->w_stage, &e->w_ws})
+                          &e->w_mpre, &e->w_mscan, &e->w_bytes, &e->w_off, &e->w_counts, &e->w_outoff, &e->w_ids,
+                          &e->w_total})
             b->release();
+        for (auto& w : e->slots) {
+            for (DevBuf* b : {&w.twords, &w.words, &w.path, &w.meta, &w.scan, &w.stage, &w.kstage, &w.ws, &w.stats})
+                b->release();
+            if (w.done) (void)hipEventDestroy(w.done);
+            if (w.maxc_ev) (void)hipEventDestroy(w.maxc_ev);
+            if (w.h_maxc) (void)hipHostFree(w.h_maxc);
+        }
         for (auto* v : {&e->ev_pool, &e->ev_pending})
             for (auto& k : *v) {
                 (void)hipEventDestroy(k.a);
                 (void)hipEventDestroy(k.b);
             }
-        if (e->last_match_done) (void)hipEventDestroy(e->last_match_done);
-        if (e->maxc_ev) (void)hipEventDestroy(e->maxc_ev);
-        if (e->h_maxc) (void)hipHostFree(e->h_maxc);
         if (e->stream) (void)hipStreamDestroy(e->stream);
     }
     delete e;
@@ -1404,7 +1426,6 @@ int tm_match_batch(tm_engine* e, const uint8_t* topic_bytes, const uint64_t* top
         HIPCHK(hipMemcpyAsync(out_off, e->w_outoff.p, (size_t)(n + 1) * 8, hipMemcpyDeviceToHost, st));
         if (cap) HIPCHK(hipMemcpyAsync(out_ids, e->w_ids.p, cap * 4, hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
-        e->match_in_flight = false;
         e->collect_stats();
         if (out_needed) *out_needed = total;
         return total > out_cap ? TM_ENOSPC : TM_OK;
@@ -1551,7 +1572,6 @@ int tm_match_routes_batch(tm_engine* e, const uint8_t* topic_bytes, const uint64
             HIPCHK(hipMemcpyAsync(out_dest, e->w_ids.as<uint32_t>() + rcap, cap * 4, hipMemcpyDeviceToHost, st));
         }
         HIPCHK(hipStreamSynchronize(st));
-        e->match_in_flight = false;
         if (out_needed) *out_needed = total;
         return total > out_cap ? TM_ENOSPC : TM_OK;
     });
@@ -1615,8 +1635,7 @@ static int match_device(tm_engine* e, const uint8_t* d_bytes, const uint64_t* d_
         e->finish_batch(st, n);
         if (e->stats_enabled) {
             HIPCHK(hipStreamSynchronize(st));
-            e->match_in_flight = false;
-            e->collect_stats();
+                e->collect_stats();
         }
         return TM_OK;
     });
@@ -1627,8 +1646,9 @@ static int match_device(tm_engine* e, const uint8_t* d_bytes, const uint64_t* d_
 extern "C" int tm_debug_hist(tm_engine* e, uint64_t* out, int n) {
     if (!e || !out || n > 48) return TM_EINVAL;
     return guarded(e, [&]() -> int {
-        if (!e->w_stats.p) return TM_EINVAL;
-        HIPCHK(hipMemcpy(out, e->w_stats.as<uint64_t>() + 8, (size_t)n * 8, hipMemcpyDeviceToHost));
+        const DevBuf& ws = e->slots[e->last_slot].stats;
+        if (!ws.p) return TM_EINVAL;
+        HIPCHK(hipMemcpy(out, ws.as<uint64_t>() + 8, (size_t)n * 8, hipMemcpyDeviceToHost));
         return TM_OK;
     });
 }
@@ -1682,6 +1702,12 @@ int tm_set_option(tm_engine* e, const char* name, int64_t value) {
             if (value < 4 || value > 4096 || (value & 3)) return TM_EINVAL;
             e->stage_k = e->stage_k_min = (uint32_t)value;
             e->stage_auto = 0;   // an explicit K is kept (set "stage_auto" after it to grow from it)
+            return TM_OK;
+        }
+        if (!std::strcmp(name, "slots")) {
+            if (value < 1 || value > tm_engine::MAX_SLOTS) return TM_EINVAL;
+            e->nslots = (int)value;
+            e->next_slot = 0;
             return TM_OK;
         }
         if (!std::strcmp(name, "stage_auto")) {

@@ -255,3 +255,43 @@ def test_every_walk_variant_bit_exact(gpu_device, golden, variant):
     tb, to = W.topics(1, n=30000)
     _by_id(o1, e, tb, to)
     e.close()
+
+
+@pytest.mark.parametrize("slots", [1, 2, 3])
+def test_batches_on_alternating_streams_bit_exact(gpu_device, slots):
+    """consecutive device batches on different streams (workspace slots
+    rotate, a slot's reuse waits for its previous batch): every batch's
+    output equals O1, whatever overlapped with it"""
+    import torch
+    dev = torch.device("cuda", gpu_device)
+    fb, fo = W.filters(1)
+    e = Engine(device=gpu_device)
+    e.insert_many(fb, fo)
+    e.set_option("slots", slots)
+    batches = [W.topics(1, n=8000 + 1000 * k, stream=k) for k in range(4)]
+    o1 = O1()
+    o1.insert_many(fb, fo)
+    want = [o1.match_ids(tb, to, threads=4) for tb, to in batches]
+    streams = [torch.cuda.Stream(device=dev) for _ in range(3)]
+    outs = []
+    for rep in range(3):
+        for k, (tb, to) in enumerate(batches):
+            n = len(to) - 1
+            st = streams[(rep * 4 + k) % 3]
+            with torch.cuda.stream(st):
+                d_b = torch.from_numpy(tb.copy()).to(dev, non_blocking=False)
+                d_o = torch.from_numpy(to.view(np.int64).copy()).to(dev)
+                c = torch.empty(n, dtype=torch.int32, device=dev)
+                o = torch.empty(n + 1, dtype=torch.int64, device=dev)
+                t = torch.zeros(1, dtype=torch.int64, device=dev)
+                ids = torch.empty(int(want[k][1][-1]) + 16, dtype=torch.int32, device=dev)
+            e.match_batch_device(d_b, d_o, n, int(to[-1]), c, o, ids, ids.numel(), t, stream=st)
+            outs.append((k, c, o, ids, t, d_b, d_o))
+    torch.cuda.synchronize()
+    for k, c, o, ids, t, _, _ in outs:
+        oc, oo, oi = want[k]
+        assert int(t.item()) == len(oi)
+        assert np.array_equal(c.cpu().numpy().view(np.uint32), oc)
+        assert np.array_equal(o.cpu().numpy().view(np.uint64), oo)
+        assert np.array_equal(ids[:len(oi)].cpu().numpy().view(np.uint32), oi)
+    e.close()
