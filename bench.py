@@ -130,10 +130,12 @@ def main():
     stats = eng.last_stats()
     if a.hist:
         import ctypes
-        h = (ctypes.c_uint64 * 48)()
-        eng.lib.tm_debug_hist(eng.h, h, 48)
+        h = (ctypes.c_uint64 * 56)()
+        eng.lib.tm_debug_hist(eng.h, h, 56)
         for k, name in enumerate(["visits", "probe_loads", "failed_probes"]):
             log("per-level %s per topic: %s" % (name, [round(h[16 * k + l] / n, 2) for l in range(16)]))
+        log("visits reached by: inline literal %.2f, table literal %.2f, '+' %.2f per topic"
+            % (h[48] / n, h[49] / n, h[50] / n))
     eng.set_stats(False)
     total = int(d_t.item())
     cap = total + 1024

@@ -1644,7 +1644,7 @@ static int match_device(tm_engine* e, const uint8_t* d_bytes, const uint64_t* d_
 // diagnostics (not part of include/topicmatch.h): the last stats-mode
 // batch's per-level histogram [visits, probe loads, failed probes] x 16
 extern "C" int tm_debug_hist(tm_engine* e, uint64_t* out, int n) {
-    if (!e || !out || n > 48) return TM_EINVAL;
+    if (!e || !out || n > 56) return TM_EINVAL;
     return guarded(e, [&]() -> int {
         const DevBuf& ws = e->slots[e->last_slot].stats;
         if (!ws.p) return TM_EINVAL;

@@ -333,6 +333,11 @@ __device__ __forceinline__ bool walk_step(const ImageView& im, Cursor& c, Path p
             if (st.probe_loads != pl0 && g.child == NODE_NONE) atomicAdd(st.hist + 32 + lv, 1ull);
         }
         const uint32_t pc = plus & NODE_MASK;
+        if (STATS && st.hist) {   // how the next visit is reached: [48] inline literal, [49] table literal,
+                                  // [50] '+' (here or by a later pop: counted at the pop)
+            if (g.child != NODE_NONE) atomicAdd(st.hist + ((plus & WIDE) ? 49 : 48), 1ull);
+            else if ((plus & NODE_MASK) != NODE_NONE) atomicAdd(st.hist + 50, 1ull);
+        }
         if (g.child != NODE_NONE) {   // literal subtree first, '+' child pending at level r
             path(r) = pc;
             v = g.child;
@@ -365,6 +370,7 @@ __device__ __forceinline__ bool walk_step(const ImageView& im, Cursor& c, Path p
         --k;
         const uint32_t p = path(k);
         if (p != NODE_NONE) {
+            if (STATS && st.hist) atomicAdd(st.hist + 50, 1ull);
             path(k) = NODE_NONE;
             c.v = p;
             c.r = k + 1;
