@@ -71,6 +71,10 @@ SIGNATURES = [
     ("tm_node_count", ctypes.c_uint64, [ctypes.c_void_p]),
     ("tm_image_bytes", ctypes.c_uint64, [ctypes.c_void_p]),
     ("tm_filter_bytes", ctypes.c_void_p, [ctypes.c_void_p, ctypes.c_uint32, c_u32p]),
+    ("tm_filters_gather", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
+                                         ctypes.c_uint64, ctypes.c_void_p]),
+    ("tm_dests_gather", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
+                                       ctypes.c_uint64, ctypes.c_void_p]),
     ("tm_match_batch", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
                                       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
                                       c_u64p]),

@@ -134,12 +134,35 @@ static ERL_NIF_TERM nif_delete(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv
 }
 
 static ERL_NIF_TERM filter_binary(ErlNifEnv* env, tm_engine* e, uint32_t fid) {
-    uint32_t len = 0;
-    const uint8_t* p = tm_filter_bytes(e, fid, &len);
+    uint64_t off[2];
+    tm_filters_gather(e, &fid, 1, NULL, 0, off);       /* length, under the engine lock */
     ERL_NIF_TERM bin;
-    unsigned char* d = enif_make_new_binary(env, len, &bin);
-    if (len) memcpy(d, p, len);
+    unsigned char* d = enif_make_new_binary(env, (size_t)off[1], &bin);
+    if (off[1]) tm_filters_gather(e, &fid, 1, d, off[1], off);
     return bin;
+}
+
+/* n filter (or dest) ids -> n binaries, copied under the engine lock in one
+ * call (safe beside subscribers that grow the engine's arenas) */
+static void make_binaries(ErlNifEnv* env, tm_engine* e, const uint32_t* ids, uint32_t n, int dests,
+                          ERL_NIF_TERM* out) {
+    uint64_t* off = (uint64_t*)enif_alloc(sizeof(uint64_t) * (n + 1));
+    uint64_t cap = (uint64_t)n * 48 + 64;
+    uint8_t* buf = (uint8_t*)enif_alloc(cap);
+    int rc = dests ? tm_dests_gather(e, ids, n, buf, cap, off) : tm_filters_gather(e, ids, n, buf, cap, off);
+    if (rc == TM_ENOSPC) {
+        cap = off[n];
+        enif_free(buf);
+        buf = (uint8_t*)enif_alloc(cap ? cap : 1);
+        rc = dests ? tm_dests_gather(e, ids, n, buf, cap, off) : tm_filters_gather(e, ids, n, buf, cap, off);
+    }
+    for (uint32_t k = 0; k < n; ++k) {
+        const size_t len = rc == TM_OK ? (size_t)(off[k + 1] - off[k]) : 0;
+        unsigned char* d = enif_make_new_binary(env, len, &out[k]);
+        if (len) memcpy(d, buf + off[k], len);
+    }
+    enif_free(buf);
+    enif_free(off);
 }
 
 static ERL_NIF_TERM nif_lookup(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
@@ -215,7 +238,7 @@ static ERL_NIF_TERM match_list(ErlNifEnv* env, engine_res* r, ERL_NIF_TERM list,
         for (unsigned i = 0; i < n; ++i) {
             uint32_t c = counts[i];
             ERL_NIF_TERM* cells = (ERL_NIF_TERM*)enif_alloc(sizeof(ERL_NIF_TERM) * (c ? c : 1));
-            for (uint32_t k = 0; k < c; ++k) cells[k] = filter_binary(env, r->e, ids[out_off[i] + k]);
+            make_binaries(env, r->e, ids + out_off[i], c, 0, cells);
             rows[i] = enif_make_list_from_array(env, cells, c);
             enif_free(cells);
         }
@@ -257,19 +280,13 @@ static void async_done(void* ctx, uint64_t ticket, int status, const uint32_t* i
         res = error_tuple(env, status);
     } else {
         ERL_NIF_TERM* cells = (ERL_NIF_TERM*)enif_alloc(sizeof(ERL_NIF_TERM) * (n ? n : 1));
+        ERL_NIF_TERM* db = dests ? (ERL_NIF_TERM*)enif_alloc(sizeof(ERL_NIF_TERM) * (n ? n : 1)) : NULL;
+        if (dests) make_binaries(env, q->r->e, dests, n, 1, db);
         for (uint32_t k = 0; k < n; ++k) {
             ERL_NIF_TERM to = ids[k] == TM_ROUTE_TOPIC ? q->topic : filter_binary(env, q->r->e, ids[k]);
-            if (dests) {
-                uint32_t dl = 0;
-                const uint8_t* dp = tm_dest_bytes(q->r->e, dests[k], &dl);
-                ERL_NIF_TERM db;
-                unsigned char* d = enif_make_new_binary(env, dl, &db);
-                if (dl) memcpy(d, dp, dl);
-                cells[k] = enif_make_tuple2(env, to, db);
-            } else {
-                cells[k] = to;
-            }
+            cells[k] = dests ? enif_make_tuple2(env, to, db[k]) : to;
         }
+        if (db) enif_free(db);
         res = enif_make_list_from_array(env, cells, n);
         enif_free(cells);
     }

@@ -1365,12 +1365,49 @@ uint64_t tm_image_bytes(tm_engine* e) {
 }
 
 const uint8_t* tm_filter_bytes(tm_engine* e, uint32_t fid, uint32_t* len) {
-    if (!e || fid >= e->filters.size() || e->filters[fid].node == NODE_NONE) {
+    if (!e) return nullptr;
+    std::lock_guard<std::recursive_mutex> lk(e->mu);
+    if (fid >= e->filters.size() || e->filters[fid].node == NODE_NONE) {
         if (len) *len = 0;
         return nullptr;
     }
     if (len) *len = e->filters[fid].len;
     return e->filter_arena.data() + e->filters[fid].off;
+}
+
+// bytes of many filters (or dests) copied under the engine lock: safe
+// against a concurrent insert that grows the arena / dest table
+int tm_filters_gather(tm_engine* e, const uint32_t* ids, uint32_t n, uint8_t* buf, uint64_t cap, uint64_t* off) {
+    if (!off || (n && !ids) || (cap && !buf)) return TM_EINVAL;
+    return guarded(e, [&]() -> int {
+        uint64_t o = 0;
+        off[0] = 0;
+        for (uint32_t i = 0; i < n; ++i) {
+            const uint32_t f = ids[i];
+            if (f >= e->filters.size() || e->filters[f].node == NODE_NONE) throw ArgError("unknown filter id");
+            const FilterRec& r = e->filters[f];
+            if (o + r.len <= cap) std::memcpy(buf + o, e->filter_arena.data() + r.off, r.len);
+            o += r.len;
+            off[i + 1] = o;
+        }
+        return o > cap ? TM_ENOSPC : TM_OK;
+    });
+}
+
+int tm_dests_gather(tm_engine* e, const uint32_t* ids, uint32_t n, uint8_t* buf, uint64_t cap, uint64_t* off) {
+    if (!off || (n && !ids) || (cap && !buf)) return TM_EINVAL;
+    return guarded(e, [&]() -> int {
+        uint64_t o = 0;
+        off[0] = 0;
+        for (uint32_t i = 0; i < n; ++i) {
+            if (ids[i] >= e->dest_names.size()) throw ArgError("unknown dest id");
+            const std::string& d = e->dest_names[ids[i]];
+            if (o + d.size() <= cap) std::memcpy(buf + o, d.data(), d.size());
+            o += d.size();
+            off[i + 1] = o;
+        }
+        return o > cap ? TM_ENOSPC : TM_OK;
+    });
 }
 
 int tm_match_batch(tm_engine* e, const uint8_t* topic_bytes, const uint64_t* topic_off, uint32_t n,

@@ -135,20 +135,32 @@ class Engine:
             self._check(rc, "tm_match_batch")
             return counts[:n], offs, ids[: int(needed.value)]
 
+    def filters_bytes(self, ids):
+        """bytes of many filter ids, copied under the engine lock (tm_filters_gather)"""
+        ids = np.ascontiguousarray(ids, dtype=np.uint32)
+        n = len(ids)
+        off = np.zeros(n + 1, dtype=np.uint64)
+        cap = n * 48 + 64
+        while True:
+            buf = np.zeros(max(cap, 1), dtype=np.uint8)
+            rc = self.lib.tm_filters_gather(self.h, _ptr(ids), n, _ptr(buf), cap, _ptr(off))
+            if rc == L.TM_ENOSPC:
+                cap = int(off[-1])
+                continue
+            self._check(rc, "tm_filters_gather")
+            b = buf.tobytes()
+            return [b[int(off[i]):int(off[i + 1])] for i in range(n)]
+
     def match(self, topics):
         """list of topics -> list of lists of filter bytes, reference order."""
         buf, off = pack(topics)
         counts, offs, ids = self.match_batch(buf, off)
-        names = {}
+        uniq, inv = np.unique(ids, return_inverse=True)
+        names = self.filters_bytes(uniq)
         out = []
         for t in range(len(topics)):
-            row = []
-            for fid in ids[int(offs[t]): int(offs[t]) + int(counts[t])]:
-                fid = int(fid)
-                if fid not in names:
-                    names[fid] = self.filter_bytes(fid)
-                row.append(names[fid])
-            out.append(row)
+            a, b = int(offs[t]), int(offs[t]) + int(counts[t])
+            out.append([names[int(k)] for k in inv[a:b]])
         return out
 
     def match_batch_device(self, d_bytes, d_off, n, topic_bytes, d_counts, d_offs, d_ids, out_cap, d_total,

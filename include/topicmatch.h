@@ -123,8 +123,18 @@ uint64_t tm_filter_count(tm_engine* e);
 uint64_t tm_node_count(tm_engine* e);
 uint64_t tm_image_bytes(tm_engine* e);
 
-/* filter id -> filter bytes (the #trie_node.topic binary) */
+/* filter id -> filter bytes (the #trie_node.topic binary).  The pointer is
+ * into the engine's arena: valid until the next insert / delete on e (an
+ * insert may grow the arena).  Threads that match while others subscribe
+ * use tm_filters_gather. */
 const uint8_t* tm_filter_bytes(tm_engine* e, uint32_t filter_id, uint32_t* len);
+
+/* Copy the bytes of n filters (ids[i]) into buf, back to back, under the
+ * engine lock: filter i is buf[off[i] .. off[i+1]) (off has n+1 entries).
+ * TM_ENOSPC when they exceed cap (off[n] = the bytes needed); TM_EINVAL for
+ * an unknown id.  tm_dests_gather does the same for route dest ids. */
+int tm_filters_gather(tm_engine* e, const uint32_t* ids, uint32_t n, uint8_t* buf, uint64_t cap, uint64_t* off);
+int tm_dests_gather(tm_engine* e, const uint32_t* ids, uint32_t n, uint8_t* buf, uint64_t cap, uint64_t* off);
 
 /* emqx_trie:match/1 over a batch — src/emqx_trie.erl:77-79, 121-145, with
  * emqx_topic:words/1 (src/emqx_topic.erl:141-147) done on the device.
@@ -206,7 +216,8 @@ int tm_get_routes(tm_engine* e, const uint8_t* topic, uint32_t tlen, uint32_t* o
 /* number of routes (ets:info(emqx_route, size), emqx_router_helper.erl:148-154) */
 uint64_t tm_route_count(tm_engine* e);
 
-/* dest id -> dest bytes (engine-owned) */
+/* dest id -> dest bytes (engine-owned; valid until the next route add on e,
+ * see tm_dests_gather) */
 const uint8_t* tm_dest_bytes(tm_engine* e, uint32_t dest_id, uint32_t* len);
 
 #define TM_ROUTE_TOPIC 0xFFFFFFFFu   /* route source: the publish topic itself */

@@ -167,3 +167,30 @@ def test_relayout_preserves_bookkeeping(hot, hot_edges):
             for nid in _prefixes(f):
                 assert e.lookup(nid) == py.lookup(nid), nid
         e.close()
+
+
+def test_filters_and_dests_gather():
+    """tm_filters_gather / tm_dests_gather copy under the engine lock; ENOSPC
+    reports the bytes needed; unknown ids are refused"""
+    e = Engine(device=-1)
+    fs = [b"a/+", b"", b"b/#", b"+/+/c" * 20]
+    for f in fs:
+        e.insert(f)                     # filter ids 0..3 in insertion order
+    assert e.filters_bytes([0, 1, 2, 3]) == fs
+    assert e.filters_bytes([3, 3, 0]) == [fs[3], fs[3], fs[0]]
+    assert e.filters_bytes([]) == []
+    import ctypes
+    off = (ctypes.c_uint64 * 3)()
+    buf = (ctypes.c_uint8 * 4)()
+    idarr = (ctypes.c_uint32 * 2)(3, 0)
+    assert e.lib.tm_filters_gather(e.h, idarr, 2, buf, 4, off) == _lib.TM_ENOSPC
+    assert off[2] == len(fs[3]) + len(fs[0])
+    bad = (ctypes.c_uint32 * 1)(99)
+    assert e.lib.tm_filters_gather(e.h, bad, 1, buf, 4, off) == _lib.TM_EINVAL
+    e.route_add(b"a/+", b"node1")
+    e.route_add(b"x", b"node2")
+    d = (ctypes.c_uint32 * 2)(1, 0)
+    big = (ctypes.c_uint8 * 64)()
+    assert e.lib.tm_dests_gather(e.h, d, 2, big, 64, off) == _lib.TM_OK
+    assert bytes(big[:off[2]]) == b"node2node1"
+    e.close()
