@@ -286,12 +286,20 @@ struct tm_batcher {
             if (pending.load(std::memory_order_acquire) == 0) {
                 cv_idle.notify_all();
                 if (stop) return;
-                cv_work.wait_for(lk, std::chrono::milliseconds(50));
+                sleep_for(lk, std::chrono::milliseconds(50));
             } else {
                 const int64_t left = first_ns.load() + (int64_t)cfg.deadline_us * 1000 - now_ns();
-                if (left > 0) cv_work.wait_for(lk, std::chrono::nanoseconds(left));
+                if (left > 0) sleep_for(lk, std::chrono::nanoseconds(left));
             }
         }
+    }
+
+    // timed wait on the system clock (pthread_cond_timedwait): libstdc++'s
+    // steady-clock wait uses pthread_cond_clockwait, which GCC 11's TSan does
+    // not intercept (bogus "double lock" reports); a woken-early wait just loops
+    template <class D>
+    void sleep_for(std::unique_lock<std::mutex>& lk, D d) {
+        cv_work.wait_until(lk, std::chrono::system_clock::now() + d);
     }
 
     void kick() {
