@@ -224,7 +224,10 @@ def test_stats_edge_reads_match_oracle(gpu_device, golden):
 
 VARIANTS = {"queue": {}, "queue_xcd": {}, "queue_xcd@nosplit@dfs": {"split": 0, "hot_levels": 0},
             "queue_xcd@hot3": {"hot_levels": 3, "layout": 2}, "queue_xcd@nosplit@hot2": {"split": 0, "hot_levels": 2},
-            "queue_xcd@nohotedges": {"hot_edges": 0}, "queue_xcd@hotedges5@relayout": {"hot_edges": 5, "layout": 2}}
+            "queue_xcd@nohotedges": {"hot_edges": 0}, "queue_xcd@hotedges5@relayout": {"hot_edges": 5, "layout": 2},
+            "queue_xcd@plusfirst": {"order": 1, "layout": 2}, "queue_xcd@hashlast": {"order": 2, "layout": 2},
+            "queue_xcd@order3@dfs": {"order": 3, "hot_levels": 0, "layout": 2},
+            "queue_xcd@order0": {"order": 0, "layout": 2}}
 
 
 @pytest.mark.parametrize("variant", list(VARIANTS))
