@@ -16,6 +16,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -193,10 +194,12 @@ struct tm_engine {
     size_t created_since_layout = 0;  // nodes created since the last relayout
     uint32_t hot_levels = 4;          // option "hot_levels": relayout puts depths <= H level by level (BFS)
                                       // first, then DFS-preorder subtrees (0 = DFS throughout)
-    uint32_t layout_order = 0;        // option "order": bit 0 = a node's '+' child directly follows it
+    uint32_t edge_div = 4;            // option "edge_load": edge tables kept at load <= 1/edge_div
+    uint32_t layout_order = 7;        // option "order" (default 7; A/B at C3, walk ms: 0 3.90, 1 3.84, 7 3.66): bit 0 = a node's '+' child directly follows it
                                       // (the walk's most frequent step, 67 of 101 visits per topic at
                                       // C3, then lands in the line the parent's load fetched); bit 1 =
-                                      // '#' nodes (never visited with words left) moved to the end
+                                      // '#' nodes (never visited with words left) moved to the end;
+                                      // bit 2 = heat order (heat_sort)
     bool force_relayout = false;
     int split_halves = 1;             // option "split": walk reads separate inner / leaf half arrays
     bool split_stale = true;
@@ -368,7 +371,7 @@ struct tm_engine {
     }
     void edge_insert(uint32_t parent, uint32_t word, uint32_t child) {
         EdgeTable& t = tab(parent);
-        if ((t.used + 1) * 4 > t.slots.size()) edge_grow(t);
+        if ((t.used + 1) * edge_div > t.slots.size()) edge_grow(t);
         place_in(t, slot_for(parent, word, child));
         ++t.used;
     }
@@ -735,6 +738,51 @@ struct tm_engine {
     }
 
     // ------------------------------------------------------------------
+    // Heat order (option "order" bit 2): nodes sorted by the estimated share
+    // of publishes that visit them, hottest first, so each 64 B line of the
+    // hot end of inner[] holds four hot halves and the set a cache level can
+    // hold is as hot as it gets.  A topic visits v iff its words equal v's
+    // literal levels ('+' levels take any word), so heat(v) = product over
+    // v's literal levels of P(word); P is estimated from the trie itself (a
+    // word's share of all literal edges: subscriptions and publishes draw on
+    // one vocabulary).  '#' nodes are never visited with words left: last.
+    // The sort is stable over the preorder built above, so a node and its
+    // '+' child (equal heat) stay adjacent.
+    void heat_sort(std::vector<uint32_t>& order, std::vector<uint32_t>& newid, uint32_t& new_hot_limit) {
+        std::unordered_map<uint32_t, uint64_t> wcnt;
+        uint64_t total = 0;
+        for (uint32_t v : order)
+            if (v != ROOT && aux[v].word < WORD_MAX) {
+                ++wcnt[aux[v].word];
+                ++total;
+            }
+        std::unordered_map<uint32_t, double> wlog;
+        wlog.reserve(wcnt.size());
+        for (const auto& kv : wcnt) wlog[kv.first] = std::log((double)kv.second / (double)total);
+        std::vector<double> heat(nodes.size(), 0.0);   // log P(visit)
+        const double COLD = -1e300;
+        for (uint32_t v : order) {
+            if (v == ROOT) continue;
+            const uint32_t p = aux[v].parent, w = aux[v].word;
+            const double hp = heat[p];
+            heat[v] = w == WORD_PLUS ? hp : w == WORD_HASH || hp == COLD ? COLD : hp + wlog[w];
+        }
+        struct Key {
+            double h;
+            uint32_t i;   // position in the preorder (ties keep it)
+        };
+        std::vector<Key> keys(order.size());
+        for (size_t i = 0; i < order.size(); ++i) keys[i] = Key{heat[order[i]], (uint32_t)i};
+        std::vector<double>().swap(heat);
+        std::sort(keys.begin(), keys.end(), [](const Key& a, const Key& b) { return a.h > b.h || (a.h == b.h && a.i < b.i); });
+        std::vector<uint32_t> sorted(order.size());
+        for (size_t i = 0; i < keys.size(); ++i) sorted[i] = order[keys[i].i];
+        order.swap(sorted);
+        for (size_t i = 0; i < order.size(); ++i) newid[order[i]] = (uint32_t)i;
+        new_hot_limit = 0;   // the depth-based hot edge table does not apply
+    }
+
+    // ------------------------------------------------------------------
     // DFS-preorder relayout: renumber the live nodes so that every subtree is
     // a contiguous id range and a node's first child in walk order (its
     // literal children, then its '+' child: the walk runs in the reference's
@@ -826,6 +874,7 @@ struct tm_engine {
         }
         std::vector<uint32_t>().swap(kids);
         std::vector<uint32_t>().swap(start);
+        if (layout_order & 4) heat_sort(order, newid, new_hot_limit);
         auto remap = [&](uint32_t id) { return id == NODE_NONE ? NODE_NONE : newid[id]; };
         std::vector<Node> nn(order.size());
         std::vector<NodeAux> na(order.size());
@@ -855,8 +904,12 @@ struct tm_engine {
         hot_limit = new_hot_limit;
         size_t nhot = 0;
         for (const EdgeSlot& e : old) nhot += newid[e.parent] < hot_limit;
-        cold.slots.assign(std::max<size_t>(1024, next_pow2((old.size() - nhot) * 4 + 1)), kEmptySlot);
-        hot.slots.assign(std::max<size_t>(1024, next_pow2(nhot * 4 + 1)), kEmptySlot);
+        cold.slots.assign(std::max<size_t>(1024, next_pow2((old.size() - nhot) * edge_div + 1)), kEmptySlot);
+        hot.slots.assign(std::max<size_t>(1024, next_pow2(nhot * edge_div + 1)), kEmptySlot);
+        // placed in order of the children's new ids: under the heat order the
+        // most visited edges are placed first and sit in their home slots
+        std::sort(old.begin(), old.end(),
+                  [&](const EdgeSlot& a, const EdgeSlot& b) { return newid[a.child] < newid[b.child]; });
         for (const EdgeSlot& e : old) {
             edge_place(slot_for(newid[e.parent], e.word, newid[e.child]));
             ++tab(newid[e.parent]).used;
@@ -1751,8 +1804,17 @@ int tm_set_option(tm_engine* e, const char* name, int64_t value) {
             }
             return TM_OK;
         }
+        if (!std::strcmp(name, "edge_load")) {
+            if (value < 2 || value > 16) return TM_EINVAL;
+            if ((uint32_t)value != e->edge_div) {
+                e->edge_div = (uint32_t)value;
+                e->force_relayout = true;
+                e->dev_dirty = true;
+            }
+            return TM_OK;
+        }
         if (!std::strcmp(name, "order")) {
-            if (value < 0 || value > 3) return TM_EINVAL;
+            if (value < 0 || value > 7) return TM_EINVAL;
             if ((uint32_t)value != e->layout_order) {
                 e->layout_order = (uint32_t)value;
                 e->force_relayout = true;

@@ -139,17 +139,21 @@ def test_router_kat_host_side(golden):
             assert r.engine.lookup(b(node)) == exp
 
 
-@pytest.mark.parametrize("hot,hot_edges", [(0, 0), (1, 3), (3, 2), (3, 3), (4, 5)])
-def test_relayout_preserves_bookkeeping(hot, hot_edges):
+@pytest.mark.parametrize("hot,hot_edges,order", [(0, 0, 0), (1, 3, 1), (3, 2, 2), (3, 3, 3), (4, 5, 1), (4, 0, 5),
+                                                 (0, 0, 7)])
+def test_relayout_preserves_bookkeeping(hot, hot_edges, order):
     """DFS-preorder relayout on every commit (layout=2), with depths <= hot
-    laid out level by level first, keeps emqx_trie's bookkeeping
-    (edge_count, topic) and the filter ids intact"""
-    rng = random.Random(31 + hot + 7 * hot_edges)
+    laid out level by level first ('+' child first / '#' nodes last / heat
+    order per `order`), keeps emqx_trie's bookkeeping (edge_count, topic)
+    and the filter ids intact"""
+    rng = random.Random(31 + hot + 7 * hot_edges + 101 * order)
     for _ in range(25):
         e, py = kat_engine(), pytrie.Trie()
         e.set_option("layout", 2)
         e.set_option("hot_levels", hot)
         e.set_option("hot_edges", hot_edges)
+        e.set_option("order", order)
+        e.set_option("edge_load", 2 + (order % 3) * 3)
         pool = [b"/".join(rng.choice([b"a", b"b", b"", b"+", b"#", b"$x", b"c", b"d", b"e"])
                           for _ in range(rng.randint(1, 6))) for _ in range(rng.randint(5, 120))]
         for step in range(300):

@@ -24,7 +24,7 @@ sys.path.insert(0, ROOT)
 from emqx_amd import Engine  # noqa: E402
 from emqx_amd import workload as W  # noqa: E402
 
-BUILD_OPTS = ("hot_levels", "layout", "hot_edges", "order")
+BUILD_OPTS = ("hot_levels", "layout", "hot_edges", "order", "edge_load")
 
 
 def log(*a):

@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 OUT=gpurun_out/${TAG:-abvar}
 mkdir -p $OUT
 A="--steps 30 --warmup 3 --check 2000 --cpu-sample 0 ${BENCH_ARGS}"
-timeout -k 10 200 python -u bench.py $A --lib emqx_amd/variants/libtopicmatch_base.so > $OUT/base1.json 2> $OUT/base1.log && \
+timeout -k 10 200 python -u bench.py $A --lib emqx_amd/variants/libtopicmatch_${VAR:-base}.so > $OUT/base1.json 2> $OUT/base1.log && \
 timeout -k 10 200 python -u bench.py $A > $OUT/new1.json 2> $OUT/new1.log && \
-timeout -k 10 200 python -u bench.py $A --lib emqx_amd/variants/libtopicmatch_base.so > $OUT/base2.json 2> $OUT/base2.log && \
+timeout -k 10 200 python -u bench.py $A --lib emqx_amd/variants/libtopicmatch_${VAR:-base}.so > $OUT/base2.json 2> $OUT/base2.log && \
 timeout -k 10 200 python -u bench.py $A > $OUT/new2.json 2> $OUT/new2.log
