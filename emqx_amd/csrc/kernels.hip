@@ -236,6 +236,8 @@ constexpr int HIST_OFF = 8;   // hist = stats + HIST_OFF
 struct Cursor {
     uint32_t v, r, n, r0;   // node to visit next and its level; topic levels; start level
     uint64_t key;           // KEYS: fold branches taken above level r (rank_sym)
+    uint64_t s;             // probe: the edge slot the next load reads
+    bool probe;             // next load: edge slot s of (v, W(r)) rather than v's node half
 };
 
 // Order keys (sharded mode).  Every match of a topic is identified by the
@@ -289,6 +291,7 @@ __device__ __forceinline__ bool walk_begin(const ImageView& im, Cursor& c, uint3
                                            WalkStats& st) {
     c.n = n;
     c.key = 0;
+    c.probe = false;
     if (!dollar) {
         c.v = ROOT;
         c.r = c.r0 = 0;
@@ -306,8 +309,8 @@ __device__ __forceinline__ bool walk_begin(const ImageView& im, Cursor& c, uint3
 // (EdgeSlot), so it is visited in the same step, and so on down a chain of
 // table children, until a child needs its own load or the walk pops.
 template <bool STATS, bool KEYS, class Path, class Words, class Emit>
-__device__ __forceinline__ bool walk_step(const ImageView& im, Cursor& c, Path path, const Words& W, Emit& emit,
-                                          WalkStats& st) {
+__device__ __forceinline__ bool walk_step2(const ImageView& im, Cursor& c, Path path, const Words& W, Emit& emit,
+                                           WalkStats& st) {
     uint32_t v = c.v, r = c.r;
     uint64_t key = KEYS ? c.key : 0ull;
     bool leaf = r == c.n;
@@ -379,6 +382,140 @@ __device__ __forceinline__ bool walk_step(const ImageView& im, Cursor& c, Path p
         }
     }
     return true;
+}
+
+// pop to the deepest '+' child pending above level r; true when none is
+// left (the topic's walk is complete)
+template <bool STATS, bool KEYS, class Path>
+__device__ __forceinline__ bool walk_pop(Cursor& c, Path path, uint32_t r, uint64_t key, WalkStats& st) {
+    for (uint32_t k = r; k > c.r0;) {
+        --k;
+        const uint32_t p = path(k);
+        if (p != NODE_NONE) {
+            if (STATS && st.hist) atomicAdd(st.hist + 50, 1ull);
+            path(k) = NODE_NONE;
+            c.v = p;
+            c.r = k + 1;
+            if (KEYS) c.key = rank_prefix(key, k) | rank_sym(k, 2);
+            return false;
+        }
+    }
+    return true;
+}
+
+// One step = ONE 16 B load per lane, so every lane of a wave pays one
+// memory round trip per step: either node v's half (inner with words left,
+// leaf at the last level) or, when v is WIDE and its Bloom mask admits the
+// topic word, the next slot of the edge probe for (v, W(r)).  (walk_step2
+// resolves the probe inside the node's step: a wave whose lanes mix probing
+// and non-probing steps then pays two dependent round trips per step.)
+// The '+' child of v is parked in path(r) while the probe runs.
+template <bool STATS, bool KEYS, class Path, class Words, class Emit>
+__device__ __forceinline__ bool walk_step1(const ImageView& im, Cursor& c, Path path, const Words& W, Emit& emit,
+                                           WalkStats& st) {
+    const uint32_t v = c.v, r = c.r;
+    const uint64_t key = KEYS ? c.key : 0ull;
+    const bool hot = v < im.hot_limit;
+    const EdgeSlot* tab = hot ? im.hot_edges : im.edges;
+    const uint64_t mask = hot ? im.hot_slot_mask : im.edge_slot_mask;
+    const bool leaf = !c.probe && r == c.n;
+    const uint8_t* addr = c.probe ? reinterpret_cast<const uint8_t*>(tab + c.s)
+                                  : (leaf ? im.leaf : im.inner) + ((uint64_t)v << im.node_shift);
+    const uint4 h = *reinterpret_cast<const uint4*>(addr);
+    if (c.probe) {
+        if (STATS) {
+            ++st.probe_loads;
+            if (st.hist) atomicAdd(st.hist + 16 + (r < 15 ? r : 15), 1ull);
+        }
+        if (h.x == v && h.y == W(r)) {   // literal child from the table; '+' child stays pending
+            if (STATS && st.hist) atomicAdd(st.hist + 49, 1ull);
+            c.probe = false;
+            c.v = h.z;
+            c.r = r + 1;
+            if (KEYS) c.key = key | rank_sym(r, 1);
+            return false;
+        }
+        if (h.x != EDGE_EMPTY) {          // linear probing
+            c.s = (c.s + 1) & mask;
+            return false;
+        }
+        if (STATS && st.hist) atomicAdd(st.hist + 32 + (r < 15 ? r : 15), 1ull);
+        c.probe = false;                  // no literal child: into the '+' subtree
+        const uint32_t pc = path(r);
+        if (pc != NODE_NONE) {
+            if (STATS && st.hist) atomicAdd(st.hist + 50, 1ull);
+            path(r) = NODE_NONE;
+            c.v = pc;
+            c.r = r + 1;
+            if (KEYS) c.key = key | rank_sym(r, 2);
+            return false;
+        }
+        return walk_pop<STATS, KEYS>(c, path, r, key, st);
+    }
+    if (STATS) {
+        ++st.visits;
+        st.edge_reads += leaf ? 1 : 3;   // 'match_#' (:141) + fold over [W, '+'] (:132)
+        st.leaf_visits += leaf ? 1 : 0;
+        if (st.hist && !leaf) atomicAdd(st.hist + (r < 15 ? r : 15), 1ull);
+    }
+    if (h.y != FILTER_NONE) emit(h.y, key);   // 'match_#': the '#' filter
+    if (leaf) {
+        if (h.x != FILTER_NONE) emit(h.x, KEYS ? key | rank_sym(r, 1) : 0ull);   // the node's own filter (:128)
+        return walk_pop<STATS, KEYS>(c, path, r, key, st);
+    }
+    const uint32_t plus = h.x, pc = plus & NODE_MASK, w = W(r);
+    uint32_t child = NODE_NONE;
+    bool probe = false;
+    if (w < WORD_MAX) {
+        if (!(plus & WIDE)) {
+            child = h.z == w ? h.w : NODE_NONE;
+        } else {
+            const uint64_t b = word_bloom(w);
+            probe = ((((uint64_t)h.w << 32) | h.z) & b) == b;
+        }
+    } else if (w == WORD_PLUS) {   // out-of-domain topic level "+": the fold follows the '+' edge
+        child = pc;
+    } else if (w == WORD_HASH) {
+        probe = true;
+    }
+    if (probe) {
+        path(r) = pc;
+        c.probe = true;
+        c.s = edge_home(v, w, mask);
+        return false;
+    }
+    if (child != NODE_NONE) {   // literal subtree first, '+' child pending at level r
+        if (STATS && st.hist) atomicAdd(st.hist + 48, 1ull);
+        path(r) = pc;
+        c.v = child;
+        c.r = r + 1;
+        if (KEYS) c.key = key | rank_sym(r, 1);
+        return false;
+    }
+    if (pc != NODE_NONE) {      // no literal child: straight into the '+' subtree
+        if (STATS && st.hist) atomicAdd(st.hist + 50, 1ull);
+        path(r) = NODE_NONE;
+        c.v = pc;
+        c.r = r + 1;
+        if (KEYS) c.key = key | rank_sym(r, 2);
+        return false;
+    }
+    return walk_pop<STATS, KEYS>(c, path, r, key, st);
+}
+
+// TM_WALK1=1 selects walk_step1.  Measured at C3 (heat layout): walk 4.10 ms
+// vs 3.59 ms for walk_step2 (profiles/r01_v12_heat/walk1_ab.json): the walk
+// is bound by the memory system's random-request rate, not by lanes idling
+// behind a neighbour's probe, and the extra loop iterations cost.  Kept as a
+// compile-time A/B variant, off.
+#ifndef TM_WALK1
+#define TM_WALK1 0
+#endif
+template <bool STATS, bool KEYS, class Path, class Words, class Emit>
+__device__ __forceinline__ bool walk_step(const ImageView& im, Cursor& c, Path path, const Words& W, Emit& emit,
+                                          WalkStats& st) {
+    if (TM_WALK1) return walk_step1<STATS, KEYS>(im, c, path, W, emit, st);
+    return walk_step2<STATS, KEYS>(im, c, path, W, emit, st);
 }
 
 template <bool STATS, bool KEYS, class Path, class Words, class Emit>
