@@ -189,7 +189,7 @@ def main():
                 assert int(d_t.item()) == total
         log("A/B ms/step (median, min): " + ", ".join(
             "%s %.2f/%.2f" % (v, sorted(x)[len(x) // 2], min(x)) for v, x in res.items()))
-        configure(a.walk or "queue")
+        configure(a.walk or "queue_xcd")
 
     # ---- timed region: K steps, kernel events recorded on the launch stream;
     # barrier + sync on both sides, max over ranks (emqx_amd/multi.py)

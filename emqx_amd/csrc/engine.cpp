@@ -195,11 +195,11 @@ struct tm_engine {
     uint32_t hot_levels = 4;          // option "hot_levels": relayout puts depths <= H level by level (BFS)
                                       // first, then DFS-preorder subtrees (0 = DFS throughout)
     uint32_t edge_div = 4;            // option "edge_load": edge tables kept at load <= 1/edge_div
-    uint32_t layout_order = 7;        // option "order" (default 7; A/B at C3, walk ms: 0 3.90, 1 3.84, 7 3.66): bit 0 = a node's '+' child directly follows it
+    uint32_t layout_order = 15;       // option "order" (default 15; A/B at C3, walk ms: 0 3.90, 1 3.84, 7 3.51-3.66, 15 3.44): bit 0 = a node's '+' child directly follows it
                                       // (the walk's most frequent step, 67 of 101 visits per topic at
                                       // C3, then lands in the line the parent's load fetched); bit 1 =
                                       // '#' nodes (never visited with words left) moved to the end;
-                                      // bit 2 = heat order (heat_sort)
+                                      // bit 2 = heat order (heat_sort); bit 3 = heat from filter counts
     bool force_relayout = false;
     int split_halves = 1;             // option "split": walk reads separate inner / leaf half arrays
     bool split_stale = true;
@@ -751,11 +751,25 @@ struct tm_engine {
     void heat_sort(std::vector<uint32_t>& order, std::vector<uint32_t>& newid, uint32_t& new_hot_limit) {
         std::unordered_map<uint32_t, uint64_t> wcnt;
         uint64_t total = 0;
-        for (uint32_t v : order)
-            if (v != ROOT && aux[v].word < WORD_MAX) {
-                ++wcnt[aux[v].word];
-                ++total;
+        if (layout_order & 8) {   // P(word) from the filters through each edge (subtree filter counts)
+            std::vector<uint32_t> sub(nodes.size(), 0);
+            for (size_t i = order.size(); i-- > 0;) {   // preorder reversed: children before parents
+                const uint32_t v = order[i];
+                sub[v] += nodes[v].self_filter != FILTER_NONE ? 1u : 0u;
+                if (v == ROOT) continue;
+                sub[aux[v].parent] += sub[v];
+                if (aux[v].word < WORD_MAX) {
+                    wcnt[aux[v].word] += sub[v];
+                    total += sub[v];
+                }
             }
+        } else {                  // P(word) from the number of edges labelled with it
+            for (uint32_t v : order)
+                if (v != ROOT && aux[v].word < WORD_MAX) {
+                    ++wcnt[aux[v].word];
+                    ++total;
+                }
+        }
         std::unordered_map<uint32_t, double> wlog;
         wlog.reserve(wcnt.size());
         for (const auto& kv : wcnt) wlog[kv.first] = std::log((double)kv.second / (double)total);
@@ -1814,7 +1828,7 @@ int tm_set_option(tm_engine* e, const char* name, int64_t value) {
             return TM_OK;
         }
         if (!std::strcmp(name, "order")) {
-            if (value < 0 || value > 7) return TM_EINVAL;
+            if (value < 0 || value > 15) return TM_EINVAL;
             if ((uint32_t)value != e->layout_order) {
                 e->layout_order = (uint32_t)value;
                 e->force_relayout = true;
