@@ -64,6 +64,7 @@ def parse():
     ap.add_argument("--presort", action="store_true",
                     help="EXPERIMENT: sort the batch by topic bytes on the host before upload (untimed)")
     ap.add_argument("--layout", type=int, default=None, help="1 = DFS relayout on commit (default), 0 = off")
+    ap.add_argument("--opt", action="append", default=[], help="EXPERIMENT: engine option name=value (repeatable)")
     return ap.parse_args()
 
 
@@ -97,6 +98,9 @@ def main():
         eng.set_option("stage_k", a.stage_k)
     if a.layout is not None:
         eng.set_option("layout", a.layout)
+    for kv in a.opt:
+        k, x = kv.split("=")
+        eng.set_option(k, int(x))
     eng.insert_many(fb, fo)
     eng.commit()
     log("rank %d: trie built + committed in %.1fs: %d filters, %d nodes, image %.2f GB" % (
