@@ -64,6 +64,8 @@ def parse():
     ap.add_argument("--presort", action="store_true",
                     help="EXPERIMENT: sort the batch by topic bytes on the host before upload (untimed)")
     ap.add_argument("--layout", type=int, default=None, help="1 = DFS relayout on commit (default), 0 = off")
+    ap.add_argument("--presort-level", type=int, default=None,
+                    help="EXPERIMENT: sort the batch by the word at this level on the host (untimed)")
     ap.add_argument("--opt", action="append", default=[], help="EXPERIMENT: engine option name=value (repeatable)")
     return ap.parse_args()
 
@@ -109,9 +111,13 @@ def main():
     tb, to = W.topics(a.config, n=a.topics, stream=multi.topic_stream(rank))
     n = len(to) - 1
     nbytes = int(to[-1])
-    if a.presort:
+    if a.presort or a.presort_level is not None:
         ts = [bytes(tb[to[i]:to[i + 1]]) for i in range(n)]
-        ts.sort()
+        if a.presort_level is not None:   # by the word at one level (then the whole topic)
+            lv = a.presort_level
+            ts.sort(key=lambda t: (t.split(b"/")[lv:lv + 1], t))
+        else:
+            ts.sort()
         lens = np.fromiter((len(t) for t in ts), dtype=np.uint64, count=n)
         to = np.zeros(n + 1, dtype=np.uint64)
         np.cumsum(lens, out=to[1:])

@@ -190,6 +190,7 @@ struct tm_engine {
     int hist_enabled = 0;             // option "hist": per-level histogram in stats mode (diagnostic, slow)
     uint32_t walk_bpc = 0;            // option "walk_bpc": walk blocks per CU (0 = full occupancy)
     int xcdq = 1;                     // option "xcdq": per-XCD dequeue ranges in the queue walk (default on)
+    int group = 0;                    // option "group": walk the batch in topic-group order (kernels.hip; A/B at C3: no gain, off)
     int layout_mode = 1;              // option "layout": 0 off, 1 auto, 2 every commit (tests)
     size_t created_since_layout = 0;  // nodes created since the last relayout
     uint32_t hot_levels = 4;          // option "hot_levels": relayout puts depths <= H level by level (BFS)
@@ -224,7 +225,7 @@ struct tm_engine {
     // walk of one beside the tokenizer / copy-out of its neighbours); a
     // slot's next user waits for its previous batch (hipStreamWaitEvent)
     struct Slot {
-        DevBuf twords, words, path, meta, scan, stage, kstage, ws, stats;
+        DevBuf twords, words, path, meta, scan, stage, kstage, ws, stats, perm;
         uint64_t* h_maxc = nullptr;     // pinned: largest match count of the slot's last walk
         hipEvent_t maxc_ev = nullptr, done = nullptr;
         bool maxc_pending = false, used = false;
@@ -1087,6 +1088,7 @@ struct tm_engine {
         w.stage.ensure(((size_t)n * stage_k + 4) * 4);
         if (keys) w.kstage.ensure(((size_t)n * stage_k + 4) * 8);
         w.ws.ensure(QWS_BYTES);
+        if (group) w.perm.ensure(((size_t)n + GROUP_WS_ELEMS) * 4);
         if (!w.done) HIPCHK(hipEventCreateWithFlags(&w.done, hipEventDisableTiming));
     }
 
@@ -1150,6 +1152,7 @@ struct tm_engine {
         qb.kstage = keys ? w.kstage.as<uint64_t>() : nullptr;
         qb.scan_tmp = w.scan.as<uint64_t>();
         qb.ws = w.ws.as<unsigned long long>();
+        qb.perm = group ? w.perm.as<uint32_t>() : nullptr;
         HIPCHK(launch_queue(stats_enabled, xcdq != 0, im, bytes, off, n, qb, stage_k, counts, out_off, ids, keys, cap,
                             total, sp, st, timing_enabled ? marks : nullptr, walk_bpc, hist_enabled != 0));
         record_maxc(w, st);
@@ -1792,6 +1795,11 @@ int tm_set_option(tm_engine* e, const char* name, int64_t value) {
         if (!std::strcmp(name, "walk_bpc")) {
             if (value < 0 || value > 64) return TM_EINVAL;
             e->walk_bpc = (uint32_t)value;
+            return TM_OK;
+        }
+        if (!std::strcmp(name, "group")) {
+            if (value < 0 || value > 1) return TM_EINVAL;
+            e->group = (int)value;
             return TM_OK;
         }
         if (!std::strcmp(name, "xcdq")) {

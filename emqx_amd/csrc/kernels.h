@@ -23,7 +23,9 @@ struct QueueBufs {
     uint64_t* kstage;     // n x K order keys (sharded mode), or null
     uint64_t* scan_tmp;   // scan_tmp_elems(n)
     unsigned long long* ws;   // QWS_BYTES of queue heads
+    uint32_t* perm;       // group order (option "group"): n positions + 2 x 1024 group counts / cursors, or null
 };
+constexpr uint32_t GROUP_WS_ELEMS = 2048;   // u32 after the n positions of perm
 
 // tokenize -> NFA walk -> scan -> copy-out, all on st.  marks: 8 events,
 // [2i] before / [2i+1] after stage i, or null.  out_cap == 0: counts and

@@ -142,11 +142,24 @@ __device__ __forceinline__ uint32_t tokenize_topic(const ImageView& im, const ui
 
 constexpr uint32_t MLONG = 1u << 30, MDOLLAR = 1u << 31, MN = (1u << 30) - 1;   // meta bits
 
-__global__ void __launch_bounds__(BLOCK)
-tm_tokenize(ImageView im, const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint32_t n,
-            uint32_t* __restrict__ twords, uint32_t* __restrict__ words, uint32_t* __restrict__ meta) {
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= n) return;
+// Topic groups (option "group"): the walk takes the batch in the order of a
+// group key of the first two words, so each XCD's dequeue range (and each
+// 64-topic chunk) holds topics that share the top of their paths: the nodes
+// below a root word are then walked by one XCD and cached in its L2.
+// Host presort A/B at C3 (profiles/r01_v12_heat/presort, each sort key
+// followed by the whole topic): whole topic -7.2 % walk time, root word
+// -6.1 %, level-4 word +0 %; this one-pass grouping by (w0, w1) hashes
+// measured no gain (3.88 vs 3.88 ms per step): the presort gain comes from
+// neighbours sharing whole prefixes, which takes a full sort.  Off.
+constexpr uint32_t NGROUP = 1024;
+__device__ __forceinline__ uint32_t group_of(uint32_t w0, uint32_t w1) {
+    return (((w0 * 0x9E3779B1u) >> 26) << 4) | ((w1 * 0x85EBCA6Bu) >> 28);
+}
+
+__device__ __forceinline__ void tokenize_one(const ImageView& im, const uint8_t* __restrict__ bytes,
+                                             const uint64_t* __restrict__ off, uint32_t t,
+                                             uint32_t* __restrict__ twords, uint32_t* __restrict__ words,
+                                             uint32_t* __restrict__ meta, uint32_t* lh) {
     const uint64_t b = off[t], e = off[t + 1];
     uint32_t tw[WREG];
 #pragma unroll
@@ -160,7 +173,69 @@ tm_tokenize(ImageView im, const uint8_t* __restrict__ bytes, const uint64_t* __r
         row[k] = make_uint4(tw[4 * k], tw[4 * k + 1], tw[4 * k + 2], tw[4 * k + 3]);
     const uint32_t dollar = (e > b && bytes[b] == '$') ? 1u : 0u;
     meta[t] = lev | (dollar << 31) | (lev > WREG ? MLONG : 0u);
+    if (lh) atomicAdd(lh + group_of(tw[0], tw[1]), 1u);
 }
+
+__global__ void __launch_bounds__(BLOCK)
+tm_tokenize(ImageView im, const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint32_t n,
+            uint32_t* __restrict__ twords, uint32_t* __restrict__ words, uint32_t* __restrict__ meta,
+            uint32_t* __restrict__ ghist) {
+    __shared__ uint32_t lh[NGROUP];
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (ghist) {
+        for (uint32_t k = threadIdx.x; k < NGROUP; k += BLOCK) lh[k] = 0;
+        __syncthreads();
+    }
+    if (t < n) tokenize_one(im, bytes, off, t, twords, words, meta, ghist ? lh : nullptr);
+    if (ghist) {
+        __syncthreads();
+        for (uint32_t k = threadIdx.x; k < NGROUP; k += BLOCK)
+            if (lh[k]) atomicAdd(ghist + k, lh[k]);
+    }
+}
+
+// exclusive scan of the group histogram -> group cursors (one block)
+__global__ void __launch_bounds__(BLOCK) tm_group_scan(const uint32_t* __restrict__ ghist, uint32_t* __restrict__ gcur) {
+    __shared__ uint64_t lds[BLOCK / 64];
+    constexpr uint32_t PER = NGROUP / BLOCK;
+    uint32_t v[PER], sum = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < PER; ++k) {
+        v[k] = ghist[threadIdx.x * PER + k];
+        sum += v[k];
+    }
+    uint64_t tot;
+    uint32_t ex = (uint32_t)block_exclusive_scan(sum, lds, tot);
+#pragma unroll
+    for (uint32_t k = 0; k < PER; ++k) {
+        gcur[threadIdx.x * PER + k] = ex;
+        ex += v[k];
+    }
+}
+
+// perm[position] = topic: a block ranks its topics per group in LDS and
+// reserves each group's range with one global atomic
+__global__ void __launch_bounds__(BLOCK)
+tm_group_scatter(const uint32_t* __restrict__ twords, uint32_t n, uint32_t* __restrict__ gcur,
+                 uint32_t* __restrict__ perm) {
+    __shared__ uint32_t lh[NGROUP];
+    __shared__ uint32_t lb[NGROUP];
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    for (uint32_t k = threadIdx.x; k < NGROUP; k += BLOCK) lh[k] = 0;
+    __syncthreads();
+    uint32_t g = 0, r = 0;
+    if (t < n) {
+        const uint2 w = *reinterpret_cast<const uint2*>(twords + (uint64_t)t * WREG);
+        g = group_of(w.x, w.y);
+        r = atomicAdd(lh + g, 1u);
+    }
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < NGROUP; k += BLOCK)
+        if (lh[k]) lb[k] = atomicAdd(gcur + k, lh[k]);
+    __syncthreads();
+    if (t < n) perm[lb[g] + r] = t;
+}
+
 
 // ---------------------------------------------------------------------------
 // The child found by a probe, with its record when the edge table delivered
@@ -619,7 +694,7 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
               const uint32_t* __restrict__ words, const uint32_t* __restrict__ meta, uint32_t* __restrict__ gpath,
               uint32_t* __restrict__ stage, uint64_t* __restrict__ kstage, uint32_t K, uint32_t* __restrict__ counts,
               unsigned long long* __restrict__ ws, unsigned long long* __restrict__ stats,
-              unsigned long long* __restrict__ hist) {
+              unsigned long long* __restrict__ hist, const uint32_t* __restrict__ perm) {
     __shared__ uint32_t lds_path[WREG * BLOCK];
     const uint32_t lane = threadIdx.x & 63;
     const LdsPath lp{lds_path + threadIdx.x};
@@ -686,6 +761,7 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
                 if (rank < avail) i = qnext + rank;
                 else if (g + (rank - avail) < gend) i = g + (rank - avail);
                 if (i != NO_TOPIC) {
+                    if (perm) i = perm[i];   // group order (queue position -> topic)
                     const uint32_t mt = meta[i];
                     const uint32_t nl = mt & MN;
                     const bool dollar = (mt & MDOLLAR) != 0;
@@ -942,14 +1018,24 @@ hipError_t launch_queue(bool stats_mode, bool xcdq, const ImageView& im, const u
     if (err != hipSuccess) return err;
     dim3 blk(BLOCK), g(div_up(n, BLOCK));
     mark(0);
-    hipLaunchKernelGGL(tm_tokenize, g, blk, 0, st, im, bytes, off, n, qb.twords, qb.words, qb.meta);
+    uint32_t* ghist = qb.perm ? qb.perm + n : nullptr;   // NGROUP counts, then NGROUP cursors
+    if (ghist) {
+        err = hipMemsetAsync(ghist, 0, NGROUP * sizeof(uint32_t), st);
+        if (err != hipSuccess) return err;
+    }
+    hipLaunchKernelGGL(tm_tokenize, g, blk, 0, st, im, bytes, off, n, qb.twords, qb.words, qb.meta, ghist);
+    if (ghist) {
+        hipLaunchKernelGGL(tm_group_scan, dim3(1), blk, 0, st, ghist, ghist + NGROUP);
+        hipLaunchKernelGGL(tm_group_scatter, g, blk, 0, st, qb.twords, n, ghist + NGROUP, qb.perm);
+    }
     mark(1);
     mark(2);
     const bool keys = qb.kstage != nullptr;
     const uint32_t wg = resident_grid(tm_walk_queue<false, false, false>, div_up(n, 64), walk_blocks_per_cu);
 #define TM_Q(S, X, Y)                                                                                              \
     hipLaunchKernelGGL((tm_walk_queue<S, X, Y>), dim3(wg), blk, 0, st, im, off, n, qb.twords, qb.words, qb.meta, \
-                       qb.path, qb.stage, qb.kstage, K, counts, qb.ws, stats, hist ? stats + HIST_OFF : nullptr)
+                       qb.path, qb.stage, qb.kstage, K, counts, qb.ws, stats, hist ? stats + HIST_OFF : nullptr, \
+                       qb.perm)
     if (keys) {
         if (stats_mode) TM_Q(true, true, true); else TM_Q(false, true, true);
     } else if (stats_mode) {
