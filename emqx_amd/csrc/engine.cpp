@@ -257,7 +257,7 @@ struct tm_engine {
                 stage_auto = 0;
             }
         }
-        dict.assign(1024, DictSlot{0, WORD_NONE, 0});
+        dict.assign(1024, DictSlot{0, WORD_NONE, 0, {0, 0}});
         nodes.reserve(1024);
         cold.slots.assign(1024, kEmptySlot);
         hot.slots.assign(1024, kEmptySlot);
@@ -279,13 +279,15 @@ struct tm_engine {
         size_t mask = dict.size() - 1;
         size_t s = h & mask;
         while (dict[s].word != WORD_NONE) s = (s + 1) & mask;
-        dict[s] = DictSlot{h, id, len};
+        DictSlot d{h, id, len, {0, 0}};
+        std::memcpy(d.head, &word_arena[word_off[id]], std::min<size_t>(16, (len + 7) & ~size_t(7)));
+        dict[s] = d;
         dict_dirty.mark(s);
     }
     void dict_grow() {
         std::vector<DictSlot> old;
         old.swap(dict);
-        dict.assign(old.size() * 2, DictSlot{0, WORD_NONE, 0});
+        dict.assign(old.size() * 2, DictSlot{0, WORD_NONE, 0, {0, 0}});
         for (const DictSlot& d : old)
             if (d.word != WORD_NONE) dict_place(d.hash, d.word, d.len);
         dict_dirty.all = true;

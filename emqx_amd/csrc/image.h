@@ -84,11 +84,14 @@ struct alignas(SLOT_RECORD ? 32 : 16) EdgeSlot {
 };
 static_assert(sizeof(EdgeSlot) == (SLOT_RECORD ? 32 : 16), "edge slot is one or two 16 B halves");
 
-struct alignas(16) DictSlot {
+struct alignas(32) DictSlot {
     uint64_t hash;         // 64-bit word hash (0 reserved for empty)
     uint32_t word;         // word id, WORD_NONE when free
     uint32_t len;          // word length in bytes
+    uint64_t head[2];      // the word's first 16 bytes, zero padded: the tokenizer verifies words of
+                           // <= 16 bytes from the slot itself (no dependent arena loads)
 };
+static_assert(sizeof(DictSlot) == 32, "dictionary slot is one 32 B half line");
 
 // device-side view of one committed image (plain pointers into HBM)
 struct ImageView {

@@ -63,17 +63,24 @@ __device__ __forceinline__ uint32_t dict_lookup(const ImageView& im, const uint8
     h = word_hash_final(h, len);
     uint64_t s = h & im.dict_slot_mask;
     for (;;) {
-        DictSlot d = im.dict[s];
-        if (d.word == WORD_NONE) return WORD_NONE;
-        if (d.hash == h && d.len == len) {
-            // byte-verify against the 8-aligned, zero-padded arena copy
-            const uint64_t* a = reinterpret_cast<const uint64_t*>(im.word_arena + im.word_off[d.word]);
-            bool eq = true;
-            for (uint32_t i = 0; i < len && eq; i += 8) {
-                uint32_t k = len - i < 8 ? len - i : 8;
-                eq = (load_chunk(bytes, p + i, k) == a[i >> 3]);
+        const uint4* slot = reinterpret_cast<const uint4*>(im.dict + s);
+        const uint4 d0 = slot[0], d1 = slot[1];   // one 32 B slot: hash, word, len | first 16 bytes
+        const uint32_t word = d0.z;
+        if (word == WORD_NONE) return WORD_NONE;
+        if ((((uint64_t)d0.y << 32) | d0.x) == h && d0.w == len) {
+            // byte-verify: the first 16 bytes against the slot's copy, the
+            // rest against the 8-aligned, zero-padded arena copy
+            const uint64_t head0 = ((uint64_t)d1.y << 32) | d1.x, head1 = ((uint64_t)d1.w << 32) | d1.z;
+            bool eq = len == 0 || load_chunk(bytes, p, len < 8 ? len : 8) == head0;
+            if (eq && len > 8) eq = load_chunk(bytes, p + 8, len < 16 ? len - 8 : 8) == head1;
+            if (eq && len > 16) {
+                const uint64_t* a = reinterpret_cast<const uint64_t*>(im.word_arena + im.word_off[word]);
+                for (uint32_t i = 16; i < len && eq; i += 8) {
+                    uint32_t k = len - i < 8 ? len - i : 8;
+                    eq = (load_chunk(bytes, p + i, k) == a[i >> 3]);
+                }
             }
-            if (eq) return d.word;
+            if (eq) return word;
         }
         s = (s + 1) & im.dict_slot_mask;
     }
@@ -831,6 +838,13 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
 // stage rows with coalesced writes (output index -> topic by binary search of
 // the block's inclusive prefix); output j of a topic with c ids is row slot
 // K-c+j; a topic with c > K re-walks and writes its first c-K outputs.
+// blocks whose mean fan-out reaches COPY_WAVE_MIN ids per topic copy one
+// topic per wave (no per-id search)
+#ifndef TM_COPY_WAVE_MIN
+#define TM_COPY_WAVE_MIN 16   // A/B at C3: copy-out 0.322 (64) vs 0.283-0.293 ms (16, 0)
+#endif
+constexpr uint32_t COPY_WAVE_MIN = TM_COPY_WAVE_MIN;
+
 template <bool KEYS>
 __global__ void __launch_bounds__(BLOCK)
 tm_copy_out(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const uint32_t* __restrict__ twords,
@@ -849,7 +863,7 @@ tm_copy_out(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const ui
     lds_inc[threadIdx.x] = (uint32_t)(ex + c);
     __syncthreads();
     const uint64_t base = out_off[t0];
-    if (agg >= 64ull * tn) {
+    if (agg >= (uint64_t)COPY_WAVE_MIN * tn) {
         // high fan-out block: one wave per topic, its lanes stride the row
         // (no per-id search); output j of a topic with ct ids is row slot
         // K-ct+j, staged for j >= ct-K
