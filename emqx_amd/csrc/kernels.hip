@@ -31,27 +31,42 @@ namespace tmx {
 constexpr int BLOCK = 256;
 
 // ---------------------------------------------------------------------------
-// byte access: aligned 8-byte loads (an aligned word holding a valid byte
-// never crosses a page), little-endian extraction.
-__device__ __forceinline__ uint64_t load_u64_aligned(const uint8_t* base, uint64_t p) {
-    return *reinterpret_cast<const uint64_t*>(base + (p & ~7ull));
-}
+// byte access: aligned 8-byte words (an aligned word holding a valid byte
+// never crosses a page), little-endian extraction.  Topic bytes are read
+// either from global memory or from a wave's LDS window (tm_tokenize stages
+// the bytes of its 64 topics with coalesced loads first).
+struct GlobalBytes {
+    const uint8_t* p;
+    __device__ __forceinline__ uint64_t word(uint64_t q) const {
+        return *reinterpret_cast<const uint64_t*>(p + (q & ~7ull));
+    }
+    __device__ __forceinline__ uint32_t byte(uint64_t q) const { return p[q]; }
+};
+struct LdsBytes {
+    const uint64_t* w;   // LDS words of bytes [base, ...), base 8-aligned
+    uint64_t base;
+    __device__ __forceinline__ uint64_t word(uint64_t q) const { return w[(q - base) >> 3]; }
+    __device__ __forceinline__ uint32_t byte(uint64_t q) const {
+        return (uint32_t)(word(q) >> (8 * (q & 7))) & 0xFFu;
+    }
+};
 
 // assemble up to 8 bytes [p, p+k) (k in 1..8) little-endian, zero padded
-__device__ __forceinline__ uint64_t load_chunk(const uint8_t* base, uint64_t p, uint32_t k) {
+template <class B>
+__device__ __forceinline__ uint64_t load_chunk(const B& bytes, uint64_t p, uint32_t k) {
     uint32_t sh = (uint32_t)(p & 7) * 8;
-    uint64_t v = load_u64_aligned(base, p) >> sh;
-    if (sh != 0 && (p & 7) + k > 8) v |= load_u64_aligned(base, p + 8) << (64 - sh);
+    uint64_t v = bytes.word(p) >> sh;
+    if (sh != 0 && (p & 7) + k > 8) v |= bytes.word(p + 8) << (64 - sh);
     if (k < 8) v &= (~0ull) >> (64 - 8 * k);
     return v;
 }
 
 // dictionary lookup of topic bytes [p, p+len): word id, WORD_PLUS/HASH for the
 // atoms '+' / '#', or WORD_NONE (bytes no filter contains: match only '+'/'#')
-__device__ __forceinline__ uint32_t dict_lookup(const ImageView& im, const uint8_t* bytes,
-                                                uint64_t p, uint32_t len) {
+template <class B>
+__device__ __forceinline__ uint32_t dict_lookup(const ImageView& im, const B& bytes, uint64_t p, uint32_t len) {
     if (len == 1) {
-        uint32_t c = bytes[p];
+        uint32_t c = bytes.byte(p);
         if (c == '+') return WORD_PLUS;
         if (c == '#') return WORD_HASH;
     }
@@ -110,15 +125,16 @@ __device__ __forceinline__ uint64_t block_exclusive_scan(uint64_t x, uint64_t* l
 // emqx_topic:words/1 of topic [b, e): word id of level k to tw[k] (k < WREG,
 // registers: AND-mask updates, no dynamic index) or lw[k] (k >= WREG);
 // returns the number of levels (N slashes -> N+1 levels, empty levels kept)
-__device__ __forceinline__ uint32_t tokenize_topic(const ImageView& im, const uint8_t* bytes, uint64_t b,
-                                                   uint64_t e, uint32_t (&tw)[WREG], uint32_t* lw) {
+template <class B>
+__device__ __forceinline__ uint32_t tokenize_topic(const ImageView& im, const B& bytes, uint64_t b, uint64_t e,
+                                                   uint32_t (&tw)[WREG], uint32_t* lw) {
     uint32_t lev = 0;
     uint64_t s = b;
     for (;;) {
         uint64_t q = s;  // next '/' at or after s, or e
         bool found = false;
         while (q < e) {
-            uint64_t word8 = load_u64_aligned(bytes, q);
+            uint64_t word8 = bytes.word(q);
             uint32_t start = (uint32_t)(q & 7);
             uint64_t rem = e - (q & ~7ull);
             uint32_t stop = rem < 8 ? (uint32_t)rem : 8;
@@ -159,11 +175,13 @@ constexpr uint32_t MLONG = 1u << 30, MDOLLAR = 1u << 31, MN = (1u << 30) - 1;   
 // measured no gain (3.88 vs 3.88 ms per step): the presort gain comes from
 // neighbours sharing whole prefixes, which takes a full sort.  Off.
 constexpr uint32_t NGROUP = 1024;
+constexpr uint32_t TOK_WIN_WORDS = 512;   // LDS bytes window per wave: 4 KiB (64 topics of <= 64 B)
 __device__ __forceinline__ uint32_t group_of(uint32_t w0, uint32_t w1) {
     return (((w0 * 0x9E3779B1u) >> 26) << 4) | ((w1 * 0x85EBCA6Bu) >> 28);
 }
 
-__device__ __forceinline__ void tokenize_one(const ImageView& im, const uint8_t* __restrict__ bytes,
+template <class B>
+__device__ __forceinline__ void tokenize_one(const ImageView& im, const B& bytes,
                                              const uint64_t* __restrict__ off, uint32_t t,
                                              uint32_t* __restrict__ twords, uint32_t* __restrict__ words,
                                              uint32_t* __restrict__ meta, uint32_t* lh) {
@@ -178,7 +196,7 @@ __device__ __forceinline__ void tokenize_one(const ImageView& im, const uint8_t*
 #pragma unroll
     for (uint32_t k = 0; k < WREG / 4; ++k)
         row[k] = make_uint4(tw[4 * k], tw[4 * k + 1], tw[4 * k + 2], tw[4 * k + 3]);
-    const uint32_t dollar = (e > b && bytes[b] == '$') ? 1u : 0u;
+    const uint32_t dollar = (e > b && bytes.byte(b) == '$') ? 1u : 0u;
     meta[t] = lev | (dollar << 31) | (lev > WREG ? MLONG : 0u);
     if (lh) atomicAdd(lh + group_of(tw[0], tw[1]), 1u);
 }
@@ -188,12 +206,33 @@ tm_tokenize(ImageView im, const uint8_t* __restrict__ bytes, const uint64_t* __r
             uint32_t* __restrict__ twords, uint32_t* __restrict__ words, uint32_t* __restrict__ meta,
             uint32_t* __restrict__ ghist) {
     __shared__ uint32_t lh[NGROUP];
+    __shared__ uint64_t win[BLOCK / 64][TOK_WIN_WORDS];
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (ghist) {
+    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (ghist)
         for (uint32_t k = threadIdx.x; k < NGROUP; k += BLOCK) lh[k] = 0;
-        __syncthreads();
+    // the wave's 64 topics are contiguous bytes: stage them in LDS with
+    // coalesced loads (per-lane 8 B loads of 64 different topics touch 64
+    // lines per instruction); a window that does not fit reads global memory
+    const uint32_t t0 = t - lane;
+    uint64_t wbase = 0;
+    bool lds = false;
+    if (t0 < n) {
+        const uint32_t t1 = t0 + 64 < n ? t0 + 64 : n;
+        wbase = off[t0] & ~7ull;
+        const uint64_t nw = (off[t1] - wbase + 7) >> 3;
+        lds = nw <= TOK_WIN_WORDS;
+        if (lds)
+            for (uint64_t k = lane; k < nw; k += 64)
+                win[wv][k] = *reinterpret_cast<const uint64_t*>(bytes + wbase + 8 * k);
     }
-    if (t < n) tokenize_one(im, bytes, off, t, twords, words, meta, ghist ? lh : nullptr);
+    __syncthreads();
+    if (t < n) {
+        if (lds)
+            tokenize_one(im, LdsBytes{win[wv], wbase}, off, t, twords, words, meta, ghist ? lh : nullptr);
+        else
+            tokenize_one(im, GlobalBytes{bytes}, off, t, twords, words, meta, ghist ? lh : nullptr);
+    }
     if (ghist) {
         __syncthreads();
         for (uint32_t k = threadIdx.x; k < NGROUP; k += BLOCK)
