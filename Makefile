@@ -34,13 +34,16 @@ $(BUILD)/shard.o: emqx_amd/csrc/shard.hip emqx_amd/csrc/kernels.h emqx_amd/csrc/
 $(BUILD)/routes.o: emqx_amd/csrc/routes.hip emqx_amd/csrc/kernels.h emqx_amd/csrc/image.h | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
+$(BUILD)/aggre.o: emqx_amd/csrc/aggre.hip emqx_amd/csrc/kernels.h emqx_amd/csrc/image.h | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
 $(BUILD)/batcher.o: emqx_amd/csrc/batcher.cpp include/topicmatch.h | $(BUILD)
 	$(HIPCC) -O2 -fPIC -std=c++17 -Wall -pthread -c $< -o $@
 
 $(BUILD)/acl.o: emqx_amd/csrc/acl.hip include/topicmatch.h | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(LIBOUT): $(BUILD)/kernels.o $(BUILD)/shard.o $(BUILD)/routes.o $(BUILD)/engine.o $(BUILD)/batcher.o $(BUILD)/acl.o
+$(LIBOUT): $(BUILD)/kernels.o $(BUILD)/shard.o $(BUILD)/routes.o $(BUILD)/aggre.o $(BUILD)/engine.o $(BUILD)/batcher.o $(BUILD)/acl.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -pthread $^ -o $@
 
 emqx_amd/libtmwork.so: emqx_amd/csrc/workload.c

@@ -108,6 +108,18 @@ SIGNATURES = [
                                                     ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p,
                                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                                     ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]),
+    ("tm_dest_target", ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint32,
+                                      ctypes.c_char_p, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]),
+    ("tm_target_bytes", ctypes.c_void_p, [ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32),
+                                          ctypes.POINTER(ctypes.c_uint32)]),
+    ("tm_match_deliveries_batch", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                 ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
+                                                 ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                                 ctypes.c_void_p]),
+    ("tm_match_deliveries_batch_device", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                        ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p,
+                                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                        ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]),
     ("tm_batcher_open", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(TmBatcherConfig),
                                        ctypes.POINTER(ctypes.c_void_p)]),
     ("tm_batcher_submit", ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint32, DONE_FN, ctypes.c_void_p,

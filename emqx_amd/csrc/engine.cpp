@@ -218,6 +218,20 @@ struct tm_engine {
     bool route_image = false;
     DevBuf w_rexact, w_rscan, w_rids, w_rcounts, w_roff;
 
+    // ---- emqx_broker:aggre/1 targets (aggre.hip) ----
+    // a dest aggregates to a target: a node (atom) or a $share group; targets
+    // are interned as kind byte + key bytes, so string order is the Erlang
+    // term order of the X in {To, X} (atom < binary, then bytewise)
+    std::unordered_map<std::string, uint32_t> target_index;
+    std::vector<std::string> target_names;
+    std::vector<uint32_t> dest_target;      // dest id -> target id (TARGET_DEFAULT: node named by the dest bytes)
+    static constexpr uint32_t TARGET_DEFAULT = 0xFFFFFFFFu;
+    struct AggKey { const std::string* key; uint32_t dest_off; uint32_t fid; };
+    std::vector<AggKey> agg_keys;           // route image entries (set by build_route_image)
+    bool aggre_dirty = true;
+    DevBuf d_fr_rank, d_ex_rank, d_dt;
+    DevBuf w_dsrc, w_dcount, w_akey, w_aflag;
+
     // ---- match workspace ----
     DevBuf w_mpre, w_mscan, w_bytes, w_off, w_counts, w_outoff, w_ids, w_total;
     // per-batch device workspace: consecutive batches rotate over `nslots`
@@ -687,16 +701,21 @@ struct tm_engine {
         std::vector<uint8_t> arena;
         std::vector<uint32_t> ex_dest;
         ex_dest.reserve(route_total);
+        agg_keys.clear();
+        agg_keys.reserve(route_bag.size());
+        aggre_dirty = true;
         for (const auto& kv : route_bag) {
             const uint8_t* t = reinterpret_cast<const uint8_t*>(kv.first.data());
             const uint32_t tlen = (uint32_t)kv.first.size();
+            uint32_t fid = FILTER_NONE;
             if (tm_topic_wildcard(t, tlen)) {
-                const uint32_t fid = filter_of(t, tlen);
+                fid = filter_of(t, tlen);
                 if (fid != FILTER_NONE) {
                     fr_off[fid + 1] = (uint32_t)kv.second.size();
                     by_fid.emplace_back(fid, &kv.second);
                 }
             }
+            agg_keys.push_back(AggKey{&kv.first, (uint32_t)ex_dest.size(), fid});
             const uint64_t h = word_hash(t, tlen);
             size_t sl = h & (cap - 1);
             while (slots[sl].hash) sl = (sl + 1) & (cap - 1);
@@ -728,6 +747,67 @@ struct tm_engine {
         HIPCHK(hipStreamSynchronize(stream));   // host vectors die here
         routes_dirty = false;
     }
+    // ------------------------------------------------------------------
+    // emqx_broker:aggre/1 (src/emqx_broker.erl:194-206) tables: to_rank of
+    // every topic with routes (std::string order = Erlang binary order:
+    // bytewise unsigned, a proper prefix first), and per dest its target's
+    // rank and id.  Rebuilt after the route image or a target changes.
+    uint32_t intern_target(uint32_t kind, const uint8_t* k, uint32_t klen) {
+        std::string key(1, (char)kind);
+        key.append(reinterpret_cast<const char*>(k), klen);
+        auto it = target_index.find(key);
+        if (it != target_index.end()) return it->second;
+        if (target_names.size() >= 0x7FFFFFF0ull) throw RangeError("target ids exhausted");
+        const uint32_t id = (uint32_t)target_names.size();
+        target_names.push_back(key);
+        target_index.emplace(std::move(key), id);
+        return id;
+    }
+    void build_aggre_image() {
+        const uint32_t nf = fr_filters;
+        std::vector<uint32_t> order(agg_keys.size());
+        for (uint32_t i = 0; i < order.size(); ++i) order[i] = i;
+        std::sort(order.begin(), order.end(),
+                  [&](uint32_t a, uint32_t b) { return *agg_keys[a].key < *agg_keys[b].key; });
+        std::vector<uint32_t> fr_rank(std::max<uint32_t>(nf, 1), 0), ex_rank(std::max<size_t>(route_total, 1), 0);
+        for (uint32_t r = 0; r < order.size(); ++r) {
+            const AggKey& a = agg_keys[order[r]];
+            if (a.fid != FILTER_NONE && a.fid < nf) fr_rank[a.fid] = r;
+            if (a.dest_off < ex_rank.size()) ex_rank[a.dest_off] = r;
+        }
+        const size_t nd = dest_names.size();
+        dest_target.resize(nd, TARGET_DEFAULT);
+        for (size_t d = 0; d < nd; ++d)
+            if (dest_target[d] == TARGET_DEFAULT)
+                dest_target[d] = intern_target(0, reinterpret_cast<const uint8_t*>(dest_names[d].data()),
+                                               (uint32_t)dest_names[d].size());
+        std::vector<uint32_t> tord(target_names.size()), trank(target_names.size());
+        for (uint32_t i = 0; i < tord.size(); ++i) tord[i] = i;
+        std::sort(tord.begin(), tord.end(), [&](uint32_t a, uint32_t b) { return target_names[a] < target_names[b]; });
+        for (uint32_t r = 0; r < tord.size(); ++r) trank[tord[r]] = r;
+        std::vector<uint2> dt(std::max<size_t>(nd, 1));
+        for (size_t d = 0; d < nd; ++d) {
+            const uint32_t tid = dest_target[d];
+            dt[d] = make_uint2(trank[tid], tid | (target_names[tid][0] ? 0x80000000u : 0u));
+        }
+        auto up = [&](DevBuf& b, const void* src, size_t bytes) {
+            b.ensure(std::max<size_t>(bytes, 16));
+            if (bytes) HIPCHK(hipMemcpyAsync(b.p, src, bytes, hipMemcpyHostToDevice, stream));
+        };
+        up(d_fr_rank, fr_rank.data(), fr_rank.size() * 4);
+        up(d_ex_rank, ex_rank.data(), ex_rank.size() * 4);
+        up(d_dt, dt.data(), dt.size() * sizeof(uint2));
+        HIPCHK(hipStreamSynchronize(stream));   // host vectors die here
+        aggre_dirty = false;
+    }
+    AggreView aggre_view() const {
+        AggreView av;
+        av.fr_rank = d_fr_rank.as<const uint32_t>();
+        av.ex_rank = d_ex_rank.as<const uint32_t>();
+        av.dt = d_dt.as<const uint2>();
+        return av;
+    }
+
     RouteView route_view() const {
         RouteView rv;
         rv.fr_off = d_fr_off.as<const uint32_t>();
@@ -1172,6 +1252,8 @@ struct tm_engine {
             if (route_bag.empty()) {
                 route_image = false;
                 routes_dirty = false;
+                agg_keys.clear();
+                aggre_dirty = true;
             } else {
                 build_route_image();
             }
@@ -1195,6 +1277,33 @@ struct tm_engine {
         HIPCHK(launch_routes(route_view(), bytes, off, n, w_rcounts.as<uint32_t>(), w_roff.as<uint64_t>(),
                              w_rids.as<uint32_t>(), w_rexact.as<uint2>(), counts, out_off, src, dest, cap, total,
                              w_rscan.as<uint64_t>(), st));
+    }
+
+    // aggre(match_routes(T)) over a device batch: the route lists go to
+    // engine workspace (one read of the route total sizes it), aggre.hip
+    // writes each topic's list at its route offset; *total = route total
+    void run_deliveries(const uint8_t* bytes, const uint64_t* off, uint32_t n, uint64_t nbytes, uint32_t* counts,
+                        uint64_t* out_off, uint32_t* to, uint32_t* target, uint64_t cap, uint64_t* total,
+                        hipStream_t st) {
+        w_dcount.ensure((size_t)n * 4 + 4);
+        uint64_t want = std::max<uint64_t>(w_dsrc.bytes / 8, (uint64_t)n * 16 + 1024);
+        w_dsrc.ensure(want * 8, 1.0);
+        uint64_t rcap = w_dsrc.bytes / 8, rtotal = 0;
+        for (int pass = 0; pass < 2; ++pass) {
+            uint32_t* src = w_dsrc.as<uint32_t>();
+            run_routes(bytes, off, n, nbytes, w_dcount.as<uint32_t>(), out_off, src, src + rcap, rcap, total, st);
+            HIPCHK(hipMemcpyAsync(&rtotal, total, 8, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipStreamSynchronize(st));
+            if (rtotal <= rcap) break;
+            w_dsrc.ensure(rtotal * 8, 1.25);
+            rcap = w_dsrc.bytes / 8;
+        }
+        if (aggre_dirty) build_aggre_image();
+        w_akey.ensure(rcap * 8 + 8, 1.0);
+        w_aflag.ensure(rcap + 8, 1.0);
+        const uint32_t* src = w_dsrc.as<uint32_t>();
+        HIPCHK(launch_aggre(aggre_view(), n, w_dcount.as<uint32_t>(), out_off, src, src + rcap, w_rexact.as<uint2>(),
+                            w_akey.as<uint64_t>(), w_aflag.as<uint8_t>(), counts, to, target, cap, st));
     }
 
     void finish_batch(hipStream_t st, uint32_t n) {
@@ -1321,7 +1430,8 @@ void tm_close(tm_engine* e) {
     if (e->device >= 0) {
         (void)hipSetDevice(e->device);
         if (e->stream) (void)hipStreamSynchronize(e->stream);
-        for (DevBuf* b : {&e->d_fr_off, &e->d_fr_dest, &e->d_ex_slots, &e->d_ex_arena, &e->d_ex_dest, &e->w_rexact,
+        for (DevBuf* b : {&e->d_fr_rank, &e->d_ex_rank, &e->d_dt, &e->w_dsrc, &e->w_dcount, &e->w_akey, &e->w_aflag,
+             &e->d_fr_off, &e->d_fr_dest, &e->d_ex_slots, &e->d_ex_arena, &e->d_ex_dest, &e->w_rexact,
                           &e->w_rscan, &e->w_rids, &e->w_rcounts, &e->w_roff})
             b->release();
         for (DevBuf* b : {&e->d_nodes, &e->d_edges, &e->d_hedges, &e->d_dict, &e->d_arena, &e->d_woff, &e->d_inner, &e->d_leaf,
@@ -1704,6 +1814,115 @@ int tm_match_routes_batch(tm_engine* e, const uint8_t* topic_bytes, const uint64
         if (cap) {
             HIPCHK(hipMemcpyAsync(out_src, e->w_ids.p, cap * 4, hipMemcpyDeviceToHost, st));
             HIPCHK(hipMemcpyAsync(out_dest, e->w_ids.as<uint32_t>() + rcap, cap * 4, hipMemcpyDeviceToHost, st));
+        }
+        HIPCHK(hipStreamSynchronize(st));
+        if (out_needed) *out_needed = total;
+        return total > out_cap ? TM_ENOSPC : TM_OK;
+    });
+}
+
+int tm_dest_target(tm_engine* e, const uint8_t* dest, uint32_t dlen, uint32_t kind, const uint8_t* key,
+                   uint32_t klen, uint32_t* target_out) {
+    if ((dlen && !dest) || (klen && !key) || kind > TM_TARGET_GROUP) return TM_EINVAL;
+    return guarded(e, [&]() -> int {
+        const uint32_t d = e->intern_dest(dest, dlen);
+        if (e->dest_target.size() <= d) e->dest_target.resize(d + 1, tm_engine::TARGET_DEFAULT);
+        const uint32_t t = e->intern_target(kind, key, klen);
+        if (e->dest_target[d] != t) {
+            e->dest_target[d] = t;
+            e->aggre_dirty = true;
+        }
+        if (target_out) *target_out = t;
+        return TM_OK;
+    });
+}
+
+const uint8_t* tm_target_bytes(tm_engine* e, uint32_t target_id, uint32_t* kind, uint32_t* len) {
+    if (!e) return nullptr;
+    std::lock_guard<std::recursive_mutex> lk(e->mu);
+    if (target_id >= e->target_names.size()) return nullptr;
+    const std::string& t = e->target_names[target_id];
+    if (kind) *kind = (uint8_t)t[0];
+    if (len) *len = (uint32_t)t.size() - 1;
+    return reinterpret_cast<const uint8_t*>(t.data()) + 1;
+}
+
+int tm_match_deliveries_batch_device(tm_engine* e, const uint8_t* d_bytes, const uint64_t* d_off, uint32_t n,
+                                     uint64_t topic_bytes, uint32_t* d_count, uint64_t* d_out_off, uint32_t* d_to,
+                                     uint32_t* d_target, uint64_t out_cap, uint64_t* d_total, void* hip_stream) {
+    if (!d_off || !d_out_off || !d_total || (n && !d_count) || (out_cap && (!d_to || !d_target))) return TM_EINVAL;
+    return guarded(e, [&]() -> int {
+        if (e->device < 0) {
+            e->last_error = "engine is host-only (device = -1): aggre runs on the GPU only";
+            return TM_EDEVICE;
+        }
+        e->commit();
+        tm_engine::Guard g(e->device);
+        hipStream_t st = hip_stream ? (hipStream_t)hip_stream : e->stream;
+        if (n == 0) {
+            HIPCHK(hipMemsetAsync(d_out_off, 0, 8, st));
+            HIPCHK(hipMemsetAsync(d_total, 0, 8, st));
+            return TM_OK;
+        }
+        e->run_deliveries(d_bytes, d_off, n, topic_bytes, d_count, d_out_off, d_to, d_target, out_cap, d_total, st);
+        e->finish_batch(st, n);
+        return TM_OK;
+    });
+}
+
+int tm_match_deliveries_batch(tm_engine* e, const uint8_t* topic_bytes, const uint64_t* topic_off, uint32_t n,
+                              uint32_t* out_count, uint64_t* out_off, uint32_t* out_to, uint32_t* out_target,
+                              uint64_t out_cap, uint64_t* out_needed) {
+    if (!topic_off || !out_off || (n && !out_count) || (out_cap && (!out_to || !out_target))) return TM_EINVAL;
+    return guarded(e, [&]() -> int {
+        if (e->device < 0) {
+            e->last_error = "engine is host-only (device = -1): aggre runs on the GPU only";
+            return TM_EDEVICE;
+        }
+        for (uint32_t i = 0; i < n; ++i)
+            if (topic_off[i + 1] < topic_off[i]) throw ArgError("topic offsets not monotone");
+        const uint64_t base = topic_off[0], nbytes = topic_off[n] - base;
+        if (n && nbytes && !topic_bytes) throw ArgError("null topic bytes");
+        if (n == 0) {
+            out_off[0] = 0;
+            if (out_needed) *out_needed = 0;
+            return TM_OK;
+        }
+        e->commit();
+        tm_engine::Guard g(e->device);
+        hipStream_t st = e->stream;
+        e->w_bytes.ensure(nbytes + 16);
+        e->w_off.ensure((size_t)(n + 1) * 8);
+        e->w_counts.ensure((size_t)n * 4 + 4);
+        e->w_outoff.ensure((size_t)(n + 1) * 8);
+        std::vector<uint64_t> rel(topic_off, topic_off + n + 1);
+        for (auto& x : rel) x -= base;
+        if (nbytes) HIPCHK(hipMemcpyAsync(e->w_bytes.p, topic_bytes + base, nbytes, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(e->w_off.p, rel.data(), (n + 1) * 8, hipMemcpyHostToDevice, st));
+        e->ensure_workspace(n, nbytes);
+        uint64_t* d_total = e->w_total.as<uint64_t>() + 1;
+        // lists sit at their route offsets: the route total sizes the output
+        uint64_t want = std::max<uint64_t>(e->w_ids.bytes / 8, std::min<uint64_t>(out_cap, (uint64_t)n * 16 + 1024));
+        e->w_ids.ensure(want * 8, 1.0);
+        uint64_t rcap = e->w_ids.bytes / 8, total = 0;
+        for (int pass = 0; pass < 2; ++pass) {
+            uint32_t* to = e->w_ids.as<uint32_t>();
+            e->run_deliveries(e->w_bytes.as<uint8_t>(), e->w_off.as<uint64_t>(), n, nbytes,
+                              e->w_counts.as<uint32_t>(), e->w_outoff.as<uint64_t>(), to, to + rcap, rcap, d_total,
+                              st);
+            HIPCHK(hipMemcpyAsync(&total, d_total, 8, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipStreamSynchronize(st));
+            if (total <= rcap || total > out_cap) break;
+            e->w_ids.ensure(total * 8, 1.25);
+            rcap = e->w_ids.bytes / 8;
+        }
+        const uint64_t cap = std::min(total, out_cap);
+        e->finish_batch(st, n);
+        HIPCHK(hipMemcpyAsync(out_count, e->w_counts.p, (size_t)n * 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(out_off, e->w_outoff.p, (size_t)(n + 1) * 8, hipMemcpyDeviceToHost, st));
+        if (cap) {
+            HIPCHK(hipMemcpyAsync(out_to, e->w_ids.p, cap * 4, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipMemcpyAsync(out_target, e->w_ids.as<uint32_t>() + rcap, cap * 4, hipMemcpyDeviceToHost, st));
         }
         HIPCHK(hipStreamSynchronize(st));
         if (out_needed) *out_needed = total;

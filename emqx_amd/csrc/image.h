@@ -136,6 +136,14 @@ struct RouteView {
     const uint32_t*  ex_dest;
 };
 
+// emqx_broker:aggre/1 tables (aggre.hip): sort ranks of every topic with
+// routes (Erlang binary order) and, per dest id, its aggre target
+struct AggreView {
+    const uint32_t* fr_rank;        // filter id -> to_rank
+    const uint32_t* ex_rank;        // exact-table dest_off -> to_rank of that topic
+    const uint2*    dt;             // dest id -> {target rank, target id | group << 31}
+};
+
 // ---- hashing (identical on host and device) ---------------------------------
 #if defined(__HIPCC__)
 #define TM_HD __host__ __device__ __forceinline__

@@ -8,6 +8,8 @@ on the GPU end to end (trie walk + route expansion, routes.hip).
     match_routes(Topic)        :116-118  -> [#route{}]: routes of the literal topic
                                first, then routes of each trie match in trie order
     get_routes / has_routes / topics   :89-90, :107-108, :110-111
+    match_deliveries(Topic)    emqx_broker:aggre(match_routes(Topic)) (emqx_broker.erl:152,
+                               194-206) -> [{To, Node} | {To, Group}], on the GPU (aggre.hip)
 
 Route = (topic, dest) mirrors #route{topic, dest} (include/emqx.hrl:84-87);
 dests are node names or {Group, Node} tuples, passed to the engine as opaque
@@ -26,6 +28,10 @@ def _enc(dest) -> bytes:
     if isinstance(dest, str):
         return b"\x02" + dest.encode()
     return b"\x03" + bytes(dest)
+
+
+def _key(x) -> bytes:
+    return x.encode() if isinstance(x, str) else bytes(x)
 
 
 class Router:
@@ -52,6 +58,11 @@ class Router:
     def add_route(self, topic: bytes, dest=None):
         dest = self.node if dest is None else dest
         e = _enc(dest)
+        if e not in self._dec:
+            if isinstance(dest, tuple):      # {Group, Node}: aggre keeps the group
+                self.engine.dest_target(e, Engine.TARGET_GROUP, _key(dest[0]))
+            else:                            # a node atom
+                self.engine.dest_target(e, Engine.TARGET_NODE, _key(dest))
         self._dec[e] = dest
         self.engine.route_add(topic, e)
         self._topics[topic] = True
@@ -86,5 +97,35 @@ class Router:
                         names[s] = self.engine.filter_bytes(s)
                     to = names[s]
                 row.append(Route(to, self._dest(int(dst[k]))))
+            res.append(row)
+        return res
+
+    # emqx_broker:aggre/1 over match_routes/1 — emqx_broker.erl:152, 194-206
+    def match_deliveries(self, topic: bytes):
+        return self.match_deliveries_many([topic])[0]
+
+    def match_deliveries_many(self, topics, tagged=False):
+        """batched aggre(match_routes(T)): [(To, Node) | (To, Group)] per
+        topic; tagged=True gives (To, (kind, key bytes)) with kind 0 for a
+        node atom and 1 for a group binary (Erlang term order of X)"""
+        topics = list(topics)
+        buf, off = pack(topics)
+        counts, offs, to, tg = self.engine.match_deliveries_batch(buf, off)
+        names, tnames, res = {}, {}, []
+        for t, topic in enumerate(topics):
+            row = []
+            for k in range(int(offs[t]), int(offs[t]) + int(counts[t])):
+                s = int(to[k])
+                if s == Engine.TOPIC_ROUTE:
+                    name = topic
+                else:
+                    if s not in names:
+                        names[s] = self.engine.filter_bytes(s)
+                    name = names[s]
+                g = int(tg[k])
+                if g not in tnames:
+                    tnames[g] = self.engine.target_bytes(g)
+                kind, key = tnames[g]
+                row.append((name, (kind, key)) if tagged else (name, key))
             res.append(row)
         return res

@@ -259,6 +259,61 @@ class Engine:
                                                    p(d_offs), p(d_src), p(d_dest), out_cap, p(d_total), st)
         return self._check(rc, "tm_match_routes_batch_device")
 
+    # -- emqx_broker:aggre/1 (aggre.hip) --------------------------------------
+    TARGET_NODE, TARGET_GROUP = 0, 1
+
+    def dest_target(self, dest: bytes, kind: int, key: bytes) -> int:
+        """declare dest's aggre target: a node atom (TARGET_NODE, key = its
+        text) or a $share group (TARGET_GROUP, key = the group binary)"""
+        t = ctypes.c_uint32()
+        self._check(self.lib.tm_dest_target(self.h, dest, len(dest), kind, key, len(key), ctypes.byref(t)),
+                    "tm_dest_target")
+        return t.value
+
+    def target_bytes(self, target_id: int):
+        """target id -> (kind, key bytes)"""
+        kind, n = ctypes.c_uint32(), ctypes.c_uint32()
+        p = self.lib.tm_target_bytes(self.h, target_id, ctypes.byref(kind), ctypes.byref(n))
+        if not p:
+            raise KeyError(target_id)
+        return kind.value, ctypes.string_at(p, n.value)
+
+    def match_deliveries_batch(self, buf, off, out_cap=None):
+        """Host batch -> (counts u32[n], offsets u64[n+1], to u32[total],
+        target u32[total]): aggre(emqx_router:match_routes(T)) per topic; to =
+        TOPIC_ROUTE for the literal topic, else the filter id."""
+        buf = np.ascontiguousarray(buf, dtype=np.uint8)
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        n = len(off) - 1
+        counts = np.zeros(max(n, 1), dtype=np.uint32)
+        offs = np.zeros(n + 1, dtype=np.uint64)
+        cap = 1 << 16 if out_cap is None else out_cap
+        while True:
+            to = np.zeros(max(cap, 1), dtype=np.uint32)
+            tg = np.zeros(max(cap, 1), dtype=np.uint32)
+            needed = ctypes.c_uint64()
+            rc = self.lib.tm_match_deliveries_batch(self.h, _ptr(buf), _ptr(off), n, _ptr(counts), _ptr(offs),
+                                                    _ptr(to), _ptr(tg), cap, ctypes.byref(needed))
+            if rc == L.TM_ENOSPC and out_cap is None:
+                cap = int(needed.value)
+                continue
+            self._check(rc, "tm_match_deliveries_batch")
+            k = int(needed.value)
+            return counts[:n], offs, to[:k], tg[:k]
+
+    def match_deliveries_batch_device(self, d_bytes, d_off, n, topic_bytes, d_counts, d_offs, d_to, d_target,
+                                      out_cap, d_total, stream=None):
+        def p(x):
+            if x is None:
+                return None
+            return ctypes.c_void_p(x.data_ptr() if hasattr(x, "data_ptr") else int(x))
+        st = None
+        if stream is not None:
+            st = ctypes.c_void_p(stream if isinstance(stream, int) else stream.cuda_stream)
+        rc = self.lib.tm_match_deliveries_batch_device(self.h, p(d_bytes), p(d_off), n, topic_bytes, p(d_counts),
+                                                       p(d_offs), p(d_to), p(d_target), out_cap, p(d_total), st)
+        return self._check(rc, "tm_match_deliveries_batch_device")
+
     # walk variants (A/B knobs of tm_walk_queue): one global dequeue head, or
     # per-XCD heads over contiguous ranges of the batch
     WALKS = {"queue": 0, "queue_xcd": 1}

@@ -240,6 +240,42 @@ int tm_match_routes_batch_device(tm_engine* e, const uint8_t* d_topic_bytes, con
                                  uint32_t* d_out_src, uint32_t* d_out_dest, uint64_t out_cap, uint64_t* d_total,
                                  void* hip_stream);
 
+/* ---- emqx_broker:aggre/1 (emqx_amd/csrc/aggre.hip) -----------
+ * publish/1 routes aggre(match_routes(Topic)) (src/emqx_broker.erl:152):
+ * each #route{topic = To, dest} becomes {To, Node} for a node dest and
+ * {To, Group} for a {Group, Node} dest; the fold prepends node entries and
+ * lists:usort()s the whole accumulator at every group entry (:194-206).
+ * Dest bytes are opaque to the engine, so the caller declares each dest's
+ * target: kind TM_TARGET_NODE (key = the node atom's text) or
+ * TM_TARGET_GROUP (key = the group binary).  An undeclared dest is a node
+ * named by its dest bytes.  Sorting follows Erlang term order: To bytewise
+ * (a proper prefix first), then node atoms before group binaries, each
+ * bytewise. */
+#define TM_TARGET_NODE  0u
+#define TM_TARGET_GROUP 1u
+int tm_dest_target(tm_engine* e, const uint8_t* dest, uint32_t dlen, uint32_t kind, const uint8_t* key,
+                   uint32_t klen, uint32_t* target_out);
+/* target id -> key bytes (engine-owned, stable; *kind = TM_TARGET_*) */
+const uint8_t* tm_target_bytes(tm_engine* e, uint32_t target_id, uint32_t* kind, uint32_t* len);
+
+/* aggre(emqx_router:match_routes(T)) per topic of a batch: entries of topic t
+ * are out_to/out_target[out_off[t] .. +out_count[t]), out_to = TM_ROUTE_TOPIC
+ * for the literal topic else the filter id (the To of the pair), out_target =
+ * target id.  out_off are match_routes/1's offsets (aggre never lengthens a
+ * list, so each list sits at its route offset and needs no compaction):
+ * out_count[t] <= out_off[t+1] - out_off[t], and out_needed / *d_total is the
+ * route total.  Host buffers, synchronous; TM_ENOSPC / out_needed as
+ * tm_match_batch.  Walk, route expansion and aggre all run on the GPU. */
+int tm_match_deliveries_batch(tm_engine* e, const uint8_t* topic_bytes, const uint64_t* topic_off, uint32_t n,
+                              uint32_t* out_count, uint64_t* out_off, uint32_t* out_to, uint32_t* out_target,
+                              uint64_t out_cap, uint64_t* out_needed);
+/* Same with device buffers on hip_stream; *d_total = route total, entries at
+ * or past out_cap are dropped. */
+int tm_match_deliveries_batch_device(tm_engine* e, const uint8_t* d_topic_bytes, const uint64_t* d_topic_off,
+                                     uint32_t n, uint64_t topic_bytes, uint32_t* d_out_count, uint64_t* d_out_off,
+                                     uint32_t* d_out_to, uint32_t* d_out_target, uint64_t out_cap,
+                                     uint64_t* d_total, void* hip_stream);
+
 /* ---- publish micro-batcher (emqx_amd/csrc/batcher.cpp) -----
  * emqx_broker:publish/1 (src/emqx_broker.erl:148-157) matches one topic per
  * call in the publisher's process.  The NIF instead submits the topic here

@@ -245,6 +245,42 @@ def match_routes(trie: Trie, routes: dict, topic: bytes):
     return out
 
 
+def _x_term(dest):
+    """the X of aggre's {To, X} as an orderable tagged term: a node atom ->
+    (0, name), the Group of {Group, Node} -> (1, group); tuple order on
+    (tag, bytes) is Erlang term order (atom < binary, then bytewise)"""
+    if isinstance(dest, tuple):
+        g = dest[0]
+        return (1, g.encode() if isinstance(g, str) else bytes(g))
+    return (0, dest.encode() if isinstance(dest, str) else bytes(dest))
+
+
+def _usort(xs):
+    """lists:usort/1: sorted in term order, duplicates removed"""
+    return sorted(set(xs))
+
+
+def aggre(routes):
+    """emqx_broker:aggre/1 (src/emqx_broker.erl:194-206), clause for clause.
+    routes: [(To, Dest)] as match_routes returns them; Dest is a node (bytes /
+    str, an atom) or a (Group, Node) tuple.  Result: [(To, (tag, bytes))] with
+    _x_term's tagging."""
+    if not routes:                                   # aggre([]) -> []
+        return []
+    if len(routes) == 1:
+        to, dest = routes[0]
+        if not isinstance(dest, tuple):              # when is_atom(Node) -> [{To, Node}]
+            return [(to, _x_term(dest))]
+        return [(to, _x_term(dest))]                 # dest = {Group, _Node} -> [{To, Group}]
+    acc = []
+    for to, dest in routes:                          # lists:foldl(..., [], Routes)
+        if not isinstance(dest, tuple):
+            acc = [(to, _x_term(dest))] + acc        # [{To, Node} | Acc]
+        else:
+            acc = _usort([(to, _x_term(dest))] + acc)   # lists:usort([{To, Group} | Acc])
+    return acc
+
+
 class RouteTable:
     """emqx_router's route bag with its trie bookkeeping (TEST ORACLE):
     handle_cast add_route (src/emqx_router.erl:153-163) + add_trie_route/1
@@ -278,3 +314,7 @@ class RouteTable:
 
     def match_routes(self, topic: bytes):
         return match_routes(self.trie, self.routes, topic)
+
+    def match_deliveries(self, topic: bytes):
+        """aggre(match_routes(Topic)) — emqx_broker.erl:152"""
+        return aggre(self.match_routes(topic))

@@ -1,11 +1,13 @@
-"""emqx_router:match_routes/1 on one MI355X at C3 scale.
+"""emqx_router:match_routes/1 and emqx_broker:aggre/1 over it on one MI355X at
+C3 scale.
 
 Route table: every one of the 10M C3 wildcard filters routes to one of 8
 nodes, every 4th filter also to a shared-subscription dest {Group, Node};
 1M publish topics carry a direct (exact-topic) route.  One step = the whole
 match_routes/1 path of a 2M-topic HBM-resident batch: tokenizer, trie walk,
 CSR emission, route count / scan / emit (routes.hip).  Timed beside the
-trie-only step (emqx_trie:match/1) on the same batch, interleaved.
+trie-only step (emqx_trie:match/1) and the deliveries step (aggre(match_routes
+(T)), aggre.hip after the route kernels) on the same batch, interleaved.
 
 Run: python tools/bench_routes.py [--filters N --topics N --steps K]
 Writes one JSON line to stdout."""
@@ -67,6 +69,9 @@ def main():
     xb, xo = W.topics(a.config, n=a.exact, stream=99)
     db, do = fixed_dests(np.zeros(a.exact, dtype=np.int64), nodes)
     e.route_add_many(xb, xo, db, do)
+    for k in range(8):   # aggre targets: node atoms and $share groups
+        e.dest_target(nodes[k], Engine.TARGET_NODE, nodes[k])
+        e.dest_target(groups[k], Engine.TARGET_GROUP, groups[k].split(b"|")[0])
     e.commit()
     log("routes: %d over %d filters + %d exact topics, built in %.1fs" % (e.route_count, e.filter_count, a.exact,
                                                                           time.time() - t0))
@@ -93,15 +98,24 @@ def main():
     itotal = int(it.item())
     d_i = torch.empty(itotal + 1024, dtype=torch.int32, device=dev)
 
+    d_ac = torch.empty(n, dtype=torch.int32, device=dev)
+    d_ao = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    d_at = torch.empty(cap, dtype=torch.int32, device=dev)
+    d_ag = torch.empty(cap, dtype=torch.int32, device=dev)
+    d_atot = torch.zeros(1, dtype=torch.int64, device=dev)
+
+    def deliveries_step():
+        e.match_deliveries_batch_device(d_b, d_o, n, int(to[-1]), d_ac, d_ao, d_at, d_ag, cap, d_atot, stream=st)
+
     def routes_step():
         e.match_routes_batch_device(d_b, d_o, n, int(to[-1]), d_c, d_oo, d_s, d_d, cap, d_t, stream=st)
 
     def trie_step():
         e.match_batch_device(d_b, d_o, n, int(to[-1]), ic, io, d_i, itotal + 1024, it, stream=st)
 
-    res = {"match_routes": [], "trie_match": []}
+    res = {"match_routes": [], "trie_match": [], "deliveries": []}
     for _ in range(3):
-        for name, fn in (("match_routes", routes_step), ("trie_match", trie_step)):
+        for name, fn in (("match_routes", routes_step), ("trie_match", trie_step), ("deliveries", deliveries_step)):
             fn()
             torch.cuda.synchronize(dev)
             t1 = time.perf_counter()
@@ -138,13 +152,47 @@ def main():
                 ok = False
                 log("mismatch at topic %d: %s vs %s" % (t, got[:6], want[:6]))
                 break
-        check = ok
         log("check of %d topics vs O1 + host route expansion: %s" % (k, ok))
+        # aggre(match_routes(T)) vs the oracle's transcription of aggre/1
+        from oracle.pytrie import aggre
+        ka = min(k, 5000)
+        at = d_at.cpu().numpy().view(np.uint32)
+        ag = d_ag.cpu().numpy().view(np.uint32)
+        ao = d_ao[: ka + 1].cpu().numpy().view(np.uint64)
+        ac = d_ac[:ka].cpu().numpy().view(np.uint32)
+        fcache, tcache = {}, {}
+
+        def fname(fid):
+            if fid not in fcache:
+                fcache[fid] = e.filter_bytes(fid)
+            return fcache[fid]
+        for t in range(ka):
+            rl = [(topics[t], nodes[0])] if topics[t] in exact else []
+            for fid in oi[int(oo[t]):int(oo[t + 1])]:
+                fid = int(fid)
+                rl.append((fname(fid), nodes[fid % 8]))
+                if fid % 4 == 0:
+                    g = groups[(fid // 4) % 8].split(b"|")
+                    rl.append((fname(fid), (g[0], g[1])))
+            got = []
+            for j in range(int(ao[t]), int(ao[t]) + int(ac[t])):
+                g = int(ag[j])
+                if g not in tcache:
+                    tcache[g] = e.target_bytes(g)
+                got.append((topics[t] if int(at[j]) == 0xFFFFFFFF else fname(int(at[j])), tcache[g]))
+            if got != aggre(rl):
+                ok = False
+                log("aggre mismatch at topic %d: %s vs %s" % (t, got[:6], aggre(rl)[:6]))
+                break
+        log("aggre check of %d topics vs oracle aggre/1: %s" % (ka, ok))
+        check = ok
     out = {"workload": "C%d: %d filters, %d routes (%d exact topics), %d-topic batch" % (
                a.config, nf, e.route_count, a.exact, n),
            "ms_per_step": ms, "topics_per_s": {k: n / (v * 1e-3) for k, v in ms.items()},
            "routes_per_topic": rtotal / n, "routes_per_s": rtotal / (ms["match_routes"] * 1e-3),
-           "route_expansion_ms": ms["match_routes"] - ms["trie_match"], "check": check}
+           "route_expansion_ms": ms["match_routes"] - ms["trie_match"],
+           "deliveries_per_topic": int(d_ac.view(torch.int32).sum().item()) / n, "aggre_ms": ms["deliveries"] - ms["match_routes"],
+           "check": check}
     print(json.dumps(out), flush=True)
     e.close()
 
