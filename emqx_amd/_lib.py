@@ -47,6 +47,7 @@ class TmBatcherStats(ctypes.Structure):
 
 
 TM_BATCHER_ROUTES = 1
+TM_BATCHER_DELIVERIES = 2
 DONE_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, c_u32p, c_u32p, ctypes.c_uint32)
 
 # (name, restype, argtypes) — every symbol include/topicmatch.h declares

@@ -2,8 +2,8 @@
 
 Many publisher threads submit single topics; the native worker thread seals
 device batches (by size or deadline) and calls back once per topic with its
-ordered match list (emqx_trie:match/1 filter ids) or its match_routes/1
-routes.  This is the NIF's path: the callback there builds
+ordered match list (emqx_trie:match/1 filter ids), its match_routes/1
+routes, or (deliveries=True) aggre(match_routes/1): To ids + target ids.  This is the NIF's path: the callback there builds
 the Erlang list and enif_send()s it to the waiting process."""
 import ctypes
 import itertools
@@ -12,10 +12,11 @@ from . import _lib as L
 
 
 class Batcher:
-    def __init__(self, engine, max_topics=65536, deadline_us=200, max_bytes=0, routes=False):
+    def __init__(self, engine, max_topics=65536, deadline_us=200, max_bytes=0, routes=False, deliveries=False):
         self.engine = engine
         self.lib = engine.lib
-        cfg = L.TmBatcherConfig(max_topics, deadline_us, max_bytes, L.TM_BATCHER_ROUTES if routes else 0, 0)
+        flags = (L.TM_BATCHER_ROUTES if routes else 0) | (L.TM_BATCHER_DELIVERIES if deliveries else 0)
+        cfg = L.TmBatcherConfig(max_topics, deadline_us, max_bytes, flags, 0)
         h = ctypes.c_void_p()
         rc = self.lib.tm_batcher_open(engine.h, ctypes.byref(cfg), ctypes.byref(h))
         if rc != L.TM_OK:

@@ -196,7 +196,7 @@ struct tm_batcher {
         return (uint32_t)n;
     }
 
-    int run_device(uint32_t n, uint64_t nbytes, bool routes, uint64_t& total) {
+    int run_device(uint32_t n, uint64_t nbytes, bool routes, bool deliv, uint64_t& total) {
         auto chk = [](hipError_t e) { return e == hipSuccess; };
         if (!d_bytes.ensure(nbytes + 16) || !d_off.ensure((n + 1) * 8) || !d_counts.ensure(n * 4 + 4) ||
             !d_outoff.ensure((n + 1) * 8) || !d_total.ensure(64) || !h_counts.ensure(n * 4 + 4) ||
@@ -210,7 +210,11 @@ struct tm_batcher {
             if (!chk(hipMemcpyAsync(d_bytes.p, h_bytes.p, nbytes, hipMemcpyHostToDevice, stream)) ||
                 !chk(hipMemcpyAsync(d_off.p, h_off.p, (n + 1) * 8, hipMemcpyHostToDevice, stream)))
                 return TM_EDEVICE;
-            int rc = routes ? tm_match_routes_batch_device(eng, (const uint8_t*)d_bytes.p, (const uint64_t*)d_off.p, n,
+            int rc = deliv ? tm_match_deliveries_batch_device(eng, (const uint8_t*)d_bytes.p, (const uint64_t*)d_off.p,
+                                                              n, nbytes, (uint32_t*)d_counts.p, (uint64_t*)d_outoff.p,
+                                                              (uint32_t*)d_src.p, (uint32_t*)d_dest.p, cap,
+                                                              (uint64_t*)d_total.p, stream)
+                     : routes ? tm_match_routes_batch_device(eng, (const uint8_t*)d_bytes.p, (const uint64_t*)d_off.p, n,
                                                            nbytes, (uint32_t*)d_counts.p, (uint64_t*)d_outoff.p,
                                                            (uint32_t*)d_src.p, (uint32_t*)d_dest.p, cap,
                                                            (uint64_t*)d_total.p, stream)
@@ -236,7 +240,8 @@ struct tm_batcher {
 
     void run() {
         const uint32_t n = gather();
-        const bool routes = (cfg.flags & TM_BATCHER_ROUTES) != 0;
+        const bool deliv = (cfg.flags & TM_BATCHER_DELIVERIES) != 0;
+        const bool routes = deliv || (cfg.flags & TM_BATCHER_ROUTES) != 0;
         uint64_t total = 0;
         int rc = n == UINT32_MAX ? TM_ENOMEM : TM_OK;
         if (rc == TM_OK && n) {
@@ -244,7 +249,11 @@ struct tm_batcher {
                 rc = TM_EDEVICE;   // host-only engine: the match path runs on the GPU only
             } else {
                 (void)hipSetDevice(device);
-                rc = run_device(n, ((uint64_t*)h_off.p)[n], routes, total);
+                rc = run_device(n, ((uint64_t*)h_off.p)[n], routes, deliv, total);
+                if (rc == TM_OK && deliv) {   // lists sit at route offsets: count the entries
+                    total = 0;
+                    for (uint32_t i = 0; i < n; ++i) total += ((const uint32_t*)h_counts.p)[i];
+                }
             }
         }
         const uint32_t m = rc == TM_ENOMEM && n == UINT32_MAX ? (uint32_t)reqs.size() : n;

@@ -19,6 +19,11 @@
  *   emqx_trie_nif:route_del(Engine, Topic, DestBin) -> ok   emqx_router del_route (:165-187)
  *   emqx_trie_nif:match_routes_async(Engine, Topic) -> Ref; later {Ref, [{To, DestBin}]}
  *                                                           emqx_router:match_routes/1 (:116-118)
+ *   emqx_trie_nif:dest_target(Engine, DestBin, node | group, Key) -> ok
+ *                                   declares Dest's aggre target: the node atom's text, or the Group
+ *   emqx_trie_nif:match_deliveries_async(Engine, Topic) -> Ref; later {Ref, [{To, Node | Group}]}
+ *                                   emqx_broker:aggre(emqx_router:match_routes(Topic))
+ *                                   (src/emqx_broker.erl:152, 194-206), route/2's input
  * DestBin is term_to_binary(Dest) (node() or {Group, node()}): opaque to the
  * engine, binary_to_term'd by the Erlang wrapper.
  *
@@ -38,6 +43,7 @@ typedef struct {
     ErlNifMutex* mu;
     tm_batcher* filters_b;   /* micro-batcher for match_async (emqx_trie:match/1)          */
     tm_batcher* routes_b;    /* micro-batcher for match_routes_async (match_routes/1)      */
+    tm_batcher* deliv_b;     /* micro-batcher for match_deliveries_async (aggre/1)         */
 } engine_res;
 
 /* one in-flight async request: where the reply goes */
@@ -47,6 +53,7 @@ typedef struct {
     ERL_NIF_TERM ref;
     engine_res* r;       /* kept alive until the reply is sent */
     ERL_NIF_TERM topic;  /* copy of the topic (route source TM_ROUTE_TOPIC) */
+    int mode;            /* 0 match/1, 1 match_routes/1, 2 aggre(match_routes/1) */
 } async_req;
 
 static ERL_NIF_TERM atom(ErlNifEnv* env, const char* name) {
@@ -72,6 +79,7 @@ static void engine_dtor(ErlNifEnv* env, void* obj) {
     engine_res* r = (engine_res*)obj;
     if (r->filters_b) tm_batcher_close(r->filters_b);
     if (r->routes_b) tm_batcher_close(r->routes_b);
+    if (r->deliv_b) tm_batcher_close(r->deliv_b);
     if (r->e) tm_close(r->e);
     if (r->mu) enif_mutex_destroy(r->mu);
 }
@@ -95,7 +103,7 @@ static ERL_NIF_TERM nif_open(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]
     cfg.device = dev;
     engine_res* r = (engine_res*)enif_alloc_resource(ENGINE_RT, sizeof(engine_res));
     r->e = NULL;
-    r->filters_b = r->routes_b = NULL;
+    r->filters_b = r->routes_b = r->deliv_b = NULL;
     r->mu = enif_mutex_create("tm_engine");
     int rc = tm_open(&cfg, &r->e);
     if (rc == TM_OK) {
@@ -105,6 +113,8 @@ static ERL_NIF_TERM nif_open(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]
         rc = tm_batcher_open(r->e, &bc, &r->filters_b);
         bc.flags = TM_BATCHER_ROUTES;
         if (rc == TM_OK) rc = tm_batcher_open(r->e, &bc, &r->routes_b);
+        bc.flags = TM_BATCHER_DELIVERIES;
+        if (rc == TM_OK) rc = tm_batcher_open(r->e, &bc, &r->deliv_b);
     }
     if (rc != TM_OK) {
         enif_release_resource(r);
@@ -281,7 +291,21 @@ static void async_done(void* ctx, uint64_t ticket, int status, const uint32_t* i
     } else {
         ERL_NIF_TERM* cells = (ERL_NIF_TERM*)enif_alloc(sizeof(ERL_NIF_TERM) * (n ? n : 1));
         ERL_NIF_TERM* db = dests ? (ERL_NIF_TERM*)enif_alloc(sizeof(ERL_NIF_TERM) * (n ? n : 1)) : NULL;
-        if (dests) make_binaries(env, q->r->e, dests, n, 1, db);
+        if (dests && q->mode == 2) {
+            /* targets: a node atom, or a $share group binary */
+            for (uint32_t k = 0; k < n; ++k) {
+                uint32_t kind = 0, len = 0;
+                const uint8_t* p = tm_target_bytes(q->r->e, dests[k], &kind, &len);
+                if (kind == TM_TARGET_NODE) {
+                    db[k] = enif_make_atom_len(env, (const char*)p, len);
+                } else {
+                    unsigned char* o = enif_make_new_binary(env, len, &db[k]);
+                    if (len) memcpy(o, p, len);
+                }
+            }
+        } else if (dests) {
+            make_binaries(env, q->r->e, dests, n, 1, db);
+        }
         for (uint32_t k = 0; k < n; ++k) {
             ERL_NIF_TERM to = ids[k] == TM_ROUTE_TOPIC ? q->topic : filter_binary(env, q->r->e, ids[k]);
             cells[k] = dests ? enif_make_tuple2(env, to, db[k]) : to;
@@ -296,7 +320,7 @@ static void async_done(void* ctx, uint64_t ticket, int status, const uint32_t* i
     enif_free(q);
 }
 
-static ERL_NIF_TERM submit_async(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[], int routes) {
+static ERL_NIF_TERM submit_async(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[], int mode) {
     engine_res* r;
     ErlNifBinary b;
     if (argc != 2 || !get_engine(env, argv[0], &r) || !enif_inspect_binary(env, argv[1], &b))
@@ -308,9 +332,11 @@ static ERL_NIF_TERM submit_async(ErlNifEnv* env, int argc, const ERL_NIF_TERM ar
     q->ref = enif_make_copy(q->env, ref);
     q->topic = enif_make_copy(q->env, argv[1]);
     q->r = r;
+    q->mode = mode;
     enif_self(env, &q->pid);
     enif_keep_resource(r);
-    int rc = tm_batcher_submit(routes ? r->routes_b : r->filters_b, b.data, (uint32_t)b.size, async_done, q, NULL);
+    tm_batcher* bt = mode == 2 ? r->deliv_b : mode == 1 ? r->routes_b : r->filters_b;
+    int rc = tm_batcher_submit(bt, b.data, (uint32_t)b.size, async_done, q, NULL);
     if (rc != TM_OK) {
         enif_release_resource(r);
         enif_free_env(q->env);
@@ -325,6 +351,26 @@ static ERL_NIF_TERM nif_match_async(ErlNifEnv* env, int argc, const ERL_NIF_TERM
 }
 static ERL_NIF_TERM nif_match_routes_async(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
     return submit_async(env, argc, argv, 1);
+}
+
+static ERL_NIF_TERM nif_match_deliveries_async(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    return submit_async(env, argc, argv, 2);
+}
+
+static ERL_NIF_TERM nif_dest_target(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    engine_res* r;
+    ErlNifBinary d, k;
+    if (argc != 4 || !get_engine(env, argv[0], &r) || !enif_inspect_binary(env, argv[1], &d) ||
+        !enif_is_atom(env, argv[2]) || !enif_inspect_binary(env, argv[3], &k))
+        return enif_make_badarg(env);
+    uint32_t kind;
+    if (enif_is_identical(argv[2], atom(env, "node"))) kind = TM_TARGET_NODE;
+    else if (enif_is_identical(argv[2], atom(env, "group"))) kind = TM_TARGET_GROUP;
+    else return enif_make_badarg(env);
+    enif_mutex_lock(r->mu);
+    int rc = tm_dest_target(r->e, d.data, (uint32_t)d.size, kind, k.data, (uint32_t)k.size, NULL);
+    enif_mutex_unlock(r->mu);
+    return rc == TM_OK ? atom(env, "ok") : error_tuple(env, rc);
 }
 
 static ERL_NIF_TERM nif_route_op(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[], int add) {
@@ -356,6 +402,8 @@ static ErlNifFunc funcs[] = {
     {"match_many", 2, nif_match_many, ERL_NIF_DIRTY_JOB_IO_BOUND},
     {"match_async", 2, nif_match_async, 0},                 /* returns at once: normal scheduler */
     {"match_routes_async", 2, nif_match_routes_async, 0},
+    {"match_deliveries_async", 2, nif_match_deliveries_async, 0},
+    {"dest_target", 4, nif_dest_target, 0},
     {"route_add", 3, nif_route_add, 0},
     {"route_del", 3, nif_route_del, 0},
 };

@@ -286,21 +286,23 @@ int tm_match_deliveries_batch_device(tm_engine* e, const uint8_t* d_topic_bytes,
  * id / dest arrays are valid only during the callback (the NIF copies them
  * into a term and enif_send()s it).  status != TM_OK: ids are null. */
 #define TM_BATCHER_ROUTES 1u   /* results are match_routes/1 (src ids + dest ids) */
+#define TM_BATCHER_DELIVERIES 2u   /* results are aggre(match_routes/1) (To ids + target ids) */
 
 typedef struct tm_batcher tm_batcher;
 typedef struct tm_batcher_config {
     uint32_t max_topics;      /* seal at this many pending topics (0 = 65536); a seal takes every pending topic */
     uint32_t deadline_us;     /* seal this long after the first topic (0 = 200)  */
     uint64_t max_bytes;       /* seal at this many topic bytes (0 = 64 MiB)      */
-    uint32_t flags;           /* TM_BATCHER_ROUTES                              */
+    uint32_t flags;           /* TM_BATCHER_ROUTES | TM_BATCHER_DELIVERIES      */
     uint32_t reserved;
 } tm_batcher_config;
 typedef struct tm_batcher_stats {
     uint64_t batches, topics, results, max_batch;
     uint64_t size_seals, deadline_seals, failed_batches;
 } tm_batcher_stats;
-/* ids: filter ids (match/1) or route sources (match_routes/1); dests: route
- * dest ids or null; n: list length */
+/* ids: filter ids (match/1), route sources (match_routes/1) or To ids
+ * (deliveries); dests: route dest ids, target ids (deliveries) or null; n:
+ * list length */
 typedef void (*tm_batch_done_fn)(void* ctx, uint64_t ticket, int status, const uint32_t* ids,
                                  const uint32_t* dests, uint32_t n);
 

@@ -18,7 +18,7 @@ from emqx_amd.batcher import Batcher  # noqa: E402
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("routes", [False, True])
+@pytest.mark.parametrize("routes", [False, True, "deliveries"])
 def test_batcher_results_equal_batch_api(gpu_device, routes):
     fb, fo = W.filters(1)
     tb, to = W.topics(1, n=40000)
@@ -29,13 +29,21 @@ def test_batcher_results_equal_batch_api(gpu_device, routes):
             e.route_add(f, b"node%d" % (i % 3))
         for t in topics[::5]:
             e.route_add(t, b"direct")
-        counts, offs, src, dst = e.match_routes_batch(tb, to)
-        want = [(list(src[offs[t]:offs[t + 1]]), list(dst[offs[t]:offs[t + 1]])) for t in range(len(topics))]
+        if routes == "deliveries":
+            for i, f in enumerate(W.unpack(fb, fo)[::3]):     # $share members: {Group, Node}
+                e.dest_target(b"grp%d|node%d" % (i % 4, i % 3), Engine.TARGET_GROUP, b"grp%d" % (i % 4))
+                e.route_add(f, b"grp%d|node%d" % (i % 4, i % 3))
+            counts, offs, src, dst = e.match_deliveries_batch(tb, to)
+            want = [(list(src[offs[t]:offs[t] + counts[t]]), list(dst[offs[t]:offs[t] + counts[t]]))
+                    for t in range(len(topics))]
+        else:
+            counts, offs, src, dst = e.match_routes_batch(tb, to)
+            want = [(list(src[offs[t]:offs[t + 1]]), list(dst[offs[t]:offs[t + 1]])) for t in range(len(topics))]
     else:
         e.insert_many(fb, fo)
         counts, offs, ids = e.match_batch(tb, to)
         want = [(list(ids[offs[t]:offs[t + 1]]), None) for t in range(len(topics))]
-    b = Batcher(e, max_topics=3000, deadline_us=500, routes=routes)
+    b = Batcher(e, max_topics=3000, deadline_us=500, routes=routes is True, deliveries=routes == "deliveries")
     got = [None] * len(topics)
 
     def producer(k):
