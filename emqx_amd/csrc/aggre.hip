@@ -22,11 +22,16 @@
 // Erlang term order of {To, X}: To (a binary) first, bytewise, a proper
 // prefix first; then X: a node atom < a group binary, each by its bytes.  The
 // host turns both into ranks (to_rank over every topic with routes, target
-// rank over every target), so a sort key is one u64 = to_rank << 32 | rank.
+// rank over every target), so a sort key is one u64 = to_rank << 32 | rank;
+// tm_route_emit writes it beside each route (routes.hip).
 //
-// tm_aggre: one wave per topic.  The usort is a bitonic sort of the keys (and
-// their route indices) in the wave's LDS row, then a ballot keeps the first
-// of each run of equal keys.  Topics with more than AG_LDS routes rank by
+// tm_aggre: one wave per topic.  The usort is a bitonic sort of the keys —
+// for topics with up to 128 routes in registers, two per lane, carrying the
+// route's source and target, so a topic costs one round of coalesced loads
+// (the kernel is bound by load latency, not by sort work: an LDS sort and a
+// register sort that re-gathered src/dest after sorting both measured 3.2-3.5
+// ms per 2M C3 topics); otherwise in the wave's LDS row with route indices —
+// then a ballot keeps the first of each run of equal keys.  Topics with more than AG_LDS routes rank by
 // counting over a global scratch row at the topic's route offset instead.
 // Output goes straight to the topic's route offset (aggre never grows a
 // list): offsets are the route CSR's, counts are aggre's, so the lists need
@@ -52,11 +57,124 @@ __device__ __forceinline__ uint32_t wave_sum_u(uint32_t x) {
     return x;
 }
 
+__device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
+    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m, 64);
+    const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m, 64);
+    return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t shfl_u64(uint64_t v, int src) {
+    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, src, 64);
+    const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), src, 64);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// bitonic sort of 128 (key, a, b) triples held two per lane (element lane
+// and lane + 64) in registers: cross-lane steps by shuffles, the distance-64
+// step inside the lane; ascending by key
+__device__ __forceinline__ void wave_sort128(uint64_t& k0, uint32_t& a0, uint32_t& b0, uint64_t& k1, uint32_t& a1,
+                                             uint32_t& b1, uint32_t P, uint32_t lane) {
+    for (uint32_t size = 2; size <= P; size <<= 1) {
+        for (uint32_t d = size >> 1; d > 0; d >>= 1) {
+            if (d == 64) {
+                // pairs (lane, lane + 64); size == 128 here, so ascending
+                if (k0 > k1) {
+                    const uint64_t tk = k0; k0 = k1; k1 = tk;
+                    const uint32_t ta = a0; a0 = a1; a1 = ta;
+                    const uint32_t tb = b0; b0 = b1; b1 = tb;
+                }
+                continue;
+            }
+            const bool lower = (lane & d) == 0;
+            {
+                const uint64_t pk = shfl_xor_u64(k0, (int)d);
+                const uint32_t pa = (uint32_t)__shfl_xor((int)a0, (int)d, 64);
+                const uint32_t pb = (uint32_t)__shfl_xor((int)b0, (int)d, 64);
+                const bool up = (lane & size) == 0;            // element index lane
+                if (lower == up ? pk < k0 : pk > k0) { k0 = pk; a0 = pa; b0 = pb; }
+            }
+            if (P > 64) {
+                const uint64_t pk = shfl_xor_u64(k1, (int)d);
+                const uint32_t pa = (uint32_t)__shfl_xor((int)a1, (int)d, 64);
+                const uint32_t pb = (uint32_t)__shfl_xor((int)b1, (int)d, 64);
+                const bool up = ((lane + 64) & size) == 0;     // element index lane + 64
+                if (lower == up ? pk < k1 : pk > k1) { k1 = pk; a1 = pa; b1 = pb; }
+            }
+        }
+    }
+}
+
+// topics with up to 128 routes, all in registers: one round of coalesced
+// loads (src, dest, key) and a gather from the small target table, then the
+// fold's reversed tail and the usort go straight to the output
+__device__ __forceinline__ uint32_t aggre_regs(const AggreView& av, uint32_t m, uint64_t base, uint32_t lane,
+                                               const uint32_t* __restrict__ src, const uint32_t* __restrict__ dest,
+                                               const uint64_t* __restrict__ gkey, uint32_t* __restrict__ out_to,
+                                               uint32_t* __restrict__ out_tg, uint64_t out_cap) {
+    uint64_t k0 = ~0ull, k1 = ~0ull;
+    uint32_t s0 = 0, s1 = 0, g0 = 0, g1 = 0;
+    if (lane < m) {
+        s0 = src[base + lane];
+        k0 = gkey[base + lane];
+        g0 = av.dt[dest[base + lane]].y;
+    }
+    if (lane + 64 < m) {
+        s1 = src[base + lane + 64];
+        k1 = gkey[base + lane + 64];
+        g1 = av.dt[dest[base + lane + 64]].y;
+    }
+    int j = (g1 & AG_GROUP_BIT) ? (int)lane + 64 : (g0 & AG_GROUP_BIT) ? (int)lane : -1;
+    j = wave_max_i(j);
+    const uint32_t tail = (uint32_t)((int)m - 1 - j);
+    // r_{m-1} .. r_{j+1}: element i goes to position m - 1 - i
+    if ((int)lane > j && lane < m && base + (m - 1 - lane) < out_cap) {
+        out_to[base + (m - 1 - lane)] = s0;
+        out_tg[base + (m - 1 - lane)] = g0 & ~AG_GROUP_BIT;
+    }
+    if ((int)lane + 64 > j && lane + 64 < m && base + (m - 65 - lane) < out_cap) {
+        out_to[base + (m - 65 - lane)] = s1;
+        out_tg[base + (m - 65 - lane)] = g1 & ~AG_GROUP_BIT;
+    }
+    if (j < 0) return tail;
+    // lists:usort over r_0 .. r_j: keys past j become ~0 (above every real key)
+    const uint32_t u = (uint32_t)j + 1;
+    if (lane >= u) k0 = ~0ull;
+    if (lane + 64 >= u) k1 = ~0ull;
+    uint32_t P = 2;
+    while (P < u) P <<= 1;
+#if !(defined(TM_AGGRE_VARIANT) && TM_AGGRE_VARIANT == 2)   // EXPERIMENT 2: no sort
+    wave_sort128(k0, s0, g0, k1, s1, g1, P, lane);
+#endif
+    const uint64_t prev0 = shfl_u64(k0, (int)((lane + 63) & 63));   // element lane - 1 (unused at lane 0)
+    const uint64_t last0 = shfl_u64(k0, 63);
+    uint64_t prev1 = shfl_u64(k1, (int)((lane + 63) & 63));
+    if (lane == 0) prev1 = last0;                                    // element 64's predecessor is element 63
+    const bool keep0 = lane < u && (lane == 0 || k0 != prev0);
+    const bool keep1 = lane + 64 < u && k1 != prev1;
+    const uint64_t bal0 = __ballot(keep0), bal1 = __ballot(keep1);
+    const uint64_t lt = (1ull << lane) - 1;
+    const uint64_t o = base + tail;
+    if (keep0) {
+        const uint64_t pos = o + (uint32_t)__popcll(bal0 & lt);
+        if (pos < out_cap) {
+            out_to[pos] = s0;
+            out_tg[pos] = g0 & ~AG_GROUP_BIT;
+        }
+    }
+    if (keep1) {
+        const uint64_t pos = o + (uint32_t)__popcll(bal0) + (uint32_t)__popcll(bal1 & lt);
+        if (pos < out_cap) {
+            out_to[pos] = s1;
+            out_tg[pos] = g1 & ~AG_GROUP_BIT;
+        }
+    }
+    return tail + (uint32_t)__popcll(bal0) + (uint32_t)__popcll(bal1);
+}
+
 __global__ void __launch_bounds__(AG_BLOCK)
 tm_aggre(AggreView av, uint32_t n, const uint32_t* __restrict__ rcount, const uint64_t* __restrict__ roff,
-         const uint32_t* __restrict__ src, const uint32_t* __restrict__ dest, const uint2* __restrict__ exact,
-         uint64_t* __restrict__ gkey, uint8_t* __restrict__ gflag, uint32_t* __restrict__ acount,
-         uint32_t* __restrict__ out_to, uint32_t* __restrict__ out_tg, uint64_t out_cap) {
+         const uint32_t* __restrict__ src, const uint32_t* __restrict__ dest, const uint64_t* __restrict__ gkey,
+         uint8_t* __restrict__ gflag, uint32_t* __restrict__ acount, uint32_t* __restrict__ out_to,
+         uint32_t* __restrict__ out_tg, uint64_t out_cap) {
     __shared__ uint64_t lkey[AG_WAVES][AG_LDS];
     __shared__ uint16_t lidx[AG_WAVES][AG_LDS];
     const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -64,25 +182,21 @@ tm_aggre(AggreView av, uint32_t n, const uint32_t* __restrict__ rcount, const ui
     if (t >= n) return;   // whole wave; no block barriers below
     const uint32_t m = rcount[t];
     const uint64_t base = roff[t];
-    const uint2 xe = exact[t];
-    const uint32_t topic_rank = xe.y ? av.ex_rank[xe.x] : 0u;
+#if defined(TM_AGGRE_VARIANT) && TM_AGGRE_VARIANT == 1   // EXPERIMENT: launch + index loads only
+    if (lane == 0) acount[t] = m;
+    return;
+#endif
+    if (m <= 128) {
+        const uint32_t c = aggre_regs(av, m, base, lane, src, dest, gkey, out_to, out_tg, out_cap);
+        if (lane == 0) acount[t] = c;
+        return;
+    }
     const bool in_lds = m <= AG_LDS;
-    uint64_t* key = in_lds ? lkey[w] : gkey + base;
+    const uint64_t* key = gkey + base;   // keys from tm_route_emit (to_rank << 32 | target rank)
 
     int j = -1;
-    for (uint32_t i = lane; i < m; i += 64) {
-        const uint32_t s = src[base + i];
-        const uint2 d = av.dt[dest[base + i]];
-        const uint32_t tr = s == TM_ROUTE_TOPIC_ID ? topic_rank : av.fr_rank[s];
-        const uint64_t k = ((uint64_t)tr << 32) | d.x;
-        if (in_lds) {
-            lkey[w][i] = k;
-            lidx[w][i] = (uint16_t)i;
-        } else {
-            gkey[base + i] = k;
-        }
-        if (d.y & AG_GROUP_BIT) j = (int)i;
-    }
+    for (uint32_t i = lane; i < m; i += 64)
+        if (av.dt[dest[base + i]].y & AG_GROUP_BIT) j = (int)i;
     j = wave_max_i(j);
     const uint32_t tail = (uint32_t)((int)m - 1 - j);   // j = -1: every route
     for (uint32_t k = lane; k < tail; k += 64) {        // r_{m-1} .. r_{j+1}, prepended by the fold
@@ -100,7 +214,10 @@ tm_aggre(AggreView av, uint32_t n, const uint32_t* __restrict__ rcount, const ui
         const uint32_t u = (uint32_t)j + 1;
         uint32_t P = 1;
         while (P < u) P <<= 1;
-        for (uint32_t i = u + lane; i < P; i += 64) lkey[w][i] = ~0ull;
+        for (uint32_t i = lane; i < P; i += 64) {
+            lkey[w][i] = i < u ? key[i] : ~0ull;
+            lidx[w][i] = (uint16_t)i;
+        }
         for (uint32_t size = 2; size <= P; size <<= 1) {
             for (uint32_t d = size >> 1; d > 0; d >>= 1) {
                 __threadfence_block();
@@ -136,9 +253,9 @@ tm_aggre(AggreView av, uint32_t n, const uint32_t* __restrict__ rcount, const ui
             kept += (uint32_t)__popcll(bal);
         }
     } else if (j >= 0) {
-        // more than AG_LDS routes: rank-by-counting over a global scratch
-        // row (entry i survives iff no earlier entry has its key, and lands
-        // at the number of surviving keys below it)
+        // more than AG_LDS routes: rank-by-counting over the topic's global
+        // key row (entry i survives iff no earlier entry has its key, and
+        // lands at the number of surviving keys below it)
         const uint32_t u = (uint32_t)j + 1;
         uint8_t* flag = gflag + base;
         __threadfence_block();
@@ -169,12 +286,12 @@ tm_aggre(AggreView av, uint32_t n, const uint32_t* __restrict__ rcount, const ui
 }
 
 hipError_t launch_aggre(const AggreView& av, uint32_t n, const uint32_t* rcount, const uint64_t* roff,
-                        const uint32_t* src, const uint32_t* dest, const uint2* exact, uint64_t* gkey, uint8_t* gflag,
+                        const uint32_t* src, const uint32_t* dest, const uint64_t* key, uint8_t* gflag,
                         uint32_t* acount, uint32_t* out_to, uint32_t* out_tg, uint64_t out_cap, hipStream_t st) {
     if (n == 0) return hipSuccess;
     const dim3 g((n + AG_WAVES - 1) / AG_WAVES), blk(AG_BLOCK);
-    hipLaunchKernelGGL(tm_aggre, g, blk, 0, st, av, n, rcount, roff, src, dest, exact, gkey, gflag, acount, out_to,
-                       out_tg, out_cap);
+    hipLaunchKernelGGL(tm_aggre, g, blk, 0, st, av, n, rcount, roff, src, dest, key, gflag, acount, out_to, out_tg,
+                       out_cap);
     return hipGetLastError();
 }
 

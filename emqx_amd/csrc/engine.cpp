@@ -212,9 +212,10 @@ struct tm_engine {
     std::unordered_map<std::string, std::vector<uint32_t>> route_bag;   // topic -> dests, insertion order
     size_t route_total = 0;
     bool routes_dirty = true;         // the route image must be rebuilt at commit
-    DevBuf d_fr_off, d_fr_dest, d_ex_slots, d_ex_arena, d_ex_dest;
+    DevBuf d_fr_meta, d_fr_dest, d_ex_slots, d_ex_arena, d_ex_dest;
+    std::vector<uint32_t> h_fr_off;   // host copy of fr_meta's offsets (aggre rewrites the ranks)
     uint64_t ex_slot_mask = 0;
-    uint32_t fr_filters = 0;          // filter ids covered by fr_off
+    uint32_t fr_filters = 0;          // filter ids covered by fr_meta
     bool route_image = false;
     DevBuf w_rexact, w_rscan, w_rids, w_rcounts, w_roff;
 
@@ -229,7 +230,7 @@ struct tm_engine {
     struct AggKey { const std::string* key; uint32_t dest_off; uint32_t fid; };
     std::vector<AggKey> agg_keys;           // route image entries (set by build_route_image)
     bool aggre_dirty = true;
-    DevBuf d_fr_rank, d_ex_rank, d_dt;
+    DevBuf d_ex_rank, d_dt;
     DevBuf w_dsrc, w_dcount, w_akey, w_aflag;
 
     // ---- match workspace ----
@@ -736,7 +737,12 @@ struct tm_engine {
             b.ensure(std::max<size_t>(bytes, 16));
             if (bytes) HIPCHK(hipMemcpyAsync(b.p, src, bytes, hipMemcpyHostToDevice, stream));
         };
-        up(d_fr_off, fr_off.data(), fr_off.size() * 4);
+        {
+            std::vector<uint2> meta(fr_off.size());
+            for (size_t f = 0; f < fr_off.size(); ++f) meta[f] = make_uint2(fr_off[f], 0u);
+            up(d_fr_meta, meta.data(), meta.size() * sizeof(uint2));
+            HIPCHK(hipStreamSynchronize(stream));
+        }
         up(d_fr_dest, fr_dest.data(), fr_dest.size() * 4);
         up(d_ex_slots, slots.data(), slots.size() * sizeof(ExactSlot));
         up(d_ex_arena, arena.data(), arena.size());
@@ -745,6 +751,7 @@ struct tm_engine {
         fr_filters = nf;
         route_image = !route_bag.empty();
         HIPCHK(hipStreamSynchronize(stream));   // host vectors die here
+        h_fr_off.swap(fr_off);
         routes_dirty = false;
     }
     // ------------------------------------------------------------------
@@ -769,10 +776,12 @@ struct tm_engine {
         for (uint32_t i = 0; i < order.size(); ++i) order[i] = i;
         std::sort(order.begin(), order.end(),
                   [&](uint32_t a, uint32_t b) { return *agg_keys[a].key < *agg_keys[b].key; });
-        std::vector<uint32_t> fr_rank(std::max<uint32_t>(nf, 1), 0), ex_rank(std::max<size_t>(route_total, 1), 0);
+        std::vector<uint2> fr_meta(h_fr_off.size());
+        for (size_t f = 0; f < h_fr_off.size(); ++f) fr_meta[f] = make_uint2(h_fr_off[f], 0u);
+        std::vector<uint32_t> ex_rank(std::max<size_t>(route_total, 1), 0);
         for (uint32_t r = 0; r < order.size(); ++r) {
             const AggKey& a = agg_keys[order[r]];
-            if (a.fid != FILTER_NONE && a.fid < nf) fr_rank[a.fid] = r;
+            if (a.fid != FILTER_NONE && a.fid < nf) fr_meta[a.fid].y = r;
             if (a.dest_off < ex_rank.size()) ex_rank[a.dest_off] = r;
         }
         const size_t nd = dest_names.size();
@@ -794,7 +803,7 @@ struct tm_engine {
             b.ensure(std::max<size_t>(bytes, 16));
             if (bytes) HIPCHK(hipMemcpyAsync(b.p, src, bytes, hipMemcpyHostToDevice, stream));
         };
-        up(d_fr_rank, fr_rank.data(), fr_rank.size() * 4);
+        if (!fr_meta.empty()) up(d_fr_meta, fr_meta.data(), fr_meta.size() * sizeof(uint2));
         up(d_ex_rank, ex_rank.data(), ex_rank.size() * 4);
         up(d_dt, dt.data(), dt.size() * sizeof(uint2));
         HIPCHK(hipStreamSynchronize(stream));   // host vectors die here
@@ -802,7 +811,6 @@ struct tm_engine {
     }
     AggreView aggre_view() const {
         AggreView av;
-        av.fr_rank = d_fr_rank.as<const uint32_t>();
         av.ex_rank = d_ex_rank.as<const uint32_t>();
         av.dt = d_dt.as<const uint2>();
         return av;
@@ -810,7 +818,7 @@ struct tm_engine {
 
     RouteView route_view() const {
         RouteView rv;
-        rv.fr_off = d_fr_off.as<const uint32_t>();
+        rv.fr_meta = d_fr_meta.as<const uint2>();
         rv.fr_dest = d_fr_dest.as<const uint32_t>();
         rv.n_filters = route_image ? fr_filters : 0u;
         rv.ex_slots = route_image ? d_ex_slots.as<const ExactSlot>() : nullptr;
@@ -1245,9 +1253,7 @@ struct tm_engine {
     }
     // emqx_router:match_routes/1 over a device batch (stream-ordered except
     // for one read of the match total that sizes the ids workspace)
-    void run_routes(const uint8_t* bytes, const uint64_t* off, uint32_t n, uint64_t nbytes, uint32_t* counts,
-                    uint64_t* out_off, uint32_t* src, uint32_t* dest, uint64_t cap, uint64_t* total,
-                    hipStream_t st) {
+    void ensure_route_image() {
         if (routes_dirty) {
             if (route_bag.empty()) {
                 route_image = false;
@@ -1258,6 +1264,11 @@ struct tm_engine {
                 build_route_image();
             }
         }
+    }
+    void run_routes(const uint8_t* bytes, const uint64_t* off, uint32_t n, uint64_t nbytes, uint32_t* counts,
+                    uint64_t* out_off, uint32_t* src, uint32_t* dest, uint64_t cap, uint64_t* total,
+                    hipStream_t st, uint64_t* out_key = nullptr) {
+        ensure_route_image();
         w_rcounts.ensure((size_t)n * 4 + 4);
         w_roff.ensure((size_t)(n + 1) * 8);
         uint64_t want = std::max<uint64_t>(w_rids.bytes / 4, (uint64_t)n * 16 + 1024);
@@ -1274,36 +1285,41 @@ struct tm_engine {
         }
         w_rexact.ensure((size_t)n * 8 + 8);
         w_rscan.ensure(scan_tmp_elems(n) * 8 + 8);
+        const AggreView av_tmp = aggre_view();
         HIPCHK(launch_routes(route_view(), bytes, off, n, w_rcounts.as<uint32_t>(), w_roff.as<uint64_t>(),
                              w_rids.as<uint32_t>(), w_rexact.as<uint2>(), counts, out_off, src, dest, cap, total,
-                             w_rscan.as<uint64_t>(), st));
+                             w_rscan.as<uint64_t>(), st, out_key ? &av_tmp : nullptr, out_key));
     }
 
-    // aggre(match_routes(T)) over a device batch: the route lists go to
-    // engine workspace (one read of the route total sizes it), aggre.hip
-    // writes each topic's list at its route offset; *total = route total
+    // aggre(match_routes(T)) over a device batch: the route lists and their
+    // sort keys go to engine workspace (one read of the route total sizes
+    // it), aggre.hip writes each topic's list at its route offset; *total =
+    // route total
     void run_deliveries(const uint8_t* bytes, const uint64_t* off, uint32_t n, uint64_t nbytes, uint32_t* counts,
                         uint64_t* out_off, uint32_t* to, uint32_t* target, uint64_t cap, uint64_t* total,
                         hipStream_t st) {
+        ensure_route_image();
+        if (aggre_dirty) build_aggre_image();
         w_dcount.ensure((size_t)n * 4 + 4);
         uint64_t want = std::max<uint64_t>(w_dsrc.bytes / 8, (uint64_t)n * 16 + 1024);
         w_dsrc.ensure(want * 8, 1.0);
-        uint64_t rcap = w_dsrc.bytes / 8, rtotal = 0;
+        w_akey.ensure(want * 8, 1.0);
+        uint64_t rcap = std::min(w_dsrc.bytes / 8, w_akey.bytes / 8), rtotal = 0;
         for (int pass = 0; pass < 2; ++pass) {
             uint32_t* src = w_dsrc.as<uint32_t>();
-            run_routes(bytes, off, n, nbytes, w_dcount.as<uint32_t>(), out_off, src, src + rcap, rcap, total, st);
+            run_routes(bytes, off, n, nbytes, w_dcount.as<uint32_t>(), out_off, src, src + rcap, rcap, total, st,
+                       w_akey.as<uint64_t>());
             HIPCHK(hipMemcpyAsync(&rtotal, total, 8, hipMemcpyDeviceToHost, st));
             HIPCHK(hipStreamSynchronize(st));
             if (rtotal <= rcap) break;
             w_dsrc.ensure(rtotal * 8, 1.25);
-            rcap = w_dsrc.bytes / 8;
+            w_akey.ensure(rtotal * 8, 1.25);
+            rcap = std::min(w_dsrc.bytes / 8, w_akey.bytes / 8);
         }
-        if (aggre_dirty) build_aggre_image();
-        w_akey.ensure(rcap * 8 + 8, 1.0);
         w_aflag.ensure(rcap + 8, 1.0);
         const uint32_t* src = w_dsrc.as<uint32_t>();
-        HIPCHK(launch_aggre(aggre_view(), n, w_dcount.as<uint32_t>(), out_off, src, src + rcap, w_rexact.as<uint2>(),
-                            w_akey.as<uint64_t>(), w_aflag.as<uint8_t>(), counts, to, target, cap, st));
+        HIPCHK(launch_aggre(aggre_view(), n, w_dcount.as<uint32_t>(), out_off, src, src + rcap, w_akey.as<uint64_t>(),
+                            w_aflag.as<uint8_t>(), counts, to, target, cap, st));
     }
 
     void finish_batch(hipStream_t st, uint32_t n) {
@@ -1430,8 +1446,8 @@ void tm_close(tm_engine* e) {
     if (e->device >= 0) {
         (void)hipSetDevice(e->device);
         if (e->stream) (void)hipStreamSynchronize(e->stream);
-        for (DevBuf* b : {&e->d_fr_rank, &e->d_ex_rank, &e->d_dt, &e->w_dsrc, &e->w_dcount, &e->w_akey, &e->w_aflag,
-             &e->d_fr_off, &e->d_fr_dest, &e->d_ex_slots, &e->d_ex_arena, &e->d_ex_dest, &e->w_rexact,
+        for (DevBuf* b : {&e->d_ex_rank, &e->d_dt, &e->w_dsrc, &e->w_dcount, &e->w_akey, &e->w_aflag,
+             &e->d_fr_meta, &e->d_fr_dest, &e->d_ex_slots, &e->d_ex_arena, &e->d_ex_dest, &e->w_rexact,
                           &e->w_rscan, &e->w_rids, &e->w_rcounts, &e->w_roff})
             b->release();
         for (DevBuf* b : {&e->d_nodes, &e->d_edges, &e->d_hedges, &e->d_dict, &e->d_arena, &e->d_woff, &e->d_inner, &e->d_leaf,

@@ -111,7 +111,7 @@ struct ImageView {
 
 // ---- route image (emqx_route bag, src/emqx_router.erl:52-59, 89-90) --------
 // Routes are (topic, dest) pairs; dests are interned to u32 ids.  The routes
-// of a trie filter are found by its filter id (CSR fr_off/fr_dest over filter
+// of a trie filter are found by its filter id (CSR fr_meta/fr_dest over filter
 // ids, bag insertion order); the routes of a literal topic (get_routes/1 of
 // the publish topic itself) through an exact-topic hash table whose keys are
 // verified byte for byte against the topic arena (8-aligned, zero padded).
@@ -127,7 +127,7 @@ struct alignas(32) ExactSlot {
 };
 
 struct RouteView {
-    const uint32_t*  fr_off;        // n_filters + 1
+    const uint2*     fr_meta;       // n_filters + 1: {dest offset (CSR), to_rank (aggre; 0 until built)}
     const uint32_t*  fr_dest;
     uint32_t         n_filters;
     const ExactSlot* ex_slots;      // null: no routes
@@ -138,8 +138,9 @@ struct RouteView {
 
 // emqx_broker:aggre/1 tables (aggre.hip): sort ranks of every topic with
 // routes (Erlang binary order) and, per dest id, its aggre target
+// (a filter's to_rank rides in RouteView::fr_meta, in the line the route
+// kernels fetch anyway)
 struct AggreView {
-    const uint32_t* fr_rank;        // filter id -> to_rank
     const uint32_t* ex_rank;        // exact-table dest_off -> to_rank of that topic
     const uint2*    dt;             // dest id -> {target rank, target id | group << 31}
 };

@@ -47,19 +47,21 @@ hipError_t launch_scan(const uint32_t* counts, uint32_t n, uint64_t* out_off, ui
 // emqx_router:match_routes/1 expansion (routes.hip) of a batch's ordered
 // match lists: per topic its literal-topic routes, then each matched filter's
 // routes.  exact: n uint2, rcount: n u32, tmp: scan_tmp_elems(n).  out_cap
-// == 0: counts and offsets only.
+// == 0: counts and offsets only.  av != null: also out_key[route] =
+// to_rank << 32 | target rank (the aggre sort key).
 hipError_t launch_routes(const RouteView& rv, const uint8_t* bytes, const uint64_t* off, uint32_t n,
                          const uint32_t* counts, const uint64_t* ids_off, const uint32_t* ids, uint2* exact,
                          uint32_t* rcount, uint64_t* out_off, uint32_t* out_src, uint32_t* out_dest,
-                         uint64_t out_cap, uint64_t* total, uint64_t* scan_tmp, hipStream_t st);
+                         uint64_t out_cap, uint64_t* total, uint64_t* scan_tmp, hipStream_t st,
+                         const AggreView* av = nullptr, uint64_t* out_key = nullptr);
 
 // emqx_broker:aggre/1 (aggre.hip) over a match_routes CSR (rcount, roff,
-// src, dest; exact from launch_routes).  gkey / gflag: one u64 / u8 per route
-// (used by topics with > 512 routes).  Output at the route offsets: topic t's
+// src, dest, key from launch_routes with av).  gflag: one u8 per route (used
+// by topics with > 512 routes).  Output at the route offsets: topic t's
 // list is out_to / out_tg[roff[t] .. + acount[t]) (out_to = TM_ROUTE_TOPIC_ID
 // or a filter id, out_tg = target id); entries at or past out_cap are dropped.
 hipError_t launch_aggre(const AggreView& av, uint32_t n, const uint32_t* rcount, const uint64_t* roff,
-                        const uint32_t* src, const uint32_t* dest, const uint2* exact, uint64_t* gkey, uint8_t* gflag,
+                        const uint32_t* src, const uint32_t* dest, const uint64_t* key, uint8_t* gflag,
                         uint32_t* acount, uint32_t* out_to, uint32_t* out_tg, uint64_t out_cap, hipStream_t st);
 
 // Sharded mode (shard.hip): merge per-topic match lists of S filter shards

@@ -11,7 +11,10 @@
 // hash table verified byte for byte), then, for each matched filter in
 // emqx_trie:match/1 order, that filter's routes (its emqx_route bag, in
 // insertion order).  Output: per-topic counts and offsets, and per route the
-// source (filter id, or TM_ROUTE_TOPIC_ID for the literal topic) and dest id.
+// source (filter id, or TM_ROUTE_TOPIC_ID for the literal topic) and dest id,
+// and, for aggre (aggre.hip), each route's sort key to_rank << 32 | target
+// rank: a filter's to_rank shares the 8 B fr_meta entry the emit reads anyway,
+// so the keys cost no extra random loads.
 //
 // Two passes over blocks of 256 topics (the ids of a block are a contiguous
 // CSR range, read coalesced): count, scan, emit.
@@ -117,7 +120,7 @@ tm_route_count(RouteView rv, const uint8_t* __restrict__ bytes, const uint64_t* 
     const uint64_t base = ids_off[t0];
     for (uint64_t j = threadIdx.x; j < agg; j += RBLOCK) {
         const uint32_t id = ids[base + j];
-        const uint32_t rc = id < rv.n_filters ? rv.fr_off[id + 1] - rv.fr_off[id] : 0u;
+        const uint32_t rc = id < rv.n_filters ? rv.fr_meta[id + 1].x - rv.fr_meta[id].x : 0u;
         if (rc) atomicAdd(&lds_mr[topic_of(lds_inc, tn, j)], rc);
     }
     __syncthreads();
@@ -127,10 +130,11 @@ tm_route_count(RouteView rv, const uint8_t* __restrict__ bytes, const uint64_t* 
 // pass 2: routes of topic t at out_off[t]: its exact routes, then the
 // routes of each matched filter in match order
 __global__ void __launch_bounds__(RBLOCK)
-tm_route_emit(RouteView rv, uint32_t n, const uint32_t* __restrict__ counts, const uint64_t* __restrict__ ids_off,
-              const uint32_t* __restrict__ ids, const uint2* __restrict__ exact,
-              const uint32_t* __restrict__ rcount, const uint64_t* __restrict__ out_off,
-              uint32_t* __restrict__ out_src, uint32_t* __restrict__ out_dest, uint64_t out_cap) {
+tm_route_emit(RouteView rv, AggreView av, uint32_t n, const uint32_t* __restrict__ counts,
+              const uint64_t* __restrict__ ids_off, const uint32_t* __restrict__ ids,
+              const uint2* __restrict__ exact, const uint32_t* __restrict__ rcount,
+              const uint64_t* __restrict__ out_off, uint32_t* __restrict__ out_src, uint32_t* __restrict__ out_dest,
+              uint64_t* __restrict__ out_key, uint64_t out_cap) {
     __shared__ uint32_t lds_inc[RBLOCK];
     __shared__ uint64_t lds_m[RBLOCK];      // exclusive prefix of matched-route counts
     __shared__ uint64_t lds_scan[RBLOCK / 64];
@@ -147,10 +151,13 @@ tm_route_emit(RouteView rv, uint32_t n, const uint32_t* __restrict__ counts, con
     lds_m[threadIdx.x] = r_block_exclusive_scan(mr, lds_scan, magg);
     if (threadIdx.x < tn) {   // get_routes(Topic): the literal topic's routes first
         const uint64_t o = out_off[t];
+        const uint64_t xr = out_key && xe.y ? (uint64_t)av.ex_rank[xe.x] << 32 : 0ull;
         for (uint32_t k = 0; k < xe.y; ++k)
             if (o + k < out_cap) {
+                const uint32_t d = rv.ex_dest[xe.x + k];
                 out_src[o + k] = TM_ROUTE_TOPIC_ID;
-                out_dest[o + k] = rv.ex_dest[xe.x + k];
+                out_dest[o + k] = d;
+                if (out_key) out_key[o + k] = xr | av.dt[d].x;
             }
     }
     __syncthreads();
@@ -158,13 +165,15 @@ tm_route_emit(RouteView rv, uint32_t n, const uint32_t* __restrict__ counts, con
     uint64_t carry = 0;
     for (uint64_t c0 = 0; c0 < agg; c0 += RBLOCK) {   // block-uniform trip count
         const uint64_t j = c0 + threadIdx.x;
-        uint32_t id = 0, rc = 0, fo = 0, lo = 0;
+        uint32_t id = 0, rc = 0, fo = 0, lo = 0, fr = 0;
         if (j < agg) {
             id = ids[base + j];
             lo = topic_of(lds_inc, tn, j);
             if (id < rv.n_filters) {
-                fo = rv.fr_off[id];
-                rc = rv.fr_off[id + 1] - fo;
+                const uint2 fm = rv.fr_meta[id];
+                fo = fm.x;
+                fr = fm.y;
+                rc = rv.fr_meta[id + 1].x - fo;
             }
         }
         uint64_t chunk;
@@ -174,8 +183,10 @@ tm_route_emit(RouteView rv, uint32_t n, const uint32_t* __restrict__ counts, con
             const uint64_t pos = out_off[tl] + exact[tl].y + (r - lds_m[lo]);
             for (uint32_t k = 0; k < rc; ++k)
                 if (pos + k < out_cap) {
+                    const uint32_t d = rv.fr_dest[fo + k];
                     out_src[pos + k] = id;
-                    out_dest[pos + k] = rv.fr_dest[fo + k];
+                    out_dest[pos + k] = d;
+                    if (out_key) out_key[pos + k] = ((uint64_t)fr << 32) | av.dt[d].x;
                 }
         }
         carry += chunk;
@@ -187,7 +198,8 @@ static inline uint32_t rdiv_up(uint64_t a, uint64_t b) { return (uint32_t)((a + 
 hipError_t launch_routes(const RouteView& rv, const uint8_t* bytes, const uint64_t* off, uint32_t n,
                          const uint32_t* counts, const uint64_t* ids_off, const uint32_t* ids, uint2* exact,
                          uint32_t* rcount, uint64_t* out_off, uint32_t* out_src, uint32_t* out_dest,
-                         uint64_t out_cap, uint64_t* total, uint64_t* scan_tmp, hipStream_t st) {
+                         uint64_t out_cap, uint64_t* total, uint64_t* scan_tmp, hipStream_t st, const AggreView* av,
+                         uint64_t* out_key) {
     if (n == 0) {
         hipError_t err = hipMemsetAsync(out_off, 0, 8, st);
         return err == hipSuccess ? hipMemsetAsync(total, 0, 8, st) : err;
@@ -197,8 +209,8 @@ hipError_t launch_routes(const RouteView& rv, const uint8_t* bytes, const uint64
     hipError_t err = launch_scan(rcount, n, out_off, total, scan_tmp, st);
     if (err != hipSuccess) return err;
     if (out_cap)
-        hipLaunchKernelGGL(tm_route_emit, g, blk, 0, st, rv, n, counts, ids_off, ids, exact, rcount, out_off,
-                           out_src, out_dest, out_cap);
+        hipLaunchKernelGGL(tm_route_emit, g, blk, 0, st, rv, av ? *av : AggreView{nullptr, nullptr}, n, counts,
+                           ids_off, ids, exact, rcount, out_off, out_src, out_dest, av ? out_key : nullptr, out_cap);
     return hipGetLastError();
 }
 

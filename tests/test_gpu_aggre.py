@@ -64,7 +64,8 @@ def test_aggre_random_ops_vs_oracle(gpu_device):
 
 
 def test_aggre_long_lists_global_scratch(gpu_device):
-    """topics with > 512 routes take the global-scratch path of tm_aggre"""
+    """route lists on every tm_aggre path: registers (<= 128), LDS (<= 512)
+    and the global-scratch path (> 512)"""
     e = Engine(device=gpu_device)
     r, o = Router(e, node="n1"), pytrie.RouteTable()
     rng = random.Random(5)
@@ -73,9 +74,15 @@ def test_aggre_long_lists_global_scratch(gpu_device):
             d = ("g%d" % (k % 37), "n%d" % (k % 5)) if k % 3 == 0 else "n%d" % k
             r.add_route(f, d)
             o.add_route(f, d)
-    topics = [b"a/b", b"a/c", b"x/b", b"a", b"$SYS/b"]
+    for k in range(40):                       # a short list with groups: the register path
+        d = ("g%d" % (k % 3), "n1") if k % 2 else "n%d" % (k % 7)
+        r.add_route(b"$SYS/z", d)
+        o.add_route(b"$SYS/z", d)
+    topics = [b"a/b", b"a/c", b"x/b", b"a", b"$SYS/b", b"q", b"$SYS/z"]
     got = r.match_deliveries_many(topics, tagged=True)
-    assert sum(len(o.match_routes(b"a/b")) for _ in [0]) > 512
+    sizes = [len(o.match_routes(tp)) for tp in topics]
+    # every kernel path: registers (<= 128 routes), LDS (<= 512), global scratch
+    assert min(sizes) <= 128 and any(128 < x <= 512 for x in sizes) and max(sizes) > 512, sizes
     for tp, row in zip(topics, got):
         assert row == o.match_deliveries(tp), tp
     e.close()

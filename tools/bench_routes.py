@@ -49,7 +49,11 @@ def main():
     ap.add_argument("--exact", type=int, default=1_000_000)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--check", type=int, default=20_000)
+    ap.add_argument("--lib", default=None, help="EXPERIMENT: alternative build of libtopicmatch.so (A/B)")
     a = ap.parse_args()
+    if a.lib:
+        from emqx_amd import _lib
+        _lib.LIB_PATH = os.path.abspath(a.lib)
     dev = torch.device("cuda", 0)
     st = torch.cuda.current_stream(dev)
     cfg = W.CONFIGS[a.config]
