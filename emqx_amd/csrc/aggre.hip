@@ -68,36 +68,29 @@ __device__ __forceinline__ uint64_t shfl_u64(uint64_t v, int src) {
     return ((uint64_t)hi << 32) | lo;
 }
 
-// bitonic sort of 128 (key, a, b) triples held two per lane (element lane
-// and lane + 64) in registers: cross-lane steps by shuffles, the distance-64
-// step inside the lane; ascending by key
-__device__ __forceinline__ void wave_sort128(uint64_t& k0, uint32_t& a0, uint32_t& b0, uint64_t& k1, uint32_t& a1,
-                                             uint32_t& b1, uint32_t P, uint32_t lane) {
+// bitonic sort of 128 u64 keys held two per lane (element lane and lane +
+// 64) in registers: cross-lane steps by shuffles, the distance-64 step inside
+// the lane; ascending.  Keys only (each carries its element index in its low
+// bits), so a step costs two 32-bit shuffles per element.
+__device__ __forceinline__ void wave_sort128(uint64_t& k0, uint64_t& k1, uint32_t P, uint32_t lane) {
     for (uint32_t size = 2; size <= P; size <<= 1) {
         for (uint32_t d = size >> 1; d > 0; d >>= 1) {
-            if (d == 64) {
-                // pairs (lane, lane + 64); size == 128 here, so ascending
-                if (k0 > k1) {
-                    const uint64_t tk = k0; k0 = k1; k1 = tk;
-                    const uint32_t ta = a0; a0 = a1; a1 = ta;
-                    const uint32_t tb = b0; b0 = b1; b1 = tb;
-                }
+            if (d == 64) {   // pairs (lane, lane + 64); size == 128 here, so ascending
+                const uint64_t lo = k0 < k1 ? k0 : k1, hi = k0 < k1 ? k1 : k0;
+                k0 = lo;
+                k1 = hi;
                 continue;
             }
             const bool lower = (lane & d) == 0;
             {
                 const uint64_t pk = shfl_xor_u64(k0, (int)d);
-                const uint32_t pa = (uint32_t)__shfl_xor((int)a0, (int)d, 64);
-                const uint32_t pb = (uint32_t)__shfl_xor((int)b0, (int)d, 64);
                 const bool up = (lane & size) == 0;            // element index lane
-                if (lower == up ? pk < k0 : pk > k0) { k0 = pk; a0 = pa; b0 = pb; }
+                if (lower == up ? pk < k0 : pk > k0) k0 = pk;
             }
             if (P > 64) {
                 const uint64_t pk = shfl_xor_u64(k1, (int)d);
-                const uint32_t pa = (uint32_t)__shfl_xor((int)a1, (int)d, 64);
-                const uint32_t pb = (uint32_t)__shfl_xor((int)b1, (int)d, 64);
                 const bool up = ((lane + 64) & size) == 0;     // element index lane + 64
-                if (lower == up ? pk < k1 : pk > k1) { k1 = pk; a1 = pa; b1 = pb; }
+                if (lower == up ? pk < k1 : pk > k1) k1 = pk;
             }
         }
     }
@@ -135,36 +128,45 @@ __device__ __forceinline__ uint32_t aggre_regs(const AggreView& av, uint32_t m, 
         out_tg[base + (m - 65 - lane)] = g1 & ~AG_GROUP_BIT;
     }
     if (j < 0) return tail;
-    // lists:usort over r_0 .. r_j: keys past j become ~0 (above every real key)
+    // lists:usort over r_0 .. r_j.  Sort word: to_rank << 32 | target rank <<
+    // 7 | element index (target ranks < 2^25, checked on the host): unique,
+    // so the sort needs no payload; keys past j become ~0 (above every real
+    // key); equal routes are equal in the word's top 57 bits.
     const uint32_t u = (uint32_t)j + 1;
-    if (lane >= u) k0 = ~0ull;
-    if (lane + 64 >= u) k1 = ~0ull;
+    k0 = lane < u ? (k0 & 0xFFFFFFFF00000000ull) | ((k0 & 0xFFFFFFFFull) << 7) | lane : ~0ull;
+    k1 = lane + 64 < u ? (k1 & 0xFFFFFFFF00000000ull) | ((k1 & 0xFFFFFFFFull) << 7) | (lane + 64) : ~0ull;
     uint32_t P = 2;
     while (P < u) P <<= 1;
 #if !(defined(TM_AGGRE_VARIANT) && TM_AGGRE_VARIANT == 2)   // EXPERIMENT 2: no sort
-    wave_sort128(k0, s0, g0, k1, s1, g1, P, lane);
+    wave_sort128(k0, k1, P, lane);
 #endif
     const uint64_t prev0 = shfl_u64(k0, (int)((lane + 63) & 63));   // element lane - 1 (unused at lane 0)
     const uint64_t last0 = shfl_u64(k0, 63);
     uint64_t prev1 = shfl_u64(k1, (int)((lane + 63) & 63));
     if (lane == 0) prev1 = last0;                                    // element 64's predecessor is element 63
-    const bool keep0 = lane < u && (lane == 0 || k0 != prev0);
-    const bool keep1 = lane + 64 < u && k1 != prev1;
+    const bool keep0 = lane < u && (lane == 0 || (k0 >> 7) != (prev0 >> 7));
+    const bool keep1 = lane + 64 < u && (k1 >> 7) != (prev1 >> 7);
+    // source and target of each sorted word's element, from its owner lane
+    const uint32_t e0 = (uint32_t)k0 & 127u, e1 = (uint32_t)k1 & 127u;
+    const uint32_t sa0 = (uint32_t)__shfl((int)s0, (int)(e0 & 63), 64), sb0 = (uint32_t)__shfl((int)s1, (int)(e0 & 63), 64);
+    const uint32_t ga0 = (uint32_t)__shfl((int)g0, (int)(e0 & 63), 64), gb0 = (uint32_t)__shfl((int)g1, (int)(e0 & 63), 64);
+    const uint32_t sa1 = (uint32_t)__shfl((int)s0, (int)(e1 & 63), 64), sb1 = (uint32_t)__shfl((int)s1, (int)(e1 & 63), 64);
+    const uint32_t ga1 = (uint32_t)__shfl((int)g0, (int)(e1 & 63), 64), gb1 = (uint32_t)__shfl((int)g1, (int)(e1 & 63), 64);
     const uint64_t bal0 = __ballot(keep0), bal1 = __ballot(keep1);
     const uint64_t lt = (1ull << lane) - 1;
     const uint64_t o = base + tail;
     if (keep0) {
         const uint64_t pos = o + (uint32_t)__popcll(bal0 & lt);
         if (pos < out_cap) {
-            out_to[pos] = s0;
-            out_tg[pos] = g0 & ~AG_GROUP_BIT;
+            out_to[pos] = e0 < 64 ? sa0 : sb0;
+            out_tg[pos] = (e0 < 64 ? ga0 : gb0) & ~AG_GROUP_BIT;
         }
     }
     if (keep1) {
         const uint64_t pos = o + (uint32_t)__popcll(bal0) + (uint32_t)__popcll(bal1 & lt);
         if (pos < out_cap) {
-            out_to[pos] = s1;
-            out_tg[pos] = g1 & ~AG_GROUP_BIT;
+            out_to[pos] = e1 < 64 ? sa1 : sb1;
+            out_tg[pos] = (e1 < 64 ? ga1 : gb1) & ~AG_GROUP_BIT;
         }
     }
     return tail + (uint32_t)__popcll(bal0) + (uint32_t)__popcll(bal1);

@@ -790,6 +790,8 @@ struct tm_engine {
             if (dest_target[d] == TARGET_DEFAULT)
                 dest_target[d] = intern_target(0, reinterpret_cast<const uint8_t*>(dest_names[d].data()),
                                                (uint32_t)dest_names[d].size());
+        if (target_names.size() >= (1u << 25))   // aggre.hip packs rank << 7 | index into 32 bits
+            throw RangeError("aggre: more than 2^25 targets");
         std::vector<uint32_t> tord(target_names.size()), trank(target_names.size());
         for (uint32_t i = 0; i < tord.size(); ++i) tord[i] = i;
         std::sort(tord.begin(), tord.end(), [&](uint32_t a, uint32_t b) { return target_names[a] < target_names[b]; });
