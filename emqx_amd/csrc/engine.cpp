@@ -1388,7 +1388,7 @@ inline void split_levels(const uint8_t* p, uint32_t len, std::vector<std::pair<u
 
 extern "C" {
 
-const char* tm_build_info(void) { return "libtopicmatch gfx950 (CDNA4) HIP; image v2 (node32+2 inline/edge16x4/dict16)"; }
+const char* tm_build_info(void) { return "libtopicmatch gfx950 (CDNA4) HIP; image v4 (inner/leaf 16 B halves, Bloom-masked edge16, dict with 16 B word prefixes), routes + aggre"; }
 
 const char* tm_strerror(int code) {
     switch (code) {
