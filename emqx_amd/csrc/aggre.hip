@@ -72,8 +72,11 @@ __device__ __forceinline__ uint64_t shfl_u64(uint64_t v, int src) {
 // 64) in registers: cross-lane steps by shuffles, the distance-64 step inside
 // the lane; ascending.  Keys only (each carries its element index in its low
 // bits), so a step costs two 32-bit shuffles per element.
-__device__ __forceinline__ void wave_sort128(uint64_t& k0, uint64_t& k1, uint32_t P, uint32_t lane) {
+template <uint32_t P>
+__device__ __forceinline__ void wave_sort_p(uint64_t& k0, uint64_t& k1, uint32_t lane) {
+#pragma unroll
     for (uint32_t size = 2; size <= P; size <<= 1) {
+#pragma unroll
         for (uint32_t d = size >> 1; d > 0; d >>= 1) {
             if (d == 64) {   // pairs (lane, lane + 64); size == 128 here, so ascending
                 const uint64_t lo = k0 < k1 ? k0 : k1, hi = k0 < k1 ? k1 : k0;
@@ -94,6 +97,15 @@ __device__ __forceinline__ void wave_sort128(uint64_t& k0, uint64_t& k1, uint32_
             }
         }
     }
+}
+// the network unrolled at compile time for the padded size P (a runtime
+// distance loop, and DPP picked per stage by a switch, measured slower)
+__device__ __forceinline__ void wave_sort128(uint64_t& k0, uint64_t& k1, uint32_t P, uint32_t lane) {
+    if (P <= 8) wave_sort_p<8>(k0, k1, lane);
+    else if (P <= 16) wave_sort_p<16>(k0, k1, lane);
+    else if (P <= 32) wave_sort_p<32>(k0, k1, lane);
+    else if (P <= 64) wave_sort_p<64>(k0, k1, lane);
+    else wave_sort_p<128>(k0, k1, lane);
 }
 
 // topics with up to 128 routes, all in registers: one round of coalesced
