@@ -25,14 +25,15 @@
 // rank over every target), so a sort key is one u64 = to_rank << 32 | rank;
 // tm_route_emit writes it beside each route (routes.hip).
 //
-// tm_aggre: one wave per topic.  The usort is a bitonic sort of the keys —
-// for topics with up to 128 routes in registers, two per lane, carrying the
-// route's source and target, so a topic costs one round of coalesced loads
-// (the kernel is bound by load latency, not by sort work: an LDS sort and a
-// register sort that re-gathered src/dest after sorting both measured 3.2-3.5
-// ms per 2M C3 topics); otherwise in the wave's LDS row with route indices —
-// then a ballot keeps the first of each run of equal keys.  Topics with more than AG_LDS routes rank by
-// counting over a global scratch row at the topic's route offset instead.
+// tm_aggre: one wave per topic with up to 128 routes, all in registers: one
+// round of coalesced loads (src, dest, key), a bitonic sort of 64-bit words
+// (key with the element index packed under the target rank, two per lane,
+// network unrolled per padded size), a ballot that keeps the first of each
+// run of equal keys; up to 512 routes the same in the wave's LDS row.
+// Larger topics go on a device-built list that
+// tm_aggre_large works through with one 256-thread block per topic (LDS
+// bitonic up to 4096 routes, rank-by-counting over the global key row
+// beyond), so nothing waits on the host.
 // Output goes straight to the topic's route offset (aggre never grows a
 // list): offsets are the route CSR's, counts are aggre's, so the lists need
 // no compaction pass (measured 0.75 ms per 2M topics at C3).
@@ -45,8 +46,8 @@ namespace tmx {
 
 constexpr int AG_BLOCK = 256;
 constexpr int AG_WAVES = AG_BLOCK / 64;
-constexpr uint32_t AG_LDS = 512;
 constexpr uint32_t AG_GROUP_BIT = 0x80000000u;
+constexpr uint32_t AG_LDS = 512;   // tm_aggre's per-wave LDS row (routes)
 
 __device__ __forceinline__ int wave_max_i(int x) {
     for (int o = 32; o > 0; o >>= 1) x = max(x, __shfl_xor(x, o, 64));
@@ -187,7 +188,7 @@ __device__ __forceinline__ uint32_t aggre_regs(const AggreView& av, uint32_t m, 
 __global__ void __launch_bounds__(AG_BLOCK)
 tm_aggre(AggreView av, uint32_t n, const uint32_t* __restrict__ rcount, const uint64_t* __restrict__ roff,
          const uint32_t* __restrict__ src, const uint32_t* __restrict__ dest, const uint64_t* __restrict__ gkey,
-         uint8_t* __restrict__ gflag, uint32_t* __restrict__ acount, uint32_t* __restrict__ out_to,
+         uint32_t* __restrict__ large, uint32_t* __restrict__ acount, uint32_t* __restrict__ out_to,
          uint32_t* __restrict__ out_tg, uint64_t out_cap) {
     __shared__ uint64_t lkey[AG_WAVES][AG_LDS];
     __shared__ uint16_t lidx[AG_WAVES][AG_LDS];
@@ -205,9 +206,13 @@ tm_aggre(AggreView av, uint32_t n, const uint32_t* __restrict__ rcount, const ui
         if (lane == 0) acount[t] = c;
         return;
     }
-    const bool in_lds = m <= AG_LDS;
-    const uint64_t* key = gkey + base;   // keys from tm_route_emit (to_rank << 32 | target rank)
-
+    if (m > AG_LDS) {
+        if (lane == 0) large[1 + atomicAdd(&large[0], 1u)] = t;   // a block of tm_aggre_large takes it
+        return;
+    }
+    // 129..AG_LDS routes: the wave's LDS row (a block per topic in
+    // tm_aggre_large measured 0.94 ms for these at C3 vs ~0.3 ms here)
+    const uint64_t* key = gkey + base;
     int j = -1;
     for (uint32_t i = lane; i < m; i += 64)
         if (av.dt[dest[base + i]].y & AG_GROUP_BIT) j = (int)i;
@@ -221,10 +226,7 @@ tm_aggre(AggreView av, uint32_t n, const uint32_t* __restrict__ rcount, const ui
         }
     }
     uint32_t kept = 0;
-    if (j >= 0 && in_lds) {
-        // lists:usort over r_0 .. r_j: bitonic sort of the u keys (padded to a
-        // power of two with ~0, above every real key) in the wave's LDS row,
-        // then keep the first of each run of equal keys
+    if (j >= 0) {
         const uint32_t u = (uint32_t)j + 1;
         uint32_t P = 1;
         while (P < u) P <<= 1;
@@ -239,8 +241,7 @@ tm_aggre(AggreView av, uint32_t n, const uint32_t* __restrict__ rcount, const ui
                 for (uint32_t q = lane; q < P / 2; q += 64) {   // pair q: i has bit d clear
                     const uint32_t i = ((q & ~(d - 1)) << 1) | (q & (d - 1)), pi = i | d;
                     const uint64_t a = lkey[w][i], b = lkey[w][pi];
-                    const bool up = (i & size) == 0;
-                    if ((a > b) == up) {
+                    if ((a > b) == ((i & size) == 0)) {
                         lkey[w][i] = b;
                         lkey[w][pi] = a;
                         const uint16_t x = lidx[w][i];
@@ -266,46 +267,156 @@ tm_aggre(AggreView av, uint32_t n, const uint32_t* __restrict__ rcount, const ui
             }
             kept += (uint32_t)__popcll(bal);
         }
-    } else if (j >= 0) {
-        // more than AG_LDS routes: rank-by-counting over the topic's global
-        // key row (entry i survives iff no earlier entry has its key, and
-        // lands at the number of surviving keys below it)
-        const uint32_t u = (uint32_t)j + 1;
-        uint8_t* flag = gflag + base;
-        __threadfence_block();
-        __builtin_amdgcn_wave_barrier();
-        for (uint32_t i = lane; i < u; i += 64) {
-            const uint64_t kx = key[i];
-            uint8_t f = 1;
-            for (uint32_t k = 0; k < i; ++k)
-                if (key[k] == kx) { f = 0; break; }
-            flag[i] = f;
-            kept += f;
-        }
-        __threadfence_block();
-        __builtin_amdgcn_wave_barrier();
-        for (uint32_t i = lane; i < u; i += 64) {
-            if (!flag[i]) continue;
-            const uint64_t kx = key[i];
-            uint32_t pos = 0;
-            for (uint32_t k = 0; k < u; ++k) pos += (flag[k] && key[k] < kx) ? 1u : 0u;
-            if (base + tail + pos < out_cap) {
-                out_to[base + tail + pos] = src[base + i];
-                out_tg[base + tail + pos] = av.dt[dest[base + i]].y & ~AG_GROUP_BIT;
-            }
-        }
-        kept = wave_sum_u(kept);
     }
     if (lane == 0) acount[t] = tail + kept;
 }
 
+// topics with more than 128 routes: one 256-thread block per topic
+// (persistent over the list tm_aggre built), keys and route indices in LDS,
+// block-wide bitonic sort; beyond AGL routes, rank-by-counting over the
+// topic's global key row
+constexpr uint32_t AGL = 4096;
+
+__device__ __forceinline__ int block_max_i(int x, int* red) {
+    x = wave_max_i(x);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = x;
+    __syncthreads();
+    int r = red[0];
+    for (int i = 1; i < AG_WAVES; ++i) r = max(r, red[i]);
+    __syncthreads();
+    return r;
+}
+// exclusive prefix of a 0/1 flag over the block, and the block total
+__device__ __forceinline__ uint32_t block_prefix_flag(bool f, uint32_t* red, uint32_t& total) {
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint64_t bal = __ballot(f);
+    if (lane == 0) red[w] = (uint32_t)__popcll(bal);
+    __syncthreads();
+    uint32_t pre = 0, tot = 0;
+    for (uint32_t i = 0; i < (uint32_t)AG_WAVES; ++i) {
+        if (i < w) pre += red[i];
+        tot += red[i];
+    }
+    __syncthreads();
+    total = tot;
+    return pre + (uint32_t)__popcll(bal & ((1ull << lane) - 1));
+}
+
+__global__ void __launch_bounds__(AG_BLOCK)
+tm_aggre_large(AggreView av, const uint32_t* __restrict__ rcount, const uint64_t* __restrict__ roff,
+               const uint32_t* __restrict__ src, const uint32_t* __restrict__ dest,
+               const uint64_t* __restrict__ gkey, uint8_t* __restrict__ gflag, const uint32_t* __restrict__ large,
+               uint32_t* __restrict__ acount, uint32_t* __restrict__ out_to, uint32_t* __restrict__ out_tg,
+               uint64_t out_cap) {
+    __shared__ uint64_t lkey[AGL];
+    __shared__ uint16_t lidx[AGL];
+    __shared__ int redi[AG_WAVES];
+    __shared__ uint32_t redu[AG_WAVES];
+    const uint32_t nl = large[0];
+    for (uint32_t q = blockIdx.x; q < nl; q += gridDim.x) {   // block-uniform
+        const uint32_t t = large[1 + q];
+        const uint32_t m = rcount[t];
+        const uint64_t base = roff[t];
+        const uint64_t* key = gkey + base;
+        int j = -1;
+        for (uint32_t i = threadIdx.x; i < m; i += AG_BLOCK)
+            if (av.dt[dest[base + i]].y & AG_GROUP_BIT) j = (int)i;
+        j = block_max_i(j, redi);
+        const uint32_t tail = (uint32_t)((int)m - 1 - j);
+        for (uint32_t k = threadIdx.x; k < tail; k += AG_BLOCK) {   // r_{m-1} .. r_{j+1}
+            const uint32_t i = m - 1 - k;
+            if (base + k < out_cap) {
+                out_to[base + k] = src[base + i];
+                out_tg[base + k] = av.dt[dest[base + i]].y & ~AG_GROUP_BIT;
+            }
+        }
+        uint32_t kept = 0;
+        const uint32_t u = (uint32_t)(j + 1);
+        if (j >= 0 && u <= AGL) {
+            uint32_t P = 1;
+            while (P < u) P <<= 1;
+            for (uint32_t i = threadIdx.x; i < P; i += AG_BLOCK) {
+                lkey[i] = i < u ? key[i] : ~0ull;
+                lidx[i] = (uint16_t)i;
+            }
+            for (uint32_t size = 2; size <= P; size <<= 1) {
+                for (uint32_t d = size >> 1; d > 0; d >>= 1) {
+                    __syncthreads();
+                    for (uint32_t p = threadIdx.x; p < P / 2; p += AG_BLOCK) {   // pair p: i has bit d clear
+                        const uint32_t i = ((p & ~(d - 1)) << 1) | (p & (d - 1)), pi = i | d;
+                        const uint64_t a = lkey[i], b = lkey[pi];
+                        if ((a > b) == ((i & size) == 0)) {
+                            lkey[i] = b;
+                            lkey[pi] = a;
+                            const uint16_t x = lidx[i];
+                            lidx[i] = lidx[pi];
+                            lidx[pi] = x;
+                        }
+                    }
+                }
+            }
+            __syncthreads();
+            for (uint32_t p0 = 0; p0 < u; p0 += AG_BLOCK) {   // block-uniform trip count
+                const uint32_t p = p0 + threadIdx.x;
+                const bool keep = p < u && (p == 0 || lkey[p] != lkey[p - 1]);
+                uint32_t chunk;
+                const uint32_t pos = kept + block_prefix_flag(keep, redu, chunk);
+                if (keep && base + tail + pos < out_cap) {
+                    const uint32_t i = lidx[p];
+                    out_to[base + tail + pos] = src[base + i];
+                    out_tg[base + tail + pos] = av.dt[dest[base + i]].y & ~AG_GROUP_BIT;
+                }
+                kept += chunk;
+            }
+        } else if (j >= 0) {
+            // rank-by-counting: entry i survives iff no earlier entry has its
+            // key, and lands at the number of surviving keys below it
+            uint8_t* flag = gflag + base;
+            uint32_t mine = 0;
+            for (uint32_t i = threadIdx.x; i < u; i += AG_BLOCK) {
+                const uint64_t kx = key[i];
+                uint8_t f = 1;
+                for (uint32_t k = 0; k < i; ++k)
+                    if (key[k] == kx) { f = 0; break; }
+                flag[i] = f;
+                mine += f;
+            }
+            __threadfence_block();
+            __syncthreads();
+            for (uint32_t i = threadIdx.x; i < u; i += AG_BLOCK) {
+                if (!flag[i]) continue;
+                const uint64_t kx = key[i];
+                uint32_t pos = 0;
+                for (uint32_t k = 0; k < u; ++k) pos += (flag[k] && key[k] < kx) ? 1u : 0u;
+                if (base + tail + pos < out_cap) {
+                    out_to[base + tail + pos] = src[base + i];
+                    out_tg[base + tail + pos] = av.dt[dest[base + i]].y & ~AG_GROUP_BIT;
+                }
+            }
+            mine = wave_sum_u(mine);
+            if ((threadIdx.x & 63) == 0) redu[threadIdx.x >> 6] = mine;
+            __syncthreads();
+            for (int i = 0; i < AG_WAVES; ++i) kept += redu[i];
+        }
+        if (threadIdx.x == 0) acount[t] = tail + kept;
+        __syncthreads();   // LDS and redu reused by the next topic
+    }
+}
+
 hipError_t launch_aggre(const AggreView& av, uint32_t n, const uint32_t* rcount, const uint64_t* roff,
                         const uint32_t* src, const uint32_t* dest, const uint64_t* key, uint8_t* gflag,
-                        uint32_t* acount, uint32_t* out_to, uint32_t* out_tg, uint64_t out_cap, hipStream_t st) {
+                        uint32_t* large, uint32_t* acount, uint32_t* out_to, uint32_t* out_tg, uint64_t out_cap,
+                        hipStream_t st) {
     if (n == 0) return hipSuccess;
+    hipError_t err = hipMemsetAsync(large, 0, 4, st);
+    if (err != hipSuccess) return err;
     const dim3 g((n + AG_WAVES - 1) / AG_WAVES), blk(AG_BLOCK);
-    hipLaunchKernelGGL(tm_aggre, g, blk, 0, st, av, n, rcount, roff, src, dest, key, gflag, acount, out_to, out_tg,
+    hipLaunchKernelGGL(tm_aggre, g, blk, 0, st, av, n, rcount, roff, src, dest, key, large, acount, out_to, out_tg,
                        out_cap);
+    // persistent: 4 blocks per CU (40 KB of LDS each) over 256 CUs
+    const dim3 gl(n < 1024u ? n : 1024u);
+    hipLaunchKernelGGL(tm_aggre_large, gl, blk, 0, st, av, rcount, roff, src, dest, key, gflag, large, acount,
+                       out_to, out_tg, out_cap);
     return hipGetLastError();
 }
 

@@ -231,7 +231,7 @@ struct tm_engine {
     std::vector<AggKey> agg_keys;           // route image entries (set by build_route_image)
     bool aggre_dirty = true;
     DevBuf d_ex_rank, d_dt;
-    DevBuf w_dsrc, w_dcount, w_akey, w_aflag;
+    DevBuf w_dsrc, w_dcount, w_akey, w_aflag, w_alarge;
 
     // ---- match workspace ----
     DevBuf w_mpre, w_mscan, w_bytes, w_off, w_counts, w_outoff, w_ids, w_total;
@@ -1319,9 +1319,10 @@ struct tm_engine {
             rcap = std::min(w_dsrc.bytes / 8, w_akey.bytes / 8);
         }
         w_aflag.ensure(rcap + 8, 1.0);
+        w_alarge.ensure((size_t)n * 4 + 16);
         const uint32_t* src = w_dsrc.as<uint32_t>();
         HIPCHK(launch_aggre(aggre_view(), n, w_dcount.as<uint32_t>(), out_off, src, src + rcap, w_akey.as<uint64_t>(),
-                            w_aflag.as<uint8_t>(), counts, to, target, cap, st));
+                            w_aflag.as<uint8_t>(), w_alarge.as<uint32_t>(), counts, to, target, cap, st));
     }
 
     void finish_batch(hipStream_t st, uint32_t n) {
@@ -1448,7 +1449,7 @@ void tm_close(tm_engine* e) {
     if (e->device >= 0) {
         (void)hipSetDevice(e->device);
         if (e->stream) (void)hipStreamSynchronize(e->stream);
-        for (DevBuf* b : {&e->d_ex_rank, &e->d_dt, &e->w_dsrc, &e->w_dcount, &e->w_akey, &e->w_aflag,
+        for (DevBuf* b : {&e->d_ex_rank, &e->d_dt, &e->w_dsrc, &e->w_dcount, &e->w_akey, &e->w_aflag, &e->w_alarge,
              &e->d_fr_meta, &e->d_fr_dest, &e->d_ex_slots, &e->d_ex_arena, &e->d_ex_dest, &e->w_rexact,
                           &e->w_rscan, &e->w_rids, &e->w_rcounts, &e->w_roff})
             b->release();

@@ -57,12 +57,14 @@ hipError_t launch_routes(const RouteView& rv, const uint8_t* bytes, const uint64
 
 // emqx_broker:aggre/1 (aggre.hip) over a match_routes CSR (rcount, roff,
 // src, dest, key from launch_routes with av).  gflag: one u8 per route (used
-// by topics with > 512 routes).  Output at the route offsets: topic t's
+// by topics with > 4096 routes); large: n + 1 u32 (list of topics with > 512
+// routes).  Output at the route offsets: topic t's
 // list is out_to / out_tg[roff[t] .. + acount[t]) (out_to = TM_ROUTE_TOPIC_ID
 // or a filter id, out_tg = target id); entries at or past out_cap are dropped.
 hipError_t launch_aggre(const AggreView& av, uint32_t n, const uint32_t* rcount, const uint64_t* roff,
                         const uint32_t* src, const uint32_t* dest, const uint64_t* key, uint8_t* gflag,
-                        uint32_t* acount, uint32_t* out_to, uint32_t* out_tg, uint64_t out_cap, hipStream_t st);
+                        uint32_t* large, uint32_t* acount, uint32_t* out_to, uint32_t* out_tg, uint64_t out_cap,
+                        hipStream_t st);
 
 // Sharded mode (shard.hip): merge per-topic match lists of S filter shards
 // for m topics.  counts [S][m]; source s's items start at src_base[s] of
