@@ -91,3 +91,27 @@ def test_routetable_match_deliveries():
     assert o.match_routes(b"a/b") == [(b"a/b", "n3"), (b"a/+", "n1"), (b"a/+", ("g", "n2")), (b"a/#", "n2")]
     assert o.match_deliveries(b"a/b") == [(b"a/#", (0, b"n2")), (b"a/+", (0, b"n1")), (b"a/+", (1, b"g")),
                                           (b"a/b", (0, b"n3"))]
+
+
+def _golden():
+    import json
+    import os
+    return json.load(open(os.path.join(os.path.dirname(__file__), "golden", "aggre_vectors.json")))
+
+
+def _dest(d):
+    return (d[1], d[2]) if d[0] == "group" else d[1]
+
+
+def test_oracle_matches_aggre_golden():
+    """the committed fixture (tests/golden/make_aggre_golden.py) replays"""
+    n = 0
+    for case in _golden()["cases"]:
+        o = pytrie.RouteTable()
+        for op, t, d in case["ops"]:
+            (o.add_route if op == "add" else o.del_route)(bytes.fromhex(t), _dest(d))
+        for tp, want in zip(case["topics"], case["deliveries"]):
+            got = [[to.hex(), x[0], x[1].hex()] for to, x in o.match_deliveries(bytes.fromhex(tp))]
+            assert got == want, tp
+            n += len(want)
+    assert n > 100

@@ -155,3 +155,20 @@ def test_aggre_device_api_and_empty(gpu_device):
     assert int(offs[-1]) == 0 and len(t2) == 0
     e2.close()
     e.close()
+
+
+def test_aggre_golden_vectors(gpu_device):
+    """tests/golden/aggre_vectors.json (oracle aggre/1 over random route tables)"""
+    import json
+    g = json.load(open(os.path.join(ROOT, "tests", "golden", "aggre_vectors.json")))
+    for case in g["cases"]:
+        e = Engine(device=gpu_device)
+        r = Router(e, node="n1")
+        for op, t, d in case["ops"]:
+            dest = (d[1], d[2]) if d[0] == "group" else d[1]
+            (r.add_route if op == "add" else r.del_route)(bytes.fromhex(t), dest)
+        topics = [bytes.fromhex(t) for t in case["topics"]]
+        got = r.match_deliveries_many(topics, tagged=True)
+        for tp, row, want in zip(topics, got, case["deliveries"]):
+            assert [[to.hex(), x[0], x[1].hex()] for to, x in row] == want, tp
+        e.close()
