@@ -32,8 +32,9 @@
 // run of equal keys; up to 512 routes the same in the wave's LDS row.
 // Larger topics go on a device-built list that
 // tm_aggre_large works through with one 256-thread block per topic (LDS
-// bitonic up to 4096 routes, rank-by-counting over the global key row
-// beyond), so nothing waits on the host.
+// bitonic up to 4096 routes; beyond, the topic's key row is sorted in place:
+// 4096-key chunks in LDS, then bitonic merge stages over the row in global
+// memory, O(u log^2 u)), so nothing waits on the host.
 // Output goes straight to the topic's route offset (aggre never grows a
 // list): offsets are the route CSR's, counts are aggre's, so the lists need
 // no compaction pass (measured 0.75 ms per 2M topics at C3).
@@ -271,11 +272,73 @@ tm_aggre(AggreView av, uint32_t n, const uint32_t* __restrict__ rcount, const ui
     if (lane == 0) acount[t] = tail + kept;
 }
 
-// topics with more than 128 routes: one 256-thread block per topic
+// topics with more than 512 routes: one 256-thread block per topic
 // (persistent over the list tm_aggre built), keys and route indices in LDS,
-// block-wide bitonic sort; beyond AGL routes, rank-by-counting over the
-// topic's global key row
+// block-wide bitonic sort; beyond AGL routes the topic's global key row is
+// sorted in place and each surviving key names its pair through the inverse
+// rank tables (AggreView::rank_src / rank_tg)
 constexpr uint32_t AGL = 4096;
+
+// ascending in-place sort of key[0..u) by one block (u > AGL).  Bitonic
+// network in the "mirror" form (the first step of each merge compares i with
+// its mirror image, later steps with i + d), whose comparators all point up:
+// positions >= u act as +inf and never move, so no padding is needed.
+// Steps of distance < AGL run on one LDS chunk at a time.
+__device__ void sort_row_inplace(uint64_t* __restrict__ key, uint32_t u, uint64_t* lkey) {
+    uint32_t P = AGL;
+    while (P < u) P <<= 1;
+    // compare-exchange (i < j), ascending
+    auto cmpx = [](uint64_t* a, uint32_t i, uint32_t j) {
+        const uint64_t x = a[i], y = a[j];
+        if (x > y) {
+            a[i] = y;
+            a[j] = x;
+        }
+    };
+    // pair p of a step: i has bit h clear (h = half the block for a mirror
+    // step, the distance for a half-cleaner)
+    auto lower = [](uint32_t p, uint32_t h) { return ((p & ~(h - 1)) << 1) | (p & (h - 1)); };
+    auto mirror = [](uint32_t i, uint32_t s) { return (i & ~(s - 1)) + (s - 1) - (i & (s - 1)); };
+    // one LDS chunk [c0, c0 + AGL): a full sort (full = true), or the
+    // half-cleaners of distance < AGL that finish a global merge stage
+    auto chunk_pass = [&](uint32_t c0, bool full) {
+        for (uint32_t i = threadIdx.x; i < AGL; i += AG_BLOCK) lkey[i] = c0 + i < u ? key[c0 + i] : ~0ull;
+        for (uint32_t s = full ? 2 : AGL; s <= AGL; s <<= 1) {
+            if (full) {
+                __syncthreads();
+                for (uint32_t p = threadIdx.x; p < AGL / 2; p += AG_BLOCK) {
+                    const uint32_t i = lower(p, s >> 1);
+                    cmpx(lkey, i, mirror(i, s));
+                }
+            }
+            for (uint32_t d = s >> (full ? 2 : 1); d > 0; d >>= 1) {
+                __syncthreads();
+                for (uint32_t p = threadIdx.x; p < AGL / 2; p += AG_BLOCK) {
+                    const uint32_t i = lower(p, d);
+                    cmpx(lkey, i, i | d);
+                }
+            }
+        }
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < AGL; i += AG_BLOCK)
+            if (c0 + i < u) key[c0 + i] = lkey[i];
+        __threadfence_block();
+        __syncthreads();
+    };
+    for (uint32_t c0 = 0; c0 < u; c0 += AGL) chunk_pass(c0, true);   // sorted runs of AGL
+    for (uint32_t size = 2 * AGL; size <= P; size <<= 1) {
+        for (uint32_t d = size >> 1; d >= AGL; d >>= 1) {
+            for (uint32_t p = threadIdx.x; p < P / 2; p += AG_BLOCK) {
+                const uint32_t i = lower(p, d);
+                const uint32_t j = d == (size >> 1) ? mirror(i, size) : (i | d);
+                if (j < u) cmpx(key, i, j);   // positions >= u are +inf: never move
+            }
+            __threadfence_block();
+            __syncthreads();
+        }
+        for (uint32_t c0 = 0; c0 < u; c0 += AGL) chunk_pass(c0, false);
+    }
+}
 
 __device__ __forceinline__ int block_max_i(int x, int* red) {
     x = wave_max_i(x);
@@ -305,7 +368,7 @@ __device__ __forceinline__ uint32_t block_prefix_flag(bool f, uint32_t* red, uin
 __global__ void __launch_bounds__(AG_BLOCK)
 tm_aggre_large(AggreView av, const uint32_t* __restrict__ rcount, const uint64_t* __restrict__ roff,
                const uint32_t* __restrict__ src, const uint32_t* __restrict__ dest,
-               const uint64_t* __restrict__ gkey, uint8_t* __restrict__ gflag, const uint32_t* __restrict__ large,
+               uint64_t* __restrict__ gkey, const uint32_t* __restrict__ large,
                uint32_t* __restrict__ acount, uint32_t* __restrict__ out_to, uint32_t* __restrict__ out_tg,
                uint64_t out_cap) {
     __shared__ uint64_t lkey[AGL];
@@ -369,34 +432,22 @@ tm_aggre_large(AggreView av, const uint32_t* __restrict__ rcount, const uint64_t
                 kept += chunk;
             }
         } else if (j >= 0) {
-            // rank-by-counting: entry i survives iff no earlier entry has its
-            // key, and lands at the number of surviving keys below it
-            uint8_t* flag = gflag + base;
-            uint32_t mine = 0;
-            for (uint32_t i = threadIdx.x; i < u; i += AG_BLOCK) {
-                const uint64_t kx = key[i];
-                uint8_t f = 1;
-                for (uint32_t k = 0; k < i; ++k)
-                    if (key[k] == kx) { f = 0; break; }
-                flag[i] = f;
-                mine += f;
-            }
-            __threadfence_block();
-            __syncthreads();
-            for (uint32_t i = threadIdx.x; i < u; i += AG_BLOCK) {
-                if (!flag[i]) continue;
-                const uint64_t kx = key[i];
-                uint32_t pos = 0;
-                for (uint32_t k = 0; k < u; ++k) pos += (flag[k] && key[k] < kx) ? 1u : 0u;
-                if (base + tail + pos < out_cap) {
-                    out_to[base + tail + pos] = src[base + i];
-                    out_tg[base + tail + pos] = av.dt[dest[base + i]].y & ~AG_GROUP_BIT;
+            // the key row of r_0 .. r_j sorted in place; a kept key is the
+            // first of its run and names its {To, X} by its two ranks
+            uint64_t* krow = gkey + base;
+            sort_row_inplace(krow, u, lkey);
+            for (uint32_t p0 = 0; p0 < u; p0 += AG_BLOCK) {   // block-uniform trip count
+                const uint32_t p = p0 + threadIdx.x;
+                const uint64_t kx = p < u ? krow[p] : 0ull;
+                const bool keep = p < u && (p == 0 || krow[p - 1] != kx);
+                uint32_t chunk;
+                const uint32_t pos = kept + block_prefix_flag(keep, redu, chunk);
+                if (keep && base + tail + pos < out_cap) {
+                    out_to[base + tail + pos] = av.rank_src[(uint32_t)(kx >> 32)];
+                    out_tg[base + tail + pos] = av.rank_tg[(uint32_t)kx];
                 }
+                kept += chunk;
             }
-            mine = wave_sum_u(mine);
-            if ((threadIdx.x & 63) == 0) redu[threadIdx.x >> 6] = mine;
-            __syncthreads();
-            for (int i = 0; i < AG_WAVES; ++i) kept += redu[i];
         }
         if (threadIdx.x == 0) acount[t] = tail + kept;
         __syncthreads();   // LDS and redu reused by the next topic
@@ -404,9 +455,8 @@ tm_aggre_large(AggreView av, const uint32_t* __restrict__ rcount, const uint64_t
 }
 
 hipError_t launch_aggre(const AggreView& av, uint32_t n, const uint32_t* rcount, const uint64_t* roff,
-                        const uint32_t* src, const uint32_t* dest, const uint64_t* key, uint8_t* gflag,
-                        uint32_t* large, uint32_t* acount, uint32_t* out_to, uint32_t* out_tg, uint64_t out_cap,
-                        hipStream_t st) {
+                        const uint32_t* src, const uint32_t* dest, uint64_t* key, uint32_t* large,
+                        uint32_t* acount, uint32_t* out_to, uint32_t* out_tg, uint64_t out_cap, hipStream_t st) {
     if (n == 0) return hipSuccess;
     hipError_t err = hipMemsetAsync(large, 0, 4, st);
     if (err != hipSuccess) return err;
@@ -415,7 +465,7 @@ hipError_t launch_aggre(const AggreView& av, uint32_t n, const uint32_t* rcount,
                        out_cap);
     // persistent: 4 blocks per CU (40 KB of LDS each) over 256 CUs
     const dim3 gl(n < 1024u ? n : 1024u);
-    hipLaunchKernelGGL(tm_aggre_large, gl, blk, 0, st, av, rcount, roff, src, dest, key, gflag, large, acount,
+    hipLaunchKernelGGL(tm_aggre_large, gl, blk, 0, st, av, rcount, roff, src, dest, key, large, acount,
                        out_to, out_tg, out_cap);
     return hipGetLastError();
 }

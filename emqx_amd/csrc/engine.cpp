@@ -218,6 +218,20 @@ struct tm_engine {
     uint32_t fr_filters = 0;          // filter ids covered by fr_meta
     bool route_image = false;
     DevBuf w_rexact, w_rscan, w_rids, w_rcounts, w_roff;
+    // the route / aggre workspaces (w_r*, w_d*, w_a*) and images are shared by
+    // every stream: rw_done is recorded after the last route or aggre kernel
+    // of a batch; the host waits on it before the next batch reuses (or
+    // reallocates) the workspaces and before it rewrites an image
+    hipEvent_t rw_done = nullptr;
+    bool rw_used = false;
+    void rw_release(hipStream_t st) {
+        if (!rw_done) HIPCHK(hipEventCreateWithFlags(&rw_done, hipEventDisableTiming));
+        HIPCHK(hipEventRecord(rw_done, st));
+        rw_used = true;
+    }
+    void rw_drain() {   // host: every route / aggre kernel issued so far has finished
+        if (rw_used) HIPCHK(hipEventSynchronize(rw_done));
+    }
 
     // ---- emqx_broker:aggre/1 targets (aggre.hip) ----
     // a dest aggregates to a target: a node (atom) or a $share group; targets
@@ -231,7 +245,8 @@ struct tm_engine {
     std::vector<AggKey> agg_keys;           // route image entries (set by build_route_image)
     bool aggre_dirty = true;
     DevBuf d_ex_rank, d_dt;
-    DevBuf w_dsrc, w_dcount, w_akey, w_aflag, w_alarge;
+    DevBuf d_rank_src, d_rank_tg;           // inverse ranks: to_rank -> route source, target rank -> target id
+    DevBuf w_dsrc, w_dcount, w_akey, w_alarge;
 
     // ---- match workspace ----
     DevBuf w_mpre, w_mscan, w_bytes, w_off, w_counts, w_outoff, w_ids, w_total;
@@ -243,7 +258,7 @@ struct tm_engine {
         DevBuf twords, words, path, meta, scan, stage, kstage, ws, stats, perm;
         uint64_t* h_maxc = nullptr;     // pinned: largest match count of the slot's last walk
         hipEvent_t maxc_ev = nullptr, done = nullptr;
-        bool maxc_pending = false, used = false;
+        bool maxc_pending = false, used = false, keyed = false;
     };
     static constexpr int MAX_SLOTS = 4;
     Slot slots[MAX_SLOTS];
@@ -691,6 +706,7 @@ struct tm_engine {
     // rebuild the route image: per-filter-id dest lists (CSR) and the
     // exact-topic table over every topic with routes
     void build_route_image() {
+        rw_drain();   // no route / aggre kernel may read the image being replaced
         const uint32_t nf = (uint32_t)filters.size();
         std::vector<uint32_t> fr_off(nf + 1, 0);
         std::vector<std::pair<uint32_t, const std::vector<uint32_t>*>> by_fid;
@@ -771,6 +787,7 @@ struct tm_engine {
         return id;
     }
     void build_aggre_image() {
+        rw_drain();
         const uint32_t nf = fr_filters;
         std::vector<uint32_t> order(agg_keys.size());
         for (uint32_t i = 0; i < order.size(); ++i) order[i] = i;
@@ -779,10 +796,14 @@ struct tm_engine {
         std::vector<uint2> fr_meta(h_fr_off.size());
         for (size_t f = 0; f < h_fr_off.size(); ++f) fr_meta[f] = make_uint2(h_fr_off[f], 0u);
         std::vector<uint32_t> ex_rank(std::max<size_t>(route_total, 1), 0);
+        std::vector<uint32_t> rank_src(std::max<size_t>(order.size(), 1), TM_ROUTE_TOPIC_ID);
         for (uint32_t r = 0; r < order.size(); ++r) {
             const AggKey& a = agg_keys[order[r]];
             if (a.fid != FILTER_NONE && a.fid < nf) fr_meta[a.fid].y = r;
             if (a.dest_off < ex_rank.size()) ex_rank[a.dest_off] = r;
+            // the To of rank r as a route source: its filter id when it is a
+            // trie filter, else the literal topic (same To binary either way)
+            rank_src[r] = a.fid != FILTER_NONE ? a.fid : TM_ROUTE_TOPIC_ID;
         }
         const size_t nd = dest_names.size();
         dest_target.resize(nd, TARGET_DEFAULT);
@@ -796,6 +817,8 @@ struct tm_engine {
         for (uint32_t i = 0; i < tord.size(); ++i) tord[i] = i;
         std::sort(tord.begin(), tord.end(), [&](uint32_t a, uint32_t b) { return target_names[a] < target_names[b]; });
         for (uint32_t r = 0; r < tord.size(); ++r) trank[tord[r]] = r;
+        std::vector<uint32_t> rank_tg(std::max<size_t>(tord.size(), 1), 0);
+        for (uint32_t r = 0; r < tord.size(); ++r) rank_tg[r] = tord[r];
         std::vector<uint2> dt(std::max<size_t>(nd, 1));
         for (size_t d = 0; d < nd; ++d) {
             const uint32_t tid = dest_target[d];
@@ -808,6 +831,8 @@ struct tm_engine {
         if (!fr_meta.empty()) up(d_fr_meta, fr_meta.data(), fr_meta.size() * sizeof(uint2));
         up(d_ex_rank, ex_rank.data(), ex_rank.size() * 4);
         up(d_dt, dt.data(), dt.size() * sizeof(uint2));
+        up(d_rank_src, rank_src.data(), rank_src.size() * 4);
+        up(d_rank_tg, rank_tg.data(), rank_tg.size() * 4);
         HIPCHK(hipStreamSynchronize(stream));   // host vectors die here
         aggre_dirty = false;
     }
@@ -815,6 +840,8 @@ struct tm_engine {
         AggreView av;
         av.ex_rank = d_ex_rank.as<const uint32_t>();
         av.dt = d_dt.as<const uint2>();
+        av.rank_src = d_rank_src.as<const uint32_t>();
+        av.rank_tg = d_rank_tg.as<const uint32_t>();
         return av;
     }
 
@@ -1119,6 +1146,7 @@ struct tm_engine {
         }
         Guard g(device);
         wait_matches();  // never patch the image under a running walk
+        rw_drain();
         upload_table(d_nodes, nodes, node_dirty, 0);
         upload_table(d_edges, cold.slots, cold.dirty, 0);
         upload_table(d_hedges, hot.slots, hot.dirty, 0);
@@ -1170,7 +1198,7 @@ struct tm_engine {
         return k;
     }
     void ensure_workspace(uint32_t n, uint64_t nbytes) { w_total.ensure(64); }
-    void ensure_slot(Slot& w, uint32_t n, uint64_t nbytes, bool keys) {
+    void ensure_slot(Slot& w, uint32_t n, uint64_t nbytes, uint32_t key_words) {
         w.twords.ensure((size_t)(n + 1) * WREG * 4);
         w.words.ensure((nbytes + n + 1) * 4);
         w.path.ensure((nbytes + 2ull * n + 2) * 4);
@@ -1178,7 +1206,7 @@ struct tm_engine {
         w.meta.ensure((size_t)(n + 1) * 4);
         w.scan.ensure(scan_tmp_elems(n) * 8 + 8);
         w.stage.ensure(((size_t)n * stage_k + 4) * 4);
-        if (keys) w.kstage.ensure(((size_t)n * stage_k + 4) * 8);
+        if (key_words) w.kstage.ensure(((size_t)n * stage_k * key_words + 4) * 8);
         w.ws.ensure(QWS_BYTES);
         if (group) w.perm.ensure(((size_t)n + GROUP_WS_ELEMS) * 4);
         if (!w.done) HIPCHK(hipEventCreateWithFlags(&w.done, hipEventDisableTiming));
@@ -1188,7 +1216,7 @@ struct tm_engine {
     // filter ids (ids past cap are dropped; *total always exact)
     // stage rows sized to the largest list of the previous walk (read back
     // asynchronously), within STAGE_BUDGET: fan-out beyond K costs a re-walk
-    void adapt_stage_k(uint32_t n, bool keys) {
+    void adapt_stage_k(uint32_t n, uint32_t key_words) {
         if (!stage_auto) return;
         uint64_t mc = 0;
         for (Slot& w : slots) {
@@ -1200,7 +1228,7 @@ struct tm_engine {
         uint64_t want = stage_k_min;
         while (want < mc && want < 4096) want <<= 1;
         uint64_t k = stage_k;
-        const uint64_t per = (uint64_t)n * (keys ? 12 : 4);
+        const uint64_t per = (uint64_t)n * (4 + 8 * key_words);
         while (k < want && per * (k << 1) <= STAGE_BUDGET) k <<= 1;
         stage_k = (uint32_t)k;
     }
@@ -1215,14 +1243,15 @@ struct tm_engine {
 
     void run_batch(const uint8_t* bytes, const uint64_t* off, uint32_t n, uint64_t nbytes, uint32_t* counts,
                    uint64_t* out_off, uint32_t* ids, uint64_t cap, uint64_t* total, hipStream_t st,
-                   uint64_t* keys = nullptr) {
-        adapt_stage_k(n, keys != nullptr);
+                   uint64_t* keys = nullptr, uint32_t key_words = 1) {
+        const uint32_t kw = keys ? key_words : 0u;
+        adapt_stage_k(n, kw);
         ensure_workspace(n, nbytes);
         const int si = next_slot;
         next_slot = (next_slot + 1) % nslots;
         Slot& w = slots[si];
         if (w.used) HIPCHK(hipStreamWaitEvent(st, w.done, 0));   // its previous batch, maybe on another stream
-        ensure_slot(w, n, nbytes, keys != nullptr);
+        ensure_slot(w, n, nbytes, kw);
         last_slot = si;
         ImageView im = view();
         unsigned long long* sp = w.stats.as<unsigned long long>();
@@ -1246,7 +1275,9 @@ struct tm_engine {
         qb.ws = w.ws.as<unsigned long long>();
         qb.perm = group ? w.perm.as<uint32_t>() : nullptr;
         HIPCHK(launch_queue(stats_enabled, xcdq != 0, im, bytes, off, n, qb, stage_k, counts, out_off, ids, keys, cap,
-                            total, sp, st, timing_enabled ? marks : nullptr, walk_bpc, hist_enabled != 0));
+                            total, sp, st, timing_enabled ? marks : nullptr, walk_bpc, hist_enabled != 0,
+                            keys ? key_words : 1u));
+        w.keyed = keys != nullptr;
         record_maxc(w, st);
         HIPCHK(hipEventRecord(w.done, st));
         w.used = true;
@@ -1271,6 +1302,10 @@ struct tm_engine {
                     uint64_t* out_off, uint32_t* src, uint32_t* dest, uint64_t cap, uint64_t* total,
                     hipStream_t st, uint64_t* out_key = nullptr) {
         ensure_route_image();
+        // this path reads the match total back anyway (host sync per batch):
+        // wait for the previous route / aggre batch of any stream, so its
+        // workspaces can be reused or reallocated
+        rw_drain();
         w_rcounts.ensure((size_t)n * 4 + 4);
         w_roff.ensure((size_t)(n + 1) * 8);
         uint64_t want = std::max<uint64_t>(w_rids.bytes / 4, (uint64_t)n * 16 + 1024);
@@ -1291,6 +1326,7 @@ struct tm_engine {
         HIPCHK(launch_routes(route_view(), bytes, off, n, w_rcounts.as<uint32_t>(), w_roff.as<uint64_t>(),
                              w_rids.as<uint32_t>(), w_rexact.as<uint2>(), counts, out_off, src, dest, cap, total,
                              w_rscan.as<uint64_t>(), st, out_key ? &av_tmp : nullptr, out_key));
+        rw_release(st);
     }
 
     // aggre(match_routes(T)) over a device batch: the route lists and their
@@ -1302,6 +1338,7 @@ struct tm_engine {
                         hipStream_t st) {
         ensure_route_image();
         if (aggre_dirty) build_aggre_image();
+        rw_drain();   // w_d* / w_a* may be reallocated below
         w_dcount.ensure((size_t)n * 4 + 4);
         uint64_t want = std::max<uint64_t>(w_dsrc.bytes / 8, (uint64_t)n * 16 + 1024);
         w_dsrc.ensure(want * 8, 1.0);
@@ -1318,11 +1355,11 @@ struct tm_engine {
             w_akey.ensure(rtotal * 8, 1.25);
             rcap = std::min(w_dsrc.bytes / 8, w_akey.bytes / 8);
         }
-        w_aflag.ensure(rcap + 8, 1.0);
         w_alarge.ensure((size_t)n * 4 + 16);
         const uint32_t* src = w_dsrc.as<uint32_t>();
         HIPCHK(launch_aggre(aggre_view(), n, w_dcount.as<uint32_t>(), out_off, src, src + rcap, w_akey.as<uint64_t>(),
-                            w_aflag.as<uint8_t>(), w_alarge.as<uint32_t>(), counts, to, target, cap, st));
+                            w_alarge.as<uint32_t>(), counts, to, target, cap, st));
+        rw_release(st);
     }
 
     void finish_batch(hipStream_t st, uint32_t n) {
@@ -1449,7 +1486,9 @@ void tm_close(tm_engine* e) {
     if (e->device >= 0) {
         (void)hipSetDevice(e->device);
         if (e->stream) (void)hipStreamSynchronize(e->stream);
-        for (DevBuf* b : {&e->d_ex_rank, &e->d_dt, &e->w_dsrc, &e->w_dcount, &e->w_akey, &e->w_aflag, &e->w_alarge,
+        if (e->rw_done) (void)hipEventDestroy(e->rw_done);
+        for (DevBuf* b : {&e->d_ex_rank, &e->d_dt, &e->d_rank_src, &e->d_rank_tg, &e->w_dsrc, &e->w_dcount, &e->w_akey,
+                          &e->w_alarge,
              &e->d_fr_meta, &e->d_fr_dest, &e->d_ex_slots, &e->d_ex_arena, &e->d_ex_dest, &e->w_rexact,
                           &e->w_rscan, &e->w_rids, &e->w_rcounts, &e->w_roff})
             b->release();
@@ -1683,7 +1722,9 @@ int tm_match_batch(tm_engine* e, const uint8_t* topic_bytes, const uint64_t* top
             e->w_ids.ensure(total * 4, 1.25);
             icap = e->w_ids.bytes / 4;
         }
-        uint64_t cap = std::min(total, out_cap);
+        // the workspace holds min(total, icap) ids; with total > out_cap the
+        // call reports TM_ENOSPC and copies what fits both
+        uint64_t cap = std::min(std::min(total, out_cap), icap);
         e->finish_batch(st, n);
         HIPCHK(hipMemcpyAsync(out_count, e->w_counts.p, (size_t)n * 4, hipMemcpyDeviceToHost, st));
         HIPCHK(hipMemcpyAsync(out_off, e->w_outoff.p, (size_t)(n + 1) * 8, hipMemcpyDeviceToHost, st));
@@ -1697,7 +1738,7 @@ int tm_match_batch(tm_engine* e, const uint8_t* topic_bytes, const uint64_t* top
 
 static int match_device(tm_engine* e, const uint8_t* d_bytes, const uint64_t* d_off, uint32_t n,
                         uint64_t topic_bytes, uint32_t* d_count, uint64_t* d_out_off, uint32_t* d_ids,
-                        uint64_t* d_keys, uint64_t out_cap, uint64_t* d_total, void* hip_stream);
+                        uint64_t* d_keys, uint32_t key_words, uint64_t out_cap, uint64_t* d_total, void* hip_stream);
 
 // ---- routes (emqx_router) ---------------------------------------------------
 int tm_route_add(tm_engine* e, const uint8_t* topic, uint32_t tlen, const uint8_t* dest, uint32_t dlen) {
@@ -1826,7 +1867,7 @@ int tm_match_routes_batch(tm_engine* e, const uint8_t* topic_bytes, const uint64
             e->w_ids.ensure(total * 8, 1.25);
             rcap = e->w_ids.bytes / 8;
         }
-        const uint64_t cap = std::min(total, out_cap);
+        const uint64_t cap = std::min(std::min(total, out_cap), rcap);   // see tm_match_batch
         e->finish_batch(st, n);
         HIPCHK(hipMemcpyAsync(out_count, e->w_counts.p, (size_t)n * 4, hipMemcpyDeviceToHost, st));
         HIPCHK(hipMemcpyAsync(out_off, e->w_outoff.p, (size_t)(n + 1) * 8, hipMemcpyDeviceToHost, st));
@@ -1935,7 +1976,7 @@ int tm_match_deliveries_batch(tm_engine* e, const uint8_t* topic_bytes, const ui
             e->w_ids.ensure(total * 8, 1.25);
             rcap = e->w_ids.bytes / 8;
         }
-        const uint64_t cap = std::min(total, out_cap);
+        const uint64_t cap = std::min(std::min(total, out_cap), rcap);   // see tm_match_batch
         e->finish_batch(st, n);
         HIPCHK(hipMemcpyAsync(out_count, e->w_counts.p, (size_t)n * 4, hipMemcpyDeviceToHost, st));
         HIPCHK(hipMemcpyAsync(out_off, e->w_outoff.p, (size_t)(n + 1) * 8, hipMemcpyDeviceToHost, st));
@@ -1952,7 +1993,7 @@ int tm_match_deliveries_batch(tm_engine* e, const uint8_t* topic_bytes, const ui
 int tm_match_batch_device(tm_engine* e, const uint8_t* d_bytes, const uint64_t* d_off, uint32_t n,
                           uint64_t topic_bytes, uint32_t* d_count, uint64_t* d_out_off, uint32_t* d_ids,
                           uint64_t out_cap, uint64_t* d_total, void* hip_stream) {
-    return match_device(e, d_bytes, d_off, n, topic_bytes, d_count, d_out_off, d_ids, nullptr, out_cap, d_total,
+    return match_device(e, d_bytes, d_off, n, topic_bytes, d_count, d_out_off, d_ids, nullptr, 1, out_cap, d_total,
                         hip_stream);
 }
 
@@ -1960,14 +2001,49 @@ int tm_match_batch_device_keys(tm_engine* e, const uint8_t* d_bytes, const uint6
                                uint64_t topic_bytes, uint32_t* d_count, uint64_t* d_out_off, uint32_t* d_ids,
                                uint64_t* d_keys, uint64_t out_cap, uint64_t* d_total, void* hip_stream) {
     if (out_cap && !d_keys) return TM_EINVAL;
-    return match_device(e, d_bytes, d_off, n, topic_bytes, d_count, d_out_off, d_ids, d_keys, out_cap, d_total,
+    return match_device(e, d_bytes, d_off, n, topic_bytes, d_count, d_out_off, d_ids, d_keys, 1, out_cap, d_total,
                         hip_stream);
+}
+
+int tm_match_batch_device_keys_w(tm_engine* e, const uint8_t* d_bytes, const uint64_t* d_off, uint32_t n,
+                                 uint64_t topic_bytes, uint32_t* d_count, uint64_t* d_out_off, uint32_t* d_ids,
+                                 uint64_t* d_keys, uint32_t key_words, uint64_t out_cap, uint64_t* d_total,
+                                 void* hip_stream) {
+    if ((out_cap && !d_keys) || key_words == 0 || key_words > TM_MAX_KEY_WORDS) return TM_EINVAL;
+    return match_device(e, d_bytes, d_off, n, topic_bytes, d_count, d_out_off, d_ids, d_keys, key_words, out_cap,
+                        d_total, hip_stream);
+}
+
+int tm_key_levels(tm_engine* e, uint32_t* max_levels) {
+    if (!max_levels) return TM_EINVAL;
+    return guarded(e, [&]() -> int {
+        *max_levels = 0;
+        if (e->device < 0) return TM_OK;
+        tm_engine::Guard g(e->device);
+        for (auto& w : e->slots) {
+            if (!w.used || !w.keyed) continue;
+            HIPCHK(hipEventSynchronize(w.done));
+            uint64_t x = 0;
+            HIPCHK(hipMemcpy(&x, w.ws.as<uint64_t>() + QWS_MAXL, 8, hipMemcpyDeviceToHost));
+            *max_levels = std::max<uint32_t>(*max_levels, (uint32_t)x);
+        }
+        return TM_OK;
+    });
 }
 
 int tm_shard_merge(tm_engine* e, uint32_t n_shards, uint32_t m, const uint32_t* d_counts,
                    const uint64_t* d_src_base, const uint32_t* d_ids, const uint64_t* d_keys, uint32_t* d_out_count,
                    uint64_t* d_out_off, uint32_t* d_out_gid, uint64_t out_cap, uint64_t* d_total, void* hip_stream) {
+    return tm_shard_merge_w(e, n_shards, m, d_counts, d_src_base, d_ids, d_keys, 1, 0, d_out_count, d_out_off,
+                            d_out_gid, out_cap, d_total, hip_stream);
+}
+
+int tm_shard_merge_w(tm_engine* e, uint32_t n_shards, uint32_t m, const uint32_t* d_counts,
+                     const uint64_t* d_src_base, const uint32_t* d_ids, const uint64_t* d_keys, uint32_t key_words,
+                     uint64_t key_stride, uint32_t* d_out_count, uint64_t* d_out_off, uint32_t* d_out_gid,
+                     uint64_t out_cap, uint64_t* d_total, void* hip_stream) {
     if (n_shards == 0 || n_shards > MAX_SHARDS || !d_out_off || !d_total) return TM_EINVAL;
+    if (key_words == 0 || key_words > TM_MAX_KEY_WORDS) return TM_EINVAL;
     if (m && (!d_counts || !d_src_base || !d_out_count)) return TM_EINVAL;
     if (out_cap && (!d_ids || !d_keys || !d_out_gid)) return TM_EINVAL;
     return guarded(e, [&]() -> int {
@@ -1981,14 +2057,15 @@ int tm_shard_merge(tm_engine* e, uint32_t n_shards, uint32_t m, const uint32_t* 
         if ((uint64_t)n_shards * m > 0xFFFFFFFFull) throw ArgError("n_shards x m exceeds 2^32");
         e->w_mscan.ensure(scan_tmp_elems(std::max<uint32_t>(n_shards * m, m)) * 8 + 8);
         HIPCHK(launch_shard_merge(n_shards, m, d_counts, d_src_base, d_ids, d_keys, d_out_count, d_out_off, d_out_gid,
-                                  out_cap, d_total, e->w_mpre.as<uint64_t>(), e->w_mscan.as<uint64_t>(), st));
+                                  out_cap, d_total, e->w_mpre.as<uint64_t>(), e->w_mscan.as<uint64_t>(), st,
+                                  key_words, key_stride));
         return TM_OK;
     });
 }
 
 static int match_device(tm_engine* e, const uint8_t* d_bytes, const uint64_t* d_off, uint32_t n,
                         uint64_t topic_bytes, uint32_t* d_count, uint64_t* d_out_off, uint32_t* d_ids,
-                        uint64_t* d_keys, uint64_t out_cap, uint64_t* d_total, void* hip_stream) {
+                        uint64_t* d_keys, uint32_t key_words, uint64_t out_cap, uint64_t* d_total, void* hip_stream) {
     if (!d_off || !d_out_off || !d_total || (n && !d_count) || (out_cap && !d_ids)) return TM_EINVAL;
     return guarded(e, [&]() -> int {
         if (e->device < 0) {
@@ -2003,7 +2080,8 @@ static int match_device(tm_engine* e, const uint8_t* d_bytes, const uint64_t* d_
             HIPCHK(hipMemsetAsync(d_total, 0, 8, st));
             return TM_OK;
         }
-        e->run_batch(d_bytes, d_off, n, topic_bytes, d_count, d_out_off, d_ids, out_cap, d_total, st, d_keys);
+        e->run_batch(d_bytes, d_off, n, topic_bytes, d_count, d_out_off, d_ids, out_cap, d_total, st, d_keys,
+                     key_words);
         e->finish_batch(st, n);
         if (e->stats_enabled) {
             HIPCHK(hipStreamSynchronize(st));

@@ -143,6 +143,8 @@ struct RouteView {
 struct AggreView {
     const uint32_t* ex_rank;        // exact-table dest_off -> to_rank of that topic
     const uint2*    dt;             // dest id -> {target rank, target id | group << 31}
+    const uint32_t* rank_src;       // to_rank -> route source of that To (filter id or TM_ROUTE_TOPIC_ID)
+    const uint32_t* rank_tg;        // target rank -> target id
 };
 
 // ---- hashing (identical on host and device) ---------------------------------

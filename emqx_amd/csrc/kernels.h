@@ -11,6 +11,7 @@ constexpr uint32_t WREG = 16;        // topic levels kept in VGPRs / LDS path sl
                                      // topics keep their path in global scratch
 constexpr size_t QWS_BYTES = 1024;   // queue heads: 8 ranges x 128 B
 constexpr size_t QWS_MAXC = 120;     // u64 slot of ws: the batch's largest match count
+constexpr size_t QWS_MAXL = 121;     // u64 slot of ws: most levels of a topic in a keyed batch
 constexpr size_t STATS_BYTES = 512;  // 8 totals + per-level diagnostic histogram
 
 // per-batch device workspace of the queue pipeline
@@ -20,7 +21,7 @@ struct QueueBufs {
     uint32_t* meta;       // n: levels | long << 30 | dollar << 31
     uint32_t* path;       // global path of long topics, at (byte offset + 2 x topic index)
     uint32_t* stage;      // n x K: first K ids of each topic (written from the row's end)
-    uint64_t* kstage;     // n x K order keys (sharded mode), or null
+    uint64_t* kstage;     // key_words planes of n x K order key words (sharded mode), or null
     uint64_t* scan_tmp;   // scan_tmp_elems(n)
     unsigned long long* ws;   // QWS_BYTES of queue heads
     uint32_t* perm;       // group order (option "group"): n positions + 2 x 1024 group counts / cursors, or null
@@ -32,11 +33,13 @@ constexpr uint32_t GROUP_WS_ELEMS = 2048;   // u32 after the n positions of perm
 // offsets only.  stats (6 x u64, zeroed by the caller) is filled when
 // stats_mode: levels, visits, edge reads, matches, leaf visits, probe loads.
 // qb.kstage != null: sharded mode, the order key of every id goes to out_keys
+// (key_words u64 planes: word j of id p at out_keys[j * out_cap + p]; topics
+// of up to 32 * key_words - 1 levels)
 hipError_t launch_queue(bool stats_mode, bool xcdq, const ImageView& im, const uint8_t* bytes, const uint64_t* off,
                         uint32_t n, const QueueBufs& qb, uint32_t K, uint32_t* counts, uint64_t* out_off,
                         uint32_t* out, uint64_t* out_keys, uint64_t out_cap, uint64_t* total,
                         unsigned long long* stats, hipStream_t st, hipEvent_t* marks, uint32_t walk_blocks_per_cu = 0,
-                        bool hist = false);
+                        bool hist = false, uint32_t key_words = 1);
 size_t scan_tmp_elems(uint32_t n);
 // split image (option "split"): n 32 B node records -> inner[n], leaf[n] 16 B halves
 hipError_t launch_split_nodes(const void* nodes, uint64_t n, void* inner, void* leaf, hipStream_t st);
@@ -56,14 +59,13 @@ hipError_t launch_routes(const RouteView& rv, const uint8_t* bytes, const uint64
                          const AggreView* av = nullptr, uint64_t* out_key = nullptr);
 
 // emqx_broker:aggre/1 (aggre.hip) over a match_routes CSR (rcount, roff,
-// src, dest, key from launch_routes with av).  gflag: one u8 per route (used
-// by topics with > 4096 routes); large: n + 1 u32 (list of topics with > 512
-// routes).  Output at the route offsets: topic t's
+// src, dest, key from launch_routes with av; key rows of topics with > 4096
+// group-prefix routes are sorted in place); large: n + 1 u32 (list of topics
+// with > 512 routes).  Output at the route offsets: topic t's
 // list is out_to / out_tg[roff[t] .. + acount[t]) (out_to = TM_ROUTE_TOPIC_ID
 // or a filter id, out_tg = target id); entries at or past out_cap are dropped.
 hipError_t launch_aggre(const AggreView& av, uint32_t n, const uint32_t* rcount, const uint64_t* roff,
-                        const uint32_t* src, const uint32_t* dest, const uint64_t* key, uint8_t* gflag,
-                        uint32_t* large, uint32_t* acount, uint32_t* out_to, uint32_t* out_tg, uint64_t out_cap,
+                        const uint32_t* src, const uint32_t* dest, uint64_t* key, uint32_t* large, uint32_t* acount, uint32_t* out_to, uint32_t* out_tg, uint64_t out_cap,
                         hipStream_t st);
 
 // Sharded mode (shard.hip): merge per-topic match lists of S filter shards
@@ -71,10 +73,11 @@ hipError_t launch_aggre(const AggreView& av, uint32_t n, const uint32_t* rcount,
 // ids / keys and are CSR-ordered by topic, each list in descending key order.
 // Output: counts[m], offsets[m+1], global ids (local * S + s) in descending
 // key order = emqx_trie:match/1 order.  pre: S*m+1 u64, tmp: scan_tmp_elems(S*m).
+// Keys of key_words words: word j of item g at keys[j * key_stride + g].
 constexpr uint32_t MAX_SHARDS = 8;
 hipError_t launch_shard_merge(uint32_t S, uint32_t m, const uint32_t* counts, const uint64_t* src_base,
                               const uint32_t* ids, const uint64_t* keys, uint32_t* out_count, uint64_t* out_off,
                               uint32_t* out_gid, uint64_t out_cap, uint64_t* total, uint64_t* pre, uint64_t* tmp,
-                              hipStream_t st);
+                              hipStream_t st, uint32_t key_words = 1, uint64_t key_stride = 0);
 
 }  // namespace tmx

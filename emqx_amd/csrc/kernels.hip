@@ -356,9 +356,7 @@ constexpr int HIST_OFF = 8;   // hist = stats + HIST_OFF
 
 struct Cursor {
     uint32_t v, r, n, r0;   // node to visit next and its level; topic levels; start level
-    uint64_t key;           // KEYS: fold branches taken above level r (rank_sym)
-    uint64_t s;             // probe: the edge slot the next load reads
-    bool probe;             // next load: edge slot s of (v, W(r)) rather than v's node half
+    uint64_t key;           // KEYS: fold branches taken above level r (rank_sym), key word 0
 };
 
 // Order keys (sharded mode).  Every match of a topic is identified by the
@@ -366,14 +364,32 @@ struct Cursor {
 // (0), the topic word's edge (1) or the '+' edge (2), and for a node's own
 // filter at the last level n an end mark (1).  Discovery order is ascending
 // lexicographic order of these sequences (emqx_trie.erl:127-145; SURVEY
-// Appendix A.3), so packing them 2 bits per level from the top of a u64
+// Appendix A.3), so packing them 2 bits per level from the top of u64 words
 // makes a key whose DESCENDING order is the reference's output order, and
-// per-shard lists merge by key.  Levels >= 32 do not fit (keys saturate).
+// per-shard lists merge by key.  Word j holds symbol positions 32j..32j+31;
+// a batch keyed with KW words covers topics of up to 32*KW-1 levels.  The
+// cursor carries word 0 incrementally; the symbols of positions >= 32 (only
+// topics longer than WREG, whose path is in global memory) are read back from
+// the path, where every level records the branch it descended by.
 __device__ __forceinline__ uint64_t rank_sym(uint32_t level, uint64_t s) {
     return level < 32 ? s << (62 - 2 * level) : 0ull;
 }
 __device__ __forceinline__ uint64_t rank_prefix(uint64_t key, uint32_t level) {   // symbols of levels < level
     return level == 0 ? 0ull : level >= 32 ? key : key & (~0ull << (64 - 2 * level));
+}
+// path(k) (KEYS): node id of the '+' child pending at level k (or NODE_NONE)
+// | the branch taken at k in bits 29-30
+constexpr uint32_t SYM_LIT = 1u << 29, SYM_PLUS = 2u << 29;
+// key word j >= 1 of an emission at level r with final symbol sym
+template <class Path>
+__device__ __forceinline__ uint64_t key_word(const Path& path, uint32_t j, uint32_t r, uint32_t sym) {
+    const uint32_t lo = 32 * j;
+    if (r < lo) return 0ull;
+    uint64_t w = 0;
+    const uint32_t hi = r < lo + 32 ? r : lo + 32;
+    for (uint32_t p = lo; p < hi; ++p) w |= (uint64_t)((path(p) >> 29) & 3u) << (62 - 2 * (p - lo));
+    if (r < lo + 32) w |= (uint64_t)sym << (62 - 2 * (r - lo));
+    return w;
 }
 
 // topic words in VGPRs (n <= WREG): dynamic index by AND-masks (a select
@@ -412,7 +428,6 @@ __device__ __forceinline__ bool walk_begin(const ImageView& im, Cursor& c, uint3
                                            WalkStats& st) {
     c.n = n;
     c.key = 0;
-    c.probe = false;
     if (!dollar) {
         c.v = ROOT;
         c.r = c.r0 = 0;
@@ -427,11 +442,14 @@ __device__ __forceinline__ bool walk_begin(const ImageView& im, Cursor& c, uint3
 
 // one step; true when the topic's walk is complete.  A step loads ONE node
 // half; a literal child found through the edge table arrives with its record
-// (EdgeSlot), so it is visited in the same step, and so on down a chain of
-// table children, until a child needs its own load or the walk pops.
+// (EdgeSlot, TM_SLOT_RECORD builds), so it is visited in the same step, and
+// so on down a chain of table children, until a child needs its own load or
+// the walk pops.  (A variant that resolved edge probes one slot per step,
+// walk_step1, measured 4.10 vs 3.59 ms at C3 and was removed:
+// profiles/r01_v12_heat/walk1_ab.json.)
 template <bool STATS, bool KEYS, class Path, class Words, class Emit>
-__device__ __forceinline__ bool walk_step2(const ImageView& im, Cursor& c, Path path, const Words& W, Emit& emit,
-                                           WalkStats& st) {
+__device__ __forceinline__ bool walk_step(const ImageView& im, Cursor& c, Path path, const Words& W, Emit& emit,
+                                          WalkStats& st) {
     uint32_t v = c.v, r = c.r;
     uint64_t key = KEYS ? c.key : 0ull;
     bool leaf = r == c.n;
@@ -443,9 +461,9 @@ __device__ __forceinline__ bool walk_step2(const ImageView& im, Cursor& c, Path 
             st.edge_reads += leaf ? 1 : 3;   // 'match_#' (:141) + fold over [W, '+'] (:132)
             st.leaf_visits += leaf ? 1 : 0;
         }
-        if (hf != FILTER_NONE) emit(hf, key);   // 'match_#': the '#' filter
+        if (hf != FILTER_NONE) emit(hf, key, path, r, 0u);   // 'match_#': the '#' filter
         if (leaf) {
-            if (sf != FILTER_NONE) emit(sf, KEYS ? key | rank_sym(r, 1) : 0ull);   // the node's own filter (:128)
+            if (sf != FILTER_NONE) emit(sf, KEYS ? key | rank_sym(r, 1) : 0ull, path, r, 1u);   // own filter (:128)
             break;
         }
         const uint64_t pl0 = st.probe_loads;
@@ -463,7 +481,7 @@ __device__ __forceinline__ bool walk_step2(const ImageView& im, Cursor& c, Path 
             else if ((plus & NODE_MASK) != NODE_NONE) atomicAdd(st.hist + 50, 1ull);
         }
         if (g.child != NODE_NONE) {   // literal subtree first, '+' child pending at level r
-            path(r) = pc;
+            path(r) = KEYS ? (pc | SYM_LIT) : pc;
             v = g.child;
             if (KEYS) key |= rank_sym(r, 1);
             ++r;
@@ -482,7 +500,7 @@ __device__ __forceinline__ bool walk_step2(const ImageView& im, Cursor& c, Path 
             continue;
         }
         if (pc != NODE_NONE) {        // no literal child: straight into the '+' subtree
-            path(r) = NODE_NONE;
+            path(r) = KEYS ? (NODE_NONE | SYM_PLUS) : NODE_NONE;
             c.v = pc;
             c.r = r + 1;
             if (KEYS) c.key = key | rank_sym(r, 2);
@@ -492,10 +510,10 @@ __device__ __forceinline__ bool walk_step2(const ImageView& im, Cursor& c, Path 
     }
     for (uint32_t k = r; k > c.r0;) {   // pop to the deepest pending '+' child
         --k;
-        const uint32_t p = path(k);
+        const uint32_t p = KEYS ? path(k) & NODE_MASK : path(k);
         if (p != NODE_NONE) {
             if (STATS && st.hist) atomicAdd(st.hist + 50, 1ull);
-            path(k) = NODE_NONE;
+            path(k) = KEYS ? (NODE_NONE | SYM_PLUS) : NODE_NONE;
             c.v = p;
             c.r = k + 1;
             if (KEYS) c.key = rank_prefix(key, k) | rank_sym(k, 2);
@@ -503,140 +521,6 @@ __device__ __forceinline__ bool walk_step2(const ImageView& im, Cursor& c, Path 
         }
     }
     return true;
-}
-
-// pop to the deepest '+' child pending above level r; true when none is
-// left (the topic's walk is complete)
-template <bool STATS, bool KEYS, class Path>
-__device__ __forceinline__ bool walk_pop(Cursor& c, Path path, uint32_t r, uint64_t key, WalkStats& st) {
-    for (uint32_t k = r; k > c.r0;) {
-        --k;
-        const uint32_t p = path(k);
-        if (p != NODE_NONE) {
-            if (STATS && st.hist) atomicAdd(st.hist + 50, 1ull);
-            path(k) = NODE_NONE;
-            c.v = p;
-            c.r = k + 1;
-            if (KEYS) c.key = rank_prefix(key, k) | rank_sym(k, 2);
-            return false;
-        }
-    }
-    return true;
-}
-
-// One step = ONE 16 B load per lane, so every lane of a wave pays one
-// memory round trip per step: either node v's half (inner with words left,
-// leaf at the last level) or, when v is WIDE and its Bloom mask admits the
-// topic word, the next slot of the edge probe for (v, W(r)).  (walk_step2
-// resolves the probe inside the node's step: a wave whose lanes mix probing
-// and non-probing steps then pays two dependent round trips per step.)
-// The '+' child of v is parked in path(r) while the probe runs.
-template <bool STATS, bool KEYS, class Path, class Words, class Emit>
-__device__ __forceinline__ bool walk_step1(const ImageView& im, Cursor& c, Path path, const Words& W, Emit& emit,
-                                           WalkStats& st) {
-    const uint32_t v = c.v, r = c.r;
-    const uint64_t key = KEYS ? c.key : 0ull;
-    const bool hot = v < im.hot_limit;
-    const EdgeSlot* tab = hot ? im.hot_edges : im.edges;
-    const uint64_t mask = hot ? im.hot_slot_mask : im.edge_slot_mask;
-    const bool leaf = !c.probe && r == c.n;
-    const uint8_t* addr = c.probe ? reinterpret_cast<const uint8_t*>(tab + c.s)
-                                  : (leaf ? im.leaf : im.inner) + ((uint64_t)v << im.node_shift);
-    const uint4 h = *reinterpret_cast<const uint4*>(addr);
-    if (c.probe) {
-        if (STATS) {
-            ++st.probe_loads;
-            if (st.hist) atomicAdd(st.hist + 16 + (r < 15 ? r : 15), 1ull);
-        }
-        if (h.x == v && h.y == W(r)) {   // literal child from the table; '+' child stays pending
-            if (STATS && st.hist) atomicAdd(st.hist + 49, 1ull);
-            c.probe = false;
-            c.v = h.z;
-            c.r = r + 1;
-            if (KEYS) c.key = key | rank_sym(r, 1);
-            return false;
-        }
-        if (h.x != EDGE_EMPTY) {          // linear probing
-            c.s = (c.s + 1) & mask;
-            return false;
-        }
-        if (STATS && st.hist) atomicAdd(st.hist + 32 + (r < 15 ? r : 15), 1ull);
-        c.probe = false;                  // no literal child: into the '+' subtree
-        const uint32_t pc = path(r);
-        if (pc != NODE_NONE) {
-            if (STATS && st.hist) atomicAdd(st.hist + 50, 1ull);
-            path(r) = NODE_NONE;
-            c.v = pc;
-            c.r = r + 1;
-            if (KEYS) c.key = key | rank_sym(r, 2);
-            return false;
-        }
-        return walk_pop<STATS, KEYS>(c, path, r, key, st);
-    }
-    if (STATS) {
-        ++st.visits;
-        st.edge_reads += leaf ? 1 : 3;   // 'match_#' (:141) + fold over [W, '+'] (:132)
-        st.leaf_visits += leaf ? 1 : 0;
-        if (st.hist && !leaf) atomicAdd(st.hist + (r < 15 ? r : 15), 1ull);
-    }
-    if (h.y != FILTER_NONE) emit(h.y, key);   // 'match_#': the '#' filter
-    if (leaf) {
-        if (h.x != FILTER_NONE) emit(h.x, KEYS ? key | rank_sym(r, 1) : 0ull);   // the node's own filter (:128)
-        return walk_pop<STATS, KEYS>(c, path, r, key, st);
-    }
-    const uint32_t plus = h.x, pc = plus & NODE_MASK, w = W(r);
-    uint32_t child = NODE_NONE;
-    bool probe = false;
-    if (w < WORD_MAX) {
-        if (!(plus & WIDE)) {
-            child = h.z == w ? h.w : NODE_NONE;
-        } else {
-            const uint64_t b = word_bloom(w);
-            probe = ((((uint64_t)h.w << 32) | h.z) & b) == b;
-        }
-    } else if (w == WORD_PLUS) {   // out-of-domain topic level "+": the fold follows the '+' edge
-        child = pc;
-    } else if (w == WORD_HASH) {
-        probe = true;
-    }
-    if (probe) {
-        path(r) = pc;
-        c.probe = true;
-        c.s = edge_home(v, w, mask);
-        return false;
-    }
-    if (child != NODE_NONE) {   // literal subtree first, '+' child pending at level r
-        if (STATS && st.hist) atomicAdd(st.hist + 48, 1ull);
-        path(r) = pc;
-        c.v = child;
-        c.r = r + 1;
-        if (KEYS) c.key = key | rank_sym(r, 1);
-        return false;
-    }
-    if (pc != NODE_NONE) {      // no literal child: straight into the '+' subtree
-        if (STATS && st.hist) atomicAdd(st.hist + 50, 1ull);
-        path(r) = NODE_NONE;
-        c.v = pc;
-        c.r = r + 1;
-        if (KEYS) c.key = key | rank_sym(r, 2);
-        return false;
-    }
-    return walk_pop<STATS, KEYS>(c, path, r, key, st);
-}
-
-// TM_WALK1=1 selects walk_step1.  Measured at C3 (heat layout): walk 4.10 ms
-// vs 3.59 ms for walk_step2 (profiles/r01_v12_heat/walk1_ab.json): the walk
-// is bound by the memory system's random-request rate, not by lanes idling
-// behind a neighbour's probe, and the extra loop iterations cost.  Kept as a
-// compile-time A/B variant, off.
-#ifndef TM_WALK1
-#define TM_WALK1 0
-#endif
-template <bool STATS, bool KEYS, class Path, class Words, class Emit>
-__device__ __forceinline__ bool walk_step(const ImageView& im, Cursor& c, Path path, const Words& W, Emit& emit,
-                                          WalkStats& st) {
-    if (TM_WALK1) return walk_step1<STATS, KEYS>(im, c, path, W, emit, st);
-    return walk_step2<STATS, KEYS>(im, c, path, W, emit, st);
 }
 
 template <bool STATS, bool KEYS, class Path, class Words, class Emit>
@@ -650,7 +534,8 @@ __device__ __forceinline__ void walk(const ImageView& im, uint32_t n, bool dolla
 
 // discovery k of a topic goes to stage row slot K-1-k (k < K), 4 ids per
 // 16 B store; the row's last `count` slots are then the output in order.
-// KEYS: its order key to the same slot of the topic's key row.
+// KEYS: key word 0 to the same slot of the topic's key row; words j >= 1
+// (KW > 1) to key plane j, kplane u64 further on.
 template <bool KEYS>
 struct RowEmit {
     uint32_t* row;
@@ -658,7 +543,10 @@ struct RowEmit {
     uint32_t K, cnt;
     uint4 buf;
     uint64_t kb;   // KEYS: key of the last even discovery, stored with the next one (16 B)
-    __device__ __forceinline__ void operator()(uint32_t f, uint64_t key) {
+    uint32_t KW;
+    uint64_t kplane;
+    template <class Path>
+    __device__ __forceinline__ void operator()(uint32_t f, uint64_t key, const Path& path, uint32_t r, uint32_t sym) {
         if (KEYS && cnt < K) {
             if (!(cnt & 1u)) {
                 kb = key;
@@ -666,6 +554,7 @@ struct RowEmit {
                 *reinterpret_cast<uint4*>(krow + K - 1 - cnt) =
                     make_uint4((uint32_t)key, (uint32_t)(key >> 32), (uint32_t)kb, (uint32_t)(kb >> 32));
             }
+            for (uint32_t j = 1; j < KW; ++j) krow[j * kplane + K - 1 - cnt] = key_word(path, j, r, sym);
         }
         if (cnt < K) {
             const uint32_t s = cnt & 3u;
@@ -683,19 +572,25 @@ struct RowEmit {
     }
 };
 // re-walk of a topic with total > K ids: discovery k >= K goes to output
-// position total-1-k (KEYS: with its key)
+// position total-1-k (KEYS: with its key words, plane stride kstride)
 template <bool KEYS>
 struct TailEmit {
     uint32_t* out;
     uint64_t* kout;
     uint64_t base, cap;
     uint32_t K, total, cnt;
-    __device__ __forceinline__ void operator()(uint32_t f, uint64_t key) {
+    uint32_t KW;
+    uint64_t kstride;
+    template <class Path>
+    __device__ __forceinline__ void operator()(uint32_t f, uint64_t key, const Path& path, uint32_t r, uint32_t sym) {
         if (cnt >= K && cnt < total) {
             const uint64_t p = base + (total - 1 - cnt);
             if (p < cap) {
                 out[p] = f;
-                if (KEYS) kout[p] = key;
+                if (KEYS) {
+                    kout[p] = key;
+                    for (uint32_t j = 1; j < KW; ++j) kout[j * kstride + p] = key_word(path, j, r, sym);
+                }
             }
         }
         ++cnt;
@@ -738,7 +633,8 @@ template <bool STATS, bool XCDQ, bool KEYS>
 __global__ void __launch_bounds__(BLOCK)
 tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const uint32_t* __restrict__ twords,
               const uint32_t* __restrict__ words, const uint32_t* __restrict__ meta, uint32_t* __restrict__ gpath,
-              uint32_t* __restrict__ stage, uint64_t* __restrict__ kstage, uint32_t K, uint32_t* __restrict__ counts,
+              uint32_t* __restrict__ stage, uint64_t* __restrict__ kstage, uint32_t K, uint32_t KW,
+              uint32_t* __restrict__ counts,
               unsigned long long* __restrict__ ws, unsigned long long* __restrict__ stats,
               unsigned long long* __restrict__ hist, const uint32_t* __restrict__ perm) {
     __shared__ uint32_t lds_path[WREG * BLOCK];
@@ -754,11 +650,12 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
     uint32_t my = NO_TOPIC;
     bool is_long = false, drained = false;
     Cursor cur;
-    RowEmit<KEYS> em{nullptr, nullptr, K, 0, make_uint4(0, 0, 0, 0), 0ull};
+    RowEmit<KEYS> em{nullptr, nullptr, K, 0, make_uint4(0, 0, 0, 0), 0ull, KW, (uint64_t)n * K};
     WalkStats st;
     if (STATS) st.hist = hist;
     uint64_t lev_sum = 0, match_sum = 0;
     uint32_t maxc = 0;                 // largest list of this lane's topics (stage-row sizing)
+    uint32_t maxl = 0;                 // KEYS: most levels of this lane's topics (key width check)
     for (;;) {
         const bool need = (my == NO_TOPIC) && !drained;
         const uint64_t m = __ballot(need);
@@ -812,6 +709,7 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
                     const uint32_t nl = mt & MN;
                     const bool dollar = (mt & MDOLLAR) != 0;
                     lev_sum += nl;
+                    if (KEYS) maxl = nl > maxl ? nl : maxl;
                     is_long = (mt & MLONG) != 0;
                     em.row = stage + (uint64_t)i * K;
                     if (KEYS) em.krow = kstage + (uint64_t)i * K;
@@ -870,6 +768,13 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
         maxc = y > maxc ? y : maxc;
     }
     if (lane == 0 && maxc) atomicMax(ws + QWS_MAXC, (unsigned long long)maxc);
+    if (KEYS) {
+        for (int o = 32; o > 0; o >>= 1) {
+            const uint32_t y = (uint32_t)__shfl_xor((int)maxl, o, 64);
+            maxl = y > maxl ? y : maxl;
+        }
+        if (lane == 0 && maxl) atomicMax(ws + QWS_MAXL, (unsigned long long)maxl);
+    }
     wave_stats_add<STATS>(stats, lev_sum, match_sum, st);
 }
 
@@ -888,9 +793,11 @@ template <bool KEYS>
 __global__ void __launch_bounds__(BLOCK)
 tm_copy_out(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const uint32_t* __restrict__ twords,
             const uint32_t* __restrict__ words, const uint32_t* __restrict__ meta, uint32_t* __restrict__ gpath,
-            const uint32_t* __restrict__ stage, const uint64_t* __restrict__ kstage, uint32_t K,
+            const uint32_t* __restrict__ stage, const uint64_t* __restrict__ kstage, uint32_t K, uint32_t KW,
             const uint32_t* __restrict__ counts, const uint64_t* __restrict__ out_off, uint32_t* __restrict__ out,
             uint64_t* __restrict__ kout, uint64_t out_cap) {
+    const uint64_t kplane = (uint64_t)n * K;   // KEYS: key word j of stage slot x at kstage[j * kplane + x],
+                                               // of output p at kout[j * out_cap + p]
     __shared__ uint32_t lds_path[WREG * BLOCK];
     __shared__ uint32_t lds_inc[BLOCK];
     __shared__ uint64_t lds_scan[BLOCK / 64];
@@ -915,7 +822,8 @@ tm_copy_out(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const ui
             for (uint32_t j = (ct > K ? ct - K : 0u) + lane; j < ct; j += 64) {
                 if (ob + j < out_cap) {
                     out[ob + j] = stage[row + j];
-                    if (KEYS) kout[ob + j] = kstage[row + j];
+                    if (KEYS)
+                        for (uint32_t q = 0; q < KW; ++q) kout[q * out_cap + ob + j] = kstage[q * kplane + row + j];
                 }
             }
         }
@@ -931,7 +839,9 @@ tm_copy_out(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const ui
         const int64_t slot = (int64_t)K - (int64_t)ct + (int64_t)k;
         if (slot >= 0 && base + j < out_cap) {
             out[base + j] = stage[(uint64_t)(t0 + lo) * K + (uint64_t)slot];
-            if (KEYS) kout[base + j] = kstage[(uint64_t)(t0 + lo) * K + (uint64_t)slot];
+            if (KEYS)
+                for (uint32_t q = 0; q < KW; ++q)
+                    kout[q * out_cap + base + j] = kstage[q * kplane + (uint64_t)(t0 + lo) * K + (uint64_t)slot];
         }
     }
     if (threadIdx.x < tn && c > K) {   // fan-out beyond the stage row: walk again, write the head
@@ -939,7 +849,7 @@ tm_copy_out(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const ui
         const uint32_t mt = meta[t];
         const uint64_t b = off[t] - off[0];
         const MemWords mw{twords + (uint64_t)t * WREG, words + b + t};
-        TailEmit<KEYS> em{out, kout, base + ex, out_cap, K, c, 0};
+        TailEmit<KEYS> em{out, kout, base + ex, out_cap, K, c, 0, KW, out_cap};
         WalkStats s2;
         if (mt & MLONG)
             walk<false, KEYS>(im, mt & MN, (mt & MDOLLAR) != 0, GlobalPath{gpath + b + 2ull * t}, mw, em, s2);
@@ -1056,7 +966,7 @@ hipError_t launch_queue(bool stats_mode, bool xcdq, const ImageView& im, const u
                         uint32_t n, const QueueBufs& qb, uint32_t K, uint32_t* counts, uint64_t* out_off,
                         uint32_t* out, uint64_t* out_keys, uint64_t out_cap, uint64_t* total,
                         unsigned long long* stats, hipStream_t st, hipEvent_t* marks, uint32_t walk_blocks_per_cu,
-                        bool hist) {
+                        bool hist, uint32_t key_words) {
     auto mark = [&](int i) {
         if (marks) (void)hipEventRecord(marks[i], st);
     };
@@ -1066,7 +976,7 @@ hipError_t launch_queue(bool stats_mode, bool xcdq, const ImageView& im, const u
         for (int i = 0; i < 8; ++i) mark(i);
         return err;
     }
-    if (K == 0 || (K & 3u)) return hipErrorInvalidValue;
+    if (K == 0 || (K & 3u) || key_words == 0) return hipErrorInvalidValue;
     hipError_t err = hipMemsetAsync(qb.ws, 0, QWS_BYTES, st);
     if (err != hipSuccess) return err;
     dim3 blk(BLOCK), g(div_up(n, BLOCK));
@@ -1087,7 +997,8 @@ hipError_t launch_queue(bool stats_mode, bool xcdq, const ImageView& im, const u
     const uint32_t wg = resident_grid(tm_walk_queue<false, false, false>, div_up(n, 64), walk_blocks_per_cu);
 #define TM_Q(S, X, Y)                                                                                              \
     hipLaunchKernelGGL((tm_walk_queue<S, X, Y>), dim3(wg), blk, 0, st, im, off, n, qb.twords, qb.words, qb.meta, \
-                       qb.path, qb.stage, qb.kstage, K, counts, qb.ws, stats, hist ? stats + HIST_OFF : nullptr, \
+                       qb.path, qb.stage, qb.kstage, K, key_words, counts, qb.ws, stats,                         \
+                       hist ? stats + HIST_OFF : nullptr,                                                           \
                        qb.perm)
     if (keys) {
         if (stats_mode) TM_Q(true, true, true); else TM_Q(false, true, true);
@@ -1106,10 +1017,10 @@ hipError_t launch_queue(bool stats_mode, bool xcdq, const ImageView& im, const u
     if (out_cap) {
         if (keys)
             hipLaunchKernelGGL(tm_copy_out<true>, g, blk, 0, st, im, off, n, qb.twords, qb.words, qb.meta, qb.path,
-                               qb.stage, qb.kstage, K, counts, out_off, out, out_keys, out_cap);
+                               qb.stage, qb.kstage, K, key_words, counts, out_off, out, out_keys, out_cap);
         else
             hipLaunchKernelGGL(tm_copy_out<false>, g, blk, 0, st, im, off, n, qb.twords, qb.words, qb.meta, qb.path,
-                               qb.stage, nullptr, K, counts, out_off, out, nullptr, out_cap);
+                               qb.stage, nullptr, K, 1u, counts, out_off, out, nullptr, out_cap);
     }
     mark(7);
     return hipGetLastError();

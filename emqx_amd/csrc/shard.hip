@@ -32,8 +32,31 @@ tm_shard_sum(uint32_t S, uint32_t m, const uint32_t* __restrict__ counts, uint32
 // topic are distinct, so positions are a permutation.  The wave loads all
 // items of the topic at once (one round trip) into LDS, searches there, and
 // writes every id once; a topic beyond MCAP ids searches the lists in global
-// memory instead (L2-resident after the first touch).
+// memory instead (L2-resident after the first touch).  Keys of KW > 1 words
+// (topics of 32+ levels, kernels.hip key_word) sit in KW planes kstride
+// apart and are compared word by word in global memory.
 constexpr uint32_t MCAP = 512;   // ids of one topic staged in LDS (6 KB)
+
+// number of keys in list a[0..len) (descending, KW words, planes kstride
+// apart) greater than the key at b
+__device__ __forceinline__ uint32_t count_greater_w(const uint64_t* keys, uint64_t kstride, uint32_t KW, uint64_t a,
+                                                    uint32_t len, uint64_t b) {
+    uint32_t lo = 0, hi = len;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        bool gt = false;
+        for (uint32_t j = 0; j < KW; ++j) {
+            const uint64_t x = keys[j * kstride + a + mid], y = keys[j * kstride + b];
+            if (x != y) {
+                gt = x > y;
+                break;
+            }
+        }
+        if (gt) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
 
 template <class Keys>
 __device__ __forceinline__ uint32_t count_greater(const Keys& a, uint32_t len, uint64_t key) {
@@ -49,7 +72,8 @@ __device__ __forceinline__ uint32_t count_greater(const Keys& a, uint32_t len, u
 __global__ void __launch_bounds__(64)
 tm_shard_merge(uint32_t S, uint32_t m, const uint32_t* __restrict__ counts, const uint64_t* __restrict__ src_base,
                const uint64_t* __restrict__ pre, const uint32_t* __restrict__ ids, const uint64_t* __restrict__ keys,
-               const uint64_t* __restrict__ out_off, uint32_t* __restrict__ out_gid, uint64_t out_cap) {
+               const uint64_t* __restrict__ out_off, uint32_t* __restrict__ out_gid, uint64_t out_cap, uint32_t KW,
+               uint64_t kstride) {
     __shared__ uint64_t lk[MCAP];
     __shared__ uint32_t lg[MCAP];
     const uint32_t lane = threadIdx.x;
@@ -87,7 +111,17 @@ tm_shard_merge(uint32_t S, uint32_t m, const uint32_t* __restrict__ counts, cons
                     g = hh[q] + j;
                 }
         };
-        if (c <= MCAP) {
+        if (KW > 1) {
+            for (uint32_t i = lane; i < c; i += 64) {
+                uint32_t s, j;
+                uint64_t g;
+                locate(i, s, j, g);
+                uint32_t r = j;
+                for (uint32_t s2 = 0; s2 < S; ++s2)
+                    if (s2 != s && ns[s2]) r += count_greater_w(keys, kstride, KW, hh[s2], ns[s2], g);
+                if (o + r < out_cap) out_gid[o + r] = ids[g] * S + s;
+            }
+        } else if (c <= MCAP) {
             for (uint32_t i = lane; i < c; i += 64) {
                 uint32_t s, j;
                 uint64_t g;
@@ -129,8 +163,8 @@ static inline uint32_t mdiv_up(uint64_t a, uint64_t b) { return (uint32_t)((a + 
 hipError_t launch_shard_merge(uint32_t S, uint32_t m, const uint32_t* counts, const uint64_t* src_base,
                               const uint32_t* ids, const uint64_t* keys, uint32_t* out_count, uint64_t* out_off,
                               uint32_t* out_gid, uint64_t out_cap, uint64_t* total, uint64_t* pre, uint64_t* tmp,
-                              hipStream_t st) {
-    if (S == 0 || S > MAX_SHARDS) return hipErrorInvalidValue;
+                              hipStream_t st, uint32_t key_words, uint64_t key_stride) {
+    if (S == 0 || S > MAX_SHARDS || key_words == 0) return hipErrorInvalidValue;
     if (m == 0) {
         hipError_t err = hipMemsetAsync(out_off, 0, 8, st);
         return err == hipSuccess ? hipMemsetAsync(total, 0, 8, st) : err;
@@ -144,7 +178,7 @@ hipError_t launch_shard_merge(uint32_t S, uint32_t m, const uint32_t* counts, co
     if (err != hipSuccess) return err;
     const uint32_t grid = m < 65536 ? m : 65536;
     hipLaunchKernelGGL(tm_shard_merge, dim3(grid), dim3(64), 0, st, S, m, counts, src_base, pre, ids, keys, out_off,
-                       out_gid, out_cap);
+                       out_gid, out_cap, key_words, key_stride);
     return hipGetLastError();
 }
 

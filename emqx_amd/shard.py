@@ -70,6 +70,19 @@ def _p(x):
     return ctypes.c_void_p(x.data_ptr() if hasattr(x, "data_ptr") else int(x))
 
 
+def key_words_for(buf, off):
+    """u64 words per order key that cover every topic of a packed batch:
+    a topic of n levels needs n <= 32 * words - 1 (kernels.hip key_word)."""
+    off = np.asarray(off, dtype=np.int64)
+    if len(off) < 2:
+        return 1
+    b = np.asarray(buf[: int(off[-1])], dtype=np.uint8)
+    c = np.zeros(len(b) + 1, dtype=np.int64)
+    np.cumsum(b == ord("/"), out=c[1:])
+    levels = c[off[1:]] - c[off[:-1]] + 1
+    return int(levels.max()) // 32 + 1
+
+
 class ShardEngine(Engine):
     """The engine of shard `shard` of `n_shards` (one per GPU)."""
 
@@ -88,26 +101,38 @@ class ShardEngine(Engine):
                                                           self.n_shards, self.shard), "tm_insert_batch_shard")
 
     def match_keys_device(self, d_bytes, d_off, n, topic_bytes, d_counts, d_offs, d_ids, d_keys, out_cap, d_total,
-                          stream=None):
+                          stream=None, key_words=1):
+        """keyed walk; d_keys holds key_words planes of out_cap u64 (word j of
+        id i at d_keys[j * out_cap + i])"""
         st = None if stream is None else ctypes.c_void_p(stream if isinstance(stream, int) else stream.cuda_stream)
-        rc = self.lib.tm_match_batch_device_keys(self.h, _p(d_bytes), _p(d_off), n, topic_bytes, _p(d_counts),
-                                                 _p(d_offs), _p(d_ids), _p(d_keys), out_cap, _p(d_total), st)
-        return self._check(rc, "tm_match_batch_device_keys")
+        rc = self.lib.tm_match_batch_device_keys_w(self.h, _p(d_bytes), _p(d_off), n, topic_bytes, _p(d_counts),
+                                                   _p(d_offs), _p(d_ids), _p(d_keys), key_words, out_cap,
+                                                   _p(d_total), st)
+        return self._check(rc, "tm_match_batch_device_keys_w")
+
+    def key_levels(self):
+        """most levels of a topic in the last keyed batches (synchronises)"""
+        x = ctypes.c_uint32()
+        self._check(self.lib.tm_key_levels(self.h, ctypes.byref(x)), "tm_key_levels")
+        return x.value
 
     def merge_device(self, m, d_counts, d_src_base, d_ids, d_keys, d_out_count, d_out_off, d_out_gid, out_cap,
-                     d_total, stream=None):
+                     d_total, stream=None, key_words=1, key_stride=0):
         st = None if stream is None else ctypes.c_void_p(stream if isinstance(stream, int) else stream.cuda_stream)
-        rc = self.lib.tm_shard_merge(self.h, self.n_shards, m, _p(d_counts), _p(d_src_base), _p(d_ids), _p(d_keys),
-                                     _p(d_out_count), _p(d_out_off), _p(d_out_gid), out_cap, _p(d_total), st)
-        return self._check(rc, "tm_shard_merge")
+        rc = self.lib.tm_shard_merge_w(self.h, self.n_shards, m, _p(d_counts), _p(d_src_base), _p(d_ids),
+                                       _p(d_keys), key_words, key_stride, _p(d_out_count), _p(d_out_off),
+                                       _p(d_out_gid), out_cap, _p(d_total), st)
+        return self._check(rc, "tm_shard_merge_w")
 
 
-def exchange(counts, offs, ids, keys, n, n_shards, rank, group=None):
+def exchange(counts, offs, ids, keys, n, n_shards, rank, group=None, key_words=1, key_stride=0):
     """All-to-all of one rank's keyed lists (torch tensors on the rank's
     device: counts int32[n], offs int64[n+1], ids int32[>= total], keys
     int64[>= total]) so that every rank receives, from every shard, the lists
     of its own topic slice.  Returns (recv_counts int32[S*m] source-major,
-    src_base int64[S], recv_ids int32, recv_keys int64, m)."""
+    src_base int64[S], recv_ids int32, recv_keys int64, m).  Keys of key_words >
+    1 words sit in planes key_stride apart; received keys are planes of the
+    received total."""
     import torch
     import torch.distributed as dist
     b = slices(n, n_shards)
@@ -127,12 +152,14 @@ def exchange(counts, offs, ids, keys, n, n_shards, rank, group=None):
     recv_items = [int(x) for x in recv_sizes.cpu().tolist()]
     tot = sum(recv_items)
     recv_ids = torch.empty(max(tot, 1), dtype=torch.int32, device=dev)
-    recv_keys = torch.empty(max(tot, 1), dtype=torch.int64, device=dev)
+    recv_keys = torch.empty(max(tot, 1) * key_words, dtype=torch.int64, device=dev)
     lo, hi = int(cut[0]), int(cut[-1])
     dist.all_to_all_single(recv_ids[:tot], ids[lo:hi].contiguous(), output_split_sizes=recv_items,
                            input_split_sizes=send_items, group=group)
-    dist.all_to_all_single(recv_keys[:tot], keys[lo:hi].contiguous(), output_split_sizes=recv_items,
-                           input_split_sizes=send_items, group=group)
+    for j in range(key_words):
+        dist.all_to_all_single(recv_keys[j * tot:(j + 1) * tot], keys[j * key_stride + lo:j * key_stride + hi]
+                               .contiguous(), output_split_sizes=recv_items, input_split_sizes=send_items,
+                               group=group)
     base = np.zeros(n_shards, dtype=np.int64)
     base[1:] = np.cumsum(recv_items)[:-1]
     src_base = torch.from_numpy(base).to(dev)

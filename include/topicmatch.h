@@ -167,12 +167,29 @@ int tm_match_batch_device(tm_engine* e, const uint8_t* d_topic_bytes, const uint
  * the reference's fold took — 'match_#' 0, topic word 1, '+' 2 — and an end
  * mark 1 for a node's own filter, packed from the top of a u64).  Each
  * topic's ids come in descending key order, which is emqx_trie:match/1's
- * order (emqx_trie.erl:127-145), so shards' lists merge by key.  Keys cover
- * topics of up to 31 levels. */
+ * order (emqx_trie.erl:127-145), so shards' lists merge by key.  One key
+ * word covers topics of up to 31 levels; tm_match_batch_device_keys_w below
+ * takes wider keys. */
 int tm_match_batch_device_keys(tm_engine* e, const uint8_t* d_topic_bytes, const uint64_t* d_topic_off,
                                uint32_t n, uint64_t topic_bytes, uint32_t* d_out_count,
                                uint64_t* d_out_off, uint32_t* d_out_filter_id, uint64_t* d_out_key,
                                uint64_t out_cap, uint64_t* d_total, void* hip_stream);
+
+/* Keys wider than one word, for topics of 32 levels or more (MQTT levels are
+ * unlimited, src/emqx_mqtt_caps.erl:110): key_words u64 words per id (1 ..
+ * TM_MAX_KEY_WORDS), word j of id i at d_out_key[j * out_cap + i]; topics of
+ * up to 32 * key_words - 1 levels are keyed exactly.  The caller sizes
+ * key_words from its topics' level counts; tm_key_levels reports the most
+ * levels a keyed batch held, so a caller can verify the width it chose.
+ * tm_match_batch_device_keys is key_words = 1. */
+#define TM_MAX_KEY_WORDS 1024u
+int tm_match_batch_device_keys_w(tm_engine* e, const uint8_t* d_topic_bytes, const uint64_t* d_topic_off,
+                                 uint32_t n, uint64_t topic_bytes, uint32_t* d_out_count, uint64_t* d_out_off,
+                                 uint32_t* d_out_filter_id, uint64_t* d_out_key, uint32_t key_words,
+                                 uint64_t out_cap, uint64_t* d_total, void* hip_stream);
+/* most levels of any topic in the engine's in-flight / last keyed batches
+ * (synchronises on them) */
+int tm_key_levels(tm_engine* e, uint32_t* max_levels);
 
 /* Merge, on e's GPU, the keyed lists of n_shards (<= 8) shards for m topics
  * (after the all-to-all exchange): d_counts [n_shards][m]; shard s's ids and
@@ -184,6 +201,11 @@ int tm_shard_merge(tm_engine* e, uint32_t n_shards, uint32_t m, const uint32_t* 
                    const uint64_t* d_src_base, const uint32_t* d_ids, const uint64_t* d_keys,
                    uint32_t* d_out_count, uint64_t* d_out_off, uint32_t* d_out_gid, uint64_t out_cap,
                    uint64_t* d_total, void* hip_stream);
+/* Same with keys of key_words words: word j of item g at d_keys[j * key_stride + g]. */
+int tm_shard_merge_w(tm_engine* e, uint32_t n_shards, uint32_t m, const uint32_t* d_counts,
+                     const uint64_t* d_src_base, const uint32_t* d_ids, const uint64_t* d_keys, uint32_t key_words,
+                     uint64_t key_stride, uint32_t* d_out_count, uint64_t* d_out_off, uint32_t* d_out_gid,
+                     uint64_t out_cap, uint64_t* d_total, void* hip_stream);
 
 /* ---- routes: the emqx_route bag and emqx_router:match_routes/1 -------------
  * A route is (topic, dest) (#route{topic, dest}, include/emqx.hrl:84-87); dest

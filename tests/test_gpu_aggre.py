@@ -172,3 +172,53 @@ def test_aggre_golden_vectors(gpu_device):
         for tp, row, want in zip(topics, got, case["deliveries"]):
             assert [[to.hex(), x[0], x[1].hex()] for to, x in row] == want, tp
         e.close()
+
+
+def test_aggre_beyond_4096_group_routes(gpu_device):
+    """a topic whose routes up to the last $share route exceed
+    4096 takes tm_aggre_large's in-place row sort (was O(u^2) counting)"""
+    e = Engine(device=gpu_device)
+    r, o = Router(e, node="n1"), pytrie.RouteTable()
+    rng = random.Random(44)
+    for f, m in [(b"#", 6000), (b"a/#", 9500), (b"a/+", 300)]:
+        for k in range(m):
+            x = rng.randrange(1 << 30)
+            d = ("g%d" % (x % 2900), "n%d" % (x % 3)) if k % 3 == 0 else "n%d" % (x % 7000)
+            r.add_route(f, d)
+            o.add_route(f, d)
+    r.add_route(b"a/b", ("g7", "n2"))
+    o.add_route(b"a/b", ("g7", "n2"))
+    topics = [b"a/b", b"a", b"x/y", b"$SYS/a"]
+    got = r.match_deliveries_many(topics, tagged=True)
+    assert max(len(o.match_routes(tp)) for tp in topics) > 10000
+    for tp, row in zip(topics, got):
+        assert row == o.match_deliveries(tp), tp
+    e.close()
+
+
+def test_routes_enospc_small_batch_high_fanout(gpu_device):
+    """out_cap > route workspace > ... with a 2-topic batch whose
+    lists exceed the first call's default 64K cap: TM_ENOSPC, then exact"""
+    from emqx_amd.engine import pack
+    from emqx_amd import _lib as L
+    e = Engine(device=gpu_device)
+    n_routes = 70_000
+    tb, to = pack([b"#"] * n_routes)
+    db, do = pack([b"n%d" % i for i in range(n_routes)])
+    e.route_add_many(tb, to, db, do)
+    topics = [b"a/b", b"c"]
+    pb, po = pack(topics)
+    with pytest.raises(L.TopicMatchError) as ex:
+        e.match_routes_batch(pb, po, out_cap=1 << 16)
+    assert ex.value.code == L.TM_ENOSPC
+    counts, offs, src, dst = e.match_routes_batch(pb, po)
+    assert list(counts) == [n_routes, n_routes]
+    assert list(dst[:n_routes]) == [e.get_routes(b"#")[i] for i in range(n_routes)]
+    assert list(dst[n_routes:]) == list(dst[:n_routes])
+    with pytest.raises(L.TopicMatchError) as ex:
+        e.match_deliveries_batch(pb, po, out_cap=1 << 16)
+    assert ex.value.code == L.TM_ENOSPC
+    counts, offs, to_, tg = e.match_deliveries_batch(pb, po)
+    assert list(counts) == [n_routes, n_routes]     # node dests only: the fold reverses
+    assert [e.target_bytes(int(x))[1] for x in tg[:3]] == [b"n69999", b"n69998", b"n69997"]
+    e.close()

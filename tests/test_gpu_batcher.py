@@ -68,3 +68,58 @@ def test_batcher_results_equal_batch_api(gpu_device, routes):
             assert [int(x) for x in want[t][1]] == dests, t
     assert sum(len(g[0]) for g in got) > 100_000
     e.close()
+
+
+def test_routes_and_deliveries_batchers_concurrently(gpu_device):
+    """a routes batcher and a deliveries batcher on ONE engine
+    (the NIF opens both), fed at once from 4 threads each; both result sets
+    must equal the batch API, which is pinned to the oracle (a sample is
+    checked against oracle/pytrie.py directly as well)"""
+    import random
+    from emqx_amd.emqx_router import Router
+    from oracle import pytrie
+    fb, fo = W.filters(1, n=4000)
+    tb, to = W.topics(1, n=20000)
+    topics = W.unpack(tb, to)
+    e = Engine(device=gpu_device)
+    r, o = Router(e, node="n1"), pytrie.RouteTable()
+    rng = random.Random(3)
+    dests = ["n1", "n2", ("g1", "n1"), ("g1", "n2"), ("g2", "n3")]
+    for f in W.unpack(fb, fo):
+        for d in rng.sample(dests, rng.randint(1, 3)):
+            r.add_route(f, d)
+            o.add_route(f, d)
+    for t in topics[::9]:
+        r.add_route(t, "n3")
+        o.add_route(t, "n3")
+    rc, ro, rs, rd = e.match_routes_batch(tb, to)
+    dc, do, dt, dg = e.match_deliveries_batch(tb, to)
+    want_r = [(list(rs[ro[t]:ro[t + 1]]), list(rd[ro[t]:ro[t + 1]])) for t in range(len(topics))]
+    want_d = [(list(dt[do[t]:do[t] + dc[t]]), list(dg[do[t]:do[t] + dc[t]])) for t in range(len(topics))]
+    tagged = r.match_deliveries_many(topics[:400], tagged=True)
+    for t in range(400):
+        assert tagged[t] == o.match_deliveries(topics[t]), t
+    br = Batcher(e, max_topics=2000, deadline_us=300, routes=True)
+    bd = Batcher(e, max_topics=1500, deadline_us=300, deliveries=True)
+    got_r, got_d = [None] * len(topics), [None] * len(topics)
+
+    def producer(b, got, k):
+        for t in range(k, len(topics), 4):
+            def cb(status, ids, ds, t=t):
+                assert status == 0
+                got[t] = (ids, ds)
+            b.submit(topics[t], cb)
+    ts = [threading.Thread(target=producer, args=(b, g, k)) for b, g in ((br, got_r), (bd, got_d)) for k in range(4)]
+    for x in ts:
+        x.start()
+    for x in ts:
+        x.join()
+    br.flush()
+    bd.flush()
+    assert br.stats()["failed_batches"] == 0 and bd.stats()["failed_batches"] == 0
+    br.close()
+    bd.close()
+    for t in range(len(topics)):
+        assert got_r[t] == ([int(x) for x in want_r[t][0]], [int(x) for x in want_r[t][1]]), t
+        assert got_d[t] == ([int(x) for x in want_d[t][0]], [int(x) for x in want_d[t][1]]), t
+    e.close()

@@ -25,6 +25,7 @@ def _run_sharded(filters, topics, S, K=None):
     n = len(topics)
     d_b = torch.from_numpy(tb).to(dev)
     d_o = torch.from_numpy(to.view(np.int64)).to(dev)
+    KW = shard.key_words_for(tb, to)
     engs, res = [], []
     for s in range(S):
         e = shard.ShardEngine(0, S, s, filters_hint=len(filters))
@@ -34,15 +35,16 @@ def _run_sharded(filters, topics, S, K=None):
         c = torch.empty(n, dtype=torch.int32, device=dev)
         o = torch.empty(n + 1, dtype=torch.int64, device=dev)
         tot = torch.zeros(1, dtype=torch.int64, device=dev)
-        e.match_keys_device(d_b, d_o, n, int(to[-1]), c, o, None, None, 0, tot)
+        e.match_keys_device(d_b, d_o, n, int(to[-1]), c, o, None, None, 0, tot, key_words=KW)
         torch.cuda.synchronize()
         cap = int(tot.item()) + 16
         ids = torch.empty(cap, dtype=torch.int32, device=dev)
-        keys = torch.empty(cap, dtype=torch.int64, device=dev)
-        e.match_keys_device(d_b, d_o, n, int(to[-1]), c, o, ids, keys, cap, tot)
+        keys = torch.empty(cap * KW, dtype=torch.int64, device=dev)
+        e.match_keys_device(d_b, d_o, n, int(to[-1]), c, o, ids, keys, cap, tot, key_words=KW)
         torch.cuda.synchronize()
+        assert e.key_levels() <= 32 * KW - 1
         engs.append(e)
-        res.append((c, o, ids, keys))
+        res.append((c, o, ids, keys.view(KW, cap)))
     b = shard.slices(n, S)
     out = []
     for r in range(S):      # what rank r receives from every shard, then merges
@@ -51,16 +53,18 @@ def _run_sharded(filters, topics, S, K=None):
         cuts = [(int(res[s][1][b[r]].item()), int(res[s][1][b[r + 1]].item())) for s in range(S)]
         rid = torch.cat([res[s][2][lo:hi] for s, (lo, hi) in enumerate(cuts)] + [torch.zeros(1, dtype=torch.int32,
                                                                                              device=dev)])
-        rk = torch.cat([res[s][3][lo:hi] for s, (lo, hi) in enumerate(cuts)] + [torch.zeros(1, dtype=torch.int64,
-                                                                                            device=dev)])
         sizes = [hi - lo for lo, hi in cuts]
+        tot_r = sum(sizes)
+        # key planes of the received total (what shard.exchange delivers)
+        rk = torch.cat([torch.cat([res[s][3][j, lo:hi] for s, (lo, hi) in enumerate(cuts)])
+                        for j in range(KW)] + [torch.zeros(1, dtype=torch.int64, device=dev)])
         base = torch.tensor(np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.int64), device=dev)
         oc = torch.empty(max(m, 1), dtype=torch.int32, device=dev)
         oo = torch.empty(m + 1, dtype=torch.int64, device=dev)
         tot = torch.zeros(1, dtype=torch.int64, device=dev)
         cap = sum(sizes) + 1
         og = torch.empty(cap, dtype=torch.int32, device=dev)
-        engs[r].merge_device(m, rc, base, rid, rk, oc, oo, og, cap, tot)
+        engs[r].merge_device(m, rc, base, rid, rk, oc, oo, og, cap, tot, key_words=KW, key_stride=tot_r)
         torch.cuda.synchronize()
         assert int(tot.item()) == sum(sizes)
         oo_h, og_h = oo.cpu().numpy(), og.cpu().numpy().view(np.uint32)
@@ -105,8 +109,6 @@ def test_sharded_kats(gpu_device, golden):
     """the reference's own trie KATs and the O1 vectors, split over 3 shards"""
     for vec in golden["o1_vectors"]:
         topics = [r["topic"].encode("latin-1") for r in vec["topics"]]
-        if any(t.count(b"/") >= 31 for t in topics):
-            continue        # > 31 levels: keys do not cover them
         filters = [f.encode("latin-1") for f in vec["filters"]]
         got = _run_sharded(filters, topics, 3)
         assert [[x.decode("latin-1") for x in row] for row in got] == [r["match"] for r in vec["topics"]], vec["name"]
@@ -125,3 +127,18 @@ def test_sharded_topic_beyond_lds_merge(gpu_device):
     assert len(want[0]) > 1024
     for S in (2, 5):
         assert _run_sharded(filters, topics, S, K=256) == want
+
+
+@pytest.mark.parametrize("S", [3, 8])
+def test_sharded_32_to_64_levels_equals_o1(gpu_device, S):
+    """keys of 2+ words; topics of 32-64 levels, id for id vs O1"""
+    from emqx_amd import shard
+    from emqx_amd.engine import pack
+    from long_topics import long_case
+    filters, topics = long_case(S)
+    tb, to = pack(topics)
+    assert shard.key_words_for(tb, to) == 3
+    want = _o1(filters, topics)
+    assert sum(len(w) for w in want) > 1000 and max(len(w) for w in want) > 8
+    assert _run_sharded(filters, topics, S) == want
+    assert _run_sharded(filters, topics, S, K=4) == want   # re-walk tail with wide keys

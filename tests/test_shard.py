@@ -43,10 +43,14 @@ def test_shard_of_partition():
 
 
 def _workload():
+    """C1 filters and topics plus a 32-64-level slice (two-word keys)"""
     from emqx_amd import workload as W
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from long_topics import long_case
     fb, fo = W.filters(1, n=6000)
     tb, to = W.topics(1, n=3000)
-    return W.unpack(fb, fo), W.unpack(tb, to)
+    lf, lt = long_case(7, n_filters=800, n_topics=120)
+    return W.unpack(fb, fo) + lf, W.unpack(tb, to) + lt
 
 
 def _worker(rank, world, port, q):
@@ -72,14 +76,18 @@ def _worker(rank, world, port, q):
     tb, to = pack(topics)
     counts, offs, ids = o1.match_ids(tb, to)
     levels = [t.count(b"/") + 1 for t in topics]
-    keys = np.zeros(max(len(ids), 1), dtype=np.uint64)
+    KW = shard.key_words_for(tb, to)
+    assert KW == 3
+    cap = max(len(ids), 1)
+    keys = np.zeros((KW, cap), dtype=np.uint64)
     for t in range(len(topics)):
         for j in range(int(offs[t]), int(offs[t + 1])):
-            keys[j] = order_key(mine[ids[j]], levels[t])
+            keys[:, j] = order_key(mine[ids[j]], levels[t], KW)
     rc, base, rid, rk, m = shard.exchange(
         torch.from_numpy(counts.astype(np.int32)), torch.from_numpy(offs.astype(np.int64)),
-        torch.from_numpy(ids.astype(np.int32)), torch.from_numpy(keys.view(np.int64)), len(topics), world, rank)
-    merged = merge_host(rc.numpy(), base.numpy(), rid.numpy(), rk.numpy(), m, world)
+        torch.from_numpy(ids.astype(np.int32)), torch.from_numpy(keys.reshape(-1).view(np.int64)), len(topics),
+        world, rank, key_words=KW, key_stride=cap)
+    merged = merge_host(rc.numpy(), base.numpy(), rid.numpy(), rk.numpy(), m, world, key_words=KW)
     # gid -> (shard, local) -> bytes: gather every shard's filter list
     lists = [None] * world
     dist.all_gather_object(lists, mine)
@@ -111,3 +119,24 @@ def test_two_rank_exchange_and_merge_equals_o1():
     assert len(got) == len(topics)
     assert sum(len(r) for r in want) > 1000
     assert got == want
+
+
+def test_wide_order_key_is_reference_order():
+    """descending multi-word order key = emqx_trie:match/1 order (O1) for
+    topics of 32-64 levels, where groups of filters tie on key word 0"""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from emqx_amd.engine import pack
+    from long_topics import long_case
+    from oracle import O1
+    from shard_ref import order_key
+    filters, topics = long_case(11)
+    o1 = O1()
+    o1.insert_many(*pack(filters))
+    ties = 0
+    for t in topics:
+        want = o1.match(t)
+        n = t.count(b"/") + 1
+        keys = [order_key(f, n, 3) for f in want]
+        assert keys == sorted(keys, reverse=True) and len(set(keys)) == len(keys), t
+        ties += len(want) - len({k[0] for k in keys})
+    assert ties > 100     # word 0 alone would not order them
