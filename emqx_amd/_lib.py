@@ -13,6 +13,7 @@ LIB_PATH = os.path.join(_HERE, "libtopicmatch.so")
 
 TM_OK, TM_EINVAL, TM_ENOSPC, TM_EDEVICE, TM_ENOMEM, TM_ENOENT, TM_ERANGE = 0, -1, -2, -3, -4, -5, -6
 TM_NO_FILTER = 0xFFFFFFFF
+TM_NO_RULE = 0xFFFFFFFF
 
 c_u8p = ctypes.POINTER(ctypes.c_uint8)
 c_u32p = ctypes.POINTER(ctypes.c_uint32)
@@ -147,6 +148,15 @@ SIGNATURES = [
     ("tm_acl_rule_end", ctypes.c_int, [ctypes.c_void_p]),
     ("tm_acl_rule_count", ctypes.c_int, [ctypes.c_void_p]),
     ("tm_acl_check_batch", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32] + [ctypes.c_void_p] * 13),
+    ("tm_acl_check_batch_device", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32] + [ctypes.c_void_p] * 14),
+    ("tm_rewrite_open", ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+    ("tm_rewrite_close", None, [ctypes.c_void_p]),
+    ("tm_rewrite_rule", ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint32]),
+    ("tm_rewrite_rule_count", ctypes.c_int, [ctypes.c_void_p]),
+    ("tm_rewrite_match_batch", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                              ctypes.c_void_p]),
+    ("tm_rewrite_match_batch_device", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                     ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]),
     ("tm_last_stats", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(TmBatchStats)]),
     ("tm_set_timing", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     ("tm_last_kernel_times", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_char_p),

@@ -452,4 +452,29 @@ int tm_acl_check_batch(tm_acl* a, uint32_t n, const uint8_t* access, const uint8
     return TM_OK;
 }
 
+int tm_acl_check_batch_device(tm_acl* a, uint32_t n, const uint8_t* d_access, const uint8_t* d_topics,
+                              const uint64_t* d_topic_off, const uint8_t* d_client_ids, const uint64_t* d_client_off,
+                              const uint8_t* d_client_defined, const uint8_t* d_usernames, const uint64_t* d_user_off,
+                              const uint8_t* d_user_defined, const uint8_t* d_peers, const uint8_t* d_peer_family,
+                              int8_t* d_out_result, uint32_t* d_out_rule, void* hip_stream) {
+    if (!a || a->open_rule || (n && (!d_access || !d_topic_off || !d_client_off || !d_client_defined ||
+                                     !d_user_off || !d_user_defined || !d_out_result)))
+        return TM_EINVAL;
+    std::lock_guard<std::mutex> lk(a->mu);
+    if (a->device < 0) return TM_EDEVICE;
+    if (n == 0) return TM_OK;
+    if (hipSetDevice(a->device) != hipSuccess) return TM_EDEVICE;
+    if (a->dirty) {
+        if (!a->d_rules.put(a->rules) || !a->d_filters.put(a->filters) || !a->d_words.put(a->words) ||
+            !a->d_who.put(a->who) || !a->d_arena.put(a->arena))
+            return TM_ENOMEM;
+        a->dirty = false;
+    }
+    AclView v{a->d_rules.p, (uint32_t)a->rules.size(), a->d_filters.p, a->d_words.p, a->d_who.p, a->d_arena.p};
+    hipLaunchKernelGGL(tm_acl_check, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)hip_stream, v, n, d_access,
+                       d_topics, d_topic_off, d_client_ids, d_client_off, d_client_defined, d_usernames, d_user_off,
+                       d_user_defined, d_peers, d_peer_family, d_out_result, d_out_rule);
+    return hipGetLastError() == hipSuccess ? TM_OK : TM_EDEVICE;
+}
+
 }  // extern "C"

@@ -1,0 +1,92 @@
+"""emqx_mod_rewrite on the GPU (src/emqx_mod_rewrite.erl).
+
+match_rule/2 (:52-59) applies the FIRST rule whose filter
+emqx_topic:match/2 accepts (binary clause, '$' rule included), then that
+rule's regex (match_regx/3, :61-71): on a regex miss the topic stays as it
+is, later rules are never tried.  The device (rewrite.hip) picks the rule for
+a whole batch of topics; the regex step runs here on the host with Python's
+`re` standing in for Erlang's PCRE-based `re` (same syntax for the common
+subset: groups, classes, anchors; `$N` in Dest is the N-th capture,
+replaced left to right like the reference's foldl of re:replace/4)."""
+import ctypes
+import re
+
+import numpy as np
+
+from . import _lib as L
+from .engine import pack
+
+NO_RULE = L.TM_NO_RULE
+
+
+def _b(x):
+    return x.encode() if isinstance(x, str) else bytes(x)
+
+
+class Rewrite:
+    """rules: [(filter, regex, dest)] in compile/1 order"""
+
+    def __init__(self, rules, device=0):
+        self.lib = L.load()
+        h = ctypes.c_void_p()
+        rc = self.lib.tm_rewrite_open(device, ctypes.byref(h))
+        if rc != L.TM_OK:
+            raise L.TopicMatchError(rc, "tm_rewrite_open(device=%d)" % device)
+        self.h = h
+        self.rules = []
+        for f, rx, dest in rules:
+            f = _b(f)
+            rc = self.lib.tm_rewrite_rule(self.h, f, len(f))
+            if rc != L.TM_OK:
+                raise L.TopicMatchError(rc, "tm_rewrite_rule")
+            self.rules.append((f, re.compile(_b(rx)), _b(dest)))
+
+    def close(self):
+        if self.h:
+            self.lib.tm_rewrite_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def rule_index_batch(self, buf, off):
+        """u32[n]: index of the first rule whose filter matches, NO_RULE if none"""
+        buf = np.ascontiguousarray(buf, dtype=np.uint8)
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        n = len(off) - 1
+        out = np.zeros(max(n, 1), dtype=np.uint32)
+        rc = self.lib.tm_rewrite_match_batch(self.h, buf.ctypes.data, off.ctypes.data, n, out.ctypes.data)
+        if rc != L.TM_OK:
+            raise L.TopicMatchError(rc, "tm_rewrite_match_batch")
+        return out[:n]
+
+    def rule_index_device(self, d_topics, d_off, n, d_out, stream=None):
+        def p(x):
+            return None if x is None else ctypes.c_void_p(x.data_ptr() if hasattr(x, "data_ptr") else int(x))
+        st = None if stream is None else ctypes.c_void_p(stream if isinstance(stream, int) else stream.cuda_stream)
+        rc = self.lib.tm_rewrite_match_batch_device(self.h, p(d_topics), p(d_off), n, p(d_out), st)
+        if rc != L.TM_OK:
+            raise L.TopicMatchError(rc, "tm_rewrite_match_batch_device")
+
+    def rewrite_many(self, topics):
+        """match_rule/2 for every topic: the rewritten topic bytes"""
+        idx = self.rule_index_batch(*pack(topics))
+        out = []
+        for t, k in zip(topics, idx):
+            t = _b(t)
+            out.append(t if k == NO_RULE else match_regx(t, self.rules[k][1], self.rules[k][2]))
+        return out
+
+
+def match_regx(topic: bytes, mp, dest: bytes) -> bytes:
+    """match_regx/3 (src/emqx_mod_rewrite.erl:61-71)"""
+    m = mp.search(topic)
+    if m is None:
+        return topic
+    acc = dest
+    for i, val in enumerate(m.groups(), start=1):     # foldl over [{"\\$1", V1}, ...]
+        acc = acc.replace(b"$%d" % i, val if val is not None else b"")
+    return acc

@@ -25,6 +25,12 @@ def topic_stream(rank: int) -> int:
     return rank
 
 
+def batch_slice(n: int, world: int, rank: int):
+    """[lo, hi) of rank's contiguous slice of an n-topic batch (strong
+    scaling: SURVEY §8(d) C3 splits one batch 1/2/4/8 ways)"""
+    return (n * rank) // world, (n * (rank + 1)) // world
+
+
 def timed_region(step, steps: int, sync, group=None):
     """Run `steps` calls of step() bracketed by barrier + device sync on both
     sides; returns the MAX over ranks of the wall time (seconds)."""

@@ -383,6 +383,35 @@ int  tm_acl_check_batch(tm_acl* a, uint32_t n, const uint8_t* access, const uint
                         const uint8_t* user_defined, const uint8_t* peers, const uint8_t* peer_family,
                         int8_t* out_result, uint32_t* out_rule);
 
+/* Same with every buffer device-resident (HBM; byte offsets index topics /
+ * client_ids / usernames directly), stream-ordered on hip_stream, no
+ * synchronisation: the form a pipelined caller and the ACL bench use. */
+int tm_acl_check_batch_device(tm_acl* a, uint32_t n, const uint8_t* d_access, const uint8_t* d_topics,
+                              const uint64_t* d_topic_off, const uint8_t* d_client_ids, const uint64_t* d_client_off,
+                              const uint8_t* d_client_defined, const uint8_t* d_usernames, const uint64_t* d_user_off,
+                              const uint8_t* d_user_defined, const uint8_t* d_peers, const uint8_t* d_peer_family,
+                              int8_t* d_out_result, uint32_t* d_out_rule, void* hip_stream);
+
+/* ---- batched topic-rewrite rule selection (rewrite.hip) -------
+ * emqx_mod_rewrite:match_rule/2 (src/emqx_mod_rewrite.erl:52-59) applies the
+ * FIRST rule whose filter emqx_topic:match/2 accepts (the binary clause with
+ * the '$' rule, src/emqx_topic.erl:56-61), then that rule's regex.  A
+ * tm_rewrite holds the rules' filters in order (compile/1 order); the batch
+ * calls return, per topic, the index of the first matching rule or
+ * TM_NO_RULE.  The regex (re:run + re:replace of match_regx/3) stays with
+ * the caller. */
+#define TM_NO_RULE 0xFFFFFFFFu
+typedef struct tm_rewrite tm_rewrite;
+int  tm_rewrite_open(int device, tm_rewrite** out);
+void tm_rewrite_close(tm_rewrite* r);
+int  tm_rewrite_rule(tm_rewrite* r, const uint8_t* filter, uint32_t len);   /* appended as the next rule */
+int  tm_rewrite_rule_count(tm_rewrite* r);
+int  tm_rewrite_match_batch(tm_rewrite* r, const uint8_t* topics, const uint64_t* topic_off, uint32_t n,
+                            uint32_t* out_rule);
+/* device buffers (topic t = d_topics[d_topic_off[t] .. d_topic_off[t+1])), stream-ordered */
+int  tm_rewrite_match_batch_device(tm_rewrite* r, const uint8_t* d_topics, const uint64_t* d_topic_off, uint32_t n,
+                                   uint32_t* d_out_rule, void* hip_stream);
+
 /* Engine knobs (the app-env analogue of SURVEY §5 config):
  *   "xcdq"     1 = per-XCD dequeue heads over contiguous ranges of the batch
  *              (default), 0 = one global head

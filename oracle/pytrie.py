@@ -318,3 +318,12 @@ class RouteTable:
     def match_deliveries(self, topic: bytes):
         """aggre(match_routes(Topic)) — emqx_broker.erl:152"""
         return aggre(self.match_routes(topic))
+
+
+def rewrite_rule_index(topic: bytes, filters):
+    """emqx_mod_rewrite:match_rule/2's rule choice (src/emqx_mod_rewrite.erl:
+    52-59): the index of the first rule whose filter match/2 accepts, or None"""
+    for i, f in enumerate(filters):
+        if match(topic, f):
+            return i
+    return None

@@ -110,8 +110,11 @@ def test_oracle_matches_aggre_golden():
         o = pytrie.RouteTable()
         for op, t, d in case["ops"]:
             (o.add_route if op == "add" else o.del_route)(bytes.fromhex(t), _dest(d))
-        for tp, want in zip(case["topics"], case["deliveries"]):
+        for tp, want in zip(case["topics"] + case["ood_topics"], case["deliveries"] + case["ood_deliveries"]):
             got = [[to.hex(), x[0], x[1].hex()] for to, x in o.match_deliveries(bytes.fromhex(tp))]
             assert got == want, tp
             n += len(want)
+        assert all(b"+" not in bytes.fromhex(tp).split(b"/") and b"#" not in bytes.fromhex(tp).split(b"/")
+                   for tp in case["topics"])
     assert n > 100
+    assert _golden()["source"].startswith("ORACLE-DERIVED")
