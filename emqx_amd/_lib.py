@@ -39,7 +39,7 @@ class TmBatchStats(ctypes.Structure):
 
 class TmBatcherConfig(ctypes.Structure):
     _fields_ = [("max_topics", ctypes.c_uint32), ("deadline_us", ctypes.c_uint32), ("max_bytes", ctypes.c_uint64),
-                ("flags", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+                ("flags", ctypes.c_uint32), ("lanes_per_replica", ctypes.c_uint32)]
 
 
 class TmBatcherStats(ctypes.Structure):
@@ -54,6 +54,10 @@ DONE_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int,
 # (name, restype, argtypes) — every symbol include/topicmatch.h declares
 SIGNATURES = [
     ("tm_open", ctypes.c_int, [ctypes.POINTER(TmConfig), ctypes.POINTER(ctypes.c_void_p)]),
+    ("tm_open_devices", ctypes.c_int, [ctypes.POINTER(TmConfig), ctypes.POINTER(ctypes.c_int32), ctypes.c_uint32,
+                                       ctypes.POINTER(ctypes.c_void_p)]),
+    ("tm_engine_replicas", ctypes.c_int, [ctypes.c_void_p]),
+    ("tm_engine_devices", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32), ctypes.c_uint32]),
     ("tm_close", None, [ctypes.c_void_p]),
     ("tm_strerror", ctypes.c_char_p, [ctypes.c_int]),
     ("tm_last_error", ctypes.c_char_p, [ctypes.c_void_p]),
@@ -80,6 +84,10 @@ SIGNATURES = [
     ("tm_match_batch", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
                                       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
                                       c_u64p]),
+    ("tm_match_batch_owned", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p),
+                                            c_u64p]),
+    ("tm_free", None, [ctypes.c_void_p]),
     ("tm_match_batch_device", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
                                              ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                              ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]),

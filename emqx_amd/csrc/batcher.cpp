@@ -12,12 +12,17 @@
 //
 // Submission is striped: a producer thread appends to one of NSTRIPE
 // buffers (its own lock), so thousands of publishers do not serialise on one
-// mutex; a seal takes every stripe.  One worker thread per batcher gathers
-// the stripes into pinned host memory, copies the batch to HBM, runs the
-// stream-ordered device path (tm_match_batch_device, or
-// tm_match_routes_batch_device with TM_BATCHER_ROUTES) and reads the results
-// back with one synchronisation, into pinned memory, sized from the previous
-// batches (a rare overflow is re-read).
+// mutex; a seal takes every stripe.  The sealing thread gathers the stripes
+// into the pinned host memory of a free LANE and hands the batch over; each
+// lane (a thread, a stream and its own pinned / HBM buffers, bound to one of
+// the engine's replicas, lanes_per_replica per GPU) copies its batch to HBM,
+// runs the stream-ordered device path (tm_match_batch_device,
+// tm_match_routes_batch_device, tm_match_deliveries_batch_device), reads back
+// counts, offsets and the total, then exactly `total` ids (no capacity-sized
+// read-back), and runs the batch's callbacks.  So several batches are in
+// flight at once (one per lane: upload, walk and read-back of neighbouring
+// batches overlap, and every GPU of a multi-device engine works), and the
+// callbacks of one batch run on its lane while the next batches proceed.
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
@@ -25,6 +30,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <new>
 #include <thread>
@@ -90,6 +96,22 @@ struct Dev {
     }
 };
 
+// one batch in flight: its requests, pinned staging and device buffers
+struct Lane {
+    int device = -1;
+    hipStream_t stream = nullptr;
+    std::thread th;
+    std::mutex mu;
+    std::condition_variable cv;
+    bool full = false, stop = false;   // a batch has been handed over / shut down
+    uint32_t n = 0;
+    bool oom = false;
+    std::vector<Req> reqs;
+    Pinned h_bytes, h_off, h_counts, h_outoff, h_src, h_dest, h_total;
+    Dev d_bytes, d_off, d_counts, d_outoff, d_src, d_dest, d_total;
+    double ids_per_topic = 64.0;      // sizing estimate of the device result buffers
+};
+
 std::atomic<uint32_t> g_stripe_rr{0};
 thread_local int t_stripe = -1;
 
@@ -98,28 +120,26 @@ thread_local int t_stripe = -1;
 struct tm_batcher {
     tm_engine* eng = nullptr;
     tm_batcher_config cfg{};
-    int device = -1;
-    hipStream_t stream = nullptr;
+    bool host_only = false;
     Stripe stripes[NSTRIPE];
     std::atomic<uint64_t> pending{0}, pending_bytes{0}, next_ticket{1};
     std::atomic<int64_t> first_ns{0};
 
-    std::mutex mu;                    // worker state, stats, wake-ups
-    std::condition_variable cv_work, cv_idle;
-    bool stop = false, busy = false;
+    std::mutex mu;                    // sealer state, stats, wake-ups, lane hand-over
+    std::condition_variable cv_work, cv_idle, cv_lane;
+    bool stop = false;
+    int sealing = 0, in_flight = 0;   // batches being gathered / on lanes
     tm_batcher_stats st{};
     std::thread worker;
+    std::vector<std::unique_ptr<Lane>> lanes;
+    std::vector<int> free_lanes;      // guarded by mu
+    uint64_t rotate = 0;              // first stripe of the next gather (sealer only)
+    uint64_t next_lane = 0;
 
-    // the batch being run (worker only)
-    std::vector<Req> reqs;
     struct Taken {
         std::vector<uint8_t> bytes;
         std::vector<uint32_t> lens;
     } taken[NSTRIPE];
-    Pinned h_bytes, h_off, h_counts, h_outoff, h_src, h_dest, h_total;
-    Dev d_bytes, d_off, d_counts, d_outoff, d_src, d_dest, d_total;
-    double ids_per_topic = 64.0;      // sizing estimate of the result read-back
-    uint64_t rotate = 0;              // first stripe of the next gather
 
     int64_t now_ns() const { return std::chrono::duration_cast<std::chrono::nanoseconds>(clk::now().time_since_epoch()).count(); }
 
@@ -130,13 +150,12 @@ struct tm_batcher {
         return now_ns() - first_ns.load(std::memory_order_acquire) >= (int64_t)cfg.deadline_us * 1000;
     }
 
-    // move every stripe's topics into the pinned batch; returns the count
-    uint32_t gather() {
-        reqs.clear();
+    // move stripes' topics (oldest first, up to max_topics) into lane L's
+    // pinned batch; sets L.n (L.oom when staging memory ran out)
+    void gather(Lane& L) {
+        L.reqs.clear();
+        L.oom = false;
         uint64_t nb = 0, n = 0;
-        // under each stripe's lock: move its topics out, oldest first, up to
-        // max_topics (pending counts them under the same lock, so the
-        // subtraction never underflows)
         const uint64_t cap = cfg.max_topics;
         const int start = (int)(rotate++ % NSTRIPE);   // no stripe starves under overload
         for (int i = 0; i < NSTRIPE && n < cap; ++i) {
@@ -150,7 +169,7 @@ struct tm_batcher {
             if (k == have) {   // the whole stripe
                 t.bytes.swap(x.bytes);
                 t.lens.swap(x.lens);
-                reqs.insert(reqs.end(), x.reqs.begin(), x.reqs.end());
+                L.reqs.insert(L.reqs.end(), x.reqs.begin(), x.reqs.end());
                 x.reqs.clear();
                 x.bytes.clear();
                 x.lens.clear();
@@ -159,7 +178,7 @@ struct tm_batcher {
                 for (size_t i = 0; i < k; ++i) kb += x.lens[i];
                 t.bytes.assign(x.bytes.begin(), x.bytes.begin() + kb);
                 t.lens.assign(x.lens.begin(), x.lens.begin() + k);
-                reqs.insert(reqs.end(), x.reqs.begin(), x.reqs.begin() + k);
+                L.reqs.insert(L.reqs.end(), x.reqs.begin(), x.reqs.begin() + k);
                 x.bytes.erase(x.bytes.begin(), x.bytes.begin() + kb);
                 x.lens.erase(x.lens.begin(), x.lens.begin() + k);
                 x.reqs.erase(x.reqs.begin(), x.reqs.begin() + k);
@@ -171,16 +190,17 @@ struct tm_batcher {
             pending_bytes.fetch_sub(t.bytes.size(), std::memory_order_relaxed);
         }
         // topics left behind keep their first_ns: they are due at once
-        if (device < 0) {   // nothing to stage: the batch fails with TM_EDEVICE
+        L.n = (uint32_t)n;
+        if (host_only || !L.h_bytes.ensure(nb + 16) || !L.h_off.ensure((n + 1) * 8)) {
+            L.oom = !host_only;
             for (auto& t : taken) {
                 t.bytes.clear();
                 t.lens.clear();
             }
-            return (uint32_t)n;
+            return;
         }
-        if (!h_bytes.ensure(nb + 16) || !h_off.ensure((n + 1) * 8)) return UINT32_MAX;
-        uint8_t* hb = (uint8_t*)h_bytes.p;
-        uint64_t* ho = (uint64_t*)h_off.p;
+        uint8_t* hb = (uint8_t*)L.h_bytes.p;
+        uint64_t* ho = (uint64_t*)L.h_off.p;
         uint64_t o = 0, k = 0;
         ho[0] = 0;
         for (int i = 0; i < NSTRIPE; ++i) {   // same stripe order as reqs
@@ -193,103 +213,127 @@ struct tm_batcher {
             t.bytes.clear();
             t.lens.clear();
         }
-        return (uint32_t)n;
     }
 
-    int run_device(uint32_t n, uint64_t nbytes, bool routes, bool deliv, uint64_t& total) {
+    // the lane's batch on its GPU; results in the lane's pinned buffers
+    int run_device(Lane& L, bool routes, bool deliv, uint64_t& total) {
         auto chk = [](hipError_t e) { return e == hipSuccess; };
-        if (!d_bytes.ensure(nbytes + 16) || !d_off.ensure((n + 1) * 8) || !d_counts.ensure(n * 4 + 4) ||
-            !d_outoff.ensure((n + 1) * 8) || !d_total.ensure(64) || !h_counts.ensure(n * 4 + 4) ||
-            !h_outoff.ensure((n + 1) * 8) || !h_total.ensure(64))
+        const uint32_t n = L.n;
+        const uint64_t nbytes = ((const uint64_t*)L.h_off.p)[n];
+        if (!L.d_bytes.ensure(nbytes + 16) || !L.d_off.ensure((n + 1) * 8) || !L.d_counts.ensure(n * 4 + 4) ||
+            !L.d_outoff.ensure((n + 1) * 8) || !L.d_total.ensure(64) || !L.h_counts.ensure(n * 4 + 4) ||
+            !L.h_outoff.ensure((n + 1) * 8) || !L.h_total.ensure(64))
             return TM_ENOMEM;
-        uint64_t cap = (uint64_t)(ids_per_topic * n * 1.25) + 1024;
+        hipStream_t s = L.stream;
+        if (!chk(hipMemcpyAsync(L.d_bytes.p, L.h_bytes.p, nbytes, hipMemcpyHostToDevice, s)) ||
+            !chk(hipMemcpyAsync(L.d_off.p, L.h_off.p, (n + 1) * 8, hipMemcpyHostToDevice, s)))
+            return TM_EDEVICE;
+        uint64_t cap = (uint64_t)(L.ids_per_topic * n * 1.25) + 1024;
         for (int pass = 0; pass < 2; ++pass) {
-            if (!d_src.ensure(cap * 4) || !h_src.ensure(cap * 4) ||
-                (routes && (!d_dest.ensure(cap * 4) || !h_dest.ensure(cap * 4))))
-                return TM_ENOMEM;
-            if (!chk(hipMemcpyAsync(d_bytes.p, h_bytes.p, nbytes, hipMemcpyHostToDevice, stream)) ||
-                !chk(hipMemcpyAsync(d_off.p, h_off.p, (n + 1) * 8, hipMemcpyHostToDevice, stream)))
-                return TM_EDEVICE;
-            int rc = deliv ? tm_match_deliveries_batch_device(eng, (const uint8_t*)d_bytes.p, (const uint64_t*)d_off.p,
-                                                              n, nbytes, (uint32_t*)d_counts.p, (uint64_t*)d_outoff.p,
-                                                              (uint32_t*)d_src.p, (uint32_t*)d_dest.p, cap,
-                                                              (uint64_t*)d_total.p, stream)
-                     : routes ? tm_match_routes_batch_device(eng, (const uint8_t*)d_bytes.p, (const uint64_t*)d_off.p, n,
-                                                           nbytes, (uint32_t*)d_counts.p, (uint64_t*)d_outoff.p,
-                                                           (uint32_t*)d_src.p, (uint32_t*)d_dest.p, cap,
-                                                           (uint64_t*)d_total.p, stream)
-                            : tm_match_batch_device(eng, (const uint8_t*)d_bytes.p, (const uint64_t*)d_off.p, n,
-                                                    nbytes, (uint32_t*)d_counts.p, (uint64_t*)d_outoff.p,
-                                                    (uint32_t*)d_src.p, cap, (uint64_t*)d_total.p, stream);
+            if (!L.d_src.ensure(cap * 4) || (routes && !L.d_dest.ensure(cap * 4))) return TM_ENOMEM;
+            int rc = deliv ? tm_match_deliveries_batch_device(eng, (const uint8_t*)L.d_bytes.p, (const uint64_t*)L.d_off.p,
+                                                              n, nbytes, (uint32_t*)L.d_counts.p, (uint64_t*)L.d_outoff.p,
+                                                              (uint32_t*)L.d_src.p, (uint32_t*)L.d_dest.p, cap,
+                                                              (uint64_t*)L.d_total.p, s)
+                     : routes ? tm_match_routes_batch_device(eng, (const uint8_t*)L.d_bytes.p, (const uint64_t*)L.d_off.p, n,
+                                                           nbytes, (uint32_t*)L.d_counts.p, (uint64_t*)L.d_outoff.p,
+                                                           (uint32_t*)L.d_src.p, (uint32_t*)L.d_dest.p, cap,
+                                                           (uint64_t*)L.d_total.p, s)
+                            : tm_match_batch_device(eng, (const uint8_t*)L.d_bytes.p, (const uint64_t*)L.d_off.p, n,
+                                                    nbytes, (uint32_t*)L.d_counts.p, (uint64_t*)L.d_outoff.p,
+                                                    (uint32_t*)L.d_src.p, cap, (uint64_t*)L.d_total.p, s);
             if (rc != TM_OK) return rc;
-            // results up to cap in the same synchronisation
-            if (!chk(hipMemcpyAsync(h_total.p, d_total.p, 8, hipMemcpyDeviceToHost, stream)) ||
-                !chk(hipMemcpyAsync(h_counts.p, d_counts.p, n * 4, hipMemcpyDeviceToHost, stream)) ||
-                !chk(hipMemcpyAsync(h_outoff.p, d_outoff.p, (n + 1) * 8, hipMemcpyDeviceToHost, stream)) ||
-                !chk(hipMemcpyAsync(h_src.p, d_src.p, cap * 4, hipMemcpyDeviceToHost, stream)) ||
-                (routes && !chk(hipMemcpyAsync(h_dest.p, d_dest.p, cap * 4, hipMemcpyDeviceToHost, stream))) ||
-                !chk(hipStreamSynchronize(stream)))
+            // the total, counts and offsets first: the list read-back is sized by them
+            if (!chk(hipMemcpyAsync(L.h_total.p, L.d_total.p, 8, hipMemcpyDeviceToHost, s)) ||
+                !chk(hipMemcpyAsync(L.h_counts.p, L.d_counts.p, n * 4, hipMemcpyDeviceToHost, s)) ||
+                !chk(hipMemcpyAsync(L.h_outoff.p, L.d_outoff.p, (n + 1) * 8, hipMemcpyDeviceToHost, s)) ||
+                !chk(hipStreamSynchronize(s)))
                 return TM_EDEVICE;
-            total = *(const uint64_t*)h_total.p;
-            ids_per_topic = 0.9 * ids_per_topic + 0.1 * ((double)total / n);
-            if (total <= cap) return TM_OK;
+            total = *(const uint64_t*)L.h_total.p;
+            L.ids_per_topic = 0.9 * L.ids_per_topic + 0.1 * ((double)total / n);
+            if (total <= cap) break;
             cap = total + total / 4 + 1024;   // overflow: rerun with room (rare)
         }
+        if (!L.h_src.ensure(total * 4 + 4) || (routes && !L.h_dest.ensure(total * 4 + 4))) return TM_ENOMEM;
+        if ((total && !chk(hipMemcpyAsync(L.h_src.p, L.d_src.p, total * 4, hipMemcpyDeviceToHost, s))) ||
+            (total && routes && !chk(hipMemcpyAsync(L.h_dest.p, L.d_dest.p, total * 4, hipMemcpyDeviceToHost, s))) ||
+            !chk(hipStreamSynchronize(s)))
+            return TM_EDEVICE;
         return TM_OK;
     }
 
-    void run() {
-        const uint32_t n = gather();
+    // lane worker: run handed-over batches and their callbacks
+    void lane_loop(Lane& L, int idx) {
+        if (L.device >= 0) (void)hipSetDevice(L.device);
         const bool deliv = (cfg.flags & TM_BATCHER_DELIVERIES) != 0;
         const bool routes = deliv || (cfg.flags & TM_BATCHER_ROUTES) != 0;
-        uint64_t total = 0;
-        int rc = n == UINT32_MAX ? TM_ENOMEM : TM_OK;
-        if (rc == TM_OK && n) {
-            if (device < 0) {
-                rc = TM_EDEVICE;   // host-only engine: the match path runs on the GPU only
-            } else {
-                (void)hipSetDevice(device);
-                rc = run_device(n, ((uint64_t*)h_off.p)[n], routes, deliv, total);
-                if (rc == TM_OK && deliv) {   // lists sit at route offsets: count the entries
-                    total = 0;
-                    for (uint32_t i = 0; i < n; ++i) total += ((const uint32_t*)h_counts.p)[i];
-                }
+        for (;;) {
+            {
+                std::unique_lock<std::mutex> lk(L.mu);
+                L.cv.wait(lk, [&] { return L.full || L.stop; });
+                if (!L.full) return;
             }
-        }
-        const uint32_t m = rc == TM_ENOMEM && n == UINT32_MAX ? (uint32_t)reqs.size() : n;
-        {
+            const uint32_t n = L.n;
+            uint64_t total = 0, results = 0;
+            int rc = L.oom ? TM_ENOMEM : host_only ? TM_EDEVICE : TM_OK;   // host-only: the GPU path only
+            if (rc == TM_OK && n) {
+                rc = run_device(L, routes, deliv, total);
+                if (rc == TM_OK)   // deliveries sit at route offsets: count the entries
+                    for (uint32_t i = 0; i < n; ++i) results += ((const uint32_t*)L.h_counts.p)[i];
+            }
+            const uint32_t* cnt = (const uint32_t*)L.h_counts.p;
+            const uint64_t* off = (const uint64_t*)L.h_outoff.p;
+            const uint32_t* src = (const uint32_t*)L.h_src.p;
+            const uint32_t* dst = (const uint32_t*)L.h_dest.p;
+            const uint32_t m = (uint32_t)L.reqs.size();
+            for (uint32_t i = 0; i < m; ++i) {   // one batch's callbacks in submission order
+                const Req& r = L.reqs[i];
+                if (rc == TM_OK)
+                    r.fn(r.ctx, r.ticket, TM_OK, src + off[i], routes ? dst + off[i] : nullptr, cnt[i]);
+                else
+                    r.fn(r.ctx, r.ticket, rc, nullptr, nullptr, 0);
+            }
+            L.reqs.clear();
+            {
+                std::lock_guard<std::mutex> lk(L.mu);
+                L.full = false;
+            }
             std::lock_guard<std::mutex> lk(mu);
             st.batches++;
             st.topics += m;
             if (m > st.max_batch) st.max_batch = m;
-            if (rc == TM_OK) st.results += total;
+            if (rc == TM_OK) st.results += results;
             else st.failed_batches++;
+            free_lanes.push_back(idx);
+            --in_flight;
+            cv_lane.notify_all();
+            cv_idle.notify_all();
         }
-        const uint32_t* cnt = (const uint32_t*)h_counts.p;
-        const uint64_t* off = (const uint64_t*)h_outoff.p;
-        const uint32_t* src = (const uint32_t*)h_src.p;
-        const uint32_t* dst = (const uint32_t*)h_dest.p;
-        for (uint32_t i = 0; i < m; ++i) {
-            const Req& r = reqs[i];
-            if (rc == TM_OK)
-                r.fn(r.ctx, r.ticket, TM_OK, src + off[i], routes ? dst + off[i] : nullptr, cnt[i]);
-            else
-                r.fn(r.ctx, r.ticket, rc, nullptr, nullptr, 0);
-        }
-        reqs.clear();
     }
 
     void loop() {
         std::unique_lock<std::mutex> lk(mu);
         for (;;) {
             if (due()) {
-                busy = true;
+                // a free lane (every lane busy: the sealed batch waits, and
+                // keeps filling to max_topics meanwhile)
+                cv_lane.wait(lk, [&] { return !free_lanes.empty(); });
+                const int li = free_lanes.back();
+                free_lanes.pop_back();
                 if (pending.load() >= cfg.max_topics) st.size_seals++;
                 else st.deadline_seals++;
+                ++sealing;
                 lk.unlock();
-                run();
+                Lane& L = *lanes[li];
+                gather(L);
+                {
+                    std::lock_guard<std::mutex> l2(L.mu);
+                    L.full = true;
+                }
+                L.cv.notify_one();
                 lk.lock();
-                busy = false;
+                --sealing;
+                ++in_flight;
                 continue;
             }
             if (pending.load(std::memory_order_acquire) == 0) {
@@ -315,6 +359,21 @@ struct tm_batcher {
         std::lock_guard<std::mutex> lk(mu);
         cv_work.notify_one();
     }
+
+    void shutdown_lanes() {
+        for (auto& L : lanes) {
+            {
+                std::lock_guard<std::mutex> lk(L->mu);
+                L->stop = true;
+            }
+            L->cv.notify_all();
+            if (L->th.joinable()) L->th.join();
+            if (L->stream) {
+                (void)hipSetDevice(L->device);
+                (void)hipStreamDestroy(L->stream);
+            }
+        }
+    }
 };
 
 extern "C" {
@@ -328,18 +387,39 @@ int tm_batcher_open(tm_engine* e, const tm_batcher_config* cfg, tm_batcher** out
     if (b->cfg.max_topics == 0) b->cfg.max_topics = 65536;
     if (b->cfg.max_bytes == 0) b->cfg.max_bytes = 64ull << 20;
     if (b->cfg.deadline_us == 0) b->cfg.deadline_us = 200;
-    b->device = tm_engine_device(e);
-    if (b->device >= 0) {
-        if (hipSetDevice(b->device) != hipSuccess ||
-            hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking) != hipSuccess) {
+    const uint32_t per = b->cfg.lanes_per_replica ? b->cfg.lanes_per_replica : 2u;
+    const int R = tm_engine_replicas(e);
+    b->host_only = R == 0;
+    std::vector<int32_t> devs(R > 0 ? R : 1, -1);
+    if (R > 0 && tm_engine_devices(e, devs.data(), (uint32_t)R) != R) {
+        delete b;
+        return TM_EDEVICE;
+    }
+    // lanes round-robin over the replicas: lane k on replica k % R
+    for (uint32_t k = 0; k < per * (uint32_t)devs.size(); ++k) {
+        std::unique_ptr<Lane> L(new (std::nothrow) Lane());
+        if (!L) {
+            b->shutdown_lanes();
+            delete b;
+            return TM_ENOMEM;
+        }
+        L->device = devs[k % devs.size()];
+        if (L->device >= 0 && (hipSetDevice(L->device) != hipSuccess ||
+                               hipStreamCreateWithFlags(&L->stream, hipStreamNonBlocking) != hipSuccess)) {
+            b->shutdown_lanes();
             delete b;
             return TM_EDEVICE;
         }
+        b->lanes.push_back(std::move(L));
     }
     try {
+        for (size_t k = 0; k < b->lanes.size(); ++k) {
+            b->free_lanes.push_back((int)(b->lanes.size() - 1 - k));   // lane 0 first
+            b->lanes[k]->th = std::thread([b, k] { b->lane_loop(*b->lanes[k], (int)k); });
+        }
         b->worker = std::thread([b] { b->loop(); });
     } catch (...) {
-        if (b->stream) (void)hipStreamDestroy(b->stream);
+        b->shutdown_lanes();
         delete b;
         return TM_ENOMEM;
     }
@@ -378,7 +458,7 @@ int tm_batcher_flush(tm_batcher* b) {
     // everything submitted before this call completes: force the deadline now
     b->first_ns.store(0, std::memory_order_release);
     b->cv_work.notify_one();
-    b->cv_idle.wait(lk, [b] { return b->pending.load() == 0 && !b->busy; });
+    b->cv_idle.wait(lk, [b] { return b->pending.load() == 0 && b->sealing == 0 && b->in_flight == 0; });
     return TM_OK;
 }
 
@@ -398,7 +478,7 @@ void tm_batcher_close(tm_batcher* b) {
         b->cv_work.notify_all();
     }
     if (b->worker.joinable()) b->worker.join();
-    if (b->stream) (void)hipStreamDestroy(b->stream);
+    b->shutdown_lanes();
     delete b;
 }
 

@@ -5,7 +5,8 @@
  * this image has no Erlang runtime.  The Erlang wrapper that loads it is in
  * INTEGRATION.md.
  *
- *   emqx_trie_nif:open(Device)                -> {ok, Engine} | {error, Reason}
+ *   emqx_trie_nif:open(Device | [Device])     -> {ok, Engine} | {error, Reason}
+ *                                     (a list opens one engine across those GPUs: tm_open_devices)
  *   emqx_trie_nif:insert(Engine, Filter)      -> ok          emqx_trie:insert/1  (src/emqx_trie.erl:62-73)
  *   emqx_trie_nif:delete(Engine, Filter)      -> ok          emqx_trie:delete/1  (src/emqx_trie.erl:88-96)
  *   emqx_trie_nif:lookup(Engine, NodeId)      -> [] | [{EdgeCount, Topic | undefined}]
@@ -29,7 +30,12 @@
  *
  * Conventions: bad input -> badarg; engine errors ->
  * {error, Atom}; the engine handle is a resource; GPU calls run on dirty IO
- * schedulers so a batch never blocks a normal scheduler.
+ * schedulers so a batch never blocks a normal scheduler.  The engine
+ * serialises its own calls, so the NIF holds no lock of its own: a match
+ * builds its reply terms while other calls proceed.  The module supports
+ * hot code upgrade (the resource type is taken over by the new version).
+ * The Erlang side is in erlang/ (emqx_trie_nif.erl, emqx_trie_gpu.erl,
+ * emqx_trie_gpu_feed.erl).
  */
 #include <erl_nif.h>
 #include <string.h>
@@ -40,7 +46,6 @@ static ErlNifResourceType* ENGINE_RT = NULL;
 
 typedef struct {
     tm_engine* e;
-    ErlNifMutex* mu;
     tm_batcher* filters_b;   /* micro-batcher for match_async (emqx_trie:match/1)          */
     tm_batcher* routes_b;    /* micro-batcher for match_routes_async (match_routes/1)      */
     tm_batcher* deliv_b;     /* micro-batcher for match_deliveries_async (aggre/1)         */
@@ -81,14 +86,28 @@ static void engine_dtor(ErlNifEnv* env, void* obj) {
     if (r->routes_b) tm_batcher_close(r->routes_b);
     if (r->deliv_b) tm_batcher_close(r->deliv_b);
     if (r->e) tm_close(r->e);
-    if (r->mu) enif_mutex_destroy(r->mu);
+}
+
+static int open_rt(ErlNifEnv* env, ErlNifResourceFlags flags) {
+    ErlNifResourceType* rt = enif_open_resource_type(env, NULL, "tm_engine", engine_dtor, flags, NULL);
+    if (!rt) return -1;
+    ENGINE_RT = rt;
+    return 0;
 }
 
 static int load(ErlNifEnv* env, void** priv, ERL_NIF_TERM info) {
     (void)priv;
     (void)info;
-    ENGINE_RT = enif_open_resource_type(env, NULL, "tm_engine", engine_dtor, ERL_NIF_RT_CREATE, NULL);
-    return ENGINE_RT ? 0 : -1;
+    return open_rt(env, ERL_NIF_RT_CREATE);
+}
+
+/* hot code upgrade: the new module version takes over the resource type, so
+ * engines opened by the old version stay valid */
+static int upgrade(ErlNifEnv* env, void** priv, void** old_priv, ERL_NIF_TERM info) {
+    (void)priv;
+    (void)old_priv;
+    (void)info;
+    return open_rt(env, ERL_NIF_RT_CREATE | ERL_NIF_RT_TAKEOVER);
 }
 
 static int get_engine(ErlNifEnv* env, ERL_NIF_TERM t, engine_res** out) {
@@ -96,16 +115,27 @@ static int get_engine(ErlNifEnv* env, ERL_NIF_TERM t, engine_res** out) {
 }
 
 static ERL_NIF_TERM nif_open(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    int32_t devs[TM_MAX_REPLICAS];
+    unsigned nd = 0;
     int dev;
-    if (argc != 1 || !enif_get_int(env, argv[0], &dev)) return enif_make_badarg(env);
+    if (argc != 1) return enif_make_badarg(env);
+    if (enif_get_int(env, argv[0], &dev)) {
+        devs[nd++] = dev;
+    } else {   /* [Device]: one engine over those GPUs */
+        ERL_NIF_TERM head, tail = argv[0];
+        if (!enif_is_list(env, tail)) return enif_make_badarg(env);
+        while (enif_get_list_cell(env, tail, &head, &tail)) {
+            if (nd == TM_MAX_REPLICAS || !enif_get_int(env, head, &dev)) return enif_make_badarg(env);
+            devs[nd++] = dev;
+        }
+    }
     tm_config cfg;
     memset(&cfg, 0, sizeof(cfg));
-    cfg.device = dev;
+    cfg.device = nd ? devs[0] : -1;
     engine_res* r = (engine_res*)enif_alloc_resource(ENGINE_RT, sizeof(engine_res));
     r->e = NULL;
     r->filters_b = r->routes_b = r->deliv_b = NULL;
-    r->mu = enif_mutex_create("tm_engine");
-    int rc = tm_open(&cfg, &r->e);
+    int rc = tm_open_devices(&cfg, devs, nd, &r->e);
     if (rc == TM_OK) {
         /* batches sealed at 64K topics or 200 us after their first topic */
         tm_batcher_config bc;
@@ -130,9 +160,7 @@ static ERL_NIF_TERM nif_filter_op(ErlNifEnv* env, int argc, const ERL_NIF_TERM a
     ErlNifBinary b;
     if (argc != 2 || !get_engine(env, argv[0], &r) || !enif_inspect_binary(env, argv[1], &b))
         return enif_make_badarg(env);
-    enif_mutex_lock(r->mu);
     int rc = is_insert ? tm_insert(r->e, b.data, (uint32_t)b.size) : tm_delete(r->e, b.data, (uint32_t)b.size);
-    enif_mutex_unlock(r->mu);
     return rc == TM_OK ? atom(env, "ok") : error_tuple(env, rc);
 }
 
@@ -181,7 +209,6 @@ static ERL_NIF_TERM nif_lookup(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv
     if (argc != 2 || !get_engine(env, argv[0], &r) || !enif_inspect_binary(env, argv[1], &b))
         return enif_make_badarg(env);
     tm_node_info info;
-    enif_mutex_lock(r->mu);
     int rc = tm_lookup(r->e, b.data, (uint32_t)b.size, &info);
     ERL_NIF_TERM res;
     if (rc == TM_ENOENT) {
@@ -193,7 +220,6 @@ static ERL_NIF_TERM nif_lookup(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv
                                                              : filter_binary(env, r->e, info.filter_id);
         res = enif_make_list1(env, enif_make_tuple2(env, enif_make_uint(env, info.edge_count), topic));
     }
-    enif_mutex_unlock(r->mu);
     return res;
 }
 
@@ -201,9 +227,7 @@ static ERL_NIF_TERM nif_commit(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv
     engine_res* r;
     if (argc != 1 || !get_engine(env, argv[0], &r)) return enif_make_badarg(env);
     uint64_t epoch = 0;
-    enif_mutex_lock(r->mu);
     int rc = tm_commit(r->e, &epoch);
-    enif_mutex_unlock(r->mu);
     if (rc != TM_OK) return error_tuple(env, rc);
     return enif_make_tuple2(env, atom(env, "ok"), enif_make_uint64(env, epoch));
 }
@@ -230,16 +254,10 @@ static ERL_NIF_TERM match_list(ErlNifEnv* env, engine_res* r, ERL_NIF_TERM list,
     }
     uint32_t* counts = (uint32_t*)enif_alloc(sizeof(uint32_t) * (n ? n : 1));
     uint64_t* out_off = (uint64_t*)enif_alloc(sizeof(uint64_t) * (n + 1));
-    uint64_t cap = (uint64_t)n * 32 + 64, need = 0;
-    uint32_t* ids = (uint32_t*)enif_alloc(sizeof(uint32_t) * cap);
-    enif_mutex_lock(r->mu);
-    int rc = tm_match_batch(r->e, buf, off, n, counts, out_off, ids, cap, &need);
-    if (rc == TM_ENOSPC) {
-        enif_free(ids);
-        cap = need;
-        ids = (uint32_t*)enif_alloc(sizeof(uint32_t) * (cap ? cap : 1));
-        rc = tm_match_batch(r->e, buf, off, n, counts, out_off, ids, cap, &need);
-    }
+    uint32_t* ids = NULL;
+    uint64_t total = 0;
+    /* the library sizes the id array at the exact total: one walk per batch */
+    int rc = tm_match_batch_owned(r->e, buf, off, n, counts, out_off, &ids, &total);
     ERL_NIF_TERM res;
     if (rc != TM_OK) {
         res = error_tuple(env, rc);
@@ -255,8 +273,7 @@ static ERL_NIF_TERM match_list(ErlNifEnv* env, engine_res* r, ERL_NIF_TERM list,
         res = single ? rows[0] : enif_make_list_from_array(env, rows, n);
         enif_free(rows);
     }
-    enif_mutex_unlock(r->mu);
-    enif_free(ids);
+    tm_free(ids);
     enif_free(out_off);
     enif_free(counts);
     enif_free(buf);
@@ -367,9 +384,7 @@ static ERL_NIF_TERM nif_dest_target(ErlNifEnv* env, int argc, const ERL_NIF_TERM
     if (enif_is_identical(argv[2], atom(env, "node"))) kind = TM_TARGET_NODE;
     else if (enif_is_identical(argv[2], atom(env, "group"))) kind = TM_TARGET_GROUP;
     else return enif_make_badarg(env);
-    enif_mutex_lock(r->mu);
     int rc = tm_dest_target(r->e, d.data, (uint32_t)d.size, kind, k.data, (uint32_t)k.size, NULL);
-    enif_mutex_unlock(r->mu);
     return rc == TM_OK ? atom(env, "ok") : error_tuple(env, rc);
 }
 
@@ -379,10 +394,8 @@ static ERL_NIF_TERM nif_route_op(ErlNifEnv* env, int argc, const ERL_NIF_TERM ar
     if (argc != 3 || !get_engine(env, argv[0], &r) || !enif_inspect_binary(env, argv[1], &t) ||
         !enif_inspect_binary(env, argv[2], &d))
         return enif_make_badarg(env);
-    enif_mutex_lock(r->mu);
     int rc = add ? tm_route_add(r->e, t.data, (uint32_t)t.size, d.data, (uint32_t)d.size)
                  : tm_route_del(r->e, t.data, (uint32_t)t.size, d.data, (uint32_t)d.size);
-    enif_mutex_unlock(r->mu);
     return rc == TM_OK ? atom(env, "ok") : error_tuple(env, rc);
 }
 static ERL_NIF_TERM nif_route_add(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
@@ -408,4 +421,4 @@ static ErlNifFunc funcs[] = {
     {"route_del", 3, nif_route_del, 0},
 };
 
-ERL_NIF_INIT(emqx_trie_nif, funcs, load, NULL, NULL, NULL)
+ERL_NIF_INIT(emqx_trie_nif, funcs, load, NULL, upgrade, NULL)

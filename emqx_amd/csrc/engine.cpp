@@ -19,12 +19,17 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <condition_variable>
 #include <cstring>
+#include <functional>
+#include <memory>
 #include <mutex>
 #include <new>
+#include <thread>
 #include <stdexcept>
 #include <string>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "../../include/topicmatch.h"
@@ -140,12 +145,101 @@ struct KTimes {
 };
 constexpr int N_KERNEL_SLOTS = 4;   // tokenize, walk, scan, copy_out
 
+// per-batch device workspace: consecutive batches rotate over the slots, so
+// batches issued on different streams overlap on the GPU (the walk of one
+// beside the tokenizer / copy-out of its neighbours); a slot's next user
+// waits for its previous batch (hipStreamWaitEvent)
+struct Slot {
+    DevBuf twords, words, path, meta, scan, stage, kstage, ws, stats, perm;
+    uint64_t* h_maxc = nullptr;     // pinned: largest match count of the slot's last walk
+    hipEvent_t maxc_ev = nullptr, done = nullptr;
+    bool maxc_pending = false, used = false, keyed = false;
+    // the slot's last batch, for a re-copy into a larger output (no re-walk)
+    uint32_t n = 0, K = 0, kw = 1;
+    const uint8_t* bytes = nullptr;
+    const uint64_t* off = nullptr;
+    const uint32_t* counts = nullptr;
+    const uint64_t* out_off = nullptr;
+};
+constexpr int MAX_SLOTS = 4;
+
+// One device replica: the committed image (trie, dictionary, route and aggre
+// tables) in that GPU's HBM, its stream and its workspaces.  An engine has
+// one replica per GPU it was opened on (tm_open_devices); they all mirror the
+// one host trie, so a batch can be cut across them with no collective.
+struct DevState {
+    int device = -1;
+    hipStream_t stream = nullptr;
+    // trie image + dictionary
+    DevBuf d_nodes, d_edges, d_hedges, d_dict, d_arena, d_woff, d_inner, d_leaf;
+    size_t arena_uploaded = 0, woff_uploaded = 0;
+    bool split_stale = true;
+    // route image (emqx_route) and aggre tables
+    DevBuf d_fr_meta, d_fr_dest, d_ex_slots, d_ex_arena, d_ex_dest, d_ex_rank, d_dt, d_rank_src, d_rank_tg;
+    // workspaces: route / aggre (w_r*, w_d*, w_a*), host-buffer batches, merge
+    DevBuf w_rexact, w_rscan, w_rids, w_rcounts, w_roff;
+    DevBuf w_dsrc, w_dcount, w_akey, w_alarge;
+    DevBuf w_mpre, w_mscan, w_bytes, w_off, w_counts, w_outoff, w_ids, w_total;
+    // the route / aggre workspaces and images are shared by every stream:
+    // rw_done is recorded after the last route or aggre kernel of a batch;
+    // the host waits on it before the next batch reuses (or reallocates) the
+    // workspaces and before it rewrites an image
+    hipEvent_t rw_done = nullptr;
+    bool rw_used = false;
+    Slot slots[MAX_SLOTS];
+    int next_slot = 0, last_slot = 0;
+    uint32_t stage_k = 512;   // ids staged per topic before a re-walk (rows are written sparsely: footprint, not traffic)
+    // per-batch event records, accumulated until tm_last_kernel_times()
+    std::vector<KTimes> ev_pool;          // recycled events
+    std::vector<KTimes> ev_pending;       // recorded, not yet read
+    KTimes ev_cur[N_KERNEL_SLOTS];
+    tm_batch_stats stats{};               // counters of this replica's last stats-mode batch
+
+    void rw_release(hipStream_t st) {
+        if (!rw_done) HIPCHK(hipEventCreateWithFlags(&rw_done, hipEventDisableTiming));
+        HIPCHK(hipEventRecord(rw_done, st));
+        rw_used = true;
+    }
+    void rw_drain() {   // host: every route / aggre kernel issued so far has finished
+        if (rw_used) HIPCHK(hipEventSynchronize(rw_done));
+    }
+    void wait_matches() {
+        for (Slot& w : slots)
+            if (w.used) HIPCHK(hipEventSynchronize(w.done));
+    }
+    void release() {
+        (void)hipSetDevice(device);
+        if (stream) (void)hipStreamSynchronize(stream);
+        if (rw_done) (void)hipEventDestroy(rw_done);
+        for (DevBuf* b : {&d_nodes, &d_edges, &d_hedges, &d_dict, &d_arena, &d_woff, &d_inner, &d_leaf, &d_fr_meta,
+                          &d_fr_dest, &d_ex_slots, &d_ex_arena, &d_ex_dest, &d_ex_rank, &d_dt, &d_rank_src,
+                          &d_rank_tg, &w_rexact, &w_rscan, &w_rids, &w_rcounts, &w_roff, &w_dsrc, &w_dcount, &w_akey,
+                          &w_alarge, &w_mpre, &w_mscan, &w_bytes, &w_off, &w_counts, &w_outoff, &w_ids, &w_total})
+            b->release();
+        for (auto& w : slots) {
+            for (DevBuf* b : {&w.twords, &w.words, &w.path, &w.meta, &w.scan, &w.stage, &w.kstage, &w.ws, &w.stats,
+                              &w.perm})
+                b->release();
+            if (w.done) (void)hipEventDestroy(w.done);
+            if (w.maxc_ev) (void)hipEventDestroy(w.maxc_ev);
+            if (w.h_maxc) (void)hipHostFree(w.h_maxc);
+        }
+        for (auto* v : {&ev_pool, &ev_pending})
+            for (auto& k : *v) {
+                (void)hipEventDestroy(k.a);
+                (void)hipEventDestroy(k.b);
+            }
+        if (stream) (void)hipStreamDestroy(stream);
+        stream = nullptr;
+    }
+};
+
 }  // namespace
 
 struct tm_engine {
     std::recursive_mutex mu;
-    int device = -1;
-    hipStream_t stream = nullptr;
+    int device = -1;                  // first replica's HIP ordinal (-1: host-only engine)
+    std::vector<std::unique_ptr<DevState>> devs;   // one replica per GPU (tm_open_devices)
     std::string last_error;
     uint64_t epoch = 0;
 
@@ -184,8 +278,7 @@ struct tm_engine {
     std::vector<uint32_t> free_filters;
     size_t live_filters = 0;
 
-    // ---- device image ----
-    DevBuf d_nodes, d_edges, d_hedges, d_dict, d_arena, d_woff;
+    // ---- device image (per replica: DevState) ----
     bool dev_dirty = true;
     int hist_enabled = 0;             // option "hist": per-level histogram in stats mode (diagnostic, slow)
     uint32_t walk_bpc = 0;            // option "walk_bpc": walk blocks per CU (0 = full occupancy)
@@ -203,36 +296,27 @@ struct tm_engine {
                                       // bit 2 = heat order (heat_sort); bit 3 = heat from filter counts
     bool force_relayout = false;
     int split_halves = 1;             // option "split": walk reads separate inner / leaf half arrays
-    bool split_stale = true;
-    DevBuf d_inner, d_leaf;
 
     // ---- route table: the emqx_route bag (src/emqx_router.erl:52-59) ----
     std::unordered_map<std::string, uint32_t> dest_index;   // dest bytes -> dest id
     std::vector<std::string> dest_names;
     std::unordered_map<std::string, std::vector<uint32_t>> route_bag;   // topic -> dests, insertion order
+    // membership index of the bags past BAG_INDEX_MIN dests (a bag is scanned
+    // linearly below that): add/del of a route stay O(1) probes for topics
+    // with tens of thousands of dests
+    static constexpr size_t BAG_INDEX_MIN = 32;
+    std::unordered_map<std::string, std::unordered_set<uint32_t>> bag_index;
+    bool bag_has(const std::string& key, const std::vector<uint32_t>& bag, uint32_t dest) const {
+        if (bag.size() < BAG_INDEX_MIN) return std::find(bag.begin(), bag.end(), dest) != bag.end();
+        auto ix = bag_index.find(key);
+        return ix != bag_index.end() && ix->second.count(dest);
+    }
     size_t route_total = 0;
     bool routes_dirty = true;         // the route image must be rebuilt at commit
-    DevBuf d_fr_meta, d_fr_dest, d_ex_slots, d_ex_arena, d_ex_dest;
     std::vector<uint32_t> h_fr_off;   // host copy of fr_meta's offsets (aggre rewrites the ranks)
     uint64_t ex_slot_mask = 0;
     uint32_t fr_filters = 0;          // filter ids covered by fr_meta
     bool route_image = false;
-    DevBuf w_rexact, w_rscan, w_rids, w_rcounts, w_roff;
-    // the route / aggre workspaces (w_r*, w_d*, w_a*) and images are shared by
-    // every stream: rw_done is recorded after the last route or aggre kernel
-    // of a batch; the host waits on it before the next batch reuses (or
-    // reallocates) the workspaces and before it rewrites an image
-    hipEvent_t rw_done = nullptr;
-    bool rw_used = false;
-    void rw_release(hipStream_t st) {
-        if (!rw_done) HIPCHK(hipEventCreateWithFlags(&rw_done, hipEventDisableTiming));
-        HIPCHK(hipEventRecord(rw_done, st));
-        rw_used = true;
-    }
-    void rw_drain() {   // host: every route / aggre kernel issued so far has finished
-        if (rw_used) HIPCHK(hipEventSynchronize(rw_done));
-    }
-
     // ---- emqx_broker:aggre/1 targets (aggre.hip) ----
     // a dest aggregates to a target: a node (atom) or a $share group; targets
     // are interned as kind byte + key bytes, so string order is the Erlang
@@ -244,36 +328,14 @@ struct tm_engine {
     struct AggKey { const std::string* key; uint32_t dest_off; uint32_t fid; };
     std::vector<AggKey> agg_keys;           // route image entries (set by build_route_image)
     bool aggre_dirty = true;
-    DevBuf d_ex_rank, d_dt;
-    DevBuf d_rank_src, d_rank_tg;           // inverse ranks: to_rank -> route source, target rank -> target id
-    DevBuf w_dsrc, w_dcount, w_akey, w_alarge;
 
-    // ---- match workspace ----
-    DevBuf w_mpre, w_mscan, w_bytes, w_off, w_counts, w_outoff, w_ids, w_total;
-    // per-batch device workspace: consecutive batches rotate over `nslots`
-    // slots, so batches issued on different streams overlap on the GPU (the
-    // walk of one beside the tokenizer / copy-out of its neighbours); a
-    // slot's next user waits for its previous batch (hipStreamWaitEvent)
-    struct Slot {
-        DevBuf twords, words, path, meta, scan, stage, kstage, ws, stats, perm;
-        uint64_t* h_maxc = nullptr;     // pinned: largest match count of the slot's last walk
-        hipEvent_t maxc_ev = nullptr, done = nullptr;
-        bool maxc_pending = false, used = false, keyed = false;
-    };
-    static constexpr int MAX_SLOTS = 4;
-    Slot slots[MAX_SLOTS];
-    int nslots = 2, next_slot = 0, last_slot = 0;   // option "slots"
-    uint32_t stage_k = 512;   // TM_STAGE_K: ids staged per topic before a re-walk (rows are
-                              // written sparsely: HBM footprint, not traffic)
-    uint32_t stage_k_min = 512;         // option "stage_k"
+    // ---- batch pipeline knobs ----
+    int nslots = 2;                     // option "slots"
+    uint32_t stage_k_min = 512;         // option "stage_k" (TM_STAGE_K)
     int stage_auto = 1;                 // option "stage_auto": grow K to the largest list seen (no re-walks)
     static constexpr size_t STAGE_BUDGET = 16ull << 30;  // stage-row footprint cap (bytes, of 288 GB HBM)
     bool stats_enabled = false, timing_enabled = false;
     tm_batch_stats last_stats{};
-    // per-batch event records, accumulated until tm_last_kernel_times()
-    std::vector<KTimes> ev_pool;          // recycled events
-    std::vector<KTimes> ev_pending;       // recorded, not yet read
-    KTimes ev_cur[N_KERNEL_SLOTS];
 
     // scratch for words of one filter
     std::vector<uint32_t> tmp_words;
@@ -283,7 +345,7 @@ struct tm_engine {
         if (const char* v = std::getenv("TM_STAGE_K")) {
             long k = std::atol(v);
             if (k >= 4 && k <= 4096 && !(k & 3)) {
-                stage_k = stage_k_min = (uint32_t)k;
+                stage_k_min = (uint32_t)k;
                 stage_auto = 0;
             }
         }
@@ -664,12 +726,14 @@ struct tm_engine {
         const uint32_t dest = intern_dest(d, dlen);
         std::string key(reinterpret_cast<const char*>(t), tlen);
         auto it = route_bag.find(key);
-        if (it != route_bag.end() &&
-            std::find(it->second.begin(), it->second.end(), dest) != it->second.end())
+        if (it != route_bag.end() && bag_has(key, it->second, dest))
             return;   // lists:member(Route, get_routes(Topic)) -> ok
         const bool had = it != route_bag.end() && !it->second.empty();
         if (tm_topic_wildcard(t, tlen) && !had) insert(t, tlen);   // mnesia:wread -> [] -> emqx_trie:insert
-        route_bag[key].push_back(dest);
+        std::vector<uint32_t>& bag = route_bag[key];
+        bag.push_back(dest);
+        if (bag.size() == BAG_INDEX_MIN) bag_index[key].insert(bag.begin(), bag.end());
+        else if (bag.size() > BAG_INDEX_MIN) bag_index[key].insert(dest);
         ++route_total;
         routes_dirty = true;
     }
@@ -682,10 +746,14 @@ struct tm_engine {
         auto it = route_bag.find(std::string(reinterpret_cast<const char*>(t), tlen));
         if (it == route_bag.end()) return;   // [] -> ok
         std::vector<uint32_t>& bag = it->second;
-        auto pos = std::find(bag.begin(), bag.end(), di->second);
-        if (pos == bag.end()) return;        // delete_object of an absent route: no-op
-        const bool last = bag.size() == 1;
-        bag.erase(pos);
+        if (!bag_has(it->first, bag, di->second)) return;   // delete_object of an absent route: no-op
+        bag.erase(std::find(bag.begin(), bag.end(), di->second));
+        if (bag.size() + 1 >= BAG_INDEX_MIN) {
+            auto ix = bag_index.find(it->first);
+            if (bag.size() < BAG_INDEX_MIN) bag_index.erase(ix);
+            else ix->second.erase(di->second);
+        }
+        const bool last = bag.empty();
         --route_total;
         if (last) {
             route_bag.erase(it);
@@ -706,7 +774,10 @@ struct tm_engine {
     // rebuild the route image: per-filter-id dest lists (CSR) and the
     // exact-topic table over every topic with routes
     void build_route_image() {
-        rw_drain();   // no route / aggre kernel may read the image being replaced
+        for (auto& d : devs) {   // no route / aggre kernel may read the image being replaced
+            Guard g(d->device);
+            d->rw_drain();
+        }
         const uint32_t nf = (uint32_t)filters.size();
         std::vector<uint32_t> fr_off(nf + 1, 0);
         std::vector<std::pair<uint32_t, const std::vector<uint32_t>*>> by_fid;
@@ -749,24 +820,25 @@ struct tm_engine {
         for (uint32_t f = 0; f < nf; ++f) fr_off[f + 1] += fr_off[f];
         std::vector<uint32_t> fr_dest(fr_off[nf]);
         for (const auto& x : by_fid) std::copy(x.second->begin(), x.second->end(), fr_dest.begin() + fr_off[x.first]);
-        auto up = [&](DevBuf& b, const void* src, size_t bytes) {
-            b.ensure(std::max<size_t>(bytes, 16));
-            if (bytes) HIPCHK(hipMemcpyAsync(b.p, src, bytes, hipMemcpyHostToDevice, stream));
-        };
-        {
-            std::vector<uint2> meta(fr_off.size());
-            for (size_t f = 0; f < fr_off.size(); ++f) meta[f] = make_uint2(fr_off[f], 0u);
-            up(d_fr_meta, meta.data(), meta.size() * sizeof(uint2));
-            HIPCHK(hipStreamSynchronize(stream));
+        std::vector<uint2> meta(fr_off.size());
+        for (size_t f = 0; f < fr_off.size(); ++f) meta[f] = make_uint2(fr_off[f], 0u);
+        for (auto& dp : devs) {
+            DevState& d = *dp;
+            Guard g(d.device);
+            auto up = [&](DevBuf& b, const void* src, size_t bytes) {
+                b.ensure(std::max<size_t>(bytes, 16));
+                if (bytes) HIPCHK(hipMemcpyAsync(b.p, src, bytes, hipMemcpyHostToDevice, d.stream));
+            };
+            up(d.d_fr_meta, meta.data(), meta.size() * sizeof(uint2));
+            up(d.d_fr_dest, fr_dest.data(), fr_dest.size() * 4);
+            up(d.d_ex_slots, slots.data(), slots.size() * sizeof(ExactSlot));
+            up(d.d_ex_arena, arena.data(), arena.size());
+            up(d.d_ex_dest, ex_dest.data(), ex_dest.size() * 4);
+            HIPCHK(hipStreamSynchronize(d.stream));   // host vectors die here
         }
-        up(d_fr_dest, fr_dest.data(), fr_dest.size() * 4);
-        up(d_ex_slots, slots.data(), slots.size() * sizeof(ExactSlot));
-        up(d_ex_arena, arena.data(), arena.size());
-        up(d_ex_dest, ex_dest.data(), ex_dest.size() * 4);
         ex_slot_mask = cap - 1;
         fr_filters = nf;
         route_image = !route_bag.empty();
-        HIPCHK(hipStreamSynchronize(stream));   // host vectors die here
         h_fr_off.swap(fr_off);
         routes_dirty = false;
     }
@@ -787,7 +859,10 @@ struct tm_engine {
         return id;
     }
     void build_aggre_image() {
-        rw_drain();
+        for (auto& d : devs) {
+            Guard g(d->device);
+            d->rw_drain();
+        }
         const uint32_t nf = fr_filters;
         std::vector<uint32_t> order(agg_keys.size());
         for (uint32_t i = 0; i < order.size(); ++i) order[i] = i;
@@ -824,36 +899,40 @@ struct tm_engine {
             const uint32_t tid = dest_target[d];
             dt[d] = make_uint2(trank[tid], tid | (target_names[tid][0] ? 0x80000000u : 0u));
         }
-        auto up = [&](DevBuf& b, const void* src, size_t bytes) {
-            b.ensure(std::max<size_t>(bytes, 16));
-            if (bytes) HIPCHK(hipMemcpyAsync(b.p, src, bytes, hipMemcpyHostToDevice, stream));
-        };
-        if (!fr_meta.empty()) up(d_fr_meta, fr_meta.data(), fr_meta.size() * sizeof(uint2));
-        up(d_ex_rank, ex_rank.data(), ex_rank.size() * 4);
-        up(d_dt, dt.data(), dt.size() * sizeof(uint2));
-        up(d_rank_src, rank_src.data(), rank_src.size() * 4);
-        up(d_rank_tg, rank_tg.data(), rank_tg.size() * 4);
-        HIPCHK(hipStreamSynchronize(stream));   // host vectors die here
+        for (auto& dp : devs) {
+            DevState& d = *dp;
+            Guard g(d.device);
+            auto up = [&](DevBuf& b, const void* src, size_t bytes) {
+                b.ensure(std::max<size_t>(bytes, 16));
+                if (bytes) HIPCHK(hipMemcpyAsync(b.p, src, bytes, hipMemcpyHostToDevice, d.stream));
+            };
+            if (!fr_meta.empty()) up(d.d_fr_meta, fr_meta.data(), fr_meta.size() * sizeof(uint2));
+            up(d.d_ex_rank, ex_rank.data(), ex_rank.size() * 4);
+            up(d.d_dt, dt.data(), dt.size() * sizeof(uint2));
+            up(d.d_rank_src, rank_src.data(), rank_src.size() * 4);
+            up(d.d_rank_tg, rank_tg.data(), rank_tg.size() * 4);
+            HIPCHK(hipStreamSynchronize(d.stream));   // host vectors die here
+        }
         aggre_dirty = false;
     }
-    AggreView aggre_view() const {
+    static AggreView aggre_view(const DevState& d) {
         AggreView av;
-        av.ex_rank = d_ex_rank.as<const uint32_t>();
-        av.dt = d_dt.as<const uint2>();
-        av.rank_src = d_rank_src.as<const uint32_t>();
-        av.rank_tg = d_rank_tg.as<const uint32_t>();
+        av.ex_rank = d.d_ex_rank.as<const uint32_t>();
+        av.dt = d.d_dt.as<const uint2>();
+        av.rank_src = d.d_rank_src.as<const uint32_t>();
+        av.rank_tg = d.d_rank_tg.as<const uint32_t>();
         return av;
     }
 
-    RouteView route_view() const {
+    RouteView route_view(const DevState& d) const {
         RouteView rv;
-        rv.fr_meta = d_fr_meta.as<const uint2>();
-        rv.fr_dest = d_fr_dest.as<const uint32_t>();
+        rv.fr_meta = d.d_fr_meta.as<const uint2>();
+        rv.fr_dest = d.d_fr_dest.as<const uint32_t>();
         rv.n_filters = route_image ? fr_filters : 0u;
-        rv.ex_slots = route_image ? d_ex_slots.as<const ExactSlot>() : nullptr;
+        rv.ex_slots = route_image ? d.d_ex_slots.as<const ExactSlot>() : nullptr;
         rv.ex_slot_mask = ex_slot_mask;
-        rv.ex_arena = d_ex_arena.as<const uint8_t>();
-        rv.ex_dest = d_ex_dest.as<const uint32_t>();
+        rv.ex_arena = d.d_ex_arena.as<const uint8_t>();
+        rv.ex_dest = d.d_ex_dest.as<const uint32_t>();
         return rv;
     }
 
@@ -1072,54 +1151,53 @@ struct tm_engine {
         }
     };
 
-    ImageView view() const {
+    ImageView view(const DevState& d) const {
         ImageView im;
-        if (split_halves && d_inner.p && !split_stale) {
-            im.inner = d_inner.as<const uint8_t>();
-            im.leaf = d_leaf.as<const uint8_t>();
+        if (split_halves && d.d_inner.p && !d.split_stale) {
+            im.inner = d.d_inner.as<const uint8_t>();
+            im.leaf = d.d_leaf.as<const uint8_t>();
             im.node_shift = 4;
         } else {
-            im.inner = d_nodes.as<const uint8_t>();
-            im.leaf = d_nodes.as<const uint8_t>() + 16;
+            im.inner = d.d_nodes.as<const uint8_t>();
+            im.leaf = d.d_nodes.as<const uint8_t>() + 16;
             im.node_shift = 5;
         }
-        im.edges = d_edges.as<const EdgeSlot>();
+        im.edges = d.d_edges.as<const EdgeSlot>();
         im.edge_slot_mask = cold.slots.size() - 1;
-        im.hot_edges = d_hedges.as<const EdgeSlot>();
+        im.hot_edges = d.d_hedges.as<const EdgeSlot>();
         im.hot_slot_mask = hot.slots.size() - 1;
         im.hot_limit = hot_limit;
-        im.dict = d_dict.as<const DictSlot>();
+        im.dict = d.d_dict.as<const DictSlot>();
         im.dict_slot_mask = dict.size() - 1;
-        im.word_arena = d_arena.as<const uint8_t>();
-        im.word_off = d_woff.as<const uint32_t>();
+        im.word_arena = d.d_arena.as<const uint8_t>();
+        im.word_off = d.d_woff.as<const uint32_t>();
         return im;
     }
 
+    // upload a host table to one replica: the whole table after a resize (or
+    // when the replica is new), else the dirty pages; the caller clears the
+    // dirty map once every replica has its copy
     template <class T>
-    void upload_table(DevBuf& buf, const std::vector<T>& host, Dirty& dirty, size_t dev_elems_min) {
-        size_t need = std::max(host.size(), dev_elems_min) * sizeof(T);
-        bool re = buf.ensure(need);
+    void upload_table(DevState& d, DevBuf& buf, const std::vector<T>& host, const Dirty& dirty) {
+        const bool re = buf.ensure(std::max<size_t>(host.size(), 1) * sizeof(T));
         if (re || dirty.all) {
-            HIPCHK(hipMemcpyAsync(buf.p, host.data(), host.size() * sizeof(T), hipMemcpyHostToDevice, stream));
-        } else {
-            size_t np = dirty.pages.size();
-            for (size_t pg = 0; pg < np;) {
-                if (!dirty.pages[pg]) { ++pg; continue; }
-                size_t q = pg;
-                while (q < np && dirty.pages[q]) ++q;
-                size_t a = pg * PAGE_ELEMS, b = std::min(host.size(), q * PAGE_ELEMS);
-                if (a < b)
-                    HIPCHK(hipMemcpyAsync(buf.as<T>() + a, host.data() + a, (b - a) * sizeof(T),
-                                          hipMemcpyHostToDevice, stream));
-                pg = q;
-            }
+            HIPCHK(hipMemcpyAsync(buf.p, host.data(), host.size() * sizeof(T), hipMemcpyHostToDevice, d.stream));
+            return;
         }
-        dirty.clear();
-    }
-
-    void wait_matches() {
-        for (Slot& w : slots)
-            if (w.used) HIPCHK(hipEventSynchronize(w.done));
+        const size_t np = dirty.pages.size();
+        for (size_t pg = 0; pg < np;) {
+            if (!dirty.pages[pg]) {
+                ++pg;
+                continue;
+            }
+            size_t q = pg;
+            while (q < np && dirty.pages[q]) ++q;
+            const size_t a = pg * PAGE_ELEMS, b = std::min(host.size(), q * PAGE_ELEMS);
+            if (a < b)
+                HIPCHK(hipMemcpyAsync(buf.as<T>() + a, host.data() + a, (b - a) * sizeof(T), hipMemcpyHostToDevice,
+                                      d.stream));
+            pg = q;
+        }
     }
 
     void maybe_relayout() {
@@ -1129,67 +1207,75 @@ struct tm_engine {
     }
 
     void commit() {
-        if (dev_dirty || !d_nodes.p) maybe_relayout();
-        if (device < 0) {
+        if (dev_dirty || devs.empty() || !devs[0]->d_nodes.p) maybe_relayout();
+        if (devs.empty()) {
             ++epoch;
             dev_dirty = false;
             return;
         }
-        if (!dev_dirty && d_nodes.p) {
-            if (split_halves && split_stale) {
-                Guard g(device);
-                wait_matches();
-                split_image();
-                HIPCHK(hipStreamSynchronize(stream));
-            }
+        if (!dev_dirty && devs[0]->d_nodes.p) {
+            for (auto& dp : devs)
+                if (split_halves && dp->split_stale) {
+                    Guard g(dp->device);
+                    dp->wait_matches();
+                    split_image(*dp);
+                    HIPCHK(hipStreamSynchronize(dp->stream));
+                }
             return;
         }
-        Guard g(device);
-        wait_matches();  // never patch the image under a running walk
-        rw_drain();
-        upload_table(d_nodes, nodes, node_dirty, 0);
-        upload_table(d_edges, cold.slots, cold.dirty, 0);
-        upload_table(d_hedges, hot.slots, hot.dirty, 0);
-        upload_table(d_dict, dict, dict_dirty, 0);
-        // append-only arrays: upload the new tail (or all after a realloc)
-        {
-            bool re = d_arena.ensure(std::max<size_t>(word_arena.size(), 8) + 16);
-            size_t from = re ? 0 : arena_uploaded;
-            if (word_arena.size() > from)
-                HIPCHK(hipMemcpyAsync(d_arena.as<uint8_t>() + from, word_arena.data() + from,
-                                      word_arena.size() - from, hipMemcpyHostToDevice, stream));
-            arena_uploaded = word_arena.size();
+        for (auto& dp : devs) {
+            DevState& d = *dp;
+            Guard g(d.device);
+            d.wait_matches();  // never patch the image under a running walk
+            d.rw_drain();
+            upload_table(d, d.d_nodes, nodes, node_dirty);
+            upload_table(d, d.d_edges, cold.slots, cold.dirty);
+            upload_table(d, d.d_hedges, hot.slots, hot.dirty);
+            upload_table(d, d.d_dict, dict, dict_dirty);
+            // append-only arrays: upload the new tail (or all after a realloc)
+            {
+                const bool re = d.d_arena.ensure(std::max<size_t>(word_arena.size(), 8) + 16);
+                const size_t from = re ? 0 : d.arena_uploaded;
+                if (word_arena.size() > from)
+                    HIPCHK(hipMemcpyAsync(d.d_arena.as<uint8_t>() + from, word_arena.data() + from,
+                                          word_arena.size() - from, hipMemcpyHostToDevice, d.stream));
+                d.arena_uploaded = word_arena.size();
+            }
+            {
+                const bool re = d.d_woff.ensure(std::max<size_t>(word_off.size(), 1) * 4);
+                const size_t from = re ? 0 : d.woff_uploaded;
+                if (word_off.size() > from)
+                    HIPCHK(hipMemcpyAsync(d.d_woff.as<uint32_t>() + from, word_off.data() + from,
+                                          (word_off.size() - from) * 4, hipMemcpyHostToDevice, d.stream));
+                d.woff_uploaded = word_off.size();
+            }
+            d.split_stale = true;
+            if (split_halves) split_image(d);
+            HIPCHK(hipStreamSynchronize(d.stream));
         }
-        {
-            bool re = d_woff.ensure(std::max<size_t>(word_off.size(), 1) * 4);
-            size_t from = re ? 0 : woff_uploaded;
-            if (word_off.size() > from)
-                HIPCHK(hipMemcpyAsync(d_woff.as<uint32_t>() + from, word_off.data() + from,
-                                      (word_off.size() - from) * 4, hipMemcpyHostToDevice, stream));
-            woff_uploaded = word_off.size();
-        }
-        split_stale = true;
-        if (split_halves) split_image();
-        HIPCHK(hipStreamSynchronize(stream));
+        node_dirty.clear();
+        cold.dirty.clear();
+        hot.dirty.clear();
+        dict_dirty.clear();
         dev_dirty = false;
         ++epoch;
     }
 
     // option "split": de-interleave the uploaded records into inner / leaf arrays
-    void split_image() {
-        d_inner.ensure(nodes.size() * 16);
-        d_leaf.ensure(nodes.size() * 16);
-        HIPCHK(launch_split_nodes(d_nodes.p, nodes.size(), d_inner.p, d_leaf.p, stream));
-        split_stale = false;
+    void split_image(DevState& d) {
+        d.d_inner.ensure(nodes.size() * 16);
+        d.d_leaf.ensure(nodes.size() * 16);
+        HIPCHK(launch_split_nodes(d.d_nodes.p, nodes.size(), d.d_inner.p, d.d_leaf.p, d.stream));
+        d.split_stale = false;
     }
 
     // ------------------------------------------------------------------
     // the match pipeline on device buffers (all stream-ordered on st)
-    KTimes take_event(const char* name) {
+    static KTimes take_event(DevState& d, const char* name) {
         KTimes k{name, nullptr, nullptr};
-        if (!ev_pool.empty()) {
-            k = ev_pool.back();
-            ev_pool.pop_back();
+        if (!d.ev_pool.empty()) {
+            k = d.ev_pool.back();
+            d.ev_pool.pop_back();
             k.name = name;
         } else {
             HIPCHK(hipEventCreate(&k.a));
@@ -1197,29 +1283,30 @@ struct tm_engine {
         }
         return k;
     }
-    void ensure_workspace(uint32_t n, uint64_t nbytes) { w_total.ensure(64); }
-    void ensure_slot(Slot& w, uint32_t n, uint64_t nbytes, uint32_t key_words) {
+    void ensure_slot(DevState& d, Slot& w, uint32_t n, uint64_t nbytes, uint32_t key_words) {
         w.twords.ensure((size_t)(n + 1) * WREG * 4);
         w.words.ensure((nbytes + n + 1) * 4);
         w.path.ensure((nbytes + 2ull * n + 2) * 4);
         w.stats.ensure(STATS_BYTES);
         w.meta.ensure((size_t)(n + 1) * 4);
         w.scan.ensure(scan_tmp_elems(n) * 8 + 8);
-        w.stage.ensure(((size_t)n * stage_k + 4) * 4);
-        if (key_words) w.kstage.ensure(((size_t)n * stage_k * key_words + 4) * 8);
+        w.stage.ensure(((size_t)n * d.stage_k + 4) * 4);
+        if (key_words) w.kstage.ensure(((size_t)n * d.stage_k * key_words + 4) * 8);
         w.ws.ensure(QWS_BYTES);
         if (group) w.perm.ensure(((size_t)n + GROUP_WS_ELEMS) * 4);
         if (!w.done) HIPCHK(hipEventCreateWithFlags(&w.done, hipEventDisableTiming));
     }
 
-    // the whole hot path of one batch, stream-ordered on st: CSR of ordered
-    // filter ids (ids past cap are dropped; *total always exact)
     // stage rows sized to the largest list of the previous walk (read back
     // asynchronously), within STAGE_BUDGET: fan-out beyond K costs a re-walk
-    void adapt_stage_k(uint32_t n, uint32_t key_words) {
-        if (!stage_auto) return;
+    void adapt_stage_k(DevState& d, uint32_t n, uint32_t key_words) {
+        if (!stage_auto) {
+            d.stage_k = stage_k_min;
+            return;
+        }
+        if (d.stage_k < stage_k_min) d.stage_k = stage_k_min;
         uint64_t mc = 0;
-        for (Slot& w : slots) {
+        for (Slot& w : d.slots) {
             if (!w.maxc_pending || hipEventQuery(w.maxc_ev) != hipSuccess) continue;
             w.maxc_pending = false;
             mc = std::max<uint64_t>(mc, *w.h_maxc);
@@ -1227,10 +1314,10 @@ struct tm_engine {
         if (!mc) return;
         uint64_t want = stage_k_min;
         while (want < mc && want < 4096) want <<= 1;
-        uint64_t k = stage_k;
+        uint64_t k = d.stage_k;
         const uint64_t per = (uint64_t)n * (4 + 8 * key_words);
         while (k < want && per * (k << 1) <= STAGE_BUDGET) k <<= 1;
-        stage_k = (uint32_t)k;
+        d.stage_k = (uint32_t)k;
     }
     void record_maxc(Slot& w, hipStream_t st) {
         if (!stage_auto) return;
@@ -1241,28 +1328,29 @@ struct tm_engine {
         w.maxc_pending = true;
     }
 
-    void run_batch(const uint8_t* bytes, const uint64_t* off, uint32_t n, uint64_t nbytes, uint32_t* counts,
-                   uint64_t* out_off, uint32_t* ids, uint64_t cap, uint64_t* total, hipStream_t st,
+    // the whole hot path of one batch on replica d, stream-ordered on st:
+    // CSR of ordered filter ids (ids past cap are dropped; *total always exact)
+    void run_batch(DevState& d, const uint8_t* bytes, const uint64_t* off, uint32_t n, uint64_t nbytes,
+                   uint32_t* counts, uint64_t* out_off, uint32_t* ids, uint64_t cap, uint64_t* total, hipStream_t st,
                    uint64_t* keys = nullptr, uint32_t key_words = 1) {
         const uint32_t kw = keys ? key_words : 0u;
-        adapt_stage_k(n, kw);
-        ensure_workspace(n, nbytes);
-        const int si = next_slot;
-        next_slot = (next_slot + 1) % nslots;
-        Slot& w = slots[si];
+        adapt_stage_k(d, n, kw);
+        const int si = d.next_slot;
+        d.next_slot = (d.next_slot + 1) % nslots;
+        Slot& w = d.slots[si];
         if (w.used) HIPCHK(hipStreamWaitEvent(st, w.done, 0));   // its previous batch, maybe on another stream
-        ensure_slot(w, n, nbytes, kw);
-        last_slot = si;
-        ImageView im = view();
+        ensure_slot(d, w, n, nbytes, kw);
+        d.last_slot = si;
+        ImageView im = view(d);
         unsigned long long* sp = w.stats.as<unsigned long long>();
         if (stats_enabled) HIPCHK(hipMemsetAsync(w.stats.p, 0, STATS_BYTES, st));
         static const char* kStage[4] = {"tokenize", "walk", "scan", "copy_out"};
         hipEvent_t marks[8];
         if (timing_enabled)
             for (int i = 0; i < 4; ++i) {
-                ev_cur[i] = take_event(kStage[i]);
-                marks[2 * i] = ev_cur[i].a;
-                marks[2 * i + 1] = ev_cur[i].b;
+                d.ev_cur[i] = take_event(d, kStage[i]);
+                marks[2 * i] = d.ev_cur[i].a;
+                marks[2 * i + 1] = d.ev_cur[i].b;
             }
         QueueBufs qb;
         qb.twords = w.twords.as<uint32_t>();
@@ -1274,15 +1362,22 @@ struct tm_engine {
         qb.scan_tmp = w.scan.as<uint64_t>();
         qb.ws = w.ws.as<unsigned long long>();
         qb.perm = group ? w.perm.as<uint32_t>() : nullptr;
-        HIPCHK(launch_queue(stats_enabled, xcdq != 0, im, bytes, off, n, qb, stage_k, counts, out_off, ids, keys, cap,
-                            total, sp, st, timing_enabled ? marks : nullptr, walk_bpc, hist_enabled != 0,
+        HIPCHK(launch_queue(stats_enabled, xcdq != 0, im, bytes, off, n, qb, d.stage_k, counts, out_off, ids, keys,
+                            cap, total, sp, st, timing_enabled ? marks : nullptr, walk_bpc, hist_enabled != 0,
                             keys ? key_words : 1u));
         w.keyed = keys != nullptr;
+        w.n = n;
+        w.K = d.stage_k;
+        w.kw = keys ? key_words : 1u;
+        w.bytes = bytes;
+        w.off = off;
+        w.counts = counts;
+        w.out_off = out_off;
         record_maxc(w, st);
         HIPCHK(hipEventRecord(w.done, st));
         w.used = true;
         if (timing_enabled)
-            for (int i = 0; i < 4; ++i) ev_pending.push_back(ev_cur[i]);
+            for (int i = 0; i < 4; ++i) d.ev_pending.push_back(d.ev_cur[i]);
     }
     // emqx_router:match_routes/1 over a device batch (stream-ordered except
     // for one read of the match total that sizes the ids workspace)
@@ -1298,86 +1393,226 @@ struct tm_engine {
             }
         }
     }
-    void run_routes(const uint8_t* bytes, const uint64_t* off, uint32_t n, uint64_t nbytes, uint32_t* counts,
-                    uint64_t* out_off, uint32_t* src, uint32_t* dest, uint64_t cap, uint64_t* total,
-                    hipStream_t st, uint64_t* out_key = nullptr) {
-        ensure_route_image();
+    // the ids of replica d's last batch again, into a larger output: only
+    // tm_copy_out runs (stage rows, counts and offsets are still in its slot)
+    void recopy(DevState& d, uint32_t* ids, uint64_t* keys, uint64_t cap, hipStream_t st) {
+        Slot& w = d.slots[d.last_slot];
+        QueueBufs qb;
+        qb.twords = w.twords.as<uint32_t>();
+        qb.words = w.words.as<uint32_t>();
+        qb.meta = w.meta.as<uint32_t>();
+        qb.path = w.path.as<uint32_t>();
+        qb.stage = w.stage.as<uint32_t>();
+        qb.kstage = keys ? w.kstage.as<uint64_t>() : nullptr;
+        qb.scan_tmp = w.scan.as<uint64_t>();
+        qb.ws = w.ws.as<unsigned long long>();
+        qb.perm = nullptr;
+        HIPCHK(launch_copy(view(d), w.bytes, w.off, w.n, qb, w.K, w.kw, w.counts, w.out_off, ids, keys, cap, st));
+        HIPCHK(hipEventRecord(w.done, st));
+    }
+
+    // match ids of a batch into d.w_rcounts / w_roff / w_rids with ONE walk
+    // (an overflowing id workspace is grown and re-copied, not re-walked)
+    void walk_ids(DevState& d, const uint8_t* bytes, const uint64_t* off, uint32_t n, uint64_t nbytes,
+                  uint64_t* total, hipStream_t st) {
+        d.w_rcounts.ensure((size_t)n * 4 + 4);
+        d.w_roff.ensure((size_t)(n + 1) * 8);
+        const uint64_t want = std::max<uint64_t>(d.w_rids.bytes / 4, (uint64_t)n * 16 + 1024);
+        d.w_rids.ensure(want * 4, 1.0);
+        const uint64_t icap = d.w_rids.bytes / 4;
+        uint64_t ids_total = 0;
+        run_batch(d, bytes, off, n, nbytes, d.w_rcounts.as<uint32_t>(), d.w_roff.as<uint64_t>(),
+                  d.w_rids.as<uint32_t>(), icap, total, st);
+        HIPCHK(hipMemcpyAsync(&ids_total, total, 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        if (ids_total > icap) {
+            d.w_rids.ensure(ids_total * 4, 1.25);   // contents not kept: the re-copy writes them all
+            recopy(d, d.w_rids.as<uint32_t>(), nullptr, d.w_rids.bytes / 4, st);
+        }
+    }
+    // match_routes/1 expansion of the ids walk_ids left in the workspace
+    void emit_routes(DevState& d, const uint8_t* bytes, const uint64_t* off, uint32_t n, uint32_t* counts,
+                     uint64_t* out_off, uint32_t* src, uint32_t* dest, uint64_t cap, uint64_t* total, hipStream_t st,
+                     uint64_t* out_key = nullptr) {
+        d.w_rexact.ensure((size_t)n * 8 + 8);
+        d.w_rscan.ensure(scan_tmp_elems(n) * 8 + 8);
+        const AggreView av_tmp = aggre_view(d);
+        HIPCHK(launch_routes(route_view(d), bytes, off, n, d.w_rcounts.as<uint32_t>(), d.w_roff.as<uint64_t>(),
+                             d.w_rids.as<uint32_t>(), d.w_rexact.as<uint2>(), counts, out_off, src, dest, cap, total,
+                             d.w_rscan.as<uint64_t>(), st, out_key ? &av_tmp : nullptr, out_key));
+    }
+    void run_routes(DevState& d, const uint8_t* bytes, const uint64_t* off, uint32_t n, uint64_t nbytes,
+                    uint32_t* counts, uint64_t* out_off, uint32_t* src, uint32_t* dest, uint64_t cap,
+                    uint64_t* total, hipStream_t st) {
         // this path reads the match total back anyway (host sync per batch):
         // wait for the previous route / aggre batch of any stream, so its
         // workspaces can be reused or reallocated
-        rw_drain();
-        w_rcounts.ensure((size_t)n * 4 + 4);
-        w_roff.ensure((size_t)(n + 1) * 8);
-        uint64_t want = std::max<uint64_t>(w_rids.bytes / 4, (uint64_t)n * 16 + 1024);
-        w_rids.ensure(want * 4, 1.0);
-        uint64_t icap = w_rids.bytes / 4, ids_total = 0;
-        for (int pass = 0; pass < 2; ++pass) {
-            run_batch(bytes, off, n, nbytes, w_rcounts.as<uint32_t>(), w_roff.as<uint64_t>(), w_rids.as<uint32_t>(),
-                      icap, total, st);
-            HIPCHK(hipMemcpyAsync(&ids_total, total, 8, hipMemcpyDeviceToHost, st));
-            HIPCHK(hipStreamSynchronize(st));
-            if (ids_total <= icap) break;
-            w_rids.ensure(ids_total * 4, 1.25);
-            icap = w_rids.bytes / 4;
-        }
-        w_rexact.ensure((size_t)n * 8 + 8);
-        w_rscan.ensure(scan_tmp_elems(n) * 8 + 8);
-        const AggreView av_tmp = aggre_view();
-        HIPCHK(launch_routes(route_view(), bytes, off, n, w_rcounts.as<uint32_t>(), w_roff.as<uint64_t>(),
-                             w_rids.as<uint32_t>(), w_rexact.as<uint2>(), counts, out_off, src, dest, cap, total,
-                             w_rscan.as<uint64_t>(), st, out_key ? &av_tmp : nullptr, out_key));
-        rw_release(st);
+        d.rw_drain();
+        walk_ids(d, bytes, off, n, nbytes, total, st);
+        emit_routes(d, bytes, off, n, counts, out_off, src, dest, cap, total, st);
+        d.rw_release(st);
     }
 
     // aggre(match_routes(T)) over a device batch: the route lists and their
-    // sort keys go to engine workspace (one read of the route total sizes
-    // it), aggre.hip writes each topic's list at its route offset; *total =
-    // route total
-    void run_deliveries(const uint8_t* bytes, const uint64_t* off, uint32_t n, uint64_t nbytes, uint32_t* counts,
-                        uint64_t* out_off, uint32_t* to, uint32_t* target, uint64_t cap, uint64_t* total,
-                        hipStream_t st) {
-        ensure_route_image();
-        if (aggre_dirty) build_aggre_image();
-        rw_drain();   // w_d* / w_a* may be reallocated below
-        w_dcount.ensure((size_t)n * 4 + 4);
-        uint64_t want = std::max<uint64_t>(w_dsrc.bytes / 8, (uint64_t)n * 16 + 1024);
-        w_dsrc.ensure(want * 8, 1.0);
-        w_akey.ensure(want * 8, 1.0);
-        uint64_t rcap = std::min(w_dsrc.bytes / 8, w_akey.bytes / 8), rtotal = 0;
+    // sort keys go to replica workspace (sized by the route total read back;
+    // an overflow re-emits the routes, never re-walks), aggre.hip writes each
+    // topic's list at its route offset; *total = route total
+    void deliveries_routes(DevState& d, const uint8_t* bytes, const uint64_t* off, uint32_t n, uint64_t nbytes,
+                           uint64_t* out_off, uint64_t* total, hipStream_t st, uint64_t& rcap) {
+        d.rw_drain();   // w_d* / w_a* may be reallocated below
+        d.w_dcount.ensure((size_t)n * 4 + 4);
+        const uint64_t want = std::max<uint64_t>(d.w_dsrc.bytes / 8, (uint64_t)n * 16 + 1024);
+        d.w_dsrc.ensure(want * 8, 1.0);
+        d.w_akey.ensure(want * 8, 1.0);
+        rcap = std::min(d.w_dsrc.bytes / 8, d.w_akey.bytes / 8);
+        walk_ids(d, bytes, off, n, nbytes, total, st);
+        uint64_t rtotal = 0;
         for (int pass = 0; pass < 2; ++pass) {
-            uint32_t* src = w_dsrc.as<uint32_t>();
-            run_routes(bytes, off, n, nbytes, w_dcount.as<uint32_t>(), out_off, src, src + rcap, rcap, total, st,
-                       w_akey.as<uint64_t>());
+            uint32_t* src = d.w_dsrc.as<uint32_t>();
+            emit_routes(d, bytes, off, n, d.w_dcount.as<uint32_t>(), out_off, src, src + rcap, rcap, total, st,
+                        d.w_akey.as<uint64_t>());
             HIPCHK(hipMemcpyAsync(&rtotal, total, 8, hipMemcpyDeviceToHost, st));
             HIPCHK(hipStreamSynchronize(st));
             if (rtotal <= rcap) break;
-            w_dsrc.ensure(rtotal * 8, 1.25);
-            w_akey.ensure(rtotal * 8, 1.25);
-            rcap = std::min(w_dsrc.bytes / 8, w_akey.bytes / 8);
+            d.w_dsrc.ensure(rtotal * 8, 1.25);
+            d.w_akey.ensure(rtotal * 8, 1.25);
+            rcap = std::min(d.w_dsrc.bytes / 8, d.w_akey.bytes / 8);
         }
-        w_alarge.ensure((size_t)n * 4 + 16);
-        const uint32_t* src = w_dsrc.as<uint32_t>();
-        HIPCHK(launch_aggre(aggre_view(), n, w_dcount.as<uint32_t>(), out_off, src, src + rcap, w_akey.as<uint64_t>(),
-                            w_alarge.as<uint32_t>(), counts, to, target, cap, st));
-        rw_release(st);
+        d.w_alarge.ensure((size_t)n * 4 + 16);
+    }
+    void aggre_out(DevState& d, uint32_t n, const uint64_t* out_off, uint64_t rcap, uint32_t* counts, uint32_t* to,
+                   uint32_t* target, uint64_t cap, hipStream_t st) {
+        const uint32_t* src = d.w_dsrc.as<uint32_t>();
+        HIPCHK(launch_aggre(aggre_view(d), n, d.w_dcount.as<uint32_t>(), out_off, src, src + rcap,
+                            d.w_akey.as<uint64_t>(), d.w_alarge.as<uint32_t>(), counts, to, target, cap, st));
+    }
+    void run_deliveries(DevState& d, const uint8_t* bytes, const uint64_t* off, uint32_t n, uint64_t nbytes,
+                        uint32_t* counts, uint64_t* out_off, uint32_t* to, uint32_t* target, uint64_t cap,
+                        uint64_t* total, hipStream_t st) {
+        uint64_t rcap = 0;
+        deliveries_routes(d, bytes, off, n, nbytes, out_off, total, st, rcap);
+        aggre_out(d, n, out_off, rcap, counts, to, target, cap, st);
+        d.rw_release(st);
     }
 
-    void finish_batch(hipStream_t st, uint32_t n) {
-        (void)st;
+    // route / aggre images must be current before any replica's route batch
+    void prepare_routes(bool deliveries) {
+        ensure_route_image();
+        if (deliveries && aggre_dirty) build_aggre_image();
+    }
+
+    void finish_batch(uint32_t n) {
         last_stats = tm_batch_stats{};
         last_stats.topics = n;
     }
-    void collect_stats() {
-        const DevBuf& ws = slots[last_slot].stats;
-        if (!stats_enabled || !ws.p) return;
+    // counters of replica d's last stats-mode batch (synchronous read)
+    tm_batch_stats read_stats(DevState& d, uint32_t n) {
+        tm_batch_stats s{};
+        s.topics = n;
+        const DevBuf& ws = d.slots[d.last_slot].stats;
+        if (!stats_enabled || !ws.p) return s;
         unsigned long long h[6] = {0, 0, 0, 0, 0, 0};
         HIPCHK(hipMemcpy(h, ws.p, sizeof(h), hipMemcpyDeviceToHost));
-        last_stats.levels = h[0];
-        last_stats.visits = h[1];
-        last_stats.edge_reads = h[2];
-        last_stats.matches = h[3];
-        last_stats.leaf_visits = h[4];
-        last_stats.probe_loads = h[5];
+        s.levels = h[0];
+        s.visits = h[1];
+        s.edge_reads = h[2];
+        s.matches = h[3];
+        s.leaf_visits = h[4];
+        s.probe_loads = h[5];
+        return s;
+    }
+
+    // ------------------------------------------------------------------
+    // replicas: which one a device-buffer call runs on, and a worker per
+    // replica for host-buffer batches cut across them
+    DevState* replica_for(const void* dptr) {
+        if (devs.size() == 1 || !dptr) return devs[0].get();
+        hipPointerAttribute_t at{};
+        if (hipPointerGetAttributes(&at, dptr) == hipSuccess)
+            for (auto& d : devs)
+                if (d->device == at.device) return d.get();
+        return devs[0].get();
+    }
+    struct Pool {
+        std::vector<std::thread> th;
+        std::mutex m;
+        std::condition_variable cv, done_cv;
+        std::vector<std::function<void()>> jobs;   // one slot per replica
+        std::vector<char> busy;
+        bool stop = false;
+        void start(size_t k) {
+            jobs.resize(k);
+            busy.assign(k, 0);
+            for (size_t i = 0; i < k; ++i)
+                th.emplace_back([this, i] {
+                    for (;;) {
+                        std::function<void()> f;
+                        {
+                            std::unique_lock<std::mutex> lk(m);
+                            cv.wait(lk, [&] { return stop || busy[i] == 1; });
+                            if (stop) return;
+                            f.swap(jobs[i]);
+                        }
+                        f();
+                        {
+                            std::lock_guard<std::mutex> lk(m);
+                            busy[i] = 2;
+                        }
+                        done_cv.notify_all();
+                    }
+                });
+        }
+        // run f(i) for i < k, replica i's call on worker i (i = 0 on the caller)
+        void run(size_t k, const std::function<void(size_t)>& f) {
+            {
+                std::lock_guard<std::mutex> lk(m);
+                for (size_t i = 1; i < k; ++i) {
+                    jobs[i] = [&f, i] { f(i); };
+                    busy[i] = 1;
+                }
+            }
+            cv.notify_all();
+            f(0);
+            std::unique_lock<std::mutex> lk(m);
+            done_cv.wait(lk, [&] {
+                for (size_t i = 1; i < k; ++i)
+                    if (busy[i] != 2) return false;
+                return true;
+            });
+            for (size_t i = 1; i < k; ++i) busy[i] = 0;
+        }
+        ~Pool() {
+            {
+                std::lock_guard<std::mutex> lk(m);
+                stop = true;
+            }
+            cv.notify_all();
+            for (auto& t : th) t.join();
+        }
+    };
+    std::unique_ptr<Pool> pool;
+    // run f(replica index) on every replica in parallel; exceptions are
+    // carried back to the caller (the first one wins)
+    void for_replicas(size_t k, const std::function<void(size_t)>& f) {
+        if (k <= 1) {
+            f(0);
+            return;
+        }
+        if (!pool) {
+            pool.reset(new Pool());
+            pool->start(devs.size());
+        }
+        std::vector<std::exception_ptr> err(k);
+        pool->run(k, [&](size_t i) {
+            try {
+                Guard g(devs[i]->device);
+                f(i);
+            } catch (...) {
+                err[i] = std::current_exception();
+            }
+        });
+        for (auto& x : err)
+            if (x) std::rethrow_exception(x);
     }
 };
 
@@ -1444,7 +1679,12 @@ const char* tm_strerror(int code) {
 const char* tm_last_error(tm_engine* e) { return e ? e->last_error.c_str() : "null engine"; }
 
 int tm_open(const tm_config* cfg, tm_engine** out) {
-    if (!out) return TM_EINVAL;
+    const int32_t dev = cfg ? cfg->device : -1;
+    return tm_open_devices(cfg, dev >= 0 ? &dev : nullptr, dev >= 0 ? 1u : 0u, out);
+}
+
+int tm_open_devices(const tm_config* cfg, const int32_t* devices, uint32_t n_devices, tm_engine** out) {
+    if (!out || (n_devices && !devices) || n_devices > TM_MAX_REPLICAS) return TM_EINVAL;
     *out = nullptr;
     tm_engine* e = nullptr;
     try {
@@ -1452,7 +1692,6 @@ int tm_open(const tm_config* cfg, tm_engine** out) {
     } catch (...) {
         return TM_ENOMEM;
     }
-    int dev = cfg ? cfg->device : -1;
     if (cfg && cfg->filters_hint) {
         size_t nodes_hint = (size_t)cfg->filters_hint * 3;
         e->nodes.reserve(nodes_hint);
@@ -1460,57 +1699,45 @@ int tm_open(const tm_config* cfg, tm_engine** out) {
         // wide nodes' literal edges and '#' edges use the table (load <= 1/4)
         e->cold.slots.assign(next_pow2(nodes_hint), kEmptySlot);
     }
-    if (dev >= 0) {
-        int ndev = 0;
-        hipError_t err = hipGetDeviceCount(&ndev);
-        if (err != hipSuccess || dev >= ndev) {
-            delete e;
-            return TM_EDEVICE;
-        }
-        int prev = -1;
-        (void)hipGetDevice(&prev);
-        if (hipSetDevice(dev) != hipSuccess ||
-            hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
-            delete e;
-            return TM_EDEVICE;
-        }
-        if (prev >= 0) (void)hipSetDevice(prev);
-        e->device = dev;
+    int ndev = 0;
+    if (n_devices && (hipGetDeviceCount(&ndev) != hipSuccess)) {
+        delete e;
+        return TM_EDEVICE;
     }
+    int prev = -1;
+    (void)hipGetDevice(&prev);
+    for (uint32_t i = 0; i < n_devices; ++i) {
+        std::unique_ptr<DevState> d(new (std::nothrow) DevState());
+        if (!d || devices[i] < 0 || devices[i] >= ndev || hipSetDevice(devices[i]) != hipSuccess ||
+            hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess) {
+            for (auto& x : e->devs) x->release();
+            delete e;
+            if (prev >= 0) (void)hipSetDevice(prev);
+            return d ? TM_EDEVICE : TM_ENOMEM;
+        }
+        d->device = devices[i];
+        d->stage_k = e->stage_k_min;
+        e->devs.push_back(std::move(d));
+    }
+    if (prev >= 0) (void)hipSetDevice(prev);
+    e->device = n_devices ? devices[0] : -1;
     *out = e;
     return TM_OK;
 }
 
 void tm_close(tm_engine* e) {
     if (!e) return;
-    if (e->device >= 0) {
-        (void)hipSetDevice(e->device);
-        if (e->stream) (void)hipStreamSynchronize(e->stream);
-        if (e->rw_done) (void)hipEventDestroy(e->rw_done);
-        for (DevBuf* b : {&e->d_ex_rank, &e->d_dt, &e->d_rank_src, &e->d_rank_tg, &e->w_dsrc, &e->w_dcount, &e->w_akey,
-                          &e->w_alarge,
-             &e->d_fr_meta, &e->d_fr_dest, &e->d_ex_slots, &e->d_ex_arena, &e->d_ex_dest, &e->w_rexact,
-                          &e->w_rscan, &e->w_rids, &e->w_rcounts, &e->w_roff})
-            b->release();
-        for (DevBuf* b : {&e->d_nodes, &e->d_edges, &e->d_hedges, &e->d_dict, &e->d_arena, &e->d_woff, &e->d_inner, &e->d_leaf,
-                          &e->w_mpre, &e->w_mscan, &e->w_bytes, &e->w_off, &e->w_counts, &e->w_outoff, &e->w_ids,
-                          &e->w_total})
-            b->release();
-        for (auto& w : e->slots) {
-            for (DevBuf* b : {&w.twords, &w.words, &w.path, &w.meta, &w.scan, &w.stage, &w.kstage, &w.ws, &w.stats})
-                b->release();
-            if (w.done) (void)hipEventDestroy(w.done);
-            if (w.maxc_ev) (void)hipEventDestroy(w.maxc_ev);
-            if (w.h_maxc) (void)hipHostFree(w.h_maxc);
-        }
-        for (auto* v : {&e->ev_pool, &e->ev_pending})
-            for (auto& k : *v) {
-                (void)hipEventDestroy(k.a);
-                (void)hipEventDestroy(k.b);
-            }
-        if (e->stream) (void)hipStreamDestroy(e->stream);
-    }
+    e->pool.reset();
+    for (auto& d : e->devs) d->release();
     delete e;
+}
+
+int tm_engine_replicas(tm_engine* e) { return e ? (int)e->devs.size() : 0; }
+
+int tm_engine_devices(tm_engine* e, int32_t* out, uint32_t cap) {
+    if (!e || (cap && !out)) return TM_EINVAL;
+    for (uint32_t i = 0; i < cap && i < e->devs.size(); ++i) out[i] = e->devs[i]->device;
+    return (int)e->devs.size();
 }
 
 int tm_insert(tm_engine* e, const uint8_t* filter, uint32_t len) {
@@ -1675,64 +1902,164 @@ int tm_dests_gather(tm_engine* e, const uint32_t* ids, uint32_t n, uint8_t* buf,
     });
 }
 
+namespace {
+enum BatchKind { K_MATCH = 0, K_ROUTES = 1, K_DELIVERIES = 2 };
+
+// A host-buffer batch cut into one contiguous slice per replica, run on all
+// replicas at once (one worker per GPU): each uploads its slice, runs the
+// pipeline into its workspace (grown and re-run only when a slice needs
+// more), and reports its total; then each copies its lists to the caller's
+// buffers at the prefix of the totals before it.  Results are identical to
+// one replica running the whole batch.
+int host_batch(tm_engine* e, BatchKind kind, const uint8_t* topic_bytes, const uint64_t* topic_off, uint32_t n,
+               uint32_t* out_count, uint64_t* out_off, uint32_t* out_a, uint32_t* out_b, uint64_t out_cap,
+               uint64_t* out_needed, uint32_t** out_alloc = nullptr) {
+    if (e->devs.empty()) {
+        e->last_error = "engine is host-only (no device): the match path runs on the GPU only";
+        return TM_EDEVICE;
+    }
+    for (uint32_t i = 0; i < n; ++i)
+        if (topic_off[i + 1] < topic_off[i]) throw ArgError("topic offsets not monotone");
+    if (n && topic_off[n] > topic_off[0] && !topic_bytes) throw ArgError("null topic bytes");
+    if (n == 0) {
+        out_off[0] = 0;
+        if (out_needed) *out_needed = 0;
+        if (out_alloc && !(*out_alloc = (uint32_t*)std::malloc(4))) throw std::bad_alloc();
+        return TM_OK;
+    }
+    e->commit();
+    if (kind != K_MATCH) e->prepare_routes(kind == K_DELIVERIES);
+    if (out_alloc) out_cap = UINT64_MAX;   // sized below at the exact total
+    const size_t R = std::min<size_t>(e->devs.size(), n);
+    const uint32_t planes = kind == K_MATCH ? 1u : 2u;
+    std::vector<uint64_t> tot(R, 0), icap(R, 0);
+    std::vector<std::vector<uint64_t>> loff(R);
+    std::vector<tm_batch_stats> st(R);
+    auto slice = [&](size_t i, uint32_t& lo, uint32_t& hi) {
+        lo = (uint32_t)((uint64_t)n * i / R);
+        hi = (uint32_t)((uint64_t)n * (i + 1) / R);
+    };
+    e->for_replicas(R, [&](size_t i) {
+        DevState& d = *e->devs[i];
+        uint32_t lo, hi;
+        slice(i, lo, hi);
+        const uint32_t m = hi - lo;
+        const uint64_t base = topic_off[lo], nb = topic_off[hi] - base;
+        hipStream_t s = d.stream;
+        d.rw_drain();   // the host-buffer workspaces below are shared with route batches' host syncs
+        d.w_bytes.ensure(nb + 16);
+        d.w_off.ensure((size_t)(m + 1) * 8);
+        d.w_counts.ensure((size_t)m * 4 + 4);
+        d.w_outoff.ensure((size_t)(m + 1) * 8);
+        d.w_total.ensure(64);
+        std::vector<uint64_t> rel(topic_off + lo, topic_off + hi + 1);
+        for (auto& x : rel) x -= base;
+        if (nb) HIPCHK(hipMemcpyAsync(d.w_bytes.p, topic_bytes + base, nb, hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(d.w_off.p, rel.data(), (m + 1) * 8, hipMemcpyHostToDevice, s));
+        uint64_t* d_total = d.w_total.as<uint64_t>();
+        const uint64_t elem = 4ull * planes;
+        const uint64_t want = std::max<uint64_t>(d.w_ids.bytes / elem, (uint64_t)m * 16 + 1024);
+        d.w_ids.ensure(want * elem, 1.0);
+        uint64_t cap = d.w_ids.bytes / elem, total = 0, rcap = 0;
+        // one walk; when the lists outgrow the workspace, only the last
+        // stage (copy-out / route emit / aggre) runs again into a larger one
+        uint32_t* a = d.w_ids.as<uint32_t>();
+        if (kind == K_MATCH) {
+            e->run_batch(d, d.w_bytes.as<uint8_t>(), d.w_off.as<uint64_t>(), m, nb, d.w_counts.as<uint32_t>(),
+                         d.w_outoff.as<uint64_t>(), a, cap, d_total, s);
+        } else if (kind == K_ROUTES) {
+            d.rw_drain();
+            e->walk_ids(d, d.w_bytes.as<uint8_t>(), d.w_off.as<uint64_t>(), m, nb, d_total, s);
+            e->emit_routes(d, d.w_bytes.as<uint8_t>(), d.w_off.as<uint64_t>(), m, d.w_counts.as<uint32_t>(),
+                           d.w_outoff.as<uint64_t>(), a, a + cap, cap, d_total, s);
+        } else {
+            e->deliveries_routes(d, d.w_bytes.as<uint8_t>(), d.w_off.as<uint64_t>(), m, nb,
+                                 d.w_outoff.as<uint64_t>(), d_total, s, rcap);
+            e->aggre_out(d, m, d.w_outoff.as<uint64_t>(), rcap, d.w_counts.as<uint32_t>(), a, a + cap, cap, s);
+        }
+        HIPCHK(hipMemcpyAsync(&total, d_total, 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        if (total > cap && (out_alloc || total <= out_cap)) {
+            d.w_ids.ensure(total * elem, 1.25);
+            cap = d.w_ids.bytes / elem;
+            a = d.w_ids.as<uint32_t>();
+            if (kind == K_MATCH)
+                e->recopy(d, a, nullptr, cap, s);
+            else if (kind == K_ROUTES)
+                e->emit_routes(d, d.w_bytes.as<uint8_t>(), d.w_off.as<uint64_t>(), m, d.w_counts.as<uint32_t>(),
+                               d.w_outoff.as<uint64_t>(), a, a + cap, cap, d_total, s);
+            else
+                e->aggre_out(d, m, d.w_outoff.as<uint64_t>(), rcap, d.w_counts.as<uint32_t>(), a, a + cap, cap, s);
+        }
+        if (kind != K_MATCH) d.rw_release(s);
+        tot[i] = total;
+        icap[i] = cap;
+        loff[i].resize(m + 1);
+        HIPCHK(hipMemcpyAsync(out_count + lo, d.w_counts.p, (size_t)m * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(loff[i].data(), d.w_outoff.p, (size_t)(m + 1) * 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        if (e->stats_enabled && kind == K_MATCH) st[i] = e->read_stats(d, m);
+    });
+    std::vector<uint64_t> pre(R + 1, 0);
+    for (size_t i = 0; i < R; ++i) pre[i + 1] = pre[i] + tot[i];
+    const uint64_t total = pre[R];
+    if (out_alloc) {
+        *out_alloc = (uint32_t*)std::malloc(std::max<uint64_t>(total, 1) * 4);
+        if (!*out_alloc) throw std::bad_alloc();
+        out_a = *out_alloc;
+        out_cap = total;
+    }
+    e->for_replicas(R, [&](size_t i) {
+        DevState& d = *e->devs[i];
+        uint32_t lo, hi;
+        slice(i, lo, hi);
+        for (uint32_t j = 0; j < hi - lo; ++j) out_off[lo + j] = pre[i] + loff[i][j];
+        // the workspace holds min(total, cap) entries; past out_cap the call
+        // reports TM_ENOSPC and copies what fits both
+        const uint64_t room = out_cap > pre[i] ? out_cap - pre[i] : 0;
+        const uint64_t c = std::min(std::min(tot[i], icap[i]), room);
+        if (!c) return;
+        HIPCHK(hipMemcpyAsync(out_a + pre[i], d.w_ids.p, c * 4, hipMemcpyDeviceToHost, d.stream));
+        if (planes == 2)
+            HIPCHK(hipMemcpyAsync(out_b + pre[i], d.w_ids.as<uint32_t>() + icap[i], c * 4, hipMemcpyDeviceToHost,
+                                  d.stream));
+        HIPCHK(hipStreamSynchronize(d.stream));
+    });
+    out_off[n] = total;
+    e->finish_batch(n);
+    if (e->stats_enabled && kind == K_MATCH)
+        for (auto& s : st) {
+            e->last_stats.levels += s.levels;
+            e->last_stats.visits += s.visits;
+            e->last_stats.edge_reads += s.edge_reads;
+            e->last_stats.matches += s.matches;
+            e->last_stats.leaf_visits += s.leaf_visits;
+            e->last_stats.probe_loads += s.probe_loads;
+        }
+    if (out_needed) *out_needed = total;
+    return total > out_cap ? TM_ENOSPC : TM_OK;
+}
+}  // namespace
+
+int tm_match_batch_owned(tm_engine* e, const uint8_t* topic_bytes, const uint64_t* topic_off, uint32_t n,
+                         uint32_t* out_count, uint64_t* out_off, uint32_t** out_ids, uint64_t* out_total) {
+    if (!topic_off || !out_off || !out_ids || (n && !out_count)) return TM_EINVAL;
+    *out_ids = nullptr;
+    return guarded(e, [&]() -> int {
+        return host_batch(e, K_MATCH, topic_bytes, topic_off, n, out_count, out_off, nullptr, nullptr, 0, out_total,
+                          out_ids);
+    });
+}
+
+void tm_free(void* p) { std::free(p); }
+
 int tm_match_batch(tm_engine* e, const uint8_t* topic_bytes, const uint64_t* topic_off, uint32_t n,
                    uint32_t* out_count, uint64_t* out_off, uint32_t* out_ids, uint64_t out_cap,
                    uint64_t* out_needed) {
     if (!topic_off || !out_off || (n && (!out_count)) || (out_cap && !out_ids)) return TM_EINVAL;
     return guarded(e, [&]() -> int {
-        if (e->device < 0) {
-            e->last_error = "engine is host-only (device = -1): the match path runs on the GPU only";
-            return TM_EDEVICE;
-        }
-        for (uint32_t i = 0; i < n; ++i)
-            if (topic_off[i + 1] < topic_off[i]) throw ArgError("topic offsets not monotone");
-        uint64_t base = topic_off[0], nbytes = topic_off[n] - base;
-        if (n && nbytes && !topic_bytes) throw ArgError("null topic bytes");
-        if (n == 0) {
-            out_off[0] = 0;
-            if (out_needed) *out_needed = 0;
-            return TM_OK;
-        }
-        e->commit();
-        tm_engine::Guard g(e->device);
-        hipStream_t st = e->stream;
-        e->w_bytes.ensure(nbytes + 16);
-        e->w_off.ensure((size_t)(n + 1) * 8);
-        e->w_counts.ensure((size_t)n * 4 + 4);
-        e->w_outoff.ensure((size_t)(n + 1) * 8);
-        std::vector<uint64_t> rel(topic_off, topic_off + n + 1);
-        for (auto& x : rel) x -= base;
-        if (nbytes)
-            HIPCHK(hipMemcpyAsync(e->w_bytes.p, topic_bytes + base, nbytes, hipMemcpyHostToDevice, st));
-        HIPCHK(hipMemcpyAsync(e->w_off.p, rel.data(), (n + 1) * 8, hipMemcpyHostToDevice, st));
-        e->ensure_workspace(n, nbytes);
-        uint64_t* d_total = e->w_total.as<uint64_t>();
-        // ids go to an engine buffer sized from the previous batch; grow and
-        // rerun only when a batch needs more (the total is always exact)
-        uint64_t want = std::max<uint64_t>(e->w_ids.bytes / 4, std::min<uint64_t>(out_cap, (uint64_t)n * 16 + 1024));
-        e->w_ids.ensure(want * 4, 1.0);
-        uint64_t icap = e->w_ids.bytes / 4;
-        uint64_t total = 0;
-        for (int pass = 0; pass < 2; ++pass) {
-            e->run_batch(e->w_bytes.as<uint8_t>(), e->w_off.as<uint64_t>(), n, nbytes, e->w_counts.as<uint32_t>(),
-                         e->w_outoff.as<uint64_t>(), e->w_ids.as<uint32_t>(), icap, d_total, st);
-            HIPCHK(hipMemcpyAsync(&total, d_total, 8, hipMemcpyDeviceToHost, st));
-            HIPCHK(hipStreamSynchronize(st));
-            if (total <= icap || total > out_cap) break;
-            e->w_ids.ensure(total * 4, 1.25);
-            icap = e->w_ids.bytes / 4;
-        }
-        // the workspace holds min(total, icap) ids; with total > out_cap the
-        // call reports TM_ENOSPC and copies what fits both
-        uint64_t cap = std::min(std::min(total, out_cap), icap);
-        e->finish_batch(st, n);
-        HIPCHK(hipMemcpyAsync(out_count, e->w_counts.p, (size_t)n * 4, hipMemcpyDeviceToHost, st));
-        HIPCHK(hipMemcpyAsync(out_off, e->w_outoff.p, (size_t)(n + 1) * 8, hipMemcpyDeviceToHost, st));
-        if (cap) HIPCHK(hipMemcpyAsync(out_ids, e->w_ids.p, cap * 4, hipMemcpyDeviceToHost, st));
-        HIPCHK(hipStreamSynchronize(st));
-        e->collect_stats();
-        if (out_needed) *out_needed = total;
-        return total > out_cap ? TM_ENOSPC : TM_OK;
+        return host_batch(e, K_MATCH, topic_bytes, topic_off, n, out_count, out_off, out_ids, nullptr, out_cap,
+                          out_needed);
     });
 }
 
@@ -1803,20 +2130,22 @@ int tm_match_routes_batch_device(tm_engine* e, const uint8_t* d_bytes, const uin
                                  uint32_t* d_dest, uint64_t out_cap, uint64_t* d_total, void* hip_stream) {
     if (!d_off || !d_out_off || !d_total || (n && !d_count) || (out_cap && (!d_src || !d_dest))) return TM_EINVAL;
     return guarded(e, [&]() -> int {
-        if (e->device < 0) {
-            e->last_error = "engine is host-only (device = -1): match_routes runs on the GPU only";
+        if (e->devs.empty()) {
+            e->last_error = "engine is host-only (no device): match_routes runs on the GPU only";
             return TM_EDEVICE;
         }
         e->commit();
-        tm_engine::Guard g(e->device);
-        hipStream_t st = hip_stream ? (hipStream_t)hip_stream : e->stream;
+        e->prepare_routes(false);
+        DevState& d = *e->replica_for(d_off);
+        tm_engine::Guard g(d.device);
+        hipStream_t st = hip_stream ? (hipStream_t)hip_stream : d.stream;
         if (n == 0) {
             HIPCHK(hipMemsetAsync(d_out_off, 0, 8, st));
             HIPCHK(hipMemsetAsync(d_total, 0, 8, st));
             return TM_OK;
         }
-        e->run_routes(d_bytes, d_off, n, topic_bytes, d_count, d_out_off, d_src, d_dest, out_cap, d_total, st);
-        e->finish_batch(st, n);
+        e->run_routes(d, d_bytes, d_off, n, topic_bytes, d_count, d_out_off, d_src, d_dest, out_cap, d_total, st);
+        e->finish_batch(n);
         return TM_OK;
     });
 }
@@ -1826,58 +2155,8 @@ int tm_match_routes_batch(tm_engine* e, const uint8_t* topic_bytes, const uint64
                           uint64_t out_cap, uint64_t* out_needed) {
     if (!topic_off || !out_off || (n && !out_count) || (out_cap && (!out_src || !out_dest))) return TM_EINVAL;
     return guarded(e, [&]() -> int {
-        if (e->device < 0) {
-            e->last_error = "engine is host-only (device = -1): match_routes runs on the GPU only";
-            return TM_EDEVICE;
-        }
-        for (uint32_t i = 0; i < n; ++i)
-            if (topic_off[i + 1] < topic_off[i]) throw ArgError("topic offsets not monotone");
-        const uint64_t base = topic_off[0], nbytes = topic_off[n] - base;
-        if (n && nbytes && !topic_bytes) throw ArgError("null topic bytes");
-        if (n == 0) {
-            out_off[0] = 0;
-            if (out_needed) *out_needed = 0;
-            return TM_OK;
-        }
-        e->commit();
-        tm_engine::Guard g(e->device);
-        hipStream_t st = e->stream;
-        e->w_bytes.ensure(nbytes + 16);
-        e->w_off.ensure((size_t)(n + 1) * 8);
-        e->w_counts.ensure((size_t)n * 4 + 4);
-        e->w_outoff.ensure((size_t)(n + 1) * 8);
-        std::vector<uint64_t> rel(topic_off, topic_off + n + 1);
-        for (auto& x : rel) x -= base;
-        if (nbytes) HIPCHK(hipMemcpyAsync(e->w_bytes.p, topic_bytes + base, nbytes, hipMemcpyHostToDevice, st));
-        HIPCHK(hipMemcpyAsync(e->w_off.p, rel.data(), (n + 1) * 8, hipMemcpyHostToDevice, st));
-        e->ensure_workspace(n, nbytes);
-        uint64_t* d_total = e->w_total.as<uint64_t>() + 1;
-        // routes into engine buffers sized from the previous batch; grow and
-        // rerun only when a batch needs more
-        uint64_t want = std::max<uint64_t>(e->w_ids.bytes / 8, std::min<uint64_t>(out_cap, (uint64_t)n * 16 + 1024));
-        e->w_ids.ensure(want * 8, 1.0);
-        uint64_t rcap = e->w_ids.bytes / 8, total = 0;
-        for (int pass = 0; pass < 2; ++pass) {
-            uint32_t* src = e->w_ids.as<uint32_t>();
-            e->run_routes(e->w_bytes.as<uint8_t>(), e->w_off.as<uint64_t>(), n, nbytes, e->w_counts.as<uint32_t>(),
-                          e->w_outoff.as<uint64_t>(), src, src + rcap, rcap, d_total, st);
-            HIPCHK(hipMemcpyAsync(&total, d_total, 8, hipMemcpyDeviceToHost, st));
-            HIPCHK(hipStreamSynchronize(st));
-            if (total <= rcap || total > out_cap) break;
-            e->w_ids.ensure(total * 8, 1.25);
-            rcap = e->w_ids.bytes / 8;
-        }
-        const uint64_t cap = std::min(std::min(total, out_cap), rcap);   // see tm_match_batch
-        e->finish_batch(st, n);
-        HIPCHK(hipMemcpyAsync(out_count, e->w_counts.p, (size_t)n * 4, hipMemcpyDeviceToHost, st));
-        HIPCHK(hipMemcpyAsync(out_off, e->w_outoff.p, (size_t)(n + 1) * 8, hipMemcpyDeviceToHost, st));
-        if (cap) {
-            HIPCHK(hipMemcpyAsync(out_src, e->w_ids.p, cap * 4, hipMemcpyDeviceToHost, st));
-            HIPCHK(hipMemcpyAsync(out_dest, e->w_ids.as<uint32_t>() + rcap, cap * 4, hipMemcpyDeviceToHost, st));
-        }
-        HIPCHK(hipStreamSynchronize(st));
-        if (out_needed) *out_needed = total;
-        return total > out_cap ? TM_ENOSPC : TM_OK;
+        return host_batch(e, K_ROUTES, topic_bytes, topic_off, n, out_count, out_off, out_src, out_dest, out_cap,
+                          out_needed);
     });
 }
 
@@ -1912,20 +2191,23 @@ int tm_match_deliveries_batch_device(tm_engine* e, const uint8_t* d_bytes, const
                                      uint32_t* d_target, uint64_t out_cap, uint64_t* d_total, void* hip_stream) {
     if (!d_off || !d_out_off || !d_total || (n && !d_count) || (out_cap && (!d_to || !d_target))) return TM_EINVAL;
     return guarded(e, [&]() -> int {
-        if (e->device < 0) {
-            e->last_error = "engine is host-only (device = -1): aggre runs on the GPU only";
+        if (e->devs.empty()) {
+            e->last_error = "engine is host-only (no device): aggre runs on the GPU only";
             return TM_EDEVICE;
         }
         e->commit();
-        tm_engine::Guard g(e->device);
-        hipStream_t st = hip_stream ? (hipStream_t)hip_stream : e->stream;
+        e->prepare_routes(true);
+        DevState& d = *e->replica_for(d_off);
+        tm_engine::Guard g(d.device);
+        hipStream_t st = hip_stream ? (hipStream_t)hip_stream : d.stream;
         if (n == 0) {
             HIPCHK(hipMemsetAsync(d_out_off, 0, 8, st));
             HIPCHK(hipMemsetAsync(d_total, 0, 8, st));
             return TM_OK;
         }
-        e->run_deliveries(d_bytes, d_off, n, topic_bytes, d_count, d_out_off, d_to, d_target, out_cap, d_total, st);
-        e->finish_batch(st, n);
+        e->run_deliveries(d, d_bytes, d_off, n, topic_bytes, d_count, d_out_off, d_to, d_target, out_cap, d_total,
+                          st);
+        e->finish_batch(n);
         return TM_OK;
     });
 }
@@ -1935,58 +2217,8 @@ int tm_match_deliveries_batch(tm_engine* e, const uint8_t* topic_bytes, const ui
                               uint64_t out_cap, uint64_t* out_needed) {
     if (!topic_off || !out_off || (n && !out_count) || (out_cap && (!out_to || !out_target))) return TM_EINVAL;
     return guarded(e, [&]() -> int {
-        if (e->device < 0) {
-            e->last_error = "engine is host-only (device = -1): aggre runs on the GPU only";
-            return TM_EDEVICE;
-        }
-        for (uint32_t i = 0; i < n; ++i)
-            if (topic_off[i + 1] < topic_off[i]) throw ArgError("topic offsets not monotone");
-        const uint64_t base = topic_off[0], nbytes = topic_off[n] - base;
-        if (n && nbytes && !topic_bytes) throw ArgError("null topic bytes");
-        if (n == 0) {
-            out_off[0] = 0;
-            if (out_needed) *out_needed = 0;
-            return TM_OK;
-        }
-        e->commit();
-        tm_engine::Guard g(e->device);
-        hipStream_t st = e->stream;
-        e->w_bytes.ensure(nbytes + 16);
-        e->w_off.ensure((size_t)(n + 1) * 8);
-        e->w_counts.ensure((size_t)n * 4 + 4);
-        e->w_outoff.ensure((size_t)(n + 1) * 8);
-        std::vector<uint64_t> rel(topic_off, topic_off + n + 1);
-        for (auto& x : rel) x -= base;
-        if (nbytes) HIPCHK(hipMemcpyAsync(e->w_bytes.p, topic_bytes + base, nbytes, hipMemcpyHostToDevice, st));
-        HIPCHK(hipMemcpyAsync(e->w_off.p, rel.data(), (n + 1) * 8, hipMemcpyHostToDevice, st));
-        e->ensure_workspace(n, nbytes);
-        uint64_t* d_total = e->w_total.as<uint64_t>() + 1;
-        // lists sit at their route offsets: the route total sizes the output
-        uint64_t want = std::max<uint64_t>(e->w_ids.bytes / 8, std::min<uint64_t>(out_cap, (uint64_t)n * 16 + 1024));
-        e->w_ids.ensure(want * 8, 1.0);
-        uint64_t rcap = e->w_ids.bytes / 8, total = 0;
-        for (int pass = 0; pass < 2; ++pass) {
-            uint32_t* to = e->w_ids.as<uint32_t>();
-            e->run_deliveries(e->w_bytes.as<uint8_t>(), e->w_off.as<uint64_t>(), n, nbytes,
-                              e->w_counts.as<uint32_t>(), e->w_outoff.as<uint64_t>(), to, to + rcap, rcap, d_total,
-                              st);
-            HIPCHK(hipMemcpyAsync(&total, d_total, 8, hipMemcpyDeviceToHost, st));
-            HIPCHK(hipStreamSynchronize(st));
-            if (total <= rcap || total > out_cap) break;
-            e->w_ids.ensure(total * 8, 1.25);
-            rcap = e->w_ids.bytes / 8;
-        }
-        const uint64_t cap = std::min(std::min(total, out_cap), rcap);   // see tm_match_batch
-        e->finish_batch(st, n);
-        HIPCHK(hipMemcpyAsync(out_count, e->w_counts.p, (size_t)n * 4, hipMemcpyDeviceToHost, st));
-        HIPCHK(hipMemcpyAsync(out_off, e->w_outoff.p, (size_t)(n + 1) * 8, hipMemcpyDeviceToHost, st));
-        if (cap) {
-            HIPCHK(hipMemcpyAsync(out_to, e->w_ids.p, cap * 4, hipMemcpyDeviceToHost, st));
-            HIPCHK(hipMemcpyAsync(out_target, e->w_ids.as<uint32_t>() + rcap, cap * 4, hipMemcpyDeviceToHost, st));
-        }
-        HIPCHK(hipStreamSynchronize(st));
-        if (out_needed) *out_needed = total;
-        return total > out_cap ? TM_ENOSPC : TM_OK;
+        return host_batch(e, K_DELIVERIES, topic_bytes, topic_off, n, out_count, out_off, out_to, out_target,
+                          out_cap, out_needed);
     });
 }
 
@@ -2018,14 +2250,15 @@ int tm_key_levels(tm_engine* e, uint32_t* max_levels) {
     if (!max_levels) return TM_EINVAL;
     return guarded(e, [&]() -> int {
         *max_levels = 0;
-        if (e->device < 0) return TM_OK;
-        tm_engine::Guard g(e->device);
-        for (auto& w : e->slots) {
-            if (!w.used || !w.keyed) continue;
-            HIPCHK(hipEventSynchronize(w.done));
-            uint64_t x = 0;
-            HIPCHK(hipMemcpy(&x, w.ws.as<uint64_t>() + QWS_MAXL, 8, hipMemcpyDeviceToHost));
-            *max_levels = std::max<uint32_t>(*max_levels, (uint32_t)x);
+        for (auto& dp : e->devs) {
+            tm_engine::Guard g(dp->device);
+            for (auto& w : dp->slots) {
+                if (!w.used || !w.keyed) continue;
+                HIPCHK(hipEventSynchronize(w.done));
+                uint64_t x = 0;
+                HIPCHK(hipMemcpy(&x, w.ws.as<uint64_t>() + QWS_MAXL, 8, hipMemcpyDeviceToHost));
+                *max_levels = std::max<uint32_t>(*max_levels, (uint32_t)x);
+            }
         }
         return TM_OK;
     });
@@ -2047,17 +2280,18 @@ int tm_shard_merge_w(tm_engine* e, uint32_t n_shards, uint32_t m, const uint32_t
     if (m && (!d_counts || !d_src_base || !d_out_count)) return TM_EINVAL;
     if (out_cap && (!d_ids || !d_keys || !d_out_gid)) return TM_EINVAL;
     return guarded(e, [&]() -> int {
-        if (e->device < 0) {
-            e->last_error = "engine is host-only (device = -1): the merge runs on the GPU only";
+        if (e->devs.empty()) {
+            e->last_error = "engine is host-only (no device): the merge runs on the GPU only";
             return TM_EDEVICE;
         }
-        tm_engine::Guard g(e->device);
-        hipStream_t st = hip_stream ? (hipStream_t)hip_stream : e->stream;
-        e->w_mpre.ensure(((size_t)n_shards * (m + 1) + 1) * 8);
+        DevState& d = *e->replica_for(d_out_off);
+        tm_engine::Guard g(d.device);
+        hipStream_t st = hip_stream ? (hipStream_t)hip_stream : d.stream;
+        d.w_mpre.ensure(((size_t)n_shards * (m + 1) + 1) * 8);
         if ((uint64_t)n_shards * m > 0xFFFFFFFFull) throw ArgError("n_shards x m exceeds 2^32");
-        e->w_mscan.ensure(scan_tmp_elems(std::max<uint32_t>(n_shards * m, m)) * 8 + 8);
+        d.w_mscan.ensure(scan_tmp_elems(std::max<uint32_t>(n_shards * m, m)) * 8 + 8);
         HIPCHK(launch_shard_merge(n_shards, m, d_counts, d_src_base, d_ids, d_keys, d_out_count, d_out_off, d_out_gid,
-                                  out_cap, d_total, e->w_mpre.as<uint64_t>(), e->w_mscan.as<uint64_t>(), st,
+                                  out_cap, d_total, d.w_mpre.as<uint64_t>(), d.w_mscan.as<uint64_t>(), st,
                                   key_words, key_stride));
         return TM_OK;
     });
@@ -2068,24 +2302,25 @@ static int match_device(tm_engine* e, const uint8_t* d_bytes, const uint64_t* d_
                         uint64_t* d_keys, uint32_t key_words, uint64_t out_cap, uint64_t* d_total, void* hip_stream) {
     if (!d_off || !d_out_off || !d_total || (n && !d_count) || (out_cap && !d_ids)) return TM_EINVAL;
     return guarded(e, [&]() -> int {
-        if (e->device < 0) {
-            e->last_error = "engine is host-only (device = -1): the match path runs on the GPU only";
+        if (e->devs.empty()) {
+            e->last_error = "engine is host-only (no device): the match path runs on the GPU only";
             return TM_EDEVICE;
         }
         e->commit();
-        tm_engine::Guard g(e->device);
-        hipStream_t st = hip_stream ? (hipStream_t)hip_stream : e->stream;
+        DevState& d = *e->replica_for(d_off);   // the replica on the GPU that holds the batch
+        tm_engine::Guard g(d.device);
+        hipStream_t st = hip_stream ? (hipStream_t)hip_stream : d.stream;
         if (n == 0) {
             HIPCHK(hipMemsetAsync(d_out_off, 0, 8, st));
             HIPCHK(hipMemsetAsync(d_total, 0, 8, st));
             return TM_OK;
         }
-        e->run_batch(d_bytes, d_off, n, topic_bytes, d_count, d_out_off, d_ids, out_cap, d_total, st, d_keys,
+        e->run_batch(d, d_bytes, d_off, n, topic_bytes, d_count, d_out_off, d_ids, out_cap, d_total, st, d_keys,
                      key_words);
-        e->finish_batch(st, n);
+        e->finish_batch(n);
         if (e->stats_enabled) {
             HIPCHK(hipStreamSynchronize(st));
-                e->collect_stats();
+            e->last_stats = e->read_stats(d, n);
         }
         return TM_OK;
     });
@@ -2096,7 +2331,8 @@ static int match_device(tm_engine* e, const uint8_t* d_bytes, const uint64_t* d_
 extern "C" int tm_debug_hist(tm_engine* e, uint64_t* out, int n) {
     if (!e || !out || n > 56) return TM_EINVAL;
     return guarded(e, [&]() -> int {
-        const DevBuf& ws = e->slots[e->last_slot].stats;
+        if (e->devs.empty()) return TM_EINVAL;
+        const DevBuf& ws = e->devs[0]->slots[e->devs[0]->last_slot].stats;
         if (!ws.p) return TM_EINVAL;
         HIPCHK(hipMemcpy(out, ws.as<uint64_t>() + 8, (size_t)n * 8, hipMemcpyDeviceToHost));
         return TM_OK;
@@ -2173,14 +2409,15 @@ int tm_set_option(tm_engine* e, const char* name, int64_t value) {
         }
         if (!std::strcmp(name, "stage_k")) {
             if (value < 4 || value > 4096 || (value & 3)) return TM_EINVAL;
-            e->stage_k = e->stage_k_min = (uint32_t)value;
+            e->stage_k_min = (uint32_t)value;
+            for (auto& d : e->devs) d->stage_k = (uint32_t)value;
             e->stage_auto = 0;   // an explicit K is kept (set "stage_auto" after it to grow from it)
             return TM_OK;
         }
         if (!std::strcmp(name, "slots")) {
-            if (value < 1 || value > tm_engine::MAX_SLOTS) return TM_EINVAL;
+            if (value < 1 || value > MAX_SLOTS) return TM_EINVAL;
             e->nslots = (int)value;
-            e->next_slot = 0;
+            for (auto& d : e->devs) d->next_slot = 0;
             return TM_OK;
         }
         if (!std::strcmp(name, "stage_auto")) {
@@ -2216,29 +2453,32 @@ int tm_set_timing(tm_engine* e, int enable) {
 
 int tm_last_kernel_times(tm_engine* e, const char** names, float* ms, int cap) {
     return guarded(e, [&]() -> int {
-        if (e->ev_pending.empty()) return 0;
-        tm_engine::Guard g(e->device);
         // average per batch of each kernel stage over every batch recorded
-        // since the previous call
+        // since the previous call, over all replicas
         std::vector<const char*> order;
         std::vector<double> sum;
         std::vector<int> cnt;
-        for (auto& t : e->ev_pending) {
-            HIPCHK(hipEventSynchronize(t.b));
-            float v = 0.f;
-            HIPCHK(hipEventElapsedTime(&v, t.a, t.b));
-            size_t i = 0;
-            while (i < order.size() && std::strcmp(order[i], t.name) != 0) ++i;
-            if (i == order.size()) {
-                order.push_back(t.name);
-                sum.push_back(0.0);
-                cnt.push_back(0);
+        for (auto& dp : e->devs) {
+            DevState& d = *dp;
+            if (d.ev_pending.empty()) continue;
+            tm_engine::Guard g(d.device);
+            for (auto& t : d.ev_pending) {
+                HIPCHK(hipEventSynchronize(t.b));
+                float v = 0.f;
+                HIPCHK(hipEventElapsedTime(&v, t.a, t.b));
+                size_t i = 0;
+                while (i < order.size() && std::strcmp(order[i], t.name) != 0) ++i;
+                if (i == order.size()) {
+                    order.push_back(t.name);
+                    sum.push_back(0.0);
+                    cnt.push_back(0);
+                }
+                sum[i] += v;
+                cnt[i] += 1;
+                d.ev_pool.push_back(t);
             }
-            sum[i] += v;
-            cnt[i] += 1;
-            e->ev_pool.push_back(t);
+            d.ev_pending.clear();
         }
-        e->ev_pending.clear();
         int k = 0;
         for (size_t i = 0; i < order.size() && k < cap; ++i, ++k) {
             if (names) names[k] = order[i];

@@ -40,6 +40,11 @@ hipError_t launch_queue(bool stats_mode, bool xcdq, const ImageView& im, const u
                         uint32_t* out, uint64_t* out_keys, uint64_t out_cap, uint64_t* total,
                         unsigned long long* stats, hipStream_t st, hipEvent_t* marks, uint32_t walk_blocks_per_cu = 0,
                         bool hist = false, uint32_t key_words = 1);
+// tm_copy_out again over a finished launch_queue's workspace (qb, same n /
+// K / key_words) into a larger output: no second walk
+hipError_t launch_copy(const ImageView& im, const uint8_t* bytes, const uint64_t* off, uint32_t n, const QueueBufs& qb,
+                       uint32_t K, uint32_t key_words, const uint32_t* counts, const uint64_t* out_off, uint32_t* out,
+                       uint64_t* out_keys, uint64_t out_cap, hipStream_t st);
 size_t scan_tmp_elems(uint32_t n);
 // split image (option "split"): n 32 B node records -> inner[n], leaf[n] 16 B halves
 hipError_t launch_split_nodes(const void* nodes, uint64_t n, void* inner, void* leaf, hipStream_t st);

@@ -962,6 +962,23 @@ hipError_t launch_scan(const uint32_t* counts, uint32_t n, uint64_t* out_off, ui
     return hipGetLastError();
 }
 
+// tm_copy_out alone, over the stage rows, counts and offsets a finished
+// launch_queue left in qb (same n, K, key_words): the ids into a larger
+// output after the first one overflowed, without walking again
+hipError_t launch_copy(const ImageView& im, const uint8_t* bytes, const uint64_t* off, uint32_t n, const QueueBufs& qb,
+                       uint32_t K, uint32_t key_words, const uint32_t* counts, const uint64_t* out_off, uint32_t* out,
+                       uint64_t* out_keys, uint64_t out_cap, hipStream_t st) {
+    if (n == 0 || out_cap == 0) return hipSuccess;
+    dim3 blk(BLOCK), g(div_up(n, BLOCK));
+    if (qb.kstage)
+        hipLaunchKernelGGL(tm_copy_out<true>, g, blk, 0, st, im, off, n, qb.twords, qb.words, qb.meta, qb.path,
+                           qb.stage, qb.kstage, K, key_words, counts, out_off, out, out_keys, out_cap);
+    else
+        hipLaunchKernelGGL(tm_copy_out<false>, g, blk, 0, st, im, off, n, qb.twords, qb.words, qb.meta, qb.path,
+                           qb.stage, nullptr, K, 1u, counts, out_off, out, nullptr, out_cap);
+    return hipGetLastError();
+}
+
 hipError_t launch_queue(bool stats_mode, bool xcdq, const ImageView& im, const uint8_t* bytes, const uint64_t* off,
                         uint32_t n, const QueueBufs& qb, uint32_t K, uint32_t* counts, uint64_t* out_off,
                         uint32_t* out, uint64_t* out_keys, uint64_t out_cap, uint64_t* total,

@@ -29,15 +29,28 @@ class Engine:
     """One subscription trie + its HBM image on `device` (-1 = host-only:
     insert/delete/lookup work, matching raises TM_EDEVICE)."""
 
-    def __init__(self, device=0, filters_hint=0, batch_topics=0, batch_bytes=0):
+    def __init__(self, device=0, filters_hint=0, batch_topics=0, batch_bytes=0, devices=None):
+        """devices: a list of HIP ordinals opens one engine with a replica on
+        each (tm_open_devices; host batches are cut across them)"""
         self.lib = L.load()
         cfg = L.TmConfig(device, 0, filters_hint, batch_topics, batch_bytes)
         h = ctypes.c_void_p()
-        rc = self.lib.tm_open(ctypes.byref(cfg), ctypes.byref(h))
+        if devices is not None:
+            arr = (ctypes.c_int32 * max(len(devices), 1))(*devices)
+            rc = self.lib.tm_open_devices(ctypes.byref(cfg), arr, len(devices), ctypes.byref(h))
+            what = "tm_open_devices(%s)" % list(devices)
+            device = devices[0] if devices else -1
+        else:
+            rc = self.lib.tm_open(ctypes.byref(cfg), ctypes.byref(h))
+            what = "tm_open(device=%d)" % device
         if rc != L.TM_OK:
-            raise L.TopicMatchError(rc, "tm_open(device=%d)" % device)
+            raise L.TopicMatchError(rc, what)
         self.h = h
         self.device = device
+
+    @property
+    def replicas(self):
+        return self.lib.tm_engine_replicas(self.h)
 
     # -- lifetime ---------------------------------------------------------
     def close(self):
@@ -123,17 +136,23 @@ class Engine:
         n = len(off) - 1
         counts = np.zeros(max(n, 1), dtype=np.uint32)
         offs = np.zeros(n + 1, dtype=np.uint64)
-        cap = 1 << 16 if out_cap is None else out_cap
-        while True:
-            ids = np.zeros(max(cap, 1), dtype=np.uint32)
-            needed = ctypes.c_uint64()
-            rc = self.lib.tm_match_batch(self.h, _ptr(buf), _ptr(off), n, _ptr(counts), _ptr(offs), _ptr(ids),
-                                         cap, ctypes.byref(needed))
-            if rc == L.TM_ENOSPC and out_cap is None:
-                cap = int(needed.value)
-                continue
-            self._check(rc, "tm_match_batch")
-            return counts[:n], offs, ids[: int(needed.value)]
+        if out_cap is None:   # library-sized output: one walk, no retry (tm_match_batch_owned)
+            p, total = ctypes.c_void_p(), ctypes.c_uint64()
+            rc = self.lib.tm_match_batch_owned(self.h, _ptr(buf), _ptr(off), n, _ptr(counts), _ptr(offs),
+                                               ctypes.byref(p), ctypes.byref(total))
+            try:
+                self._check(rc, "tm_match_batch_owned")
+                k = int(total.value)
+                ids = np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(ctypes.c_uint32)), shape=(max(k, 1),))
+                return counts[:n], offs, ids[:k].copy()
+            finally:
+                self.lib.tm_free(p)
+        ids = np.zeros(max(out_cap, 1), dtype=np.uint32)
+        needed = ctypes.c_uint64()
+        rc = self.lib.tm_match_batch(self.h, _ptr(buf), _ptr(off), n, _ptr(counts), _ptr(offs), _ptr(ids),
+                                     out_cap, ctypes.byref(needed))
+        self._check(rc, "tm_match_batch")
+        return counts[:n], offs, ids[: int(needed.value)]
 
     def filters_bytes(self, ids):
         """bytes of many filter ids, copied under the engine lock (tm_filters_gather)"""

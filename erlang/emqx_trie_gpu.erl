@@ -1,0 +1,61 @@
+%% emqx_trie_gpu — the GPU-backed forms of the hot-path functions, with the
+%% reference's names, arities and return shapes:
+%%
+%%   match/1           = emqx_trie:match/1           (src/emqx_trie.erl:77-79)
+%%   match_routes/1    = emqx_router:match_routes/1  (src/emqx_router.erl:116-118)
+%%   match_deliveries/1 = emqx_broker:aggre(emqx_router:match_routes(T))
+%%                                                  (src/emqx_broker.erl:152, 194-206)
+%%
+%% A call submits the topic to the engine's micro-batcher and waits for its
+%% own reply (the batcher seals device batches across all publishing
+%% processes; nothing blocks a scheduler).  The engine handle lives in the
+%% public ETS table ?TAB, written once by emqx_trie_gpu_feed at boot (OTP 21.0
+%% has no persistent_term).  Usage in the reference:
+%%
+%%   emqx_trie:match(Topic)          -> emqx_trie_gpu:match(Topic)
+%%   emqx_router:match_routes(Topic) -> emqx_trie_gpu:match_routes(Topic)
+%%   emqx_broker:publish/1:  route(aggre(match_routes(Topic)), D)
+%%                        -> route(emqx_trie_gpu:match_deliveries(Topic), D)
+-module(emqx_trie_gpu).
+
+-include_lib("emqx/include/emqx.hrl").
+
+-export([engine/0, match/1, match_routes/1, match_deliveries/1, match_many/1]).
+
+-define(TAB, emqx_trie_gpu).
+-define(TIMEOUT, 5000).
+
+engine() ->
+    [{engine, E}] = ets:lookup(?TAB, engine),
+    E.
+
+%% emqx_trie:match/1: [Filter] in the reference's order
+match(Topic) when is_binary(Topic) ->
+    wait(emqx_trie_nif:match_async(engine(), Topic)).
+
+%% many topics in one device batch (print_routes, tests, bulk callers)
+match_many(Topics) when is_list(Topics) ->
+    case emqx_trie_nif:match_many(engine(), Topics) of
+        {error, _} = E -> error(E);
+        Lists -> Lists
+    end.
+
+%% emqx_router:match_routes/1: [#route{}] — the literal topic's routes first,
+%% then each matched filter's, in trie order
+match_routes(Topic) when is_binary(Topic) ->
+    [#route{topic = To, dest = binary_to_term(D)}
+     || {To, D} <- wait(emqx_trie_nif:match_routes_async(engine(), Topic))].
+
+%% aggre(match_routes(Topic)): [{To, Node} | {To, Group}] in aggre/1's order
+match_deliveries(Topic) when is_binary(Topic) ->
+    wait(emqx_trie_nif:match_deliveries_async(engine(), Topic)).
+
+wait({error, _} = E) ->
+    error(E);
+wait(Ref) when is_reference(Ref) ->
+    receive
+        {Ref, {error, _} = E} -> error(E);
+        {Ref, Result} -> Result
+    after ?TIMEOUT ->
+        error({emqx_trie_gpu, timeout})
+    end.

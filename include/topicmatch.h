@@ -15,7 +15,7 @@
  *
  * Threading: every call on one engine is serialised by the engine (single
  * writer; matches read a committed snapshot).  Different engines are
- * independent (one engine per GPU is the multi-GPU model).
+ * independent.  One engine may span several GPUs (tm_open_devices).
  */
 #ifndef TOPICMATCH_H
 #define TOPICMATCH_H
@@ -69,6 +69,23 @@ typedef struct tm_batch_stats {
 
 /* engine lifetime ------------------------------------------------------------ */
 int  tm_open(const tm_config* cfg, tm_engine** out);
+/* One engine over several GPUs of the node (SURVEY §8(e) replicated mode):
+ * the host trie is kept once and committed to a replica of the HBM image on
+ * each of devices[0..n) (an ordinal may repeat: two replicas on one GPU).
+ * Host-buffer batches (tm_match_batch, tm_match_routes_batch,
+ * tm_match_deliveries_batch, the micro-batcher) are cut into one contiguous
+ * slice per replica and run on all GPUs at once, with results identical to
+ * one GPU; device-buffer calls run on the replica of the GPU holding the
+ * batch.  This is how one BEAM process (emqx_broker:publish/1 on every
+ * scheduler, src/emqx_broker.erl:148-157) drives the whole node through one
+ * NIF handle.  cfg->device is ignored; n_devices = 0 opens a host-only
+ * engine. */
+#define TM_MAX_REPLICAS 64u
+int  tm_open_devices(const tm_config* cfg, const int32_t* devices, uint32_t n_devices, tm_engine** out);
+/* number of device replicas (0: host-only) */
+int  tm_engine_replicas(tm_engine* e);
+/* the replicas' HIP ordinals into out[0..cap); returns their number */
+int  tm_engine_devices(tm_engine* e, int32_t* out, uint32_t cap);
 void tm_close(tm_engine* e);
 const char* tm_strerror(int code);
 const char* tm_last_error(tm_engine* e);  /* text of the last failure on e */
@@ -147,6 +164,14 @@ int tm_dests_gather(tm_engine* e, const uint32_t* ids, uint32_t n, uint8_t* buf,
 int tm_match_batch(tm_engine* e, const uint8_t* topic_bytes, const uint64_t* topic_off,
                    uint32_t n, uint32_t* out_count, uint64_t* out_off,
                    uint32_t* out_filter_id, uint64_t out_cap, uint64_t* out_needed);
+
+/* tm_match_batch with the id array allocated by the library at the exact
+ * total (*out_ids, released with tm_free; *out_total = its length): one walk
+ * per batch whatever the fan-out, no caller-side capacity guess or retry.
+ * The NIF's synchronous match/1 and match_many/2 use this. */
+int  tm_match_batch_owned(tm_engine* e, const uint8_t* topic_bytes, const uint64_t* topic_off, uint32_t n,
+                          uint32_t* out_count, uint64_t* out_off, uint32_t** out_ids, uint64_t* out_total);
+void tm_free(void* p);
 
 /* Same, with every buffer device-resident (HBM) and stream-ordered on
  * `hip_stream` (a hipStream_t; NULL = the engine's stream).  Does not
@@ -301,12 +326,17 @@ int tm_match_deliveries_batch_device(tm_engine* e, const uint8_t* d_topic_bytes,
 /* ---- publish micro-batcher (emqx_amd/csrc/batcher.cpp) -----
  * emqx_broker:publish/1 (src/emqx_broker.erl:148-157) matches one topic per
  * call in the publisher's process.  The NIF instead submits the topic here
- * and returns at once; a worker thread seals a batch at max_topics /
- * max_bytes, or deadline_us after its first topic, runs it on the GPU
- * (tm_match_batch, or tm_match_routes_batch with TM_BATCHER_ROUTES) and calls
- * done() once per topic, in submission order, from the worker thread.  The
- * id / dest arrays are valid only during the callback (the NIF copies them
- * into a term and enif_send()s it).  status != TM_OK: ids are null. */
+ * and returns at once; a sealing thread closes a batch at max_topics /
+ * max_bytes, or deadline_us after its first topic, and hands it to a free
+ * lane: lanes_per_replica lanes per GPU of the engine, each with its own
+ * thread and stream, so several batches are in flight on every GPU.  A lane
+ * runs its batch (match/1, or match_routes/1 with TM_BATCHER_ROUTES, or
+ * aggre(match_routes/1) with TM_BATCHER_DELIVERIES), reads back exactly the
+ * results, and calls done() once per topic of the batch, in submission
+ * order, from the lane's thread; different batches complete independently
+ * (a publisher waits for its own reply before publishing again).  The id /
+ * dest arrays are valid only during the callback (the NIF copies them into a
+ * term and enif_send()s it).  status != TM_OK: ids are null. */
 #define TM_BATCHER_ROUTES 1u   /* results are match_routes/1 (src ids + dest ids) */
 #define TM_BATCHER_DELIVERIES 2u   /* results are aggre(match_routes/1) (To ids + target ids) */
 
@@ -316,7 +346,7 @@ typedef struct tm_batcher_config {
     uint32_t deadline_us;     /* seal this long after the first topic (0 = 200)  */
     uint64_t max_bytes;       /* seal at this many topic bytes (0 = 64 MiB)      */
     uint32_t flags;           /* TM_BATCHER_ROUTES | TM_BATCHER_DELIVERIES      */
-    uint32_t reserved;
+    uint32_t lanes_per_replica; /* batches in flight per GPU (0 = 2)            */
 } tm_batcher_config;
 typedef struct tm_batcher_stats {
     uint64_t batches, topics, results, max_batch;

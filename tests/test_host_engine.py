@@ -9,6 +9,7 @@ import re
 import pytest
 
 from emqx_amd import Engine, _lib
+from emqx_amd.engine import pack
 from emqx_amd.emqx_router import Router
 from oracle import pytrie
 
@@ -198,3 +199,20 @@ def test_filters_and_dests_gather():
     assert e.lib.tm_dests_gather(e.h, d, 2, big, 64, off) == _lib.TM_OK
     assert bytes(big[:off[2]]) == b"node2node1"
     e.close()
+
+
+def test_open_devices_host_only_and_bad_ordinals():
+    import ctypes
+    from emqx_amd import _lib as L
+    e = Engine(devices=[])           # no replica: host-only
+    assert e.replicas == 0
+    e.insert(b"a/+")
+    with pytest.raises(L.TopicMatchError) as ex:
+        e.match_batch(*pack([b"a/b"]))
+    assert ex.value.code == L.TM_EDEVICE
+    e.close()
+    lib = L.load()
+    h = ctypes.c_void_p()
+    cfg = L.TmConfig(-1, 0, 0, 0, 0)
+    arr = (ctypes.c_int32 * 1)(-5)
+    assert lib.tm_open_devices(ctypes.byref(cfg), arr, 1, ctypes.byref(h)) in (L.TM_EDEVICE, L.TM_EINVAL)
