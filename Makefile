@@ -10,7 +10,7 @@ HIPFLAGS = --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -Wall -Wno-unused-result 
 BUILD   ?= build
 LIBOUT  ?= emqx_amd/libtopicmatch.so
 
-all: $(LIBOUT) emqx_amd/libtmwork.so oracle/liboracle.so tools/ubench/batcher_bench
+all: $(LIBOUT) emqx_amd/libtmwork.so oracle/liboracle.so tools/ubench/batcher_bench tools/ubench/libbatchdrive.so
 
 $(BUILD):
 	mkdir -p $(BUILD)
@@ -37,6 +37,9 @@ $(BUILD)/routes.o: emqx_amd/csrc/routes.hip emqx_amd/csrc/kernels.h emqx_amd/csr
 $(BUILD)/aggre.o: emqx_amd/csrc/aggre.hip emqx_amd/csrc/kernels.h emqx_amd/csrc/image.h | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
+$(BUILD)/exchange.o: emqx_amd/csrc/exchange.cpp emqx_amd/csrc/kernels.h include/topicmatch.h | $(BUILD)
+	$(HIPCC) -O2 -fPIC -std=c++17 -Wall -c $< -o $@
+
 $(BUILD)/batcher.o: emqx_amd/csrc/batcher.cpp include/topicmatch.h | $(BUILD)
 	$(HIPCC) -O2 -fPIC -std=c++17 -Wall -pthread -c $< -o $@
 
@@ -46,14 +49,14 @@ $(BUILD)/acl.o: emqx_amd/csrc/acl.hip include/topicmatch.h | $(BUILD)
 $(BUILD)/rewrite.o: emqx_amd/csrc/rewrite.hip include/topicmatch.h | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(LIBOUT): $(BUILD)/kernels.o $(BUILD)/shard.o $(BUILD)/routes.o $(BUILD)/aggre.o $(BUILD)/engine.o $(BUILD)/batcher.o $(BUILD)/acl.o $(BUILD)/rewrite.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -pthread $^ -o $@
+$(LIBOUT): $(BUILD)/kernels.o $(BUILD)/shard.o $(BUILD)/routes.o $(BUILD)/aggre.o $(BUILD)/engine.o $(BUILD)/batcher.o $(BUILD)/acl.o $(BUILD)/rewrite.o $(BUILD)/exchange.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -pthread $^ -L/opt/rocm/lib -lrccl -o $@
 
 emqx_amd/libtmwork.so: emqx_amd/csrc/workload.c
 	$(CC) -O2 -fPIC -shared -Wall $< -o $@ -lm
 
-oracle/liboracle.so: oracle/o1_trie.c
-	$(CC) -O2 -fPIC -shared -Wall $< -o $@ -lpthread
+oracle/liboracle.so: oracle/o1_trie.c oracle/o3_interned.c
+	$(CC) -O2 -fPIC -shared -Wall $^ -o $@ -lpthread
 
 clean:
 	rm -rf $(BUILD) emqx_amd/libtopicmatch.so emqx_amd/libtmwork.so oracle/liboracle.so
@@ -71,3 +74,7 @@ nif: emqx_amd/libtopicmatch.so
 # micro-batcher benchmark (single-topic submits from producer threads)
 tools/ubench/batcher_bench: tools/ubench/batcher_bench.cpp emqx_amd/libtopicmatch.so emqx_amd/libtmwork.so include/topicmatch.h
 	$(CXX) -O2 -std=c++17 -pthread $< -Lemqx_amd -ltopicmatch -ltmwork -Wl,-rpath,'$$ORIGIN/../../emqx_amd' -o $@
+
+# batcher driver for bench.py's batcher leg (measurement helper, ctypes)
+tools/ubench/libbatchdrive.so: tools/ubench/batchdrive.cpp emqx_amd/libtopicmatch.so include/topicmatch.h
+	$(CXX) -O2 -std=c++17 -fPIC -shared -pthread $< -Lemqx_amd -ltopicmatch -Wl,-rpath,'$$ORIGIN/../../emqx_amd' -o $@

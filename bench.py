@@ -1,21 +1,33 @@
 """bench.py — topic matches/sec at 10M wildcard filters on MI355X.
 
-One step = one batch of publish topics (bytes + offsets already resident in
-HBM) through the whole hot path of emqx_trie:match/1: device tokenizer
+One step = one publish batch (bytes + offsets already resident in HBM)
+through the whole hot path of emqx_trie:match/1: device tokenizer
 (emqx_topic:words/1), NFA walk, CSR emission of the ordered match lists.
 
 Workload: 10M distinct wildcard filters (8 levels max,
 p+ 0.20, p# 0.05, Zipf(1.0) words over 16/64/256/1024/4096x4), replicated on
-every GPU; each rank matches its own batch of 8-level topics (weak scaling,
-no collective on the data path).  `value` = topics matched per second over all
-ranks (max-over-ranks step time).
+every GPU.  Strong scaling (default, as §8(d) defines C3): one batch of 8M
+8-level topics per step, split 1/2/4/8 ways over the ranks; `--scaling weak`
+gives every rank its own batch instead.  Steps rotate over `--batches`
+distinct batches (no batch is replayed back to back, so L2 / MALL never hold
+the previous step's topics).  No collective on the data path.  `value` =
+topics matched per second over all ranks (max-over-ranks step time).
+
+Extra legs at N = 1 (not `value`): the CPU baseline (O1 = C restatement of
+emqx_trie, on all host threads and on one; O3 = the same algorithm over
+interned ids), the host-buffer path tm_match_batch (PCIe both ways
+included), and the micro-batcher driven by 16 producer threads with one
+submit per publish (the NIF's path).
 
 Run: python bench.py [--gpus N --steps K --warmup W]
      torchrun --nproc-per-node N bench.py --gpus N ...
+     python bench.py --single-process --gpus N   (one process, one engine over N GPUs: tm_open_devices)
 """
 import argparse
+import ctypes
 import json
 import os
+import platform
 import sys
 import time
 
@@ -45,29 +57,109 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", type=int, default=3, help="SURVEY §8(d) config (3 = the metric's)")
     ap.add_argument("--filters", type=int, default=None, help="override filter count")
+    ap.add_argument("--scaling", choices=["strong", "weak"], default="strong",
+                    help="strong: one batch per step split over the ranks (C3 as §8(d) defines it); "
+                         "weak: a batch per rank")
     ap.add_argument("--topics", type=int, default=None,
-                    help="topics per GPU per step (replicated, default 2M) / per batch (sharded, default: config's)")
+                    help="topics per batch (strong, default the config's: 8M at C3) or per GPU (weak, default 1M)")
+    ap.add_argument("--batches", type=int, default=2, help="distinct batches the steps rotate over")
     ap.add_argument("--mode", choices=["replicated", "sharded"], default=None,
                     help="replicated trie per GPU (default) or filter shards per GPU (default for --config 4)")
+    ap.add_argument("--single-process", action="store_true",
+                    help="one process drives --gpus GPUs through ONE engine (tm_open_devices)")
+    ap.add_argument("--replicas", default=None,
+                    help="single-process: comma list of HIP ordinals (repeats allowed), default 0..gpus-1")
     ap.add_argument("--cpu-sample", type=int, default=1_500_000, help="topics timed on the host (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=None)
-    ap.add_argument("--check", type=int, default=20_000, help="topics checked bit-exactly vs the oracle")
+    ap.add_argument("--check", type=int, default=20_000, help="topics of each batch checked bit-exactly vs O1")
     ap.add_argument("--streams", type=int, default=3,
                     help="streams the steps alternate over (batches overlap on the GPU; 1 = strictly serial)")
     ap.add_argument("--roof-steps", type=int, default=5,
                     help="serial steps after the timed region that time each kernel for the roofline")
+    ap.add_argument("--no-extras", action="store_true", help="skip the host-buffer and batcher legs")
     ap.add_argument("--walk", default=None, help="walk variant (queue|queue_xcd)")
-    ap.add_argument("--ab", default=None, help="comma list of walk variants timed interleaved (extra report)")
     ap.add_argument("--stage-k", type=int, default=None)
     ap.add_argument("--lib", default=None, help="EXPERIMENT: alternative build of libtopicmatch.so (A/B of build options)")
     ap.add_argument("--hist", action="store_true", help="log per-level visit/probe histogram (diagnostic)")
-    ap.add_argument("--presort", action="store_true",
-                    help="EXPERIMENT: sort the batch by topic bytes on the host before upload (untimed)")
     ap.add_argument("--layout", type=int, default=None, help="1 = DFS relayout on commit (default), 0 = off")
-    ap.add_argument("--presort-level", type=int, default=None,
-                    help="EXPERIMENT: sort the batch by the word at this level on the host (untimed)")
     ap.add_argument("--opt", action="append", default=[], help="EXPERIMENT: engine option name=value (repeatable)")
     return ap.parse_args()
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def host_threads(a):
+    return a.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count())
+
+
+def make_batches(a, cfg, rank, world):
+    """this rank's topic batches: strong = slice `rank` of each global batch,
+    weak = batches of its own stream"""
+    out = []
+    for b in range(a.batches):
+        if a.scaling == "strong":
+            tb, to = W.topics(a.config, n=a.topics, stream=b)
+            lo, hi = multi.batch_slice(len(to) - 1, world, rank)
+            sub = (to[lo:hi + 1] - to[lo]).astype(np.uint64)
+            out.append((np.ascontiguousarray(tb[int(to[lo]):int(to[hi]) + 8]), sub))
+        else:
+            out.append(W.topics(a.config, n=a.topics, stream=multi.topic_stream(rank) * 64 + b))
+    return out
+
+
+def cpu_baseline(a, fb, fo, n_filters, tb, to):
+    """O1 (the C restatement of emqx_trie: string-path ids, ETS-like tables)
+    on all host threads and on one; O3 (interned ids) likewise"""
+    from oracle import O1, O3   # checker / CPU baseline only
+    threads = host_threads(a)
+    n = len(to) - 1
+    res = {}
+    t0 = time.time()
+    o3 = O3(n_filters)
+    o3.insert_many(fb, fo)
+    log("O3 built in %.1fs" % (time.time() - t0))
+    legs = [("o3_all", o3, min(a.cpu_sample, n), threads), ("o3_1core", o3, min(a.cpu_sample // 8, n), 1)]
+    for name, o, k, th in legs:
+        secs, m = o.match_batch(tb, to[: k + 1], threads=th)
+        res[name] = {"value": k / secs, "threads": th, "topics": k, "secs": round(secs, 2)}
+        log("cpu %s: %.0f topics/s (%d topics, %d threads)" % (name, k / secs, k, th))
+    o3.close()
+    return res
+
+
+def o1_check_and_baseline(a, fb, fo, n_filters, batches, results, do_cpu):
+    from oracle import O1   # checker / CPU baseline only
+    t0 = time.time()
+    o1 = O1(n_filters)
+    o1.insert_many(fb, fo)
+    log("oracle O1 built in %.1fs (%d nodes)" % (time.time() - t0, o1.node_count))
+    threads = host_threads(a)
+    ok = True
+    for (tb, to), (dc, doo, di) in zip(batches, results):
+        k = min(a.check, len(to) - 1)
+        oc, oo, oi = o1.match_ids(tb, to[: k + 1], threads=threads)
+        ok = ok and bool(np.array_equal(dc[:k], oc) and np.array_equal(doo[: k + 1], oo) and
+                         np.array_equal(di[: int(oo[-1])], oi))
+    log("bit-exact check of %d topics of each of %d batches vs O1: %s" % (min(a.check, len(batches[0][1]) - 1),
+                                                                          len(batches), ok))
+    legs = {}
+    if do_cpu:
+        tb, to = batches[0]
+        n = len(to) - 1
+        for name, k, th in [("o1_all", min(a.cpu_sample, n), threads), ("o1_1core", min(a.cpu_sample // 30, n), 1)]:
+            secs, m, e = o1.match_batch(tb, to[: k + 1], threads=th)
+            legs[name] = {"value": k / secs, "threads": th, "topics": k, "secs": round(secs, 2)}
+            log("cpu %s: %.0f topics/s (%d topics, %d threads)" % (name, k / secs, k, th))
+    o1.close()
+    return ok, legs
 
 
 def main():
@@ -76,6 +168,8 @@ def main():
         from emqx_amd import _lib
         _lib.LIB_PATH = os.path.abspath(a.lib)
     rank, world, local = multi.env_rank()
+    if a.single_process:
+        return main_single_process(a)
     if world > 1:
         dist.init_process_group("nccl" if torch.cuda.is_available() else "gloo")
     torch.cuda.set_device(local)
@@ -85,9 +179,8 @@ def main():
         if world > 1:
             dist.destroy_process_group()
         return
-    a.topics = a.topics or 2_000_000
-
     cfg = W.CONFIGS[a.config]
+    a.topics = a.topics or (cfg["topics"] if a.scaling == "strong" else 1_000_000)
     n_filters = a.filters or cfg["filters"]
     t0 = time.time()
     fb, fo = W.filters(a.config, n=n_filters)
@@ -108,152 +201,119 @@ def main():
     log("rank %d: trie built + committed in %.1fs: %d filters, %d nodes, image %.2f GB" % (
         rank, time.time() - t0, eng.filter_count, eng.node_count, eng.image_bytes / 1e9))
 
-    tb, to = W.topics(a.config, n=a.topics, stream=multi.topic_stream(rank))
-    n = len(to) - 1
-    nbytes = int(to[-1])
-    if a.presort or a.presort_level is not None:
-        ts = [bytes(tb[to[i]:to[i + 1]]) for i in range(n)]
-        if a.presort_level is not None:   # by the word at one level (then the whole topic)
-            lv = a.presort_level
-            ts.sort(key=lambda t: (t.split(b"/")[lv:lv + 1], t))
-        else:
-            ts.sort()
-        lens = np.fromiter((len(t) for t in ts), dtype=np.uint64, count=n)
-        to = np.zeros(n + 1, dtype=np.uint64)
-        np.cumsum(lens, out=to[1:])
-        tb = np.frombuffer(b"".join(ts), dtype=np.uint8).copy()
-        del ts
-        log("presorted %d topics (experiment, untimed)" % n)
-    d_b = torch.from_numpy(tb).to(dev)
-    d_o = torch.from_numpy(to.view(np.int64)).to(dev)
-    d_c = torch.empty(n, dtype=torch.int32, device=dev)
-    d_oo = torch.empty(n + 1, dtype=torch.int64, device=dev)
-    d_t = torch.zeros(1, dtype=torch.int64, device=dev)
+    t0 = time.time()
+    batches = make_batches(a, cfg, rank, world)
+    log("rank %d: %d batches of %d topics generated in %.1fs" % (rank, len(batches), len(batches[0][1]) - 1,
+                                                                 time.time() - t0))
     st = torch.cuda.current_stream(dev)
-
-    # size the output from one counting pass (untimed), with exact stats
-    eng.set_stats(True)
+    dbat = []
+    for tb, to in batches:
+        n = len(to) - 1
+        d_b = torch.from_numpy(tb).to(dev)
+        d_o = torch.from_numpy(to.view(np.int64)).to(dev)
+        dbat.append((d_b, d_o, n, int(to[-1])))
+    # size the outputs from one counting pass per batch (untimed), exact stats of batch 0
+    totals = []
+    for i, (d_b, d_o, n, nb) in enumerate(dbat):
+        c = torch.empty(n, dtype=torch.int32, device=dev)
+        oo = torch.empty(n + 1, dtype=torch.int64, device=dev)
+        t = torch.zeros(1, dtype=torch.int64, device=dev)
+        eng.set_stats(i == 0)
+        if i == 0 and a.hist:
+            eng.set_option("hist", 1)
+        eng.match_batch_device(d_b, d_o, n, nb, c, oo, None, 0, t, stream=st)
+        torch.cuda.synchronize(dev)
+        if i == 0:
+            stats = eng.last_stats()
+            fan = np.sort(c.cpu().numpy().view(np.uint32))
+        totals.append(int(t.item()))
+    eng.set_stats(False)
     if a.hist:
-        eng.set_option("hist", 1)
-    eng.match_batch_device(d_b, d_o, n, nbytes, d_c, d_oo, None, 0, d_t, stream=st)
-    torch.cuda.synchronize(dev)
-    stats = eng.last_stats()
-    if a.hist:
-        import ctypes
         h = (ctypes.c_uint64 * 56)()
         eng.lib.tm_debug_hist(eng.h, h, 56)
+        n0 = dbat[0][2]
         for k, name in enumerate(["visits", "probe_loads", "failed_probes"]):
-            log("per-level %s per topic: %s" % (name, [round(h[16 * k + l] / n, 2) for l in range(16)]))
-        log("visits reached by: inline literal %.2f, table literal %.2f, '+' %.2f per topic"
-            % (h[48] / n, h[49] / n, h[50] / n))
-    eng.set_stats(False)
-    total = int(d_t.item())
-    cap = total + 1024
-    fan = np.sort(d_c.cpu().numpy().view(np.uint32))
+            log("per-level %s per topic: %s" % (name, [round(h[16 * k + l] / n0, 2) for l in range(16)]))
     fanout = {"mean": float(fan.mean()), "p50": int(fan[len(fan) // 2]), "p90": int(fan[int(len(fan) * 0.9)]),
               "p99": int(fan[int(len(fan) * 0.99)]), "max": int(fan[-1])}
     log("fan-out per topic: %s" % fanout)
-    d_i = torch.empty(cap, dtype=torch.int32, device=dev)
-
-    # consecutive steps alternate over a.streams streams, each with its own
+    cap = max(totals) + 1024
+    # consecutive steps alternate over a.streams streams (each with its own
     # output buffers: a batch's tokenizer / copy-out overlap its neighbours'
-    # walks (the engine rotates its per-batch workspace slots likewise)
-    lanes = [(st, d_c, d_oo, d_i, d_t)]
-    for _ in range(1, a.streams):
-        lanes.append((torch.cuda.Stream(device=dev), torch.empty_like(d_c), torch.empty_like(d_oo),
-                      torch.empty_like(d_i), torch.zeros_like(d_t)))
+    # walks; the engine rotates its per-batch workspace slots likewise) and
+    # rotate over the distinct batches
+    nmax = max(x[2] for x in dbat)
+    lanes = []
+    for k in range(a.streams):
+        s_ = st if k == 0 else torch.cuda.Stream(device=dev)
+        lanes.append((s_, torch.empty(nmax, dtype=torch.int32, device=dev),
+                      torch.empty(nmax + 1, dtype=torch.int64, device=dev),
+                      torch.empty(cap, dtype=torch.int32, device=dev), torch.zeros(1, dtype=torch.int64, device=dev)))
     eng.set_option("slots", min(4, max(2, a.streams)))
     k_step = [0]
+    last = {}
 
     def step():
-        s_, c_, oo_, i_, t_ = lanes[k_step[0] % len(lanes)]
+        j = k_step[0]
         k_step[0] += 1
-        eng.match_batch_device(d_b, d_o, n, nbytes, c_, oo_, i_, cap, t_, stream=s_)
+        s_, c_, oo_, i_, t_ = lanes[j % len(lanes)]
+        bi = j % len(dbat)
+        d_b, d_o, n, nb = dbat[bi]
+        eng.match_batch_device(d_b, d_o, n, nb, c_, oo_, i_, cap, t_, stream=s_)
+        last[bi] = j % len(lanes)
 
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize(dev)
 
-    if a.ab:
-        # interleaved A/B of walk variants on the same image and batch
-        # (rounds x variants, one process: methodology rule 24)
-        res = {v: [] for v in a.ab.split(",")}
-
-        def configure(v):   # "walk[@option=value[@...]]"
-            parts = v.split("@")
-            eng.set_walk(parts[0])
-            eng.set_option("walk_bpc", 0)
-            for kv in parts[1:]:
-                k, x = kv.split("=")
-                eng.set_option(k, int(x))
-        for _ in range(5):
-            for v in res:
-                configure(v)
-                step()
-                torch.cuda.synchronize(dev)
-                t1 = time.perf_counter()
-                for _ in range(3):
-                    step()
-                torch.cuda.synchronize(dev)
-                res[v].append((time.perf_counter() - t1) / 3 * 1e3)
-                assert int(d_t.item()) == total
-        log("A/B ms/step (median, min): " + ", ".join(
-            "%s %.2f/%.2f" % (v, sorted(x)[len(x) // 2], min(x)) for v, x in res.items()))
-        configure(a.walk or "queue_xcd")
-
-    # ---- timed region: K steps, kernel events recorded on the launch stream;
-    # barrier + sync on both sides, max over ranks (emqx_amd/multi.py)
+    # ---- timed region: K steps; barrier + sync on both sides, max over ranks
     dt = multi.timed_region(step, a.steps, lambda: torch.cuda.synchronize(dev))
-    assert int(d_t.item()) == total, "match total changed between steps"
+    for bi, li in last.items():   # every batch's last result is complete and exact
+        assert int(lanes[li][4].item()) == totals[bi], "match total changed between steps"
     # per-kernel durations for the roofline: with batches overlapping, a
     # kernel's event interval also holds its neighbours' work, so the kernels
-    # are timed over a.roof_steps extra steps issued serially on one stream
+    # are timed over a.roof_steps extra serial steps of batch 0 on one stream
+    d_b, d_o, n0, nb0 = dbat[0]
+    s0, c0, oo0, i0, t0_ = lanes[0]
     torch.cuda.synchronize(dev)
     eng.set_timing(True)
     for _ in range(a.roof_steps):
-        eng.match_batch_device(d_b, d_o, n, nbytes, d_c, d_oo, d_i, cap, d_t, stream=st)
+        eng.match_batch_device(d_b, d_o, n0, nb0, c0, oo0, i0, cap, t0_, stream=s0)
     torch.cuda.synchronize(dev)
     kms = eng.last_kernel_times()
     eng.set_timing(False)
-    for _, c_, oo_, i_, t_ in lanes[1:]:   # overlapping batches: identical results in every lane
-        assert int(t_.item()) == total and torch.equal(c_, d_c) and torch.equal(oo_, d_oo) and \
-            torch.equal(i_[:total], d_i[:total]), "batches on different streams disagree"
+    # every batch's full result (the bit-exact check reads them back)
+    results = []
+    for bi, (d_b, d_o, n, nb) in enumerate(dbat):
+        eng.match_batch_device(d_b, d_o, n, nb, c0, oo0, i0, cap, t0_, stream=s0)
+        torch.cuda.synchronize(dev)
+        results.append((c0[:n].cpu().numpy().view(np.uint32).copy(), oo0[: n + 1].cpu().numpy().view(np.uint64).copy(),
+                        i0[: totals[bi]].cpu().numpy().view(np.uint32).copy()))
 
-    # ---- bit-exact spot check of this rank's batch against the oracle
-    check_ok = None
-    o1 = None
-    cpu = None
+    extras = {}
+    if world == 1 and not a.no_extras:
+        extras = host_legs(a, eng, batches[0], totals[0])
+
+    check_ok, cpu = None, None
     if rank == 0 and (a.check > 0 or (world == 1 and a.cpu_sample > 0)):
-        from oracle import O1   # checker / CPU baseline only
-        t0 = time.time()
-        o1 = O1(n_filters)
-        o1.insert_many(fb, fo)
-        log("oracle O1 built in %.1fs (%d nodes)" % (time.time() - t0, o1.node_count))
-        threads = a.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count())
-        if a.check > 0:
-            k = min(a.check, n)
-            ksub = to[: k + 1]
-            oc, oo, oi = o1.match_ids(tb, ksub, threads=threads)
-            dc = d_c[:k].cpu().numpy().view(np.uint32)
-            doo = d_oo[: k + 1].cpu().numpy().view(np.uint64)
-            di = d_i[: int(doo[-1])].cpu().numpy().view(np.uint32)
-            check_ok = bool(np.array_equal(dc, oc) and np.array_equal(doo, oo) and np.array_equal(di, oi))
-            log("bit-exact check of %d topics vs O1: %s" % (k, check_ok))
-        if world == 1 and a.cpu_sample > 0:
-            k = min(a.cpu_sample, n)
-            secs, m, e = o1.match_batch(tb, to[: k + 1], threads=threads)
-            cpu = {"value": k / secs, "unit": "topics/s", "cores": threads, "kind": "port",
-                   "sample": "%d topics of the same batch against the same %d-filter trie, C restatement "
-                             "of emqx_trie (string-path ids, ETS-like tables), %d pthreads, %.1f s"
-                             % (k, n_filters, threads, secs)}
-            log("cpu baseline: %.0f topics/s on %d threads" % (k / secs, threads))
+        check_ok, legs = o1_check_and_baseline(a, fb, fo, n_filters, batches, results, world == 1 and a.cpu_sample > 0)
+        if legs:
+            legs.update(cpu_baseline(a, fb, fo, n_filters, *batches[0]))
+            th = host_threads(a)
+            cpu = {"value": legs["o1_all"]["value"], "unit": "topics/s", "cores": th, "kind": "port",
+                   "sample": "%d topics of the bench batch against the same %d-filter trie: O1, the C "
+                             "restatement of emqx_trie (string-path node ids, ETS-like {trie_edge, NodeId, "
+                             "Word} tables), %d pthreads, %.1f s" % (legs["o1_all"]["topics"], n_filters, th,
+                                                                     legs["o1_all"]["secs"]),
+                   "cpu_model": cpu_model(), "nproc": os.cpu_count(), "threads_used": th, "legs": legs}
 
     if rank == 0:
-        topics_per_s = n * a.steps * world / dt
+        topics_per_step = sum(x[2] for x in dbat) / len(dbat) * (world if a.scaling == "weak" else 1)
+        if a.scaling == "strong":
+            topics_per_step = a.topics
+        topics_per_s = topics_per_step * a.steps / dt
         levels = stats["levels"]
-        B = 8 * levels + 16 * stats["edge_reads"] + 4 * stats["matches"]   # SURVEY §8(d), per launch
-        # dominant kernel = the longest stage (the walk); B is what one launch
-        # of it processes
+        B = 8 * levels + 16 * stats["edge_reads"] + 4 * stats["matches"]   # SURVEY §8(d), per launch of batch 0
         kname = max(kms, key=kms.get) if kms else None
         walk_ms = kms.get(kname, 0.0) if kname else 0.0
         achieved = B / (walk_ms * 1e-3) / 1e9 if walk_ms > 0 else None
@@ -264,7 +324,7 @@ def main():
         if os.path.exists(tpath) and kname == "walk":
             tj = json.load(open(tpath))
             tc = tj.get("config") or {}
-            if tc.get("filters") == n_filters and tc.get("topics_per_gpu_step") == n and tc.get("levels") == cfg["levels"]:
+            if tc.get("filters") == n_filters and tc.get("topics_per_gpu_step") == n0 and tc.get("levels") == cfg["levels"]:
                 traffic = tj["traffic_bytes_per_launch"] / (walk_ms * 1e-3) / 1e9
         out = {
             "metric": METRIC,
@@ -275,15 +335,19 @@ def main():
             "warmup": a.warmup,
             "ms_per_step": dt / a.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": a.scaling,
             "vs_baseline": None,
             "dtype": "u32",
             "data": "synthetic",
             "config": {"workload": "C%d: %d distinct wildcard filters replicated per GPU, %d-level topics, "
-                                   "%d topics per GPU per step, steps alternating over %d streams" % (
-                                       a.config, n_filters, cfg["levels"], n, a.streams),
-                       "filters": n_filters, "topics_per_gpu_step": n, "levels": cfg["levels"],
-                       "parallelism": "replicated trie x %d, topic batches sharded by rank" % world},
+                                   "%s, steps rotating over %d distinct batches and %d streams" % (
+                                       a.config, n_filters, cfg["levels"],
+                                       ("one %d-topic batch per step split over %d GPU(s)" % (a.topics, world))
+                                       if a.scaling == "strong" else "%d topics per GPU per step" % a.topics,
+                                       a.batches, a.streams),
+                       "filters": n_filters, "topics_per_step": int(topics_per_step),
+                       "topics_per_gpu_step": n0, "levels": cfg["levels"],
+                       "parallelism": "replicated trie x %d, topic batch split by rank" % world},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
                          "traffic_source": ("FETCH_SIZE+WRITE_SIZE per launch, profiles/traffic_c%d.json, over this "
@@ -291,33 +355,141 @@ def main():
                          "kernel": {"walk": "tm_walk_queue (balanced NFA walk, one 16 B node-half load per step)"
                                     }.get(kname, kname),
                          "kernel_ms": walk_ms,
-                         "kernel_ms_source": "HIP events around each kernel on its stream, %d serial steps after "
-                                             "the timed region" % a.roof_steps,
+                         "kernel_ms_source": "HIP events around each kernel on its stream, %d serial steps of "
+                                             "batch 0 after the timed region" % a.roof_steps,
                          "algorithmic_bytes_per_launch": B,
-                         "per_topic": {"n": levels / n, "E": stats["edge_reads"] / n, "M": stats["matches"] / n,
-                                       "visits": stats["visits"] / n, "leaf_visits": stats["leaf_visits"] / n,
-                                       "probe_loads": stats["probe_loads"] / n}},
+                         "topics_per_launch": n0,
+                         "per_topic": {"n": levels / n0, "E": stats["edge_reads"] / n0, "M": stats["matches"] / n0,
+                                       "visits": stats["visits"] / n0, "leaf_visits": stats["leaf_visits"] / n0,
+                                       "probe_loads": stats["probe_loads"] / n0}},
             "cpu_baseline": cpu,
             "kernel_ms": kms,
-            "filter_hits_per_s": stats["matches"] * a.steps * world / dt,
+            "filter_hits_per_s": stats["matches"] / n0 * topics_per_s,
             "fanout": fanout,
             "parity_check": check_ok,
         }
+        out.update(extras)
         print(json.dumps(out), flush=True)
     eng.close()
     if world > 1:
         dist.destroy_process_group()
 
 
+def host_legs(a, eng, batch, total):
+    """the product paths a broker takes (N = 1): host buffers through
+    tm_match_batch (topics up and lists down over PCIe included), and the
+    micro-batcher fed one publish at a time by 16 producer threads"""
+    tb, to = batch
+    n = len(to) - 1
+    out = {}
+    eng.match_batch(tb, to)   # warm the host-path workspace
+    reps = 3
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        counts, offs, ids = eng.match_batch(tb, to)
+    secs = (time.perf_counter() - t0) / reps
+    assert int(offs[-1]) == total
+    moved = int(to[-1]) + 8 * (n + 1) + 4 * n + 8 * (n + 1) + 4 * total
+    out["host_path"] = {"topics_per_s": n / secs, "ms_per_batch": secs * 1e3, "topics": n,
+                        "pcie_bytes": moved, "pcie_gbs": moved / secs / 1e9,
+                        "path": "tm_match_batch: host topics -> HBM -> walk -> ids back to host (one library-sized "
+                                "read-back), PCIe both ways included"}
+    log("host path: %.0f topics/s, %.2f ms per %d-topic batch, %.1f GB/s over PCIe" % (
+        n / secs, secs * 1e3, n, moved / secs / 1e9))
+    lib_path = os.path.join(ROOT, "tools", "ubench", "libbatchdrive.so")
+    if os.path.exists(lib_path):
+        drv = ctypes.CDLL(lib_path)
+        drv.tm_bench_batcher.restype = ctypes.c_int
+        drv.tm_bench_batcher.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                         ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                         ctypes.c_uint32, ctypes.POINTER(ctypes.c_double)]
+        k = min(n, 2_000_000)
+        res = (ctypes.c_double * 8)()
+        rc = drv.tm_bench_batcher(eng.h, tb.ctypes.data, to.ctypes.data, k, 16, 200, 65536, 2, 0, res)
+        if rc == 0:
+            out["batcher"] = {"topics_per_s": res[1], "topics": k, "producers": 16, "deadline_us": 200,
+                              "lanes_per_replica": 2, "batches": int(res[2]), "mean_batch": res[3],
+                              "lat_us_p50": res[4], "lat_us_p99": res[5], "failed": int(res[6]),
+                              "matches": int(res[7]),
+                              "path": "tm_batcher_submit per publish from 16 threads, per-topic callbacks (NIF path)"}
+            log("batcher: %.0f topics/s, mean batch %.0f, p50 %.0f us, p99 %.0f us" % (res[1], res[3], res[4],
+                                                                                     res[5]))
+    return out
+
+
+def main_single_process(a):
+    """one process, one engine over N replicas (tm_open_devices): a
+    resident batch slice on each replica's GPU, every step issues all N
+    batches (device API, each on its GPU's stream) and waits for all — the
+    whole node driven through the C-ABI the NIF uses"""
+    devs = [int(x) for x in a.replicas.split(",")] if a.replicas else list(range(a.gpus))
+    N = len(devs)
+    cfg = W.CONFIGS[a.config]
+    a.topics = a.topics or cfg["topics"]
+    n_filters = a.filters or cfg["filters"]
+    fb, fo = W.filters(a.config, n=n_filters)
+    t0 = time.time()
+    eng = Engine(devices=devs, filters_hint=n_filters)
+    eng.insert_many(fb, fo)
+    eng.commit()
+    log("engine over %s built in %.1fs" % (devs, time.time() - t0))
+    tb, to = W.topics(a.config, n=a.topics, stream=0)
+    parts = []
+    for r, d in enumerate(devs):
+        dev = torch.device("cuda", d)
+        lo, hi = multi.batch_slice(len(to) - 1, N, r)
+        sub = (to[lo:hi + 1] - to[lo]).astype(np.uint64)
+        sb = np.ascontiguousarray(tb[int(to[lo]):int(to[hi]) + 8])
+        n = hi - lo
+        with torch.cuda.device(dev):
+            s_ = torch.cuda.Stream(device=dev)
+        parts.append(dict(dev=dev, s=s_, b=torch.from_numpy(sb).to(dev), o=torch.from_numpy(sub.view(np.int64)).to(dev),
+                          n=n, nb=int(sub[-1]), c=torch.empty(n, dtype=torch.int32, device=dev),
+                          oo=torch.empty(n + 1, dtype=torch.int64, device=dev),
+                          t=torch.zeros(1, dtype=torch.int64, device=dev)))
+    for p in parts:   # exact output sizes
+        eng.match_batch_device(p["b"], p["o"], p["n"], p["nb"], p["c"], p["oo"], None, 0, p["t"], stream=p["s"])
+    for p in parts:
+        torch.cuda.synchronize(p["dev"])
+        p["cap"] = int(p["t"].item()) + 1024
+        p["i"] = torch.empty(p["cap"], dtype=torch.int32, device=p["dev"])
+
+    def step():
+        for p in parts:
+            eng.match_batch_device(p["b"], p["o"], p["n"], p["nb"], p["c"], p["oo"], p["i"], p["cap"], p["t"],
+                                   stream=p["s"])
+
+    def sync():
+        for p in parts:
+            torch.cuda.synchronize(p["dev"])
+    for _ in range(a.warmup):
+        step()
+    dt = multi.timed_region(step, a.steps, sync)
+    counts, offs, ids = eng.match_batch(tb, to)   # the host path over all replicas: the same lists
+    got = np.concatenate([p["i"][: int(p["t"].item())].cpu().numpy().view(np.uint32) for p in parts])
+    assert np.array_equal(got, ids), "replica results differ from the whole-batch host path"
+    print(json.dumps({"metric": METRIC, "value": a.topics * a.steps / dt, "unit": "topics/s", "n_gpus": N,
+                      "steps": a.steps, "warmup": a.warmup, "ms_per_step": dt / a.steps * 1e3,
+                      "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u32",
+                      "data": "synthetic",
+                      "config": {"workload": "C%d single process, one engine over replicas %s, one %d-topic batch "
+                                             "per step split over them" % (a.config, devs, a.topics),
+                                 "filters": n_filters, "topics_per_step": a.topics,
+                                 "parallelism": "one process, tm_open_devices x %d" % N},
+                      "replicas_consistent": True}), flush=True)
+    eng.close()
+
+
 def main_sharded(a, rank, world, local, dev):
     """Config C4: the filter set partitioned over the ranks by
-    literal-prefix (one shard per GPU).  Every rank holds the same topic batch,
+    literal prefix (one shard per GPU).  Every rank holds the same topic batch,
     walks it against its own sub-trie with order keys, then the ranks
-    exchange per-topic keyed lists (all-to-all, RCCL over xGMI) and each
-    merges the lists of its topic slice into emqx_trie:match/1 order on its
-    GPU.  One step = walk + exchange + merge of one batch; `value` = batch
-    topics / max-over-ranks step time (strong scaling: the batch and filter
-    set are fixed, N GPUs share them)."""
+    exchange per-topic keyed lists natively over RCCL (tm_shard_exchange: an
+    all-to-all, each id crosses xGMI once) and each merges the lists of its
+    topic slice into emqx_trie:match/1 order on its GPU.  One step = walk +
+    exchange + merge of one batch; `value` = batch topics / max-over-ranks
+    step time (strong scaling: the batch and filter set are fixed, N GPUs
+    share them)."""
     from emqx_amd import shard
     S = world
     cfg = W.CONFIGS[a.config]
@@ -332,11 +504,17 @@ def main_sharded(a, rank, world, local, dev):
     eng.commit()
     log("rank %d: shard %d/%d built + committed in %.1fs: %d filters, %d nodes, image %.2f GB" % (
         rank, rank, S, time.time() - t0, eng.filter_count, eng.node_count, eng.image_bytes / 1e9))
+    # one RCCL communicator over the ranks, its id shared over torch.distributed
+    uid = [shard.Comm.unique_id() if rank == 0 else None]
+    if world > 1:
+        dist.broadcast_object_list(uid, src=0)
+    comm = shard.Comm.init_rank(uid[0], S, rank, local)
 
     n_topics = a.topics if a.topics else cfg["topics"]
     tb, to = W.topics(a.config, n=n_topics, stream=0)     # the same batch on every shard
     n = len(to) - 1
     nbytes = int(to[-1])
+    KW = shard.key_words_for(tb, to)
     d_b = torch.from_numpy(tb).to(dev)
     d_o = torch.from_numpy(to.view(np.int64)).to(dev)
     d_c = torch.empty(n, dtype=torch.int32, device=dev)
@@ -345,35 +523,33 @@ def main_sharded(a, rank, world, local, dev):
     st = torch.cuda.current_stream(dev)
 
     eng.set_stats(True)
-    eng.match_keys_device(d_b, d_o, n, nbytes, d_c, d_oo, None, None, 0, d_t, stream=st)
+    eng.match_keys_device(d_b, d_o, n, nbytes, d_c, d_oo, None, None, 0, d_t, stream=st, key_words=KW)
     torch.cuda.synchronize(dev)
     stats = eng.last_stats()
     eng.set_stats(False)
     total = int(d_t.item())
     cap = total + 1024
     d_i = torch.empty(cap, dtype=torch.int32, device=dev)
-    d_k = torch.empty(cap, dtype=torch.int64, device=dev)
+    d_k = torch.empty(cap * KW, dtype=torch.int64, device=dev)
     b = shard.slices(n, S)
     m = b[rank + 1] - b[rank]
-    # merge output: sized after one exchange (the received total is exact)
     merged = {}
 
     def walk():
-        eng.match_keys_device(d_b, d_o, n, nbytes, d_c, d_oo, d_i, d_k, cap, d_t, stream=st)
+        eng.match_keys_device(d_b, d_o, n, nbytes, d_c, d_oo, d_i, d_k, cap, d_t, stream=st, key_words=KW)
 
     def exchange():
-        return shard.exchange(d_c, d_oo, d_i, d_k, n, S, rank)
+        return shard.exchange_native(comm, d_c, d_oo, d_i, d_k, n, key_words=KW, key_stride=cap, stream=st)
 
     def merge(x):
-        rc, base, rid, rk, mm = x
-        if "cap" not in merged:
-            merged["cap"] = max(int(rid.numel()), 1) + 1024
-            merged["c"] = torch.empty(max(mm, 1), dtype=torch.int32, device=dev)
-            merged["o"] = torch.empty(mm + 1, dtype=torch.int64, device=dev)
+        if merged.get("cap", 0) < x.total + 1:
+            merged["cap"] = x.total + 1 + 1024
+            merged["c"] = torch.empty(max(x.m, 1), dtype=torch.int32, device=dev)
+            merged["o"] = torch.empty(x.m + 1, dtype=torch.int64, device=dev)
             merged["g"] = torch.empty(merged["cap"], dtype=torch.int32, device=dev)
             merged["t"] = torch.zeros(1, dtype=torch.int64, device=dev)
-        eng.merge_device(mm, rc, base, rid, rk, merged["c"], merged["o"], merged["g"], merged["cap"], merged["t"],
-                         stream=st)
+        eng.merge_device(x.m, x.d_counts, x.d_src_base, x.d_ids, x.d_keys, merged["c"], merged["o"], merged["g"],
+                         merged["cap"], merged["t"], stream=st, key_words=KW, key_stride=x.total)
 
     def step():
         walk()
@@ -384,13 +560,11 @@ def main_sharded(a, rank, world, local, dev):
     torch.cuda.synchronize(dev)
     dt = multi.timed_region(step, a.steps, lambda: torch.cuda.synchronize(dev))
     assert int(d_t.item()) == total, "match total changed between steps"
-    # per-kernel durations for the roofline: with batches overlapping, a
-    # kernel's event interval also holds its neighbours' work, so the kernels
-    # are timed over a.roof_steps extra steps issued serially on one stream
+    # the dominant kernel of this mode is the KEYED walk: time it serially
     torch.cuda.synchronize(dev)
     eng.set_timing(True)
     for _ in range(a.roof_steps):
-        eng.match_batch_device(d_b, d_o, n, nbytes, d_c, d_oo, d_i, cap, d_t, stream=st)
+        walk()
     torch.cuda.synchronize(dev)
     kms = eng.last_kernel_times()
     eng.set_timing(False)
@@ -410,11 +584,10 @@ def main_sharded(a, rank, world, local, dev):
     check_ok = None
     if rank == 0 and a.check > 0 and n_filters <= 20_000_000:
         from oracle import O1   # checker only
-        threads = a.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count())
         o1 = O1(n_filters)
         o1.insert_many(fb, fo)
         k = min(a.check, m)
-        oc, oo, oi = o1.match_ids(tb, to[: k + 1], threads=threads)
+        oc, oo, oi = o1.match_ids(tb, to[: k + 1], threads=host_threads(a))
         g2i = shard.gid_to_index(shard.shard_of_batch(fb, fo, S), S)
         mo = merged["o"][: k + 1].cpu().numpy().view(np.uint64)
         mg = merged["g"][: int(mo[-1])].cpu().numpy().view(np.uint32).astype(np.int64)
@@ -422,7 +595,7 @@ def main_sharded(a, rank, world, local, dev):
         log("bit-exact check of %d topics (rank 0 slice) vs O1: %s" % (k, check_ok))
 
     levels = stats["levels"]
-    B = 8 * levels + 16 * stats["edge_reads"] + 4 * stats["matches"]
+    B = 8 * levels + 16 * stats["edge_reads"] + 4 * stats["matches"] + 8 * stats["matches"] * KW   # + the keys
     walk_ms = kms.get("walk", 0.0)
     achieved = B / (walk_ms * 1e-3) / 1e9 if walk_ms > 0 else None
     if rank == 0:
@@ -443,11 +616,12 @@ def main_sharded(a, rank, world, local, dev):
                                    "%d-level topics, one %d-topic batch per step" % (
                                        a.config, n_filters, S, cfg["levels"], n),
                        "filters": n_filters, "topics_per_step": n, "levels": cfg["levels"],
-                       "parallelism": "filter shards x %d, all-to-all of keyed match lists (RCCL), device merge"
-                                      % S},
+                       "parallelism": "filter shards x %d, RCCL all-to-all of keyed match lists "
+                                      "(tm_shard_exchange, %s), device merge" % (
+                                          S, "RCCL" if comm.rccl else "device copies")},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": None,
-                         "kernel": "tm_walk_queue<KEYS> on rank 0's shard", "kernel_ms": walk_ms,
+                         "kernel": "tm_walk_queue<KEYS> (keyed walk) on rank 0's shard", "kernel_ms": walk_ms,
                          "algorithmic_bytes_per_launch": B},
             "cpu_baseline": None,
             "kernel_ms": kms,
@@ -457,6 +631,7 @@ def main_sharded(a, rank, world, local, dev):
             "parity_check": check_ok,
         }
         print(json.dumps(out), flush=True)
+    comm.close()
     eng.close()
 
 

@@ -47,6 +47,19 @@ class TmBatcherStats(ctypes.Structure):
                                                "deadline_seals", "failed_batches")]
 
 
+class TmExchangeIn(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_uint32), ("key_words", ctypes.c_uint32), ("d_counts", ctypes.c_void_p),
+                ("d_offs", ctypes.c_void_p), ("d_ids", ctypes.c_void_p), ("d_keys", ctypes.c_void_p),
+                ("key_stride", ctypes.c_uint64), ("hip_stream", ctypes.c_void_p)]
+
+
+class TmExchangeOut(ctypes.Structure):
+    _fields_ = [("m", ctypes.c_uint32), ("reserved", ctypes.c_uint32), ("total", ctypes.c_uint64),
+                ("d_counts", ctypes.c_void_p), ("d_src_base", ctypes.c_void_p), ("d_ids", ctypes.c_void_p),
+                ("d_keys", ctypes.c_void_p)]
+
+
+TM_COMM_ID_BYTES = 128
 TM_BATCHER_ROUTES = 1
 TM_BATCHER_DELIVERIES = 2
 DONE_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, c_u32p, c_u32p, ctypes.c_uint32)
@@ -111,6 +124,18 @@ SIGNATURES = [
                                       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
                                       ctypes.c_void_p]),
+    ("tm_comm_unique_id", ctypes.c_int, [ctypes.c_void_p]),
+    ("tm_comm_init_rank", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,
+                                         ctypes.POINTER(ctypes.c_void_p)]),
+    ("tm_comm_init_all", ctypes.c_int, [ctypes.POINTER(ctypes.c_int32), ctypes.c_uint32,
+                                        ctypes.POINTER(ctypes.c_void_p)]),
+    ("tm_comm_destroy", None, [ctypes.c_void_p]),
+    ("tm_comm_uses_rccl", ctypes.c_int, [ctypes.c_void_p]),
+    ("tm_comm_last_error", ctypes.c_char_p, [ctypes.c_void_p]),
+    ("tm_shard_exchange", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(TmExchangeIn),
+                                         ctypes.POINTER(TmExchangeOut)]),
+    ("tm_shard_exchange_group", ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint32,
+                                               ctypes.POINTER(TmExchangeIn), ctypes.POINTER(TmExchangeOut)]),
     ("tm_route_add", ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p,
                                     ctypes.c_uint32]),
     ("tm_route_add_batch", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,

@@ -85,4 +85,10 @@ hipError_t launch_shard_merge(uint32_t S, uint32_t m, const uint32_t* counts, co
                               uint32_t* out_gid, uint64_t out_cap, uint64_t* total, uint64_t* pre, uint64_t* tmp,
                               hipStream_t st, uint32_t key_words = 1, uint64_t key_stride = 0);
 
+// exchange bookkeeping (shard.hip): out[d] = ids of topic slice d of a CSR
+// (offs[n+1]) cut S ways as b[d] = n*d/S, out[S+d] = the slice's first id;
+// and per-source totals of a received [S][m] counts block
+hipError_t launch_slice_sizes(const uint64_t* offs, uint32_t n, uint32_t S, uint64_t* out, hipStream_t st);
+hipError_t launch_source_totals(const uint32_t* counts, uint32_t m, uint32_t S, uint64_t* out, hipStream_t st);
+
 }  // namespace tmx

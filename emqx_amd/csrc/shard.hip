@@ -160,6 +160,46 @@ tm_shard_merge(uint32_t S, uint32_t m, const uint32_t* __restrict__ counts, cons
 
 static inline uint32_t mdiv_up(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
 
+// exchange bookkeeping: out[d] = ids of topic slice d (offs[b[d+1]] -
+// offs[b[d]]), out[S + d] = where slice d starts (offs[b[d]]), for
+// b[d] = n * d / S
+__global__ void tm_slice_sizes(const uint64_t* __restrict__ offs, uint32_t n, uint32_t S, uint64_t* __restrict__ out) {
+    const uint32_t d = threadIdx.x;
+    if (d >= S) return;
+    const uint64_t lo = offs[(uint64_t)n * d / S], hi = offs[(uint64_t)n * (d + 1) / S];
+    out[d] = hi - lo;
+    out[S + d] = lo;
+}
+
+// per-source totals of a received counts block [S][m] (one block per source)
+__global__ void __launch_bounds__(MBLOCK)
+tm_source_totals(const uint32_t* __restrict__ counts, uint32_t m, uint64_t* __restrict__ out) {
+    __shared__ uint64_t red[MBLOCK / 64];
+    const uint32_t s = blockIdx.x;
+    uint64_t x = 0;
+    for (uint32_t t = threadIdx.x; t < m; t += MBLOCK) x += counts[(uint64_t)s * m + t];
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t t = 0;
+        for (int i = 0; i < MBLOCK / 64; ++i) t += red[i];
+        out[s] = t;
+    }
+}
+
+hipError_t launch_slice_sizes(const uint64_t* offs, uint32_t n, uint32_t S, uint64_t* out, hipStream_t st) {
+    if (S == 0 || S > 64) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(tm_slice_sizes, dim3(1), dim3(64), 0, st, offs, n, S, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_source_totals(const uint32_t* counts, uint32_t m, uint32_t S, uint64_t* out, hipStream_t st) {
+    if (S == 0) return hipSuccess;
+    hipLaunchKernelGGL(tm_source_totals, dim3(S), dim3(MBLOCK), 0, st, counts, m, out);
+    return hipGetLastError();
+}
+
 hipError_t launch_shard_merge(uint32_t S, uint32_t m, const uint32_t* counts, const uint64_t* src_base,
                               const uint32_t* ids, const uint64_t* keys, uint32_t* out_count, uint64_t* out_off,
                               uint32_t* out_gid, uint64_t out_cap, uint64_t* total, uint64_t* pre, uint64_t* tmp,

@@ -1,5 +1,12 @@
 """Sharded mode of the topic-routing engine.
 
+The exchange runs natively over RCCL (emqx_amd/csrc/exchange.cpp):
+`Comm.init_rank` + `exchange_native` for one rank per process (the bench and
+a broker node with one OS process per GPU), `ShardSet` for all shards of one
+process (the C-ABI `tm_comm_init_all` / `tm_shard_exchange_group`; shards
+that share a GPU exchange by device copies).  `exchange` below is the
+torch.distributed form kept for the gloo CPU tests.
+
 When the filter set is partitioned over S GPUs (one process per GPU), every
 GPU holds the sub-trie of its shard (`tm_shard_of`: a hash of the filter's
 prefix through its second literal level, so Zipf-heavy root words and
@@ -164,3 +171,152 @@ def exchange(counts, offs, ids, keys, n, n_shards, rank, group=None, key_words=1
     base[1:] = np.cumsum(recv_items)[:-1]
     src_base = torch.from_numpy(base).to(dev)
     return recv_counts, src_base, recv_ids, recv_keys, m
+
+
+# ---------------------------------------------------------------------------
+# native RCCL exchange (exchange.cpp)
+
+class Comm:
+    """one rank's RCCL communicator (tm_comm)"""
+
+    def __init__(self, h, lib):
+        self.h, self.lib = h, lib
+
+    @staticmethod
+    def unique_id() -> bytes:
+        lib = L.load()
+        buf = (ctypes.c_uint8 * L.TM_COMM_ID_BYTES)()
+        rc = lib.tm_comm_unique_id(buf)
+        if rc != L.TM_OK:
+            raise L.TopicMatchError(rc, "tm_comm_unique_id")
+        return bytes(buf)
+
+    @classmethod
+    def init_rank(cls, uid: bytes, nranks: int, rank: int, device: int):
+        lib = L.load()
+        h = ctypes.c_void_p()
+        buf = (ctypes.c_uint8 * L.TM_COMM_ID_BYTES).from_buffer_copy(uid)
+        rc = lib.tm_comm_init_rank(buf, nranks, rank, device, ctypes.byref(h))
+        if rc != L.TM_OK:
+            raise L.TopicMatchError(rc, "tm_comm_init_rank")
+        return cls(h, lib)
+
+    @classmethod
+    def init_all(cls, devices):
+        lib = L.load()
+        n = len(devices)
+        hs = (ctypes.c_void_p * n)()
+        rc = lib.tm_comm_init_all((ctypes.c_int32 * n)(*devices), n, hs)
+        if rc != L.TM_OK:
+            raise L.TopicMatchError(rc, "tm_comm_init_all")
+        return [cls(ctypes.c_void_p(hs[i]), lib) for i in range(n)]
+
+    @property
+    def rccl(self):
+        return bool(self.lib.tm_comm_uses_rccl(self.h))
+
+    def close(self):
+        if self.h:
+            self.lib.tm_comm_destroy(self.h)
+            self.h = None
+
+
+def _xin(n, counts, offs, ids, keys, key_words, key_stride, stream):
+    p = lambda x: None if x is None else (x.data_ptr() if hasattr(x, "data_ptr") else int(x))  # noqa: E731
+    st = None if stream is None else (stream if isinstance(stream, int) else stream.cuda_stream)
+    return L.TmExchangeIn(n, key_words, p(counts), p(offs), p(ids), p(keys), key_stride, st)
+
+
+def exchange_native(comm, counts, offs, ids, keys, n, key_words=1, key_stride=0, stream=None):
+    """this rank's part of the all-to-all over RCCL; returns the received
+    (m, total, d_counts, d_src_base, d_ids, d_keys) device pointers (owned by
+    the comm, valid until its next exchange)"""
+    xin = _xin(n, counts, offs, ids, keys, key_words, key_stride, stream)
+    out = L.TmExchangeOut()
+    rc = comm.lib.tm_shard_exchange(comm.h, ctypes.byref(xin), ctypes.byref(out))
+    if rc != L.TM_OK:
+        raise L.TopicMatchError(rc, "tm_shard_exchange: " + comm.lib.tm_comm_last_error(comm.h).decode())
+    return out
+
+
+class ShardSet:
+    """All S shards of one process (one per device in `devices`, repeats
+    allowed): the filter set partitioned with tm_shard_of, every batch walked
+    by each shard with order keys, exchanged natively (RCCL between distinct
+    GPUs, device copies between shards sharing one) and merged per topic slice
+    on the slice's GPU.  match_batch returns the merged lists with global ids
+    (local * S + shard), in emqx_trie:match/1 order."""
+
+    def __init__(self, devices, filters_hint=0):
+        import torch
+        self.torch = torch
+        self.devices = list(devices)
+        self.S = len(self.devices)
+        self.engines = [ShardEngine(d, self.S, s, filters_hint=filters_hint // max(self.S, 1) + 1)
+                        for s, d in enumerate(self.devices)]
+        self.comms = Comm.init_all(self.devices)
+
+    def insert_many(self, buf, off):
+        for e in self.engines:
+            e.insert_many(buf, off)
+            e.commit()
+
+    def filter_bytes(self, gid: int) -> bytes:
+        return self.engines[gid % self.S].filter_bytes(gid // self.S)
+
+    def match_batch(self, tb, to):
+        """host batch -> (counts u32[n], offsets u64[n+1], gids u32[total])"""
+        torch = self.torch
+        S, n = self.S, len(to) - 1
+        KW = key_words_for(tb, to)
+        lists = []
+        for s, e in enumerate(self.engines):
+            dev = torch.device("cuda", self.devices[s])
+            d_b = torch.from_numpy(np.ascontiguousarray(tb).copy()).to(dev)
+            d_o = torch.from_numpy(np.ascontiguousarray(to).view(np.int64).copy()).to(dev)
+            c = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+            o = torch.empty(n + 1, dtype=torch.int64, device=dev)
+            t = torch.zeros(1, dtype=torch.int64, device=dev)
+            e.match_keys_device(d_b, d_o, n, int(to[-1]), c, o, None, None, 0, t, key_words=KW)
+            cap = int(t.item()) + 1
+            ids = torch.empty(cap, dtype=torch.int32, device=dev)
+            keys = torch.empty(cap * KW, dtype=torch.int64, device=dev)
+            e.match_keys_device(d_b, d_o, n, int(to[-1]), c, o, ids, keys, cap, t, key_words=KW)
+            torch.cuda.synchronize(dev)
+            if e.key_levels() > 32 * KW - 1:
+                raise RuntimeError("order keys too narrow for the batch")
+            lists.append((c, o, ids, keys, cap, d_b, d_o))
+        # the exchange and the merges run on each device's current torch stream
+        streams = [torch.cuda.current_stream(torch.device("cuda", d)) for d in self.devices]
+        ins = (L.TmExchangeIn * S)(*[_xin(n, c, o, ids, keys, KW, cap, streams[s])
+                                     for s, (c, o, ids, keys, cap, _, _) in enumerate(lists)])
+        outs = (L.TmExchangeOut * S)()
+        hs = (ctypes.c_void_p * S)(*[c.h.value for c in self.comms])
+        rc = self.comms[0].lib.tm_shard_exchange_group(hs, S, ins, outs)
+        if rc != L.TM_OK:
+            raise L.TopicMatchError(rc, "tm_shard_exchange_group: " +
+                                    self.comms[0].lib.tm_comm_last_error(self.comms[0].h).decode())
+        counts, offs, gids = [], [0], []
+        for r in range(S):
+            x = outs[r]
+            dev = torch.device("cuda", self.devices[r])
+            m = x.m
+            oc = torch.empty(max(m, 1), dtype=torch.int32, device=dev)
+            oo = torch.empty(m + 1, dtype=torch.int64, device=dev)
+            tot = torch.zeros(1, dtype=torch.int64, device=dev)
+            og = torch.empty(x.total + 1, dtype=torch.int32, device=dev)
+            # the merge runs on the comm's stream, after the exchange's copies
+            self.engines[r].merge_device(m, x.d_counts, x.d_src_base, x.d_ids, x.d_keys, oc, oo, og, x.total + 1,
+                                         tot, stream=streams[r], key_words=KW, key_stride=x.total)
+            torch.cuda.synchronize(dev)
+            counts.append(oc[:m].cpu().numpy().view(np.uint32))
+            offs.extend((oo[1:].cpu().numpy() + offs[-1]).tolist())
+            gids.append(og[: x.total].cpu().numpy().view(np.uint32))
+        return (np.concatenate(counts) if counts else np.zeros(0, np.uint32), np.asarray(offs, dtype=np.uint64),
+                np.concatenate(gids) if gids else np.zeros(0, np.uint32))
+
+    def close(self):
+        for c in self.comms:
+            c.close()
+        for e in self.engines:
+            e.close()

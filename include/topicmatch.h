@@ -232,6 +232,49 @@ int tm_shard_merge_w(tm_engine* e, uint32_t n_shards, uint32_t m, const uint32_t
                      uint64_t key_stride, uint32_t* d_out_count, uint64_t* d_out_off, uint32_t* d_out_gid,
                      uint64_t out_cap, uint64_t* d_total, void* hip_stream);
 
+/* ---- sharded-mode exchange over RCCL (exchange.cpp) ---------
+ * After the keyed walks, topic slice d (topics [n*d/S, n*(d+1)/S)) of every
+ * shard's lists goes to rank d (an all-to-all: each id crosses xGMI once),
+ * which merges them with tm_shard_merge_w.  A tm_comm is one rank's RCCL
+ * communicator: tm_comm_init_rank for one rank per process (rank 0 makes the
+ * id with tm_comm_unique_id and shares it, e.g. over torch.distributed),
+ * tm_comm_init_all for all ranks of one process (ranks that share a GPU,
+ * which RCCL refuses, exchange by device copies instead).  Receive buffers
+ * belong to the comm and stay valid until its next exchange. */
+#define TM_COMM_ID_BYTES 128
+typedef struct tm_comm tm_comm;
+typedef struct tm_exchange_in {
+    uint32_t n;                 /* topics of the batch (the same batch on every rank)      */
+    uint32_t key_words;         /* order key words per id                                   */
+    const uint32_t* d_counts;   /* n: this shard's list lengths                            */
+    const uint64_t* d_offs;     /* n + 1: CSR offsets                                      */
+    const uint32_t* d_ids;      /* local filter ids                                        */
+    const uint64_t* d_keys;     /* key_words planes, key_stride apart                      */
+    uint64_t key_stride;
+    void* hip_stream;           /* stream the lists were produced on (NULL: the comm's)    */
+} tm_exchange_in;
+typedef struct tm_exchange_out {
+    uint32_t m;                 /* topics of this rank's slice                             */
+    uint32_t reserved;
+    uint64_t total;             /* ids received                                            */
+    const uint32_t* d_counts;   /* [S][m], source-major                                    */
+    const uint64_t* d_src_base; /* S: where source s's ids / keys start                    */
+    const uint32_t* d_ids;      /* total                                                    */
+    const uint64_t* d_keys;     /* key_words planes of `total`                             */
+} tm_exchange_out;
+int  tm_comm_unique_id(uint8_t id[TM_COMM_ID_BYTES]);
+int  tm_comm_init_rank(const uint8_t id[TM_COMM_ID_BYTES], uint32_t nranks, uint32_t rank, int device,
+                       tm_comm** out);
+int  tm_comm_init_all(const int32_t* devices, uint32_t n, tm_comm** comms);
+void tm_comm_destroy(tm_comm* c);
+int  tm_comm_uses_rccl(tm_comm* c);   /* 1: RCCL, 0: device copies */
+const char* tm_comm_last_error(tm_comm* c);
+/* one rank (RCCL communicator) of a multi-process exchange; stream-ordered
+ * after two small host syncs that size the sends and receives */
+int  tm_shard_exchange(tm_comm* c, const tm_exchange_in* in, tm_exchange_out* out);
+/* all S ranks of one process at once (comms from tm_comm_init_all) */
+int  tm_shard_exchange_group(tm_comm** comms, uint32_t S, const tm_exchange_in* ins, tm_exchange_out* outs);
+
 /* ---- routes: the emqx_route bag and emqx_router:match_routes/1 -------------
  * A route is (topic, dest) (#route{topic, dest}, include/emqx.hrl:84-87); dest
  * is opaque bytes (the NIF passes term_to_binary(node() | {Group, node()})),

@@ -5,6 +5,9 @@ import this package, and only as the checker (never the thing measured on the
 GPU, never a fallback of the product path).
 
     O1      faithful C restatement of emqx_trie (oracle/o1_trie.c)
+    O3      the same algorithm over interned word ids and dense node ids
+            (oracle/o3_interned.c): the "optimized C++ variant" leg of the
+            CPU baseline, checked against O1
     o2_*    brute-force emqx_topic:match/2 scans (same file)
     pytrie  independent pure-Python transcription (oracle/pytrie.py)
 
@@ -47,6 +50,10 @@ def load():
         "o1_node_count": (U64, [V]),
         "o1_edge_count": (U64, [V]),
         "o2_topic_match": (I, [ctypes.c_char_p, U32, ctypes.c_char_p, U32]),
+        "o3_new": (V, [U64]),
+        "o3_free": (None, [V]),
+        "o3_insert_batch": (None, [V, V, V, U32]),
+        "o3_match_batch": (ctypes.c_double, [V, V, V, U32, I, V, V, V, ctypes.POINTER(U64)]),
         "o2_match": (U32, [V, V, U32, ctypes.c_char_p, U32, V, U32]),
     }
     for name, (res, args) in sig.items():
@@ -152,3 +159,50 @@ def o2_topic_match(name: bytes, filt: bytes) -> bool:
 def o2_match(filters, topic: bytes):
     """brute force over a list of filters -> set of matching filters"""
     return {f for f in filters if o2_topic_match(topic, f)}
+
+
+class O3:
+    """emqx_trie:match/1 over interned ids (oracle/o3_interned.c): the
+    optimized CPU baseline leg; insert-only."""
+
+    def __init__(self, hint=0):
+        self.lib = load()
+        self.h = self.lib.o3_new(hint)
+
+    def close(self):
+        if self.h:
+            self.lib.o3_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def insert_many(self, buf, off):
+        buf = np.ascontiguousarray(buf, dtype=np.uint8)
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        self.lib.o3_insert_batch(self.h, _p(buf), _p(off), len(off) - 1)
+
+    def match_batch(self, buf, off, threads=1):
+        """-> (seconds, total_matches)"""
+        buf = np.ascontiguousarray(buf, dtype=np.uint8)
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        tm = ctypes.c_uint64()
+        secs = self.lib.o3_match_batch(self.h, _p(buf), _p(off), len(off) - 1, threads, None, None, None,
+                                       ctypes.byref(tm))
+        return secs, tm.value
+
+    def match_ids(self, buf, off, threads=1):
+        """CSR of filter indices (first-insertion order) in reference order"""
+        buf = np.ascontiguousarray(buf, dtype=np.uint8)
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        n = len(off) - 1
+        counts = np.zeros(max(n, 1), dtype=np.uint32)
+        self.lib.o3_match_batch(self.h, _p(buf), _p(off), n, threads, _p(counts), None, None, None)
+        offs = np.zeros(n + 1, dtype=np.uint64)
+        offs[1:] = np.cumsum(counts[:n], dtype=np.uint64)
+        ids = np.zeros(max(int(offs[-1]), 1), dtype=np.uint32)
+        self.lib.o3_match_batch(self.h, _p(buf), _p(off), n, threads, None, _p(offs), _p(ids), None)
+        return counts[:n], offs, ids[: int(offs[-1])]

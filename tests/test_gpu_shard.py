@@ -142,3 +142,76 @@ def test_sharded_32_to_64_levels_equals_o1(gpu_device, S):
     assert sum(len(w) for w in want) > 1000 and max(len(w) for w in want) > 8
     assert _run_sharded(filters, topics, S) == want
     assert _run_sharded(filters, topics, S, K=4) == want   # re-walk tail with wide keys
+
+
+@pytest.mark.parametrize("S", [2, 3])
+def test_shardset_native_exchange_equals_o1(gpu_device, S):
+    """all shards of one process through the C-ABI exchange
+    (tm_comm_init_all + tm_shard_exchange_group; the shards share GPU 0, so
+    it moves the lists by device copies) and the device merge"""
+    from emqx_amd import shard
+    from emqx_amd import workload as W
+    from emqx_amd.engine import pack
+    from long_topics import long_case
+    filters = W.unpack(*W.filters(1))
+    topics = W.unpack(*W.topics(1, n=8000))
+    lf, lt = long_case(5, n_filters=600, n_topics=100)
+    filters, topics = filters + lf, topics + lt
+    fb, fo = pack(filters)
+    tb, to = pack(topics)
+    ss = shard.ShardSet([gpu_device] * S)
+    assert not any(c.rccl for c in ss.comms)
+    ss.insert_many(fb, fo)
+    counts, offs, gids = ss.match_batch(tb, to)
+    want = _o1(filters, topics)
+    got = [[ss.filter_bytes(int(g)) for g in gids[offs[t]:offs[t + 1]]] for t in range(len(topics))]
+    assert got == want
+    ss.close()
+
+
+def test_rccl_one_rank_exchange_equals_o1(gpu_device):
+    """the RCCL path of tm_shard_exchange on the one GPU of the box: a
+    one-rank communicator (send / receive to itself inside ncclGroup), then
+    the merge"""
+    import torch
+    from emqx_amd import shard
+    from emqx_amd import workload as W
+    from emqx_amd.engine import pack
+    filters = W.unpack(*W.filters(1))
+    topics = W.unpack(*W.topics(1, n=5000))
+    fb, fo = pack(filters)
+    tb, to = pack(topics)
+    comm = shard.Comm.init_rank(shard.Comm.unique_id(), 1, 0, gpu_device)
+    assert comm.rccl
+    e = shard.ShardEngine(gpu_device, 1, 0)
+    e.insert_many(fb, fo)
+    dev = torch.device("cuda", gpu_device)
+    n = len(topics)
+    d_b = torch.from_numpy(tb.copy()).to(dev)
+    d_o = torch.from_numpy(to.view(np.int64).copy()).to(dev)
+    c = torch.empty(n, dtype=torch.int32, device=dev)
+    o = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    t = torch.zeros(1, dtype=torch.int64, device=dev)
+    e.match_keys_device(d_b, d_o, n, int(to[-1]), c, o, None, None, 0, t)
+    cap = int(t.item()) + 1
+    ids = torch.empty(cap, dtype=torch.int32, device=dev)
+    keys = torch.empty(cap, dtype=torch.int64, device=dev)
+    st = torch.cuda.current_stream(dev)
+    e.match_keys_device(d_b, d_o, n, int(to[-1]), c, o, ids, keys, cap, t, stream=st)
+    x = shard.exchange_native(comm, c, o, ids, keys, n, key_words=1, key_stride=cap, stream=st)
+    assert x.m == n and x.total == cap - 1
+    oc = torch.empty(n, dtype=torch.int32, device=dev)
+    oo = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    tot = torch.zeros(1, dtype=torch.int64, device=dev)
+    og = torch.empty(cap, dtype=torch.int32, device=dev)
+    e.merge_device(n, x.d_counts, x.d_src_base, x.d_ids, x.d_keys, oc, oo, og, cap, tot, stream=st,
+                   key_words=1, key_stride=x.total)
+    torch.cuda.synchronize()
+    from oracle import O1
+    o1 = O1()
+    o1.insert_many(fb, fo)
+    wc, wo, wi = o1.match_ids(tb, to, threads=4)
+    assert np.array_equal(oo.cpu().numpy().view(np.uint64), wo)
+    assert np.array_equal(og[: int(wo[-1])].cpu().numpy().view(np.uint32), wi)
+    comm.close()
+    e.close()

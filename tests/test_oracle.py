@@ -5,11 +5,14 @@ restatements of emqx_trie; both must reproduce every known-answer test of the
 reference suites (tests/golden/kat_*.json) and agree with each other and with
 brute-force emqx_topic:match/2 (O2) on randomized tries.
 """
+import os
 import random
 
 import pytest
 
 from oracle import O1, o2_topic_match, pytrie
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 L1 = "latin-1"
 
@@ -155,3 +158,29 @@ def test_o1_delete_matches_pytrie_random():
             for k in range(1, len(parts) + 1):
                 nid = b("/".join(parts[:k]))
                 assert o1.lookup(nid) == py.lookup(nid), nid
+
+
+def test_o3_interned_equals_o1():
+    """the optimized CPU baseline leg (oracle/o3_interned.c) returns O1's
+    ordered lists: C1, a C5 sample ($ topics, '#'-heavy, fan-out > 500) and
+    the O1 vectors (empty levels, 31-41 levels)"""
+    import json
+    import numpy as np
+    from emqx_amd import emqx_topic as T
+    from emqx_amd import workload as W
+    from emqx_amd.engine import pack
+    from oracle import O1, O3
+    cases = [(W.filters(1), W.topics(1, n=20000))]
+    f5 = [T.parse(f)[0] for f in W.unpack(*W.filters(5, n=30000))]
+    cases.append((pack(list(dict.fromkeys(f5))), W.topics(5, n=300)))
+    g = json.load(open(os.path.join(ROOT, "tests", "golden", "o1_vectors.json")))
+    for vec in g["vectors"] if isinstance(g, dict) and "vectors" in g else g:
+        fs = list(dict.fromkeys(f.encode("latin-1") for f in vec["filters"]))
+        cases.append((pack(fs), pack([r["topic"].encode("latin-1") for r in vec["topics"]])))
+    for (fb, fo), (tb, to) in cases:
+        o1, o3 = O1(), O3()
+        o1.insert_many(fb, fo)
+        o3.insert_many(fb, fo)
+        a = o1.match_ids(tb, to, threads=4)
+        b = o3.match_ids(tb, to, threads=4)
+        assert all(np.array_equal(x, y) for x, y in zip(a, b))

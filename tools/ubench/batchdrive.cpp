@@ -1,0 +1,74 @@
+// batchdrive.cpp — measurement helper (not product code): drives an
+// engine's micro-batcher (tm_batcher_*) the way the NIF does — P producer
+// threads, one tm_batcher_submit per publish, a completion callback per
+// topic — over a packed topic batch, and reports end-to-end topics/s and
+// submit->callback latency.  bench.py loads it with ctypes to add the
+// batcher leg (PCIe and host threads included) to its line.
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <thread>
+#include <vector>
+
+#include "../../include/topicmatch.h"
+
+namespace {
+using clk = std::chrono::steady_clock;
+struct Rec {
+    clk::time_point t0;
+    int64_t lat_ns = -1;
+    uint32_t n = 0;
+};
+void on_done(void* ctx, uint64_t, int status, const uint32_t*, const uint32_t*, uint32_t n) {
+    Rec* r = (Rec*)ctx;
+    r->n = status == TM_OK ? n : 0xFFFFFFFFu;
+    r->lat_ns = std::chrono::duration_cast<std::chrono::nanoseconds>(clk::now() - r->t0).count();
+}
+}  // namespace
+
+// out[8]: seconds, topics/s, batches, mean batch, p50 us, p99 us, failed, matches
+extern "C" int tm_bench_batcher(tm_engine* e, const uint8_t* tb, const uint64_t* to, uint64_t nt, int producers,
+                                uint32_t deadline_us, uint32_t max_topics, uint32_t lanes, uint32_t flags,
+                                double* out) {
+    tm_batcher_config bc{};
+    bc.max_topics = max_topics;
+    bc.deadline_us = deadline_us;
+    bc.lanes_per_replica = lanes;
+    bc.flags = flags;
+    tm_batcher* b;
+    int rc = tm_batcher_open(e, &bc, &b);
+    if (rc != TM_OK) return rc;
+    std::vector<Rec> recs(nt);
+    const auto t0 = clk::now();
+    std::vector<std::thread> th;
+    for (int k = 0; k < producers; ++k)
+        th.emplace_back([&, k] {
+            for (uint64_t i = k; i < nt; i += producers) {
+                recs[i].t0 = clk::now();
+                tm_batcher_submit(b, tb + to[i], (uint32_t)(to[i + 1] - to[i]), on_done, &recs[i], nullptr);
+            }
+        });
+    for (auto& x : th) x.join();
+    tm_batcher_flush(b);
+    const double secs = std::chrono::duration<double>(clk::now() - t0).count();
+    tm_batcher_stats st;
+    tm_batcher_get_stats(b, &st);
+    tm_batcher_close(b);
+    std::vector<int64_t> lat(nt);
+    uint64_t fails = 0, ids = 0;
+    for (uint64_t i = 0; i < nt; ++i) {
+        lat[i] = recs[i].lat_ns;
+        if (recs[i].n == 0xFFFFFFFFu) ++fails;
+        else ids += recs[i].n;
+    }
+    std::sort(lat.begin(), lat.end());
+    out[0] = secs;
+    out[1] = nt / secs;
+    out[2] = (double)st.batches;
+    out[3] = (double)st.topics / (st.batches ? st.batches : 1);
+    out[4] = lat[(size_t)(0.5 * (nt - 1))] / 1e3;
+    out[5] = lat[(size_t)(0.99 * (nt - 1))] / 1e3;
+    out[6] = (double)fails;
+    out[7] = (double)ids;
+    return TM_OK;
+}
