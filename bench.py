@@ -382,18 +382,27 @@ def host_legs(a, eng, batch, total):
     tb, to = batch
     n = len(to) - 1
     out = {}
-    eng.match_batch(tb, to)   # warm the host-path workspace
+    # the caller stages topics and receives counts / offsets in pinned host
+    # memory (as the batcher's lanes do); the ids come back into the
+    # library's pinned output pool (tm_match_batch_owned)
+    ptb = torch.from_numpy(tb).pin_memory().numpy()
+    pto = torch.from_numpy(to.view(np.int64)).pin_memory().numpy().view(np.uint64)
+    pc = torch.empty(n, dtype=torch.int32).pin_memory().numpy().view(np.uint32)
+    po = torch.empty(n + 1, dtype=torch.int64).pin_memory().numpy().view(np.uint64)
+    counts, offs, ids = eng.match_batch(ptb, pto, counts=pc, offs=po, keep=True)   # warm the workspace
+    del ids
     reps = 3
     t0 = time.perf_counter()
     for _ in range(reps):
-        counts, offs, ids = eng.match_batch(tb, to)
+        counts, offs, ids = eng.match_batch(ptb, pto, counts=pc, offs=po, keep=True)
+        del ids
     secs = (time.perf_counter() - t0) / reps
     assert int(offs[-1]) == total
     moved = int(to[-1]) + 8 * (n + 1) + 4 * n + 8 * (n + 1) + 4 * total
     out["host_path"] = {"topics_per_s": n / secs, "ms_per_batch": secs * 1e3, "topics": n,
                         "pcie_bytes": moved, "pcie_gbs": moved / secs / 1e9,
-                        "path": "tm_match_batch: host topics -> HBM -> walk -> ids back to host (one library-sized "
-                                "read-back), PCIe both ways included"}
+                        "path": "tm_match_batch_owned: pinned host topics -> HBM -> walk -> counts, offsets and ids "
+                                "back to pinned host memory (one library-sized read-back), PCIe both ways included"}
     log("host path: %.0f topics/s, %.2f ms per %d-topic batch, %.1f GB/s over PCIe" % (
         n / secs, secs * 1e3, n, moved / secs / 1e9))
     lib_path = os.path.join(ROOT, "tools", "ubench", "libbatchdrive.so")

@@ -49,11 +49,18 @@ struct Req {
     uint64_t ticket;
 };
 
+// A producer thread appends to its own stripe; everything a submit touches
+// lives in the stripe's cache lines (no shared counter is written per
+// publish): its lock, its buffers, its pending count / bytes, the arrival
+// time of its oldest topic and its ticket sequence.
 struct alignas(64) Stripe {
     std::mutex mu;
     std::vector<uint8_t> bytes;
     std::vector<uint32_t> lens;
     std::vector<Req> reqs;
+    std::atomic<uint64_t> pending{0}, pending_bytes{0};
+    std::atomic<int64_t> first_ns{INT64_MAX};   // INT64_MAX: empty
+    uint64_t seq = 0;                           // under mu
 };
 
 // pinned host buffer / device buffer that only grow
@@ -122,8 +129,8 @@ struct tm_batcher {
     tm_batcher_config cfg{};
     bool host_only = false;
     Stripe stripes[NSTRIPE];
-    std::atomic<uint64_t> pending{0}, pending_bytes{0}, next_ticket{1};
-    std::atomic<int64_t> first_ns{0};
+    std::atomic<bool> sealer_idle{false};   // the sealer sleeps with nothing pending: the next submit wakes it
+    std::atomic<bool> force{false};         // flush: seal whatever is pending now
 
     std::mutex mu;                    // sealer state, stats, wake-ups, lane hand-over
     std::condition_variable cv_work, cv_idle, cv_lane;
@@ -143,11 +150,26 @@ struct tm_batcher {
 
     int64_t now_ns() const { return std::chrono::duration_cast<std::chrono::nanoseconds>(clk::now().time_since_epoch()).count(); }
 
+    // pending topics / bytes over the stripes and the oldest arrival
+    uint64_t pending(uint64_t* bytes = nullptr, int64_t* oldest = nullptr) const {
+        uint64_t n = 0, b = 0;
+        int64_t o = INT64_MAX;
+        for (const Stripe& x : stripes) {
+            n += x.pending.load(std::memory_order_seq_cst);
+            b += x.pending_bytes.load(std::memory_order_relaxed);
+            o = std::min<int64_t>(o, x.first_ns.load(std::memory_order_acquire));
+        }
+        if (bytes) *bytes = b;
+        if (oldest) *oldest = o;
+        return n;
+    }
     bool due() const {
-        const uint64_t n = pending.load(std::memory_order_acquire);
+        uint64_t b;
+        int64_t o;
+        const uint64_t n = pending(&b, &o);
         if (n == 0) return false;
-        if (n >= cfg.max_topics || pending_bytes.load(std::memory_order_relaxed) >= cfg.max_bytes) return true;
-        return now_ns() - first_ns.load(std::memory_order_acquire) >= (int64_t)cfg.deadline_us * 1000;
+        if (n >= cfg.max_topics || b >= cfg.max_bytes || force.load(std::memory_order_acquire)) return true;
+        return now_ns() - o >= (int64_t)cfg.deadline_us * 1000;
     }
 
     // move stripes' topics (oldest first, up to max_topics) into lane L's
@@ -185,11 +207,12 @@ struct tm_batcher {
             }
             nb += t.bytes.size();
             n += t.lens.size();
-            // pending is counted under this lock: subtract while holding it
-            pending.fetch_sub(t.lens.size(), std::memory_order_acq_rel);
-            pending_bytes.fetch_sub(t.bytes.size(), std::memory_order_relaxed);
+            // pending is counted under this lock: subtract while holding it;
+            // topics left behind keep their stripe's first_ns (due at once)
+            x.pending.fetch_sub(t.lens.size(), std::memory_order_acq_rel);
+            x.pending_bytes.fetch_sub(t.bytes.size(), std::memory_order_relaxed);
+            if (x.lens.empty()) x.first_ns.store(INT64_MAX, std::memory_order_release);
         }
-        // topics left behind keep their first_ns: they are due at once
         L.n = (uint32_t)n;
         if (host_only || !L.h_bytes.ensure(nb + 16) || !L.h_off.ensure((n + 1) * 8)) {
             L.oom = !host_only;
@@ -320,7 +343,7 @@ struct tm_batcher {
                 cv_lane.wait(lk, [&] { return !free_lanes.empty(); });
                 const int li = free_lanes.back();
                 free_lanes.pop_back();
-                if (pending.load() >= cfg.max_topics) st.size_seals++;
+                if (pending() >= cfg.max_topics) st.size_seals++;
                 else st.deadline_seals++;
                 ++sealing;
                 lk.unlock();
@@ -336,13 +359,19 @@ struct tm_batcher {
                 ++in_flight;
                 continue;
             }
-            if (pending.load(std::memory_order_acquire) == 0) {
+            int64_t oldest;
+            if (pending(nullptr, &oldest) == 0) {
+                force.store(false, std::memory_order_release);
                 cv_idle.notify_all();
                 if (stop) return;
-                sleep_for(lk, std::chrono::milliseconds(50));
+                // seq_cst store then re-check: either the submitter's pending++
+                // is seen here, or its exchange() sees idle and wakes us
+                sealer_idle.store(true, std::memory_order_seq_cst);
+                if (pending() == 0) sleep_for(lk, std::chrono::milliseconds(50));
+                sealer_idle.store(false, std::memory_order_release);
             } else {
-                const int64_t left = first_ns.load() + (int64_t)cfg.deadline_us * 1000 - now_ns();
-                if (left > 0) sleep_for(lk, std::chrono::nanoseconds(left));
+                const int64_t left = oldest + (int64_t)cfg.deadline_us * 1000 - now_ns();
+                if (left > 0) sleep_for(lk, std::chrono::nanoseconds(std::min<int64_t>(left, 1000000)));
             }
         }
     }
@@ -431,23 +460,23 @@ int tm_batcher_submit(tm_batcher* b, const uint8_t* topic, uint32_t len, tm_batc
                       uint64_t* ticket_out) {
     if (!b || !fn || (!topic && len)) return TM_EINVAL;
     if (t_stripe < 0) t_stripe = (int)(g_stripe_rr.fetch_add(1, std::memory_order_relaxed) % NSTRIPE);
-    const uint64_t t = b->next_ticket.fetch_add(1, std::memory_order_relaxed);
     Stripe& s = b->stripes[t_stripe];
-    uint64_t was;
+    uint64_t t, was;
     {
         std::lock_guard<std::mutex> lk(s.mu);
+        t = ++s.seq * NSTRIPE + (uint64_t)t_stripe;   // unique per batcher, no shared counter
         s.bytes.insert(s.bytes.end(), topic, topic + len);
         s.lens.push_back(len);
         s.reqs.push_back(Req{fn, ctx, t});
-        b->pending_bytes.fetch_add(len, std::memory_order_relaxed);
-        was = b->pending.fetch_add(1, std::memory_order_acq_rel);
-        if (was == 0) b->first_ns.store(b->now_ns(), std::memory_order_release);
+        s.pending_bytes.fetch_add(len, std::memory_order_relaxed);
+        was = s.pending.fetch_add(1, std::memory_order_seq_cst);
+        if (was == 0) s.first_ns.store(b->now_ns(), std::memory_order_release);
     }
-    if (was == 0) {
-        b->kick();   // arm the deadline
-    } else if (was + 1 == b->cfg.max_topics) {
-        b->kick();   // full
-    }
+    // wake the sealer only when it sleeps with nothing pending (it times the
+    // deadline itself), or when this stripe alone could fill a batch
+    if ((was == 0 && b->sealer_idle.exchange(false, std::memory_order_seq_cst)) ||
+        was + 1 == b->cfg.max_topics / NSTRIPE)
+        b->kick();
     if (ticket_out) *ticket_out = t;
     return TM_OK;
 }
@@ -455,10 +484,10 @@ int tm_batcher_submit(tm_batcher* b, const uint8_t* topic, uint32_t len, tm_batc
 int tm_batcher_flush(tm_batcher* b) {
     if (!b) return TM_EINVAL;
     std::unique_lock<std::mutex> lk(b->mu);
-    // everything submitted before this call completes: force the deadline now
-    b->first_ns.store(0, std::memory_order_release);
+    // everything submitted before this call completes: force the seal now
+    b->force.store(true, std::memory_order_release);
     b->cv_work.notify_one();
-    b->cv_idle.wait(lk, [b] { return b->pending.load() == 0 && b->sealing == 0 && b->in_flight == 0; });
+    b->cv_idle.wait(lk, [b] { return b->pending() == 0 && b->sealing == 0 && b->in_flight == 0; });
     return TM_OK;
 }
 

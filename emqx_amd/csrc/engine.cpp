@@ -22,6 +22,7 @@
 #include <condition_variable>
 #include <cstring>
 #include <functional>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <new>
@@ -1619,6 +1620,50 @@ struct tm_engine {
 // ---------------------------------------------------------------------------
 namespace {
 
+// Pinned host memory for library-sized outputs (tm_match_batch_owned): the
+// lists come back over PCIe by DMA straight into them, and tm_free returns a
+// block to a small pool for the next batch instead of unpinning it.
+struct PinnedPool {
+    std::mutex mu;
+    std::unordered_map<void*, size_t> live;   // handed out: pointer -> bytes
+    std::multimap<size_t, void*> spare;       // returned, kept pinned
+    size_t spare_bytes = 0;
+    static constexpr size_t SPARE_MAX = 8ull << 30;
+    void* get(size_t need) {
+        std::lock_guard<std::mutex> lk(mu);
+        auto it = spare.lower_bound(need);
+        if (it != spare.end() && it->first <= need * 2) {
+            void* p = it->second;
+            live[p] = it->first;
+            spare_bytes -= it->first;
+            spare.erase(it);
+            return p;
+        }
+        void* p = nullptr;
+        const size_t want = std::max<size_t>(need + need / 4, 4096);
+        if (hipHostMalloc(&p, want, hipHostMallocPortable) != hipSuccess) return nullptr;
+        live[p] = want;
+        return p;
+    }
+    bool put(void* p) {
+        std::lock_guard<std::mutex> lk(mu);
+        auto it = live.find(p);
+        if (it == live.end()) return false;
+        const size_t b = it->second;
+        live.erase(it);
+        spare.emplace(b, p);
+        spare_bytes += b;
+        while (spare_bytes > SPARE_MAX && !spare.empty()) {   // drop the largest spare blocks
+            auto last = std::prev(spare.end());
+            spare_bytes -= last->first;
+            (void)hipHostFree(last->second);
+            spare.erase(last);
+        }
+        return true;
+    }
+};
+PinnedPool g_pinned;
+
 template <class F>
 int guarded(tm_engine* e, F&& f) {
     if (!e) return TM_EINVAL;
@@ -1933,7 +1978,6 @@ int host_batch(tm_engine* e, BatchKind kind, const uint8_t* topic_bytes, const u
     const size_t R = std::min<size_t>(e->devs.size(), n);
     const uint32_t planes = kind == K_MATCH ? 1u : 2u;
     std::vector<uint64_t> tot(R, 0), icap(R, 0);
-    std::vector<std::vector<uint64_t>> loff(R);
     std::vector<tm_batch_stats> st(R);
     auto slice = [&](size_t i, uint32_t& lo, uint32_t& hi) {
         lo = (uint32_t)((uint64_t)n * i / R);
@@ -1994,17 +2038,19 @@ int host_batch(tm_engine* e, BatchKind kind, const uint8_t* topic_bytes, const u
         if (kind != K_MATCH) d.rw_release(s);
         tot[i] = total;
         icap[i] = cap;
-        loff[i].resize(m + 1);
+        // straight into the caller's arrays (DMA when they are pinned): the
+        // slice's local offsets, rebased below once every total is known
         HIPCHK(hipMemcpyAsync(out_count + lo, d.w_counts.p, (size_t)m * 4, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipMemcpyAsync(loff[i].data(), d.w_outoff.p, (size_t)(m + 1) * 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(out_off + lo, d.w_outoff.p, (size_t)m * 8, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
         if (e->stats_enabled && kind == K_MATCH) st[i] = e->read_stats(d, m);
     });
     std::vector<uint64_t> pre(R + 1, 0);
     for (size_t i = 0; i < R; ++i) pre[i + 1] = pre[i] + tot[i];
     const uint64_t total = pre[R];
-    if (out_alloc) {
-        *out_alloc = (uint32_t*)std::malloc(std::max<uint64_t>(total, 1) * 4);
+    if (out_alloc) {   // pinned (DMA target), else pageable
+        *out_alloc = (uint32_t*)g_pinned.get(std::max<uint64_t>(total, 1) * 4);
+        if (!*out_alloc) *out_alloc = (uint32_t*)std::malloc(std::max<uint64_t>(total, 1) * 4);
         if (!*out_alloc) throw std::bad_alloc();
         out_a = *out_alloc;
         out_cap = total;
@@ -2013,7 +2059,8 @@ int host_batch(tm_engine* e, BatchKind kind, const uint8_t* topic_bytes, const u
         DevState& d = *e->devs[i];
         uint32_t lo, hi;
         slice(i, lo, hi);
-        for (uint32_t j = 0; j < hi - lo; ++j) out_off[lo + j] = pre[i] + loff[i][j];
+        if (pre[i])
+            for (uint32_t j = lo; j < hi; ++j) out_off[j] += pre[i];
         // the workspace holds min(total, cap) entries; past out_cap the call
         // reports TM_ENOSPC and copies what fits both
         const uint64_t room = out_cap > pre[i] ? out_cap - pre[i] : 0;
@@ -2051,7 +2098,9 @@ int tm_match_batch_owned(tm_engine* e, const uint8_t* topic_bytes, const uint64_
     });
 }
 
-void tm_free(void* p) { std::free(p); }
+void tm_free(void* p) {
+    if (p && !g_pinned.put(p)) std::free(p);
+}
 
 int tm_match_batch(tm_engine* e, const uint8_t* topic_bytes, const uint64_t* topic_off, uint32_t n,
                    uint32_t* out_count, uint64_t* out_off, uint32_t* out_ids, uint64_t out_cap,

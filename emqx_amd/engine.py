@@ -129,21 +129,31 @@ class Engine:
         return self.lib.tm_image_bytes(self.h)
 
     # -- emqx_trie:match/1 over a batch ------------------------------------
-    def match_batch(self, buf, off, out_cap=None):
-        """Host batch -> (counts u32[n], offsets u64[n+1], filter ids u32[total])."""
+    def match_batch(self, buf, off, out_cap=None, counts=None, offs=None, keep=False):
+        """Host batch -> (counts u32[n], offsets u64[n+1], filter ids u32[total]).
+        counts / offs: caller arrays to fill (e.g. pinned); keep=True returns
+        the ids as a view of the library's pinned output buffer, released
+        when the array is garbage-collected (no copy)."""
         buf = np.ascontiguousarray(buf, dtype=np.uint8)
         off = np.ascontiguousarray(off, dtype=np.uint64)
         n = len(off) - 1
-        counts = np.zeros(max(n, 1), dtype=np.uint32)
-        offs = np.zeros(n + 1, dtype=np.uint64)
+        counts = np.zeros(max(n, 1), dtype=np.uint32) if counts is None else counts
+        offs = np.zeros(n + 1, dtype=np.uint64) if offs is None else offs
         if out_cap is None:   # library-sized output: one walk, no retry (tm_match_batch_owned)
             p, total = ctypes.c_void_p(), ctypes.c_uint64()
             rc = self.lib.tm_match_batch_owned(self.h, _ptr(buf), _ptr(off), n, _ptr(counts), _ptr(offs),
                                                ctypes.byref(p), ctypes.byref(total))
-            try:
+            if rc != L.TM_OK:
+                self.lib.tm_free(p)
                 self._check(rc, "tm_match_batch_owned")
-                k = int(total.value)
-                ids = np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(ctypes.c_uint32)), shape=(max(k, 1),))
+            k = int(total.value)
+            ids = np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(ctypes.c_uint32)), shape=(max(k, 1),))
+            if keep:
+                import weakref
+                view = ids[:k]
+                weakref.finalize(view, self.lib.tm_free, ctypes.c_void_p(p.value))
+                return counts[:n], offs, view
+            try:
                 return counts[:n], offs, ids[:k].copy()
             finally:
                 self.lib.tm_free(p)

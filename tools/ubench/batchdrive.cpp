@@ -41,9 +41,9 @@ extern "C" int tm_bench_batcher(tm_engine* e, const uint8_t* tb, const uint64_t*
     std::vector<Rec> recs(nt);
     const auto t0 = clk::now();
     std::vector<std::thread> th;
-    for (int k = 0; k < producers; ++k)
+    for (int k = 0; k < producers; ++k)   // contiguous blocks: no false sharing between producers
         th.emplace_back([&, k] {
-            for (uint64_t i = k; i < nt; i += producers) {
+            for (uint64_t i = nt * k / producers; i < nt * (k + 1) / producers; ++i) {
                 recs[i].t0 = clk::now();
                 tm_batcher_submit(b, tb + to[i], (uint32_t)(to[i + 1] - to[i]), on_done, &recs[i], nullptr);
             }
