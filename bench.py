@@ -205,7 +205,7 @@ def main():
     batches = make_batches(a, cfg, rank, world)
     log("rank %d: %d batches of %d topics generated in %.1fs" % (rank, len(batches), len(batches[0][1]) - 1,
                                                                  time.time() - t0))
-    st = torch.cuda.current_stream(dev)
+    st = torch.cuda.Stream(device=dev)   # explicit (handle 0 would select the engine's own stream)
     dbat = []
     for tb, to in batches:
         n = len(to) - 1
@@ -529,7 +529,9 @@ def main_sharded(a, rank, world, local, dev):
     d_c = torch.empty(n, dtype=torch.int32, device=dev)
     d_oo = torch.empty(n + 1, dtype=torch.int64, device=dev)
     d_t = torch.zeros(1, dtype=torch.int64, device=dev)
-    st = torch.cuda.current_stream(dev)
+    # one explicit stream orders walk -> RCCL exchange -> merge (the legacy
+    # default stream's handle 0 would select the engine's / comm's own)
+    st = torch.cuda.Stream(device=dev)
 
     eng.set_stats(True)
     eng.match_keys_device(d_b, d_o, n, nbytes, d_c, d_oo, None, None, 0, d_t, stream=st, key_words=KW)

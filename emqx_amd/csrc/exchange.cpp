@@ -72,7 +72,7 @@ struct tm_comm {
     Buf sizes;                    // 2S u64: send counts per destination, then their first ids
     Buf rsizes;                   // S u64: ids to receive from each source
     Buf recv_counts, src_base, recv_ids, recv_keys;
-    std::vector<uint64_t> h_send, h_recv;
+    std::vector<uint64_t> h_send, h_recv, h_base;   // h_base: source of the async src_base upload
     std::string last_error;
 };
 
@@ -113,7 +113,8 @@ int send_sizes(tm_comm* c, const tm_exchange_in& in) {
 int alloc_recv(tm_comm* c, const tm_exchange_in& in, tm_exchange_out& out) {
     const uint32_t S = c->nranks;
     const uint32_t m = slice_lo(in.n, S, c->rank + 1) - slice_lo(in.n, S, c->rank);
-    std::vector<uint64_t> base(S, 0);
+    std::vector<uint64_t>& base = c->h_base;   // outlives the async upload below
+    base.assign(S, 0);
     uint64_t tot = 0;
     for (uint32_t s = 0; s < S; ++s) {
         base[s] = tot;

@@ -270,6 +270,9 @@ class ShardSet:
         S, n = self.S, len(to) - 1
         KW = key_words_for(tb, to)
         lists = []
+        # one explicit stream per shard orders walk -> exchange -> merge (the
+        # legacy default stream, handle 0, would mean "the engine's stream")
+        streams = [torch.cuda.Stream(device=torch.device("cuda", d)) for d in self.devices]
         for s, e in enumerate(self.engines):
             dev = torch.device("cuda", self.devices[s])
             d_b = torch.from_numpy(np.ascontiguousarray(tb).copy()).to(dev)
@@ -277,17 +280,17 @@ class ShardSet:
             c = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
             o = torch.empty(n + 1, dtype=torch.int64, device=dev)
             t = torch.zeros(1, dtype=torch.int64, device=dev)
-            e.match_keys_device(d_b, d_o, n, int(to[-1]), c, o, None, None, 0, t, key_words=KW)
+            st = streams[s]
+            e.match_keys_device(d_b, d_o, n, int(to[-1]), c, o, None, None, 0, t, key_words=KW, stream=st)
+            st.synchronize()
             cap = int(t.item()) + 1
             ids = torch.empty(cap, dtype=torch.int32, device=dev)
             keys = torch.empty(cap * KW, dtype=torch.int64, device=dev)
-            e.match_keys_device(d_b, d_o, n, int(to[-1]), c, o, ids, keys, cap, t, key_words=KW)
-            torch.cuda.synchronize(dev)
+            e.match_keys_device(d_b, d_o, n, int(to[-1]), c, o, ids, keys, cap, t, key_words=KW, stream=st)
+            st.synchronize()
             if e.key_levels() > 32 * KW - 1:
                 raise RuntimeError("order keys too narrow for the batch")
             lists.append((c, o, ids, keys, cap, d_b, d_o))
-        # the exchange and the merges run on each device's current torch stream
-        streams = [torch.cuda.current_stream(torch.device("cuda", d)) for d in self.devices]
         ins = (L.TmExchangeIn * S)(*[_xin(n, c, o, ids, keys, KW, cap, streams[s])
                                      for s, (c, o, ids, keys, cap, _, _) in enumerate(lists)])
         outs = (L.TmExchangeOut * S)()
@@ -308,7 +311,7 @@ class ShardSet:
             # the merge runs on the comm's stream, after the exchange's copies
             self.engines[r].merge_device(m, x.d_counts, x.d_src_base, x.d_ids, x.d_keys, oc, oo, og, x.total + 1,
                                          tot, stream=streams[r], key_words=KW, key_stride=x.total)
-            torch.cuda.synchronize(dev)
+            streams[r].synchronize()
             counts.append(oc[:m].cpu().numpy().view(np.uint32))
             offs.extend((oo[1:].cpu().numpy() + offs[-1]).tolist())
             gids.append(og[: x.total].cpu().numpy().view(np.uint32))

@@ -192,11 +192,12 @@ def test_rccl_one_rank_exchange_equals_o1(gpu_device):
     c = torch.empty(n, dtype=torch.int32, device=dev)
     o = torch.empty(n + 1, dtype=torch.int64, device=dev)
     t = torch.zeros(1, dtype=torch.int64, device=dev)
-    e.match_keys_device(d_b, d_o, n, int(to[-1]), c, o, None, None, 0, t)
+    st = torch.cuda.Stream(device=dev)   # one explicit stream: walk -> RCCL exchange -> merge
+    e.match_keys_device(d_b, d_o, n, int(to[-1]), c, o, None, None, 0, t, stream=st)
+    st.synchronize()
     cap = int(t.item()) + 1
     ids = torch.empty(cap, dtype=torch.int32, device=dev)
     keys = torch.empty(cap, dtype=torch.int64, device=dev)
-    st = torch.cuda.current_stream(dev)
     e.match_keys_device(d_b, d_o, n, int(to[-1]), c, o, ids, keys, cap, t, stream=st)
     x = shard.exchange_native(comm, c, o, ids, keys, n, key_words=1, key_stride=cap, stream=st)
     assert x.m == n and x.total == cap - 1
