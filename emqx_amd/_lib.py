@@ -34,7 +34,7 @@ class TmBatchStats(ctypes.Structure):
     _fields_ = [("topics", ctypes.c_uint64), ("levels", ctypes.c_uint64),
                 ("visits", ctypes.c_uint64), ("edge_reads", ctypes.c_uint64),
                 ("matches", ctypes.c_uint64), ("leaf_visits", ctypes.c_uint64),
-                ("probe_loads", ctypes.c_uint64)]
+                ("probe_loads", ctypes.c_uint64), ("prunable_visits", ctypes.c_uint64)]
 
 
 class TmBatcherConfig(ctypes.Structure):

@@ -132,6 +132,8 @@ struct NodeAux {
     uint32_t word;        // word by which the parent reaches it (id, WORD_PLUS, WORD_HASH)
     uint32_t edge_count;  // #trie_node.edge_count
     uint32_t lit_count;   // literal children (inline when 1, WIDE + edges[] once 2 or more)
+    uint16_t sum;         // S(v), the subtree summary (image.h): a superset between relayouts
+    uint16_t lsum;        // union of S over v's literal children
 };
 
 struct FilterRec {
@@ -297,6 +299,8 @@ struct tm_engine {
                                       // bit 2 = heat order (heat_sort); bit 3 = heat from filter counts
     bool force_relayout = false;
     int split_halves = 1;             // option "split": walk reads separate inner / leaf half arrays
+    int summaries = 1;                // option "summaries": subtree summaries in the inner half prune dead
+                                      // '+' / literal subtrees (0: field 1 is FILTER_NONE, nothing pruned)
 
     // ---- route table: the emqx_route bag (src/emqx_router.erl:52-59) ----
     std::unordered_map<std::string, uint32_t> dest_index;   // dest bytes -> dest id
@@ -338,8 +342,8 @@ struct tm_engine {
     bool stats_enabled = false, timing_enabled = false;
     tm_batch_stats last_stats{};
 
-    // scratch for words of one filter
-    std::vector<uint32_t> tmp_words;
+    // scratch for words of one filter, and its path of nodes
+    std::vector<uint32_t> tmp_words, tmp_path;
 
     tm_engine() {
         if (const char* v = std::getenv("TM_XCDQ")) xcdq = std::atoi(v) ? 1 : 0;
@@ -522,7 +526,7 @@ struct tm_engine {
             aux.push_back(NodeAux{});
         }
         nodes[id] = empty_node();
-        aux[id] = NodeAux{parent, word, 0, 0};
+        aux[id] = NodeAux{parent, word, 0, 0, (uint16_t)SUM_NONE, (uint16_t)SUM_NONE};
         node_dirty.mark(id);
         ++live_nodes;
         ++created_since_layout;
@@ -624,10 +628,11 @@ struct tm_engine {
         aux[v].edge_count--;
         touched(v);
         nodes[c] = empty_node();
-        aux[c] = NodeAux{NODE_NONE, 0, 0, 0};
+        aux[c] = NodeAux{NODE_NONE, 0, 0, 0, (uint16_t)SUM_NONE, (uint16_t)SUM_NONE};
         node_dirty.mark(c);
         free_nodes.push_back(c);
         --live_nodes;
+        refresh_hf(v);   // a removed '#' child gives the field back to the summaries
     }
     uint32_t walk(const std::vector<uint32_t>& ws) const {
         uint32_t v = ROOT;
@@ -643,10 +648,43 @@ struct tm_engine {
         nodes[c].self_filter = fid;
         touched(c);
         if (aux[c].word == WORD_HASH && aux[c].parent != NODE_NONE) {
-            nodes[aux[c].parent].hash_filter = fid;
             nodes[aux[c].parent].hash_filter2 = fid;
             touched(aux[c].parent);
+            refresh_hf(aux[c].parent);
         }
+    }
+    // the inner half's field 1 (image.h): the '#' child's filter, else the
+    // summaries of the '+' child and of the literal children
+    uint32_t hf_value(uint32_t v) const {
+        const Node& x = nodes[v];
+        if (x.hash != NODE_NONE && nodes[x.hash].self_filter != FILTER_NONE) return nodes[x.hash].self_filter;
+        const uint32_t pc = x.plus & NODE_MASK;
+        const uint32_t sp = pc == NODE_NONE ? SUM_NONE : aux[pc].sum;
+        const uint32_t sl = aux[v].lit_count ? aux[v].lsum : SUM_NONE;
+        return summaries ? (SUM_TAG | sp | (sl << 15)) : FILTER_NONE;
+    }
+    void refresh_hf(uint32_t v) {
+        const uint32_t x = hf_value(v);
+        if (nodes[v].hash_filter != x) {
+            nodes[v].hash_filter = x;
+            touched(v);
+        }
+    }
+    // a new filter at the end of tmp_path: OR it into the summaries of its
+    // path (emqx_trie's insert only adds; deletes leave supersets)
+    void add_summaries(bool hash_filter) {
+        const uint32_t D = (uint32_t)tmp_path.size() - 1;
+        for (uint32_t i = D + 1; i-- > 0;) {
+            const uint32_t rel = D - i;
+            uint32_t s = (rel < 10 ? (1u << rel) : 0x400u) | SUM_NONE;   // ends rel levels below path[i]
+            if (hash_filter && i < D)   // the '#' filter fires at path[D-1], D-1-i levels below path[i]
+                s = sum_union(s, std::min<uint32_t>(D - 1 - i, 15u) << 11);
+            NodeAux& a = aux[tmp_path[i]];
+            a.sum = (uint16_t)sum_union(a.sum, s);
+            if (i > 0 && tmp_words[i - 1] < WORD_MAX)
+                aux[tmp_path[i - 1]].lsum = (uint16_t)sum_union(aux[tmp_path[i - 1]].lsum, a.sum);
+        }
+        for (uint32_t i = 0; i < D; ++i) refresh_hf(tmp_path[i]);
     }
 
     // ------------------------------------------------------------------
@@ -657,7 +695,7 @@ struct tm_engine {
             id = free_filters.back();
             free_filters.pop_back();
         } else {
-            if (filters.size() >= 0xFFFFFFF0ull) throw RangeError("filter ids exhausted");
+            if (filters.size() >= 0x7FFFFFF0ull) throw RangeError("filter ids exhausted (2^31: the image tags summaries with bit 31)");
             id = (uint32_t)filters.size();
             filters.push_back(FilterRec{});
         }
@@ -677,8 +715,15 @@ struct tm_engine {
     void insert(const uint8_t* p, uint32_t len) {
         split_words(p, len, true);
         uint32_t v = ROOT;
-        for (uint32_t w : tmp_words) v = child_or_create(v, w);
-        if (nodes[v].self_filter == FILTER_NONE) set_topic(v, new_filter(p, len, v));
+        tmp_path.assign(1, ROOT);
+        for (uint32_t w : tmp_words) {
+            v = child_or_create(v, w);
+            tmp_path.push_back(v);
+        }
+        if (nodes[v].self_filter == FILTER_NONE) {
+            set_topic(v, new_filter(p, len, v));
+            add_summaries(!tmp_words.empty() && tmp_words.back() == WORD_HASH);
+        }
         dev_dirty = true;
         routes_dirty = true;   // filter ids may have changed
     }
@@ -1088,6 +1133,20 @@ struct tm_engine {
         }
         std::vector<uint32_t>().swap(kids);
         std::vector<uint32_t>().swap(start);
+        // exact subtree summaries: `order` lists parents before children, so
+        // in reverse every subtree is complete before its root
+        for (uint32_t v : order) aux[v].sum = aux[v].lsum = (uint16_t)SUM_NONE;
+        for (size_t i = order.size(); i-- > 0;) {
+            const uint32_t v = order[i];
+            NodeAux& a = aux[v];
+            if (nodes[v].self_filter != FILTER_NONE) a.sum = (uint16_t)sum_union(a.sum, sum_end0());
+            if (v == ROOT || a.parent == NODE_NONE) continue;
+            NodeAux& pa = aux[a.parent];
+            pa.sum = (uint16_t)sum_union(pa.sum, sum_shift(a.sum));
+            if (a.word < WORD_MAX) pa.lsum = (uint16_t)sum_union(pa.lsum, a.sum);
+            if (a.word == WORD_HASH && nodes[v].self_filter != FILTER_NONE)
+                pa.sum = (uint16_t)sum_union(pa.sum, sum_hash0(SUM_NONE));
+        }
         if (layout_order & 4) heat_sort(order, newid, new_hot_limit);
         auto remap = [&](uint32_t id) { return id == NODE_NONE ? NODE_NONE : newid[id]; };
         std::vector<Node> nn(order.size());
@@ -1131,6 +1190,7 @@ struct tm_engine {
         for (FilterRec& f : filters)
             if (f.node != NODE_NONE) f.node = newid[f.node];
         aux.swap(na);
+        for (uint32_t v = 0; v < nodes.size(); ++v) nodes[v].hash_filter = hf_value(v);
         free_nodes.clear();
         created_since_layout = 0;
         force_relayout = false;
@@ -1512,8 +1572,9 @@ struct tm_engine {
         s.topics = n;
         const DevBuf& ws = d.slots[d.last_slot].stats;
         if (!stats_enabled || !ws.p) return s;
-        unsigned long long h[6] = {0, 0, 0, 0, 0, 0};
+        unsigned long long h[7] = {0, 0, 0, 0, 0, 0, 0};
         HIPCHK(hipMemcpy(h, ws.p, sizeof(h), hipMemcpyDeviceToHost));
+        s.prunable_visits = h[6];
         s.levels = h[0];
         s.visits = h[1];
         s.edge_reads = h[2];
@@ -2082,6 +2143,7 @@ int host_batch(tm_engine* e, BatchKind kind, const uint8_t* topic_bytes, const u
             e->last_stats.matches += s.matches;
             e->last_stats.leaf_visits += s.leaf_visits;
             e->last_stats.probe_loads += s.probe_loads;
+            e->last_stats.prunable_visits += s.prunable_visits;
         }
     if (out_needed) *out_needed = total;
     return total > out_cap ? TM_ENOSPC : TM_OK;
@@ -2413,6 +2475,16 @@ int tm_set_option(tm_engine* e, const char* name, int64_t value) {
         if (!std::strcmp(name, "layout")) {
             if (value < 0 || value > 2) return TM_EINVAL;
             e->layout_mode = (int)value;
+            return TM_OK;
+        }
+        if (!std::strcmp(name, "summaries")) {
+            if (value < 0 || value > 1) return TM_EINVAL;
+            if ((int)value != e->summaries) {
+                e->summaries = (int)value;
+                for (uint32_t v = 0; v < e->nodes.size(); ++v)
+                    if (e->aux[v].parent != NODE_NONE || v == ROOT) e->refresh_hf(v);
+                e->dev_dirty = true;
+            }
             return TM_OK;
         }
         if (!std::strcmp(name, "split")) {

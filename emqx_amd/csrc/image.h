@@ -46,10 +46,25 @@ constexpr uint32_t WORD_MAX   = 0xFFFFFFF0u;   // interned ids are < WORD_MAX
 
 constexpr uint32_t EDGE_EMPTY = 0xFFFFFFFFu;   // slot.parent of an empty slot
 
+// Subtree summaries.  The 15-bit summary S(c) of the subtree below node c:
+// bits 0-9 "a filter ends k levels below c" (k = 0..9), bit 10 "one ends 10
+// or more below", bits 11-14 the fewest levels below c of a node whose '#'
+// child holds a filter (15: none within 14).  A walk that reaches c with k
+// topic levels still to consume (n - depth(c)) can match something below c
+// only if sum_useful(S(c), k): a non-'#' filter must end exactly k below, a
+// '#' filter fires at any visited node, i.e. within k.  Summaries are kept
+// as supersets (inserts OR into them, deletes leave them, relayout rebuilds
+// them exactly), so a prune is never wrong.
+constexpr uint32_t SUM_TAG  = 0x80000000u;   // Node::hash_filter holds summaries, not a filter id
+constexpr uint32_t SUM_ALL  = 0x7FFFu;       // summary that never prunes
+constexpr uint32_t SUM_NONE = 15u << 11;     // empty subtree (no filter at all)
+
 struct alignas(32) Node {
     // inner half: read by a visit with words left (level r < n)
     uint32_t plus;         // '+' child node id (NODE_NONE if none) | WIDE
-    uint32_t hash_filter;  // filter id of the '#' child (its topic), FILTER_NONE if none
+    uint32_t hash_filter;  // filter id (< 2^31) of the '#' child (its topic), or, when there is none,
+                           // SUM_TAG | S('+' child) | S(literal children, their union) << 15;
+                           // FILTER_NONE (= SUM_TAG | all ones) never prunes
     uint32_t lw;           // narrow: word of the single literal child (WORD_NONE if none); WIDE: Bloom bits 0-31
     uint32_t lc;           // narrow: that child's node id; WIDE: Bloom bits 32-63
     // leaf half: read by a visit at the topic's last level (r == n)
@@ -153,6 +168,24 @@ struct AggreView {
 #else
 #define TM_HD inline
 #endif
+
+TM_HD bool sum_useful(uint32_t s, uint32_t k) {
+    const uint32_t ends = k < 10 ? (s >> k) & 1u : (s >> 10) & 1u;
+    return ends != 0 || ((s >> 11) & 15u) <= k;
+}
+TM_HD uint32_t sum_union(uint32_t a, uint32_t b) {
+    const uint32_t ha = (a >> 11) & 15u, hb = (b >> 11) & 15u;
+    return ((a | b) & 0x7FFu) | ((ha < hb ? ha : hb) << 11);
+}
+// S of a parent seen from one level up: every depth one more
+TM_HD uint32_t sum_shift(uint32_t s) {
+    const uint32_t ends = ((s & 0x3FFu) << 1) | (s & 0x600u ? 0x400u : 0u);   // bit 9 -> "10 or more"
+    const uint32_t hm = (s >> 11) & 15u;
+    return (ends & 0x7FEu) | ((hm < 15u ? hm + 1u : 15u) << 11);
+}
+// S of a subtree whose root ends a filter (k = 0), or fires a '#' filter
+TM_HD uint32_t sum_end0() { return 1u | SUM_NONE; }
+TM_HD uint32_t sum_hash0(uint32_t s) { return s & 0x7FFu; }   // hmin = 0
 
 TM_HD uint64_t fmix64(uint64_t k) {
     k ^= k >> 33; k *= 0xff51afd7ed558ccdULL;

@@ -349,7 +349,7 @@ __device__ __forceinline__ uint4 load_half(const ImageView& im, uint32_t v, bool
 // literal subtree below it runs; a step visits one node with one 16 B load
 // and then either descends or pops to the deepest pending '+' child.
 struct WalkStats {
-    uint64_t visits = 0, edge_reads = 0, leaf_visits = 0, probe_loads = 0;
+    uint64_t visits = 0, edge_reads = 0, leaf_visits = 0, probe_loads = 0, prunable = 0;
     unsigned long long* hist = nullptr;   // STATS diagnostics: [visits, probe loads, failed probes] x 16 levels
 };
 constexpr int HIST_OFF = 8;   // hist = stats + HIST_OFF
@@ -461,20 +461,34 @@ __device__ __forceinline__ bool walk_step(const ImageView& im, Cursor& c, Path p
             st.edge_reads += leaf ? 1 : 3;   // 'match_#' (:141) + fold over [W, '+'] (:132)
             st.leaf_visits += leaf ? 1 : 0;
         }
-        if (hf != FILTER_NONE) emit(hf, key, path, r, 0u);   // 'match_#': the '#' filter
+        if (!(hf & SUM_TAG)) emit(hf, key, path, r, 0u);   // 'match_#': the '#' filter
         if (leaf) {
             if (sf != FILTER_NONE) emit(sf, KEYS ? key | rank_sym(r, 1) : 0ull, path, r, 1u);   // own filter (:128)
             break;
         }
         const uint64_t pl0 = st.probe_loads;
-        const Hit g = lit_child<STATS>(im, v, plus, lw, lc, W(r), st.probe_loads);
+        // subtree summaries (image.h): a child whose subtree cannot match
+        // with k = n - r - 1 levels left below it is never loaded.  The
+        // stats walk (STATS) prunes nothing, so its E and visits are the
+        // reference's, and counts what the summaries would skip.
+        const uint32_t w = W(r);
+        bool lit_ok = true, plus_ok = true;
+        if (hf & SUM_TAG) {
+            const uint32_t k = c.n - r - 1;
+            plus_ok = sum_useful(hf & SUM_ALL, k);
+            lit_ok = w < WORD_MAX ? sum_useful((hf >> 15) & SUM_ALL, k) : w == WORD_PLUS ? plus_ok : true;
+        }
+        const Hit g = (!STATS && !lit_ok) ? Hit{NODE_NONE, 0, 0, 0, 0, 0, false}
+                                          : lit_child<STATS>(im, v, plus, lw, lc, w, st.probe_loads);
         if (STATS && st.hist) {
             const uint32_t lv = r < 15 ? r : 15;
             atomicAdd(st.hist + lv, 1ull);
             if (st.probe_loads != pl0) atomicAdd(st.hist + 16 + lv, (unsigned long long)(st.probe_loads - pl0));
             if (st.probe_loads != pl0 && g.child == NODE_NONE) atomicAdd(st.hist + 32 + lv, 1ull);
         }
-        const uint32_t pc = plus & NODE_MASK;
+        if (STATS) st.prunable += (g.child != NODE_NONE && !lit_ok ? 1u : 0u) +
+                                  ((plus & NODE_MASK) != NODE_NONE && !plus_ok ? 1u : 0u);
+        const uint32_t pc = (STATS || plus_ok) ? (plus & NODE_MASK) : NODE_NONE;
         if (STATS && st.hist) {   // how the next visit is reached: [48] inline literal, [49] table literal,
                                   // [50] '+' (here or by a later pop: counted at the pop)
             if (g.child != NODE_NONE) atomicAdd(st.hist + ((plus & WIDE) ? 49 : 48), 1ull);
@@ -601,9 +615,9 @@ template <bool STATS>
 __device__ __forceinline__ void wave_stats_add(unsigned long long* stats, uint64_t lev, uint64_t matches,
                                                const WalkStats& st) {
     if (!STATS) return;
-    uint64_t v[6] = {lev, st.visits, st.edge_reads, matches, st.leaf_visits, st.probe_loads};
+    uint64_t v[7] = {lev, st.visits, st.edge_reads, matches, st.leaf_visits, st.probe_loads, st.prunable};
 #pragma unroll
-    for (int k = 0; k < 6; ++k) {
+    for (int k = 0; k < 7; ++k) {
         uint64_t x = v[k];
         for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
         if ((threadIdx.x & 63) == 0 && x) atomicAdd(stats + k, (unsigned long long)x);

@@ -65,6 +65,8 @@ typedef struct tm_batch_stats {
     uint64_t matches;         /* sum M_t                                         */
     uint64_t leaf_visits;     /* visits at the topic's last level (leaf half)    */
     uint64_t probe_loads;     /* 16 B edge-table slot loads (wide nodes, '#')    */
+    uint64_t prunable_visits; /* visits the subtree summaries skip (the counting */
+                              /* walk of stats mode skips none, so E is exact)   */
 } tm_batch_stats;
 
 /* engine lifetime ------------------------------------------------------------ */

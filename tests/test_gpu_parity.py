@@ -228,6 +228,7 @@ VARIANTS = {"queue": {}, "queue_xcd": {}, "queue_xcd@nosplit@dfs": {"split": 0, 
             "queue_xcd@plusfirst": {"order": 1, "layout": 2}, "queue_xcd@hashlast": {"order": 2, "layout": 2},
             "queue_xcd@order3@dfs": {"order": 3, "hot_levels": 0, "layout": 2},
             "queue_xcd@order0": {"order": 0, "layout": 2}, "queue_xcd@nogroup": {"group": 0},
+            "queue_xcd@nosummaries": {"summaries": 0}, "queue_xcd@summaries_nolayout": {"layout": 0},
             "queue@group": {"group": 1}, "queue_xcd@heat": {"order": 5, "layout": 2},
             "queue@heat@hashlast@split0": {"order": 7, "layout": 2, "split": 0}, "queue_xcd@heatf": {"order": 15, "layout": 2},
             "queue_xcd@edgeload2": {"edge_load": 2, "layout": 2}, "queue_xcd@edgeload16": {"edge_load": 16}}
@@ -300,4 +301,38 @@ def test_batches_on_alternating_streams_bit_exact(gpu_device, slots):
         assert np.array_equal(c.cpu().numpy().view(np.uint32), oc)
         assert np.array_equal(o.cpu().numpy().view(np.uint64), oo)
         assert np.array_equal(ids[:len(oi)].cpu().numpy().view(np.uint32), oi)
+    e.close()
+
+
+def test_summaries_prune_and_stay_exact_under_churn(gpu_device):
+    """subtree summaries (image.h) skip dead '+' / literal subtrees; deletes
+    leave supersets, relayout rebuilds them exactly — lists stay O1's"""
+    from oracle import O1
+    fb, fo = W.filters(2, n=300_000)
+    tb, to = W.topics(2, n=30_000)
+    filters = W.unpack(fb, fo)
+    e = Engine(device=gpu_device)
+    e.insert_many(fb, fo)
+    e.set_stats(True)
+    e.match_batch(tb, to)
+    st = e.last_stats()
+    e.set_stats(False)
+    assert st["prunable_visits"] > 0.05 * st["visits"], st
+    rng = np.random.default_rng(2)
+    live = set(range(len(filters)))
+    for rnd in range(3):
+        dels = rng.choice(sorted(live), size=20_000, replace=False)
+        for i in dels:
+            e.delete(filters[i])
+        live -= set(int(i) for i in dels)
+        if rnd == 1:
+            e.set_option("layout", 2)    # relayout on the next commit: exact summaries again
+        o1 = O1()
+        ids = sorted(live)
+        o1.insert_many(*pack([filters[i] for i in ids]))
+        want = [[filters[ids[j]] for j in row] for row in
+                (lambda c, o, i: [list(i[o[t]:o[t + 1]]) for t in range(len(c))])(*o1.match_ids(tb, to, threads=8))]
+        got = e.match(W.unpack(tb, to))
+        assert got == want, rnd
+        e.set_option("layout", 1)
     e.close()
