@@ -166,17 +166,65 @@ struct Slot {
 };
 constexpr int MAX_SLOTS = 4;
 
-// One device replica: the committed image (trie, dictionary, route and aggre
+// One committed trie image (nodes, edge tables, dictionary, word arena) in a
+// GPU's HBM.  A replica keeps two (epochs): a commit writes the one no batch
+// is reading and then flips, so tm_commit never waits for running walks;
+// `uses` holds an event per batch launched on the image since it was last
+// written, and only the next write to it waits for them (by then they are
+// long done).
+struct Image {
+    DevBuf d_nodes, d_edges, d_hedges, d_dict, d_arena, d_woff, d_inner, d_leaf;
+    size_t arena_uploaded = 0, woff_uploaded = 0;
+    bool split_stale = true, written = false;
+    uint64_t epoch = 0;
+    std::vector<hipEvent_t> uses;
+    void release() {
+        for (DevBuf* b : {&d_nodes, &d_edges, &d_hedges, &d_dict, &d_arena, &d_woff, &d_inner, &d_leaf}) b->release();
+        for (hipEvent_t ev : uses) (void)hipEventDestroy(ev);
+        uses.clear();
+    }
+};
+
+// One device replica: the committed images (trie, dictionary, route and aggre
 // tables) in that GPU's HBM, its stream and its workspaces.  An engine has
 // one replica per GPU it was opened on (tm_open_devices); they all mirror the
 // one host trie, so a batch can be cut across them with no collective.
 struct DevState {
     int device = -1;
     hipStream_t stream = nullptr;
-    // trie image + dictionary
-    DevBuf d_nodes, d_edges, d_hedges, d_dict, d_arena, d_woff, d_inner, d_leaf;
-    size_t arena_uploaded = 0, woff_uploaded = 0;
-    bool split_stale = true;
+    // trie image + dictionary, two epochs (Image)
+    Image img[2];
+    int cur = 0;                          // the image batches launch on
+    std::vector<hipEvent_t> ev_spare;     // recycled use events
+    Image& live() { return img[cur]; }
+    // one use of the live image by a batch on st (pruned as uses complete)
+    void note_use(hipStream_t st) {
+        Image& im = img[cur];
+        if (im.uses.size() >= 64) {   // drop the completed ones
+            size_t k = 0;
+            for (hipEvent_t ev : im.uses)
+                if (hipEventQuery(ev) == hipSuccess) ev_spare.push_back(ev);
+                else im.uses[k++] = ev;
+            im.uses.resize(k);
+        }
+        hipEvent_t ev = nullptr;
+        if (!ev_spare.empty()) {
+            ev = ev_spare.back();
+            ev_spare.pop_back();
+        } else {
+            HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        }
+        HIPCHK(hipEventRecord(ev, st));
+        im.uses.push_back(ev);
+    }
+    // host: every batch that read image i has finished
+    void drain_image(int i) {
+        for (hipEvent_t ev : img[i].uses) {
+            HIPCHK(hipEventSynchronize(ev));
+            ev_spare.push_back(ev);
+        }
+        img[i].uses.clear();
+    }
     // route image (emqx_route) and aggre tables
     DevBuf d_fr_meta, d_fr_dest, d_ex_slots, d_ex_arena, d_ex_dest, d_ex_rank, d_dt, d_rank_src, d_rank_tg;
     // workspaces: route / aggre (w_r*, w_d*, w_a*), host-buffer batches, merge
@@ -206,16 +254,15 @@ struct DevState {
     void rw_drain() {   // host: every route / aggre kernel issued so far has finished
         if (rw_used) HIPCHK(hipEventSynchronize(rw_done));
     }
-    void wait_matches() {
-        for (Slot& w : slots)
-            if (w.used) HIPCHK(hipEventSynchronize(w.done));
-    }
     void release() {
         (void)hipSetDevice(device);
         if (stream) (void)hipStreamSynchronize(stream);
         if (rw_done) (void)hipEventDestroy(rw_done);
-        for (DevBuf* b : {&d_nodes, &d_edges, &d_hedges, &d_dict, &d_arena, &d_woff, &d_inner, &d_leaf, &d_fr_meta,
-                          &d_fr_dest, &d_ex_slots, &d_ex_arena, &d_ex_dest, &d_ex_rank, &d_dt, &d_rank_src,
+        img[0].release();
+        img[1].release();
+        for (hipEvent_t ev : ev_spare) (void)hipEventDestroy(ev);
+        ev_spare.clear();
+        for (DevBuf* b : {&d_fr_meta, &d_fr_dest, &d_ex_slots, &d_ex_arena, &d_ex_dest, &d_ex_rank, &d_dt, &d_rank_src,
                           &d_rank_tg, &w_rexact, &w_rscan, &w_rids, &w_rcounts, &w_roff, &w_dsrc, &w_dcount, &w_akey,
                           &w_alarge, &w_mpre, &w_mscan, &w_bytes, &w_off, &w_counts, &w_outoff, &w_ids, &w_total})
             b->release();
@@ -252,7 +299,6 @@ struct tm_engine {
     std::vector<uint8_t> word_arena;   // 8-aligned, zero-padded words
     std::vector<uint32_t> word_off;
     Dirty dict_dirty;
-    size_t arena_uploaded = 0, woff_uploaded = 0;
 
     // ---- trie mirror / image ----
     std::vector<Node> nodes;
@@ -272,6 +318,8 @@ struct tm_engine {
     uint32_t hot_limit = 0;
     uint32_t hot_edge_depth = 0;      // option "hot_edges": parents of depth < D use `hot` (0 = off; A/B: no gain at C3)
     Dirty node_dirty;
+    // the dirty maps of the previous commit (the other image missed them)
+    Dirty prev_node_dirty, prev_cold_dirty, prev_hot_dirty, prev_dict_dirty;
     EdgeTable& tab(uint32_t parent) { return parent < hot_limit ? hot : cold; }
     const EdgeTable& tab(uint32_t parent) const { return parent < hot_limit ? hot : cold; }
 
@@ -299,6 +347,8 @@ struct tm_engine {
                                       // bit 2 = heat order (heat_sort); bit 3 = heat from filter counts
     bool force_relayout = false;
     int split_halves = 1;             // option "split": walk reads separate inner / leaf half arrays
+    int double_buffer = 1;            // option "double_buffer": two image epochs per replica (commit never waits
+                                      // on running walks); 0: one image, commit waits for the walks on it
     int summaries = 1;                // option "summaries": subtree summaries in the inner half prune dead
                                       // '+' / literal subtrees (0: field 1 is FILTER_NONE, nothing pruned)
 
@@ -1212,47 +1262,59 @@ struct tm_engine {
         }
     };
 
+    // the live image of replica d (its sizes are the host tables' at the
+    // last commit, and every match commits first)
     ImageView view(const DevState& d) const {
+        const Image& g = d.img[d.cur];
         ImageView im;
-        if (split_halves && d.d_inner.p && !d.split_stale) {
-            im.inner = d.d_inner.as<const uint8_t>();
-            im.leaf = d.d_leaf.as<const uint8_t>();
+        if (split_halves && g.d_inner.p && !g.split_stale) {
+            im.inner = g.d_inner.as<const uint8_t>();
+            im.leaf = g.d_leaf.as<const uint8_t>();
             im.node_shift = 4;
         } else {
-            im.inner = d.d_nodes.as<const uint8_t>();
-            im.leaf = d.d_nodes.as<const uint8_t>() + 16;
+            im.inner = g.d_nodes.as<const uint8_t>();
+            im.leaf = g.d_nodes.as<const uint8_t>() + 16;
             im.node_shift = 5;
         }
-        im.edges = d.d_edges.as<const EdgeSlot>();
+        im.edges = g.d_edges.as<const EdgeSlot>();
         im.edge_slot_mask = cold.slots.size() - 1;
-        im.hot_edges = d.d_hedges.as<const EdgeSlot>();
+        im.hot_edges = g.d_hedges.as<const EdgeSlot>();
         im.hot_slot_mask = hot.slots.size() - 1;
         im.hot_limit = hot_limit;
-        im.dict = d.d_dict.as<const DictSlot>();
+        im.dict = g.d_dict.as<const DictSlot>();
         im.dict_slot_mask = dict.size() - 1;
-        im.word_arena = d.d_arena.as<const uint8_t>();
-        im.word_off = d.d_woff.as<const uint32_t>();
+        im.word_arena = g.d_arena.as<const uint8_t>();
+        im.word_off = g.d_woff.as<const uint32_t>();
         return im;
     }
 
     // upload a host table to one replica: the whole table after a resize (or
     // when the replica is new), else the dirty pages; the caller clears the
     // dirty map once every replica has its copy
+    // pages dirtied since image g was last written: this commit's and, when g
+    // missed the previous commit (two epochs), that one's too
     template <class T>
-    void upload_table(DevState& d, DevBuf& buf, const std::vector<T>& host, const Dirty& dirty) {
+    void upload_table(DevState& d, Image& g, DevBuf& buf, const std::vector<T>& host, const Dirty& dirty,
+                      const Dirty& prev) {
         const bool re = buf.ensure(std::max<size_t>(host.size(), 1) * sizeof(T));
-        if (re || dirty.all) {
+        // g holds commit g.epoch; this one makes epoch + 1
+        const bool two = g.written && g.epoch + 1 == epoch;        // g missed exactly the previous commit
+        const bool stale = !g.written || g.epoch + 1 < epoch;      // missed more (double_buffer switched on)
+        if (re || stale || dirty.all || (two && prev.all)) {
             HIPCHK(hipMemcpyAsync(buf.p, host.data(), host.size() * sizeof(T), hipMemcpyHostToDevice, d.stream));
             return;
         }
-        const size_t np = dirty.pages.size();
+        const size_t np = std::max(dirty.pages.size(), two ? prev.pages.size() : 0);
+        auto is_dirty = [&](size_t pg) {
+            return (pg < dirty.pages.size() && dirty.pages[pg]) || (two && pg < prev.pages.size() && prev.pages[pg]);
+        };
         for (size_t pg = 0; pg < np;) {
-            if (!dirty.pages[pg]) {
+            if (!is_dirty(pg)) {
                 ++pg;
                 continue;
             }
             size_t q = pg;
-            while (q < np && dirty.pages[q]) ++q;
+            while (q < np && is_dirty(q)) ++q;
             const size_t a = pg * PAGE_ELEMS, b = std::min(host.size(), q * PAGE_ELEMS);
             if (a < b)
                 HIPCHK(hipMemcpyAsync(buf.as<T>() + a, host.data() + a, (b - a) * sizeof(T), hipMemcpyHostToDevice,
@@ -1267,67 +1329,81 @@ struct tm_engine {
             relayout();
     }
 
+    // Publish the host trie to every replica: the changes go to the image no
+    // batch reads (after the batches that read it before the previous flip
+    // have finished: normally long ago), then that image becomes live for the
+    // batches launched from now on.  Batches in flight keep the image they
+    // were launched on, consistent and untouched.
     void commit() {
-        if (dev_dirty || devs.empty() || !devs[0]->d_nodes.p) maybe_relayout();
+        if (dev_dirty || devs.empty() || !devs[0]->img[devs[0]->cur].written) maybe_relayout();
         if (devs.empty()) {
             ++epoch;
             dev_dirty = false;
             return;
         }
-        if (!dev_dirty && devs[0]->d_nodes.p) {
-            for (auto& dp : devs)
-                if (split_halves && dp->split_stale) {
-                    Guard g(dp->device);
-                    dp->wait_matches();
-                    split_image(*dp);
+        if (!dev_dirty && devs[0]->img[devs[0]->cur].written) {
+            for (auto& dp : devs) {
+                Image& g = dp->live();
+                if (split_halves && g.split_stale) {   // option "split" turned on: derive the halves
+                    Guard gd(dp->device);
+                    dp->drain_image(dp->cur);
+                    split_image(*dp, g);
                     HIPCHK(hipStreamSynchronize(dp->stream));
                 }
+            }
             return;
         }
         for (auto& dp : devs) {
             DevState& d = *dp;
-            Guard g(d.device);
-            d.wait_matches();  // never patch the image under a running walk
-            d.rw_drain();
-            upload_table(d, d.d_nodes, nodes, node_dirty);
-            upload_table(d, d.d_edges, cold.slots, cold.dirty);
-            upload_table(d, d.d_hedges, hot.slots, hot.dirty);
-            upload_table(d, d.d_dict, dict, dict_dirty);
+            Guard gd(d.device);
+            const int back = double_buffer ? 1 - d.cur : d.cur;
+            Image& g = d.img[back];
+            d.drain_image(back);   // the batches launched on it before the last flip
+            upload_table(d, g, g.d_nodes, nodes, node_dirty, prev_node_dirty);
+            upload_table(d, g, g.d_edges, cold.slots, cold.dirty, prev_cold_dirty);
+            upload_table(d, g, g.d_hedges, hot.slots, hot.dirty, prev_hot_dirty);
+            upload_table(d, g, g.d_dict, dict, dict_dirty, prev_dict_dirty);
             // append-only arrays: upload the new tail (or all after a realloc)
             {
-                const bool re = d.d_arena.ensure(std::max<size_t>(word_arena.size(), 8) + 16);
-                const size_t from = re ? 0 : d.arena_uploaded;
+                const bool re = g.d_arena.ensure(std::max<size_t>(word_arena.size(), 8) + 16);
+                const size_t from = re ? 0 : g.arena_uploaded;
                 if (word_arena.size() > from)
-                    HIPCHK(hipMemcpyAsync(d.d_arena.as<uint8_t>() + from, word_arena.data() + from,
+                    HIPCHK(hipMemcpyAsync(g.d_arena.as<uint8_t>() + from, word_arena.data() + from,
                                           word_arena.size() - from, hipMemcpyHostToDevice, d.stream));
-                d.arena_uploaded = word_arena.size();
+                g.arena_uploaded = word_arena.size();
             }
             {
-                const bool re = d.d_woff.ensure(std::max<size_t>(word_off.size(), 1) * 4);
-                const size_t from = re ? 0 : d.woff_uploaded;
+                const bool re = g.d_woff.ensure(std::max<size_t>(word_off.size(), 1) * 4);
+                const size_t from = re ? 0 : g.woff_uploaded;
                 if (word_off.size() > from)
-                    HIPCHK(hipMemcpyAsync(d.d_woff.as<uint32_t>() + from, word_off.data() + from,
+                    HIPCHK(hipMemcpyAsync(g.d_woff.as<uint32_t>() + from, word_off.data() + from,
                                           (word_off.size() - from) * 4, hipMemcpyHostToDevice, d.stream));
-                d.woff_uploaded = word_off.size();
+                g.woff_uploaded = word_off.size();
             }
-            d.split_stale = true;
-            if (split_halves) split_image(d);
-            HIPCHK(hipStreamSynchronize(d.stream));
+            g.split_stale = true;
+            if (split_halves) split_image(d, g);
+            HIPCHK(hipStreamSynchronize(d.stream));   // host tables may change once this returns
+            g.written = true;
+            g.epoch = epoch + 1;
+            d.cur = back;   // live from the next batch on
         }
-        node_dirty.clear();
-        cold.dirty.clear();
-        hot.dirty.clear();
-        dict_dirty.clear();
+        // this commit's dirty pages become the "previous" set the other image
+        // still needs at the next commit
+        for (auto pr : {std::make_pair(&node_dirty, &prev_node_dirty), std::make_pair(&cold.dirty, &prev_cold_dirty),
+                        std::make_pair(&hot.dirty, &prev_hot_dirty), std::make_pair(&dict_dirty, &prev_dict_dirty)}) {
+            *pr.second = *pr.first;
+            pr.first->clear();
+        }
         dev_dirty = false;
         ++epoch;
     }
 
     // option "split": de-interleave the uploaded records into inner / leaf arrays
-    void split_image(DevState& d) {
-        d.d_inner.ensure(nodes.size() * 16);
-        d.d_leaf.ensure(nodes.size() * 16);
-        HIPCHK(launch_split_nodes(d.d_nodes.p, nodes.size(), d.d_inner.p, d.d_leaf.p, d.stream));
-        d.split_stale = false;
+    void split_image(DevState& d, Image& g) {
+        g.d_inner.ensure(nodes.size() * 16);
+        g.d_leaf.ensure(nodes.size() * 16);
+        HIPCHK(launch_split_nodes(g.d_nodes.p, nodes.size(), g.d_inner.p, g.d_leaf.p, d.stream));
+        g.split_stale = false;
     }
 
     // ------------------------------------------------------------------
@@ -1426,6 +1502,7 @@ struct tm_engine {
         HIPCHK(launch_queue(stats_enabled, xcdq != 0, im, bytes, off, n, qb, d.stage_k, counts, out_off, ids, keys,
                             cap, total, sp, st, timing_enabled ? marks : nullptr, walk_bpc, hist_enabled != 0,
                             keys ? key_words : 1u));
+        d.note_use(st);   // the live image is read until this point of st
         w.keyed = keys != nullptr;
         w.n = n;
         w.K = d.stage_k;
@@ -1470,6 +1547,7 @@ struct tm_engine {
         qb.perm = nullptr;
         HIPCHK(launch_copy(view(d), w.bytes, w.off, w.n, qb, w.K, w.kw, w.counts, w.out_off, ids, keys, cap, st));
         HIPCHK(hipEventRecord(w.done, st));
+        d.note_use(st);
     }
 
     // match ids of a batch into d.w_rcounts / w_roff / w_rids with ONE walk
@@ -2475,6 +2553,11 @@ int tm_set_option(tm_engine* e, const char* name, int64_t value) {
         if (!std::strcmp(name, "layout")) {
             if (value < 0 || value > 2) return TM_EINVAL;
             e->layout_mode = (int)value;
+            return TM_OK;
+        }
+        if (!std::strcmp(name, "double_buffer")) {
+            if (value < 0 || value > 1) return TM_EINVAL;
+            e->double_buffer = (int)value;
             return TM_OK;
         }
         if (!std::strcmp(name, "summaries")) {

@@ -1,0 +1,33 @@
+#!/bin/bash
+# One parameterised GPU job (run through gpurun), output under gpurun_out/$TAG.
+# Steps (space-separated in STEPS, run in order, each under its own time
+# limit, stopping at the first failure):
+#   tests     pytest -m gpu over $TESTS (default: tests)
+#   smoke     __graft_entry__.smoke()
+#   bench     python bench.py $BENCH_ARGS                -> bench.json / bench.log
+#   prof      rocprofv3 --kernel-trace --stats of the bench -> prof/ (kernel_stats.csv)
+#   pmc       PMC passes (tools/pmc_passes.sh)           -> pmc/summary.json
+#   cmd       an arbitrary python command in $CMD         -> cmd.log
+# e.g. gpurun -- 'STEPS="tests bench prof" TAG=r02_head bash tools/gpu.sh'
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-.}"
+export TMPDIR=/tmp
+OUT=gpurun_out/${TAG:-job}
+mkdir -p "$OUT"
+for s in ${STEPS:-tests}; do
+  case $s in
+    tests) timeout -k 10 ${T_TESTS:-900} python -u -m pytest ${TESTS:-tests} -m gpu -x -v --durations=20 \
+             --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1 ;;
+    smoke) timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 ;;
+    bench) timeout -k 10 ${T_BENCH:-600} python -u bench.py ${BENCH_ARGS} > "$OUT/bench.json" 2> "$OUT/bench.log" ;;
+    prof)  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
+             python3 bench.py --steps 10 --warmup 2 --cpu-sample 0 --check 0 --streams 1 --no-extras ${BENCH_ARGS} \
+             > "$OUT/prof_bench.json" 2> "$OUT/prof_bench.log" ;;
+    pmc)   PMC_DIR=${TAG:-job}/pmc bash tools/pmc_passes.sh ;;
+    cmd)   timeout -k 10 ${T_CMD:-600} python -u -c "$CMD" > "$OUT/cmd.log" 2>&1 ;;
+    *)     echo "unknown step $s"; false ;;
+  esac
+  rc=$?
+  echo "step $s rc=$rc"
+  [ $rc -eq 0 ] || exit $rc
+done
