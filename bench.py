@@ -361,7 +361,8 @@ def main():
                          "topics_per_launch": n0,
                          "per_topic": {"n": levels / n0, "E": stats["edge_reads"] / n0, "M": stats["matches"] / n0,
                                        "visits": stats["visits"] / n0, "leaf_visits": stats["leaf_visits"] / n0,
-                                       "probe_loads": stats["probe_loads"] / n0}},
+                                       "probe_loads": stats["probe_loads"] / n0,
+                                       "prunable_visits": stats.get("prunable_visits", 0) / n0}},
             "cpu_baseline": cpu,
             "kernel_ms": kms,
             "filter_hits_per_s": stats["matches"] / n0 * topics_per_s,

@@ -98,10 +98,41 @@ struct Dirty {
 struct DevBuf {
     void* p = nullptr;
     size_t bytes = 0;
+    bool pooled = false;   // from the device's stream-ordered pool (ensure_async)
     void release() {
-        if (p) (void)hipFree(p);
+        if (p) {
+            if (pooled) {
+                (void)hipFreeAsync(p, nullptr);
+                (void)hipStreamSynchronize(nullptr);
+            } else {
+                (void)hipFree(p);
+            }
+        }
         p = nullptr;
         bytes = 0;
+    }
+    // ensure() through the stream-ordered pool on st: neither the free nor the
+    // allocation synchronises the device (hipFree waits for every stream, so
+    // an image commit would wait for the walks in flight on the other image).
+    // The caller guarantees the old contents have no readers left, and orders
+    // every use of the new buffer after st.
+    bool ensure_async(size_t need, hipStream_t st, double slack = 1.25) {
+        if (need <= bytes && p) return false;
+        if (p) {
+            if (pooled) HIPCHK(hipFreeAsync(p, st));
+            else (void)hipFree(p);
+        }
+        p = nullptr;
+        bytes = 0;
+        size_t want = std::max<size_t>(256, (size_t)(need * slack));
+        hipError_t e = hipMallocAsync(&p, want, st);
+        if (e != hipSuccess) {
+            p = nullptr;
+            throw DevError(std::string("hipMallocAsync(") + std::to_string(want) + "): " + hipGetErrorString(e));
+        }
+        bytes = want;
+        pooled = true;
+        return true;
     }
     // grow to at least `need` bytes (contents not preserved); true if reallocated
     bool ensure(size_t need, double slack = 1.25) {
@@ -1296,7 +1327,7 @@ struct tm_engine {
     template <class T>
     void upload_table(DevState& d, Image& g, DevBuf& buf, const std::vector<T>& host, const Dirty& dirty,
                       const Dirty& prev) {
-        const bool re = buf.ensure(std::max<size_t>(host.size(), 1) * sizeof(T));
+        const bool re = buf.ensure_async(std::max<size_t>(host.size(), 1) * sizeof(T), d.stream);
         // g holds commit g.epoch; this one makes epoch + 1
         const bool two = g.written && g.epoch + 1 == epoch;        // g missed exactly the previous commit
         const bool stale = !g.written || g.epoch + 1 < epoch;      // missed more (double_buffer switched on)
@@ -1365,7 +1396,7 @@ struct tm_engine {
             upload_table(d, g, g.d_dict, dict, dict_dirty, prev_dict_dirty);
             // append-only arrays: upload the new tail (or all after a realloc)
             {
-                const bool re = g.d_arena.ensure(std::max<size_t>(word_arena.size(), 8) + 16);
+                const bool re = g.d_arena.ensure_async(std::max<size_t>(word_arena.size(), 8) + 16, d.stream);
                 const size_t from = re ? 0 : g.arena_uploaded;
                 if (word_arena.size() > from)
                     HIPCHK(hipMemcpyAsync(g.d_arena.as<uint8_t>() + from, word_arena.data() + from,
@@ -1373,7 +1404,7 @@ struct tm_engine {
                 g.arena_uploaded = word_arena.size();
             }
             {
-                const bool re = g.d_woff.ensure(std::max<size_t>(word_off.size(), 1) * 4);
+                const bool re = g.d_woff.ensure_async(std::max<size_t>(word_off.size(), 1) * 4, d.stream);
                 const size_t from = re ? 0 : g.woff_uploaded;
                 if (word_off.size() > from)
                     HIPCHK(hipMemcpyAsync(g.d_woff.as<uint32_t>() + from, word_off.data() + from,
@@ -1400,8 +1431,8 @@ struct tm_engine {
 
     // option "split": de-interleave the uploaded records into inner / leaf arrays
     void split_image(DevState& d, Image& g) {
-        g.d_inner.ensure(nodes.size() * 16);
-        g.d_leaf.ensure(nodes.size() * 16);
+        g.d_inner.ensure_async(nodes.size() * 16, d.stream);
+        g.d_leaf.ensure_async(nodes.size() * 16, d.stream);
         HIPCHK(launch_split_nodes(g.d_nodes.p, nodes.size(), g.d_inner.p, g.d_leaf.p, d.stream));
         g.split_stale = false;
     }
@@ -1901,6 +1932,13 @@ int tm_open_devices(const tm_config* cfg, const int32_t* devices, uint32_t n_dev
         }
         d->device = devices[i];
         d->stage_k = e->stage_k_min;
+        {   // image buffers come from the stream-ordered pool (DevBuf::ensure_async);
+            // keep what they free cached there, so trimming never waits on the device
+            hipMemPool_t pool = nullptr;
+            uint64_t keep = UINT64_MAX;
+            if (hipDeviceGetDefaultMemPool(&pool, devices[i]) == hipSuccess)
+                (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+        }
         e->devs.push_back(std::move(d));
     }
     if (prev >= 0) (void)hipSetDevice(prev);

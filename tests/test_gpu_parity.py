@@ -8,6 +8,7 @@ against the oracle, through the C-ABI.  Bit-exact: same filters, same order.
     - C5 (16 levels, '#'-heavy, $SYS, $share) on a sample
     - subscribe/unsubscribe deltas between batches, ENOSPC, the device API
 """
+import os
 import random
 
 import numpy as np
@@ -20,6 +21,7 @@ from emqx_amd.emqx_router import Router
 from oracle import O1, pytrie
 
 pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 L1 = "latin-1"
 
 
@@ -338,77 +340,21 @@ def test_summaries_prune_and_stay_exact_under_churn(gpu_device):
     e.close()
 
 
+def test_commit_while_walk_in_flight_exact(gpu_device):
+    """tests/inflight_commit.py in this process: the batch launched before a
+    commit sees the old trie, the next the new one (O1's lists both)"""
+    import inflight_commit
+    inflight_commit.run(gpu_device, require_overlap=False)
+
+
 def test_commit_does_not_wait_for_walks_in_flight(gpu_device):
-    """two image epochs per replica (engine.cpp Image): a batch queued behind
-    a 0.3 s spin keeps reading the image it was launched on while the host
-    deletes / inserts filters and commits; the commit returns before the spin
-    ends, the batch sees the old trie and the next one the new trie (both
-    O1's lists); a second commit (which must reuse the first batch's image)
-    waits for it, and results stay exact"""
-    import time
-    import torch
-    dev = torch.device("cuda", gpu_device)
-    fb, fo = W.filters(2, n=200_000)
-    tb, to = W.topics(2, n=20_000)
-    filters = W.unpack(fb, fo)
-    e = Engine(device=gpu_device)
-    e.insert_many(*pack(filters[:150_000]))
-    e.commit()
-    n = len(to) - 1
-    st = torch.cuda.Stream(device=dev)
-
-    def launch():
-        with torch.cuda.stream(st):
-            d_b = torch.from_numpy(tb.copy()).to(dev)
-            d_o = torch.from_numpy(to.view(np.int64).copy()).to(dev)
-            c = torch.empty(n, dtype=torch.int32, device=dev)
-            o = torch.empty(n + 1, dtype=torch.int64, device=dev)
-            t = torch.zeros(1, dtype=torch.int64, device=dev)
-            ids = torch.empty(4_000_000, dtype=torch.int32, device=dev)
-        e.match_batch_device(d_b, d_o, n, int(to[-1]), c, o, ids, ids.numel(), t, stream=st)
-        return c, o, ids, t, d_b, d_o
-
-    def oracle_lists(live):
-        o1 = O1()
-        o1.insert_many(*pack([filters[i] for i in live]))
-        c, o, i = o1.match_ids(tb, to, threads=8)
-        return [[filters[live[j]] for j in i[o[k]:o[k + 1]]] for k in range(n)]
-
-    def host_ids(live):
-        """the host API on the live image, pinned to O1 by filter bytes"""
-        c, o, ids = e.match_batch(tb, to)
-        rows = [[int(x) for x in ids[o[k]:o[k + 1]]] for k in range(n)]
-        assert [[e.filter_bytes(x) for x in r] for r in rows] == oracle_lists(live)
-        return rows
-
-    def dev_ids(res):
-        c, o, ids, t, _, _ = res
-        c, o, ids = c.cpu().numpy().view(np.uint32), o.cpu().numpy().view(np.uint64), ids.cpu().numpy().view(np.uint32)
-        assert int(t.item()) == int(o[-1])
-        return [[int(x) for x in ids[o[k]:o[k + 1]]] for k in range(n)]
-
-    want0 = host_ids(list(range(150_000)))
-    torch.cuda.synchronize(dev)
-    with torch.cuda.stream(st):
-        torch.cuda._sleep(int(2.1e9 * 0.3))     # ~0.3 s of spinning ahead of batch 1
-    r1 = launch()
-    for f in filters[:20_000]:
-        e.delete(f)
-    e.insert_many(*pack(filters[150_000:]))
-    t0 = time.perf_counter()
-    e.commit()
-    dt = time.perf_counter() - t0
-    assert not st.query(), "the spin ended before the commit: the test proves nothing"
-    want1 = host_ids(list(range(20_000, 200_000)))
-    r2 = launch()
-    for f in filters[20_000:40_000]:
-        e.delete(f)
-    e.commit()                                   # writes batch 1's image: waits for it
-    want2 = host_ids(list(range(40_000, 200_000)))
-    r3 = launch()
-    st.synchronize()
-    assert dev_ids(r1) == want0
-    assert dev_ids(r2) == want1
-    assert dev_ids(r3) == want2
-    assert dt < 0.25, dt
-    e.close()
+    """the same in a child process with 16 hardware queues and raw streams,
+    so the engine's stream and the spinning stream are distinct queues: the
+    commit must return before the spin ends"""
+    import subprocess
+    import sys
+    env = dict(os.environ, GPU_MAX_HW_QUEUES="16")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "inflight_commit.py"), str(gpu_device),
+                        "--overlap"], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    print(r.stdout.strip())

@@ -31,16 +31,24 @@ __global__ void fill(uint4* t, uint64_t n) {
     }
 }
 
-int main() {
+// no arguments: the sweep below; "W WAVES MIB": one configuration (for PMC
+// passes, so each chase dispatch of the run is the same shape)
+int main(int argc, char** argv) {
     int cus = 0; CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
     const uint64_t maxb = 4ull << 30;
     uint4* t; CK(hipMalloc(&t, maxb));
     hipLaunchKernelGGL(fill, dim3(4096), dim3(256), 0, 0, t, maxb / 16);
     uint32_t* out; CK(hipMalloc(&out, 64ull << 20));
     CK(hipDeviceSynchronize());
-    uint64_t sizes[] = {2ull << 20, 16ull << 20, 128ull << 20, 512ull << 20, 1ull << 30, 4ull << 30};
-    for (int W = 1; W <= 2; ++W)
-    for (int waves_per_cu : {8, 16, 32})
+    std::vector<uint64_t> sizes = {2ull << 20, 16ull << 20, 128ull << 20, 512ull << 20, 1ull << 30, 4ull << 30};
+    std::vector<int> Ws = {1, 2}, waves = {8, 16, 32};
+    if (argc == 4) {
+        Ws = {atoi(argv[1])};
+        waves = {atoi(argv[2])};
+        sizes = {(uint64_t)atoll(argv[3]) << 20};
+    }
+    for (int W : Ws)
+    for (int waves_per_cu : waves)
     for (uint64_t sz : sizes) {
         uint64_t nslots = sz / (16 * W);
         uint64_t mask = 1; while (mask * 2 <= nslots) mask *= 2; mask -= 1;
@@ -54,8 +62,9 @@ int main() {
         CK(hipEventRecord(a)); for (int r = 0; r < 5; ++r) run(); CK(hipEventRecord(b)); CK(hipEventSynchronize(b));
         float ms; CK(hipEventElapsedTime(&ms, a, b)); ms /= 5;
         double loads = (double)blocks * 256 * steps;
-        printf("W=%d x16B waves/CU=%2d table=%6.0f MiB: %7.2f ms  %6.2f G lane-accesses/s  (%.1f ns/access/lane)\n",
-               W, waves_per_cu, sz / 1048576.0, ms, loads / ms / 1e6, ms * 1e6 / steps);
+        printf("W=%d x16B waves/CU=%2d table=%6.0f MiB: %7.2f ms  %6.2f G lane-accesses/s  (%.1f ns/access/lane)"
+               "  %.0f accesses per dispatch\n",
+               W, waves_per_cu, sz / 1048576.0, ms, loads / ms / 1e6, ms * 1e6 / steps, loads);
         fflush(stdout);
     }
     return 0;
