@@ -142,6 +142,8 @@ SIGNATURES = [
                                           ctypes.c_void_p, ctypes.c_uint32]),
     ("tm_route_del", ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p,
                                     ctypes.c_uint32]),
+    ("tm_route_del_batch", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                          ctypes.c_void_p, ctypes.c_uint32]),
     ("tm_get_routes", ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_void_p,
                                      ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]),
     ("tm_route_count", ctypes.c_uint64, [ctypes.c_void_p]),

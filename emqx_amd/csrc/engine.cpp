@@ -26,6 +26,7 @@
 #include <memory>
 #include <mutex>
 #include <new>
+#include <set>
 #include <thread>
 #include <stdexcept>
 #include <string>
@@ -43,7 +44,6 @@ extern "C" int tm_topic_wildcard(const uint8_t* topic, uint32_t len);
 
 namespace {
 
-constexpr size_t PAGE_ELEMS = 4096;  // dirty granule: 4096 elements (64 KiB of 16 B slots, 128 KiB of nodes)
 
 struct DevError : std::runtime_error {
     using std::runtime_error::runtime_error;
@@ -80,18 +80,40 @@ size_t next_pow2(size_t x) {
     return p;
 }
 
-// dirty-page bitmap over a table of 16 B elements
+// the elements of a host table written since the last commit: a log of
+// indices (repeats allowed: the commit uploads each one's current value), or
+// "all" once the log passes `limit` (a sixteenth of the table, set at every
+// commit) -- then a plain copy of the whole table is cheaper than a scatter
 struct Dirty {
-    std::vector<uint8_t> pages;
-    bool all = true;  // whole table must be (re)uploaded
-    void mark(size_t idx) {
-        size_t pg = idx / PAGE_ELEMS;
-        if (pg >= pages.size()) pages.resize(pg + 1, 0);
-        pages[pg] = 1;
+    std::vector<uint32_t> idx;
+    bool all = true;            // whole table must be (re)uploaded
+    size_t limit = 1u << 16;
+    void mark(size_t i) {
+        if (all) return;
+        if (idx.size() >= limit) {
+            all = true;
+            std::vector<uint32_t>().swap(idx);
+            return;
+        }
+        idx.push_back((uint32_t)i);
     }
     void clear() {
-        std::fill(pages.begin(), pages.end(), 0);
+        idx.clear();
         all = false;
+    }
+};
+
+// a host table's dirty log since the last commit, and the previous commit's
+// (which the other image epoch missed)
+struct Track {
+    Dirty cur, prev;
+    void rotate(size_t table_elems) {
+        prev = cur;
+        cur.clear();
+        cur.limit = std::max<size_t>(4096, table_elems / 16);
+    }
+    void mark_range(size_t from, size_t to) {   // elements [from, to)
+        for (size_t i = from; i < to && !cur.all; ++i) cur.mark(i);
     }
 };
 
@@ -205,12 +227,18 @@ constexpr int MAX_SLOTS = 4;
 // long done).
 struct Image {
     DevBuf d_nodes, d_edges, d_hedges, d_dict, d_arena, d_woff, d_inner, d_leaf;
+    // route image (routes.hip) and aggre tables (aggre.hip), same epoch as the
+    // trie: a batch's filter ids and the route lists it expands them with
+    // always come from one commit
+    DevBuf d_rslots, d_rarena, d_rdest, d_fr_meta, d_rank_src, d_dt, d_rank_tg;
     size_t arena_uploaded = 0, woff_uploaded = 0;
     bool split_stale = true, written = false;
     uint64_t epoch = 0;
     std::vector<hipEvent_t> uses;
     void release() {
-        for (DevBuf* b : {&d_nodes, &d_edges, &d_hedges, &d_dict, &d_arena, &d_woff, &d_inner, &d_leaf}) b->release();
+        for (DevBuf* b : {&d_nodes, &d_edges, &d_hedges, &d_dict, &d_arena, &d_woff, &d_inner, &d_leaf, &d_rslots,
+                          &d_rarena, &d_rdest, &d_fr_meta, &d_rank_src, &d_dt, &d_rank_tg})
+            b->release();
         for (hipEvent_t ev : uses) (void)hipEventDestroy(ev);
         uses.clear();
     }
@@ -256,13 +284,21 @@ struct DevState {
         }
         img[i].uses.clear();
     }
-    // route image (emqx_route) and aggre tables
-    DevBuf d_fr_meta, d_fr_dest, d_ex_slots, d_ex_arena, d_ex_dest, d_ex_rank, d_dt, d_rank_src, d_rank_tg;
+    // commit packets: the changed elements of every table, one H2D copy,
+    // then a scatter per table into the back image
+    struct ScatterOp {
+        void* table;
+        uint64_t off, n;
+        uint32_t words;
+    };
+    std::vector<uint8_t> stage_host;
+    std::vector<ScatterOp> stage_ops;
+    DevBuf stage_dev;
     // workspaces: route / aggre (w_r*, w_d*, w_a*), host-buffer batches, merge
     DevBuf w_rexact, w_rscan, w_rids, w_rcounts, w_roff;
     DevBuf w_dsrc, w_dcount, w_akey, w_alarge;
     DevBuf w_mpre, w_mscan, w_bytes, w_off, w_counts, w_outoff, w_ids, w_total;
-    // the route / aggre workspaces and images are shared by every stream:
+    // the route / aggre workspaces are shared by every stream:
     // rw_done is recorded after the last route or aggre kernel of a batch;
     // the host waits on it before the next batch reuses (or reallocates) the
     // workspaces and before it rewrites an image
@@ -293,8 +329,7 @@ struct DevState {
         img[1].release();
         for (hipEvent_t ev : ev_spare) (void)hipEventDestroy(ev);
         ev_spare.clear();
-        for (DevBuf* b : {&d_fr_meta, &d_fr_dest, &d_ex_slots, &d_ex_arena, &d_ex_dest, &d_ex_rank, &d_dt, &d_rank_src,
-                          &d_rank_tg, &w_rexact, &w_rscan, &w_rids, &w_rcounts, &w_roff, &w_dsrc, &w_dcount, &w_akey,
+        for (DevBuf* b : {&stage_dev, &w_rexact, &w_rscan, &w_rids, &w_rcounts, &w_roff, &w_dsrc, &w_dcount, &w_akey,
                           &w_alarge, &w_mpre, &w_mscan, &w_bytes, &w_off, &w_counts, &w_outoff, &w_ids, &w_total})
             b->release();
         for (auto& w : slots) {
@@ -386,23 +421,57 @@ struct tm_engine {
     // ---- route table: the emqx_route bag (src/emqx_router.erl:52-59) ----
     std::unordered_map<std::string, uint32_t> dest_index;   // dest bytes -> dest id
     std::vector<std::string> dest_names;
-    std::unordered_map<std::string, std::vector<uint32_t>> route_bag;   // topic -> dests, insertion order
-    // membership index of the bags past BAG_INDEX_MIN dests (a bag is scanned
-    // linearly below that): add/del of a route stay O(1) probes for topics
-    // with tens of thousands of dests
+    static constexpr uint32_t SLOT_NONE = 0xFFFFFFFFu;
+    // one topic with routes, and where the route image holds it
+    struct RouteRec {
+        std::vector<uint32_t> dests;          // the bag, insertion order
+        // membership index once the bag passes BAG_INDEX_MIN dests (scanned
+        // linearly below that): add/del of a route stay O(1) probes for
+        // topics with tens of thousands of dests
+        std::unique_ptr<std::unordered_set<uint32_t>> index;
+        const std::string* key = nullptr;     // the route_bag key (node-stable)
+        uint32_t slot = SLOT_NONE;            // exact-table slot (rt_slots)
+        uint32_t fid = FILTER_NONE;           // trie filter of a wildcard topic, while both exist
+        uint32_t label = 0;                   // to_rank: order label, Erlang binary order of the topics
+        uint32_t off = 0, cap = 0;            // dest segment in rt_dest
+        uint64_t arena = 0, words = 0;        // topic bytes in rt_arena (u64 words)
+        bool has(uint32_t d) const {
+            return index ? index->count(d) != 0 : std::find(dests.begin(), dests.end(), d) != dests.end();
+        }
+    };
     static constexpr size_t BAG_INDEX_MIN = 32;
-    std::unordered_map<std::string, std::unordered_set<uint32_t>> bag_index;
-    bool bag_has(const std::string& key, const std::vector<uint32_t>& bag, uint32_t dest) const {
-        if (bag.size() < BAG_INDEX_MIN) return std::find(bag.begin(), bag.end(), dest) != bag.end();
-        auto ix = bag_index.find(key);
-        return ix != bag_index.end() && ix->second.count(dest);
-    }
+    std::unordered_map<std::string, RouteRec> route_bag;   // topic -> its routes
     size_t route_total = 0;
-    bool routes_dirty = true;         // the route image must be rebuilt at commit
-    std::vector<uint32_t> h_fr_off;   // host copy of fr_meta's offsets (aggre rewrites the ranks)
-    uint64_t ex_slot_mask = 0;
-    uint32_t fr_filters = 0;          // filter ids covered by fr_meta
-    bool route_image = false;
+    // The route image, maintained in place by every add / del (no rebuild):
+    // commit uploads the dirty pages into the back image epoch.
+    //   rt_slots  exact-topic table (open addressing, load <= 1/2, backward-
+    //             shift deletion): get_routes(Topic) of a publish topic
+    //   rt_arena  topic bytes of the slots (u64 words, zero padded)
+    //   rt_dest   dest segments, one per topic (capacity doubles; a moved
+    //             segment leaves garbage, compacted past half the pool)
+    //   fr_meta   filter id -> {segment, count, label}: the routes of a
+    //             matched wildcard filter (the same segment as its slot)
+    //   rank_src  label -> that topic as a route source (aggre's large lists)
+    std::vector<ExactSlot> rt_slots = std::vector<ExactSlot>(16, ExactSlot{0, 0, 0, 0, 0, 0});
+    std::vector<RouteRec*> rt_slot_rec = std::vector<RouteRec*>(16, nullptr);
+    size_t rt_used = 0;
+    std::vector<uint64_t> rt_arena;
+    size_t rt_arena_garbage = 0;
+    std::vector<uint32_t> rt_dest;
+    size_t rt_dest_garbage = 0;
+    size_t route_gc_min = 1u << 20;   // option "route_gc": garbage entries before a compaction is considered
+    std::vector<uint4> fr_meta;
+    std::vector<RouteRec*> fr_rec;   // filter id -> linked topic
+    // to_rank labels: an order-maintenance labelling of the topics (list
+    // labelling with density thresholds per window), so a new topic costs
+    // O(log^2 n) amortised relabels, not a re-rank of every topic
+    struct RecLess {
+        bool operator()(const RouteRec* a, const RouteRec* b) const { return *a->key < *b->key; }
+    };
+    std::set<RouteRec*, RecLess> rt_order;
+    uint32_t label_bits = 16;        // label universe 2^label_bits
+    std::vector<uint32_t> rank_src = std::vector<uint32_t>(1u << 16, TM_ROUTE_TOPIC_ID);
+    Track t_slots, t_rarena, t_rdest, t_fr_meta, t_rank_src, t_dt, t_rank_tg;
     // ---- emqx_broker:aggre/1 targets (aggre.hip) ----
     // a dest aggregates to a target: a node (atom) or a $share group; targets
     // are interned as kind byte + key bytes, so string order is the Erlang
@@ -411,9 +480,9 @@ struct tm_engine {
     std::vector<std::string> target_names;
     std::vector<uint32_t> dest_target;      // dest id -> target id (TARGET_DEFAULT: node named by the dest bytes)
     static constexpr uint32_t TARGET_DEFAULT = 0xFFFFFFFFu;
-    struct AggKey { const std::string* key; uint32_t dest_off; uint32_t fid; };
-    std::vector<AggKey> agg_keys;           // route image entries (set by build_route_image)
-    bool aggre_dirty = true;
+    std::vector<uint2> dt;                  // dest id -> {target rank, target id | group << 31}
+    std::vector<uint32_t> rank_tg;          // target rank -> target id
+    bool targets_dirty = true;              // a dest or a dest's target was added: re-rank the targets
 
     // ---- batch pipeline knobs ----
     int nslots = 2;                     // option "slots"
@@ -784,9 +853,11 @@ struct tm_engine {
         filter_arena.insert(filter_arena.end(), p, p + len);
         filters[id] = FilterRec{off, len, node};
         ++live_filters;
+        on_filter_new(p, len, id);
         return id;
     }
     void free_filter(uint32_t id) {
+        on_filter_free(id);
         filters[id].node = NODE_NONE;
         free_filters.push_back(id);
         --live_filters;
@@ -806,7 +877,6 @@ struct tm_engine {
             add_summaries(!tmp_words.empty() && tmp_words.back() == WORD_HASH);
         }
         dev_dirty = true;
-        routes_dirty = true;   // filter ids may have changed
     }
 
     // emqx_trie:delete/1 (src/emqx_trie.erl:88-96) + delete_path/1 (:149-163)
@@ -832,7 +902,6 @@ struct tm_engine {
             }
         }
         dev_dirty = true;
-        routes_dirty = true;
     }
 
     // ------------------------------------------------------------------
@@ -846,6 +915,8 @@ struct tm_engine {
         const uint32_t id = (uint32_t)dest_names.size();
         dest_names.push_back(k);
         dest_index.emplace(std::move(k), id);
+        targets_dirty = true;   // dt must cover the new dest
+        dev_dirty = true;
         return id;
     }
     // handle_cast({add_route, Route}) (:153-163) + add_trie_route/1 (:226-231)
@@ -853,16 +924,27 @@ struct tm_engine {
         const uint32_t dest = intern_dest(d, dlen);
         std::string key(reinterpret_cast<const char*>(t), tlen);
         auto it = route_bag.find(key);
-        if (it != route_bag.end() && bag_has(key, it->second, dest))
-            return;   // lists:member(Route, get_routes(Topic)) -> ok
-        const bool had = it != route_bag.end() && !it->second.empty();
-        if (tm_topic_wildcard(t, tlen) && !had) insert(t, tlen);   // mnesia:wread -> [] -> emqx_trie:insert
-        std::vector<uint32_t>& bag = route_bag[key];
-        bag.push_back(dest);
-        if (bag.size() == BAG_INDEX_MIN) bag_index[key].insert(bag.begin(), bag.end());
-        else if (bag.size() > BAG_INDEX_MIN) bag_index[key].insert(dest);
+        if (it != route_bag.end() && it->second.has(dest)) return;   // lists:member(Route, get_routes(Topic)) -> ok
+        const bool wild = tm_topic_wildcard(t, tlen);
+        if (it == route_bag.end()) {
+            if (wild) insert(t, tlen);   // mnesia:wread -> [] -> emqx_trie:insert
+            it = route_bag.emplace(std::move(key), RouteRec{}).first;
+            RouteRec& r = it->second;
+            r.key = &it->first;
+            rt_arena_put(r);
+            rt_slot_put(&r);
+            order_insert(&r);
+            if (wild) fr_link(&r, filter_of(t, tlen));
+        }
+        RouteRec& r = it->second;
+        r.dests.push_back(dest);
+        if (r.dests.size() == BAG_INDEX_MIN)
+            r.index.reset(new std::unordered_set<uint32_t>(r.dests.begin(), r.dests.end()));
+        else if (r.index)
+            r.index->insert(dest);
+        seg_write(r, r.dests.size() - 1);
         ++route_total;
-        routes_dirty = true;
+        dev_dirty = true;
     }
     // handle_cast({del_route, Route}) (:165-187) + del_trie_route/1 (:252-260)
     // or del_direct_route/1 (:240-241); the emqx_subscriber check (:179) is
@@ -872,25 +954,33 @@ struct tm_engine {
         if (di == dest_index.end()) return;
         auto it = route_bag.find(std::string(reinterpret_cast<const char*>(t), tlen));
         if (it == route_bag.end()) return;   // [] -> ok
-        std::vector<uint32_t>& bag = it->second;
-        if (!bag_has(it->first, bag, di->second)) return;   // delete_object of an absent route: no-op
-        bag.erase(std::find(bag.begin(), bag.end(), di->second));
-        if (bag.size() + 1 >= BAG_INDEX_MIN) {
-            auto ix = bag_index.find(it->first);
-            if (bag.size() < BAG_INDEX_MIN) bag_index.erase(ix);
-            else ix->second.erase(di->second);
+        RouteRec& r = it->second;
+        if (!r.has(di->second)) return;      // delete_object of an absent route: no-op
+        const size_t at = std::find(r.dests.begin(), r.dests.end(), di->second) - r.dests.begin();
+        r.dests.erase(r.dests.begin() + at);
+        if (r.index) {
+            if (r.dests.size() < BAG_INDEX_MIN) r.index.reset();
+            else r.index->erase(di->second);
         }
-        const bool last = bag.empty();
         --route_total;
-        if (last) {
-            route_bag.erase(it);
-            if (tm_topic_wildcard(t, tlen)) remove(t, tlen);   // [Route] -> emqx_trie:delete(Topic)
+        dev_dirty = true;
+        if (!r.dests.empty()) {
+            seg_write(r, at);
+            return;
         }
-        routes_dirty = true;
+        // the last route of the topic: out of the image, then [Route] -> emqx_trie:delete(Topic)
+        fr_unlink(&r);
+        rt_slot_del(&r);
+        order_erase(&r);
+        rt_dest_garbage += r.cap;
+        rt_arena_garbage += r.words;
+        route_bag.erase(it);
+        if (tm_topic_wildcard(t, tlen)) remove(t, tlen);
+        maybe_compact_routes();
     }
     const std::vector<uint32_t>* get_routes(const uint8_t* t, uint32_t tlen) const {
         auto it = route_bag.find(std::string(reinterpret_cast<const char*>(t), tlen));
-        return it == route_bag.end() ? nullptr : &it->second;
+        return it == route_bag.end() ? nullptr : &it->second.dests;
     }
     // filter id of a trie filter (or FILTER_NONE)
     uint32_t filter_of(const uint8_t* p, uint32_t len) {
@@ -898,82 +988,233 @@ struct tm_engine {
         const uint32_t v = walk(tmp_words);
         return v == NODE_NONE ? FILTER_NONE : nodes[v].self_filter;
     }
-    // rebuild the route image: per-filter-id dest lists (CSR) and the
-    // exact-topic table over every topic with routes
-    void build_route_image() {
-        for (auto& d : devs) {   // no route / aggre kernel may read the image being replaced
-            Guard g(d->device);
-            d->rw_drain();
+
+    // ---- route image maintenance ----
+    // the slot, filter entry and label entry of topic r, from its record
+    void rt_sync(const RouteRec& r) {
+        const uint32_t count = (uint32_t)r.dests.size();
+        if (r.slot != SLOT_NONE) {
+            ExactSlot& s = rt_slots[r.slot];
+            s.count = count;
+            s.dest_off = r.off;
+            s.rank = r.label;
+            s.arena = r.arena * 8;
+            t_slots.cur.mark(r.slot);
         }
-        const uint32_t nf = (uint32_t)filters.size();
-        std::vector<uint32_t> fr_off(nf + 1, 0);
-        std::vector<std::pair<uint32_t, const std::vector<uint32_t>*>> by_fid;
-        by_fid.reserve(route_bag.size());
-        size_t cap = 16;
-        while (cap < route_bag.size() * 2) cap <<= 1;
-        std::vector<ExactSlot> slots(cap);
-        for (auto& x : slots) x = ExactSlot{0, 0, 0, 0, 0, 0};
-        std::vector<uint8_t> arena;
-        std::vector<uint32_t> ex_dest;
-        ex_dest.reserve(route_total);
-        agg_keys.clear();
-        agg_keys.reserve(route_bag.size());
-        aggre_dirty = true;
-        for (const auto& kv : route_bag) {
-            const uint8_t* t = reinterpret_cast<const uint8_t*>(kv.first.data());
-            const uint32_t tlen = (uint32_t)kv.first.size();
-            uint32_t fid = FILTER_NONE;
-            if (tm_topic_wildcard(t, tlen)) {
-                fid = filter_of(t, tlen);
-                if (fid != FILTER_NONE) {
-                    fr_off[fid + 1] = (uint32_t)kv.second.size();
-                    by_fid.emplace_back(fid, &kv.second);
-                }
-            }
-            agg_keys.push_back(AggKey{&kv.first, (uint32_t)ex_dest.size(), fid});
-            const uint64_t h = word_hash(t, tlen);
-            size_t sl = h & (cap - 1);
-            while (slots[sl].hash) sl = (sl + 1) & (cap - 1);
-            ExactSlot& e = slots[sl];
-            e.hash = h;
-            e.len = tlen;
-            e.count = (uint32_t)kv.second.size();
-            e.arena = arena.size();
-            e.dest_off = (uint32_t)ex_dest.size();
-            arena.resize(arena.size() + std::max<size_t>(8, (tlen + 7) & ~size_t(7)), 0);
-            if (tlen) std::memcpy(&arena[e.arena], t, tlen);
-            ex_dest.insert(ex_dest.end(), kv.second.begin(), kv.second.end());
+        if (r.fid != FILTER_NONE) {
+            fr_meta[r.fid] = make_uint4(r.off, count, r.label, 0u);
+            t_fr_meta.cur.mark(r.fid);
         }
-        for (uint32_t f = 0; f < nf; ++f) fr_off[f + 1] += fr_off[f];
-        std::vector<uint32_t> fr_dest(fr_off[nf]);
-        for (const auto& x : by_fid) std::copy(x.second->begin(), x.second->end(), fr_dest.begin() + fr_off[x.first]);
-        std::vector<uint2> meta(fr_off.size());
-        for (size_t f = 0; f < fr_off.size(); ++f) meta[f] = make_uint2(fr_off[f], 0u);
-        for (auto& dp : devs) {
-            DevState& d = *dp;
-            Guard g(d.device);
-            auto up = [&](DevBuf& b, const void* src, size_t bytes) {
-                b.ensure(std::max<size_t>(bytes, 16));
-                if (bytes) HIPCHK(hipMemcpyAsync(b.p, src, bytes, hipMemcpyHostToDevice, d.stream));
-            };
-            up(d.d_fr_meta, meta.data(), meta.size() * sizeof(uint2));
-            up(d.d_fr_dest, fr_dest.data(), fr_dest.size() * 4);
-            up(d.d_ex_slots, slots.data(), slots.size() * sizeof(ExactSlot));
-            up(d.d_ex_arena, arena.data(), arena.size());
-            up(d.d_ex_dest, ex_dest.data(), ex_dest.size() * 4);
-            HIPCHK(hipStreamSynchronize(d.stream));   // host vectors die here
-        }
-        ex_slot_mask = cap - 1;
-        fr_filters = nf;
-        route_image = !route_bag.empty();
-        h_fr_off.swap(fr_off);
-        routes_dirty = false;
+        rank_src[r.label] = r.fid != FILTER_NONE ? r.fid : TM_ROUTE_TOPIC_ID;
+        t_rank_src.cur.mark(r.label);
     }
+    // dests [from, end) of r into its segment (a new, doubled segment at the
+    // pool's end when they no longer fit; the old one becomes garbage)
+    void seg_write(RouteRec& r, size_t from) {
+        const size_t n = r.dests.size();
+        if (n > r.cap) {
+            rt_dest_garbage += r.cap;
+            uint32_t cap = std::max<uint32_t>(r.cap * 2, 2);
+            while (cap < n) cap *= 2;
+            if (rt_dest.size() + cap >= 0xFFFFFFF0ull) throw RangeError("route dest pool past 2^32 entries");
+            r.off = (uint32_t)rt_dest.size();
+            r.cap = cap;
+            rt_dest.resize(rt_dest.size() + cap, 0);
+            from = 0;
+        }
+        if (n > from) {
+            std::copy(r.dests.begin() + from, r.dests.end(), rt_dest.begin() + r.off + from);
+            t_rdest.mark_range(r.off + from, r.off + n);
+        }
+        rt_sync(r);
+    }
+    void rt_arena_put(RouteRec& r) {
+        const uint32_t len = (uint32_t)r.key->size();
+        r.words = std::max<uint64_t>(1, (len + 7) / 8);
+        r.arena = rt_arena.size();
+        rt_arena.resize(rt_arena.size() + r.words, 0);
+        if (len) std::memcpy(&rt_arena[r.arena], r.key->data(), len);
+        t_rarena.mark_range(r.arena, r.arena + r.words);
+    }
+    void rt_slot_put(RouteRec* r) {
+        if ((rt_used + 1) * 2 > rt_slots.size()) rt_regrow(rt_slots.size() * 2);
+        const uint8_t* t = reinterpret_cast<const uint8_t*>(r->key->data());
+        const uint64_t h = word_hash(t, (uint32_t)r->key->size());
+        const size_t mask = rt_slots.size() - 1;
+        size_t s = h & mask;
+        while (rt_slots[s].hash) s = (s + 1) & mask;
+        rt_slots[s] = ExactSlot{h, (uint32_t)r->key->size(), 0, r->arena * 8, 0, 0};
+        rt_slot_rec[s] = r;
+        r->slot = (uint32_t)s;
+        ++rt_used;
+        t_slots.cur.mark(s);
+    }
+    // backward-shift deletion: later members of the probe run move up, so
+    // lookups never need tombstones
+    void rt_slot_del(RouteRec* r) {
+        const size_t mask = rt_slots.size() - 1;
+        size_t i = r->slot;
+        for (size_t j = (i + 1) & mask; rt_slots[j].hash; j = (j + 1) & mask) {
+            const size_t home = rt_slots[j].hash & mask;
+            // move j into the hole at i unless its home lies cyclically in (i, j]
+            const bool stays = i <= j ? (home > i && home <= j) : (home > i || home <= j);
+            if (stays) continue;
+            rt_slots[i] = rt_slots[j];
+            rt_slot_rec[i] = rt_slot_rec[j];
+            rt_slot_rec[i]->slot = (uint32_t)i;
+            t_slots.cur.mark(i);
+            i = j;
+        }
+        rt_slots[i] = ExactSlot{0, 0, 0, 0, 0, 0};
+        rt_slot_rec[i] = nullptr;
+        t_slots.cur.mark(i);
+        r->slot = SLOT_NONE;
+        --rt_used;
+    }
+    void rt_regrow(size_t cap) {
+        std::vector<RouteRec*> recs;
+        recs.reserve(rt_used);
+        for (RouteRec* r : rt_slot_rec)
+            if (r) recs.push_back(r);
+        rt_slots.assign(cap, ExactSlot{0, 0, 0, 0, 0, 0});
+        rt_slot_rec.assign(cap, nullptr);
+        rt_used = 0;
+        for (RouteRec* r : recs) {
+            rt_slot_put(r);
+            rt_sync(*r);
+        }
+        t_slots.cur.all = true;
+    }
+    // the pool and the arena rewritten without garbage (all pages re-uploaded)
+    void maybe_compact_routes() {
+        const bool dest_gc = rt_dest_garbage > route_gc_min && rt_dest_garbage * 2 > rt_dest.size();
+        const bool arena_gc = rt_arena_garbage > route_gc_min / 4 && rt_arena_garbage * 2 > rt_arena.size();
+        if (!dest_gc && !arena_gc) return;
+        std::vector<uint32_t> nd;
+        std::vector<uint64_t> na;
+        if (dest_gc) nd.reserve(rt_dest.size() - rt_dest_garbage);
+        if (arena_gc) na.reserve(rt_arena.size() - rt_arena_garbage);
+        for (auto& kv : route_bag) {
+            RouteRec& r = kv.second;
+            if (dest_gc) {
+                const uint32_t off = (uint32_t)nd.size();
+                nd.insert(nd.end(), rt_dest.begin() + r.off, rt_dest.begin() + r.off + r.cap);
+                r.off = off;
+            }
+            if (arena_gc) {
+                const uint64_t a = na.size();
+                na.insert(na.end(), rt_arena.begin() + r.arena, rt_arena.begin() + r.arena + r.words);
+                r.arena = a;
+            }
+            rt_sync(r);
+        }
+        if (dest_gc) {
+            rt_dest.swap(nd);
+            rt_dest_garbage = 0;
+            t_rdest.cur.all = true;
+        }
+        if (arena_gc) {
+            rt_arena.swap(na);
+            rt_arena_garbage = 0;
+            t_rarena.cur.all = true;
+        }
+    }
+    // a wildcard topic's filter id <-> its routes
+    void fr_link(RouteRec* r, uint32_t fid) {
+        if (fid == FILTER_NONE) return;
+        if (fid >= fr_meta.size()) {
+            const size_t old = fr_meta.size(), n = std::max<size_t>(fid + 1, filters.size());
+            fr_meta.resize(n, make_uint4(0, 0, 0, 0));
+            fr_rec.resize(n, nullptr);
+            t_fr_meta.mark_range(old, n);
+        }
+        r->fid = fid;
+        fr_rec[fid] = r;
+        rt_sync(*r);
+    }
+    void fr_unlink(RouteRec* r) {
+        if (r->fid == FILTER_NONE) return;
+        fr_meta[r->fid] = make_uint4(0, 0, 0, 0);
+        fr_rec[r->fid] = nullptr;
+        t_fr_meta.cur.mark(r->fid);
+        r->fid = FILTER_NONE;
+        rt_sync(*r);
+    }
+    // trie hooks (new_filter / free_filter): a filter created or deleted
+    // outside add_route / del_route (tm_insert / tm_delete of a topic that
+    // has routes) keeps the link right
+    void on_filter_new(const uint8_t* p, uint32_t len, uint32_t fid) {
+        if (route_bag.empty() || !tm_topic_wildcard(p, len)) return;
+        auto it = route_bag.find(std::string(reinterpret_cast<const char*>(p), len));
+        if (it != route_bag.end() && it->second.fid == FILTER_NONE) fr_link(&it->second, fid);
+    }
+    void on_filter_free(uint32_t fid) {
+        if (fid < fr_rec.size() && fr_rec[fid]) fr_unlink(fr_rec[fid]);
+    }
+
+    // ---- to_rank labels (order maintenance) ----
+    void set_label(RouteRec* r, uint32_t label) {
+        r->label = label;
+        rt_sync(*r);
+    }
+    void order_insert(RouteRec* r) {
+        auto it = rt_order.insert(r).first;
+        if ((uint64_t)rt_order.size() * 4 > (1ull << label_bits)) {   // keep the universe >= 4n
+            relabel_all(label_bits + 1);
+            return;
+        }
+        const int64_t U = int64_t(1) << label_bits;
+        const int64_t lo = it == rt_order.begin() ? -1 : (int64_t)(*std::prev(it))->label;
+        const int64_t hi = std::next(it) == rt_order.end() ? U : (int64_t)(*std::next(it))->label;
+        if (hi - lo >= 2) {
+            set_label(r, (uint32_t)(lo + (hi - lo) / 2));
+            return;
+        }
+        // no gap: the smallest aligned window around the neighbours whose
+        // density is under its threshold (1 at width 2, falling to 1/2 at the
+        // whole universe) is spread evenly, the new topic included
+        const int64_t anchor = lo >= 0 ? lo : 0;
+        auto left = it, right = std::next(it);   // [left, right) = the window's members
+        int64_t count = 1;
+        for (uint32_t k = 1; k <= label_bits; ++k) {
+            const int64_t L = (anchor >> k) << k, R = L + (int64_t(1) << k);
+            while (left != rt_order.begin() && (int64_t)(*std::prev(left))->label >= L) {
+                --left;
+                ++count;
+            }
+            while (right != rt_order.end() && (int64_t)(*right)->label < R) {
+                ++right;
+                ++count;
+            }
+            const double tau = 1.0 - 0.5 * (double)k / (double)label_bits;
+            if ((double)count <= tau * (double)(R - L)) {
+                spread(left, right, count, L, R);
+                return;
+            }
+        }
+        relabel_all(label_bits + 1);
+    }
+    // members [a, b) (count of them) get labels evenly spaced in [L, R)
+    void spread(std::set<RouteRec*, RecLess>::iterator a, std::set<RouteRec*, RecLess>::iterator b, int64_t count,
+                int64_t L, int64_t R) {
+        const double step = (double)(R - L) / (double)count;
+        int64_t i = 0;
+        for (auto x = a; x != b; ++x, ++i) set_label(*x, (uint32_t)(L + (int64_t)(step * (double)i + step / 2)));
+    }
+    void relabel_all(uint32_t bits) {
+        while ((uint64_t)rt_order.size() * 4 > (1ull << bits)) ++bits;
+        if (bits > 31) throw RangeError("route topics past 2^29: to_rank labels exhausted");
+        label_bits = bits;
+        rank_src.assign(size_t(1) << bits, TM_ROUTE_TOPIC_ID);
+        t_rank_src.cur.all = true;
+        if (!rt_order.empty()) spread(rt_order.begin(), rt_order.end(), (int64_t)rt_order.size(), 0, int64_t(1) << bits);
+    }
+    void order_erase(RouteRec* r) { rt_order.erase(r); }   // its label is simply free again
+
     // ------------------------------------------------------------------
-    // emqx_broker:aggre/1 (src/emqx_broker.erl:194-206) tables: to_rank of
-    // every topic with routes (std::string order = Erlang binary order:
-    // bytewise unsigned, a proper prefix first), and per dest its target's
-    // rank and id.  Rebuilt after the route image or a target changes.
+    // emqx_broker:aggre/1 (src/emqx_broker.erl:194-206) targets: per dest its
+    // target's rank and id, the targets in Erlang term order.  Small tables
+    // (nodes and $share groups), re-ranked when a dest or a target is added.
     uint32_t intern_target(uint32_t kind, const uint8_t* k, uint32_t klen) {
         std::string key(1, (char)kind);
         key.append(reinterpret_cast<const char*>(k), klen);
@@ -985,28 +1226,7 @@ struct tm_engine {
         target_index.emplace(std::move(key), id);
         return id;
     }
-    void build_aggre_image() {
-        for (auto& d : devs) {
-            Guard g(d->device);
-            d->rw_drain();
-        }
-        const uint32_t nf = fr_filters;
-        std::vector<uint32_t> order(agg_keys.size());
-        for (uint32_t i = 0; i < order.size(); ++i) order[i] = i;
-        std::sort(order.begin(), order.end(),
-                  [&](uint32_t a, uint32_t b) { return *agg_keys[a].key < *agg_keys[b].key; });
-        std::vector<uint2> fr_meta(h_fr_off.size());
-        for (size_t f = 0; f < h_fr_off.size(); ++f) fr_meta[f] = make_uint2(h_fr_off[f], 0u);
-        std::vector<uint32_t> ex_rank(std::max<size_t>(route_total, 1), 0);
-        std::vector<uint32_t> rank_src(std::max<size_t>(order.size(), 1), TM_ROUTE_TOPIC_ID);
-        for (uint32_t r = 0; r < order.size(); ++r) {
-            const AggKey& a = agg_keys[order[r]];
-            if (a.fid != FILTER_NONE && a.fid < nf) fr_meta[a.fid].y = r;
-            if (a.dest_off < ex_rank.size()) ex_rank[a.dest_off] = r;
-            // the To of rank r as a route source: its filter id when it is a
-            // trie filter, else the literal topic (same To binary either way)
-            rank_src[r] = a.fid != FILTER_NONE ? a.fid : TM_ROUTE_TOPIC_ID;
-        }
+    void rank_targets() {
         const size_t nd = dest_names.size();
         dest_target.resize(nd, TARGET_DEFAULT);
         for (size_t d = 0; d < nd; ++d)
@@ -1019,47 +1239,33 @@ struct tm_engine {
         for (uint32_t i = 0; i < tord.size(); ++i) tord[i] = i;
         std::sort(tord.begin(), tord.end(), [&](uint32_t a, uint32_t b) { return target_names[a] < target_names[b]; });
         for (uint32_t r = 0; r < tord.size(); ++r) trank[tord[r]] = r;
-        std::vector<uint32_t> rank_tg(std::max<size_t>(tord.size(), 1), 0);
-        for (uint32_t r = 0; r < tord.size(); ++r) rank_tg[r] = tord[r];
-        std::vector<uint2> dt(std::max<size_t>(nd, 1));
+        rank_tg.assign(tord.begin(), tord.end());
+        dt.resize(nd);
         for (size_t d = 0; d < nd; ++d) {
             const uint32_t tid = dest_target[d];
             dt[d] = make_uint2(trank[tid], tid | (target_names[tid][0] ? 0x80000000u : 0u));
         }
-        for (auto& dp : devs) {
-            DevState& d = *dp;
-            Guard g(d.device);
-            auto up = [&](DevBuf& b, const void* src, size_t bytes) {
-                b.ensure(std::max<size_t>(bytes, 16));
-                if (bytes) HIPCHK(hipMemcpyAsync(b.p, src, bytes, hipMemcpyHostToDevice, d.stream));
-            };
-            if (!fr_meta.empty()) up(d.d_fr_meta, fr_meta.data(), fr_meta.size() * sizeof(uint2));
-            up(d.d_ex_rank, ex_rank.data(), ex_rank.size() * 4);
-            up(d.d_dt, dt.data(), dt.size() * sizeof(uint2));
-            up(d.d_rank_src, rank_src.data(), rank_src.size() * 4);
-            up(d.d_rank_tg, rank_tg.data(), rank_tg.size() * 4);
-            HIPCHK(hipStreamSynchronize(d.stream));   // host vectors die here
-        }
-        aggre_dirty = false;
+        t_dt.cur.all = true;
+        t_rank_tg.cur.all = true;
+        targets_dirty = false;
     }
-    static AggreView aggre_view(const DevState& d) {
+    AggreView aggre_view(const DevState& d) const {
+        const Image& g = d.img[d.cur];
         AggreView av;
-        av.ex_rank = d.d_ex_rank.as<const uint32_t>();
-        av.dt = d.d_dt.as<const uint2>();
-        av.rank_src = d.d_rank_src.as<const uint32_t>();
-        av.rank_tg = d.d_rank_tg.as<const uint32_t>();
+        av.dt = g.d_dt.as<const uint2>();
+        av.rank_src = g.d_rank_src.as<const uint32_t>();
+        av.rank_tg = g.d_rank_tg.as<const uint32_t>();
         return av;
     }
-
     RouteView route_view(const DevState& d) const {
+        const Image& g = d.img[d.cur];
         RouteView rv;
-        rv.fr_meta = d.d_fr_meta.as<const uint2>();
-        rv.fr_dest = d.d_fr_dest.as<const uint32_t>();
-        rv.n_filters = route_image ? fr_filters : 0u;
-        rv.ex_slots = route_image ? d.d_ex_slots.as<const ExactSlot>() : nullptr;
-        rv.ex_slot_mask = ex_slot_mask;
-        rv.ex_arena = d.d_ex_arena.as<const uint8_t>();
-        rv.ex_dest = d.d_ex_dest.as<const uint32_t>();
+        rv.fr_meta = g.d_fr_meta.as<const uint4>();
+        rv.n_filters = (uint32_t)fr_meta.size();
+        rv.ex_slots = g.d_rslots.as<const ExactSlot>();
+        rv.ex_slot_mask = rt_slots.size() - 1;
+        rv.ex_arena = g.d_rarena.as<const uint8_t>();
+        rv.dest = g.d_rdest.as<const uint32_t>();
         return rv;
     }
 
@@ -1322,36 +1528,54 @@ struct tm_engine {
     // upload a host table to one replica: the whole table after a resize (or
     // when the replica is new), else the dirty pages; the caller clears the
     // dirty map once every replica has its copy
-    // pages dirtied since image g was last written: this commit's and, when g
-    // missed the previous commit (two epochs), that one's too
+    // the elements changed since image g was last written (this commit's log
+    // and, when g missed the previous commit (two epochs), that one's too):
+    // packed for one scatter, or the whole table copied when that is cheaper
     template <class T>
     void upload_table(DevState& d, Image& g, DevBuf& buf, const std::vector<T>& host, const Dirty& dirty,
                       const Dirty& prev) {
+        static_assert(sizeof(T) % 4 == 0, "tables are scattered in 32-bit words");
         const bool re = buf.ensure_async(std::max<size_t>(host.size(), 1) * sizeof(T), d.stream);
         // g holds commit g.epoch; this one makes epoch + 1
         const bool two = g.written && g.epoch + 1 == epoch;        // g missed exactly the previous commit
         const bool stale = !g.written || g.epoch + 1 < epoch;      // missed more (double_buffer switched on)
-        if (re || stale || dirty.all || (two && prev.all)) {
-            HIPCHK(hipMemcpyAsync(buf.p, host.data(), host.size() * sizeof(T), hipMemcpyHostToDevice, d.stream));
+        const size_t n = dirty.idx.size() + (two ? prev.idx.size() : 0);
+        if (re || stale || dirty.all || (two && prev.all) || n * (4 + sizeof(T)) * 4 > host.size() * sizeof(T)) {
+            if (!host.empty())
+                HIPCHK(hipMemcpyAsync(buf.p, host.data(), host.size() * sizeof(T), hipMemcpyHostToDevice, d.stream));
             return;
         }
-        const size_t np = std::max(dirty.pages.size(), two ? prev.pages.size() : 0);
-        auto is_dirty = [&](size_t pg) {
-            return (pg < dirty.pages.size() && dirty.pages[pg]) || (two && pg < prev.pages.size() && prev.pages[pg]);
-        };
-        for (size_t pg = 0; pg < np;) {
-            if (!is_dirty(pg)) {
-                ++pg;
-                continue;
+        if (n == 0) return;
+        const uint64_t off = (d.stage_host.size() + 15) & ~uint64_t(15);
+        d.stage_host.resize(off + n * (4 + sizeof(T)));
+        uint32_t* ix = reinterpret_cast<uint32_t*>(d.stage_host.data() + off);
+        // values as bytes: ix + n need not meet T's alignment (ExactSlot is
+        // alignas(32)), so no T* may point there
+        uint8_t* val = reinterpret_cast<uint8_t*>(ix + n);
+        size_t k = 0;
+        for (const Dirty* dl : {&dirty, &prev}) {
+            if (dl == &prev && !two) break;
+            for (uint32_t i : dl->idx) {
+                if (i >= host.size())
+                    throw DevError("commit: dirty index " + std::to_string(i) + " past a table of " +
+                                   std::to_string(host.size()) + " elements of " + std::to_string(sizeof(T)) + " B");
+                ix[k] = i;
+                std::memcpy(val + k * sizeof(T), &host[i], sizeof(T));
+                ++k;
             }
-            size_t q = pg;
-            while (q < np && is_dirty(q)) ++q;
-            const size_t a = pg * PAGE_ELEMS, b = std::min(host.size(), q * PAGE_ELEMS);
-            if (a < b)
-                HIPCHK(hipMemcpyAsync(buf.as<T>() + a, host.data() + a, (b - a) * sizeof(T), hipMemcpyHostToDevice,
-                                      d.stream));
-            pg = q;
         }
+        d.stage_ops.push_back(DevState::ScatterOp{buf.p, off, n, (uint32_t)(sizeof(T) / 4)});
+    }
+    // the packed changes of every table: one copy, a scatter per table
+    void flush_stage(DevState& d) {
+        if (d.stage_ops.empty()) return;
+        d.stage_dev.ensure_async(d.stage_host.size(), d.stream);
+        HIPCHK(hipMemcpyAsync(d.stage_dev.p, d.stage_host.data(), d.stage_host.size(), hipMemcpyHostToDevice, d.stream));
+        for (const auto& op : d.stage_ops)
+            HIPCHK(launch_scatter(op.table, reinterpret_cast<const uint32_t*>(d.stage_dev.as<uint8_t>() + op.off), op.n,
+                                  op.words, d.stream));
+        d.stage_ops.clear();
+        d.stage_host.clear();
     }
 
     void maybe_relayout() {
@@ -1367,6 +1591,7 @@ struct tm_engine {
     // were launched on, consistent and untouched.
     void commit() {
         if (dev_dirty || devs.empty() || !devs[0]->img[devs[0]->cur].written) maybe_relayout();
+        if (targets_dirty && !devs.empty()) rank_targets();
         if (devs.empty()) {
             ++epoch;
             dev_dirty = false;
@@ -1394,6 +1619,14 @@ struct tm_engine {
             upload_table(d, g, g.d_edges, cold.slots, cold.dirty, prev_cold_dirty);
             upload_table(d, g, g.d_hedges, hot.slots, hot.dirty, prev_hot_dirty);
             upload_table(d, g, g.d_dict, dict, dict_dirty, prev_dict_dirty);
+            upload_table(d, g, g.d_rslots, rt_slots, t_slots.cur, t_slots.prev);
+            upload_table(d, g, g.d_rarena, rt_arena, t_rarena.cur, t_rarena.prev);
+            upload_table(d, g, g.d_rdest, rt_dest, t_rdest.cur, t_rdest.prev);
+            upload_table(d, g, g.d_fr_meta, fr_meta, t_fr_meta.cur, t_fr_meta.prev);
+            upload_table(d, g, g.d_rank_src, rank_src, t_rank_src.cur, t_rank_src.prev);
+            upload_table(d, g, g.d_dt, dt, t_dt.cur, t_dt.prev);
+            upload_table(d, g, g.d_rank_tg, rank_tg, t_rank_tg.cur, t_rank_tg.prev);
+            flush_stage(d);
             // append-only arrays: upload the new tail (or all after a realloc)
             {
                 const bool re = g.d_arena.ensure_async(std::max<size_t>(word_arena.size(), 8) + 16, d.stream);
@@ -1420,11 +1653,25 @@ struct tm_engine {
         }
         // this commit's dirty pages become the "previous" set the other image
         // still needs at the next commit
-        for (auto pr : {std::make_pair(&node_dirty, &prev_node_dirty), std::make_pair(&cold.dirty, &prev_cold_dirty),
-                        std::make_pair(&hot.dirty, &prev_hot_dirty), std::make_pair(&dict_dirty, &prev_dict_dirty)}) {
-            *pr.second = *pr.first;
-            pr.first->clear();
+        struct Rot {
+            Dirty *cur, *prev;
+            size_t elems;
+        };
+        for (const Rot& r : {Rot{&node_dirty, &prev_node_dirty, nodes.size()},
+                             Rot{&cold.dirty, &prev_cold_dirty, cold.slots.size()},
+                             Rot{&hot.dirty, &prev_hot_dirty, hot.slots.size()},
+                             Rot{&dict_dirty, &prev_dict_dirty, dict.size()}}) {
+            *r.prev = *r.cur;
+            r.cur->clear();
+            r.cur->limit = std::max<size_t>(4096, r.elems / 16);
         }
+        t_slots.rotate(rt_slots.size());
+        t_rarena.rotate(rt_arena.size());
+        t_rdest.rotate(rt_dest.size());
+        t_fr_meta.rotate(fr_meta.size());
+        t_rank_src.rotate(rank_src.size());
+        t_dt.rotate(dt.size());
+        t_rank_tg.rotate(rank_tg.size());
         dev_dirty = false;
         ++epoch;
     }
@@ -1550,18 +1797,6 @@ struct tm_engine {
     }
     // emqx_router:match_routes/1 over a device batch (stream-ordered except
     // for one read of the match total that sizes the ids workspace)
-    void ensure_route_image() {
-        if (routes_dirty) {
-            if (route_bag.empty()) {
-                route_image = false;
-                routes_dirty = false;
-                agg_keys.clear();
-                aggre_dirty = true;
-            } else {
-                build_route_image();
-            }
-        }
-    }
     // the ids of replica d's last batch again, into a larger output: only
     // tm_copy_out runs (stage rows, counts and offsets are still in its slot)
     void recopy(DevState& d, uint32_t* ids, uint64_t* keys, uint64_t cap, hipStream_t st) {
@@ -1604,11 +1839,11 @@ struct tm_engine {
     void emit_routes(DevState& d, const uint8_t* bytes, const uint64_t* off, uint32_t n, uint32_t* counts,
                      uint64_t* out_off, uint32_t* src, uint32_t* dest, uint64_t cap, uint64_t* total, hipStream_t st,
                      uint64_t* out_key = nullptr) {
-        d.w_rexact.ensure((size_t)n * 8 + 8);
+        d.w_rexact.ensure((size_t)n * 16 + 16);
         d.w_rscan.ensure(scan_tmp_elems(n) * 8 + 8);
         const AggreView av_tmp = aggre_view(d);
         HIPCHK(launch_routes(route_view(d), bytes, off, n, d.w_rcounts.as<uint32_t>(), d.w_roff.as<uint64_t>(),
-                             d.w_rids.as<uint32_t>(), d.w_rexact.as<uint2>(), counts, out_off, src, dest, cap, total,
+                             d.w_rids.as<uint32_t>(), d.w_rexact.as<uint4>(), counts, out_off, src, dest, cap, total,
                              d.w_rscan.as<uint64_t>(), st, out_key ? &av_tmp : nullptr, out_key));
     }
     void run_routes(DevState& d, const uint8_t* bytes, const uint64_t* off, uint32_t n, uint64_t nbytes,
@@ -1663,12 +1898,6 @@ struct tm_engine {
         deliveries_routes(d, bytes, off, n, nbytes, out_off, total, st, rcap);
         aggre_out(d, n, out_off, rcap, counts, to, target, cap, st);
         d.rw_release(st);
-    }
-
-    // route / aggre images must be current before any replica's route batch
-    void prepare_routes(bool deliveries) {
-        ensure_route_image();
-        if (deliveries && aggre_dirty) build_aggre_image();
     }
 
     void finish_batch(uint32_t n) {
@@ -1861,6 +2090,23 @@ int guarded(tm_engine* e, F&& f) {
     }
 }
 
+// a batch of deltas applied in chunks, the engine lock taken per chunk: each
+// delta is its own transaction in the reference (mnesia, per route), so a
+// batch need not be atomic, and a match launched meanwhile waits for one
+// chunk at most instead of the whole batch
+constexpr uint32_t DELTA_CHUNK = 1024;
+template <class F>
+int chunked(tm_engine* e, uint32_t n, F&& one) {
+    for (uint32_t c = 0; c < n; c += DELTA_CHUNK) {
+        const int rc = guarded(e, [&] {
+            for (uint32_t i = c; i < std::min(n, c + DELTA_CHUNK); ++i) one(i);
+            return TM_OK;
+        });
+        if (rc != TM_OK) return rc;
+    }
+    return guarded(e, [] { return TM_OK; });
+}
+
 // emqx_topic:words/1 over a byte string, into (start, len) pairs
 inline void split_levels(const uint8_t* p, uint32_t len, std::vector<std::pair<uint32_t, uint32_t>>& out) {
     out.clear();
@@ -1972,12 +2218,9 @@ int tm_insert(tm_engine* e, const uint8_t* filter, uint32_t len) {
 
 int tm_insert_batch(tm_engine* e, const uint8_t* bytes, const uint64_t* off, uint32_t n) {
     if (n && (!bytes || !off)) return TM_EINVAL;
-    return guarded(e, [&] {
-        for (uint32_t i = 0; i < n; ++i) {
-            if (off[i + 1] < off[i] || off[i + 1] - off[i] > 0xFFFFFFFFull) throw ArgError("bad offsets");
-            e->insert(bytes + off[i], (uint32_t)(off[i + 1] - off[i]));
-        }
-        return TM_OK;
+    return chunked(e, n, [&](uint32_t i) {
+        if (off[i + 1] < off[i] || off[i + 1] - off[i] > 0xFFFFFFFFull) throw ArgError("bad offsets");
+        e->insert(bytes + off[i], (uint32_t)(off[i + 1] - off[i]));
     });
 }
 
@@ -2030,12 +2273,9 @@ int tm_insert_batch_shard(tm_engine* e, const uint8_t* bytes, const uint64_t* of
 
 int tm_delete_batch(tm_engine* e, const uint8_t* bytes, const uint64_t* off, uint32_t n) {
     if (n && (!bytes || !off)) return TM_EINVAL;
-    return guarded(e, [&] {
-        for (uint32_t i = 0; i < n; ++i) {
-            if (off[i + 1] < off[i] || off[i + 1] - off[i] > 0xFFFFFFFFull) throw ArgError("bad offsets");
-            e->remove(bytes + off[i], (uint32_t)(off[i + 1] - off[i]));
-        }
-        return TM_OK;
+    return chunked(e, n, [&](uint32_t i) {
+        if (off[i + 1] < off[i] || off[i + 1] - off[i] > 0xFFFFFFFFull) throw ArgError("bad offsets");
+        e->remove(bytes + off[i], (uint32_t)(off[i + 1] - off[i]));
     });
 }
 
@@ -2150,7 +2390,6 @@ int host_batch(tm_engine* e, BatchKind kind, const uint8_t* topic_bytes, const u
         return TM_OK;
     }
     e->commit();
-    if (kind != K_MATCH) e->prepare_routes(kind == K_DELIVERIES);
     if (out_alloc) out_cap = UINT64_MAX;   // sized below at the exact total
     const size_t R = std::min<size_t>(e->devs.size(), n);
     const uint32_t planes = kind == K_MATCH ? 1u : 2u;
@@ -2306,15 +2545,12 @@ int tm_route_add(tm_engine* e, const uint8_t* topic, uint32_t tlen, const uint8_
 int tm_route_add_batch(tm_engine* e, const uint8_t* topics, const uint64_t* topic_off, const uint8_t* dests,
                        const uint64_t* dest_off, uint32_t n) {
     if (n && (!topics || !topic_off || !dests || !dest_off)) return TM_EINVAL;
-    return guarded(e, [&] {
-        for (uint32_t i = 0; i < n; ++i) {
-            if (topic_off[i + 1] < topic_off[i] || topic_off[i + 1] - topic_off[i] > 0xFFFFFFFFull ||
-                dest_off[i + 1] < dest_off[i] || dest_off[i + 1] - dest_off[i] > 0xFFFFFFFFull)
-                throw ArgError("bad offsets");
-            e->route_add(topics + topic_off[i], (uint32_t)(topic_off[i + 1] - topic_off[i]), dests + dest_off[i],
-                         (uint32_t)(dest_off[i + 1] - dest_off[i]));
-        }
-        return TM_OK;
+    return chunked(e, n, [&](uint32_t i) {
+        if (topic_off[i + 1] < topic_off[i] || topic_off[i + 1] - topic_off[i] > 0xFFFFFFFFull ||
+            dest_off[i + 1] < dest_off[i] || dest_off[i + 1] - dest_off[i] > 0xFFFFFFFFull)
+            throw ArgError("bad offsets");
+        e->route_add(topics + topic_off[i], (uint32_t)(topic_off[i + 1] - topic_off[i]), dests + dest_off[i],
+                     (uint32_t)(dest_off[i + 1] - dest_off[i]));
     });
 }
 
@@ -2323,6 +2559,18 @@ int tm_route_del(tm_engine* e, const uint8_t* topic, uint32_t tlen, const uint8_
     return guarded(e, [&] {
         e->route_del(topic, tlen, dest, dlen);
         return TM_OK;
+    });
+}
+
+int tm_route_del_batch(tm_engine* e, const uint8_t* topics, const uint64_t* topic_off, const uint8_t* dests,
+                       const uint64_t* dest_off, uint32_t n) {
+    if (n && (!topics || !topic_off || !dests || !dest_off)) return TM_EINVAL;
+    return chunked(e, n, [&](uint32_t i) {
+        if (topic_off[i + 1] < topic_off[i] || topic_off[i + 1] - topic_off[i] > 0xFFFFFFFFull ||
+            dest_off[i + 1] < dest_off[i] || dest_off[i + 1] - dest_off[i] > 0xFFFFFFFFull)
+            throw ArgError("bad offsets");
+        e->route_del(topics + topic_off[i], (uint32_t)(topic_off[i + 1] - topic_off[i]), dests + dest_off[i],
+                     (uint32_t)(dest_off[i + 1] - dest_off[i]));
     });
 }
 
@@ -2362,7 +2610,6 @@ int tm_match_routes_batch_device(tm_engine* e, const uint8_t* d_bytes, const uin
             return TM_EDEVICE;
         }
         e->commit();
-        e->prepare_routes(false);
         DevState& d = *e->replica_for(d_off);
         tm_engine::Guard g(d.device);
         hipStream_t st = hip_stream ? (hipStream_t)hip_stream : d.stream;
@@ -2396,7 +2643,8 @@ int tm_dest_target(tm_engine* e, const uint8_t* dest, uint32_t dlen, uint32_t ki
         const uint32_t t = e->intern_target(kind, key, klen);
         if (e->dest_target[d] != t) {
             e->dest_target[d] = t;
-            e->aggre_dirty = true;
+            e->targets_dirty = true;
+            e->dev_dirty = true;
         }
         if (target_out) *target_out = t;
         return TM_OK;
@@ -2423,7 +2671,6 @@ int tm_match_deliveries_batch_device(tm_engine* e, const uint8_t* d_bytes, const
             return TM_EDEVICE;
         }
         e->commit();
-        e->prepare_routes(true);
         DevState& d = *e->replica_for(d_off);
         tm_engine::Guard g(d.device);
         hipStream_t st = hip_stream ? (hipStream_t)hip_stream : d.stream;
@@ -2566,6 +2813,67 @@ extern "C" int tm_debug_hist(tm_engine* e, uint64_t* out, int n) {
     });
 }
 
+// diagnostics (not part of include/topicmatch.h): the in-place route image
+// against the route bags it mirrors -- every topic found in the exact table
+// by the kernel's probe, its segment equal to its bag, its filter entry, the
+// labels strictly increasing in topic order, rank_src -- TM_OK or TM_EINVAL
+// with the first inconsistency in tm_last_error
+extern "C" int tm_debug_check_routes(tm_engine* e) {
+    return guarded(e, [&]() -> int {
+        auto fail = [&](const std::string& what) -> int { throw ArgError("route image: " + what); };
+        size_t used = 0;
+        for (size_t s = 0; s < e->rt_slots.size(); ++s)
+            if (e->rt_slots[s].hash) {
+                ++used;
+                if (!e->rt_slot_rec[s] || e->rt_slot_rec[s]->slot != s) return fail("slot owner");
+            }
+        if (used != e->rt_used || used != e->route_bag.size()) return fail("slot count");
+        size_t total = 0;
+        for (auto& kv : e->route_bag) {
+            const tm_engine::RouteRec& r = kv.second;
+            const uint8_t* t = reinterpret_cast<const uint8_t*>(kv.first.data());
+            const uint32_t len = (uint32_t)kv.first.size();
+            total += r.dests.size();
+            if (r.key != &kv.first || r.dests.empty()) return fail("record of " + kv.first);
+            // the probe the kernel runs (routes.hip exact_lookup)
+            const uint64_t h = word_hash(t, len);
+            const size_t mask = e->rt_slots.size() - 1;
+            size_t s = h & mask;
+            while (e->rt_slots[s].hash && !(e->rt_slots[s].hash == h && e->rt_slots[s].len == len &&
+                                             std::memcmp(&e->rt_arena[e->rt_slots[s].arena / 8], t, len) == 0))
+                s = (s + 1) & mask;
+            if (!e->rt_slots[s].hash || s != r.slot) return fail("probe of " + kv.first);
+            const ExactSlot& x = e->rt_slots[s];
+            if (x.count != r.dests.size() || x.dest_off != r.off || x.rank != r.label) return fail("slot of " + kv.first);
+            if (len % 8 && (e->rt_arena[x.arena / 8 + len / 8] >> (8 * (len % 8))) != 0) return fail("arena padding");
+            if (r.cap < r.dests.size() || (uint64_t)r.off + r.cap > e->rt_dest.size() ||
+                !std::equal(r.dests.begin(), r.dests.end(), e->rt_dest.begin() + r.off))
+                return fail("segment of " + kv.first);
+            const bool wild = tm_topic_wildcard(t, len);
+            const uint32_t fid = wild ? e->filter_of(t, len) : FILTER_NONE;
+            if (r.fid != fid) return fail("filter link of " + kv.first);
+            if (fid != FILTER_NONE) {
+                const uint4 m = e->fr_meta[fid];
+                if (m.x != r.off || m.y != r.dests.size() || m.z != r.label || e->fr_rec[fid] != &r)
+                    return fail("fr_meta of " + kv.first);
+            }
+            if (r.label >= e->rank_src.size() || e->rank_src[r.label] != (fid != FILTER_NONE ? fid : TM_ROUTE_TOPIC_ID))
+                return fail("rank_src of " + kv.first);
+            if ((r.index != nullptr) != (r.dests.size() >= tm_engine::BAG_INDEX_MIN)) return fail("bag index");
+        }
+        if (total != e->route_total) return fail("route total");
+        for (size_t f = 0; f < e->fr_meta.size(); ++f)
+            if (e->fr_meta[f].y && (!e->fr_rec[f] || e->fr_rec[f]->fid != f)) return fail("stale fr_meta");
+        if (e->rt_order.size() != e->route_bag.size()) return fail("order size");
+        const tm_engine::RouteRec* prev = nullptr;
+        for (const tm_engine::RouteRec* r : e->rt_order) {
+            if (prev && !(prev->label < r->label && *prev->key < *r->key)) return fail("label order at " + *r->key);
+            prev = r;
+        }
+        return TM_OK;
+    });
+}
+
 int tm_set_option(tm_engine* e, const char* name, int64_t value) {
     if (!name) return TM_EINVAL;
     return guarded(e, [&]() -> int {
@@ -2591,6 +2899,11 @@ int tm_set_option(tm_engine* e, const char* name, int64_t value) {
         if (!std::strcmp(name, "layout")) {
             if (value < 0 || value > 2) return TM_EINVAL;
             e->layout_mode = (int)value;
+            return TM_OK;
+        }
+        if (!std::strcmp(name, "route_gc")) {
+            if (value < 0) return TM_EINVAL;
+            e->route_gc_min = (size_t)value;
             return TM_OK;
         }
         if (!std::strcmp(name, "double_buffer")) {

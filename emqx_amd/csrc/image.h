@@ -125,11 +125,13 @@ struct ImageView {
 };
 
 // ---- route image (emqx_route bag, src/emqx_router.erl:52-59, 89-90) --------
-// Routes are (topic, dest) pairs; dests are interned to u32 ids.  The routes
-// of a trie filter are found by its filter id (CSR fr_meta/fr_dest over filter
-// ids, bag insertion order); the routes of a literal topic (get_routes/1 of
-// the publish topic itself) through an exact-topic hash table whose keys are
-// verified byte for byte against the topic arena (8-aligned, zero padded).
+// Routes are (topic, dest) pairs; dests are interned to u32 ids.  Each topic
+// with routes owns a segment of one dest pool (bag insertion order).  The
+// routes of a trie filter are found by its filter id (fr_meta: segment, count,
+// to_rank); the routes of a literal topic (get_routes/1 of the publish topic
+// itself) through an exact-topic hash table whose keys are verified byte for
+// byte against the topic arena (8-aligned, zero padded).  The host patches
+// all of it in place per add / del (engine.cpp, route image maintenance).
 constexpr uint32_t TM_ROUTE_TOPIC_ID = 0xFFFFFFFFu;   // route source = the literal topic
 
 struct alignas(32) ExactSlot {
@@ -137,26 +139,24 @@ struct alignas(32) ExactSlot {
     uint32_t len;          // topic length
     uint32_t count;        // routes of the topic
     uint64_t arena;        // topic bytes in the arena
-    uint32_t dest_off;     // first route's dest in ex_dest[]
-    uint32_t pad;
+    uint32_t dest_off;     // first route's dest in the dest pool
+    uint32_t rank;         // to_rank of the topic (aggre)
 };
 
 struct RouteView {
-    const uint2*     fr_meta;       // n_filters + 1: {dest offset (CSR), to_rank (aggre; 0 until built)}
-    const uint32_t*  fr_dest;
+    const uint4*     fr_meta;       // n_filters: {dest offset, count, to_rank, 0} (count 0: no routes)
     uint32_t         n_filters;
-    const ExactSlot* ex_slots;      // null: no routes
+    const ExactSlot* ex_slots;      // power-of-two table, hash 0 = empty
     uint64_t         ex_slot_mask;
     const uint8_t*   ex_arena;
-    const uint32_t*  ex_dest;
+    const uint32_t*  dest;          // the dest pool
 };
 
-// emqx_broker:aggre/1 tables (aggre.hip): sort ranks of every topic with
-// routes (Erlang binary order) and, per dest id, its aggre target
-// (a filter's to_rank rides in RouteView::fr_meta, in the line the route
-// kernels fetch anyway)
+// emqx_broker:aggre/1 tables (aggre.hip): per dest id its aggre target.  A
+// topic's to_rank (an order label: Erlang binary order of the topics with
+// routes) rides in its fr_meta entry and its exact slot, which the route
+// kernels fetch anyway.
 struct AggreView {
-    const uint32_t* ex_rank;        // exact-table dest_off -> to_rank of that topic
     const uint2*    dt;             // dest id -> {target rank, target id | group << 31}
     const uint32_t* rank_src;       // to_rank -> route source of that To (filter id or TM_ROUTE_TOPIC_ID)
     const uint32_t* rank_tg;        // target rank -> target id

@@ -48,6 +48,8 @@ hipError_t launch_copy(const ImageView& im, const uint8_t* bytes, const uint64_t
 size_t scan_tmp_elems(uint32_t n);
 // split image (option "split"): n 32 B node records -> inner[n], leaf[n] 16 B halves
 hipError_t launch_split_nodes(const void* nodes, uint64_t n, void* inner, void* leaf, hipStream_t st);
+// element scatter of a commit packet [idx u32 x n][values: words u32 x n]
+hipError_t launch_scatter(void* table, const uint32_t* pkt, uint64_t n, uint32_t words, hipStream_t st);
 // exclusive scan of n u32 counts -> out_off[n+1] (u64), *total (tmp: scan_tmp_elems(n))
 hipError_t launch_scan(const uint32_t* counts, uint32_t n, uint64_t* out_off, uint64_t* total, uint64_t* tmp,
                        hipStream_t st);
@@ -58,7 +60,7 @@ hipError_t launch_scan(const uint32_t* counts, uint32_t n, uint64_t* out_off, ui
 // == 0: counts and offsets only.  av != null: also out_key[route] =
 // to_rank << 32 | target rank (the aggre sort key).
 hipError_t launch_routes(const RouteView& rv, const uint8_t* bytes, const uint64_t* off, uint32_t n,
-                         const uint32_t* counts, const uint64_t* ids_off, const uint32_t* ids, uint2* exact,
+                         const uint32_t* counts, const uint64_t* ids_off, const uint32_t* ids, uint4* exact,
                          uint32_t* rcount, uint64_t* out_off, uint32_t* out_src, uint32_t* out_dest,
                          uint64_t out_cap, uint64_t* total, uint64_t* scan_tmp, hipStream_t st,
                          const AggreView* av = nullptr, uint64_t* out_key = nullptr);

@@ -965,6 +965,27 @@ hipError_t launch_split_nodes(const void* nodes, uint64_t n, void* inner, void* 
     return hipGetLastError();
 }
 
+// commit: the elements a host table changed since an image last saw it, as
+// one packet [idx u32 x n][values: words u32 x n], written into the image's
+// copy of the table (later duplicates of an index carry the same value)
+__global__ void __launch_bounds__(BLOCK)
+tm_scatter(uint32_t* __restrict__ table, const uint32_t* __restrict__ pkt, uint64_t n, uint32_t words) {
+    const uint32_t* vals = pkt + n;
+    const uint64_t total = n * words;
+    for (uint64_t t = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; t < total; t += (uint64_t)gridDim.x * BLOCK) {
+        const uint64_t i = t / words;
+        table[(uint64_t)pkt[i] * words + (t - i * words)] = vals[t];
+    }
+}
+
+hipError_t launch_scatter(void* table, const uint32_t* pkt, uint64_t n, uint32_t words, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    const uint64_t blocks = (n * words + BLOCK - 1) / BLOCK;
+    hipLaunchKernelGGL(tm_scatter, dim3((uint32_t)(blocks < 16384 ? blocks : 16384)), dim3(BLOCK), 0, st,
+                       (uint32_t*)table, pkt, n, words);
+    return hipGetLastError();
+}
+
 size_t scan_tmp_elems(uint32_t n) { return div_up(n ? n : 1, SCAN_TILE); }
 
 hipError_t launch_scan(const uint32_t* counts, uint32_t n, uint64_t* out_off, uint64_t* total, uint64_t* tmp,

@@ -228,6 +228,16 @@ class Engine:
     def route_del(self, topic: bytes, dest: bytes):
         return self._check(self.lib.tm_route_del(self.h, topic, len(topic), dest, len(dest)), "tm_route_del")
 
+    def route_del_many(self, tbuf, toff, dbuf, doff):
+        """route i = (topic i of (tbuf, toff), dest i of (dbuf, doff)), removed in order"""
+        n = len(toff) - 1
+        tbuf = np.ascontiguousarray(tbuf, dtype=np.uint8)
+        toff = np.ascontiguousarray(toff, dtype=np.uint64)
+        dbuf = np.ascontiguousarray(dbuf, dtype=np.uint8)
+        doff = np.ascontiguousarray(doff, dtype=np.uint64)
+        return self._check(self.lib.tm_route_del_batch(self.h, _ptr(tbuf), _ptr(toff), _ptr(dbuf), _ptr(doff), n),
+                           "tm_route_del_batch")
+
     def get_routes(self, topic: bytes):
         """dest ids of topic's routes, insertion order (get_routes/1)"""
         n = ctypes.c_uint32()
@@ -290,6 +300,11 @@ class Engine:
 
     # -- emqx_broker:aggre/1 (aggre.hip) --------------------------------------
     TARGET_NODE, TARGET_GROUP = 0, 1
+
+    def debug_check_routes(self):
+        """host-side consistency check of the in-place route image (diagnostic,
+        tm_debug_check_routes): raises TopicMatchError naming the first defect"""
+        return self._check(self.lib.tm_debug_check_routes(self.h), "tm_debug_check_routes")
 
     def dest_target(self, dest: bytes, kind: int, key: bytes) -> int:
         """declare dest's aggre target: a node atom (TARGET_NODE, key = its

@@ -300,6 +300,10 @@ int tm_route_add_batch(tm_engine* e, const uint8_t* topics, const uint64_t* topi
  * broker and stays with the caller.) */
 int tm_route_del(tm_engine* e, const uint8_t* topic, uint32_t tlen, const uint8_t* dest, uint32_t dlen);
 
+/* Bulk tm_route_del, laid out as tm_route_add_batch, applied in order. */
+int tm_route_del_batch(tm_engine* e, const uint8_t* topics, const uint64_t* topic_off, const uint8_t* dests,
+                       const uint64_t* dest_off, uint32_t n);
+
 /* get_routes/1 — :89-90: the dest ids of topic's routes in insertion order;
  * *out_n = their number (TM_ENOSPC when it exceeds cap). */
 int tm_get_routes(tm_engine* e, const uint8_t* topic, uint32_t tlen, uint32_t* out_dest, uint32_t cap,
