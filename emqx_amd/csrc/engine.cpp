@@ -16,6 +16,8 @@
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <chrono>
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -235,6 +237,12 @@ struct Image {
     bool split_stale = true, written = false;
     uint64_t epoch = 0;
     std::vector<hipEvent_t> uses;
+    int pins = 0;   // batches between pin and unpin on it (their launches not all recorded in uses yet)
+    // the views kernels get, captured when the image was written: a batch
+    // reads these, never the host tables, which change under it
+    ImageView iv{};
+    RouteView rv{};
+    AggreView av{};
     void release() {
         for (DevBuf* b : {&d_nodes, &d_edges, &d_hedges, &d_dict, &d_arena, &d_woff, &d_inner, &d_leaf, &d_rslots,
                           &d_rarena, &d_rdest, &d_fr_meta, &d_rank_src, &d_dt, &d_rank_tg})
@@ -251,14 +259,33 @@ struct Image {
 struct DevState {
     int device = -1;
     hipStream_t stream = nullptr;
+    hipStream_t ustream = nullptr;   // commits: image uploads and scatters (never behind a batch on `stream`)
     // trie image + dictionary, two epochs (Image)
     Image img[2];
-    int cur = 0;                          // the image batches launch on
+    int cur = 0;                          // the image new batches pin (switched by commit, under the engine lock)
+    int bimg = 0;                         // the image the running batch pinned
     std::vector<hipEvent_t> ev_spare;     // recycled use events
+    // Locks: bmu = one batch at a time on this replica's workspaces, held for
+    // the whole call; the engine lock is taken inside it only to commit and
+    // pin (so host deltas run while the GPU works); umu guards pins, uses and
+    // ev_spare (a leaf lock)
+    std::mutex bmu, umu;
+    std::condition_variable ucv;
     Image& live() { return img[cur]; }
-    // one use of the live image by a batch on st (pruned as uses complete)
+    void pin() {
+        std::lock_guard<std::mutex> lk(umu);
+        bimg = cur;
+        ++img[bimg].pins;
+    }
+    void unpin() {
+        std::lock_guard<std::mutex> lk(umu);
+        --img[bimg].pins;
+        ucv.notify_all();
+    }
+    // one use of the pinned image by a batch on st (pruned as uses complete)
     void note_use(hipStream_t st) {
-        Image& im = img[cur];
+        std::lock_guard<std::mutex> lk(umu);
+        Image& im = img[bimg];
         if (im.uses.size() >= 64) {   // drop the completed ones
             size_t k = 0;
             for (hipEvent_t ev : im.uses)
@@ -276,13 +303,18 @@ struct DevState {
         HIPCHK(hipEventRecord(ev, st));
         im.uses.push_back(ev);
     }
-    // host: every batch that read image i has finished
+    // host: every batch that read image i has finished (none still pinned,
+    // every recorded use complete)
     void drain_image(int i) {
-        for (hipEvent_t ev : img[i].uses) {
-            HIPCHK(hipEventSynchronize(ev));
-            ev_spare.push_back(ev);
+        std::vector<hipEvent_t> evs;
+        {
+            std::unique_lock<std::mutex> lk(umu);
+            ucv.wait(lk, [&] { return img[i].pins == 0; });
+            evs.swap(img[i].uses);
         }
-        img[i].uses.clear();
+        for (hipEvent_t ev : evs) HIPCHK(hipEventSynchronize(ev));
+        std::lock_guard<std::mutex> lk(umu);
+        ev_spare.insert(ev_spare.end(), evs.begin(), evs.end());
     }
     // commit packets: the changed elements of every table, one H2D copy,
     // then a scatter per table into the back image
@@ -324,6 +356,7 @@ struct DevState {
     void release() {
         (void)hipSetDevice(device);
         if (stream) (void)hipStreamSynchronize(stream);
+        if (ustream) (void)hipStreamSynchronize(ustream);
         if (rw_done) (void)hipEventDestroy(rw_done);
         img[0].release();
         img[1].release();
@@ -346,7 +379,8 @@ struct DevState {
                 (void)hipEventDestroy(k.b);
             }
         if (stream) (void)hipStreamDestroy(stream);
-        stream = nullptr;
+        if (ustream) (void)hipStreamDestroy(ustream);
+        stream = ustream = nullptr;
     }
 };
 
@@ -354,6 +388,7 @@ struct DevState {
 
 struct tm_engine {
     std::recursive_mutex mu;
+    std::atomic<int> lock_waiters{0};   // API calls blocked on mu (a chunked delta batch yields to them)
     int device = -1;                  // first replica's HIP ordinal (-1: host-only engine)
     std::vector<std::unique_ptr<DevState>> devs;   // one replica per GPU (tm_open_devices)
     std::string last_error;
@@ -422,6 +457,27 @@ struct tm_engine {
     std::unordered_map<std::string, uint32_t> dest_index;   // dest bytes -> dest id
     std::vector<std::string> dest_names;
     static constexpr uint32_t SLOT_NONE = 0xFFFFFFFFu;
+    // to_rank labels: an order-maintenance labelling of the topics (list
+    // labelling with density thresholds per window), so a new topic costs
+    // O(log^2 n) amortised relabels, not a re-rank of every topic.  The
+    // ordered index keeps each topic's first 32 bytes (big-endian u64s, zero
+    // padded: their numeric order is the bytes' order whenever they differ)
+    // and its label in the tree node, so a search reads a full topic only on
+    // a 32-byte tie (16 bytes tied ~6 topics each at C3, 32 almost none).
+    struct RouteRec;
+    struct OrdKey {
+        uint64_t p[4];
+        RouteRec* r;
+        mutable uint32_t label;   // == r->label
+    };
+    struct OrdLess {
+        bool operator()(const OrdKey& a, const OrdKey& b) const {
+            for (int i = 0; i < 4; ++i)
+                if (a.p[i] != b.p[i]) return a.p[i] < b.p[i];
+            return a.r != b.r && *a.r->key < *b.r->key;
+        }
+    };
+    using OrdSet = std::set<OrdKey, OrdLess>;
     // one topic with routes, and where the route image holds it
     struct RouteRec {
         std::vector<uint32_t> dests;          // the bag, insertion order
@@ -435,6 +491,7 @@ struct tm_engine {
         uint32_t label = 0;                   // to_rank: order label, Erlang binary order of the topics
         uint32_t off = 0, cap = 0;            // dest segment in rt_dest
         uint64_t arena = 0, words = 0;        // topic bytes in rt_arena (u64 words)
+        OrdSet::iterator ord;                 // its entry in rt_order
         bool has(uint32_t d) const {
             return index ? index->count(d) != 0 : std::find(dests.begin(), dests.end(), d) != dests.end();
         }
@@ -462,13 +519,7 @@ struct tm_engine {
     size_t route_gc_min = 1u << 20;   // option "route_gc": garbage entries before a compaction is considered
     std::vector<uint4> fr_meta;
     std::vector<RouteRec*> fr_rec;   // filter id -> linked topic
-    // to_rank labels: an order-maintenance labelling of the topics (list
-    // labelling with density thresholds per window), so a new topic costs
-    // O(log^2 n) amortised relabels, not a re-rank of every topic
-    struct RecLess {
-        bool operator()(const RouteRec* a, const RouteRec* b) const { return *a->key < *b->key; }
-    };
-    std::set<RouteRec*, RecLess> rt_order;
+    OrdSet rt_order;
     uint32_t label_bits = 16;        // label universe 2^label_bits
     std::vector<uint32_t> rank_src = std::vector<uint32_t>(1u << 16, TM_ROUTE_TOPIC_ID);
     Track t_slots, t_rarena, t_rdest, t_fr_meta, t_rank_src, t_dt, t_rank_tg;
@@ -1153,21 +1204,31 @@ struct tm_engine {
     }
 
     // ---- to_rank labels (order maintenance) ----
-    void set_label(RouteRec* r, uint32_t label) {
-        r->label = label;
-        rt_sync(*r);
+    static OrdKey ord_key(RouteRec* r) {
+        uint8_t b[32] = {0};
+        std::memcpy(b, r->key->data(), std::min<size_t>(32, r->key->size()));
+        OrdKey k{{0, 0, 0, 0}, r, 0};
+        for (int w = 0; w < 4; ++w)
+            for (int i = 0; i < 8; ++i) k.p[w] = k.p[w] << 8 | b[8 * w + i];
+        return k;
+    }
+    void set_label(const OrdKey& k, uint32_t label) {
+        k.label = label;
+        k.r->label = label;
+        rt_sync(*k.r);
     }
     void order_insert(RouteRec* r) {
-        auto it = rt_order.insert(r).first;
+        auto it = rt_order.insert(ord_key(r)).first;
+        r->ord = it;
         if ((uint64_t)rt_order.size() * 4 > (1ull << label_bits)) {   // keep the universe >= 4n
             relabel_all(label_bits + 1);
             return;
         }
         const int64_t U = int64_t(1) << label_bits;
-        const int64_t lo = it == rt_order.begin() ? -1 : (int64_t)(*std::prev(it))->label;
-        const int64_t hi = std::next(it) == rt_order.end() ? U : (int64_t)(*std::next(it))->label;
+        const int64_t lo = it == rt_order.begin() ? -1 : (int64_t)std::prev(it)->label;
+        const int64_t hi = std::next(it) == rt_order.end() ? U : (int64_t)std::next(it)->label;
         if (hi - lo >= 2) {
-            set_label(r, (uint32_t)(lo + (hi - lo) / 2));
+            set_label(*it, (uint32_t)(lo + (hi - lo) / 2));
             return;
         }
         // no gap: the smallest aligned window around the neighbours whose
@@ -1178,11 +1239,11 @@ struct tm_engine {
         int64_t count = 1;
         for (uint32_t k = 1; k <= label_bits; ++k) {
             const int64_t L = (anchor >> k) << k, R = L + (int64_t(1) << k);
-            while (left != rt_order.begin() && (int64_t)(*std::prev(left))->label >= L) {
+            while (left != rt_order.begin() && (int64_t)std::prev(left)->label >= L) {
                 --left;
                 ++count;
             }
-            while (right != rt_order.end() && (int64_t)(*right)->label < R) {
+            while (right != rt_order.end() && (int64_t)right->label < R) {
                 ++right;
                 ++count;
             }
@@ -1195,8 +1256,7 @@ struct tm_engine {
         relabel_all(label_bits + 1);
     }
     // members [a, b) (count of them) get labels evenly spaced in [L, R)
-    void spread(std::set<RouteRec*, RecLess>::iterator a, std::set<RouteRec*, RecLess>::iterator b, int64_t count,
-                int64_t L, int64_t R) {
+    void spread(OrdSet::iterator a, OrdSet::iterator b, int64_t count, int64_t L, int64_t R) {
         const double step = (double)(R - L) / (double)count;
         int64_t i = 0;
         for (auto x = a; x != b; ++x, ++i) set_label(*x, (uint32_t)(L + (int64_t)(step * (double)i + step / 2)));
@@ -1209,7 +1269,7 @@ struct tm_engine {
         t_rank_src.cur.all = true;
         if (!rt_order.empty()) spread(rt_order.begin(), rt_order.end(), (int64_t)rt_order.size(), 0, int64_t(1) << bits);
     }
-    void order_erase(RouteRec* r) { rt_order.erase(r); }   // its label is simply free again
+    void order_erase(RouteRec* r) { rt_order.erase(r->ord); }   // its label is simply free again
 
     // ------------------------------------------------------------------
     // emqx_broker:aggre/1 (src/emqx_broker.erl:194-206) targets: per dest its
@@ -1249,16 +1309,14 @@ struct tm_engine {
         t_rank_tg.cur.all = true;
         targets_dirty = false;
     }
-    AggreView aggre_view(const DevState& d) const {
-        const Image& g = d.img[d.cur];
+    AggreView make_aggre_view(const Image& g) const {
         AggreView av;
         av.dt = g.d_dt.as<const uint2>();
         av.rank_src = g.d_rank_src.as<const uint32_t>();
         av.rank_tg = g.d_rank_tg.as<const uint32_t>();
         return av;
     }
-    RouteView route_view(const DevState& d) const {
-        const Image& g = d.img[d.cur];
+    RouteView make_route_view(const Image& g) const {
         RouteView rv;
         rv.fr_meta = g.d_fr_meta.as<const uint4>();
         rv.n_filters = (uint32_t)fr_meta.size();
@@ -1499,10 +1557,17 @@ struct tm_engine {
         }
     };
 
-    // the live image of replica d (its sizes are the host tables' at the
-    // last commit, and every match commits first)
-    ImageView view(const DevState& d) const {
-        const Image& g = d.img[d.cur];
+    // what a batch's kernels read: the views of the image it pinned
+    static const ImageView& view(const DevState& d) { return d.img[d.bimg].iv; }
+    static const RouteView& route_view(const DevState& d) { return d.img[d.bimg].rv; }
+    static const AggreView& aggre_view(const DevState& d) { return d.img[d.bimg].av; }
+    void capture_views(Image& g) const {
+        g.iv = make_view(g);
+        g.rv = make_route_view(g);
+        g.av = make_aggre_view(g);
+    }
+    // the views of image g, from the host tables it was just written from
+    ImageView make_view(const Image& g) const {
         ImageView im;
         if (split_halves && g.d_inner.p && !g.split_stale) {
             im.inner = g.d_inner.as<const uint8_t>();
@@ -1535,14 +1600,14 @@ struct tm_engine {
     void upload_table(DevState& d, Image& g, DevBuf& buf, const std::vector<T>& host, const Dirty& dirty,
                       const Dirty& prev) {
         static_assert(sizeof(T) % 4 == 0, "tables are scattered in 32-bit words");
-        const bool re = buf.ensure_async(std::max<size_t>(host.size(), 1) * sizeof(T), d.stream);
+        const bool re = buf.ensure_async(std::max<size_t>(host.size(), 1) * sizeof(T), d.ustream);
         // g holds commit g.epoch; this one makes epoch + 1
         const bool two = g.written && g.epoch + 1 == epoch;        // g missed exactly the previous commit
         const bool stale = !g.written || g.epoch + 1 < epoch;      // missed more (double_buffer switched on)
         const size_t n = dirty.idx.size() + (two ? prev.idx.size() : 0);
         if (re || stale || dirty.all || (two && prev.all) || n * (4 + sizeof(T)) * 4 > host.size() * sizeof(T)) {
             if (!host.empty())
-                HIPCHK(hipMemcpyAsync(buf.p, host.data(), host.size() * sizeof(T), hipMemcpyHostToDevice, d.stream));
+                HIPCHK(hipMemcpyAsync(buf.p, host.data(), host.size() * sizeof(T), hipMemcpyHostToDevice, d.ustream));
             return;
         }
         if (n == 0) return;
@@ -1569,11 +1634,11 @@ struct tm_engine {
     // the packed changes of every table: one copy, a scatter per table
     void flush_stage(DevState& d) {
         if (d.stage_ops.empty()) return;
-        d.stage_dev.ensure_async(d.stage_host.size(), d.stream);
-        HIPCHK(hipMemcpyAsync(d.stage_dev.p, d.stage_host.data(), d.stage_host.size(), hipMemcpyHostToDevice, d.stream));
+        d.stage_dev.ensure_async(d.stage_host.size(), d.ustream);
+        HIPCHK(hipMemcpyAsync(d.stage_dev.p, d.stage_host.data(), d.stage_host.size(), hipMemcpyHostToDevice, d.ustream));
         for (const auto& op : d.stage_ops)
             HIPCHK(launch_scatter(op.table, reinterpret_cast<const uint32_t*>(d.stage_dev.as<uint8_t>() + op.off), op.n,
-                                  op.words, d.stream));
+                                  op.words, d.ustream));
         d.stage_ops.clear();
         d.stage_host.clear();
     }
@@ -1604,7 +1669,8 @@ struct tm_engine {
                     Guard gd(dp->device);
                     dp->drain_image(dp->cur);
                     split_image(*dp, g);
-                    HIPCHK(hipStreamSynchronize(dp->stream));
+                    HIPCHK(hipStreamSynchronize(dp->ustream));
+                    capture_views(g);
                 }
             }
             return;
@@ -1629,26 +1695,27 @@ struct tm_engine {
             flush_stage(d);
             // append-only arrays: upload the new tail (or all after a realloc)
             {
-                const bool re = g.d_arena.ensure_async(std::max<size_t>(word_arena.size(), 8) + 16, d.stream);
+                const bool re = g.d_arena.ensure_async(std::max<size_t>(word_arena.size(), 8) + 16, d.ustream);
                 const size_t from = re ? 0 : g.arena_uploaded;
                 if (word_arena.size() > from)
                     HIPCHK(hipMemcpyAsync(g.d_arena.as<uint8_t>() + from, word_arena.data() + from,
-                                          word_arena.size() - from, hipMemcpyHostToDevice, d.stream));
+                                          word_arena.size() - from, hipMemcpyHostToDevice, d.ustream));
                 g.arena_uploaded = word_arena.size();
             }
             {
-                const bool re = g.d_woff.ensure_async(std::max<size_t>(word_off.size(), 1) * 4, d.stream);
+                const bool re = g.d_woff.ensure_async(std::max<size_t>(word_off.size(), 1) * 4, d.ustream);
                 const size_t from = re ? 0 : g.woff_uploaded;
                 if (word_off.size() > from)
                     HIPCHK(hipMemcpyAsync(g.d_woff.as<uint32_t>() + from, word_off.data() + from,
-                                          (word_off.size() - from) * 4, hipMemcpyHostToDevice, d.stream));
+                                          (word_off.size() - from) * 4, hipMemcpyHostToDevice, d.ustream));
                 g.woff_uploaded = word_off.size();
             }
             g.split_stale = true;
             if (split_halves) split_image(d, g);
-            HIPCHK(hipStreamSynchronize(d.stream));   // host tables may change once this returns
+            HIPCHK(hipStreamSynchronize(d.ustream));   // host tables may change once this returns
             g.written = true;
             g.epoch = epoch + 1;
+            capture_views(g);
             d.cur = back;   // live from the next batch on
         }
         // this commit's dirty pages become the "previous" set the other image
@@ -1678,9 +1745,9 @@ struct tm_engine {
 
     // option "split": de-interleave the uploaded records into inner / leaf arrays
     void split_image(DevState& d, Image& g) {
-        g.d_inner.ensure_async(nodes.size() * 16, d.stream);
-        g.d_leaf.ensure_async(nodes.size() * 16, d.stream);
-        HIPCHK(launch_split_nodes(g.d_nodes.p, nodes.size(), g.d_inner.p, g.d_leaf.p, d.stream));
+        g.d_inner.ensure_async(nodes.size() * 16, d.ustream);
+        g.d_leaf.ensure_async(nodes.size() * 16, d.ustream);
+        HIPCHK(launch_split_nodes(g.d_nodes.p, nodes.size(), g.d_inner.p, g.d_leaf.p, d.ustream));
         g.split_stale = false;
     }
 
@@ -2063,45 +2130,116 @@ struct PinnedPool {
 };
 PinnedPool g_pinned;
 
+// the C-ABI's error mapping: exception -> status code and message
 template <class F>
-int guarded(tm_engine* e, F&& f) {
-    if (!e) return TM_EINVAL;
-    std::lock_guard<std::recursive_mutex> lk(e->mu);
+int catching(std::string& err, F&& f) {
     try {
         return f();
     } catch (const ArgError& x) {
-        e->last_error = x.what();
+        err = x.what();
         return TM_EINVAL;
     } catch (const RangeError& x) {
-        e->last_error = x.what();
+        err = x.what();
         return TM_ERANGE;
     } catch (const DevError& x) {
-        e->last_error = x.what();
+        err = x.what();
         return TM_EDEVICE;
     } catch (const std::bad_alloc&) {
-        e->last_error = "out of host memory";
+        err = "out of host memory";
         return TM_ENOMEM;
     } catch (const std::exception& x) {
-        e->last_error = x.what();
+        err = x.what();
         return TM_EDEVICE;
     } catch (...) {
-        e->last_error = "unknown failure";
+        err = "unknown failure";
         return TM_EDEVICE;
     }
+}
+
+template <class F>
+int guarded(tm_engine* e, F&& f, bool counted = true) {
+    if (!e) return TM_EINVAL;
+    if (counted) e->lock_waiters.fetch_add(1, std::memory_order_relaxed);
+    std::lock_guard<std::recursive_mutex> lk(e->mu);
+    if (counted) e->lock_waiters.fetch_sub(1, std::memory_order_relaxed);
+    std::string err;
+    const int rc = catching(err, f);
+    if (!err.empty()) e->last_error = err;
+    return rc;
+}
+
+// A batch on replicas `reps` (ascending): their batch locks for the whole
+// call; the engine lock only to commit and pin each replica's live image
+// (its captured views), so deltas and commits proceed on the host while the
+// batch runs and waits on the GPU; then, after the pins are released, the
+// engine lock again for `post` (stats) or the error text.
+template <class W, class P>
+int batch_call(tm_engine* e, const std::vector<DevState*>& reps, W&& work, P&& post) {
+    if (!e) return TM_EINVAL;
+    std::vector<std::unique_lock<std::mutex>> held;
+    held.reserve(reps.size());
+    for (DevState* d : reps) held.emplace_back(d->bmu);
+    int rc = guarded(e, [&] {
+        e->commit();
+        for (DevState* d : reps) d->pin();
+        return TM_OK;
+    });
+    if (rc != TM_OK) return rc;
+    std::string err;
+    rc = catching(err, work);
+    for (DevState* d : reps) d->unpin();
+    return guarded(e, [&] {
+        if (rc != TM_OK) {
+            e->last_error = err;
+            return rc;
+        }
+        post();
+        return rc;
+    });
+}
+int no_device(tm_engine* e, const char* what) {
+    return guarded(e, [&] {
+        e->last_error = std::string("engine is host-only (no device): ") + what + " runs on the GPU only";
+        return TM_EDEVICE;
+    });
+}
+std::vector<DevState*> all_replicas(tm_engine* e) {
+    std::vector<DevState*> v;
+    for (auto& d : e->devs) v.push_back(d.get());
+    return v;
+}
+// the batch locks of every replica (in order): for the calls that read what
+// batches write (slots, kernel-time events) outside the engine lock
+std::vector<std::unique_lock<std::mutex>> lock_batches(tm_engine* e) {
+    std::vector<std::unique_lock<std::mutex>> held;
+    if (e)
+        for (auto& d : e->devs) held.emplace_back(d->bmu);
+    return held;
 }
 
 // a batch of deltas applied in chunks, the engine lock taken per chunk: each
 // delta is its own transaction in the reference (mnesia, per route), so a
 // batch need not be atomic, and a match launched meanwhile waits for one
-// chunk at most instead of the whole batch
+// chunk at most instead of the whole batch.  Between chunks the batch lets
+// every call already waiting for the lock go first (a plain mutex would
+// hand it straight back to the thread that just released it).
+// A chunk ends after 1024 deltas or 0.5 ms, whichever comes first.
 constexpr uint32_t DELTA_CHUNK = 1024;
 template <class F>
 int chunked(tm_engine* e, uint32_t n, F&& one) {
-    for (uint32_t c = 0; c < n; c += DELTA_CHUNK) {
+    for (uint32_t c = 0; c < n;) {
+        if (e && c)
+            for (int spin = 0; e->lock_waiters.load(std::memory_order_relaxed) > 0 && spin < 100000; ++spin)
+                std::this_thread::yield();
         const int rc = guarded(e, [&] {
-            for (uint32_t i = c; i < std::min(n, c + DELTA_CHUNK); ++i) one(i);
+            const auto t0 = std::chrono::steady_clock::now();
+            const uint32_t end = std::min(n, c + DELTA_CHUNK);
+            while (c < end) {
+                one(c++);
+                if ((c & 31) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(500)) break;
+            }
             return TM_OK;
-        });
+        }, false);
         if (rc != TM_OK) return rc;
     }
     return guarded(e, [] { return TM_OK; });
@@ -2170,7 +2308,8 @@ int tm_open_devices(const tm_config* cfg, const int32_t* devices, uint32_t n_dev
     for (uint32_t i = 0; i < n_devices; ++i) {
         std::unique_ptr<DevState> d(new (std::nothrow) DevState());
         if (!d || devices[i] < 0 || devices[i] >= ndev || hipSetDevice(devices[i]) != hipSuccess ||
-            hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess) {
+            hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess ||
+            hipStreamCreateWithFlags(&d->ustream, hipStreamNonBlocking) != hipSuccess) {
             for (auto& x : e->devs) x->release();
             delete e;
             if (prev >= 0) (void)hipSetDevice(prev);
@@ -2373,13 +2512,13 @@ enum BatchKind { K_MATCH = 0, K_ROUTES = 1, K_DELIVERIES = 2 };
 // more), and reports its total; then each copies its lists to the caller's
 // buffers at the prefix of the totals before it.  Results are identical to
 // one replica running the whole batch.
-int host_batch(tm_engine* e, BatchKind kind, const uint8_t* topic_bytes, const uint64_t* topic_off, uint32_t n,
-               uint32_t* out_count, uint64_t* out_off, uint32_t* out_a, uint32_t* out_b, uint64_t out_cap,
-               uint64_t* out_needed, uint32_t** out_alloc = nullptr) {
-    if (e->devs.empty()) {
-        e->last_error = "engine is host-only (no device): the match path runs on the GPU only";
-        return TM_EDEVICE;
-    }
+// the body of a host-buffer batch, inside batch_call over every replica
+// (the batch is cut across them); *stats_out gets the merged counters
+int host_batch_work(tm_engine* e, BatchKind kind, const uint8_t* topic_bytes, const uint64_t* topic_off, uint32_t n,
+                    uint32_t* out_count, uint64_t* out_off, uint32_t* out_a, uint32_t* out_b, uint64_t out_cap,
+                    uint64_t* out_needed, uint32_t** out_alloc, tm_batch_stats* stats_out) {
+    *stats_out = tm_batch_stats{};
+    stats_out->topics = n;
     for (uint32_t i = 0; i < n; ++i)
         if (topic_off[i + 1] < topic_off[i]) throw ArgError("topic offsets not monotone");
     if (n && topic_off[n] > topic_off[0] && !topic_bytes) throw ArgError("null topic bytes");
@@ -2389,7 +2528,6 @@ int host_batch(tm_engine* e, BatchKind kind, const uint8_t* topic_bytes, const u
         if (out_alloc && !(*out_alloc = (uint32_t*)std::malloc(4))) throw std::bad_alloc();
         return TM_OK;
     }
-    e->commit();
     if (out_alloc) out_cap = UINT64_MAX;   // sized below at the exact total
     const size_t R = std::min<size_t>(e->devs.size(), n);
     const uint32_t planes = kind == K_MATCH ? 1u : 2u;
@@ -2489,19 +2627,29 @@ int host_batch(tm_engine* e, BatchKind kind, const uint8_t* topic_bytes, const u
         HIPCHK(hipStreamSynchronize(d.stream));
     });
     out_off[n] = total;
-    e->finish_batch(n);
     if (e->stats_enabled && kind == K_MATCH)
         for (auto& s : st) {
-            e->last_stats.levels += s.levels;
-            e->last_stats.visits += s.visits;
-            e->last_stats.edge_reads += s.edge_reads;
-            e->last_stats.matches += s.matches;
-            e->last_stats.leaf_visits += s.leaf_visits;
-            e->last_stats.probe_loads += s.probe_loads;
-            e->last_stats.prunable_visits += s.prunable_visits;
+            stats_out->levels += s.levels;
+            stats_out->visits += s.visits;
+            stats_out->edge_reads += s.edge_reads;
+            stats_out->matches += s.matches;
+            stats_out->leaf_visits += s.leaf_visits;
+            stats_out->probe_loads += s.probe_loads;
+            stats_out->prunable_visits += s.prunable_visits;
         }
     if (out_needed) *out_needed = total;
     return total > out_cap ? TM_ENOSPC : TM_OK;
+}
+int host_batch(tm_engine* e, BatchKind kind, const uint8_t* topic_bytes, const uint64_t* topic_off, uint32_t n,
+               uint32_t* out_count, uint64_t* out_off, uint32_t* out_a, uint32_t* out_b, uint64_t out_cap,
+               uint64_t* out_needed, uint32_t** out_alloc = nullptr) {
+    if (!e) return TM_EINVAL;
+    if (e->devs.empty()) return no_device(e, "the match path");
+    tm_batch_stats stats{};
+    return batch_call(e, all_replicas(e), [&] {
+        return host_batch_work(e, kind, topic_bytes, topic_off, n, out_count, out_off, out_a, out_b, out_cap,
+                               out_needed, out_alloc, &stats);
+    }, [&] { e->last_stats = stats; });
 }
 }  // namespace
 
@@ -2509,10 +2657,8 @@ int tm_match_batch_owned(tm_engine* e, const uint8_t* topic_bytes, const uint64_
                          uint32_t* out_count, uint64_t* out_off, uint32_t** out_ids, uint64_t* out_total) {
     if (!topic_off || !out_off || !out_ids || (n && !out_count)) return TM_EINVAL;
     *out_ids = nullptr;
-    return guarded(e, [&]() -> int {
-        return host_batch(e, K_MATCH, topic_bytes, topic_off, n, out_count, out_off, nullptr, nullptr, 0, out_total,
+    return host_batch(e, K_MATCH, topic_bytes, topic_off, n, out_count, out_off, nullptr, nullptr, 0, out_total,
                           out_ids);
-    });
 }
 
 void tm_free(void* p) {
@@ -2523,10 +2669,8 @@ int tm_match_batch(tm_engine* e, const uint8_t* topic_bytes, const uint64_t* top
                    uint32_t* out_count, uint64_t* out_off, uint32_t* out_ids, uint64_t out_cap,
                    uint64_t* out_needed) {
     if (!topic_off || !out_off || (n && (!out_count)) || (out_cap && !out_ids)) return TM_EINVAL;
-    return guarded(e, [&]() -> int {
-        return host_batch(e, K_MATCH, topic_bytes, topic_off, n, out_count, out_off, out_ids, nullptr, out_cap,
+    return host_batch(e, K_MATCH, topic_bytes, topic_off, n, out_count, out_off, out_ids, nullptr, out_cap,
                           out_needed);
-    });
 }
 
 static int match_device(tm_engine* e, const uint8_t* d_bytes, const uint64_t* d_off, uint32_t n,
@@ -2604,13 +2748,10 @@ int tm_match_routes_batch_device(tm_engine* e, const uint8_t* d_bytes, const uin
                                  uint64_t topic_bytes, uint32_t* d_count, uint64_t* d_out_off, uint32_t* d_src,
                                  uint32_t* d_dest, uint64_t out_cap, uint64_t* d_total, void* hip_stream) {
     if (!d_off || !d_out_off || !d_total || (n && !d_count) || (out_cap && (!d_src || !d_dest))) return TM_EINVAL;
-    return guarded(e, [&]() -> int {
-        if (e->devs.empty()) {
-            e->last_error = "engine is host-only (no device): match_routes runs on the GPU only";
-            return TM_EDEVICE;
-        }
-        e->commit();
-        DevState& d = *e->replica_for(d_off);
+    if (!e) return TM_EINVAL;
+    if (e->devs.empty()) return no_device(e, "match_routes");
+    DevState& d = *e->replica_for(d_off);
+    return batch_call(e, {&d}, [&]() -> int {
         tm_engine::Guard g(d.device);
         hipStream_t st = hip_stream ? (hipStream_t)hip_stream : d.stream;
         if (n == 0) {
@@ -2619,19 +2760,16 @@ int tm_match_routes_batch_device(tm_engine* e, const uint8_t* d_bytes, const uin
             return TM_OK;
         }
         e->run_routes(d, d_bytes, d_off, n, topic_bytes, d_count, d_out_off, d_src, d_dest, out_cap, d_total, st);
-        e->finish_batch(n);
         return TM_OK;
-    });
+    }, [&] { e->finish_batch(n); });
 }
 
 int tm_match_routes_batch(tm_engine* e, const uint8_t* topic_bytes, const uint64_t* topic_off, uint32_t n,
                           uint32_t* out_count, uint64_t* out_off, uint32_t* out_src, uint32_t* out_dest,
                           uint64_t out_cap, uint64_t* out_needed) {
     if (!topic_off || !out_off || (n && !out_count) || (out_cap && (!out_src || !out_dest))) return TM_EINVAL;
-    return guarded(e, [&]() -> int {
-        return host_batch(e, K_ROUTES, topic_bytes, topic_off, n, out_count, out_off, out_src, out_dest, out_cap,
+    return host_batch(e, K_ROUTES, topic_bytes, topic_off, n, out_count, out_off, out_src, out_dest, out_cap,
                           out_needed);
-    });
 }
 
 int tm_dest_target(tm_engine* e, const uint8_t* dest, uint32_t dlen, uint32_t kind, const uint8_t* key,
@@ -2665,13 +2803,10 @@ int tm_match_deliveries_batch_device(tm_engine* e, const uint8_t* d_bytes, const
                                      uint64_t topic_bytes, uint32_t* d_count, uint64_t* d_out_off, uint32_t* d_to,
                                      uint32_t* d_target, uint64_t out_cap, uint64_t* d_total, void* hip_stream) {
     if (!d_off || !d_out_off || !d_total || (n && !d_count) || (out_cap && (!d_to || !d_target))) return TM_EINVAL;
-    return guarded(e, [&]() -> int {
-        if (e->devs.empty()) {
-            e->last_error = "engine is host-only (no device): aggre runs on the GPU only";
-            return TM_EDEVICE;
-        }
-        e->commit();
-        DevState& d = *e->replica_for(d_off);
+    if (!e) return TM_EINVAL;
+    if (e->devs.empty()) return no_device(e, "aggre");
+    DevState& d = *e->replica_for(d_off);
+    return batch_call(e, {&d}, [&]() -> int {
         tm_engine::Guard g(d.device);
         hipStream_t st = hip_stream ? (hipStream_t)hip_stream : d.stream;
         if (n == 0) {
@@ -2681,19 +2816,16 @@ int tm_match_deliveries_batch_device(tm_engine* e, const uint8_t* d_bytes, const
         }
         e->run_deliveries(d, d_bytes, d_off, n, topic_bytes, d_count, d_out_off, d_to, d_target, out_cap, d_total,
                           st);
-        e->finish_batch(n);
         return TM_OK;
-    });
+    }, [&] { e->finish_batch(n); });
 }
 
 int tm_match_deliveries_batch(tm_engine* e, const uint8_t* topic_bytes, const uint64_t* topic_off, uint32_t n,
                               uint32_t* out_count, uint64_t* out_off, uint32_t* out_to, uint32_t* out_target,
                               uint64_t out_cap, uint64_t* out_needed) {
     if (!topic_off || !out_off || (n && !out_count) || (out_cap && (!out_to || !out_target))) return TM_EINVAL;
-    return guarded(e, [&]() -> int {
-        return host_batch(e, K_DELIVERIES, topic_bytes, topic_off, n, out_count, out_off, out_to, out_target,
+    return host_batch(e, K_DELIVERIES, topic_bytes, topic_off, n, out_count, out_off, out_to, out_target,
                           out_cap, out_needed);
-    });
 }
 
 int tm_match_batch_device(tm_engine* e, const uint8_t* d_bytes, const uint64_t* d_off, uint32_t n,
@@ -2722,6 +2854,7 @@ int tm_match_batch_device_keys_w(tm_engine* e, const uint8_t* d_bytes, const uin
 
 int tm_key_levels(tm_engine* e, uint32_t* max_levels) {
     if (!max_levels) return TM_EINVAL;
+    auto held = lock_batches(e);
     return guarded(e, [&]() -> int {
         *max_levels = 0;
         for (auto& dp : e->devs) {
@@ -2775,13 +2908,12 @@ static int match_device(tm_engine* e, const uint8_t* d_bytes, const uint64_t* d_
                         uint64_t topic_bytes, uint32_t* d_count, uint64_t* d_out_off, uint32_t* d_ids,
                         uint64_t* d_keys, uint32_t key_words, uint64_t out_cap, uint64_t* d_total, void* hip_stream) {
     if (!d_off || !d_out_off || !d_total || (n && !d_count) || (out_cap && !d_ids)) return TM_EINVAL;
-    return guarded(e, [&]() -> int {
-        if (e->devs.empty()) {
-            e->last_error = "engine is host-only (no device): the match path runs on the GPU only";
-            return TM_EDEVICE;
-        }
-        e->commit();
-        DevState& d = *e->replica_for(d_off);   // the replica on the GPU that holds the batch
+    if (!e) return TM_EINVAL;
+    if (e->devs.empty()) return no_device(e, "the match path");
+    DevState& d = *e->replica_for(d_off);   // the replica on the GPU that holds the batch
+    tm_batch_stats stats{};
+    stats.topics = n;
+    return batch_call(e, {&d}, [&]() -> int {
         tm_engine::Guard g(d.device);
         hipStream_t st = hip_stream ? (hipStream_t)hip_stream : d.stream;
         if (n == 0) {
@@ -2791,19 +2923,19 @@ static int match_device(tm_engine* e, const uint8_t* d_bytes, const uint64_t* d_
         }
         e->run_batch(d, d_bytes, d_off, n, topic_bytes, d_count, d_out_off, d_ids, out_cap, d_total, st, d_keys,
                      key_words);
-        e->finish_batch(n);
         if (e->stats_enabled) {
             HIPCHK(hipStreamSynchronize(st));
-            e->last_stats = e->read_stats(d, n);
+            stats = e->read_stats(d, n);
         }
         return TM_OK;
-    });
+    }, [&] { e->last_stats = stats; });
 }
 
 // diagnostics (not part of include/topicmatch.h): the last stats-mode
 // batch's per-level histogram [visits, probe loads, failed probes] x 16
 extern "C" int tm_debug_hist(tm_engine* e, uint64_t* out, int n) {
     if (!e || !out || n > 56) return TM_EINVAL;
+    auto held = lock_batches(e);
     return guarded(e, [&]() -> int {
         if (e->devs.empty()) return TM_EINVAL;
         const DevBuf& ws = e->devs[0]->slots[e->devs[0]->last_slot].stats;
@@ -2866,7 +2998,9 @@ extern "C" int tm_debug_check_routes(tm_engine* e) {
             if (e->fr_meta[f].y && (!e->fr_rec[f] || e->fr_rec[f]->fid != f)) return fail("stale fr_meta");
         if (e->rt_order.size() != e->route_bag.size()) return fail("order size");
         const tm_engine::RouteRec* prev = nullptr;
-        for (const tm_engine::RouteRec* r : e->rt_order) {
+        for (const tm_engine::OrdKey& k : e->rt_order) {
+            const tm_engine::RouteRec* r = k.r;
+            if (k.label != r->label || r->ord->r != r) return fail("order entry of " + *r->key);
             if (prev && !(prev->label < r->label && *prev->key < *r->key)) return fail("label order at " + *r->key);
             prev = r;
         }
@@ -3007,6 +3141,7 @@ int tm_set_timing(tm_engine* e, int enable) {
 }
 
 int tm_last_kernel_times(tm_engine* e, const char** names, float* ms, int cap) {
+    auto held = lock_batches(e);
     return guarded(e, [&]() -> int {
         // average per batch of each kernel stage over every batch recorded
         // since the previous call, over all replicas

@@ -92,19 +92,21 @@ class AclRules:
             self.add(r)
         return self
 
-    def check_many(self, creds, pubsubs, topics):
-        """-> [(allow|deny|nomatch, rule index or None)] per check (GPU)"""
+    @staticmethod
+    def pack(creds, pubsubs, topics):
+        """the batch as the C-ABI's arrays (name -> numpy array), in
+        tm_acl_check_batch's argument order"""
         n = len(topics)
 
-        def pack(items):
+        def strs(items):
             bs = [_b(x) for x in items]
             off = np.zeros(n + 1, dtype=np.uint64)
             if n:
                 off[1:] = np.cumsum([len(x) for x in bs])
-            return np.frombuffer(b"".join(bs) + b"\0" * 8, dtype=np.uint8), off
-        tb, to = pack(topics)
-        cb, co = pack([c.get("client_id") or b"" for c in creds])
-        ub, uo = pack([c.get("username") or b"" for c in creds])
+            return np.frombuffer(b"".join(bs) + b"\0" * 8, dtype=np.uint8).copy(), off
+        tb, to = strs(topics)
+        cb, co = strs([c.get("client_id") or b"" for c in creds])
+        ub, uo = strs([c.get("username") or b"" for c in creds])
         cd = np.array([c.get("client_id") is not None for c in creds], dtype=np.uint8)
         ud = np.array([c.get("username") is not None for c in creds], dtype=np.uint8)
         peers = np.zeros((max(n, 1), 16), dtype=np.uint8)
@@ -117,9 +119,34 @@ class AclRules:
                 peers[i, :len(raw)] = np.frombuffer(raw, dtype=np.uint8)
                 fam[i] = 4 if ip.version == 4 else 6
         acc = np.array([1 if p == "publish" else 2 for p in pubsubs], dtype=np.uint8)
+        return {"access": acc, "topics": tb, "topic_off": to, "client_ids": cb, "client_off": co,
+                "client_defined": cd, "usernames": ub, "user_off": uo, "user_defined": ud, "peers": peers,
+                "peer_family": fam}
+
+    ARGS = ("access", "topics", "topic_off", "client_ids", "client_off", "client_defined", "usernames", "user_off",
+            "user_defined", "peers", "peer_family")
+
+    def check_packed(self, n, arrs):
+        """host arrays from pack() -> (result int8[n], rule u32[n])"""
         out = np.zeros(max(n, 1), dtype=np.int8)
         rule = np.zeros(max(n, 1), dtype=np.uint32)
         P = lambda a: ctypes.c_void_p(a.ctypes.data)  # noqa: E731
-        self._ck(self.lib.tm_acl_check_batch(self.h, n, P(acc), P(tb), P(to), P(cb), P(co), P(cd), P(ub), P(uo),
-                                             P(ud), P(peers), P(fam), P(out), P(rule)), "tm_acl_check_batch")
+        self._ck(self.lib.tm_acl_check_batch(self.h, n, *[P(arrs[k]) for k in self.ARGS], P(out), P(rule)),
+                 "tm_acl_check_batch")
+        return out[:n], rule[:n]
+
+    def check_device(self, n, d, d_out, d_rule, stream=None):
+        """device tensors (the pack() names) -> d_out / d_rule, stream-ordered
+        (tm_acl_check_batch_device)"""
+        P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+        st = None
+        if stream is not None:
+            st = ctypes.c_void_p(stream if isinstance(stream, int) else stream.cuda_stream)
+        self._ck(self.lib.tm_acl_check_batch_device(self.h, n, *[P(d[k]) for k in self.ARGS], P(d_out), P(d_rule),
+                                                    st), "tm_acl_check_batch_device")
+
+    def check_many(self, creds, pubsubs, topics):
+        """-> [(allow|deny|nomatch, rule index or None)] per check (GPU)"""
+        n = len(topics)
+        out, rule = self.check_packed(n, self.pack(creds, pubsubs, topics))
         return [(RESULT[int(out[i])], None if rule[i] == 0xFFFFFFFF else int(rule[i])) for i in range(n)]
