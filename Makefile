@@ -34,6 +34,9 @@ $(BUILD)/shard.o: emqx_amd/csrc/shard.hip emqx_amd/csrc/kernels.h emqx_amd/csrc/
 $(BUILD)/routes.o: emqx_amd/csrc/routes.hip emqx_amd/csrc/kernels.h emqx_amd/csrc/image.h | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
+$(BUILD)/presort.o: emqx_amd/csrc/presort.hip emqx_amd/csrc/kernels.h emqx_amd/csrc/image.h | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
 $(BUILD)/aggre.o: emqx_amd/csrc/aggre.hip emqx_amd/csrc/kernels.h emqx_amd/csrc/image.h | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
@@ -49,7 +52,7 @@ $(BUILD)/acl.o: emqx_amd/csrc/acl.hip include/topicmatch.h | $(BUILD)
 $(BUILD)/rewrite.o: emqx_amd/csrc/rewrite.hip include/topicmatch.h | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(LIBOUT): $(BUILD)/kernels.o $(BUILD)/shard.o $(BUILD)/routes.o $(BUILD)/aggre.o $(BUILD)/engine.o $(BUILD)/batcher.o $(BUILD)/acl.o $(BUILD)/rewrite.o $(BUILD)/exchange.o
+$(LIBOUT): $(BUILD)/kernels.o $(BUILD)/shard.o $(BUILD)/routes.o $(BUILD)/presort.o $(BUILD)/aggre.o $(BUILD)/engine.o $(BUILD)/batcher.o $(BUILD)/acl.o $(BUILD)/rewrite.o $(BUILD)/exchange.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -pthread $^ -L/opt/rocm/lib -lrccl -o $@
 
 emqx_amd/libtmwork.so: emqx_amd/csrc/workload.c

@@ -83,6 +83,7 @@ def parse():
     ap.add_argument("--hist", action="store_true", help="log per-level visit/probe histogram (diagnostic)")
     ap.add_argument("--layout", type=int, default=None, help="1 = DFS relayout on commit (default), 0 = off")
     ap.add_argument("--opt", action="append", default=[], help="EXPERIMENT: engine option name=value (repeatable)")
+    ap.add_argument("--presort", default=None, help="EXPERIMENT: batches sorted on the host: bytes | hN (N-bit word hashes)")
     return ap.parse_args()
 
 
@@ -112,6 +113,17 @@ def make_batches(a, cfg, rank, world):
             out.append((np.ascontiguousarray(tb[int(to[lo]):int(to[hi]) + 8]), sub))
         else:
             out.append(W.topics(a.config, n=a.topics, stream=multi.topic_stream(rank) * 64 + b))
+    if a.presort:   # EXPERIMENT: the batch in topic byte order (lanes of a wave walk shared prefixes)
+        from emqx_amd.engine import pack
+        import zlib
+        if a.presort == "bytes":
+            key = None
+        else:   # "hN": each level's word hashed to N bits, level-major (what a device radix sort could use)
+            nb = int(a.presort[1:])
+
+            def key(t):
+                return tuple(zlib.crc32(w) & ((1 << nb) - 1) for w in t.split(b"/"))
+        out = [pack(sorted(W.unpack(tb, to), key=key)) for tb, to in out]
     return out
 
 
@@ -260,7 +272,7 @@ def main():
         bi = j % len(dbat)
         d_b, d_o, n, nb = dbat[bi]
         eng.match_batch_device(d_b, d_o, n, nb, c_, oo_, i_, cap, t_, stream=s_)
-        last[bi] = j % len(lanes)
+        last[j % len(lanes)] = bi   # a lane's outputs hold its latest batch
 
     for _ in range(a.warmup):
         step()
@@ -268,7 +280,7 @@ def main():
 
     # ---- timed region: K steps; barrier + sync on both sides, max over ranks
     dt = multi.timed_region(step, a.steps, lambda: torch.cuda.synchronize(dev))
-    for bi, li in last.items():   # every batch's last result is complete and exact
+    for li, bi in last.items():   # every lane's last result is complete and exact
         assert int(lanes[li][4].item()) == totals[bi], "match total changed between steps"
     # per-kernel durations for the roofline: with batches overlapping, a
     # kernel's event interval also holds its neighbours' work, so the kernels

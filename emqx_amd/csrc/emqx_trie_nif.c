@@ -405,20 +405,23 @@ static ERL_NIF_TERM nif_route_del(ErlNifEnv* env, int argc, const ERL_NIF_TERM a
     return nif_route_op(env, argc, argv, 0);
 }
 
+/* Deltas run on dirty CPU schedulers: they take the engine lock, which a
+ * commit can hold while it waits for a batch pinned on the image it is about
+ * to rewrite (milliseconds), longer than a normal scheduler slice. */
 static ErlNifFunc funcs[] = {
     {"open", 1, nif_open, 0},
-    {"insert", 2, nif_insert, 0},
-    {"delete", 2, nif_delete, 0},
-    {"lookup", 2, nif_lookup, 0},
+    {"insert", 2, nif_insert, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"delete", 2, nif_delete, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"lookup", 2, nif_lookup, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"commit", 1, nif_commit, ERL_NIF_DIRTY_JOB_IO_BOUND},
     {"match", 2, nif_match, ERL_NIF_DIRTY_JOB_IO_BOUND},
     {"match_many", 2, nif_match_many, ERL_NIF_DIRTY_JOB_IO_BOUND},
     {"match_async", 2, nif_match_async, 0},                 /* returns at once: normal scheduler */
     {"match_routes_async", 2, nif_match_routes_async, 0},
     {"match_deliveries_async", 2, nif_match_deliveries_async, 0},
-    {"dest_target", 4, nif_dest_target, 0},
-    {"route_add", 3, nif_route_add, 0},
-    {"route_del", 3, nif_route_del, 0},
+    {"dest_target", 4, nif_dest_target, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"route_add", 3, nif_route_add, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"route_del", 3, nif_route_del, ERL_NIF_DIRTY_JOB_CPU_BOUND},
 };
 
 ERL_NIF_INIT(emqx_trie_nif, funcs, load, NULL, upgrade, NULL)

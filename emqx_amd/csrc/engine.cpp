@@ -208,7 +208,9 @@ constexpr int N_KERNEL_SLOTS = 4;   // tokenize, walk, scan, copy_out
 // beside the tokenizer / copy-out of its neighbours); a slot's next user
 // waits for its previous batch (hipStreamWaitEvent)
 struct Slot {
-    DevBuf twords, words, path, meta, scan, stage, kstage, ws, stats, perm;
+    DevBuf twords, words, path, meta, scan, stage, kstage, ws, stats, perm, skeys, svals, scount, soff, sscan,
+        twords_s, meta_s;
+    bool sorted = false;            // the slot's last batch walked in presort order (perm valid)
     uint64_t* h_maxc = nullptr;     // pinned: largest match count of the slot's last walk
     hipEvent_t maxc_ev = nullptr, done = nullptr;
     bool maxc_pending = false, used = false, keyed = false;
@@ -367,7 +369,7 @@ struct DevState {
             b->release();
         for (auto& w : slots) {
             for (DevBuf* b : {&w.twords, &w.words, &w.path, &w.meta, &w.scan, &w.stage, &w.kstage, &w.ws, &w.stats,
-                              &w.perm})
+                              &w.perm, &w.skeys, &w.svals, &w.scount, &w.soff, &w.sscan, &w.twords_s, &w.meta_s})
                 b->release();
             if (w.done) (void)hipEventDestroy(w.done);
             if (w.maxc_ev) (void)hipEventDestroy(w.maxc_ev);
@@ -435,7 +437,8 @@ struct tm_engine {
     int hist_enabled = 0;             // option "hist": per-level histogram in stats mode (diagnostic, slow)
     uint32_t walk_bpc = 0;            // option "walk_bpc": walk blocks per CU (0 = full occupancy)
     int xcdq = 1;                     // option "xcdq": per-XCD dequeue ranges in the queue walk (default on)
-    int group = 0;                    // option "group": walk the batch in topic-group order (kernels.hip; A/B at C3: no gain, off)
+    int presort = 0;                  // option "presort": walk the batch in the order of a key of its first
+                                      // eight words (presort.hip; 0 = arrival order)
     int layout_mode = 1;              // option "layout": 0 off, 1 auto, 2 every commit (tests)
     size_t created_since_layout = 0;  // nodes created since the last relayout
     uint32_t hot_levels = 4;          // option "hot_levels": relayout puts depths <= H level by level (BFS)
@@ -1775,7 +1778,17 @@ struct tm_engine {
         w.stage.ensure(((size_t)n * d.stage_k + 4) * 4);
         if (key_words) w.kstage.ensure(((size_t)n * d.stage_k * key_words + 4) * 8);
         w.ws.ensure(QWS_BYTES);
-        if (group) w.perm.ensure(((size_t)n + GROUP_WS_ELEMS) * 4);
+        if (presort) {
+            w.perm.ensure((size_t)n * 4 + 4);
+            w.twords_s.ensure((size_t)(n + 1) * WREG * 4);
+            w.meta_s.ensure((size_t)n * 4 + 4);
+            const uint32_t nc = presort_counts(n);
+            w.skeys.ensure((size_t)n * 8 + 8);
+            w.svals.ensure((size_t)n * 4 + 4);
+            w.scount.ensure((size_t)nc * 4 + 4);
+            w.soff.ensure(((size_t)nc + 1) * 8);
+            w.sscan.ensure(scan_tmp_elems(nc) * 8 + 8);
+        }
         if (!w.done) HIPCHK(hipEventCreateWithFlags(&w.done, hipEventDisableTiming));
     }
 
@@ -1843,7 +1856,17 @@ struct tm_engine {
         qb.kstage = keys ? w.kstage.as<uint64_t>() : nullptr;
         qb.scan_tmp = w.scan.as<uint64_t>();
         qb.ws = w.ws.as<unsigned long long>();
-        qb.perm = group ? w.perm.as<uint32_t>() : nullptr;
+        qb.perm = presort ? w.perm.as<uint32_t>() : nullptr;
+        if (presort) {
+            qb.sort_keys = w.skeys.as<uint32_t>();
+            qb.sort_vals = w.svals.as<uint32_t>();
+            qb.sort_counts = w.scount.as<uint32_t>();
+            qb.sort_off = w.soff.as<uint64_t>();
+            qb.sort_scan = w.sscan.as<uint64_t>();
+            qb.twords_s = w.twords_s.as<uint32_t>();
+            qb.meta_s = w.meta_s.as<uint32_t>();
+        }
+        w.sorted = presort != 0;
         HIPCHK(launch_queue(stats_enabled, xcdq != 0, im, bytes, off, n, qb, d.stage_k, counts, out_off, ids, keys,
                             cap, total, sp, st, timing_enabled ? marks : nullptr, walk_bpc, hist_enabled != 0,
                             keys ? key_words : 1u));
@@ -1877,7 +1900,7 @@ struct tm_engine {
         qb.kstage = keys ? w.kstage.as<uint64_t>() : nullptr;
         qb.scan_tmp = w.scan.as<uint64_t>();
         qb.ws = w.ws.as<unsigned long long>();
-        qb.perm = nullptr;
+        qb.perm = w.sorted ? w.perm.as<uint32_t>() : nullptr;   // the rows of a presorted walk
         HIPCHK(launch_copy(view(d), w.bytes, w.off, w.n, qb, w.K, w.kw, w.counts, w.out_off, ids, keys, cap, st));
         HIPCHK(hipEventRecord(w.done, st));
         d.note_use(st);
@@ -3020,11 +3043,6 @@ int tm_set_option(tm_engine* e, const char* name, int64_t value) {
             e->walk_bpc = (uint32_t)value;
             return TM_OK;
         }
-        if (!std::strcmp(name, "group")) {
-            if (value < 0 || value > 1) return TM_EINVAL;
-            e->group = (int)value;
-            return TM_OK;
-        }
         if (!std::strcmp(name, "xcdq")) {
             if (value < 0 || value > 1) return TM_EINVAL;
             e->xcdq = (int)value;
@@ -3033,6 +3051,11 @@ int tm_set_option(tm_engine* e, const char* name, int64_t value) {
         if (!std::strcmp(name, "layout")) {
             if (value < 0 || value > 2) return TM_EINVAL;
             e->layout_mode = (int)value;
+            return TM_OK;
+        }
+        if (!std::strcmp(name, "presort")) {
+            if (value < 0 || value > 1) return TM_EINVAL;
+            e->presort = (int)value;
             return TM_OK;
         }
         if (!std::strcmp(name, "route_gc")) {

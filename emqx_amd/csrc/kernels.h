@@ -24,9 +24,30 @@ struct QueueBufs {
     uint64_t* kstage;     // key_words planes of n x K order key words (sharded mode), or null
     uint64_t* scan_tmp;   // scan_tmp_elems(n)
     unsigned long long* ws;   // QWS_BYTES of queue heads
-    uint32_t* perm;       // group order (option "group"): n positions + 2 x 1024 group counts / cursors, or null
+    uint32_t* perm;       // option "presort": queue position -> topic (n), or null (arrival order)
+    // option "presort": the batch walked in the order of a 32-bit key of
+    // its first eight words (each hashed, level-major: 6,5,5,4,4,3,3,2 bits),
+    // so a wave's 64 lanes walk shared prefixes -- their loads of one node
+    // are one request, and a prefix's nodes are hot in L2 while its topics
+    // run.  An LSD radix sort, 4 passes of 8 bits (presort.hip): 2n u32 keys
+    // (the first n written by the tokenizer), n u32 values (ping-pong with
+    // perm), presort_counts(n) u32 and
+    // presort_counts(n) + 1 u64 offsets, scan_tmp_elems(presort_counts(n))
+    // The walk then reads twords_s / meta_s (the rows in walk order) and
+    // writes stage row p for position p; copy-out moves row p to topic
+    // perm[p] (launch_copy: the perm of the batch's walk, or null).
+    uint32_t* sort_keys = nullptr;
+    uint32_t* sort_vals = nullptr;
+    uint32_t* sort_counts = nullptr;
+    uint64_t* sort_off = nullptr;
+    uint64_t* sort_scan = nullptr;
+    uint32_t* twords_s = nullptr;   // n x WREG
+    uint32_t* meta_s = nullptr;     // n
 };
-constexpr uint32_t GROUP_WS_ELEMS = 2048;   // u32 after the n positions of perm
+// digit counters of the presort of n topics (256 per 4096-topic tile)
+uint32_t presort_counts(uint32_t n);
+hipError_t launch_presort(const uint32_t* twords, const uint32_t* meta, uint32_t n, const QueueBufs& qb,
+                          hipStream_t st);
 
 // tokenize -> NFA walk -> scan -> copy-out, all on st.  marks: 8 events,
 // [2i] before / [2i+1] after stage i, or null.  out_cap == 0: counts and

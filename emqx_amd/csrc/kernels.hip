@@ -165,26 +165,25 @@ __device__ __forceinline__ uint32_t tokenize_topic(const ImageView& im, const B&
 
 constexpr uint32_t MLONG = 1u << 30, MDOLLAR = 1u << 31, MN = (1u << 30) - 1;   // meta bits
 
-// Topic groups (option "group"): the walk takes the batch in the order of a
-// group key of the first two words, so each XCD's dequeue range (and each
-// 64-topic chunk) holds topics that share the top of their paths: the nodes
-// below a root word are then walked by one XCD and cached in its L2.
-// Host presort A/B at C3 (profiles/r01_v12_heat/presort, each sort key
-// followed by the whole topic): whole topic -7.2 % walk time, root word
-// -6.1 %, level-4 word +0 %; this one-pass grouping by (w0, w1) hashes
-// measured no gain (3.88 vs 3.88 ms per step): the presort gain comes from
-// neighbours sharing whole prefixes, which takes a full sort.  Off.
-constexpr uint32_t NGROUP = 1024;
 constexpr uint32_t TOK_WIN_WORDS = 512;   // LDS bytes window per wave: 4 KiB (64 topics of <= 64 B)
-__device__ __forceinline__ uint32_t group_of(uint32_t w0, uint32_t w1) {
-    return (((w0 * 0x9E3779B1u) >> 26) << 4) | ((w1 * 0x85EBCA6Bu) >> 28);
+
+// option "presort" (presort.hip): a topic's walk-order key -- its first
+// eight words hashed to 6,5,5,4,4,3,3,2 bits, level-major (levels past the
+// topic's end are 0)
+__device__ __forceinline__ uint32_t presort_key(const uint32_t (&tw)[WREG], uint32_t lev) {
+    constexpr uint32_t bits[8] = {6, 5, 5, 4, 4, 3, 3, 2};
+    uint32_t k = 0;
+#pragma unroll
+    for (uint32_t l = 0; l < 8; ++l) k = (k << bits[l]) | (l < lev ? (tw[l] * 0x9E3779B1u) >> (32 - bits[l]) : 0u);
+    return k;
 }
 
 template <class B>
 __device__ __forceinline__ void tokenize_one(const ImageView& im, const B& bytes,
                                              const uint64_t* __restrict__ off, uint32_t t,
                                              uint32_t* __restrict__ twords, uint32_t* __restrict__ words,
-                                             uint32_t* __restrict__ meta, uint32_t* lh) {
+                                             uint32_t* __restrict__ meta, uint32_t* __restrict__ skeys,
+                                             uint32_t* __restrict__ svals) {
     const uint64_t b = off[t], e = off[t + 1];
     uint32_t tw[WREG];
 #pragma unroll
@@ -198,19 +197,19 @@ __device__ __forceinline__ void tokenize_one(const ImageView& im, const B& bytes
         row[k] = make_uint4(tw[4 * k], tw[4 * k + 1], tw[4 * k + 2], tw[4 * k + 3]);
     const uint32_t dollar = (e > b && bytes.byte(b) == '$') ? 1u : 0u;
     meta[t] = lev | (dollar << 31) | (lev > WREG ? MLONG : 0u);
-    if (lh) atomicAdd(lh + group_of(tw[0], tw[1]), 1u);
+    if (skeys) {   // option "presort": the walk-order key (presort.hip)
+        skeys[t] = presort_key(tw, lev);
+        svals[t] = t;
+    }
 }
 
 __global__ void __launch_bounds__(BLOCK)
 tm_tokenize(ImageView im, const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint32_t n,
             uint32_t* __restrict__ twords, uint32_t* __restrict__ words, uint32_t* __restrict__ meta,
-            uint32_t* __restrict__ ghist) {
-    __shared__ uint32_t lh[NGROUP];
+            uint32_t* __restrict__ skeys, uint32_t* __restrict__ svals) {
     __shared__ uint64_t win[BLOCK / 64][TOK_WIN_WORDS];
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    if (ghist)
-        for (uint32_t k = threadIdx.x; k < NGROUP; k += BLOCK) lh[k] = 0;
     // the wave's 64 topics are contiguous bytes: stage them in LDS with
     // coalesced loads (per-lane 8 B loads of 64 different topics touch 64
     // lines per instruction); a window that does not fit reads global memory
@@ -229,58 +228,12 @@ tm_tokenize(ImageView im, const uint8_t* __restrict__ bytes, const uint64_t* __r
     __syncthreads();
     if (t < n) {
         if (lds)
-            tokenize_one(im, LdsBytes{win[wv], wbase}, off, t, twords, words, meta, ghist ? lh : nullptr);
+            tokenize_one(im, LdsBytes{win[wv], wbase}, off, t, twords, words, meta, skeys, svals);
         else
-            tokenize_one(im, GlobalBytes{bytes}, off, t, twords, words, meta, ghist ? lh : nullptr);
-    }
-    if (ghist) {
-        __syncthreads();
-        for (uint32_t k = threadIdx.x; k < NGROUP; k += BLOCK)
-            if (lh[k]) atomicAdd(ghist + k, lh[k]);
+            tokenize_one(im, GlobalBytes{bytes}, off, t, twords, words, meta, skeys, svals);
     }
 }
 
-// exclusive scan of the group histogram -> group cursors (one block)
-__global__ void __launch_bounds__(BLOCK) tm_group_scan(const uint32_t* __restrict__ ghist, uint32_t* __restrict__ gcur) {
-    __shared__ uint64_t lds[BLOCK / 64];
-    constexpr uint32_t PER = NGROUP / BLOCK;
-    uint32_t v[PER], sum = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < PER; ++k) {
-        v[k] = ghist[threadIdx.x * PER + k];
-        sum += v[k];
-    }
-    uint64_t tot;
-    uint32_t ex = (uint32_t)block_exclusive_scan(sum, lds, tot);
-#pragma unroll
-    for (uint32_t k = 0; k < PER; ++k) {
-        gcur[threadIdx.x * PER + k] = ex;
-        ex += v[k];
-    }
-}
-
-// perm[position] = topic: a block ranks its topics per group in LDS and
-// reserves each group's range with one global atomic
-__global__ void __launch_bounds__(BLOCK)
-tm_group_scatter(const uint32_t* __restrict__ twords, uint32_t n, uint32_t* __restrict__ gcur,
-                 uint32_t* __restrict__ perm) {
-    __shared__ uint32_t lh[NGROUP];
-    __shared__ uint32_t lb[NGROUP];
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    for (uint32_t k = threadIdx.x; k < NGROUP; k += BLOCK) lh[k] = 0;
-    __syncthreads();
-    uint32_t g = 0, r = 0;
-    if (t < n) {
-        const uint2 w = *reinterpret_cast<const uint2*>(twords + (uint64_t)t * WREG);
-        g = group_of(w.x, w.y);
-        r = atomicAdd(lh + g, 1u);
-    }
-    __syncthreads();
-    for (uint32_t k = threadIdx.x; k < NGROUP; k += BLOCK)
-        if (lh[k]) lb[k] = atomicAdd(gcur + k, lh[k]);
-    __syncthreads();
-    if (t < n) perm[lb[g] + r] = t;
-}
 
 
 // ---------------------------------------------------------------------------
@@ -638,7 +591,9 @@ __device__ __forceinline__ uint32_t xcc_id() {
 // XCDQ: the batch is cut into QRANGES contiguous ranges with one head each
 // (ws[16 * r], 128 B apart); a wave drains its own XCD's range first and then
 // steals, so neighbouring topics share one XCD's L2.  Otherwise one head.
-// Writes counts[t] and the first K ids of t to stage row t.
+// Writes counts[t] and the first K ids of t to stage row t.  With perm
+// (option "presort"), queue position p walks topic perm[p] from the sorted
+// rows twords_s / meta_s, into stage row p (copy-out finds it by pos_of).
 constexpr uint32_t QCHUNK = 64;
 constexpr uint32_t QRANGES = 8;
 constexpr uint32_t NO_TOPIC = 0xFFFFFFFFu;
@@ -650,7 +605,8 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
               uint32_t* __restrict__ stage, uint64_t* __restrict__ kstage, uint32_t K, uint32_t KW,
               uint32_t* __restrict__ counts,
               unsigned long long* __restrict__ ws, unsigned long long* __restrict__ stats,
-              unsigned long long* __restrict__ hist, const uint32_t* __restrict__ perm) {
+              unsigned long long* __restrict__ hist, const uint32_t* __restrict__ perm,
+              const uint32_t* __restrict__ twords_s, const uint32_t* __restrict__ meta_s) {
     __shared__ uint32_t lds_path[WREG * BLOCK];
     const uint32_t lane = threadIdx.x & 63;
     const LdsPath lp{lds_path + threadIdx.x};
@@ -661,7 +617,7 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
     bool exhausted = false;            // every head ran past its range (uniform)
     const uint32_t home = XCDQ ? xcc_id() : 0u;
     uint32_t qr = 0;                   // ranges given up so far (uniform)
-    uint32_t my = NO_TOPIC;
+    uint32_t my = NO_TOPIC, myt = 0;   // the lane's queue position and its topic
     bool is_long = false, drained = false;
     Cursor cur;
     RowEmit<KEYS> em{nullptr, nullptr, K, 0, make_uint4(0, 0, 0, 0), 0ull, KW, (uint64_t)n * K};
@@ -718,8 +674,10 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
                 if (rank < avail) i = qnext + rank;
                 else if (g + (rank - avail) < gend) i = g + (rank - avail);
                 if (i != NO_TOPIC) {
-                    if (perm) i = perm[i];   // group order (queue position -> topic)
-                    const uint32_t mt = meta[i];
+                    // i: queue position = stage row; ti: the topic
+                    const uint32_t ti = perm ? perm[i] : i;
+                    const uint32_t* tws = perm ? twords_s : twords;
+                    const uint32_t mt = perm ? meta_s[i] : meta[i];
                     const uint32_t nl = mt & MN;
                     const bool dollar = (mt & MDOLLAR) != 0;
                     lev_sum += nl;
@@ -728,7 +686,7 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
                     em.row = stage + (uint64_t)i * K;
                     if (KEYS) em.krow = kstage + (uint64_t)i * K;
                     em.cnt = 0;
-                    const uint32_t* tw = twords + (uint64_t)i * WREG;
+                    const uint32_t* tw = tws + (uint64_t)i * WREG;
                     bool go;
                     if (!is_long) {
 #pragma unroll
@@ -743,13 +701,17 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
                         }
                         go = walk_begin(im, cur, nl, dollar, rw, st);
                     } else {
-                        const uint64_t b = off[i] - off[0];
-                        mw = MemWords{tw, words + b + i};
-                        gp.base = gpath + b + 2ull * i;
+                        const uint64_t b = off[ti] - off[0];
+                        mw = MemWords{tw, words + b + ti};
+                        gp.base = gpath + b + 2ull * ti;
                         go = walk_begin(im, cur, nl, dollar, mw, st);
                     }
-                    if (go) my = i;
-                    else counts[i] = 0;
+                    if (go) {
+                        my = i;
+                        myt = ti;
+                    } else {
+                        counts[ti] = 0;
+                    }
                 } else if (exhausted) {
                     drained = true;
                 }
@@ -771,7 +733,7 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
                                  : walk_step<STATS, KEYS>(im, cur, lp, rw, em, st);
         if (fin) {
             em.flush();
-            counts[my] = em.cnt;
+            counts[myt] = em.cnt;
             match_sum += em.cnt;
             maxc = em.cnt > maxc ? em.cnt : maxc;
             my = NO_TOPIC;
@@ -864,6 +826,61 @@ tm_copy_out(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const ui
         const uint64_t b = off[t] - off[0];
         const MemWords mw{twords + (uint64_t)t * WREG, words + b + t};
         TailEmit<KEYS> em{out, kout, base + ex, out_cap, K, c, 0, KW, out_cap};
+        WalkStats s2;
+        if (mt & MLONG)
+            walk<false, KEYS>(im, mt & MN, (mt & MDOLLAR) != 0, GlobalPath{gpath + b + 2ull * t}, mw, em, s2);
+        else
+            walk<false, KEYS>(im, mt & MN, (mt & MDOLLAR) != 0, LdsPath{lds_path + threadIdx.x}, mw, em, s2);
+    }
+}
+
+// tm_copy_out over a presorted walk (option "presort"): stage row p holds
+// topic perm[p].  A block takes 256 positions: its threads fetch each one's
+// topic, count and output offset at once (the random reads overlap), then
+// one wave per position copies the row to the topic's output range (rows
+// read in order, each topic's output written contiguously); a topic past K
+// ids has its head re-walked by its thread
+template <bool KEYS>
+__global__ void __launch_bounds__(BLOCK)
+tm_copy_out_sorted(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const uint32_t* __restrict__ twords,
+                   const uint32_t* __restrict__ words, const uint32_t* __restrict__ meta,
+                   uint32_t* __restrict__ gpath, const uint32_t* __restrict__ stage,
+                   const uint64_t* __restrict__ kstage, uint32_t K, uint32_t KW, const uint32_t* __restrict__ counts,
+                   const uint64_t* __restrict__ out_off, uint32_t* __restrict__ out, uint64_t* __restrict__ kout,
+                   uint64_t out_cap, const uint32_t* __restrict__ perm) {
+    __shared__ uint32_t lds_path[WREG * BLOCK];
+    __shared__ uint32_t s_c[BLOCK];
+    __shared__ uint64_t s_o[BLOCK];
+    const uint64_t kplane = (uint64_t)n * K;
+    const uint32_t p0 = blockIdx.x * BLOCK;
+    const uint32_t tn = n - p0 < (uint32_t)BLOCK ? n - p0 : (uint32_t)BLOCK;
+    uint32_t t = 0, c = 0;
+    uint64_t ob = 0;
+    if (threadIdx.x < tn) {
+        t = perm[p0 + threadIdx.x];
+        c = counts[t];
+        ob = out_off[t];
+    }
+    s_c[threadIdx.x] = c;
+    s_o[threadIdx.x] = ob;
+    __syncthreads();
+    const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (uint32_t lt = w; lt < tn; lt += BLOCK / 64) {
+        const uint32_t ct = s_c[lt];
+        const uint64_t o = s_o[lt];
+        const uint64_t row = (uint64_t)(p0 + lt) * K + K - ct;   // + j: slot of output j (j >= ct - K)
+        for (uint32_t j = (ct > K ? ct - K : 0u) + lane; j < ct; j += 64)
+            if (o + j < out_cap) {
+                out[o + j] = stage[row + j];
+                if (KEYS)
+                    for (uint32_t q = 0; q < KW; ++q) kout[q * out_cap + o + j] = kstage[q * kplane + row + j];
+            }
+    }
+    if (threadIdx.x < tn && c > K) {   // fan-out beyond the stage row: walk again, write the head
+        const uint32_t mt = meta[t];
+        const uint64_t b = off[t] - off[0];
+        const MemWords mw{twords + (uint64_t)t * WREG, words + b + t};
+        TailEmit<KEYS> em{out, kout, ob, out_cap, K, c, 0, KW, out_cap};
         WalkStats s2;
         if (mt & MLONG)
             walk<false, KEYS>(im, mt & MN, (mt & MDOLLAR) != 0, GlobalPath{gpath + b + 2ull * t}, mw, em, s2);
@@ -1005,12 +1022,21 @@ hipError_t launch_copy(const ImageView& im, const uint8_t* bytes, const uint64_t
                        uint64_t* out_keys, uint64_t out_cap, hipStream_t st) {
     if (n == 0 || out_cap == 0) return hipSuccess;
     dim3 blk(BLOCK), g(div_up(n, BLOCK));
-    if (qb.kstage)
+    if (qb.perm) {   // a presorted walk: stage row p is topic perm[p]
+        if (qb.kstage)
+            hipLaunchKernelGGL(tm_copy_out_sorted<true>, g, blk, 0, st, im, off, n, qb.twords, qb.words, qb.meta,
+                               qb.path, qb.stage, qb.kstage, K, key_words, counts, out_off, out, out_keys, out_cap,
+                               qb.perm);
+        else
+            hipLaunchKernelGGL(tm_copy_out_sorted<false>, g, blk, 0, st, im, off, n, qb.twords, qb.words, qb.meta,
+                               qb.path, qb.stage, nullptr, K, 1u, counts, out_off, out, nullptr, out_cap, qb.perm);
+    } else if (qb.kstage) {
         hipLaunchKernelGGL(tm_copy_out<true>, g, blk, 0, st, im, off, n, qb.twords, qb.words, qb.meta, qb.path,
                            qb.stage, qb.kstage, K, key_words, counts, out_off, out, out_keys, out_cap);
-    else
+    } else {
         hipLaunchKernelGGL(tm_copy_out<false>, g, blk, 0, st, im, off, n, qb.twords, qb.words, qb.meta, qb.path,
                            qb.stage, nullptr, K, 1u, counts, out_off, out, nullptr, out_cap);
+    }
     return hipGetLastError();
 }
 
@@ -1033,15 +1059,11 @@ hipError_t launch_queue(bool stats_mode, bool xcdq, const ImageView& im, const u
     if (err != hipSuccess) return err;
     dim3 blk(BLOCK), g(div_up(n, BLOCK));
     mark(0);
-    uint32_t* ghist = qb.perm ? qb.perm + n : nullptr;   // NGROUP counts, then NGROUP cursors
-    if (ghist) {
-        err = hipMemsetAsync(ghist, 0, NGROUP * sizeof(uint32_t), st);
+    hipLaunchKernelGGL(tm_tokenize, g, blk, 0, st, im, bytes, off, n, qb.twords, qb.words, qb.meta,
+                       qb.perm ? qb.sort_keys : nullptr, qb.perm ? qb.perm : nullptr);
+    if (qb.perm) {   // option "presort": perm and the rows in walk order (presort.hip)
+        err = launch_presort(qb.twords, qb.meta, n, qb, st);
         if (err != hipSuccess) return err;
-    }
-    hipLaunchKernelGGL(tm_tokenize, g, blk, 0, st, im, bytes, off, n, qb.twords, qb.words, qb.meta, ghist);
-    if (ghist) {
-        hipLaunchKernelGGL(tm_group_scan, dim3(1), blk, 0, st, ghist, ghist + NGROUP);
-        hipLaunchKernelGGL(tm_group_scatter, g, blk, 0, st, qb.twords, n, ghist + NGROUP, qb.perm);
     }
     mark(1);
     mark(2);
@@ -1050,8 +1072,7 @@ hipError_t launch_queue(bool stats_mode, bool xcdq, const ImageView& im, const u
 #define TM_Q(S, X, Y)                                                                                              \
     hipLaunchKernelGGL((tm_walk_queue<S, X, Y>), dim3(wg), blk, 0, st, im, off, n, qb.twords, qb.words, qb.meta, \
                        qb.path, qb.stage, qb.kstage, K, key_words, counts, qb.ws, stats,                         \
-                       hist ? stats + HIST_OFF : nullptr,                                                           \
-                       qb.perm)
+                       hist ? stats + HIST_OFF : nullptr, qb.perm, qb.twords_s, qb.meta_s)
     if (keys) {
         if (stats_mode) TM_Q(true, true, true); else TM_Q(false, true, true);
     } else if (stats_mode) {
@@ -1067,12 +1088,8 @@ hipError_t launch_queue(bool stats_mode, bool xcdq, const ImageView& im, const u
     mark(5);
     mark(6);
     if (out_cap) {
-        if (keys)
-            hipLaunchKernelGGL(tm_copy_out<true>, g, blk, 0, st, im, off, n, qb.twords, qb.words, qb.meta, qb.path,
-                               qb.stage, qb.kstage, K, key_words, counts, out_off, out, out_keys, out_cap);
-        else
-            hipLaunchKernelGGL(tm_copy_out<false>, g, blk, 0, st, im, off, n, qb.twords, qb.words, qb.meta, qb.path,
-                               qb.stage, nullptr, K, 1u, counts, out_off, out, nullptr, out_cap);
+        err = launch_copy(im, bytes, off, n, qb, K, key_words, counts, out_off, out, out_keys, out_cap, st);
+        if (err != hipSuccess) return err;
     }
     mark(7);
     return hipGetLastError();

@@ -229,11 +229,13 @@ VARIANTS = {"queue": {}, "queue_xcd": {}, "queue_xcd@nosplit@dfs": {"split": 0, 
             "queue_xcd@nohotedges": {"hot_edges": 0}, "queue_xcd@hotedges5@relayout": {"hot_edges": 5, "layout": 2},
             "queue_xcd@plusfirst": {"order": 1, "layout": 2}, "queue_xcd@hashlast": {"order": 2, "layout": 2},
             "queue_xcd@order3@dfs": {"order": 3, "hot_levels": 0, "layout": 2},
-            "queue_xcd@order0": {"order": 0, "layout": 2}, "queue_xcd@nogroup": {"group": 0},
+            "queue_xcd@order0": {"order": 0, "layout": 2},
             "queue_xcd@nosummaries": {"summaries": 0}, "queue_xcd@summaries_nolayout": {"layout": 0},
-            "queue@group": {"group": 1}, "queue_xcd@heat": {"order": 5, "layout": 2},
+            "queue_xcd@heat": {"order": 5, "layout": 2},
             "queue@heat@hashlast@split0": {"order": 7, "layout": 2, "split": 0}, "queue_xcd@heatf": {"order": 15, "layout": 2},
-            "queue_xcd@edgeload2": {"edge_load": 2, "layout": 2}, "queue_xcd@edgeload16": {"edge_load": 16}}
+            "queue_xcd@edgeload2": {"edge_load": 2, "layout": 2}, "queue_xcd@edgeload16": {"edge_load": 16},
+            "queue_xcd@presort": {"presort": 1}, "queue@presort": {"presort": 1},
+            "queue_xcd@presort@stagek16": {"presort": 1, "stage_k": 16, "stage_auto": 0}}
 
 
 @pytest.mark.parametrize("variant", list(VARIANTS))
