@@ -5,8 +5,10 @@
 Units and corrections (/opt/skills/guides/MI355X_MICROARCH.md, HBM section):
 FETCH_SIZE/WRITE_SIZE are in KB.  The guide's x2 correction is for wide
 coalesced streaming reads; the walk's reads are random 16 B gathers, which
-profiles/ubench/gather_rates.txt calibrates at exactly one 64 B TCC_EA0_RDREQ
-(= 64 B of FETCH_SIZE) per L2-missing access, so FETCH_SIZE is taken as is.
+the gather microbenchmark calibrates at exactly one TCC_EA0_RDREQ = 64 B of
+FETCH_SIZE per L2-missing access (profiles/r02_gather/gather_pmc.json:
+33.5M accesses over a 4 GiB table -> 33.5M EA read requests, 63.9 B of
+FETCH_SIZE each), so FETCH_SIZE is taken as is.
 
 usage: python tools/traffic.py gpurun_out/pmc_x profiles/traffic_c3.json
 """
@@ -29,7 +31,8 @@ out = {
     "traffic_bytes_per_launch": (w["FETCH_SIZE"] + w["WRITE_SIZE"]) * 1024.0,
     "l2_hit_rate": w["TCC_HIT_sum"] / (w["TCC_HIT_sum"] + w["TCC_MISS_sum"]),
     "ea_read_requests_per_launch": w.get("TCC_EA0_RDREQ_sum"),
-    "correction": "none: random 16 B gathers, 1 EA read request = 64 B (profiles/ubench/gather_rates.txt)",
+    "correction": "none: random 16 B gathers, 1 EA read request = 64 B of FETCH_SIZE per missed access "
+                  "(profiles/r02_gather/gather_pmc.json)",
     "source": src,
     "build": rev,
 }
