@@ -174,7 +174,27 @@ def o1_check_and_baseline(a, fb, fo, n_filters, batches, results, do_cpu):
     return ok, legs
 
 
+# The one JSON line goes to the process's original stdout; everything else
+# written to fd 1 -- RCCL's version banner at communicator init, library
+# prints -- is sent to stderr, so stdout holds exactly the result line.
+_RESULT_FD = None
+
+
+def quiet_stdout():
+    global _RESULT_FD
+    if _RESULT_FD is None:
+        sys.stdout.flush()
+        _RESULT_FD = os.dup(1)
+        os.dup2(2, 1)
+
+
+def emit(obj):
+    line = (json.dumps(obj) + "\n").encode()
+    os.write(_RESULT_FD if _RESULT_FD is not None else 1, line)
+
+
 def main():
+    quiet_stdout()
     a = parse()
     if a.lib:
         from emqx_amd import _lib
@@ -382,7 +402,7 @@ def main():
             "parity_check": check_ok,
         }
         out.update(extras)
-        print(json.dumps(out), flush=True)
+        emit(out)
     eng.close()
     if world > 1:
         dist.destroy_process_group()
@@ -490,7 +510,7 @@ def main_single_process(a):
     counts, offs, ids = eng.match_batch(tb, to)   # the host path over all replicas: the same lists
     got = np.concatenate([p["i"][: int(p["t"].item())].cpu().numpy().view(np.uint32) for p in parts])
     assert np.array_equal(got, ids), "replica results differ from the whole-batch host path"
-    print(json.dumps({"metric": METRIC, "value": a.topics * a.steps / dt, "unit": "topics/s", "n_gpus": N,
+    emit({"metric": METRIC, "value": a.topics * a.steps / dt, "unit": "topics/s", "n_gpus": N,
                       "steps": a.steps, "warmup": a.warmup, "ms_per_step": dt / a.steps * 1e3,
                       "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u32",
                       "data": "synthetic",
@@ -498,7 +518,7 @@ def main_single_process(a):
                                              "per step split over them" % (a.config, devs, a.topics),
                                  "filters": n_filters, "topics_per_step": a.topics,
                                  "parallelism": "one process, tm_open_devices x %d" % N},
-                      "replicas_consistent": True}), flush=True)
+                      "replicas_consistent": True})
     eng.close()
 
 
@@ -654,7 +674,7 @@ def main_sharded(a, rank, world, local, dev):
                        "ids_walked": total, "ids_merged": mtotal},
             "parity_check": check_ok,
         }
-        print(json.dumps(out), flush=True)
+        emit(out)
     comm.close()
     eng.close()
 
