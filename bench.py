@@ -445,7 +445,7 @@ def host_legs(a, eng, batch, total):
         drv.tm_bench_batcher.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
                                          ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                          ctypes.c_uint32, ctypes.POINTER(ctypes.c_double)]
-        k = min(n, 2_000_000)
+        k = n   # the whole batch, after a warm-up run inside the driver
         res = (ctypes.c_double * 8)()
         rc = drv.tm_bench_batcher(eng.h, tb.ctypes.data, to.ctypes.data, k, 16, 200, 65536, 2, 0, res)
         if rc == 0:
