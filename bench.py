@@ -447,10 +447,13 @@ def host_legs(a, eng, batch, total):
                                          ctypes.c_uint32, ctypes.POINTER(ctypes.c_double)]
         k = n   # the whole batch, after a warm-up run inside the driver
         res = (ctypes.c_double * 8)()
-        rc = drv.tm_bench_batcher(eng.h, tb.ctypes.data, to.ctypes.data, k, 16, 200, 65536, 2, 0, res)
+        # 4 lanes, batches up to 256K topics: the best point of tools/bench_batcher.py
+        # (profiles/r02_misc/batcher_sweep.md)
+        rc = drv.tm_bench_batcher(eng.h, tb.ctypes.data, to.ctypes.data, k, 16, 200, 262144, 4, 0, res)
         if rc == 0:
             out["batcher"] = {"topics_per_s": res[1], "topics": k, "producers": 16, "deadline_us": 200,
-                              "lanes_per_replica": 2, "batches": int(res[2]), "mean_batch": res[3],
+                              "max_topics": 262144, "lanes_per_replica": 4, "batches": int(res[2]),
+                              "mean_batch": res[3],
                               "lat_us_p50": res[4], "lat_us_p99": res[5], "failed": int(res[6]),
                               "matches": int(res[7]),
                               "path": "tm_batcher_submit per publish from 16 threads, per-topic callbacks (NIF path)"}
