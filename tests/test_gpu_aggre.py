@@ -224,3 +224,51 @@ def test_routes_enospc_small_batch_high_fanout(gpu_device):
     assert list(counts) == [n_routes, n_routes]     # node dests only: the fold reverses
     assert [e.target_bytes(int(x))[1] for x in tg[:3]] == [b"n69999", b"n69998", b"n69997"]
     e.close()
+
+
+@pytest.mark.parametrize("double_buffer", [1, 0])
+def test_route_image_churn_on_device_vs_oracle(gpu_device, double_buffer):
+    """the in-place route image (engine.cpp) on the device under heavy churn:
+    compactions (option route_gc tiny), exact-table regrowth, label
+    relabels (topics added in order), a filter deleted and re-inserted
+    behind the router's back; every burst's match_routes/1 and
+    aggre(match_routes/1) equal the oracle's, with two image epochs and with
+    one (double_buffer 0)"""
+    rng = random.Random(31 + double_buffer)
+    e = Engine(device=gpu_device)
+    e.set_option("route_gc", 64)
+    e.set_option("double_buffer", double_buffer)
+    r, o = Router(e, node="n1"), pytrie.RouteTable()
+    pool = _pool(rng, 400) + [b"t/%05d" % i for i in range(600)]
+    live = {}
+    for burst in range(12):
+        for _ in range(700):
+            t = rng.choice(pool)
+            d = rng.choice(DESTS)
+            if rng.random() < 0.6 or not live:
+                r.add_route(t, d)
+                o.add_route(t, d)
+                live.setdefault(t, set()).add(d)
+            else:
+                t = rng.choice(sorted(live))
+                d = rng.choice(sorted(live[t], key=str))
+                r.del_route(t, d)
+                o.del_route(t, d)
+                live[t].discard(d)
+                if not live[t]:
+                    del live[t]
+        if burst % 3 == 2:   # a wildcard filter deleted and re-inserted behind the router's back
+            w = [t for t in live if b"+" in t or t.endswith(b"#")]
+            if w:
+                t = rng.choice(w)
+                e.delete(t)
+                e.insert(t)
+        if burst % 4 == 3:
+            e.debug_check_routes()
+        topics = _topics(rng, 200) + [t for t in pool[:50] if b"+" not in t and b"#" not in t]
+        got = r.match_deliveries_many(topics, tagged=True)
+        for tp, row in zip(topics, got):
+            assert row == o.match_deliveries(tp), (burst, tp)
+        for tp, row in zip(topics, r.match_routes_many(topics)):
+            assert [(x.topic, x.dest) for x in row] == o.match_routes(tp), (burst, tp)
+    e.close()

@@ -15,7 +15,7 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 pytestmark = pytest.mark.gpu
 
 
-def _run_sharded(filters, topics, S, K=None):
+def _run_sharded(filters, topics, S, K=None, opts=None):
     import torch
     from emqx_amd import shard
     from emqx_amd.engine import pack
@@ -31,6 +31,8 @@ def _run_sharded(filters, topics, S, K=None):
         e = shard.ShardEngine(0, S, s, filters_hint=len(filters))
         if K:
             e.set_option("stage_k", K)
+        for k, v in (opts or {}).items():
+            e.set_option(k, v)
         e.insert_many(fb, fo)
         c = torch.empty(n, dtype=torch.int32, device=dev)
         o = torch.empty(n + 1, dtype=torch.int64, device=dev)
@@ -90,6 +92,18 @@ def test_sharded_c1_equals_o1(gpu_device, S):
     filters = W.unpack(*W.filters(1))
     topics = W.unpack(*W.topics(1, n=20000))
     got = _run_sharded(filters, topics, S)
+    assert got == _o1(filters, topics)
+
+
+@pytest.mark.parametrize("S", [1, 3])
+def test_sharded_presorted_walk_equals_o1(gpu_device, S):
+    """option presort on the keyed walk: stage rows in walk order, keys and
+    ids copied out by position (tm_copy_out_sorted<KEYS>), merged by key;
+    with a small stage row, so topics past K re-walk their heads"""
+    from emqx_amd import workload as W
+    filters = W.unpack(*W.filters(1))
+    topics = W.unpack(*W.topics(1, n=20000))
+    got = _run_sharded(filters, topics, S, K=16, opts={"presort": 1, "stage_auto": 0})
     assert got == _o1(filters, topics)
 
 
