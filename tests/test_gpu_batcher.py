@@ -43,6 +43,14 @@ def test_batcher_results_equal_batch_api(gpu_device, routes):
         e.insert_many(fb, fo)
         counts, offs, ids = e.match_batch(tb, to)
         want = [(list(ids[offs[t]:offs[t + 1]]), None) for t in range(len(topics))]
+        # the batch API itself against O1 (no self-comparison only)
+        from oracle import O1
+        o1 = O1()
+        o1.insert_many(fb, fo)
+        oc, oo, oi = o1.match_ids(tb, to, threads=8)
+        filters = W.unpack(fb, fo)
+        for t in range(0, len(topics), 7):
+            assert [e.filter_bytes(int(x)) for x in want[t][0]] == [filters[j] for j in oi[oo[t]:oo[t + 1]]], t
     b = Batcher(e, max_topics=3000, deadline_us=500, routes=routes is True, deliveries=routes == "deliveries")
     got = [None] * len(topics)
 
