@@ -258,14 +258,14 @@ def main():
         if i == 0:
             stats = eng.last_stats()
             fan = np.sort(c.cpu().numpy().view(np.uint32))
+            if a.hist:   # the stats batch's slot, before the next batch takes another
+                h = (ctypes.c_uint64 * 56)()
+                eng.lib.tm_debug_hist(eng.h, h, 56)
+                for k, name in enumerate(["visits", "probe_loads", "failed_probes"]):
+                    log("per-level %s per topic: %s" % (name, [round(h[16 * k + l] / n, 2) for l in range(16)]))
+                eng.set_option("hist", 0)
         totals.append(int(t.item()))
     eng.set_stats(False)
-    if a.hist:
-        h = (ctypes.c_uint64 * 56)()
-        eng.lib.tm_debug_hist(eng.h, h, 56)
-        n0 = dbat[0][2]
-        for k, name in enumerate(["visits", "probe_loads", "failed_probes"]):
-            log("per-level %s per topic: %s" % (name, [round(h[16 * k + l] / n0, 2) for l in range(16)]))
     fanout = {"mean": float(fan.mean()), "p50": int(fan[len(fan) // 2]), "p90": int(fan[int(len(fan) * 0.9)]),
               "p99": int(fan[int(len(fan) * 0.99)]), "max": int(fan[-1])}
     log("fan-out per topic: %s" % fanout)
