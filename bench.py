@@ -202,8 +202,13 @@ def main():
     rank, world, local = multi.env_rank()
     if a.single_process:
         return main_single_process(a)
+    # TM_BENCH_SHARE_GPU=1 (rehearsal on a one-GPU box): every rank on GPU 0,
+    # the control plane (barrier, max of step times) over gloo
+    share = os.environ.get("TM_BENCH_SHARE_GPU") == "1"
+    if share:
+        local = 0
     if world > 1:
-        dist.init_process_group("nccl" if torch.cuda.is_available() else "gloo")
+        dist.init_process_group("nccl" if torch.cuda.is_available() and not share else "gloo")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if (a.mode or ("sharded" if a.config == 4 else "replicated")) == "sharded":
