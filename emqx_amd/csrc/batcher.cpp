@@ -11,18 +11,20 @@
 // callback (the NIF's callback builds the list and enif_send()s it).
 //
 // Submission is striped: a producer thread appends to one of NSTRIPE
-// buffers (its own lock), so thousands of publishers do not serialise on one
-// mutex; a seal takes every stripe.  The sealing thread gathers the stripes
-// into the pinned host memory of a free LANE and hands the batch over; each
-// lane (a thread, a stream and its own pinned / HBM buffers, bound to one of
-// the engine's replicas, lanes_per_replica per GPU) copies its batch to HBM,
-// runs the stream-ordered device path (tm_match_batch_device,
-// tm_match_routes_batch_device, tm_match_deliveries_batch_device), reads back
-// counts, offsets and the total, then exactly `total` ids (no capacity-sized
-// read-back), and runs the batch's callbacks.  So several batches are in
-// flight at once (one per lane: upload, walk and read-back of neighbouring
-// batches overlap, and every GPU of a multi-device engine works), and the
-// callbacks of one batch run on its lane while the next batches proceed.
+// chunks (its stripe's lock), so thousands of publishers do not serialise on
+// one mutex.  A seal is O(stripes): the sealing thread moves each stripe's
+// whole chunk out (a vector swap; only a stripe holding more than the batch
+// has room for copies its oldest topics out) and hands the chunks to a free
+// LANE; the lane (a thread, a stream and its own pinned / HBM buffers, bound
+// to one of the engine's replicas, lanes_per_replica per GPU) packs them into
+// its pinned memory, copies the batch to HBM, runs the stream-ordered device
+// path (tm_match_batch_device, tm_match_routes_batch_device,
+// tm_match_deliveries_batch_device), reads back counts, offsets and the
+// total, then exactly `total` ids (no capacity-sized read-back), runs the
+// batch's callbacks and recycles the chunks.  So several batches are in
+// flight at once (one per lane: packing, upload, walk, read-back and
+// callbacks of neighbouring batches overlap, and every GPU of a multi-device
+// engine works), and no per-topic work runs on the single sealing thread.
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
@@ -49,15 +51,37 @@ struct Req {
     uint64_t ticket;
 };
 
-// A producer thread appends to its own stripe; everything a submit touches
-// lives in the stripe's cache lines (no shared counter is written per
-// publish): its lock, its buffers, its pending count / bytes, the arrival
-// time of its oldest topic and its ticket sequence.
-struct alignas(64) Stripe {
-    std::mutex mu;
+// Topics of one stripe, oldest first, from `head` on (a partial take
+// advances head instead of moving the rest to the front).
+struct Chunk {
     std::vector<uint8_t> bytes;
     std::vector<uint32_t> lens;
     std::vector<Req> reqs;
+    size_t head = 0, bhead = 0;   // topics / bytes already taken
+    size_t size() const { return lens.size() - head; }
+    size_t nbytes() const { return bytes.size() - bhead; }
+    void reset() {
+        bytes.clear();
+        lens.clear();
+        reqs.clear();
+        head = bhead = 0;
+    }
+    void compact() {   // drop the taken prefix once it is the larger part
+        if (head == 0 || head < lens.size() / 2) return;
+        bytes.erase(bytes.begin(), bytes.begin() + bhead);
+        lens.erase(lens.begin(), lens.begin() + head);
+        reqs.erase(reqs.begin(), reqs.begin() + head);
+        head = bhead = 0;
+    }
+};
+
+// A producer thread appends to its own stripe; everything a submit touches
+// lives in the stripe's cache lines (no shared counter is written per
+// publish): its lock, its chunk, its pending count / bytes, the arrival
+// time of its oldest topic and its ticket sequence.
+struct alignas(64) Stripe {
+    std::mutex mu;
+    Chunk cur;
     std::atomic<uint64_t> pending{0}, pending_bytes{0};
     std::atomic<int64_t> first_ns{INT64_MAX};   // INT64_MAX: empty
     uint64_t seq = 0;                           // under mu
@@ -112,8 +136,7 @@ struct Lane {
     std::condition_variable cv;
     bool full = false, stop = false;   // a batch has been handed over / shut down
     uint32_t n = 0;
-    bool oom = false;
-    std::vector<Req> reqs;
+    std::vector<Chunk> chunks;        // the batch: stripe chunks in gather order
     Pinned h_bytes, h_off, h_counts, h_outoff, h_src, h_dest, h_total;
     Dev d_bytes, d_off, d_counts, d_outoff, d_src, d_dest, d_total;
     double ids_per_topic = 64.0;      // sizing estimate of the device result buffers
@@ -143,10 +166,23 @@ struct tm_batcher {
     uint64_t rotate = 0;              // first stripe of the next gather (sealer only)
     uint64_t next_lane = 0;
 
-    struct Taken {
-        std::vector<uint8_t> bytes;
-        std::vector<uint32_t> lens;
-    } taken[NSTRIPE];
+    std::mutex pool_mu;               // emptied chunks (capacity kept) for the stripes
+    std::vector<Chunk> pool;
+
+    Chunk spare() {
+        std::lock_guard<std::mutex> lk(pool_mu);
+        if (pool.empty()) return Chunk();
+        Chunk c = std::move(pool.back());
+        pool.pop_back();
+        return c;
+    }
+    void recycle(std::vector<Chunk>& cs) {
+        for (Chunk& c : cs) c.reset();
+        std::lock_guard<std::mutex> lk(pool_mu);
+        for (Chunk& c : cs)
+            if (pool.size() < 4 * NSTRIPE) pool.push_back(std::move(c));
+        cs.clear();
+    }
 
     int64_t now_ns() const { return std::chrono::duration_cast<std::chrono::nanoseconds>(clk::now().time_since_epoch()).count(); }
 
@@ -173,69 +209,76 @@ struct tm_batcher {
     }
 
     // move stripes' topics (oldest first, up to max_topics) into lane L's
-    // pinned batch; sets L.n (L.oom when staging memory ran out)
+    // chunk list: a stripe that fits whole is swapped out, one holding more
+    // than the batch has room for gives its oldest topics; sets L.n
     void gather(Lane& L) {
-        L.reqs.clear();
-        L.oom = false;
-        uint64_t nb = 0, n = 0;
+        L.chunks.clear();
+        uint64_t n = 0;
         const uint64_t cap = cfg.max_topics;
         const int start = (int)(rotate++ % NSTRIPE);   // no stripe starves under overload
         for (int i = 0; i < NSTRIPE && n < cap; ++i) {
             const int s = (start + i) % NSTRIPE;
             Stripe& x = stripes[s];
+            if (x.pending.load(std::memory_order_acquire) == 0) continue;
+            Chunk fresh = spare();   // outside the stripe lock
             std::lock_guard<std::mutex> lk(x.mu);
-            const size_t have = x.lens.size();
-            if (have == 0) continue;
-            const size_t k = (size_t)std::min<uint64_t>(have, cap - n);
-            Taken& t = taken[s];
-            if (k == have) {   // the whole stripe
-                t.bytes.swap(x.bytes);
-                t.lens.swap(x.lens);
-                L.reqs.insert(L.reqs.end(), x.reqs.begin(), x.reqs.end());
-                x.reqs.clear();
-                x.bytes.clear();
-                x.lens.clear();
-            } else {           // its oldest k topics (the batch stays within max_topics)
-                size_t kb = 0;
-                for (size_t i = 0; i < k; ++i) kb += x.lens[i];
-                t.bytes.assign(x.bytes.begin(), x.bytes.begin() + kb);
-                t.lens.assign(x.lens.begin(), x.lens.begin() + k);
-                L.reqs.insert(L.reqs.end(), x.reqs.begin(), x.reqs.begin() + k);
-                x.bytes.erase(x.bytes.begin(), x.bytes.begin() + kb);
-                x.lens.erase(x.lens.begin(), x.lens.begin() + k);
-                x.reqs.erase(x.reqs.begin(), x.reqs.begin() + k);
+            const size_t have = x.cur.size();
+            if (have == 0) {
+                recycle_one(std::move(fresh));
+                continue;
             }
-            nb += t.bytes.size();
-            n += t.lens.size();
+            const size_t k = (size_t)std::min<uint64_t>(have, cap - n);
+            size_t kb;
+            if (k == have) {   // the whole stripe
+                kb = x.cur.nbytes();
+                L.chunks.push_back(std::move(x.cur));
+                x.cur = std::move(fresh);
+            } else {           // its oldest k topics (the batch stays within max_topics)
+                Chunk& c = fresh;
+                const size_t h = x.cur.head;
+                kb = 0;
+                for (size_t j = 0; j < k; ++j) kb += x.cur.lens[h + j];
+                const uint8_t* b0 = x.cur.bytes.data() + x.cur.bhead;
+                c.bytes.assign(b0, b0 + kb);
+                c.lens.assign(x.cur.lens.begin() + h, x.cur.lens.begin() + h + k);
+                c.reqs.assign(x.cur.reqs.begin() + h, x.cur.reqs.begin() + h + k);
+                x.cur.head += k;
+                x.cur.bhead += kb;
+                x.cur.compact();
+                L.chunks.push_back(std::move(c));
+            }
+            n += k;
             // pending is counted under this lock: subtract while holding it;
             // topics left behind keep their stripe's first_ns (due at once)
-            x.pending.fetch_sub(t.lens.size(), std::memory_order_acq_rel);
-            x.pending_bytes.fetch_sub(t.bytes.size(), std::memory_order_relaxed);
-            if (x.lens.empty()) x.first_ns.store(INT64_MAX, std::memory_order_release);
+            x.pending.store(x.pending.load(std::memory_order_relaxed) - k, std::memory_order_release);
+            x.pending_bytes.store(x.pending_bytes.load(std::memory_order_relaxed) - kb, std::memory_order_relaxed);
+            if (x.cur.size() == 0) x.first_ns.store(INT64_MAX, std::memory_order_release);
         }
         L.n = (uint32_t)n;
-        if (host_only || !L.h_bytes.ensure(nb + 16) || !L.h_off.ensure((n + 1) * 8)) {
-            L.oom = !host_only;
-            for (auto& t : taken) {
-                t.bytes.clear();
-                t.lens.clear();
-            }
-            return;
-        }
+    }
+    void recycle_one(Chunk&& c) {
+        std::lock_guard<std::mutex> lk(pool_mu);
+        if (pool.size() < 4 * NSTRIPE) pool.push_back(std::move(c));
+    }
+
+    // the lane packs its chunks into pinned memory (bytes, offsets); false:
+    // staging memory ran out
+    bool pack(Lane& L) {
+        uint64_t nb = 0;
+        for (const Chunk& c : L.chunks) nb += c.nbytes();
+        if (!L.h_bytes.ensure(nb + 16) || !L.h_off.ensure(((uint64_t)L.n + 1) * 8)) return false;
         uint8_t* hb = (uint8_t*)L.h_bytes.p;
         uint64_t* ho = (uint64_t*)L.h_off.p;
         uint64_t o = 0, k = 0;
         ho[0] = 0;
-        for (int i = 0; i < NSTRIPE; ++i) {   // same stripe order as reqs
-            Taken& t = taken[(start + i) % NSTRIPE];
-            if (!t.bytes.empty()) std::memcpy(hb + o, t.bytes.data(), t.bytes.size());
-            for (uint32_t len : t.lens) {
-                o += len;
+        for (const Chunk& c : L.chunks) {
+            if (c.nbytes()) std::memcpy(hb + o, c.bytes.data() + c.bhead, c.nbytes());
+            for (size_t j = c.head; j < c.lens.size(); ++j) {
+                o += c.lens[j];
                 ho[++k] = o;
             }
-            t.bytes.clear();
-            t.lens.clear();
         }
+        return true;
     }
 
     // the lane's batch on its GPU; results in the lane's pinned buffers
@@ -298,9 +341,9 @@ struct tm_batcher {
             }
             const uint32_t n = L.n;
             uint64_t total = 0, results = 0;
-            int rc = L.oom ? TM_ENOMEM : host_only ? TM_EDEVICE : TM_OK;   // host-only: the GPU path only
+            int rc = host_only ? TM_EDEVICE : TM_OK;   // host-only: the GPU path only
             if (rc == TM_OK && n) {
-                rc = run_device(L, routes, deliv, total);
+                rc = pack(L) ? run_device(L, routes, deliv, total) : TM_ENOMEM;
                 if (rc == TM_OK)   // deliveries sit at route offsets: count the entries
                     for (uint32_t i = 0; i < n; ++i) results += ((const uint32_t*)L.h_counts.p)[i];
             }
@@ -308,15 +351,17 @@ struct tm_batcher {
             const uint64_t* off = (const uint64_t*)L.h_outoff.p;
             const uint32_t* src = (const uint32_t*)L.h_src.p;
             const uint32_t* dst = (const uint32_t*)L.h_dest.p;
-            const uint32_t m = (uint32_t)L.reqs.size();
-            for (uint32_t i = 0; i < m; ++i) {   // one batch's callbacks in submission order
-                const Req& r = L.reqs[i];
-                if (rc == TM_OK)
-                    r.fn(r.ctx, r.ticket, TM_OK, src + off[i], routes ? dst + off[i] : nullptr, cnt[i]);
-                else
-                    r.fn(r.ctx, r.ticket, rc, nullptr, nullptr, 0);
-            }
-            L.reqs.clear();
+            uint32_t i = 0;
+            for (const Chunk& c : L.chunks)   // one batch's callbacks in gather order
+                for (size_t j = c.head; j < c.reqs.size(); ++j, ++i) {
+                    const Req& r = c.reqs[j];
+                    if (rc == TM_OK)
+                        r.fn(r.ctx, r.ticket, TM_OK, src + off[i], routes ? dst + off[i] : nullptr, cnt[i]);
+                    else
+                        r.fn(r.ctx, r.ticket, rc, nullptr, nullptr, 0);
+                }
+            const uint32_t m = i;
+            recycle(L.chunks);
             {
                 std::lock_guard<std::mutex> lk(L.mu);
                 L.full = false;
@@ -465,11 +510,15 @@ int tm_batcher_submit(tm_batcher* b, const uint8_t* topic, uint32_t len, tm_batc
     {
         std::lock_guard<std::mutex> lk(s.mu);
         t = ++s.seq * NSTRIPE + (uint64_t)t_stripe;   // unique per batcher, no shared counter
-        s.bytes.insert(s.bytes.end(), topic, topic + len);
-        s.lens.push_back(len);
-        s.reqs.push_back(Req{fn, ctx, t});
-        s.pending_bytes.fetch_add(len, std::memory_order_relaxed);
-        was = s.pending.fetch_add(1, std::memory_order_seq_cst);
+        s.cur.bytes.insert(s.cur.bytes.end(), topic, topic + len);
+        s.cur.lens.push_back(len);
+        s.cur.reqs.push_back(Req{fn, ctx, t});
+        // the counters change only under the stripe lock: plain load + store
+        // (no read-modify-write per publish); the 0 -> 1 step is seq_cst for
+        // the sealer's idle hand-shake below
+        s.pending_bytes.store(s.pending_bytes.load(std::memory_order_relaxed) + len, std::memory_order_relaxed);
+        was = s.pending.load(std::memory_order_relaxed);
+        s.pending.store(was + 1, was == 0 ? std::memory_order_seq_cst : std::memory_order_release);
         if (was == 0) s.first_ns.store(b->now_ns(), std::memory_order_release);
     }
     // wake the sealer only when it sleeps with nothing pending (it times the

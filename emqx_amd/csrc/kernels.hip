@@ -246,6 +246,19 @@ struct Hit {
     bool have;                       // layout sends the struct to scratch)
 };
 
+// TM_NT_PROBE (A/B builds): edge-table loads below the hot top non-temporal
+#ifndef TM_NT_PROBE
+#define TM_NT_PROBE 0
+#endif
+typedef uint32_t u32x4_nt __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 nt_load16(const void* p) {
+    const u32x4_nt x = __builtin_nontemporal_load(reinterpret_cast<const u32x4_nt*>(p));
+    return make_uint4(x.x, x.y, x.z, x.w);
+}
+__device__ __forceinline__ void nt_store16(void* p, uint4 v) {
+    u32x4_nt x = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(x, reinterpret_cast<u32x4_nt*>(p));
+}
 // literal (or '#') edge (v, w) in the edge table: linear probing, one 16 B
 // key half per slot (load factor <= 1/4: ~1.2 loads per hit); on a hit the
 // slot's second half completes the child's record
@@ -257,7 +270,7 @@ __device__ __forceinline__ Hit probe_edge(const ImageView& im, uint32_t v, uint3
     uint64_t s = edge_home(v, w, mask);
     for (;;) {
         const uint4* slot = reinterpret_cast<const uint4*>(tab + s);
-        const uint4 e = slot[0];
+        const uint4 e = (TM_NT_PROBE && !hot) ? nt_load16(slot) : slot[0];
         if (STATS) ++loads;
         if (e.x == v && e.y == w) {
             if (!SLOT_RECORD) return Hit{e.z, 0, 0, 0, 0, 0, false};
@@ -288,8 +301,24 @@ __device__ __forceinline__ Hit lit_child(const ImageView& im, uint32_t v, uint32
     return none;   // WORD_NONE: bytes no filter contains
 }
 
-__device__ __forceinline__ uint4 load_half(const ImageView& im, uint32_t v, bool leaf) {
-    return *reinterpret_cast<const uint4*>((leaf ? im.leaf : im.inner) + ((uint64_t)v << im.node_shift));
+// Cache policy (A/B builds): TM_NT_LEVEL = d marks node loads at depth >= d
+// (and leaf halves) non-temporal, so deep, rarely re-used nodes do not push
+// the shared upper levels out of L2; TM_NT_STAGE marks the stage-row stores
+// non-temporal.  0 / unset: ordinary loads and stores.
+#ifndef TM_NT_LEVEL
+#define TM_NT_LEVEL 0
+#endif
+#ifndef TM_NT_STAGE
+#define TM_NT_STAGE 0
+#endif
+__device__ __forceinline__ uint4 load_half(const ImageView& im, uint32_t v, bool leaf, uint32_t r = 0) {
+    const uint4* p = reinterpret_cast<const uint4*>((leaf ? im.leaf : im.inner) + ((uint64_t)v << im.node_shift));
+    if (TM_NT_LEVEL > 0 && (leaf || r >= (uint32_t)TM_NT_LEVEL)) return nt_load16(p);
+    return *p;
+}
+__device__ __forceinline__ void store_stage(uint32_t* p, uint4 x) {
+    if (TM_NT_STAGE) nt_store16(p, x);
+    else *reinterpret_cast<uint4*>(p) = x;
 }
 
 // ---------------------------------------------------------------------------
@@ -406,7 +435,7 @@ __device__ __forceinline__ bool walk_step(const ImageView& im, Cursor& c, Path p
     uint32_t v = c.v, r = c.r;
     uint64_t key = KEYS ? c.key : 0ull;
     bool leaf = r == c.n;
-    const uint4 h = load_half(im, v, leaf);   // inner {plus, hf, lw, lc} / leaf {sf, hf, hash, pad}
+    const uint4 h = load_half(im, v, leaf, r);   // inner {plus, hf, lw, lc} / leaf {sf, hf, hash, pad}
     uint32_t plus = h.x, hf = h.y, lw = h.z, lc = h.w, sf = h.x;
     for (;;) {
         if (STATS) {
@@ -529,12 +558,12 @@ struct RowEmit {
             buf.z = s == 1 ? f : buf.z;
             buf.y = s == 2 ? f : buf.y;
             buf.x = s == 3 ? f : buf.x;
-            if (s == 3) *reinterpret_cast<uint4*>(row + K - 4 - (cnt & ~3u)) = buf;
+            if (s == 3) store_stage(row + K - 4 - (cnt & ~3u), buf);
         }
         ++cnt;
     }
     __device__ __forceinline__ void flush() {
-        if ((cnt & 3u) && cnt < K) *reinterpret_cast<uint4*>(row + K - 4 - (cnt & ~3u)) = buf;
+        if ((cnt & 3u) && cnt < K) store_stage(row + K - 4 - (cnt & ~3u), buf);
         if (KEYS && (cnt & 1u) && cnt <= K) krow[K - cnt] = kb;   // the unpaired last even discovery
     }
 };

@@ -148,6 +148,10 @@ def test_c4_100m_filters_sharded_8_vs_replicated(gpu_device, capsys):
 
     def build_rep():
         e = Engine(device=gpu_device, filters_hint=n_f)
+        # the whole-set reference side keeps insertion order (no relayout of
+        # its 252M nodes: the long pole of this test); layout variants are
+        # parity-tested against O1 in test_gpu_parity.py
+        e.set_option("layout", 0)
         e.insert_many(fb, fo)
         e.commit()
         box["rep"] = e

@@ -16,8 +16,8 @@ OUT=gpurun_out/${TAG:-job}
 mkdir -p "$OUT"
 for s in ${STEPS:-tests}; do
   case $s in
-    tests) timeout -k 10 ${T_TESTS:-900} python -u -m pytest ${TESTS:-tests} -m gpu -x -v --durations=20 \
-             --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1 ;;
+    tests) timeout -k 10 ${T_TESTS:-1500} python -u -m pytest ${TESTS:-tests} -m gpu -x -v --durations=20 \
+             --timeout ${T_TEST1:-420} --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1 ;;
     smoke) timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 ;;
     bench) timeout -k 10 ${T_BENCH:-600} python -u bench.py ${BENCH_ARGS} > "$OUT/bench.json" 2> "$OUT/bench.log" ;;
     prof)  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
