@@ -87,6 +87,15 @@ def parse():
     return ap.parse_args()
 
 
+def kernel_src_sha():
+    """hash of the walk's sources (as tools/traffic.py records it with the PMC passes)"""
+    import hashlib
+    h = hashlib.sha256()
+    for f in ("kernels.hip", "image.h", "kernels.h"):
+        h.update(open(os.path.join(ROOT, "emqx_amd", "csrc", f), "rb").read())
+    return h.hexdigest()[:16]
+
+
 def cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -375,7 +384,9 @@ def main():
         if os.path.exists(tpath) and kname == "walk":
             tj = json.load(open(tpath))
             tc = tj.get("config") or {}
-            if tc.get("filters") == n_filters and tc.get("topics_per_gpu_step") == n0 and tc.get("levels") == cfg["levels"]:
+            same_kernel = tj.get("kernel_src_sha") == kernel_src_sha()
+            if same_kernel and tc.get("filters") == n_filters and tc.get("topics_per_gpu_step") == n0 and \
+                    tc.get("levels") == cfg["levels"]:
                 traffic = tj["traffic_bytes_per_launch"] / (walk_ms * 1e-3) / 1e9
         out = {
             "metric": METRIC,
@@ -401,8 +412,9 @@ def main():
                        "parallelism": "replicated trie x %d, topic batch split by rank" % world},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
-                         "traffic_source": ("FETCH_SIZE+WRITE_SIZE per launch, profiles/traffic_c%d.json, over this "
-                                            "run's walk time" % a.config) if traffic else None,
+                         "traffic_source": ("FETCH_SIZE+WRITE_SIZE per launch from the PMC passes of the same kernel "
+                                            "sources (profiles/traffic_c%d.json, kernel_src_sha %s), over this run's "
+                                            "walk time" % (a.config, kernel_src_sha())) if traffic else None,
                          "kernel": {"walk": "tm_walk_queue (balanced NFA walk, one 16 B node-half load per step)"
                                     }.get(kname, kname),
                          "kernel_ms": walk_ms,

@@ -309,7 +309,7 @@ __device__ __forceinline__ Hit lit_child(const ImageView& im, uint32_t v, uint32
 #define TM_NT_LEVEL 0
 #endif
 #ifndef TM_NT_STAGE
-#define TM_NT_STAGE 0
+#define TM_NT_STAGE 1   // A/B at C3: walk 12.18-12.22 vs 12.37-12.59 ms (profiles/r02_ab/ab_nt.jsonl)
 #endif
 __device__ __forceinline__ uint4 load_half(const ImageView& im, uint32_t v, bool leaf, uint32_t r = 0) {
     const uint4* p = reinterpret_cast<const uint4*>((leaf ? im.leaf : im.inner) + ((uint64_t)v << im.node_shift));
@@ -339,7 +339,23 @@ constexpr int HIST_OFF = 8;   // hist = stats + HIST_OFF
 struct Cursor {
     uint32_t v, r, n, r0;   // node to visit next and its level; topic levels; start level
     uint64_t key;           // KEYS: fold branches taken above level r (rank_sym), key word 0
+    uint32_t pf, pfr;       // PF: '+' child to prefetch with the next load (NODE_NONE: none), its level slot
+    bool rec;               // PF: the node to visit next has its half in the record slot of level r - 1
 };
+
+// '+'-child prefetch (TM_PF_LEVELS = L > 0; 0 = off).  Descending into a
+// literal child at level r < L while a '+' child p stays pending, the next
+// step loads p's half beside the literal child's and keeps it in an LDS
+// record slot of level r; the pop to p later visits it from LDS.  p sits
+// right after its parent in the heat layout, so its line is usually the one
+// the parent's visit just brought into L2, while at pop time -- after the
+// whole literal subtree -- it has mostly been evicted: the prefetch turns a
+// fabric request into an L2 hit.  Path entries of such levels carry PF_BIT.
+#ifndef TM_PF_LEVELS
+#define TM_PF_LEVELS 0
+#endif
+constexpr uint32_t PF_LEVELS = TM_PF_LEVELS;
+constexpr uint32_t PF_BIT = 0x80000000u;
 
 // Order keys (sharded mode).  Every match of a topic is identified by the
 // branches the reference's fold took to discover it: at level i 'match_#'
@@ -393,13 +409,20 @@ struct MemWords {
     __device__ __forceinline__ uint32_t operator()(uint32_t r) const { return r < WREG ? tw[r] : lw[r]; }
 };
 
-struct LdsPath {
+template <bool WITH_PF>
+struct LdsPathT {
     uint32_t* base;   // [level][BLOCK]
+    uint4* recs;      // PF: [level < PF_LEVELS][BLOCK] prefetched '+'-child halves
+    static constexpr bool PF = WITH_PF && PF_LEVELS > 0;
     __device__ __forceinline__ uint32_t& operator()(uint32_t r) const { return base[r * BLOCK]; }
+    __device__ __forceinline__ uint4& rec(uint32_t r) const { return recs[r * BLOCK]; }
 };
+using LdsPath = LdsPathT<false>;   // re-walks: no prefetch records
 struct GlobalPath {
     uint32_t* base;
+    static constexpr bool PF = false;
     __device__ __forceinline__ uint32_t& operator()(uint32_t r) const { return base[r]; }
+    __device__ __forceinline__ uint4& rec(uint32_t) const { return *reinterpret_cast<uint4*>(base); }   // unused
 };
 
 // '$' rule (emqx_trie.erl:121-122): a topic whose first word starts with '$'
@@ -410,6 +433,9 @@ __device__ __forceinline__ bool walk_begin(const ImageView& im, Cursor& c, uint3
                                            WalkStats& st) {
     c.n = n;
     c.key = 0;
+    c.pf = NODE_NONE;
+    c.pfr = 0;
+    c.rec = false;
     if (!dollar) {
         c.v = ROOT;
         c.r = c.r0 = 0;
@@ -435,7 +461,18 @@ __device__ __forceinline__ bool walk_step(const ImageView& im, Cursor& c, Path p
     uint32_t v = c.v, r = c.r;
     uint64_t key = KEYS ? c.key : 0ull;
     bool leaf = r == c.n;
-    const uint4 h = load_half(im, v, leaf, r);   // inner {plus, hf, lw, lc} / leaf {sf, hf, hash, pad}
+    constexpr bool PF = Path::PF && !STATS;
+    uint4 h;   // inner {plus, hf, lw, lc} / leaf {sf, hf, hash, pad}
+    if (PF && c.rec) {
+        h = path.rec(r - 1);
+        c.rec = false;
+    } else {
+        h = load_half(im, v, leaf, r);
+    }
+    if (PF && c.pf != NODE_NONE) {   // beside this step's load: the pending '+' child of level pfr
+        path.rec(c.pfr) = load_half(im, c.pf, c.pfr + 1 == c.n, c.pfr + 1);
+        c.pf = NODE_NONE;
+    }
     uint32_t plus = h.x, hf = h.y, lw = h.z, lc = h.w, sf = h.x;
     for (;;) {
         if (STATS) {
@@ -477,7 +514,12 @@ __device__ __forceinline__ bool walk_step(const ImageView& im, Cursor& c, Path p
             else if ((plus & NODE_MASK) != NODE_NONE) atomicAdd(st.hist + 50, 1ull);
         }
         if (g.child != NODE_NONE) {   // literal subtree first, '+' child pending at level r
-            path(r) = KEYS ? (pc | SYM_LIT) : pc;
+            const bool pf = PF && pc != NODE_NONE && r < PF_LEVELS && c.pf == NODE_NONE;
+            path(r) = (KEYS ? (pc | SYM_LIT) : pc) | (pf ? PF_BIT : 0u);
+            if (pf) {
+                c.pf = pc;
+                c.pfr = r;
+            }
             v = g.child;
             if (KEYS) key |= rank_sym(r, 1);
             ++r;
@@ -506,12 +548,14 @@ __device__ __forceinline__ bool walk_step(const ImageView& im, Cursor& c, Path p
     }
     for (uint32_t k = r; k > c.r0;) {   // pop to the deepest pending '+' child
         --k;
-        const uint32_t p = KEYS ? path(k) & NODE_MASK : path(k);
+        const uint32_t raw = path(k);
+        const uint32_t p = raw & NODE_MASK;
         if (p != NODE_NONE) {
             if (STATS && st.hist) atomicAdd(st.hist + 50, 1ull);
             path(k) = KEYS ? (NODE_NONE | SYM_PLUS) : NODE_NONE;
             c.v = p;
             c.r = k + 1;
+            if (PF) c.rec = (raw & PF_BIT) != 0;
             if (KEYS) c.key = rank_prefix(key, k) | rank_sym(k, 2);
             return false;
         }
@@ -637,8 +681,14 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
               unsigned long long* __restrict__ hist, const uint32_t* __restrict__ perm,
               const uint32_t* __restrict__ twords_s, const uint32_t* __restrict__ meta_s) {
     __shared__ uint32_t lds_path[WREG * BLOCK];
+#if TM_PF_LEVELS > 0
+    __shared__ uint4 lds_rec[PF_LEVELS * BLOCK];
+    uint4* const recs = lds_rec + threadIdx.x;
+#else
+    uint4* const recs = nullptr;
+#endif
     const uint32_t lane = threadIdx.x & 63;
-    const LdsPath lp{lds_path + threadIdx.x};
+    const LdsPathT<true> lp{lds_path + threadIdx.x, recs};
     GlobalPath gp{nullptr};
     RegWords rw;
     MemWords mw{nullptr, nullptr};
@@ -819,7 +869,33 @@ tm_copy_out(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const ui
         // (no per-id search); output j of a topic with ct ids is row slot
         // K-ct+j, staged for j >= ct-K
         const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-        for (uint32_t lt = w; lt < tn; lt += BLOCK / 64) {
+        uint32_t lt0 = w;
+        if (!KEYS) {
+            // CU topics per wave at a time, each list of <= 64 staged ids one
+            // load per lane: the CU row loads are in flight together (one
+            // dependent load per topic would leave the wave waiting on each)
+            constexpr uint32_t CU = 4, WS = BLOCK / 64;
+            for (; lt0 + WS * (CU - 1) < tn; lt0 += WS * CU) {
+                uint32_t v[CU];
+                uint64_t dst[CU];
+                bool ok[CU], easy = true;
+#pragma unroll
+                for (uint32_t u = 0; u < CU; ++u) {
+                    const uint32_t lt = lt0 + WS * u;
+                    const uint32_t prev = lt ? lds_inc[lt - 1] : 0u;
+                    const uint32_t ct = lds_inc[lt] - prev;
+                    easy = easy && ct <= 64u && ct <= K;
+                    dst[u] = base + prev + lane;
+                    ok[u] = lane < ct && ct <= K && dst[u] < out_cap;   // (a row slot, never before the row)
+                    v[u] = ok[u] ? stage[(uint64_t)(t0 + lt) * K + K - ct + lane] : 0u;
+                }
+                if (!__all(easy)) break;   // (uniform) a long list: the general loop from here
+#pragma unroll
+                for (uint32_t u = 0; u < CU; ++u)
+                    if (ok[u]) out[dst[u]] = v[u];
+            }
+        }
+        for (uint32_t lt = lt0; lt < tn; lt += BLOCK / 64) {
             const uint32_t prev = lt ? lds_inc[lt - 1] : 0u;
             const uint32_t ct = lds_inc[lt] - prev;
             const uint64_t ob = base + prev;
@@ -859,7 +935,7 @@ tm_copy_out(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const ui
         if (mt & MLONG)
             walk<false, KEYS>(im, mt & MN, (mt & MDOLLAR) != 0, GlobalPath{gpath + b + 2ull * t}, mw, em, s2);
         else
-            walk<false, KEYS>(im, mt & MN, (mt & MDOLLAR) != 0, LdsPath{lds_path + threadIdx.x}, mw, em, s2);
+            walk<false, KEYS>(im, mt & MN, (mt & MDOLLAR) != 0, LdsPath{lds_path + threadIdx.x, nullptr}, mw, em, s2);
     }
 }
 
@@ -914,7 +990,7 @@ tm_copy_out_sorted(ImageView im, const uint64_t* __restrict__ off, uint32_t n, c
         if (mt & MLONG)
             walk<false, KEYS>(im, mt & MN, (mt & MDOLLAR) != 0, GlobalPath{gpath + b + 2ull * t}, mw, em, s2);
         else
-            walk<false, KEYS>(im, mt & MN, (mt & MDOLLAR) != 0, LdsPath{lds_path + threadIdx.x}, mw, em, s2);
+            walk<false, KEYS>(im, mt & MN, (mt & MDOLLAR) != 0, LdsPath{lds_path + threadIdx.x, nullptr}, mw, em, s2);
     }
 }
 

@@ -12,9 +12,22 @@ FETCH_SIZE each), so FETCH_SIZE is taken as is.
 
 usage: python tools/traffic.py gpurun_out/pmc_x profiles/traffic_c3.json
 """
+import hashlib
 import json
+import os
 import subprocess
 import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def kernel_src_sha():
+    """hash of the walk's sources: bench.py reports the traffic only for the same kernel"""
+    h = hashlib.sha256()
+    for f in ("kernels.hip", "image.h", "kernels.h"):
+        h.update(open(os.path.join(ROOT, "emqx_amd", "csrc", f), "rb").read())
+    return h.hexdigest()[:16]
+
 
 src, dst = sys.argv[1], sys.argv[2]
 summ = json.load(open(src + "/summary.json"))
@@ -35,6 +48,7 @@ out = {
                   "(profiles/r02_gather/gather_pmc.json)",
     "source": src,
     "build": rev,
+    "kernel_src_sha": kernel_src_sha(),
 }
 json.dump(out, open(dst, "w"), indent=1)
 print(json.dumps(out, indent=1))
