@@ -43,6 +43,8 @@ from emqx_amd import multi  # noqa: E402
 from emqx_amd import workload as W  # noqa: E402
 
 METRIC = "topic matches/sec (whole node) at 10M wildcard filters; % HBM roofline"
+# micro-batcher leg: the best point of tools/bench_batcher.py (profiles/r02_ab)
+BATCHER = {"producers": 16, "deadline_us": 200, "max_topics": 262144, "lanes_per_replica": 4, "callback_threads": 0}
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak, /opt/skills/guides/MI355X_MICROARCH.md
 
 
@@ -475,19 +477,17 @@ def host_legs(a, eng, batch, total):
         drv.tm_bench_batcher.restype = ctypes.c_int
         drv.tm_bench_batcher.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
                                          ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
-                                         ctypes.c_uint32, ctypes.POINTER(ctypes.c_double)]
+                                         ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_double)]
         k = n   # the whole batch, after a warm-up run inside the driver
         res = (ctypes.c_double * 8)()
-        # 4 lanes, batches up to 256K topics: the best point of tools/bench_batcher.py
-        # (profiles/r02_misc/batcher_sweep.md)
-        rc = drv.tm_bench_batcher(eng.h, tb.ctypes.data, to.ctypes.data, k, 16, 200, 262144, 4, 0, res)
+        bc = BATCHER
+        rc = drv.tm_bench_batcher(eng.h, tb.ctypes.data, to.ctypes.data, k, bc["producers"], bc["deadline_us"],
+                                  bc["max_topics"], bc["lanes_per_replica"], 0, bc["callback_threads"], res)
         if rc == 0:
-            out["batcher"] = {"topics_per_s": res[1], "topics": k, "producers": 16, "deadline_us": 200,
-                              "max_topics": 262144, "lanes_per_replica": 4, "batches": int(res[2]),
-                              "mean_batch": res[3],
-                              "lat_us_p50": res[4], "lat_us_p99": res[5], "failed": int(res[6]),
-                              "matches": int(res[7]),
-                              "path": "tm_batcher_submit per publish from 16 threads, per-topic callbacks (NIF path)"}
+            out["batcher"] = dict(bc, topics_per_s=res[1], topics=k, batches=int(res[2]), mean_batch=res[3],
+                                  lat_us_p50=res[4], lat_us_p99=res[5], failed=int(res[6]), matches=int(res[7]),
+                                  path="tm_batcher_submit per publish from %d threads, per-topic callbacks "
+                                       "(NIF path), PCIe both ways included" % bc["producers"])
             log("batcher: %.0f topics/s, mean batch %.0f, p50 %.0f us, p99 %.0f us" % (res[1], res[3], res[4],
                                                                                      res[5]))
     return out

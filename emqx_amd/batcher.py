@@ -13,11 +13,11 @@ from . import _lib as L
 
 class Batcher:
     def __init__(self, engine, max_topics=65536, deadline_us=200, max_bytes=0, routes=False, deliveries=False,
-                 lanes_per_replica=0):
+                 lanes_per_replica=0, callback_threads=0):
         self.engine = engine
         self.lib = engine.lib
         flags = (L.TM_BATCHER_ROUTES if routes else 0) | (L.TM_BATCHER_DELIVERIES if deliveries else 0)
-        cfg = L.TmBatcherConfig(max_topics, deadline_us, max_bytes, flags, lanes_per_replica)
+        cfg = L.TmBatcherConfig(max_topics, deadline_us, max_bytes, flags, lanes_per_replica, callback_threads)
         h = ctypes.c_void_p()
         rc = self.lib.tm_batcher_open(engine.h, ctypes.byref(cfg), ctypes.byref(h))
         if rc != L.TM_OK:

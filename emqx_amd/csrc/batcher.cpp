@@ -31,6 +31,7 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <deque>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -137,6 +138,8 @@ struct Lane {
     bool full = false, stop = false;   // a batch has been handed over / shut down
     uint32_t n = 0;
     std::vector<Chunk> chunks;        // the batch: stripe chunks in gather order
+    std::condition_variable cb_cv;    // callback parts still running on the callback threads (under mu)
+    uint32_t cb_left = 0;
     Pinned h_bytes, h_off, h_counts, h_outoff, h_src, h_dest, h_total;
     Dev d_bytes, d_off, d_counts, d_outoff, d_src, d_dest, d_total;
     double ids_per_topic = 64.0;      // sizing estimate of the device result buffers
@@ -165,6 +168,18 @@ struct tm_batcher {
     std::vector<int> free_lanes;      // guarded by mu
     uint64_t rotate = 0;              // first stripe of the next gather (sealer only)
     uint64_t next_lane = 0;
+
+    struct CbJob {
+        Lane* L;
+        int rc;
+        bool routes;
+        uint32_t lo, hi;
+    };
+    std::mutex cb_mu;                 // callback threads: parts of lanes' batches
+    std::condition_variable cb_cv;
+    std::deque<CbJob> cb_q;
+    bool cb_stop = false;
+    std::vector<std::thread> cb_threads;
 
     std::mutex pool_mu;               // emptied chunks (capacity kept) for the stripes
     std::vector<Chunk> pool;
@@ -328,6 +343,73 @@ struct tm_batcher {
         return TM_OK;
     }
 
+    // callbacks of topics [lo, hi) of lane L's batch (gather order)
+    void callbacks(const Lane& L, int rc, bool routes, uint32_t lo, uint32_t hi) {
+        const uint32_t* cnt = (const uint32_t*)L.h_counts.p;
+        const uint64_t* off = (const uint64_t*)L.h_outoff.p;
+        const uint32_t* src = (const uint32_t*)L.h_src.p;
+        const uint32_t* dst = (const uint32_t*)L.h_dest.p;
+        uint32_t i = 0;
+        for (const Chunk& c : L.chunks) {
+            const uint32_t cn = (uint32_t)c.size();
+            if (i + cn <= lo) {
+                i += cn;
+                continue;
+            }
+            for (size_t j = c.head + (lo > i ? lo - i : 0u); j < c.reqs.size() && i + (j - c.head) < hi; ++j) {
+                const uint32_t k = i + (uint32_t)(j - c.head);
+                const Req& r = c.reqs[j];
+                if (rc == TM_OK)
+                    r.fn(r.ctx, r.ticket, TM_OK, src + off[k], routes ? dst + off[k] : nullptr, cnt[k]);
+                else
+                    r.fn(r.ctx, r.ticket, rc, nullptr, nullptr, 0);
+            }
+            i += cn;
+            if (i >= hi) break;
+        }
+    }
+
+    // a batch's callbacks: on the lane, or cut into parts of >= CB_MIN topics
+    // shared with the callback threads (the lane takes part 0 and waits for
+    // the rest: its buffers are reused by the next batch)
+    static constexpr uint32_t CB_MIN = 8192;
+    void run_callbacks(Lane& L, int rc, bool routes, uint32_t m) {
+        const uint32_t parts = std::min<uint32_t>((uint32_t)cb_threads.size() + 1, std::max<uint32_t>(1, m / CB_MIN));
+        if (parts <= 1) {
+            callbacks(L, rc, routes, 0, m);
+            return;
+        }
+        {
+            std::lock_guard<std::mutex> lk(L.mu);
+            L.cb_left = parts - 1;
+        }
+        {
+            std::lock_guard<std::mutex> lk(cb_mu);
+            for (uint32_t p = 1; p < parts; ++p)
+                cb_q.push_back(CbJob{&L, rc, routes, (uint32_t)((uint64_t)m * p / parts),
+                                     (uint32_t)((uint64_t)m * (p + 1) / parts)});
+        }
+        cb_cv.notify_all();
+        callbacks(L, rc, routes, 0, (uint32_t)((uint64_t)m / parts));
+        std::unique_lock<std::mutex> lk(L.mu);
+        L.cb_cv.wait(lk, [&] { return L.cb_left == 0; });
+    }
+    void cb_loop() {
+        for (;;) {
+            CbJob j;
+            {
+                std::unique_lock<std::mutex> lk(cb_mu);
+                cb_cv.wait(lk, [&] { return cb_stop || !cb_q.empty(); });
+                if (cb_q.empty()) return;
+                j = cb_q.front();
+                cb_q.pop_front();
+            }
+            callbacks(*j.L, j.rc, j.routes, j.lo, j.hi);
+            std::lock_guard<std::mutex> lk(j.L->mu);
+            if (--j.L->cb_left == 0) j.L->cb_cv.notify_all();
+        }
+    }
+
     // lane worker: run handed-over batches and their callbacks
     void lane_loop(Lane& L, int idx) {
         if (L.device >= 0) (void)hipSetDevice(L.device);
@@ -347,20 +429,8 @@ struct tm_batcher {
                 if (rc == TM_OK)   // deliveries sit at route offsets: count the entries
                     for (uint32_t i = 0; i < n; ++i) results += ((const uint32_t*)L.h_counts.p)[i];
             }
-            const uint32_t* cnt = (const uint32_t*)L.h_counts.p;
-            const uint64_t* off = (const uint64_t*)L.h_outoff.p;
-            const uint32_t* src = (const uint32_t*)L.h_src.p;
-            const uint32_t* dst = (const uint32_t*)L.h_dest.p;
-            uint32_t i = 0;
-            for (const Chunk& c : L.chunks)   // one batch's callbacks in gather order
-                for (size_t j = c.head; j < c.reqs.size(); ++j, ++i) {
-                    const Req& r = c.reqs[j];
-                    if (rc == TM_OK)
-                        r.fn(r.ctx, r.ticket, TM_OK, src + off[i], routes ? dst + off[i] : nullptr, cnt[i]);
-                    else
-                        r.fn(r.ctx, r.ticket, rc, nullptr, nullptr, 0);
-                }
-            const uint32_t m = i;
+            const uint32_t m = n;
+            run_callbacks(L, rc, routes, m);
             recycle(L.chunks);
             {
                 std::lock_guard<std::mutex> lk(L.mu);
@@ -434,7 +504,7 @@ struct tm_batcher {
         cv_work.notify_one();
     }
 
-    void shutdown_lanes() {
+    void shutdown_lanes() {   // lanes first: a lane mid-batch may wait on the callback threads
         for (auto& L : lanes) {
             {
                 std::lock_guard<std::mutex> lk(L->mu);
@@ -447,6 +517,13 @@ struct tm_batcher {
                 (void)hipStreamDestroy(L->stream);
             }
         }
+        {
+            std::lock_guard<std::mutex> lk(cb_mu);
+            cb_stop = true;
+        }
+        cb_cv.notify_all();
+        for (auto& t : cb_threads)
+            if (t.joinable()) t.join();
     }
 };
 
@@ -491,6 +568,8 @@ int tm_batcher_open(tm_engine* e, const tm_batcher_config* cfg, tm_batcher** out
             b->free_lanes.push_back((int)(b->lanes.size() - 1 - k));   // lane 0 first
             b->lanes[k]->th = std::thread([b, k] { b->lane_loop(*b->lanes[k], (int)k); });
         }
+        for (uint32_t k = 0; k < std::min<uint32_t>(b->cfg.callback_threads, 256u); ++k)
+            b->cb_threads.emplace_back([b] { b->cb_loop(); });
         b->worker = std::thread([b] { b->loop(); });
     } catch (...) {
         b->shutdown_lanes();

@@ -178,12 +178,19 @@ __device__ __forceinline__ uint32_t presort_key(const uint32_t (&tw)[WREG], uint
     return k;
 }
 
+// option "xbucket": the walk bucket (XCD) of a topic, a hash of its first
+// xlev words (1 or 2)
+__device__ __forceinline__ uint32_t xbucket_of(const uint32_t (&tw)[WREG], uint32_t xlev) {
+    const uint32_t h = tw[0] * 0x9E3779B1u ^ (xlev > 1 ? tw[1] * 0x85EBCA77u : 0u);
+    return (h ^ (h >> 15)) * 0x2C1B3C6Du >> 29;
+}
+
 template <class B>
-__device__ __forceinline__ void tokenize_one(const ImageView& im, const B& bytes,
-                                             const uint64_t* __restrict__ off, uint32_t t,
-                                             uint32_t* __restrict__ twords, uint32_t* __restrict__ words,
-                                             uint32_t* __restrict__ meta, uint32_t* __restrict__ skeys,
-                                             uint32_t* __restrict__ svals) {
+__device__ __forceinline__ uint32_t tokenize_one(const ImageView& im, const B& bytes,
+                                                 const uint64_t* __restrict__ off, uint32_t t,
+                                                 uint32_t* __restrict__ twords, uint32_t* __restrict__ words,
+                                                 uint32_t* __restrict__ meta, uint32_t* __restrict__ skeys,
+                                                 uint32_t* __restrict__ svals, uint32_t xlev) {
     const uint64_t b = off[t], e = off[t + 1];
     uint32_t tw[WREG];
 #pragma unroll
@@ -201,12 +208,14 @@ __device__ __forceinline__ void tokenize_one(const ImageView& im, const B& bytes
         skeys[t] = presort_key(tw, lev);
         svals[t] = t;
     }
+    return xlev ? xbucket_of(tw, xlev) : 0u;
 }
 
 __global__ void __launch_bounds__(BLOCK)
 tm_tokenize(ImageView im, const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint32_t n,
             uint32_t* __restrict__ twords, uint32_t* __restrict__ words, uint32_t* __restrict__ meta,
-            uint32_t* __restrict__ skeys, uint32_t* __restrict__ svals) {
+            uint32_t* __restrict__ skeys, uint32_t* __restrict__ svals, uint32_t* __restrict__ xlist,
+            uint32_t* __restrict__ xcnt, uint32_t xlev) {
     __shared__ uint64_t win[BLOCK / 64][TOK_WIN_WORDS];
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -226,11 +235,28 @@ tm_tokenize(ImageView im, const uint8_t* __restrict__ bytes, const uint64_t* __r
                 win[wv][k] = *reinterpret_cast<const uint64_t*>(bytes + wbase + 8 * k);
     }
     __syncthreads();
+    uint32_t bk = 0;
     if (t < n) {
         if (lds)
-            tokenize_one(im, LdsBytes{win[wv], wbase}, off, t, twords, words, meta, skeys, svals);
+            bk = tokenize_one(im, LdsBytes{win[wv], wbase}, off, t, twords, words, meta, skeys, svals, xlev);
         else
-            tokenize_one(im, GlobalBytes{bytes}, off, t, twords, words, meta, skeys, svals);
+            bk = tokenize_one(im, GlobalBytes{bytes}, off, t, twords, words, meta, skeys, svals, xlev);
+    }
+    if (xlist) {   // option "xbucket": append t to its bucket, one atomic per (wave, bucket)
+        const bool act = t < n;
+        uint64_t rem = __ballot(act);
+        while (rem) {
+            const uint32_t leader = (uint32_t)(__ffsll((long long)rem) - 1);
+            const uint32_t bl = __shfl(bk, leader, 64);
+            const uint64_t m = __ballot(act && bk == bl);
+            uint32_t base = 0;
+            if (lane == leader) base = atomicAdd(xcnt + bl, (uint32_t)__popcll(m));
+            base = __shfl(base, leader, 64);
+            if (act && bk == bl)
+                xlist[(uint64_t)bl * n + base +
+                      __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = t;
+            rem &= ~m;
+        }
     }
 }
 
@@ -679,7 +705,8 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
               uint32_t* __restrict__ counts,
               unsigned long long* __restrict__ ws, unsigned long long* __restrict__ stats,
               unsigned long long* __restrict__ hist, const uint32_t* __restrict__ perm,
-              const uint32_t* __restrict__ twords_s, const uint32_t* __restrict__ meta_s) {
+              const uint32_t* __restrict__ twords_s, const uint32_t* __restrict__ meta_s,
+              const uint32_t* __restrict__ xlist) {
     __shared__ uint32_t lds_path[WREG * BLOCK];
 #if TM_PF_LEVELS > 0
     __shared__ uint4 lds_rec[PF_LEVELS * BLOCK];
@@ -717,8 +744,10 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
                 if (XCDQ) {
                     while (qr < QRANGES) {
                         const uint32_t r = (home + qr) & (QRANGES - 1);
-                        const uint32_t rb = (uint32_t)((uint64_t)n * r / QRANGES);
-                        const uint32_t re = (uint32_t)((uint64_t)n * (r + 1) / QRANGES);
+                        // xbucket: range r = bucket r's list; else the r-th eighth of the batch
+                        const uint32_t rb = xlist ? r * n : (uint32_t)((uint64_t)n * r / QRANGES);
+                        const uint32_t re = xlist ? r * n + reinterpret_cast<const uint32_t*>(ws + QWS_XCNT)[r]
+                                                  : (uint32_t)((uint64_t)n * (r + 1) / QRANGES);
                         uint32_t x = 0;
                         if (lane == leader)
                             x = (uint32_t)__hip_atomic_fetch_add(ws + 16 * r, (unsigned long long)QCHUNK,
@@ -753,19 +782,21 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
                 if (rank < avail) i = qnext + rank;
                 else if (g + (rank - avail) < gend) i = g + (rank - avail);
                 if (i != NO_TOPIC) {
-                    // i: queue position = stage row; ti: the topic
-                    const uint32_t ti = perm ? perm[i] : i;
+                    // i: queue position; ti: the topic; ri: its row (rows and stage
+                    // rows are in walk order with perm, in topic order otherwise)
+                    const uint32_t ti = XCDQ && xlist ? xlist[i] : perm ? perm[i] : i;
+                    const uint32_t ri = XCDQ && xlist ? ti : i;
                     const uint32_t* tws = perm ? twords_s : twords;
-                    const uint32_t mt = perm ? meta_s[i] : meta[i];
+                    const uint32_t mt = perm ? meta_s[i] : meta[ri];
                     const uint32_t nl = mt & MN;
                     const bool dollar = (mt & MDOLLAR) != 0;
                     lev_sum += nl;
                     if (KEYS) maxl = nl > maxl ? nl : maxl;
                     is_long = (mt & MLONG) != 0;
-                    em.row = stage + (uint64_t)i * K;
-                    if (KEYS) em.krow = kstage + (uint64_t)i * K;
+                    em.row = stage + (uint64_t)ri * K;
+                    if (KEYS) em.krow = kstage + (uint64_t)ri * K;
                     em.cnt = 0;
-                    const uint32_t* tw = tws + (uint64_t)i * WREG;
+                    const uint32_t* tw = tws + (uint64_t)ri * WREG;
                     bool go;
                     if (!is_long) {
 #pragma unroll
@@ -1164,8 +1195,10 @@ hipError_t launch_queue(bool stats_mode, bool xcdq, const ImageView& im, const u
     if (err != hipSuccess) return err;
     dim3 blk(BLOCK), g(div_up(n, BLOCK));
     mark(0);
+    const bool xb = xcdq && qb.xlist && !qb.perm && n <= (1u << 28);   // option "xbucket" (8n positions in u32)
     hipLaunchKernelGGL(tm_tokenize, g, blk, 0, st, im, bytes, off, n, qb.twords, qb.words, qb.meta,
-                       qb.perm ? qb.sort_keys : nullptr, qb.perm ? qb.perm : nullptr);
+                       qb.perm ? qb.sort_keys : nullptr, qb.perm ? qb.perm : nullptr, xb ? qb.xlist : nullptr,
+                       reinterpret_cast<uint32_t*>(qb.ws + QWS_XCNT), xb ? qb.xlev : 0u);
     if (qb.perm) {   // option "presort": perm and the rows in walk order (presort.hip)
         err = launch_presort(qb.twords, qb.meta, n, qb, st);
         if (err != hipSuccess) return err;
@@ -1177,7 +1210,7 @@ hipError_t launch_queue(bool stats_mode, bool xcdq, const ImageView& im, const u
 #define TM_Q(S, X, Y)                                                                                              \
     hipLaunchKernelGGL((tm_walk_queue<S, X, Y>), dim3(wg), blk, 0, st, im, off, n, qb.twords, qb.words, qb.meta, \
                        qb.path, qb.stage, qb.kstage, K, key_words, counts, qb.ws, stats,                         \
-                       hist ? stats + HIST_OFF : nullptr, qb.perm, qb.twords_s, qb.meta_s)
+                       hist ? stats + HIST_OFF : nullptr, qb.perm, qb.twords_s, qb.meta_s, xb ? qb.xlist : nullptr)
     if (keys) {
         if (stats_mode) TM_Q(true, true, true); else TM_Q(false, true, true);
     } else if (stats_mode) {

@@ -382,7 +382,9 @@ int tm_match_deliveries_batch_device(tm_engine* e, const uint8_t* d_topic_bytes,
  * runs its batch (match/1, or match_routes/1 with TM_BATCHER_ROUTES, or
  * aggre(match_routes/1) with TM_BATCHER_DELIVERIES), reads back exactly the
  * results, and calls done() once per topic of the batch, in submission
- * order, from the lane's thread; different batches complete independently
+ * order, from the lane's thread (or, with callback_threads, from the lane and
+ * those threads, each part of the batch in submission order); different
+ * batches complete independently
  * (a publisher waits for its own reply before publishing again).  The id /
  * dest arrays are valid only during the callback (the NIF copies them into a
  * term and enif_send()s it).  status != TM_OK: ids are null. */
@@ -396,6 +398,9 @@ typedef struct tm_batcher_config {
     uint64_t max_bytes;       /* seal at this many topic bytes (0 = 64 MiB)      */
     uint32_t flags;           /* TM_BATCHER_ROUTES | TM_BATCHER_DELIVERIES      */
     uint32_t lanes_per_replica; /* batches in flight per GPU (0 = 2)            */
+    uint32_t callback_threads;  /* threads that share a batch's callbacks with its lane
+                                   (parts of >= 8192 topics; 0 = the lane alone) */
+    uint32_t reserved;
 } tm_batcher_config;
 typedef struct tm_batcher_stats {
     uint64_t batches, topics, results, max_batch;
@@ -507,6 +512,10 @@ int  tm_rewrite_match_batch_device(tm_rewrite* r, const uint8_t* d_topics, const
  *              0 = interleaved 32 B records
  *   "hot_levels" depths laid out level by level first at relayout (0..16,
  *              default 4; 0 = DFS preorder throughout); forces a relayout
+ *   "presort"  1 = walk each batch in the order of a key of its first words
+ *              (device radix sort; default 0)
+ *   "xbucket"  1 / 2 = per-XCD walk buckets by a hash of the topic's first
+ *              1 / 2 words (with "xcdq"; default 0 = contiguous eighths)
  * TM_EINVAL for unknown names / values. */
 int tm_set_option(tm_engine* e, const char* name, int64_t value);
 

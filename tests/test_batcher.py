@@ -45,3 +45,32 @@ def test_batcher_fails_loudly_without_gpu_and_seals():
     assert len(got) == 1001 and b.stats()["deadline_seals"] >= 1
     b.close()
     e.close()
+
+
+def test_callback_threads_complete_every_topic_once():
+    """callback threads take parts of a batch (>= 8192 topics each): every
+    topic still completes exactly once, before flush returns"""
+    e = Engine(device=-1)
+    b = Batcher(e, max_topics=40000, deadline_us=2000, callback_threads=3)
+    seen = {}
+    lock = threading.Lock()
+
+    def producer(k):
+        for i in range(20000):
+            t = k * 100000 + i
+
+            def cb(status, ids, dests, t=t):
+                with lock:
+                    seen[t] = seen.get(t, 0) + 1
+            b.submit(b"a/%d" % t, cb)
+    ts = [threading.Thread(target=producer, args=(k,)) for k in range(4)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    b.flush()
+    assert len(seen) == 80000 and set(seen.values()) == {1}
+    st = b.stats()
+    assert st["topics"] == 80000
+    b.close()
+    e.close()

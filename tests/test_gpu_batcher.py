@@ -18,8 +18,10 @@ from emqx_amd.batcher import Batcher  # noqa: E402
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("routes", [False, True, "deliveries"])
-def test_batcher_results_equal_batch_api(gpu_device, routes):
+@pytest.mark.parametrize("routes,cbt", [(False, 0), (True, 0), ("deliveries", 0), (False, 3), ("deliveries", 2)])
+def test_batcher_results_equal_batch_api(gpu_device, routes, cbt):
+    """cbt > 0: callback threads share each batch's callbacks with its lane
+    (batches of up to 20K topics: parts of >= 8192)"""
     fb, fo = W.filters(1)
     tb, to = W.topics(1, n=40000)
     topics = W.unpack(tb, to)
@@ -51,7 +53,8 @@ def test_batcher_results_equal_batch_api(gpu_device, routes):
         filters = W.unpack(fb, fo)
         for t in range(0, len(topics), 7):
             assert [e.filter_bytes(int(x)) for x in want[t][0]] == [filters[j] for j in oi[oo[t]:oo[t + 1]]], t
-    b = Batcher(e, max_topics=3000, deadline_us=500, routes=routes is True, deliveries=routes == "deliveries")
+    b = Batcher(e, max_topics=20000 if cbt else 3000, deadline_us=500, routes=routes is True,
+                deliveries=routes == "deliveries", callback_threads=cbt)
     got = [None] * len(topics)
 
     def producer(k):
@@ -68,7 +71,7 @@ def test_batcher_results_equal_batch_api(gpu_device, routes):
     b.flush()
     st = b.stats()
     b.close()
-    assert st["topics"] == len(topics) and st["failed_batches"] == 0 and st["batches"] >= 5
+    assert st["topics"] == len(topics) and st["failed_batches"] == 0 and st["batches"] >= (2 if cbt else 5)
     for t in range(len(topics)):
         ids, dests = got[t]
         assert [int(x) for x in want[t][0]] == ids, t

@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--max-topics", default="65536,262144")
     ap.add_argument("--deadline-us", default="200")
     ap.add_argument("--producers", default="16")
+    ap.add_argument("--cb-threads", default="0")
     a = ap.parse_args()
     fb, fo = W.filters(a.config)
     e = Engine(device=0)
@@ -39,15 +40,16 @@ def main():
     drv.tm_bench_batcher.restype = ctypes.c_int
     drv.tm_bench_batcher.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
                                      ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
-                                     ctypes.c_uint32, ctypes.POINTER(ctypes.c_double)]
+                                     ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_double)]
     ints = lambda s: [int(x) for x in s.split(",")]  # noqa: E731
-    for lanes, mt, dl, prod in itertools.product(ints(a.lanes), ints(a.max_topics), ints(a.deadline_us),
-                                                 ints(a.producers)):
-        print("[batcher] lanes %d, max_topics %d, deadline %d us, producers %d ..." % (lanes, mt, dl, prod),
-              file=sys.stderr, flush=True)
+    for lanes, mt, dl, prod, cbt in itertools.product(ints(a.lanes), ints(a.max_topics), ints(a.deadline_us),
+                                                      ints(a.producers), ints(a.cb_threads)):
+        print("[batcher] lanes %d, max_topics %d, deadline %d us, producers %d, callback threads %d ..." % (
+            lanes, mt, dl, prod, cbt), file=sys.stderr, flush=True)
         res = (ctypes.c_double * 8)()
-        rc = drv.tm_bench_batcher(e.h, tb.ctypes.data, to.ctypes.data, len(to) - 1, prod, dl, mt, lanes, 0, res)
-        print(json.dumps({"lanes": lanes, "max_topics": mt, "deadline_us": dl, "producers": prod, "rc": rc,
+        rc = drv.tm_bench_batcher(e.h, tb.ctypes.data, to.ctypes.data, len(to) - 1, prod, dl, mt, lanes, 0, cbt, res)
+        print(json.dumps({"lanes": lanes, "max_topics": mt, "deadline_us": dl, "producers": prod,
+                          "callback_threads": cbt, "rc": rc,
                           "topics": len(to) - 1, "secs": res[0], "topics_per_s": res[1], "batches": int(res[2]),
                           "mean_batch": res[3], "lat_us_p50": res[4], "lat_us_p99": res[5], "failed": int(res[6]),
                           "matches": int(res[7])}), flush=True)

@@ -29,8 +29,9 @@ void on_done(void* ctx, uint64_t, int status, const uint32_t*, const uint32_t*, 
 // out[8]: seconds, topics/s, batches, mean batch, p50 us, p99 us, failed, matches
 extern "C" int tm_bench_batcher(tm_engine* e, const uint8_t* tb, const uint64_t* to, uint64_t nt, int producers,
                                 uint32_t deadline_us, uint32_t max_topics, uint32_t lanes, uint32_t flags,
-                                double* out) {
+                                uint32_t cb_threads, double* out) {
     tm_batcher_config bc{};
+    bc.callback_threads = cb_threads;
     bc.max_topics = max_topics;
     bc.deadline_us = deadline_us;
     bc.lanes_per_replica = lanes;
