@@ -184,9 +184,22 @@ struct tm_batcher {
     std::mutex pool_mu;               // emptied chunks (capacity kept) for the stripes
     std::vector<Chunk> pool;
 
+    // Chunks are never freed while the batcher runs: every chunk in flight
+    // (a stripe's, the lanes' batches) fits in the pool, so the heap pages
+    // behind them stay mapped (a freed multi-MB vector goes back to the OS
+    // and its replacement page-faults all over again), and a new chunk starts
+    // at twice a stripe's share of a batch instead of growing by doubling.
+    size_t pool_cap() const { return (size_t)NSTRIPE * (lanes.size() + 2); }
     Chunk spare() {
         std::lock_guard<std::mutex> lk(pool_mu);
-        if (pool.empty()) return Chunk();
+        if (pool.empty()) {
+            Chunk c;
+            const size_t k = 2 * (size_t)cfg.max_topics / NSTRIPE + 64;
+            c.lens.reserve(k);
+            c.reqs.reserve(k);
+            c.bytes.reserve(k * 64);
+            return c;
+        }
         Chunk c = std::move(pool.back());
         pool.pop_back();
         return c;
@@ -195,7 +208,7 @@ struct tm_batcher {
         for (Chunk& c : cs) c.reset();
         std::lock_guard<std::mutex> lk(pool_mu);
         for (Chunk& c : cs)
-            if (pool.size() < 4 * NSTRIPE) pool.push_back(std::move(c));
+            if (pool.size() < pool_cap()) pool.push_back(std::move(c));
         cs.clear();
     }
 
@@ -273,7 +286,7 @@ struct tm_batcher {
     }
     void recycle_one(Chunk&& c) {
         std::lock_guard<std::mutex> lk(pool_mu);
-        if (pool.size() < 4 * NSTRIPE) pool.push_back(std::move(c));
+        if (pool.size() < pool_cap()) pool.push_back(std::move(c));
     }
 
     // the lane packs its chunks into pinned memory (bytes, offsets); false:
@@ -564,6 +577,7 @@ int tm_batcher_open(tm_engine* e, const tm_batcher_config* cfg, tm_batcher** out
         b->lanes.push_back(std::move(L));
     }
     try {
+        for (Stripe& x : b->stripes) x.cur = b->spare();
         for (size_t k = 0; k < b->lanes.size(); ++k) {
             b->free_lanes.push_back((int)(b->lanes.size() - 1 - k));   // lane 0 first
             b->lanes[k]->th = std::thread([b, k] { b->lane_loop(*b->lanes[k], (int)k); });

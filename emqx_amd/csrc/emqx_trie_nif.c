@@ -137,9 +137,13 @@ static ERL_NIF_TERM nif_open(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]
     r->filters_b = r->routes_b = r->deliv_b = NULL;
     int rc = tm_open_devices(&cfg, devs, nd, &r->e);
     if (rc == TM_OK) {
-        /* batches sealed at 64K topics or 200 us after their first topic */
+        /* batches sealed at 64K topics or 200 us after their first topic; 4
+         * batches in flight per GPU, and the callbacks (term building +
+         * enif_send, the per-topic host cost) shared with 8 threads */
         tm_batcher_config bc;
         memset(&bc, 0, sizeof(bc));
+        bc.lanes_per_replica = 4;
+        bc.callback_threads = 8;
         rc = tm_batcher_open(r->e, &bc, &r->filters_b);
         bc.flags = TM_BATCHER_ROUTES;
         if (rc == TM_OK) rc = tm_batcher_open(r->e, &bc, &r->routes_b);
@@ -323,10 +327,20 @@ static void async_done(void* ctx, uint64_t ticket, int status, const uint32_t* i
         } else if (dests) {
             make_binaries(env, q->r->e, dests, n, 1, db);
         }
-        for (uint32_t k = 0; k < n; ++k) {
-            ERL_NIF_TERM to = ids[k] == TM_ROUTE_TOPIC ? q->topic : filter_binary(env, q->r->e, ids[k]);
+        /* every filter binary of the list in ONE gather under the engine lock
+         * (the literal topic's own routes, TM_ROUTE_TOPIC, reuse its term) */
+        uint32_t* fids = (uint32_t*)enif_alloc(sizeof(uint32_t) * (n ? n : 1));
+        ERL_NIF_TERM* fb = (ERL_NIF_TERM*)enif_alloc(sizeof(ERL_NIF_TERM) * (n ? n : 1));
+        uint32_t nf = 0;
+        for (uint32_t k = 0; k < n; ++k)
+            if (ids[k] != TM_ROUTE_TOPIC) fids[nf++] = ids[k];
+        if (nf) make_binaries(env, q->r->e, fids, nf, 0, fb);
+        for (uint32_t k = 0, j = 0; k < n; ++k) {
+            ERL_NIF_TERM to = ids[k] == TM_ROUTE_TOPIC ? q->topic : fb[j++];
             cells[k] = dests ? enif_make_tuple2(env, to, db[k]) : to;
         }
+        enif_free(fb);
+        enif_free(fids);
         if (db) enif_free(db);
         res = enif_make_list_from_array(env, cells, n);
         enif_free(cells);

@@ -209,7 +209,7 @@ constexpr int N_KERNEL_SLOTS = 4;   // tokenize, walk, scan, copy_out
 // waits for its previous batch (hipStreamWaitEvent)
 struct Slot {
     DevBuf twords, words, path, meta, scan, stage, kstage, ws, stats, perm, skeys, svals, scount, soff, sscan,
-        twords_s, meta_s, xlist;
+        twords_s, meta_s;
     bool sorted = false;            // the slot's last batch walked in presort order (perm valid)
     uint64_t* h_maxc = nullptr;     // pinned: largest match count of the slot's last walk
     hipEvent_t maxc_ev = nullptr, done = nullptr;
@@ -369,8 +369,7 @@ struct DevState {
             b->release();
         for (auto& w : slots) {
             for (DevBuf* b : {&w.twords, &w.words, &w.path, &w.meta, &w.scan, &w.stage, &w.kstage, &w.ws, &w.stats,
-                              &w.perm, &w.skeys, &w.svals, &w.scount, &w.soff, &w.sscan, &w.twords_s, &w.meta_s,
-                              &w.xlist})
+                              &w.perm, &w.skeys, &w.svals, &w.scount, &w.soff, &w.sscan, &w.twords_s, &w.meta_s})
                 b->release();
             if (w.done) (void)hipEventDestroy(w.done);
             if (w.maxc_ev) (void)hipEventDestroy(w.maxc_ev);
@@ -440,8 +439,6 @@ struct tm_engine {
     int xcdq = 1;                     // option "xcdq": per-XCD dequeue ranges in the queue walk (default on)
     int presort = 0;                  // option "presort": walk the batch in the order of a key of its first
                                       // eight words (presort.hip; 0 = arrival order)
-    uint32_t xbucket = 0;             // option "xbucket": per-XCD walk buckets by a hash of the first 1 / 2
-                                      // words (kernels.h QueueBufs::xlist; 0 = contiguous eighths)
     int layout_mode = 1;              // option "layout": 0 off, 1 auto, 2 every commit (tests)
     size_t created_since_layout = 0;  // nodes created since the last relayout
     uint32_t hot_levels = 4;          // option "hot_levels": relayout puts depths <= H level by level (BFS)
@@ -1781,7 +1778,6 @@ struct tm_engine {
         w.stage.ensure(((size_t)n * d.stage_k + 4) * 4);
         if (key_words) w.kstage.ensure(((size_t)n * d.stage_k * key_words + 4) * 8);
         w.ws.ensure(QWS_BYTES);
-        if (xbucket) w.xlist.ensure((size_t)n * 8 * 4 + 4);
         if (presort) {
             w.perm.ensure((size_t)n * 4 + 4);
             w.twords_s.ensure((size_t)(n + 1) * WREG * 4);
@@ -1869,10 +1865,6 @@ struct tm_engine {
             qb.sort_scan = w.sscan.as<uint64_t>();
             qb.twords_s = w.twords_s.as<uint32_t>();
             qb.meta_s = w.meta_s.as<uint32_t>();
-        }
-        if (xbucket) {
-            qb.xlist = w.xlist.as<uint32_t>();
-            qb.xlev = xbucket;
         }
         w.sorted = presort != 0;
         HIPCHK(launch_queue(stats_enabled, xcdq != 0, im, bytes, off, n, qb, d.stage_k, counts, out_off, ids, keys,
@@ -3064,11 +3056,6 @@ int tm_set_option(tm_engine* e, const char* name, int64_t value) {
         if (!std::strcmp(name, "presort")) {
             if (value < 0 || value > 1) return TM_EINVAL;
             e->presort = (int)value;
-            return TM_OK;
-        }
-        if (!std::strcmp(name, "xbucket")) {
-            if (value < 0 || value > 2) return TM_EINVAL;
-            e->xbucket = (uint32_t)value;
             return TM_OK;
         }
         if (!std::strcmp(name, "route_gc")) {

@@ -12,7 +12,6 @@ constexpr uint32_t WREG = 16;        // topic levels kept in VGPRs / LDS path sl
 constexpr size_t QWS_BYTES = 1024;   // queue heads: 8 ranges x 128 B
 constexpr size_t QWS_MAXC = 120;     // u64 slot of ws: the batch's largest match count
 constexpr size_t QWS_MAXL = 121;     // u64 slot of ws: most levels of a topic in a keyed batch
-constexpr size_t QWS_XCNT = 122;     // u64 slots 122..125 of ws: 8 u32 bucket counts (option "xbucket")
 constexpr size_t STATS_BYTES = 512;  // 8 totals + per-level diagnostic histogram
 
 // per-batch device workspace of the queue pipeline
@@ -44,13 +43,6 @@ struct QueueBufs {
     uint64_t* sort_scan = nullptr;
     uint32_t* twords_s = nullptr;   // n x WREG
     uint32_t* meta_s = nullptr;     // n
-    // option "xbucket" (per-XCD walk queues, XCDQ only): the tokenizer files
-    // topic t under bucket b = hash(first xlev words) & 7 at xlist[b * n +
-    // pos] (per-bucket counts in ws, QWS_XCNT); XCD b's waves walk bucket b
-    // first, so the subtrees under those first words are read by ONE XCD and
-    // stay in its L2.  Rows, stage rows and outputs stay in topic order.
-    uint32_t* xlist = nullptr;      // 8 x n
-    uint32_t xlev = 0;
 };
 // digit counters of the presort of n topics (256 per 4096-topic tile)
 uint32_t presort_counts(uint32_t n);

@@ -178,19 +178,12 @@ __device__ __forceinline__ uint32_t presort_key(const uint32_t (&tw)[WREG], uint
     return k;
 }
 
-// option "xbucket": the walk bucket (XCD) of a topic, a hash of its first
-// xlev words (1 or 2)
-__device__ __forceinline__ uint32_t xbucket_of(const uint32_t (&tw)[WREG], uint32_t xlev) {
-    const uint32_t h = tw[0] * 0x9E3779B1u ^ (xlev > 1 ? tw[1] * 0x85EBCA77u : 0u);
-    return (h ^ (h >> 15)) * 0x2C1B3C6Du >> 29;
-}
-
 template <class B>
-__device__ __forceinline__ uint32_t tokenize_one(const ImageView& im, const B& bytes,
-                                                 const uint64_t* __restrict__ off, uint32_t t,
-                                                 uint32_t* __restrict__ twords, uint32_t* __restrict__ words,
-                                                 uint32_t* __restrict__ meta, uint32_t* __restrict__ skeys,
-                                                 uint32_t* __restrict__ svals, uint32_t xlev) {
+__device__ __forceinline__ void tokenize_one(const ImageView& im, const B& bytes,
+                                             const uint64_t* __restrict__ off, uint32_t t,
+                                             uint32_t* __restrict__ twords, uint32_t* __restrict__ words,
+                                             uint32_t* __restrict__ meta, uint32_t* __restrict__ skeys,
+                                             uint32_t* __restrict__ svals) {
     const uint64_t b = off[t], e = off[t + 1];
     uint32_t tw[WREG];
 #pragma unroll
@@ -208,14 +201,12 @@ __device__ __forceinline__ uint32_t tokenize_one(const ImageView& im, const B& b
         skeys[t] = presort_key(tw, lev);
         svals[t] = t;
     }
-    return xlev ? xbucket_of(tw, xlev) : 0u;
 }
 
 __global__ void __launch_bounds__(BLOCK)
 tm_tokenize(ImageView im, const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint32_t n,
             uint32_t* __restrict__ twords, uint32_t* __restrict__ words, uint32_t* __restrict__ meta,
-            uint32_t* __restrict__ skeys, uint32_t* __restrict__ svals, uint32_t* __restrict__ xlist,
-            uint32_t* __restrict__ xcnt, uint32_t xlev) {
+            uint32_t* __restrict__ skeys, uint32_t* __restrict__ svals) {
     __shared__ uint64_t win[BLOCK / 64][TOK_WIN_WORDS];
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -235,28 +226,11 @@ tm_tokenize(ImageView im, const uint8_t* __restrict__ bytes, const uint64_t* __r
                 win[wv][k] = *reinterpret_cast<const uint64_t*>(bytes + wbase + 8 * k);
     }
     __syncthreads();
-    uint32_t bk = 0;
     if (t < n) {
         if (lds)
-            bk = tokenize_one(im, LdsBytes{win[wv], wbase}, off, t, twords, words, meta, skeys, svals, xlev);
+            tokenize_one(im, LdsBytes{win[wv], wbase}, off, t, twords, words, meta, skeys, svals);
         else
-            bk = tokenize_one(im, GlobalBytes{bytes}, off, t, twords, words, meta, skeys, svals, xlev);
-    }
-    if (xlist) {   // option "xbucket": append t to its bucket, one atomic per (wave, bucket)
-        const bool act = t < n;
-        uint64_t rem = __ballot(act);
-        while (rem) {
-            const uint32_t leader = (uint32_t)(__ffsll((long long)rem) - 1);
-            const uint32_t bl = __shfl(bk, leader, 64);
-            const uint64_t m = __ballot(act && bk == bl);
-            uint32_t base = 0;
-            if (lane == leader) base = atomicAdd(xcnt + bl, (uint32_t)__popcll(m));
-            base = __shfl(base, leader, 64);
-            if (act && bk == bl)
-                xlist[(uint64_t)bl * n + base +
-                      __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = t;
-            rem &= ~m;
-        }
+            tokenize_one(im, GlobalBytes{bytes}, off, t, twords, words, meta, skeys, svals);
     }
 }
 
@@ -335,7 +309,7 @@ __device__ __forceinline__ Hit lit_child(const ImageView& im, uint32_t v, uint32
 #define TM_NT_LEVEL 0
 #endif
 #ifndef TM_NT_STAGE
-#define TM_NT_STAGE 1   // A/B at C3: walk 12.18-12.22 vs 12.37-12.59 ms (profiles/r02_ab/ab_nt.jsonl)
+#define TM_NT_STAGE 1   // A/B at C3: walk 11.9-12.2 vs 12.4-12.6 ms (profiles/r02_ab)
 #endif
 __device__ __forceinline__ uint4 load_half(const ImageView& im, uint32_t v, bool leaf, uint32_t r = 0) {
     const uint4* p = reinterpret_cast<const uint4*>((leaf ? im.leaf : im.inner) + ((uint64_t)v << im.node_shift));
@@ -365,23 +339,7 @@ constexpr int HIST_OFF = 8;   // hist = stats + HIST_OFF
 struct Cursor {
     uint32_t v, r, n, r0;   // node to visit next and its level; topic levels; start level
     uint64_t key;           // KEYS: fold branches taken above level r (rank_sym), key word 0
-    uint32_t pf, pfr;       // PF: '+' child to prefetch with the next load (NODE_NONE: none), its level slot
-    bool rec;               // PF: the node to visit next has its half in the record slot of level r - 1
 };
-
-// '+'-child prefetch (TM_PF_LEVELS = L > 0; 0 = off).  Descending into a
-// literal child at level r < L while a '+' child p stays pending, the next
-// step loads p's half beside the literal child's and keeps it in an LDS
-// record slot of level r; the pop to p later visits it from LDS.  p sits
-// right after its parent in the heat layout, so its line is usually the one
-// the parent's visit just brought into L2, while at pop time -- after the
-// whole literal subtree -- it has mostly been evicted: the prefetch turns a
-// fabric request into an L2 hit.  Path entries of such levels carry PF_BIT.
-#ifndef TM_PF_LEVELS
-#define TM_PF_LEVELS 0
-#endif
-constexpr uint32_t PF_LEVELS = TM_PF_LEVELS;
-constexpr uint32_t PF_BIT = 0x80000000u;
 
 // Order keys (sharded mode).  Every match of a topic is identified by the
 // branches the reference's fold took to discover it: at level i 'match_#'
@@ -435,20 +393,13 @@ struct MemWords {
     __device__ __forceinline__ uint32_t operator()(uint32_t r) const { return r < WREG ? tw[r] : lw[r]; }
 };
 
-template <bool WITH_PF>
-struct LdsPathT {
+struct LdsPath {
     uint32_t* base;   // [level][BLOCK]
-    uint4* recs;      // PF: [level < PF_LEVELS][BLOCK] prefetched '+'-child halves
-    static constexpr bool PF = WITH_PF && PF_LEVELS > 0;
     __device__ __forceinline__ uint32_t& operator()(uint32_t r) const { return base[r * BLOCK]; }
-    __device__ __forceinline__ uint4& rec(uint32_t r) const { return recs[r * BLOCK]; }
 };
-using LdsPath = LdsPathT<false>;   // re-walks: no prefetch records
 struct GlobalPath {
     uint32_t* base;
-    static constexpr bool PF = false;
     __device__ __forceinline__ uint32_t& operator()(uint32_t r) const { return base[r]; }
-    __device__ __forceinline__ uint4& rec(uint32_t) const { return *reinterpret_cast<uint4*>(base); }   // unused
 };
 
 // '$' rule (emqx_trie.erl:121-122): a topic whose first word starts with '$'
@@ -459,9 +410,6 @@ __device__ __forceinline__ bool walk_begin(const ImageView& im, Cursor& c, uint3
                                            WalkStats& st) {
     c.n = n;
     c.key = 0;
-    c.pf = NODE_NONE;
-    c.pfr = 0;
-    c.rec = false;
     if (!dollar) {
         c.v = ROOT;
         c.r = c.r0 = 0;
@@ -487,18 +435,7 @@ __device__ __forceinline__ bool walk_step(const ImageView& im, Cursor& c, Path p
     uint32_t v = c.v, r = c.r;
     uint64_t key = KEYS ? c.key : 0ull;
     bool leaf = r == c.n;
-    constexpr bool PF = Path::PF && !STATS;
-    uint4 h;   // inner {plus, hf, lw, lc} / leaf {sf, hf, hash, pad}
-    if (PF && c.rec) {
-        h = path.rec(r - 1);
-        c.rec = false;
-    } else {
-        h = load_half(im, v, leaf, r);
-    }
-    if (PF && c.pf != NODE_NONE) {   // beside this step's load: the pending '+' child of level pfr
-        path.rec(c.pfr) = load_half(im, c.pf, c.pfr + 1 == c.n, c.pfr + 1);
-        c.pf = NODE_NONE;
-    }
+    const uint4 h = load_half(im, v, leaf, r);   // inner {plus, hf, lw, lc} / leaf {sf, hf, hash, pad}
     uint32_t plus = h.x, hf = h.y, lw = h.z, lc = h.w, sf = h.x;
     for (;;) {
         if (STATS) {
@@ -540,12 +477,7 @@ __device__ __forceinline__ bool walk_step(const ImageView& im, Cursor& c, Path p
             else if ((plus & NODE_MASK) != NODE_NONE) atomicAdd(st.hist + 50, 1ull);
         }
         if (g.child != NODE_NONE) {   // literal subtree first, '+' child pending at level r
-            const bool pf = PF && pc != NODE_NONE && r < PF_LEVELS && c.pf == NODE_NONE;
-            path(r) = (KEYS ? (pc | SYM_LIT) : pc) | (pf ? PF_BIT : 0u);
-            if (pf) {
-                c.pf = pc;
-                c.pfr = r;
-            }
+            path(r) = KEYS ? (pc | SYM_LIT) : pc;
             v = g.child;
             if (KEYS) key |= rank_sym(r, 1);
             ++r;
@@ -574,14 +506,12 @@ __device__ __forceinline__ bool walk_step(const ImageView& im, Cursor& c, Path p
     }
     for (uint32_t k = r; k > c.r0;) {   // pop to the deepest pending '+' child
         --k;
-        const uint32_t raw = path(k);
-        const uint32_t p = raw & NODE_MASK;
+        const uint32_t p = KEYS ? path(k) & NODE_MASK : path(k);
         if (p != NODE_NONE) {
             if (STATS && st.hist) atomicAdd(st.hist + 50, 1ull);
             path(k) = KEYS ? (NODE_NONE | SYM_PLUS) : NODE_NONE;
             c.v = p;
             c.r = k + 1;
-            if (PF) c.rec = (raw & PF_BIT) != 0;
             if (KEYS) c.key = rank_prefix(key, k) | rank_sym(k, 2);
             return false;
         }
@@ -705,17 +635,10 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
               uint32_t* __restrict__ counts,
               unsigned long long* __restrict__ ws, unsigned long long* __restrict__ stats,
               unsigned long long* __restrict__ hist, const uint32_t* __restrict__ perm,
-              const uint32_t* __restrict__ twords_s, const uint32_t* __restrict__ meta_s,
-              const uint32_t* __restrict__ xlist) {
+              const uint32_t* __restrict__ twords_s, const uint32_t* __restrict__ meta_s) {
     __shared__ uint32_t lds_path[WREG * BLOCK];
-#if TM_PF_LEVELS > 0
-    __shared__ uint4 lds_rec[PF_LEVELS * BLOCK];
-    uint4* const recs = lds_rec + threadIdx.x;
-#else
-    uint4* const recs = nullptr;
-#endif
     const uint32_t lane = threadIdx.x & 63;
-    const LdsPathT<true> lp{lds_path + threadIdx.x, recs};
+    const LdsPath lp{lds_path + threadIdx.x};
     GlobalPath gp{nullptr};
     RegWords rw;
     MemWords mw{nullptr, nullptr};
@@ -744,10 +667,8 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
                 if (XCDQ) {
                     while (qr < QRANGES) {
                         const uint32_t r = (home + qr) & (QRANGES - 1);
-                        // xbucket: range r = bucket r's list; else the r-th eighth of the batch
-                        const uint32_t rb = xlist ? r * n : (uint32_t)((uint64_t)n * r / QRANGES);
-                        const uint32_t re = xlist ? r * n + reinterpret_cast<const uint32_t*>(ws + QWS_XCNT)[r]
-                                                  : (uint32_t)((uint64_t)n * (r + 1) / QRANGES);
+                        const uint32_t rb = (uint32_t)((uint64_t)n * r / QRANGES);
+                        const uint32_t re = (uint32_t)((uint64_t)n * (r + 1) / QRANGES);
                         uint32_t x = 0;
                         if (lane == leader)
                             x = (uint32_t)__hip_atomic_fetch_add(ws + 16 * r, (unsigned long long)QCHUNK,
@@ -782,21 +703,19 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
                 if (rank < avail) i = qnext + rank;
                 else if (g + (rank - avail) < gend) i = g + (rank - avail);
                 if (i != NO_TOPIC) {
-                    // i: queue position; ti: the topic; ri: its row (rows and stage
-                    // rows are in walk order with perm, in topic order otherwise)
-                    const uint32_t ti = XCDQ && xlist ? xlist[i] : perm ? perm[i] : i;
-                    const uint32_t ri = XCDQ && xlist ? ti : i;
+                    // i: queue position = stage row; ti: the topic
+                    const uint32_t ti = perm ? perm[i] : i;
                     const uint32_t* tws = perm ? twords_s : twords;
-                    const uint32_t mt = perm ? meta_s[i] : meta[ri];
+                    const uint32_t mt = perm ? meta_s[i] : meta[i];
                     const uint32_t nl = mt & MN;
                     const bool dollar = (mt & MDOLLAR) != 0;
                     lev_sum += nl;
                     if (KEYS) maxl = nl > maxl ? nl : maxl;
                     is_long = (mt & MLONG) != 0;
-                    em.row = stage + (uint64_t)ri * K;
-                    if (KEYS) em.krow = kstage + (uint64_t)ri * K;
+                    em.row = stage + (uint64_t)i * K;
+                    if (KEYS) em.krow = kstage + (uint64_t)i * K;
                     em.cnt = 0;
-                    const uint32_t* tw = tws + (uint64_t)ri * WREG;
+                    const uint32_t* tw = tws + (uint64_t)i * WREG;
                     bool go;
                     if (!is_long) {
 #pragma unroll
@@ -900,33 +819,7 @@ tm_copy_out(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const ui
         // (no per-id search); output j of a topic with ct ids is row slot
         // K-ct+j, staged for j >= ct-K
         const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-        uint32_t lt0 = w;
-        if (!KEYS) {
-            // CU topics per wave at a time, each list of <= 64 staged ids one
-            // load per lane: the CU row loads are in flight together (one
-            // dependent load per topic would leave the wave waiting on each)
-            constexpr uint32_t CU = 4, WS = BLOCK / 64;
-            for (; lt0 + WS * (CU - 1) < tn; lt0 += WS * CU) {
-                uint32_t v[CU];
-                uint64_t dst[CU];
-                bool ok[CU], easy = true;
-#pragma unroll
-                for (uint32_t u = 0; u < CU; ++u) {
-                    const uint32_t lt = lt0 + WS * u;
-                    const uint32_t prev = lt ? lds_inc[lt - 1] : 0u;
-                    const uint32_t ct = lds_inc[lt] - prev;
-                    easy = easy && ct <= 64u && ct <= K;
-                    dst[u] = base + prev + lane;
-                    ok[u] = lane < ct && ct <= K && dst[u] < out_cap;   // (a row slot, never before the row)
-                    v[u] = ok[u] ? stage[(uint64_t)(t0 + lt) * K + K - ct + lane] : 0u;
-                }
-                if (!__all(easy)) break;   // (uniform) a long list: the general loop from here
-#pragma unroll
-                for (uint32_t u = 0; u < CU; ++u)
-                    if (ok[u]) out[dst[u]] = v[u];
-            }
-        }
-        for (uint32_t lt = lt0; lt < tn; lt += BLOCK / 64) {
+        for (uint32_t lt = w; lt < tn; lt += BLOCK / 64) {
             const uint32_t prev = lt ? lds_inc[lt - 1] : 0u;
             const uint32_t ct = lds_inc[lt] - prev;
             const uint64_t ob = base + prev;
@@ -966,7 +859,7 @@ tm_copy_out(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const ui
         if (mt & MLONG)
             walk<false, KEYS>(im, mt & MN, (mt & MDOLLAR) != 0, GlobalPath{gpath + b + 2ull * t}, mw, em, s2);
         else
-            walk<false, KEYS>(im, mt & MN, (mt & MDOLLAR) != 0, LdsPath{lds_path + threadIdx.x, nullptr}, mw, em, s2);
+            walk<false, KEYS>(im, mt & MN, (mt & MDOLLAR) != 0, LdsPath{lds_path + threadIdx.x}, mw, em, s2);
     }
 }
 
@@ -1021,7 +914,7 @@ tm_copy_out_sorted(ImageView im, const uint64_t* __restrict__ off, uint32_t n, c
         if (mt & MLONG)
             walk<false, KEYS>(im, mt & MN, (mt & MDOLLAR) != 0, GlobalPath{gpath + b + 2ull * t}, mw, em, s2);
         else
-            walk<false, KEYS>(im, mt & MN, (mt & MDOLLAR) != 0, LdsPath{lds_path + threadIdx.x, nullptr}, mw, em, s2);
+            walk<false, KEYS>(im, mt & MN, (mt & MDOLLAR) != 0, LdsPath{lds_path + threadIdx.x}, mw, em, s2);
     }
 }
 
@@ -1195,10 +1088,8 @@ hipError_t launch_queue(bool stats_mode, bool xcdq, const ImageView& im, const u
     if (err != hipSuccess) return err;
     dim3 blk(BLOCK), g(div_up(n, BLOCK));
     mark(0);
-    const bool xb = xcdq && qb.xlist && !qb.perm && n <= (1u << 28);   // option "xbucket" (8n positions in u32)
     hipLaunchKernelGGL(tm_tokenize, g, blk, 0, st, im, bytes, off, n, qb.twords, qb.words, qb.meta,
-                       qb.perm ? qb.sort_keys : nullptr, qb.perm ? qb.perm : nullptr, xb ? qb.xlist : nullptr,
-                       reinterpret_cast<uint32_t*>(qb.ws + QWS_XCNT), xb ? qb.xlev : 0u);
+                       qb.perm ? qb.sort_keys : nullptr, qb.perm ? qb.perm : nullptr);
     if (qb.perm) {   // option "presort": perm and the rows in walk order (presort.hip)
         err = launch_presort(qb.twords, qb.meta, n, qb, st);
         if (err != hipSuccess) return err;
@@ -1210,7 +1101,7 @@ hipError_t launch_queue(bool stats_mode, bool xcdq, const ImageView& im, const u
 #define TM_Q(S, X, Y)                                                                                              \
     hipLaunchKernelGGL((tm_walk_queue<S, X, Y>), dim3(wg), blk, 0, st, im, off, n, qb.twords, qb.words, qb.meta, \
                        qb.path, qb.stage, qb.kstage, K, key_words, counts, qb.ws, stats,                         \
-                       hist ? stats + HIST_OFF : nullptr, qb.perm, qb.twords_s, qb.meta_s, xb ? qb.xlist : nullptr)
+                       hist ? stats + HIST_OFF : nullptr, qb.perm, qb.twords_s, qb.meta_s)
     if (keys) {
         if (stats_mode) TM_Q(true, true, true); else TM_Q(false, true, true);
     } else if (stats_mode) {

@@ -514,8 +514,6 @@ int  tm_rewrite_match_batch_device(tm_rewrite* r, const uint8_t* d_topics, const
  *              default 4; 0 = DFS preorder throughout); forces a relayout
  *   "presort"  1 = walk each batch in the order of a key of its first words
  *              (device radix sort; default 0)
- *   "xbucket"  1 / 2 = per-XCD walk buckets by a hash of the topic's first
- *              1 / 2 words (with "xcdq"; default 0 = contiguous eighths)
  * TM_EINVAL for unknown names / values. */
 int tm_set_option(tm_engine* e, const char* name, int64_t value);
 

@@ -235,9 +235,7 @@ VARIANTS = {"queue": {}, "queue_xcd": {}, "queue_xcd@nosplit@dfs": {"split": 0, 
             "queue@heat@hashlast@split0": {"order": 7, "layout": 2, "split": 0}, "queue_xcd@heatf": {"order": 15, "layout": 2},
             "queue_xcd@edgeload2": {"edge_load": 2, "layout": 2}, "queue_xcd@edgeload16": {"edge_load": 16},
             "queue_xcd@presort": {"presort": 1}, "queue@presort": {"presort": 1},
-            "queue_xcd@presort@stagek16": {"presort": 1, "stage_k": 16, "stage_auto": 0},
-            "queue_xcd@xbucket1": {"xbucket": 1}, "queue_xcd@xbucket2": {"xbucket": 2},
-            "queue@xbucket2": {"xbucket": 2}}
+            "queue_xcd@presort@stagek16": {"presort": 1, "stage_k": 16, "stage_auto": 0}}
 
 
 @pytest.mark.parametrize("variant", list(VARIANTS))
