@@ -43,8 +43,8 @@ from emqx_amd import multi  # noqa: E402
 from emqx_amd import workload as W  # noqa: E402
 
 METRIC = "topic matches/sec (whole node) at 10M wildcard filters; % HBM roofline"
-# micro-batcher leg: the best point of tools/bench_batcher.py (profiles/r02_ab)
-BATCHER = {"producers": 16, "deadline_us": 200, "max_topics": 262144, "lanes_per_replica": 4, "callback_threads": 0}
+# micro-batcher leg: the NIF's configuration, among the best points of tools/bench_batcher.py (profiles/r02_b)
+BATCHER = {"producers": 16, "deadline_us": 200, "max_topics": 262144, "lanes_per_replica": 4, "callback_threads": 8}
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak, /opt/skills/guides/MI355X_MICROARCH.md
 
 

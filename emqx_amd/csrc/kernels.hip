@@ -308,6 +308,9 @@ __device__ __forceinline__ Hit lit_child(const ImageView& im, uint32_t v, uint32
 #ifndef TM_NT_LEVEL
 #define TM_NT_LEVEL 0
 #endif
+#ifndef TM_NT_ROWS
+#define TM_NT_ROWS 0   // the walk's reads of the tokenized rows (once per topic) non-temporal
+#endif
 #ifndef TM_NT_STAGE
 #define TM_NT_STAGE 1   // A/B at C3: walk 11.9-12.2 vs 12.4-12.6 ms (profiles/r02_ab)
 #endif
@@ -721,7 +724,8 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
 #pragma unroll
                         for (uint32_t k = 0; k < WREG / 4; ++k) {
                             if (4 * k < nl) {
-                                const uint4 x = reinterpret_cast<const uint4*>(tw)[k];
+                                const uint4 x = TM_NT_ROWS ? nt_load16(reinterpret_cast<const uint4*>(tw) + k)
+                                                           : reinterpret_cast<const uint4*>(tw)[k];
                                 rw.w[4 * k] = x.x;
                                 rw.w[4 * k + 1] = x.y;
                                 rw.w[4 * k + 2] = x.z;
