@@ -35,7 +35,7 @@ w = summ["tm_walk_queue"]
 log = open(src + "/fetch/log.txt").read().splitlines()
 line = next((json.loads(x) for x in log if x.startswith("{")), None)
 cfg = line["config"] if line else None
-rev = subprocess.run(["git", "rev-parse", "--short", "HEAD"], capture_output=True, text=True).stdout.strip()
+rev = subprocess.run(["git", "rev-parse", "--short", "HEAD"], capture_output=True, text=True).stdout.strip() or None
 out = {
     "kernel": "tm_walk_queue",
     "config": cfg,
