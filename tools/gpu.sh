@@ -7,6 +7,7 @@
 #   bench     python bench.py $BENCH_ARGS                -> bench.json / bench.log
 #   prof      rocprofv3 --kernel-trace --stats of the bench -> prof/ (kernel_stats.csv)
 #   pmc       PMC passes (tools/pmc_passes.sh)           -> pmc/summary.json
+#   traffic   per-launch walk traffic from those passes  -> profiles/traffic_c3.json (read by bench)
 #   cmd       an arbitrary python command in $CMD         -> cmd.log
 # e.g. gpurun -- 'STEPS="tests bench prof" TAG=r02_head bash tools/gpu.sh'
 set -o pipefail
@@ -24,6 +25,7 @@ for s in ${STEPS:-tests}; do
              python3 bench.py --steps 10 --warmup 2 --cpu-sample 0 --check 0 --streams 1 --no-extras ${BENCH_ARGS} \
              > "$OUT/prof_bench.json" 2> "$OUT/prof_bench.log" ;;
     pmc)   PMC_DIR=${TAG:-job}/pmc bash tools/pmc_passes.sh ;;
+    traffic) python3 tools/traffic.py "$OUT/pmc" profiles/traffic_c3.json > "$OUT/traffic_c3.json" ;;
     cmd)   timeout -k 10 ${T_CMD:-600} python -u -c "$CMD" > "$OUT/cmd.log" 2>&1 ;;
     *)     echo "unknown step $s"; false ;;
   esac
