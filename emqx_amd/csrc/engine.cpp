@@ -209,9 +209,11 @@ constexpr int N_KERNEL_SLOTS = 4;   // tokenize, walk, scan, copy_out
 // waits for its previous batch (hipStreamWaitEvent)
 struct Slot {
     DevBuf twords, words, path, meta, scan, stage, kstage, ws, stats, perm, skeys, svals, scount, soff, sscan,
-        twords_s, meta_s;
+        twords_s, meta_s, spill, spill_head;
+    uint32_t spill_chunks = 0;      // spill capacity of the slot's last batch (0: none)
     bool sorted = false;            // the slot's last batch walked in presort order (perm valid)
-    uint64_t* h_maxc = nullptr;     // pinned: largest match count of the slot's last walk
+    uint64_t* h_maxc = nullptr;     // pinned copy of the slot's ws after its last walk (largest match count,
+                                    // spill chunks taken per XCD)
     hipEvent_t maxc_ev = nullptr, done = nullptr;
     bool maxc_pending = false, used = false, keyed = false;
     // the slot's last batch, for a re-copy into a larger output (no re-walk)
@@ -340,7 +342,10 @@ struct DevState {
     bool rw_used = false;
     Slot slots[MAX_SLOTS];
     int next_slot = 0, last_slot = 0;
-    uint32_t stage_k = 512;   // ids staged per topic before a re-walk (rows are written sparsely: footprint, not traffic)
+    uint32_t stage_k = 128;   // ids staged per topic (stage footprint n x K x 4 B: a wide row costs walk
+                              // time in address translation, profiles/r02_ab/ab_stage_k.jsonl)
+    uint32_t keyed_k = 0;     // K of keyed walks (grown by stage_auto)
+    uint64_t spill_chunks = 0;   // spill area of unkeyed walks (adapted per batch)
     // per-batch event records, accumulated until tm_last_kernel_times()
     std::vector<KTimes> ev_pool;          // recycled events
     std::vector<KTimes> ev_pending;       // recorded, not yet read
@@ -369,7 +374,8 @@ struct DevState {
             b->release();
         for (auto& w : slots) {
             for (DevBuf* b : {&w.twords, &w.words, &w.path, &w.meta, &w.scan, &w.stage, &w.kstage, &w.ws, &w.stats,
-                              &w.perm, &w.skeys, &w.svals, &w.scount, &w.soff, &w.sscan, &w.twords_s, &w.meta_s})
+                              &w.perm, &w.skeys, &w.svals, &w.scount, &w.soff, &w.sscan, &w.twords_s, &w.meta_s,
+                              &w.spill, &w.spill_head})
                 b->release();
             if (w.done) (void)hipEventDestroy(w.done);
             if (w.maxc_ev) (void)hipEventDestroy(w.maxc_ev);
@@ -540,8 +546,11 @@ struct tm_engine {
 
     // ---- batch pipeline knobs ----
     int nslots = 2;                     // option "slots"
-    uint32_t stage_k_min = 512;         // option "stage_k" (TM_STAGE_K)
-    int stage_auto = 1;                 // option "stage_auto": grow K to the largest list seen (no re-walks)
+    uint32_t stage_k_min = 128;         // option "stage_k" (TM_STAGE_K)
+    int stage_auto = 1;                 // option "stage_auto": keyed walks grow K to the largest list seen
+                                        // (no re-walks); unkeyed walks keep K and spill (kernels.h)
+    int spill_on = 1;                   // option "spill": ids past K to spill chunks (0: re-walk, as keyed)
+    static constexpr size_t SPILL_BUDGET = 8ull << 30;   // spill-area cap per slot (bytes)
     static constexpr size_t STAGE_BUDGET = 16ull << 30;  // stage-row footprint cap (bytes, of 288 GB HBM)
     bool stats_enabled = false, timing_enabled = false;
     tm_batch_stats last_stats{};
@@ -1777,6 +1786,12 @@ struct tm_engine {
         w.scan.ensure(scan_tmp_elems(n) * 8 + 8);
         w.stage.ensure(((size_t)n * d.stage_k + 4) * 4);
         if (key_words) w.kstage.ensure(((size_t)n * d.stage_k * key_words + 4) * 8);
+        w.spill_chunks = 0;
+        if (!key_words && spill_on && !presort && d.spill_chunks >= 8) {
+            w.spill.ensure((size_t)d.spill_chunks * SPILL_CHUNK * 4);
+            w.spill_head.ensure((size_t)n * 4 + 4);
+            w.spill_chunks = (uint32_t)d.spill_chunks;
+        }
         w.ws.ensure(QWS_BYTES);
         if (presort) {
             w.perm.ensure((size_t)n * 4 + 4);
@@ -1795,30 +1810,42 @@ struct tm_engine {
     // stage rows sized to the largest list of the previous walk (read back
     // asynchronously), within STAGE_BUDGET: fan-out beyond K costs a re-walk
     void adapt_stage_k(DevState& d, uint32_t n, uint32_t key_words) {
+        uint64_t mc = 0, sp = 0;
+        for (Slot& w : d.slots) {
+            if (!w.maxc_pending || hipEventQuery(w.maxc_ev) != hipSuccess) continue;
+            w.maxc_pending = false;
+            mc = std::max<uint64_t>(mc, w.h_maxc[QWS_MAXC]);
+            for (uint32_t x = 0; x < 8; ++x) sp = std::max<uint64_t>(sp, w.h_maxc[QWS_SPILL + 16 * x]);
+        }
+        // spill area: n/16 chunks, or twice the most any XCD took last time
+        // (an area that ran out re-walked its topics)
+        const uint64_t want = std::max<uint64_t>((uint64_t)n / 16, 2 * 8 * sp);
+        d.spill_chunks = std::min<uint64_t>(std::max<uint64_t>(d.spill_chunks, (want + 7) & ~7ull),
+                                            SPILL_BUDGET / (SPILL_CHUNK * 4));
+        if (!key_words && spill_on) {   // unkeyed: a narrow row, the rest spills
+            d.stage_k = stage_k_min;
+            return;
+        }
         if (!stage_auto) {
             d.stage_k = stage_k_min;
             return;
         }
         if (d.stage_k < stage_k_min) d.stage_k = stage_k_min;
-        uint64_t mc = 0;
-        for (Slot& w : d.slots) {
-            if (!w.maxc_pending || hipEventQuery(w.maxc_ev) != hipSuccess) continue;
-            w.maxc_pending = false;
-            mc = std::max<uint64_t>(mc, *w.h_maxc);
+        d.keyed_k = std::max(d.keyed_k, d.stage_k);
+        if (mc) {
+            uint64_t wk = stage_k_min;
+            while (wk < mc && wk < 4096) wk <<= 1;
+            uint64_t k = d.keyed_k;
+            const uint64_t per = (uint64_t)n * (4 + 8 * key_words);
+            while (k < wk && per * (k << 1) <= STAGE_BUDGET) k <<= 1;
+            d.keyed_k = (uint32_t)k;
         }
-        if (!mc) return;
-        uint64_t want = stage_k_min;
-        while (want < mc && want < 4096) want <<= 1;
-        uint64_t k = d.stage_k;
-        const uint64_t per = (uint64_t)n * (4 + 8 * key_words);
-        while (k < want && per * (k << 1) <= STAGE_BUDGET) k <<= 1;
-        d.stage_k = (uint32_t)k;
+        d.stage_k = d.keyed_k;
     }
     void record_maxc(Slot& w, hipStream_t st) {
-        if (!stage_auto) return;
-        if (!w.h_maxc) HIPCHK(hipHostMalloc((void**)&w.h_maxc, 64, hipHostMallocDefault));
+        if (!w.h_maxc) HIPCHK(hipHostMalloc((void**)&w.h_maxc, QWS_BYTES, hipHostMallocDefault));
         if (!w.maxc_ev) HIPCHK(hipEventCreateWithFlags(&w.maxc_ev, hipEventDisableTiming));
-        HIPCHK(hipMemcpyAsync(w.h_maxc, w.ws.as<uint64_t>() + QWS_MAXC, 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(w.h_maxc, w.ws.p, QWS_BYTES, hipMemcpyDeviceToHost, st));
         HIPCHK(hipEventRecord(w.maxc_ev, st));
         w.maxc_pending = true;
     }
@@ -1866,6 +1893,11 @@ struct tm_engine {
             qb.twords_s = w.twords_s.as<uint32_t>();
             qb.meta_s = w.meta_s.as<uint32_t>();
         }
+        if (w.spill_chunks) {
+            qb.spill = w.spill.as<uint32_t>();
+            qb.spill_head = w.spill_head.as<uint32_t>();
+            qb.spill_chunks = w.spill_chunks;
+        }
         w.sorted = presort != 0;
         HIPCHK(launch_queue(stats_enabled, xcdq != 0, im, bytes, off, n, qb, d.stage_k, counts, out_off, ids, keys,
                             cap, total, sp, st, timing_enabled ? marks : nullptr, walk_bpc, hist_enabled != 0,
@@ -1901,6 +1933,11 @@ struct tm_engine {
         qb.scan_tmp = w.scan.as<uint64_t>();
         qb.ws = w.ws.as<unsigned long long>();
         qb.perm = w.sorted ? w.perm.as<uint32_t>() : nullptr;   // the rows of a presorted walk
+        if (w.spill_chunks && !keys) {   // the spill chunks of the same walk
+            qb.spill = w.spill.as<uint32_t>();
+            qb.spill_head = w.spill_head.as<uint32_t>();
+            qb.spill_chunks = w.spill_chunks;
+        }
         HIPCHK(launch_copy(view(d), w.bytes, w.off, w.n, qb, w.K, w.kw, w.counts, w.out_off, ids, keys, cap, st));
         HIPCHK(hipEventRecord(w.done, st));
         d.note_use(st);
@@ -3122,7 +3159,7 @@ int tm_set_option(tm_engine* e, const char* name, int64_t value) {
         if (!std::strcmp(name, "stage_k")) {
             if (value < 4 || value > 4096 || (value & 3)) return TM_EINVAL;
             e->stage_k_min = (uint32_t)value;
-            for (auto& d : e->devs) d->stage_k = (uint32_t)value;
+            for (auto& d : e->devs) d->stage_k = d->keyed_k = (uint32_t)value;
             e->stage_auto = 0;   // an explicit K is kept (set "stage_auto" after it to grow from it)
             return TM_OK;
         }
@@ -3135,6 +3172,11 @@ int tm_set_option(tm_engine* e, const char* name, int64_t value) {
         if (!std::strcmp(name, "stage_auto")) {
             if (value < 0 || value > 1) return TM_EINVAL;
             e->stage_auto = (int)value;
+            return TM_OK;
+        }
+        if (!std::strcmp(name, "spill")) {
+            if (value < 0 || value > 1) return TM_EINVAL;
+            e->spill_on = (int)value;
             return TM_OK;
         }
         return TM_EINVAL;

@@ -9,9 +9,19 @@ namespace tmx {
 
 constexpr uint32_t WREG = 16;        // topic levels kept in VGPRs / LDS path slots; longer
                                      // topics keep their path in global scratch
-constexpr size_t QWS_BYTES = 1024;   // queue heads: 8 ranges x 128 B
+constexpr size_t QWS_BYTES = 2048;   // queue heads: 8 ranges x 128 B, then 8 spill counters x 128 B
 constexpr size_t QWS_MAXC = 120;     // u64 slot of ws: the batch's largest match count
 constexpr size_t QWS_MAXL = 121;     // u64 slot of ws: most levels of a topic in a keyed batch
+constexpr size_t QWS_SPILL = 128;    // u64 slots 128 + 16 x: spill chunks taken by XCD x's waves
+// Spill chunks (unkeyed walks): ids of a topic past its K-slot stage row go
+// to chunks of SPILL_CHUNK u32 -- slot 0 the next chunk of the topic, slots
+// 1.. ids in discovery order -- taken from the walking XCD's area (capacity
+// spill_chunks / 8 chunks per XCD); spill_head[t] = the first chunk of a
+// topic with more than K ids, or NO_SPILL when an area ran out (the
+// copy-out then re-walks the topic, as keyed walks always do).  A narrow
+// stage row keeps the walk's stage footprint (n x K x 4 B) small.
+constexpr uint32_t SPILL_CHUNK = 128;
+constexpr uint32_t NO_SPILL = 0xFFFFFFFFu;
 constexpr size_t STATS_BYTES = 512;  // 8 totals + per-level diagnostic histogram
 
 // per-batch device workspace of the queue pipeline
@@ -43,6 +53,9 @@ struct QueueBufs {
     uint64_t* sort_scan = nullptr;
     uint32_t* twords_s = nullptr;   // n x WREG
     uint32_t* meta_s = nullptr;     // n
+    uint32_t* spill = nullptr;      // spill_chunks x SPILL_CHUNK (null: fan-out beyond K re-walks)
+    uint32_t* spill_head = nullptr; // n
+    uint32_t spill_chunks = 0;      // a multiple of 8
 };
 // digit counters of the presort of n topics (256 per 4096-topic tile)
 uint32_t presort_counts(uint32_t n);

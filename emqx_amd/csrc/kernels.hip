@@ -544,6 +544,12 @@ struct RowEmit {
     uint64_t kb;   // KEYS: key of the last even discovery, stored with the next one (16 B)
     uint32_t KW;
     uint64_t kplane;
+    // !KEYS: discoveries past K go to spill chunks of this XCD's area
+    uint32_t* spill = nullptr;
+    unsigned long long* sctr = nullptr;
+    uint32_t sbase = 0, scap = 0;
+    uint32_t shead = 0, scur = 0;
+    bool sfail = false;
     template <class Path>
     __device__ __forceinline__ void operator()(uint32_t f, uint64_t key, const Path& path, uint32_t r, uint32_t sym) {
         if (KEYS && cnt < K) {
@@ -562,6 +568,19 @@ struct RowEmit {
             buf.y = s == 2 ? f : buf.y;
             buf.x = s == 3 ? f : buf.x;
             if (s == 3) store_stage(row + K - 4 - (cnt & ~3u), buf);
+        } else if (!KEYS && spill && !sfail) {
+            const uint32_t o = cnt - K, j = o % (SPILL_CHUNK - 1);
+            if (j == 0) {   // a new chunk, linked from the previous one
+                const uint32_t c = (uint32_t)atomicAdd(sctr, 1ull);
+                if (c >= scap) {
+                    sfail = true;
+                } else {
+                    if (o == 0) shead = sbase + c;
+                    else spill[(uint64_t)scur * SPILL_CHUNK] = sbase + c;
+                    scur = sbase + c;
+                }
+            }
+            if (!sfail) spill[(uint64_t)scur * SPILL_CHUNK + 1 + j] = f;
         }
         ++cnt;
     }
@@ -638,7 +657,8 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
               uint32_t* __restrict__ counts,
               unsigned long long* __restrict__ ws, unsigned long long* __restrict__ stats,
               unsigned long long* __restrict__ hist, const uint32_t* __restrict__ perm,
-              const uint32_t* __restrict__ twords_s, const uint32_t* __restrict__ meta_s) {
+              const uint32_t* __restrict__ twords_s, const uint32_t* __restrict__ meta_s,
+              uint32_t* __restrict__ spill, uint32_t* __restrict__ spill_head, uint32_t spill_chunks) {
     __shared__ uint32_t lds_path[WREG * BLOCK];
     const uint32_t lane = threadIdx.x & 63;
     const LdsPath lp{lds_path + threadIdx.x};
@@ -653,6 +673,13 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
     bool is_long = false, drained = false;
     Cursor cur;
     RowEmit<KEYS> em{nullptr, nullptr, K, 0, make_uint4(0, 0, 0, 0), 0ull, KW, (uint64_t)n * K};
+    if (!KEYS && spill) {   // this XCD's spill area and counter (placement only: any XCD id is valid)
+        const uint32_t x = xcc_id();
+        em.spill = spill;
+        em.sctr = ws + QWS_SPILL + 16 * x;
+        em.scap = spill_chunks / QRANGES;
+        em.sbase = x * em.scap;
+    }
     WalkStats st;
     if (STATS) st.hist = hist;
     uint64_t lev_sum = 0, match_sum = 0;
@@ -718,6 +745,7 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
                     em.row = stage + (uint64_t)i * K;
                     if (KEYS) em.krow = kstage + (uint64_t)i * K;
                     em.cnt = 0;
+                    em.sfail = false;
                     const uint32_t* tw = tws + (uint64_t)i * WREG;
                     bool go;
                     if (!is_long) {
@@ -767,6 +795,7 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
         if (fin) {
             em.flush();
             counts[myt] = em.cnt;
+            if (!KEYS && spill && em.cnt > K) spill_head[myt] = em.sfail ? NO_SPILL : em.shead;
             match_sum += em.cnt;
             maxc = em.cnt > maxc ? em.cnt : maxc;
             my = NO_TOPIC;
@@ -804,7 +833,8 @@ tm_copy_out(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const ui
             const uint32_t* __restrict__ words, const uint32_t* __restrict__ meta, uint32_t* __restrict__ gpath,
             const uint32_t* __restrict__ stage, const uint64_t* __restrict__ kstage, uint32_t K, uint32_t KW,
             const uint32_t* __restrict__ counts, const uint64_t* __restrict__ out_off, uint32_t* __restrict__ out,
-            uint64_t* __restrict__ kout, uint64_t out_cap) {
+            uint64_t* __restrict__ kout, uint64_t out_cap, const uint32_t* __restrict__ spill,
+            const uint32_t* __restrict__ spill_head) {
     const uint64_t kplane = (uint64_t)n * K;   // KEYS: key word j of stage slot x at kstage[j * kplane + x],
                                                // of output p at kout[j * out_cap + p]
     __shared__ uint32_t lds_path[WREG * BLOCK];
@@ -853,7 +883,29 @@ tm_copy_out(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const ui
                     kout[q * out_cap + base + j] = kstage[q * kplane + (uint64_t)(t0 + lo) * K + (uint64_t)slot];
         }
     }
-    if (threadIdx.x < tn && c > K) {   // fan-out beyond the stage row: walk again, write the head
+    if (!KEYS && spill) {
+        // the head of a list past K ids (outputs [0, ct - K), in reverse
+        // discovery order) from its spill chunks, one wave per topic
+        const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+        for (uint32_t lt = w; lt < tn; lt += BLOCK / 64) {
+            const uint32_t prev = lt ? lds_inc[lt - 1] : 0u;
+            const uint32_t ct = lds_inc[lt] - prev;
+            if (ct <= K) continue;
+            uint32_t cur = spill_head[t0 + lt];
+            if (cur == NO_SPILL) continue;   // re-walked below
+            const uint32_t m = ct - K;
+            const uint64_t ob = base + prev;
+            for (uint32_t o0 = 0; o0 < m; o0 += SPILL_CHUNK - 1) {
+                for (uint32_t j = lane; j < SPILL_CHUNK - 1 && o0 + j < m; j += 64) {
+                    const uint64_t p = ob + m - 1 - (o0 + j);
+                    if (p < out_cap) out[p] = spill[(uint64_t)cur * SPILL_CHUNK + 1 + j];
+                }
+                if (o0 + SPILL_CHUNK - 1 < m) cur = spill[(uint64_t)cur * SPILL_CHUNK];
+            }
+        }
+    }
+    if (threadIdx.x < tn && c > K && (KEYS || !spill || spill_head[t0 + threadIdx.x] == NO_SPILL)) {
+        // fan-out beyond the stage row and no spill: walk again, write the head
         const uint32_t t = t0 + threadIdx.x;
         const uint32_t mt = meta[t];
         const uint64_t b = off[t] - off[0];
@@ -1065,10 +1117,12 @@ hipError_t launch_copy(const ImageView& im, const uint8_t* bytes, const uint64_t
                                qb.path, qb.stage, nullptr, K, 1u, counts, out_off, out, nullptr, out_cap, qb.perm);
     } else if (qb.kstage) {
         hipLaunchKernelGGL(tm_copy_out<true>, g, blk, 0, st, im, off, n, qb.twords, qb.words, qb.meta, qb.path,
-                           qb.stage, qb.kstage, K, key_words, counts, out_off, out, out_keys, out_cap);
+                           qb.stage, qb.kstage, K, key_words, counts, out_off, out, out_keys, out_cap, nullptr,
+                           nullptr);
     } else {
         hipLaunchKernelGGL(tm_copy_out<false>, g, blk, 0, st, im, off, n, qb.twords, qb.words, qb.meta, qb.path,
-                           qb.stage, nullptr, K, 1u, counts, out_off, out, nullptr, out_cap);
+                           qb.stage, nullptr, K, 1u, counts, out_off, out, nullptr, out_cap,
+                           qb.spill_chunks >= QRANGES ? qb.spill : nullptr, qb.spill_head);
     }
     return hipGetLastError();
 }
@@ -1101,11 +1155,14 @@ hipError_t launch_queue(bool stats_mode, bool xcdq, const ImageView& im, const u
     mark(1);
     mark(2);
     const bool keys = qb.kstage != nullptr;
+    // spill chunks: unkeyed walks in arrival order (presorted rows re-walk)
+    uint32_t* const spill = (!keys && !qb.perm && qb.spill_chunks >= QRANGES) ? qb.spill : nullptr;
     const uint32_t wg = resident_grid(tm_walk_queue<false, false, false>, div_up(n, 64), walk_blocks_per_cu);
 #define TM_Q(S, X, Y)                                                                                              \
     hipLaunchKernelGGL((tm_walk_queue<S, X, Y>), dim3(wg), blk, 0, st, im, off, n, qb.twords, qb.words, qb.meta, \
                        qb.path, qb.stage, qb.kstage, K, key_words, counts, qb.ws, stats,                         \
-                       hist ? stats + HIST_OFF : nullptr, qb.perm, qb.twords_s, qb.meta_s)
+                       hist ? stats + HIST_OFF : nullptr, qb.perm, qb.twords_s, qb.meta_s, spill, qb.spill_head,   \
+                       qb.spill_chunks)
     if (keys) {
         if (stats_mode) TM_Q(true, true, true); else TM_Q(false, true, true);
     } else if (stats_mode) {

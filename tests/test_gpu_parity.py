@@ -235,7 +235,9 @@ VARIANTS = {"queue": {}, "queue_xcd": {}, "queue_xcd@nosplit@dfs": {"split": 0, 
             "queue@heat@hashlast@split0": {"order": 7, "layout": 2, "split": 0}, "queue_xcd@heatf": {"order": 15, "layout": 2},
             "queue_xcd@edgeload2": {"edge_load": 2, "layout": 2}, "queue_xcd@edgeload16": {"edge_load": 16},
             "queue_xcd@presort": {"presort": 1}, "queue@presort": {"presort": 1},
-            "queue_xcd@presort@stagek16": {"presort": 1, "stage_k": 16, "stage_auto": 0}}
+            "queue_xcd@presort@stagek16": {"presort": 1, "stage_k": 16, "stage_auto": 0},
+            "queue_xcd@nospill": {"spill": 0}, "queue@stagek8": {"stage_k": 8},
+            "queue_xcd@stagek32@nospill": {"stage_k": 32, "spill": 0}}
 
 
 @pytest.mark.parametrize("variant", list(VARIANTS))
