@@ -1861,7 +1861,10 @@ struct tm_engine {
         d.next_slot = (d.next_slot + 1) % nslots;
         Slot& w = d.slots[si];
         if (w.used) HIPCHK(hipStreamWaitEvent(st, w.done, 0));   // its previous batch, maybe on another stream
-        ensure_slot(d, w, n, nbytes, kw);
+        // every slot sized for this batch now: a slot first used later would
+        // allocate (hipMalloc of GBs of stage rows) in the middle of a stream
+        // of batches
+        for (int k = 0; k < nslots; ++k) ensure_slot(d, d.slots[(si + k) % nslots], n, nbytes, kw);
         d.last_slot = si;
         ImageView im = view(d);
         unsigned long long* sp = w.stats.as<unsigned long long>();

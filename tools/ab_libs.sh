@@ -18,7 +18,7 @@ for r in $(seq 1 ${ROUNDS:-2}); do
     if [ "$l" = base ]; then lib=emqx_amd/libtopicmatch.so; else lib=emqx_amd/variants/libtopicmatch_$l.so; fi
     l=$(echo "$spec" | tr ':=,' '_-_')
     echo "round $r lib $l"
-    timeout -k 10 ${T_RUN:-240} python -u bench.py --lib $lib $opts --steps ${STEPS_N:-10} --warmup 2 --cpu-sample 0 \
+    timeout -k 10 ${T_RUN:-240} python -u bench.py --lib $lib $opts --steps ${STEPS_N:-10} --warmup 3 --cpu-sample 0 \
       --check ${CHECK:-2000} --no-extras ${BENCH_ARGS} > "$OUT/run_${r}_$l.json" 2> "$OUT/run_${r}_$l.log"
     rc=$?
     [ $rc -eq 0 ] || { echo "run $r $l rc=$rc"; exit $rc; }
