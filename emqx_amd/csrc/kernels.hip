@@ -62,24 +62,45 @@ __device__ __forceinline__ uint64_t load_chunk(const B& bytes, uint64_t p, uint3
 }
 
 // dictionary lookup of topic bytes [p, p+len): word id, WORD_PLUS/HASH for the
-// atoms '+' / '#', or WORD_NONE (bytes no filter contains: match only '+'/'#')
+// atoms '+' / '#', or WORD_NONE (bytes no filter contains: match only '+'/'#').
+// Split in two so the tokenizer can issue a level's slot load (dict_begin),
+// scan and hash the next level while it is in flight, then resolve it
+// (dict_end: byte-verify, probe on).
+struct DictProbe {
+    uint64_t p, h, s;
+    uint32_t len, atom;   // atom: WORD_PLUS / WORD_HASH, or 0 (a dictionary word)
+    uint4 d0, d1;         // the home slot: hash, word, len | first 16 bytes
+};
 template <class B>
-__device__ __forceinline__ uint32_t dict_lookup(const ImageView& im, const B& bytes, uint64_t p, uint32_t len) {
+__device__ __forceinline__ DictProbe dict_begin(const ImageView& im, const B& bytes, uint64_t p, uint32_t len) {
+    DictProbe q;
+    q.p = p;
+    q.len = len;
+    q.atom = 0;
     if (len == 1) {
-        uint32_t c = bytes.byte(p);
-        if (c == '+') return WORD_PLUS;
-        if (c == '#') return WORD_HASH;
+        const uint32_t c = bytes.byte(p);
+        q.atom = c == '+' ? WORD_PLUS : c == '#' ? WORD_HASH : 0u;
     }
     uint64_t h = 0x243F6A8885A308D3ULL;
     for (uint32_t i = 0; i < len; i += 8) {
         uint32_t k = len - i < 8 ? len - i : 8;
         h = word_hash_step(h, load_chunk(bytes, p + i, k));
     }
-    h = word_hash_final(h, len);
-    uint64_t s = h & im.dict_slot_mask;
+    q.h = word_hash_final(h, len);
+    q.s = q.h & im.dict_slot_mask;
+    const uint4* slot = reinterpret_cast<const uint4*>(im.dict + q.s);
+    q.d0 = slot[0];
+    q.d1 = slot[1];
+    return q;
+}
+template <class B>
+__device__ __forceinline__ uint32_t dict_end(const ImageView& im, const B& bytes, DictProbe q) {
+    if (q.atom) return q.atom;
+    const uint64_t p = q.p, h = q.h;
+    const uint32_t len = q.len;
+    uint64_t s = q.s;
+    uint4 d0 = q.d0, d1 = q.d1;
     for (;;) {
-        const uint4* slot = reinterpret_cast<const uint4*>(im.dict + s);
-        const uint4 d0 = slot[0], d1 = slot[1];   // one 32 B slot: hash, word, len | first 16 bytes
         const uint32_t word = d0.z;
         if (word == WORD_NONE) return WORD_NONE;
         if ((((uint64_t)d0.y << 32) | d0.x) == h && d0.w == len) {
@@ -98,6 +119,9 @@ __device__ __forceinline__ uint32_t dict_lookup(const ImageView& im, const B& by
             if (eq) return word;
         }
         s = (s + 1) & im.dict_slot_mask;
+        const uint4* slot = reinterpret_cast<const uint4*>(im.dict + s);
+        d0 = slot[0];
+        d1 = slot[1];
     }
 }
 
@@ -126,31 +150,47 @@ __device__ __forceinline__ uint64_t block_exclusive_scan(uint64_t x, uint64_t* l
 // registers: AND-mask updates, no dynamic index) or lw[k] (k >= WREG);
 // returns the number of levels (N slashes -> N+1 levels, empty levels kept)
 template <class B>
+__device__ __forceinline__ uint64_t next_slash(const B& bytes, uint64_t q, uint64_t e, bool& found) {
+    found = false;   // next '/' at or after q, or e
+    while (q < e) {
+        uint64_t word8 = bytes.word(q);
+        uint32_t start = (uint32_t)(q & 7);
+        uint64_t rem = e - (q & ~7ull);
+        uint32_t stop = rem < 8 ? (uint32_t)rem : 8;
+        uint64_t x = word8 ^ 0x2F2F2F2F2F2F2F2FULL;  // '/' -> 0x00
+        uint64_t z = (x - 0x0101010101010101ULL) & ~x & 0x8080808080808080ULL;
+        z &= (~0ull) << (8 * start);
+        if (stop < 8) z &= (~0ull) >> (64 - 8 * stop);
+        if (z) {
+            found = true;
+            return (q & ~7ull) + (__builtin_ctzll(z) >> 3);
+        }
+        q = (q & ~7ull) + 8;
+    }
+    return e;
+}
+
+// emqx_topic:words/1 of topic [b, e): word id of level k to tw[k] (k < WREG,
+// registers: AND-mask updates, no dynamic index) or lw[k] (k >= WREG);
+// returns the number of levels (N slashes -> N+1 levels, empty levels kept).
+// Software-pipelined by one level: level k+1 is scanned, hashed and its
+// dictionary slot requested before level k's slot is resolved.
+template <class B>
 __device__ __forceinline__ uint32_t tokenize_topic(const ImageView& im, const B& bytes, uint64_t b, uint64_t e,
                                                    uint32_t (&tw)[WREG], uint32_t* lw) {
     uint32_t lev = 0;
-    uint64_t s = b;
+    bool found;
+    uint64_t q = next_slash(bytes, b, e, found);
+    DictProbe cur = dict_begin(im, bytes, b, (uint32_t)(q - b));
     for (;;) {
-        uint64_t q = s;  // next '/' at or after s, or e
-        bool found = false;
-        while (q < e) {
-            uint64_t word8 = bytes.word(q);
-            uint32_t start = (uint32_t)(q & 7);
-            uint64_t rem = e - (q & ~7ull);
-            uint32_t stop = rem < 8 ? (uint32_t)rem : 8;
-            uint64_t x = word8 ^ 0x2F2F2F2F2F2F2F2FULL;  // '/' -> 0x00
-            uint64_t z = (x - 0x0101010101010101ULL) & ~x & 0x8080808080808080ULL;
-            z &= (~0ull) << (8 * start);
-            if (stop < 8) z &= (~0ull) >> (64 - 8 * stop);
-            if (z) {
-                q = (q & ~7ull) + (__builtin_ctzll(z) >> 3);
-                found = true;
-                break;
-            }
-            q = (q & ~7ull) + 8;
+        const bool more = found;
+        DictProbe nxt;
+        if (more) {
+            const uint64_t s = q + 1;
+            q = next_slash(bytes, s, e, found);
+            nxt = dict_begin(im, bytes, s, (uint32_t)(q - s));
         }
-        if (!found) q = e;
-        const uint32_t w = dict_lookup(im, bytes, s, (uint32_t)(q - s));
+        const uint32_t w = dict_end(im, bytes, cur);
         if (lev < WREG) {
 #pragma unroll
             for (uint32_t k = 0; k < WREG; ++k) tw[k] = lev == k ? w : tw[k];
@@ -158,8 +198,8 @@ __device__ __forceinline__ uint32_t tokenize_topic(const ImageView& im, const B&
             lw[lev] = w;
         }
         ++lev;
-        if (!found) return lev;
-        s = q + 1;
+        if (!more) return lev;
+        cur = nxt;
     }
 }
 
