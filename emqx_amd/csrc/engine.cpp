@@ -345,6 +345,7 @@ struct DevState {
     uint32_t stage_k = 128;   // ids staged per topic (stage footprint n x K x 4 B: a wide row costs walk
                               // time in address translation, profiles/r02_ab/ab_stage_k.jsonl)
     uint32_t keyed_k = 0;     // K of keyed walks (grown by stage_auto)
+    uint32_t unkeyed_k = 0;   // K of unkeyed walks once their lists mostly spilled (grown by stage_auto)
     uint64_t spill_chunks = 0;   // spill area of unkeyed walks (adapted per batch)
     // per-batch event records, accumulated until tm_last_kernel_times()
     std::vector<KTimes> ev_pool;          // recycled events
@@ -1810,20 +1811,35 @@ struct tm_engine {
     // stage rows sized to the largest list of the previous walk (read back
     // asynchronously), within STAGE_BUDGET: fan-out beyond K costs a re-walk
     void adapt_stage_k(DevState& d, uint32_t n, uint32_t key_words) {
-        uint64_t mc = 0, sp = 0;
+        uint64_t mc = 0, sp = 0, spt = 0;
         for (Slot& w : d.slots) {
             if (!w.maxc_pending || hipEventQuery(w.maxc_ev) != hipSuccess) continue;
             w.maxc_pending = false;
             mc = std::max<uint64_t>(mc, w.h_maxc[QWS_MAXC]);
-            for (uint32_t x = 0; x < 8; ++x) sp = std::max<uint64_t>(sp, w.h_maxc[QWS_SPILL + 16 * x]);
+            uint64_t t = 0;
+            for (uint32_t x = 0; x < 8; ++x) {
+                sp = std::max<uint64_t>(sp, w.h_maxc[QWS_SPILL + 16 * x]);
+                t += w.h_maxc[QWS_SPILL + 16 * x];
+            }
+            spt = std::max(spt, t);
         }
         // spill area: n/16 chunks, or twice the most any XCD took last time
         // (an area that ran out re-walked its topics)
         const uint64_t want = std::max<uint64_t>((uint64_t)n / 16, 2 * 8 * sp);
         d.spill_chunks = std::min<uint64_t>(std::max<uint64_t>(d.spill_chunks, (want + 7) & ~7ull),
                                             SPILL_BUDGET / (SPILL_CHUNK * 4));
-        if (!key_words && spill_on) {   // unkeyed: a narrow row, the rest spills
-            d.stage_k = stage_k_min;
+        if (!key_words && spill_on) {
+            // unkeyed: a narrow row, the rare long list spills.  Batches whose
+            // lists mostly pass K (more than one spill chunk per 8 topics: an
+            // atomic per chunk, e.g. C5 at ~900 ids per topic) widen the rows
+            // as keyed walks do (stage_auto), once: the spill stays the tail.
+            if (stage_auto && mc && spt * 8 > n) {
+                uint64_t wk = std::max<uint64_t>(stage_k_min, d.unkeyed_k);
+                while (wk < mc && wk < 4096) wk <<= 1;
+                while (wk > stage_k_min && (uint64_t)n * 4 * wk > STAGE_BUDGET) wk >>= 1;
+                d.unkeyed_k = std::max<uint32_t>(d.unkeyed_k, (uint32_t)wk);
+            }
+            d.stage_k = std::max<uint32_t>(stage_k_min, d.unkeyed_k);
             return;
         }
         if (!stage_auto) {
@@ -3162,7 +3178,10 @@ int tm_set_option(tm_engine* e, const char* name, int64_t value) {
         if (!std::strcmp(name, "stage_k")) {
             if (value < 4 || value > 4096 || (value & 3)) return TM_EINVAL;
             e->stage_k_min = (uint32_t)value;
-            for (auto& d : e->devs) d->stage_k = d->keyed_k = (uint32_t)value;
+            for (auto& d : e->devs) {
+                d->stage_k = d->keyed_k = (uint32_t)value;
+                d->unkeyed_k = 0;
+            }
             e->stage_auto = 0;   // an explicit K is kept (set "stage_auto" after it to grow from it)
             return TM_OK;
         }
