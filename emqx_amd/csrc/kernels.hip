@@ -146,12 +146,10 @@ __device__ __forceinline__ uint64_t block_exclusive_scan(uint64_t x, uint64_t* l
     return wpre + inc - x;
 }
 
-// emqx_topic:words/1 of topic [b, e): word id of level k to tw[k] (k < WREG,
-// registers: AND-mask updates, no dynamic index) or lw[k] (k >= WREG);
-// returns the number of levels (N slashes -> N+1 levels, empty levels kept)
+// the next '/' of topic bytes [q, e) eight bytes at a time (e when none)
 template <class B>
 __device__ __forceinline__ uint64_t next_slash(const B& bytes, uint64_t q, uint64_t e, bool& found) {
-    found = false;   // next '/' at or after q, or e
+    found = false;
     while (q < e) {
         uint64_t word8 = bytes.word(q);
         uint32_t start = (uint32_t)(q & 7);
