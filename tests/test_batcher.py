@@ -74,3 +74,31 @@ def test_callback_threads_complete_every_topic_once():
     assert st["topics"] == 80000
     b.close()
     e.close()
+
+
+def test_backlog_partial_takes_complete_every_topic_once():
+    """producers far ahead of small batches: seals take a stripe's oldest
+    topics and leave the rest (head advance + compaction); every topic still
+    completes exactly once and each producer's topics complete in order"""
+    e = Engine(device=-1)
+    b = Batcher(e, max_topics=64, deadline_us=50, lanes_per_replica=1)
+    order = {}
+    lock = threading.Lock()
+
+    def producer(k):
+        for i in range(5000):
+            def cb(status, ids, dests, k=k, i=i):
+                with lock:
+                    order.setdefault(k, []).append(i)
+            b.submit(b"p/%d/%d" % (k, i), cb)
+    ts = [threading.Thread(target=producer, args=(k,)) for k in range(3)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    b.flush()
+    assert sorted(order) == [0, 1, 2]
+    for k in range(3):   # one lane: batches complete in seal order, a stripe's topics oldest first
+        assert order[k] == list(range(5000)), k
+    b.close()
+    e.close()
