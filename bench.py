@@ -414,6 +414,7 @@ def main():
                        "parallelism": "replicated trie x %d, topic batch split by rank" % world},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
+                         "traffic_frac": (traffic / HBM_PEAK_GBS) if traffic else None,
                          "traffic_source": ("FETCH_SIZE+WRITE_SIZE per launch from the PMC passes of the same kernel "
                                             "sources (profiles/traffic_c%d.json, kernel_src_sha %s), over this run's "
                                             "walk time" % (a.config, kernel_src_sha())) if traffic else None,
