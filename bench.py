@@ -55,8 +55,8 @@ def log(*a):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", type=int, default=3, help="SURVEY §8(d) config (3 = the metric's)")
     ap.add_argument("--filters", type=int, default=None, help="override filter count")
     ap.add_argument("--scaling", choices=["strong", "weak"], default="strong",
@@ -76,7 +76,7 @@ def parse():
     ap.add_argument("--check", type=int, default=20_000, help="topics of each batch checked bit-exactly vs O1")
     ap.add_argument("--streams", type=int, default=3,
                     help="streams the steps alternate over (batches overlap on the GPU; 1 = strictly serial)")
-    ap.add_argument("--roof-steps", type=int, default=5,
+    ap.add_argument("--roof-steps", type=int, default=20,
                     help="serial steps after the timed region that time each kernel for the roofline")
     ap.add_argument("--no-extras", action="store_true", help="skip the host-buffer and batcher legs")
     ap.add_argument("--walk", default=None, help="walk variant (queue|queue_xcd)")
@@ -108,8 +108,25 @@ def cpu_model():
     return platform.processor() or "unknown"
 
 
+def host_cpus():
+    """the CPUs this process may run on ("all host cores"):
+    the scheduler affinity mask, plus the cgroup v2 CPU quota when one is set
+    (quota / period CPUs), as evidence for the line"""
+    aff = sorted(os.sched_getaffinity(0))
+    quota = None
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            q, per = open(path).read().split()[:2]
+            quota = None if q == "max" else int(q) / int(per)
+        except (OSError, ValueError):
+            pass
+    return {"affinity_cpus": len(aff), "affinity_first_last": [aff[0], aff[-1]] if aff else None,
+            "cgroup_cpu_max_cpus": quota, "nproc": os.cpu_count()}
+
+
 def host_threads(a):
-    return a.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count())
+    """threads of the all-cores CPU legs: every CPU of the affinity mask"""
+    return a.cpu_threads or len(os.sched_getaffinity(0))
 
 
 def make_batches(a, cfg, rank, world):
@@ -192,7 +209,11 @@ def o1_check_and_baseline(a, fb, fo, n_filters, batches, results, do_cpu):
     if do_cpu:
         tb, to = batches[0]
         n = len(to) - 1
-        for name, k, th in [("o1_all", min(a.cpu_sample, n), threads), ("o1_1core", min(a.cpu_sample // 30, n), 1)]:
+        legs_o1 = [("o1_all", min(a.cpu_sample, n), threads)]
+        if threads != 16:   # the 16-thread leg of round 2's lines, for continuity
+            legs_o1.append(("o1_16", min(a.cpu_sample, n), 16))
+        legs_o1.append(("o1_1core", min(a.cpu_sample // 30, n), 1))
+        for name, k, th in legs_o1:
             legs[name] = median_leg(lambda b, o, t: o1.match_batch(b, o, threads=t)[0], tb, to, k, th)
             log("cpu %s: %.0f topics/s (%d topics, %d threads)" % (name, legs[name]["value"], k, th))
     o1.close()
@@ -367,7 +388,8 @@ def main():
                              "restatement of emqx_trie (string-path node ids, ETS-like {trie_edge, NodeId, "
                              "Word} tables), %d pthreads, 1 warm-up then the median of 5 runs of %d topics"
                              % (legs["o1_all"]["topics"], n_filters, th, legs["o1_all"]["topics"] // 5),
-                   "cpu_model": cpu_model(), "nproc": os.cpu_count(), "threads_used": th, "legs": legs}
+                   "cpu_model": cpu_model(), "nproc": os.cpu_count(), "threads_used": th,
+                   "host_cpus": host_cpus(), "legs": legs}
 
     if rank == 0:
         topics_per_step = sum(x[2] for x in dbat) / len(dbat) * (world if a.scaling == "weak" else 1)

@@ -145,6 +145,14 @@ SIGNATURES = [
                                     ctypes.c_uint32]),
     ("tm_route_del_batch", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                           ctypes.c_void_p, ctypes.c_uint32]),
+    ("tm_lease_begin", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]),
+    ("tm_lease_end", None, [ctypes.c_void_p, ctypes.c_uint64]),
+    ("tm_route_write", ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p,
+                                      ctypes.c_uint32]),
+    ("tm_route_delete_object", ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p,
+                                              ctypes.c_uint32]),
+    ("tm_route_write_batch", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                            ctypes.c_void_p, ctypes.c_uint32]),
     ("tm_get_routes", ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_void_p,
                                      ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]),
     ("tm_route_count", ctypes.c_uint64, [ctypes.c_void_p]),

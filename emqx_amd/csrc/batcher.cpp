@@ -437,6 +437,10 @@ struct tm_batcher {
             const uint32_t n = L.n;
             uint64_t total = 0, results = 0;
             int rc = host_only ? TM_EDEVICE : TM_OK;   // host-only: the GPU path only
+            // the batch's filter ids stay bound to their bytes until its
+            // callbacks have gathered them (tm_lease_begin)
+            uint64_t lease = 0;
+            const bool leased = rc == TM_OK && n && tm_lease_begin(eng, &lease) == TM_OK;
             if (rc == TM_OK && n) {
                 rc = pack(L) ? run_device(L, routes, deliv, total) : TM_ENOMEM;
                 if (rc == TM_OK)   // deliveries sit at route offsets: count the entries
@@ -444,6 +448,7 @@ struct tm_batcher {
             }
             const uint32_t m = n;
             run_callbacks(L, rc, routes, m);
+            if (leased) tm_lease_end(eng, lease);
             recycle(L.chunks);
             {
                 std::lock_guard<std::mutex> lk(L.mu);

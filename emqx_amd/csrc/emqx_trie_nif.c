@@ -18,6 +18,9 @@
  *                                                           (micro-batched: tm_batcher_*, H5)
  *   emqx_trie_nif:route_add(Engine, Topic, DestBin) -> ok   emqx_router add_route (src/emqx_router.erl:153-163)
  *   emqx_trie_nif:route_del(Engine, Topic, DestBin) -> ok   emqx_router del_route (:165-187)
+ *   emqx_trie_nif:route_write(Engine, Topic, DestBin) -> ok          emqx_route write event (bag only)
+ *   emqx_trie_nif:route_delete_object(Engine, Topic, DestBin) -> ok  emqx_route delete_object event
+ *                                   (bag only: node-down cleanup keeps the trie, emqx_router_helper.erl:156-160)
  *   emqx_trie_nif:match_routes_async(Engine, Topic) -> Ref; later {Ref, [{To, DestBin}]}
  *                                                           emqx_router:match_routes/1 (:116-118)
  *   emqx_trie_nif:dest_target(Engine, DestBin, node | group, Key) -> ok
@@ -32,7 +35,9 @@
  * {error, Atom}; the engine handle is a resource; GPU calls run on dirty IO
  * schedulers so a batch never blocks a normal scheduler.  The engine
  * serialises its own calls, so the NIF holds no lock of its own: a match
- * builds its reply terms while other calls proceed.  The module supports
+ * builds its reply terms while other calls proceed, under a filter id lease
+ * (tm_lease_begin) so a concurrent delete + insert never re-binds an id the
+ * reply still has to turn into a binary.  The module supports
  * hot code upgrade (the resource type is taken over by the new version).
  * The Erlang side is in erlang/ (emqx_trie_nif.erl, emqx_trie_gpu.erl,
  * emqx_trie_gpu_feed.erl).
@@ -175,36 +180,38 @@ static ERL_NIF_TERM nif_delete(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv
     return nif_filter_op(env, argc, argv, 0);
 }
 
-static ERL_NIF_TERM filter_binary(ErlNifEnv* env, tm_engine* e, uint32_t fid) {
-    uint64_t off[2];
-    tm_filters_gather(e, &fid, 1, NULL, 0, off);       /* length, under the engine lock */
-    ERL_NIF_TERM bin;
-    unsigned char* d = enif_make_new_binary(env, (size_t)off[1], &bin);
-    if (off[1]) tm_filters_gather(e, &fid, 1, d, off[1], off);
-    return bin;
-}
-
 /* n filter (or dest) ids -> n binaries, copied under the engine lock in one
- * call (safe beside subscribers that grow the engine's arenas) */
-static void make_binaries(ErlNifEnv* env, tm_engine* e, const uint32_t* ids, uint32_t n, int dests,
-                          ERL_NIF_TERM* out) {
+ * call (safe beside subscribers that grow the engine's arenas).  The caller
+ * holds a lease (tm_lease_begin) from before the match that produced the
+ * ids, so a deleted filter's id still names its own bytes.  Returns the
+ * gather's status; out[] is only valid on TM_OK. */
+static int make_binaries(ErlNifEnv* env, tm_engine* e, const uint32_t* ids, uint32_t n, int dests,
+                         ERL_NIF_TERM* out) {
     uint64_t* off = (uint64_t*)enif_alloc(sizeof(uint64_t) * (n + 1));
     uint64_t cap = (uint64_t)n * 48 + 64;
     uint8_t* buf = (uint8_t*)enif_alloc(cap);
+    if (!off || !buf) {
+        if (off) enif_free(off);
+        if (buf) enif_free(buf);
+        return TM_ENOMEM;
+    }
+    memset(off, 0, sizeof(uint64_t) * (n + 1));
     int rc = dests ? tm_dests_gather(e, ids, n, buf, cap, off) : tm_filters_gather(e, ids, n, buf, cap, off);
     if (rc == TM_ENOSPC) {
         cap = off[n];
         enif_free(buf);
         buf = (uint8_t*)enif_alloc(cap ? cap : 1);
-        rc = dests ? tm_dests_gather(e, ids, n, buf, cap, off) : tm_filters_gather(e, ids, n, buf, cap, off);
+        rc = buf ? (dests ? tm_dests_gather(e, ids, n, buf, cap, off) : tm_filters_gather(e, ids, n, buf, cap, off))
+                 : TM_ENOMEM;
     }
-    for (uint32_t k = 0; k < n; ++k) {
-        const size_t len = rc == TM_OK ? (size_t)(off[k + 1] - off[k]) : 0;
+    for (uint32_t k = 0; rc == TM_OK && k < n; ++k) {
+        const size_t len = (size_t)(off[k + 1] - off[k]);
         unsigned char* d = enif_make_new_binary(env, len, &out[k]);
         if (len) memcpy(d, buf + off[k], len);
     }
-    enif_free(buf);
+    if (buf) enif_free(buf);
     enif_free(off);
+    return rc;
 }
 
 static ERL_NIF_TERM nif_lookup(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
@@ -220,8 +227,10 @@ static ERL_NIF_TERM nif_lookup(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv
     } else if (rc != TM_OK) {
         res = error_tuple(env, rc);
     } else {
-        ERL_NIF_TERM topic = info.filter_id == TM_NO_FILTER ? atom(env, "undefined")
-                                                             : filter_binary(env, r->e, info.filter_id);
+        /* #trie_node.topic is the node id itself when set (emqx_trie.erl:67,
+         * :72): the argument binary, with no second engine call that a
+         * concurrent delete could race */
+        ERL_NIF_TERM topic = info.filter_id == TM_NO_FILTER ? atom(env, "undefined") : argv[1];
         res = enif_make_list1(env, enif_make_tuple2(env, enif_make_uint(env, info.edge_count), topic));
     }
     return res;
@@ -260,23 +269,26 @@ static ERL_NIF_TERM match_list(ErlNifEnv* env, engine_res* r, ERL_NIF_TERM list,
     uint64_t* out_off = (uint64_t*)enif_alloc(sizeof(uint64_t) * (n + 1));
     uint32_t* ids = NULL;
     uint64_t total = 0;
+    uint64_t lease = 0;
+    int rc = tm_lease_begin(r->e, &lease);   /* ids keep naming their filters until the gather below */
     /* the library sizes the id array at the exact total: one walk per batch */
-    int rc = tm_match_batch_owned(r->e, buf, off, n, counts, out_off, &ids, &total);
+    if (rc == TM_OK) rc = tm_match_batch_owned(r->e, buf, off, n, counts, out_off, &ids, &total);
     ERL_NIF_TERM res;
-    if (rc != TM_OK) {
-        res = error_tuple(env, rc);
-    } else {
+    if (rc == TM_OK) {
         ERL_NIF_TERM* rows = (ERL_NIF_TERM*)enif_alloc(sizeof(ERL_NIF_TERM) * (n ? n : 1));
-        for (unsigned i = 0; i < n; ++i) {
+        for (unsigned i = 0; i < n && rc == TM_OK; ++i) {
             uint32_t c = counts[i];
             ERL_NIF_TERM* cells = (ERL_NIF_TERM*)enif_alloc(sizeof(ERL_NIF_TERM) * (c ? c : 1));
-            make_binaries(env, r->e, ids + out_off[i], c, 0, cells);
-            rows[i] = enif_make_list_from_array(env, cells, c);
+            rc = make_binaries(env, r->e, ids + out_off[i], c, 0, cells);
+            if (rc == TM_OK) rows[i] = enif_make_list_from_array(env, cells, c);
             enif_free(cells);
         }
-        res = single ? rows[0] : enif_make_list_from_array(env, rows, n);
+        res = rc != TM_OK ? error_tuple(env, rc) : single ? rows[0] : enif_make_list_from_array(env, rows, n);
         enif_free(rows);
+    } else {
+        res = error_tuple(env, rc);
     }
+    tm_lease_end(r->e, lease);
     tm_free(ids);
     enif_free(out_off);
     enif_free(counts);
@@ -324,25 +336,30 @@ static void async_done(void* ctx, uint64_t ticket, int status, const uint32_t* i
                     if (len) memcpy(o, p, len);
                 }
             }
-        } else if (dests) {
-            make_binaries(env, q->r->e, dests, n, 1, db);
         }
+        int grc = TM_OK;
+        if (dests && q->mode != 2) grc = make_binaries(env, q->r->e, dests, n, 1, db);
         /* every filter binary of the list in ONE gather under the engine lock
-         * (the literal topic's own routes, TM_ROUTE_TOPIC, reuse its term) */
+         * (the literal topic's own routes, TM_ROUTE_TOPIC, reuse its term);
+         * the batcher holds the batch's lease until this callback returns */
         uint32_t* fids = (uint32_t*)enif_alloc(sizeof(uint32_t) * (n ? n : 1));
         ERL_NIF_TERM* fb = (ERL_NIF_TERM*)enif_alloc(sizeof(ERL_NIF_TERM) * (n ? n : 1));
         uint32_t nf = 0;
         for (uint32_t k = 0; k < n; ++k)
             if (ids[k] != TM_ROUTE_TOPIC) fids[nf++] = ids[k];
-        if (nf) make_binaries(env, q->r->e, fids, nf, 0, fb);
-        for (uint32_t k = 0, j = 0; k < n; ++k) {
-            ERL_NIF_TERM to = ids[k] == TM_ROUTE_TOPIC ? q->topic : fb[j++];
-            cells[k] = dests ? enif_make_tuple2(env, to, db[k]) : to;
+        if (grc == TM_OK && nf) grc = make_binaries(env, q->r->e, fids, nf, 0, fb);
+        if (grc == TM_OK) {
+            for (uint32_t k = 0, j = 0; k < n; ++k) {
+                ERL_NIF_TERM to = ids[k] == TM_ROUTE_TOPIC ? q->topic : fb[j++];
+                cells[k] = dests ? enif_make_tuple2(env, to, db[k]) : to;
+            }
+            res = enif_make_list_from_array(env, cells, n);
+        } else {
+            res = error_tuple(env, grc);
         }
         enif_free(fb);
         enif_free(fids);
         if (db) enif_free(db);
-        res = enif_make_list_from_array(env, cells, n);
         enif_free(cells);
     }
     enif_send(NULL, &q->pid, env, enif_make_tuple2(env, q->ref, res));
@@ -402,21 +419,32 @@ static ERL_NIF_TERM nif_dest_target(ErlNifEnv* env, int argc, const ERL_NIF_TERM
     return rc == TM_OK ? atom(env, "ok") : error_tuple(env, rc);
 }
 
-static ERL_NIF_TERM nif_route_op(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[], int add) {
+enum { ROUTE_ADD, ROUTE_DEL, ROUTE_WRITE, ROUTE_DELETE_OBJECT };
+static ERL_NIF_TERM nif_route_op(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[], int op) {
     engine_res* r;
     ErlNifBinary t, d;
     if (argc != 3 || !get_engine(env, argv[0], &r) || !enif_inspect_binary(env, argv[1], &t) ||
         !enif_inspect_binary(env, argv[2], &d))
         return enif_make_badarg(env);
-    int rc = add ? tm_route_add(r->e, t.data, (uint32_t)t.size, d.data, (uint32_t)d.size)
-                 : tm_route_del(r->e, t.data, (uint32_t)t.size, d.data, (uint32_t)d.size);
+    const uint32_t tl = (uint32_t)t.size, dl = (uint32_t)d.size;
+    int rc = op == ROUTE_ADD     ? tm_route_add(r->e, t.data, tl, d.data, dl)
+           : op == ROUTE_DEL     ? tm_route_del(r->e, t.data, tl, d.data, dl)
+           : op == ROUTE_WRITE   ? tm_route_write(r->e, t.data, tl, d.data, dl)
+                                 : tm_route_delete_object(r->e, t.data, tl, d.data, dl);
     return rc == TM_OK ? atom(env, "ok") : error_tuple(env, rc);
 }
 static ERL_NIF_TERM nif_route_add(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
-    return nif_route_op(env, argc, argv, 1);
+    return nif_route_op(env, argc, argv, ROUTE_ADD);
 }
 static ERL_NIF_TERM nif_route_del(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
-    return nif_route_op(env, argc, argv, 0);
+    return nif_route_op(env, argc, argv, ROUTE_DEL);
+}
+/* the emqx_route table events of the delta feed: the bag only, never the trie */
+static ERL_NIF_TERM nif_route_write(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    return nif_route_op(env, argc, argv, ROUTE_WRITE);
+}
+static ERL_NIF_TERM nif_route_delete_object(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    return nif_route_op(env, argc, argv, ROUTE_DELETE_OBJECT);
 }
 
 /* Deltas run on dirty CPU schedulers: they take the engine lock, which a
@@ -436,6 +464,8 @@ static ErlNifFunc funcs[] = {
     {"dest_target", 4, nif_dest_target, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"route_add", 3, nif_route_add, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"route_del", 3, nif_route_del, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"route_write", 3, nif_route_write, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"route_delete_object", 3, nif_route_delete_object, ERL_NIF_DIRTY_JOB_CPU_BOUND},
 };
 
 ERL_NIF_INIT(emqx_trie_nif, funcs, load, NULL, upgrade, NULL)

@@ -23,6 +23,7 @@
 #include <cstdlib>
 #include <condition_variable>
 #include <cstring>
+#include <deque>
 #include <functional>
 #include <map>
 #include <memory>
@@ -401,7 +402,7 @@ struct tm_engine {
     int device = -1;                  // first replica's HIP ordinal (-1: host-only engine)
     std::vector<std::unique_ptr<DevState>> devs;   // one replica per GPU (tm_open_devices)
     std::string last_error;
-    uint64_t epoch = 0;
+    std::atomic<uint64_t> epoch{0};   // commits published so far (the live image's epoch)
 
     // ---- word dictionary (host copy of dict/word_arena/word_off) ----
     std::vector<DictSlot> dict;
@@ -437,6 +438,39 @@ struct tm_engine {
     std::vector<uint8_t> filter_arena;
     std::vector<FilterRec> filters;
     std::vector<uint32_t> free_filters;
+    // Deferred filter id reuse.  A batch's ids name filters of the image it
+    // pinned, and its caller turns them into bytes afterwards (the NIF's
+    // callbacks, tm_filters_gather): a deleted filter's id is reusable only
+    // once no image holds it (two commits after the delete: both epochs
+    // rewritten) and no lease (tm_lease_begin: a reader between its match
+    // and its last gather) predates the commit that dropped it.  Until then
+    // the id keeps its bytes, and the gather keeps serving them.
+    std::deque<std::pair<uint64_t, uint32_t>> quarantine;   // (epoch from which images lack the id, id)
+    std::mutex lease_mu;                                     // leaf lock
+    std::multiset<uint64_t> leases;                          // epochs of the open leases
+    uint64_t lease_begin() {
+        std::lock_guard<std::mutex> lk(lease_mu);
+        const uint64_t x = epoch.load();
+        leases.insert(x);
+        return x;
+    }
+    void lease_end(uint64_t x) {
+        std::lock_guard<std::mutex> lk(lease_mu);
+        auto it = leases.find(x);
+        if (it != leases.end()) leases.erase(it);
+    }
+    void release_quarantine() {
+        if (quarantine.empty()) return;
+        std::lock_guard<std::mutex> lk(lease_mu);
+        const uint64_t now = epoch.load();
+        const uint64_t oldest = leases.empty() ? UINT64_MAX : *leases.begin();
+        while (!quarantine.empty()) {
+            const uint64_t vis = quarantine.front().first;
+            if (now < vis + 1 || oldest < vis) break;
+            free_filters.push_back(quarantine.front().second);
+            quarantine.pop_front();
+        }
+    }
     size_t live_filters = 0;
 
     // ---- device image (per replica: DevState) ----
@@ -674,7 +708,7 @@ struct tm_engine {
         e.parent = parent;
         e.word = word;
         e.child = child;
-        e.plus = c.plus;
+        e.plus = SLOT_RECORD ? c.plus : child_sum(child);
 #if TM_SLOT_RECORD
         e.hash_filter = c.hash_filter;
         e.lw = c.lw;
@@ -682,6 +716,23 @@ struct tm_engine {
         e.self_filter = c.self_filter;
 #endif
         return e;
+    }
+    // the summary a child's edge slot carries (image.h EdgeSlot): its own
+    // S(c), so the walk drops a table child whose subtree cannot match
+    uint32_t child_sum(uint32_t x) const { return summaries ? aux[x].sum : SUM_ALL; }
+    void refresh_slot_sum(uint32_t x) {
+        if (SLOT_RECORD) return;   // such slots carry the child's record instead
+        const uint32_t p = aux[x].parent, w = aux[x].word;
+        if (p == NODE_NONE || w == WORD_PLUS) return;
+        if (w != WORD_HASH && !(nodes[p].plus & WIDE)) return;
+        const size_t s = edge_find_slot(p, w);
+        if (s == SIZE_MAX) return;
+        EdgeSlot& e = tab(p).slots[s];
+        const uint32_t v = child_sum(x);
+        if (e.plus != v) {
+            e.plus = v;
+            tab(p).dirty.mark(s);
+        }
     }
     void edge_insert(uint32_t parent, uint32_t word, uint32_t child) {
         EdgeTable& t = tab(parent);
@@ -897,6 +948,7 @@ struct tm_engine {
             a.sum = (uint16_t)sum_union(a.sum, s);
             if (i > 0 && tmp_words[i - 1] < WORD_MAX)
                 aux[tmp_path[i - 1]].lsum = (uint16_t)sum_union(aux[tmp_path[i - 1]].lsum, a.sum);
+            if (i > 0) refresh_slot_sum(tmp_path[i]);
         }
         for (uint32_t i = 0; i < D; ++i) refresh_hf(tmp_path[i]);
     }
@@ -905,6 +957,7 @@ struct tm_engine {
     // filters
     uint32_t new_filter(const uint8_t* p, uint32_t len, uint32_t node) {
         uint32_t id;
+        if (free_filters.empty()) release_quarantine();
         if (!free_filters.empty()) {
             id = free_filters.back();
             free_filters.pop_back();
@@ -922,8 +975,8 @@ struct tm_engine {
     }
     void free_filter(uint32_t id) {
         on_filter_free(id);
-        filters[id].node = NODE_NONE;
-        free_filters.push_back(id);
+        filters[id].node = NODE_NONE;   // off / len stay: the gather serves the id until it is reused
+        quarantine.emplace_back(epoch.load() + 1, id);   // the next commit drops it from the images
         --live_filters;
     }
 
@@ -983,15 +1036,18 @@ struct tm_engine {
         dev_dirty = true;
         return id;
     }
-    // handle_cast({add_route, Route}) (:153-163) + add_trie_route/1 (:226-231)
-    void route_add(const uint8_t* t, uint32_t tlen, const uint8_t* d, uint32_t dlen) {
+    // handle_cast({add_route, Route}) (:153-163) + add_trie_route/1 (:226-231);
+    // trie = false: the bare mnesia:write of #route{} to emqx_route (a table
+    // event of the delta feed): the route bag only, the trie is driven by
+    // its own emqx_trie_node events
+    void route_add(const uint8_t* t, uint32_t tlen, const uint8_t* d, uint32_t dlen, bool trie = true) {
         const uint32_t dest = intern_dest(d, dlen);
         std::string key(reinterpret_cast<const char*>(t), tlen);
         auto it = route_bag.find(key);
         if (it != route_bag.end() && it->second.has(dest)) return;   // lists:member(Route, get_routes(Topic)) -> ok
         const bool wild = tm_topic_wildcard(t, tlen);
         if (it == route_bag.end()) {
-            if (wild) insert(t, tlen);   // mnesia:wread -> [] -> emqx_trie:insert
+            if (wild && trie) insert(t, tlen);   // mnesia:wread -> [] -> emqx_trie:insert
             it = route_bag.emplace(std::move(key), RouteRec{}).first;
             RouteRec& r = it->second;
             r.key = &it->first;
@@ -1012,8 +1068,11 @@ struct tm_engine {
     }
     // handle_cast({del_route, Route}) (:165-187) + del_trie_route/1 (:252-260)
     // or del_direct_route/1 (:240-241); the emqx_subscriber check (:179) is
-    // the broker's and stays in the caller
-    void route_del(const uint8_t* t, uint32_t tlen, const uint8_t* d, uint32_t dlen) {
+    // the broker's and stays in the caller.  trie = false: the bare
+    // mnesia:delete_object of #route{} (emqx_router_helper:cleanup_routes/1,
+    // src/emqx_router_helper.erl:156-160, deletes routes only: the filter
+    // stays in the trie and match/1 keeps returning it)
+    void route_del(const uint8_t* t, uint32_t tlen, const uint8_t* d, uint32_t dlen, bool trie = true) {
         auto di = dest_index.find(std::string(reinterpret_cast<const char*>(d), dlen));
         if (di == dest_index.end()) return;
         auto it = route_bag.find(std::string(reinterpret_cast<const char*>(t), tlen));
@@ -1039,7 +1098,7 @@ struct tm_engine {
         rt_dest_garbage += r.cap;
         rt_arena_garbage += r.words;
         route_bag.erase(it);
-        if (tm_topic_wildcard(t, tlen)) remove(t, tlen);
+        if (trie && tm_topic_wildcard(t, tlen)) remove(t, tlen);
         maybe_compact_routes();
     }
     const std::vector<uint32_t>* get_routes(const uint8_t* t, uint32_t tlen) const {
@@ -1532,6 +1591,7 @@ struct tm_engine {
         for (const EdgeSlot& e : old)
             if (e.word != WORD_HASH) bloom_add(nn[newid[e.parent]], e.word);
         nodes.swap(nn);
+        aux.swap(na);   // before the edges are placed: slot_for reads the children's new summaries
         hot_limit = new_hot_limit;
         size_t nhot = 0;
         for (const EdgeSlot& e : old) nhot += newid[e.parent] < hot_limit;
@@ -1547,7 +1607,6 @@ struct tm_engine {
         }
         for (FilterRec& f : filters)
             if (f.node != NODE_NONE) f.node = newid[f.node];
-        aux.swap(na);
         for (uint32_t v = 0; v < nodes.size(); ++v) nodes[v].hash_filter = hf_value(v);
         free_nodes.clear();
         created_since_layout = 0;
@@ -2517,6 +2576,16 @@ int tm_lookup(tm_engine* e, const uint8_t* node_id, uint32_t len, tm_node_info* 
     });
 }
 
+int tm_lease_begin(tm_engine* e, uint64_t* lease) {
+    if (!e || !lease) return TM_EINVAL;
+    *lease = e->lease_begin();
+    return TM_OK;
+}
+
+void tm_lease_end(tm_engine* e, uint64_t lease) {
+    if (e) e->lease_end(lease);
+}
+
 int tm_commit(tm_engine* e, uint64_t* epoch_out) {
     return guarded(e, [&] {
         e->commit();
@@ -2556,7 +2625,7 @@ int tm_filters_gather(tm_engine* e, const uint32_t* ids, uint32_t n, uint8_t* bu
         off[0] = 0;
         for (uint32_t i = 0; i < n; ++i) {
             const uint32_t f = ids[i];
-            if (f >= e->filters.size() || e->filters[f].node == NODE_NONE) throw ArgError("unknown filter id");
+            if (f >= e->filters.size()) throw ArgError("unknown filter id");   // deleted ids: their bytes until reuse
             const FilterRec& r = e->filters[f];
             if (o + r.len <= cap) std::memcpy(buf + o, e->filter_arena.data() + r.off, r.len);
             o += r.len;
@@ -2794,6 +2863,35 @@ int tm_route_del_batch(tm_engine* e, const uint8_t* topics, const uint64_t* topi
             throw ArgError("bad offsets");
         e->route_del(topics + topic_off[i], (uint32_t)(topic_off[i + 1] - topic_off[i]), dests + dest_off[i],
                      (uint32_t)(dest_off[i + 1] - dest_off[i]));
+    });
+}
+
+// the emqx_route table events (delta feed): the bag only, never the trie
+int tm_route_write(tm_engine* e, const uint8_t* topic, uint32_t tlen, const uint8_t* dest, uint32_t dlen) {
+    if ((!topic && tlen) || (!dest && dlen)) return TM_EINVAL;
+    return guarded(e, [&] {
+        e->route_add(topic, tlen, dest, dlen, false);
+        return TM_OK;
+    });
+}
+
+int tm_route_delete_object(tm_engine* e, const uint8_t* topic, uint32_t tlen, const uint8_t* dest, uint32_t dlen) {
+    if ((!topic && tlen) || (!dest && dlen)) return TM_EINVAL;
+    return guarded(e, [&] {
+        e->route_del(topic, tlen, dest, dlen, false);
+        return TM_OK;
+    });
+}
+
+int tm_route_write_batch(tm_engine* e, const uint8_t* topics, const uint64_t* topic_off, const uint8_t* dests,
+                         const uint64_t* dest_off, uint32_t n) {
+    if (n && (!topics || !topic_off || !dests || !dest_off)) return TM_EINVAL;
+    return chunked(e, n, [&](uint32_t i) {
+        if (topic_off[i + 1] < topic_off[i] || topic_off[i + 1] - topic_off[i] > 0xFFFFFFFFull ||
+            dest_off[i + 1] < dest_off[i] || dest_off[i + 1] - dest_off[i] > 0xFFFFFFFFull)
+            throw ArgError("bad offsets");
+        e->route_add(topics + topic_off[i], (uint32_t)(topic_off[i + 1] - topic_off[i]), dests + dest_off[i],
+                     (uint32_t)(dest_off[i + 1] - dest_off[i]), false);
     });
 }
 
@@ -3129,7 +3227,10 @@ int tm_set_option(tm_engine* e, const char* name, int64_t value) {
             if ((int)value != e->summaries) {
                 e->summaries = (int)value;
                 for (uint32_t v = 0; v < e->nodes.size(); ++v)
-                    if (e->aux[v].parent != NODE_NONE || v == ROOT) e->refresh_hf(v);
+                    if (e->aux[v].parent != NODE_NONE || v == ROOT) {
+                        e->refresh_hf(v);
+                        e->refresh_slot_sum(v);
+                    }
                 e->dev_dirty = true;
             }
             return TM_OK;

@@ -76,8 +76,9 @@ struct alignas(32) Node {
 static_assert(sizeof(Node) == 32, "node record is two 16 B halves");
 
 // Edge slot layout (build-time A/B, TM_SLOT_RECORD):
-//   0: 16 B {parent, word, child, child.plus}: the probe finds the child id,
-//      the child's visit loads its node half;
+//   0: 16 B {parent, word, child, S(child)}: the probe finds the child id
+//      and the child's own subtree summary (a child that cannot match below
+//      is dropped), the child's visit loads its node half;
 //   1: 32 B, second half {child.hash_filter, child.lw, child.lc,
 //      child.self_filter}: the probe that finds the edge also delivers the
 //      child's record (same 64 B sector), at twice the table footprint.
@@ -89,7 +90,7 @@ struct alignas(SLOT_RECORD ? 32 : 16) EdgeSlot {
     uint32_t parent;       // EDGE_EMPTY when free
     uint32_t word;
     uint32_t child;
-    uint32_t plus;         // child's record ...
+    uint32_t plus;         // TM_SLOT_RECORD 0: S(child), the child's subtree summary; 1: child's record ...
 #if TM_SLOT_RECORD
     uint32_t hash_filter;
     uint32_t lw;

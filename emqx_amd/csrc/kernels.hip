@@ -311,7 +311,7 @@ __device__ __forceinline__ Hit probe_edge(const ImageView& im, uint32_t v, uint3
         const uint4 e = (TM_NT_PROBE && !hot) ? nt_load16(slot) : slot[0];
         if (STATS) ++loads;
         if (e.x == v && e.y == w) {
-            if (!SLOT_RECORD) return Hit{e.z, 0, 0, 0, 0, 0, false};
+            if (!SLOT_RECORD) return Hit{e.z, e.w, 0, 0, 0, 0, false};   // plus: the child's summary S(c)
             const uint4 d = slot[1];   // same 32 B: hash_filter, lw, lc, self_filter
             return Hit{e.z, e.w, d.x, d.y, d.z, d.w, true};
         }
@@ -329,12 +329,12 @@ __device__ __forceinline__ Hit lit_child(const ImageView& im, uint32_t v, uint32
                                          uint32_t w, uint64_t& loads) {
     const Hit none{NODE_NONE, 0, 0, 0, 0, 0, false};
     if (w < WORD_MAX) {
-        if (!(plus & WIDE)) return Hit{lw == w ? lc : NODE_NONE, 0, 0, 0, 0, 0, false};
+        if (!(plus & WIDE)) return Hit{lw == w ? lc : NODE_NONE, SUM_ALL, 0, 0, 0, 0, false};
         const uint64_t b = word_bloom(w);
         const uint64_t mask = ((uint64_t)lc << 32) | lw;
         return (mask & b) == b ? probe_edge<STATS>(im, v, w, loads) : none;
     }
-    if (w == WORD_PLUS) return Hit{plus & NODE_MASK, 0, 0, 0, 0, 0, false};
+    if (w == WORD_PLUS) return Hit{plus & NODE_MASK, SUM_ALL, 0, 0, 0, 0, false};
     if (w == WORD_HASH) return probe_edge<STATS>(im, v, WORD_HASH, loads);
     return none;   // WORD_NONE: bytes no filter contains
 }
@@ -501,8 +501,13 @@ __device__ __forceinline__ bool walk_step(const ImageView& im, Cursor& c, Path p
             plus_ok = sum_useful(hf & SUM_ALL, k);
             lit_ok = w < WORD_MAX ? sum_useful((hf >> 15) & SUM_ALL, k) : w == WORD_PLUS ? plus_ok : true;
         }
-        const Hit g = (!STATS && !lit_ok) ? Hit{NODE_NONE, 0, 0, 0, 0, 0, false}
-                                          : lit_child<STATS>(im, v, plus, lw, lc, w, st.probe_loads);
+        Hit g = (!STATS && !lit_ok) ? Hit{NODE_NONE, 0, 0, 0, 0, 0, false}
+                                    : lit_child<STATS>(im, v, plus, lw, lc, w, st.probe_loads);
+        // a table child's own summary (its edge slot's fourth word): the
+        // union summary above admitted the literal children as a whole
+        const bool child_ok = SLOT_RECORD || g.child == NODE_NONE || sum_useful(g.plus & SUM_ALL, c.n - r - 1);
+        if (STATS) st.prunable += (g.child != NODE_NONE && lit_ok && !child_ok) ? 1u : 0u;
+        if (!STATS && !child_ok) g.child = NODE_NONE;
         if (STATS && st.hist) {
             const uint32_t lv = r < 15 ? r : 15;
             atomicAdd(st.hist + lv, 1ull);

@@ -104,6 +104,23 @@ class Engine:
         topic = None if info.filter_id == L.TM_NO_FILTER else self.filter_bytes(info.filter_id)
         return [(info.edge_count, topic)]
 
+    def lease(self):
+        """a filter id lease (tm_lease_begin/end), as a context manager: ids
+        returned by matches inside it keep naming their filters (a deleted
+        filter's id is not reused, its bytes stay gatherable) until it ends"""
+        eng = self
+
+        class _Lease:
+            def __enter__(self):
+                x = ctypes.c_uint64()
+                eng._check(eng.lib.tm_lease_begin(eng.h, ctypes.byref(x)), "tm_lease_begin")
+                self.x = x.value
+                return self
+
+            def __exit__(self, *a):
+                eng.lib.tm_lease_end(eng.h, self.x)
+        return _Lease()
+
     def commit(self):
         ep = ctypes.c_uint64()
         self._check(self.lib.tm_commit(self.h, ctypes.byref(ep)), "tm_commit")
@@ -237,6 +254,27 @@ class Engine:
         doff = np.ascontiguousarray(doff, dtype=np.uint64)
         return self._check(self.lib.tm_route_del_batch(self.h, _ptr(tbuf), _ptr(toff), _ptr(dbuf), _ptr(doff), n),
                            "tm_route_del_batch")
+
+    # the emqx_route table events of the delta feed (route bag only, never
+    # the trie: emqx_trie_gpu_feed.erl drives the trie from emqx_trie_node)
+    def route_write(self, topic: bytes, dest: bytes):
+        """mnesia:write(emqx_route, #route{}) (add_trie_route/1 :231, add_direct_route/1 :223-224)"""
+        return self._check(self.lib.tm_route_write(self.h, topic, len(topic), dest, len(dest)), "tm_route_write")
+
+    def route_delete_object(self, topic: bytes, dest: bytes):
+        """mnesia:delete_object(emqx_route, #route{}) (del_trie_route/1 :255-258,
+        emqx_router_helper:cleanup_routes/1 :156-160): the filter stays in the trie"""
+        return self._check(self.lib.tm_route_delete_object(self.h, topic, len(topic), dest, len(dest)),
+                           "tm_route_delete_object")
+
+    def route_write_many(self, tbuf, toff, dbuf, doff):
+        n = len(toff) - 1
+        tbuf = np.ascontiguousarray(tbuf, dtype=np.uint8)
+        toff = np.ascontiguousarray(toff, dtype=np.uint64)
+        dbuf = np.ascontiguousarray(dbuf, dtype=np.uint8)
+        doff = np.ascontiguousarray(doff, dtype=np.uint64)
+        return self._check(self.lib.tm_route_write_batch(self.h, _ptr(tbuf), _ptr(toff), _ptr(dbuf), _ptr(doff), n),
+                           "tm_route_write_batch")
 
     def get_routes(self, topic: bytes):
         """dest ids of topic's routes, insertion order (get_routes/1)"""

@@ -8,7 +8,7 @@
 
 -export([open/1, insert/2, delete/2, lookup/2, commit/1, match/2, match_many/2,
          match_async/2, match_routes_async/2, match_deliveries_async/2,
-         dest_target/4, route_add/3, route_del/3]).
+         dest_target/4, route_add/3, route_del/3, route_write/3, route_delete_object/3]).
 
 -on_load(init/0).
 
@@ -39,3 +39,8 @@ dest_target(_Engine, _DestBin, _Kind, _Key) -> erlang:nif_error(nif_not_loaded).
 %% emqx_router add/del route (src/emqx_router.erl:153-187, 226-260)
 route_add(_Engine, _Topic, _DestBin) -> erlang:nif_error(nif_not_loaded).
 route_del(_Engine, _Topic, _DestBin) -> erlang:nif_error(nif_not_loaded).
+%% the emqx_route table events (emqx_trie_gpu_feed): the route bag only, never
+%% the trie -- mnesia:write / mnesia:delete_object of #route{}
+%% (src/emqx_router.erl:223-224, 231, 240-241, 255-257; emqx_router_helper.erl:156-160)
+route_write(_Engine, _Topic, _DestBin) -> erlang:nif_error(nif_not_loaded).
+route_delete_object(_Engine, _Topic, _DestBin) -> erlang:nif_error(nif_not_loaded).

@@ -129,6 +129,18 @@ int tm_delete_batch(tm_engine* e, const uint8_t* bytes, const uint64_t* off, uin
  * binary (emqx_topic:join of the words).  TM_ENOENT when the node is absent. */
 int tm_lookup(tm_engine* e, const uint8_t* node_id, uint32_t len, tm_node_info* out);
 
+/* Filter id leases.  The ids a match returns name filters of the image
+ * epoch it ran on; a caller that turns them into bytes later
+ * (tm_filters_gather, the NIF's reply terms) holds a lease from before the
+ * match until its last gather: a deleted filter's id is not reused while a
+ * lease older than the deletion's commit is open, nor before both image
+ * epochs have dropped it, and tm_filters_gather keeps returning its bytes
+ * until then.  (The reference hands out the filter binaries themselves:
+ * emqx_trie.erl:79.)  The micro-batcher leases each batch through its
+ * callbacks. */
+int  tm_lease_begin(tm_engine* e, uint64_t* lease);
+void tm_lease_end(tm_engine* e, uint64_t lease);
+
 /* Publish pending deltas to the HBM image (mnesia transaction commit,
  * src/emqx_router.erl:264-268).  tm_match_* commit implicitly. */
 int tm_commit(tm_engine* e, uint64_t* epoch_out);
@@ -303,6 +315,28 @@ int tm_route_del(tm_engine* e, const uint8_t* topic, uint32_t tlen, const uint8_
 /* Bulk tm_route_del, laid out as tm_route_add_batch, applied in order. */
 int tm_route_del_batch(tm_engine* e, const uint8_t* topics, const uint64_t* topic_off, const uint8_t* dests,
                        const uint64_t* dest_off, uint32_t n);
+
+/* The emqx_route table events the delta feed receives
+ * (mnesia:subscribe({table, emqx_route, detailed}); erlang/emqx_trie_gpu_feed.erl):
+ * the route bag ONLY, never the trie, whose membership the feed drives from
+ * emqx_trie_node events alone (tm_insert / tm_delete).
+ *   tm_route_write          = mnesia:write(emqx_route, #route{}) — add_trie_route/1
+ *                             :231, add_direct_route/1 :223-224; an existing
+ *                             route is a no-op, a new one goes last in its bag.
+ *   tm_route_delete_object  = mnesia:delete_object(emqx_route, #route{}) —
+ *                             del_trie_route/1 :255-258, del_direct_route/1
+ *                             :240-241 and the node-down cleanup
+ *                             emqx_router_helper:cleanup_routes/1
+ *                             (src/emqx_router_helper.erl:156-160), which deletes
+ *                             routes only: a stale filter stays in the trie and
+ *                             emqx_trie:match/1 keeps returning it.  Absent: no-op.
+ * A wildcard topic's routes join its trie filter whenever both exist, in either
+ * order of arrival (match_routes/1 finds routes through the filter). */
+int tm_route_write(tm_engine* e, const uint8_t* topic, uint32_t tlen, const uint8_t* dest, uint32_t dlen);
+int tm_route_delete_object(tm_engine* e, const uint8_t* topic, uint32_t tlen, const uint8_t* dest, uint32_t dlen);
+/* Bulk tm_route_write (the feed's boot snapshot), laid out as tm_route_add_batch. */
+int tm_route_write_batch(tm_engine* e, const uint8_t* topics, const uint64_t* topic_off, const uint8_t* dests,
+                         const uint64_t* dest_off, uint32_t n);
 
 /* get_routes/1 — :89-90: the dest ids of topic's routes in insertion order;
  * *out_n = their number (TM_ENOSPC when it exceeds cap). */

@@ -140,10 +140,27 @@ def _nk(node_id):
 
 
 class Trie:
-    def __init__(self):
+    def __init__(self, events=None):
         self.trie = {}        # ?TRIE
         self.trie_node = {}   # ?TRIE_NODE: key -> [edge_count, topic or None]
         self.edge_reads = 0   # mnesia:read(?TRIE, ...) calls during match
+        # events: a list that records the emqx_trie_node table events a
+        # mnesia:subscribe({table, emqx_trie_node, detailed}) subscriber
+        # receives, in write order: ("write", "emqx_trie_node", node_id,
+        # edge_count, topic) / ("delete", "emqx_trie_node", node_id); node_id
+        # is bytes or ROOT (the atom root)
+        self.events = events
+
+    def _w(self, key):
+        if self.events is not None:
+            rec = self.trie_node[key]
+            nid = ROOT if key[0] == "atom" else key[1]
+            self.events.append(("write", "emqx_trie_node", nid, rec[0], rec[1]))
+
+    def _d(self, key):
+        if self.events is not None:
+            nid = ROOT if key[0] == "atom" else key[1]
+            self.events.append(("delete", "emqx_trie_node", nid))
 
     # insert/1 — src/emqx_trie.erl:62-73
     def insert(self, topic: bytes):
@@ -152,10 +169,12 @@ class Trie:
             return
         if rec is not None and rec[1] is None:
             rec[1] = topic
+            self._w(_nk(topic))
             return
         for t in triples(topic):
             self._add_path(t)
         self.trie_node[_nk(topic)] = [0, topic]
+        self._w(_nk(topic))
 
     # add_path/1 — src/emqx_trie.erl:104-117
     def _add_path(self, triple):
@@ -164,9 +183,11 @@ class Trie:
         if rec is not None:
             if _ek(node, w) not in self.trie:
                 rec[0] += 1
+                self._w(_nk(node))
                 self.trie[_ek(node, w)] = child
         else:
             self.trie_node[_nk(node)] = [1, None]
+            self._w(_nk(node))
             self.trie[_ek(node, w)] = child
 
     # match/1 — src/emqx_trie.erl:77-79
@@ -216,9 +237,11 @@ class Trie:
             return
         if rec[0] == 0:
             del self.trie_node[_nk(topic)]
+            self._d(_nk(topic))
             self._delete_path(list(reversed(triples(topic))))
         else:
             rec[1] = None
+            self._w(_nk(topic))
 
     # delete_path/1 — src/emqx_trie.erl:149-163
     def _delete_path(self, path):
@@ -229,8 +252,10 @@ class Trie:
                 raise RuntimeError(("node_not_found", node_id))   # mnesia:abort
             if rec[0] == 1 and rec[1] is None:
                 del self.trie_node[_nk(node_id)]
+                self._d(_nk(node_id))
                 continue
             rec[0] -= 1
+            self._w(_nk(node_id))
             return
 
 
@@ -287,8 +312,12 @@ class RouteTable:
     (:226-231), handle_cast del_route (:165-187) + del_trie_route/1
     (:252-260) / del_direct_route/1 (:240-241), get_routes/1 (:89-90)."""
 
-    def __init__(self):
-        self.trie = Trie()
+    def __init__(self, events=None):
+        # events: a list recording the emqx_trie_node and emqx_route table
+        # events (Trie.events; ("write" | "delete_object", "emqx_route",
+        # topic, dest)) in the order the transactions write them
+        self.events = events
+        self.trie = Trie(events)
         self.routes = {}
 
     def add_route(self, topic: bytes, dest):
@@ -298,16 +327,36 @@ class RouteTable:
         if wildcard(topic) and not bag:       # mnesia:wread -> [] -> emqx_trie:insert
             self.trie.insert(topic)
         self.routes.setdefault(topic, []).append(dest)
+        if self.events is not None:           # mnesia:write(?ROUTE, Route, ...) :231 / :224
+            self.events.append(("write", "emqx_route", topic, dest))
 
     def del_route(self, topic: bytes, dest):
         bag = self.routes.get(topic)
         if not bag or dest not in bag:        # [] -> ok / delete_object of an absent route
             return
+        if self.events is not None:           # mnesia:delete_object(?ROUTE, Route, ...) :255 / :257 / :241
+            self.events.append(("delete_object", "emqx_route", topic, dest))
         if wildcard(topic) and bag == [dest]:  # [Route] -> delete route and trie path
             self.trie.delete(topic)
         bag.remove(dest)
         if not bag:
             del self.routes[topic]
+
+    def cleanup_routes(self, node):
+        """emqx_router_helper:cleanup_routes/1 (src/emqx_router_helper.erl:
+        156-160), run on nodedown (:118-124): delete_object of every route
+        whose dest is Node or {_, Node} -- routes ONLY, the trie keeps the
+        filters (stale filters: match/1 still returns them)"""
+        pats = [lambda d: not isinstance(d, tuple) and d == node,      # #route{dest = Node}
+                lambda d: isinstance(d, tuple) and d[1] == node]       # #route{dest = {'_', Node}}
+        for pat in pats:
+            for topic in list(self.routes):
+                for dest in [d for d in self.routes[topic] if pat(d)]:
+                    self.routes[topic].remove(dest)
+                    if self.events is not None:
+                        self.events.append(("delete_object", "emqx_route", topic, dest))
+                if not self.routes[topic]:
+                    del self.routes[topic]
 
     def get_routes(self, topic: bytes):
         return list(self.routes.get(topic, []))
