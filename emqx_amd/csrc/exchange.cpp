@@ -62,12 +62,24 @@ struct Buf {
 
 inline uint32_t slice_lo(uint32_t n, uint32_t S, uint32_t d) { return (uint32_t)((uint64_t)n * d / S); }
 
+
+// The RCCL group this thread has open (ncclGroupStart .. ncclGroupEnd) and
+// the communicators queued into it.  A failure between the two must not
+// return with the group open (the next collective on these communicators
+// would be queued into the broken group): fail() closes it and aborts those
+// communicators, whose operations the peers can no longer complete; later
+// exchanges on them report TM_EDEVICE.
+thread_local int t_group_depth = 0;
+thread_local std::vector<tm_comm*> t_group_comms;
+
+int fail(tm_comm* c, const std::string& what, int code = TM_EDEVICE);
 }  // namespace
 
 struct tm_comm {
     int device = -1;
     uint32_t nranks = 1, rank = 0;
     ncclComm_t nccl = nullptr;    // RCCL backend (null: device copies within one process)
+    bool aborted = false;         // aborted after a failure inside an RCCL group
     hipStream_t stream = nullptr;
     Buf sizes;                    // 2S u64: send counts per destination, then their first ids
     Buf rsizes;                   // S u64: ids to receive from each source
@@ -77,9 +89,20 @@ struct tm_comm {
 };
 
 namespace {
-
-int fail(tm_comm* c, const std::string& what, int code = TM_EDEVICE) {
+int fail(tm_comm* c, const std::string& what, int code) {
     if (c) c->last_error = what;
+    if (t_group_depth > 0) {
+        t_group_depth = 0;
+        (void)ncclGroupEnd();
+        for (tm_comm* g : t_group_comms)
+            if (g && g->nccl && !g->aborted) {
+                (void)ncclCommAbort(g->nccl);
+                g->nccl = nullptr;
+                g->aborted = true;
+                if (g != c) g->last_error = "aborted with its RCCL group: " + what;
+            }
+        t_group_comms.clear();
+    }
     return code;
 }
 #define XHIP(c, x)                                                                          \
@@ -91,6 +114,19 @@ int fail(tm_comm* c, const std::string& what, int code = TM_EDEVICE) {
     do {                                                                                        \
         ncclResult_t _r = (x);                                                                  \
         if (_r != ncclSuccess) return fail(c, std::string(#x) + ": " + ncclGetErrorString(_r)); \
+    } while (0)
+
+#define XGROUP_START(c, comms)                 \
+    do {                                       \
+        XNCCL(c, ncclGroupStart());            \
+        ++t_group_depth;                       \
+        t_group_comms = (comms);               \
+    } while (0)
+#define XGROUP_END(c)                          \
+    do {                                       \
+        t_group_depth = 0;                     \
+        t_group_comms.clear();                 \
+        XNCCL(c, ncclGroupEnd());              \
     } while (0)
 
 hipStream_t stream_of(tm_comm* c, const tm_exchange_in& in) {
@@ -213,6 +249,7 @@ const char* tm_comm_last_error(tm_comm* c) { return c ? c->last_error.c_str() : 
 // one rank of a multi-process (or one-rank) RCCL exchange
 int tm_shard_exchange(tm_comm* c, const tm_exchange_in* in, tm_exchange_out* out) {
     if (!c || !in || !out || !valid_in(*in)) return TM_EINVAL;
+    if (c->aborted) return fail(c, "communicator aborted after a failed RCCL group");
     if (!c->nccl) return fail(c, "tm_shard_exchange needs an RCCL communicator (use tm_shard_exchange_group)",
                               TM_EINVAL);
     if (hipSetDevice(c->device) != hipSuccess) return TM_EDEVICE;
@@ -223,21 +260,21 @@ int tm_shard_exchange(tm_comm* c, const tm_exchange_in* in, tm_exchange_out* out
     const uint32_t m = slice_lo(n, S, me + 1) - slice_lo(n, S, me);
     if (!c->recv_counts.ensure((size_t)S * m * 4 + 4)) return fail(c, "hipMalloc", TM_ENOMEM);
     // counts of slice p -> rank p, and the id count of each slice (all-to-all of one u64)
-    XNCCL(c, ncclGroupStart());
+    XGROUP_START(c, std::vector<tm_comm*>{c});
     for (uint32_t p = 0; p < S; ++p) {
         const uint32_t lo = slice_lo(n, S, p), mp = slice_lo(n, S, p + 1) - lo;
         XNCCL(c, ncclSend(in->d_counts + lo, mp, ncclUint32, (int)p, c->nccl, st));
         XNCCL(c, ncclRecv(c->recv_counts.as<uint32_t>() + (size_t)p * m, m, ncclUint32, (int)p, c->nccl, st));
     }
     XNCCL(c, ncclAllToAll(c->sizes.p, c->rsizes.p, 1, ncclUint64, c->nccl, st));
-    XNCCL(c, ncclGroupEnd());
+    XGROUP_END(c);
     c->h_recv.resize(S);
     XHIP(c, hipMemcpyAsync(c->h_recv.data(), c->rsizes.p, S * 8, hipMemcpyDeviceToHost, st));
     XHIP(c, hipStreamSynchronize(st));
     rc = alloc_recv(c, *in, *out);
     if (rc != TM_OK) return rc;
     // ids, then each key plane: slice p -> rank p
-    XNCCL(c, ncclGroupStart());
+    XGROUP_START(c, std::vector<tm_comm*>{c});
     uint64_t base = 0;
     for (uint32_t p = 0; p < S; ++p) {
         const uint64_t items = c->h_send[p], from = c->h_send[S + p], ritems = c->h_recv[p];
@@ -250,7 +287,7 @@ int tm_shard_exchange(tm_comm* c, const tm_exchange_in* in, tm_exchange_out* out
         }
         base += ritems;
     }
-    XNCCL(c, ncclGroupEnd());
+    XGROUP_END(c);
     return TM_OK;
 }
 
@@ -277,11 +314,12 @@ int tm_shard_exchange_group(tm_comm** comms, uint32_t S, const tm_exchange_in* i
         int rc = alloc_recv(c, ins[d], outs[d]);
         if (rc != TM_OK) return rc;
     }
-    if (rccl) XNCCL(comms[0], ncclGroupStart());
+    const std::vector<tm_comm*> group(comms, comms + S);
+    if (rccl) XGROUP_START(comms[0], group);
     for (uint32_t d = 0; d < S; ++d) {
         tm_comm* c = comms[d];
         hipStream_t st = stream_of(c, ins[d]);
-        if (hipSetDevice(c->device) != hipSuccess) return TM_EDEVICE;
+        if (hipSetDevice(c->device) != hipSuccess) return fail(c, "hipSetDevice");
         const uint32_t m = outs[d].m;
         uint64_t base = 0;
         for (uint32_t s = 0; s < S; ++s) {
@@ -320,7 +358,7 @@ int tm_shard_exchange_group(tm_comm** comms, uint32_t S, const tm_exchange_in* i
             }
         }
     }
-    if (rccl) XNCCL(comms[0], ncclGroupEnd());
+    if (rccl) XGROUP_END(comms[0]);
     return TM_OK;
 }
 

@@ -81,12 +81,55 @@ class Rewrite:
         return out
 
 
+def _erl_replacement(val: bytes, whole: bytes) -> bytes:
+    """the Replacement argument of re:replace/4 expanded for a pattern with
+    no subexpressions (OTP re docs: '&' inserts the whole match, \\N /
+    \\gN / \\g{N} subexpression N -- 0 the whole match, none other exists
+    here, so nothing -- and \\& / \\\\ a literal '&' / backslash; a
+    backslash before any other byte keeps that byte).  Parity unpinned: the
+    reference holds no vector for it (tests/test_rewrite.py works cases by
+    hand)."""
+    out, i, n = bytearray(), 0, len(val)
+    while i < n:
+        c = val[i]
+        if c == 0x26:                                   # '&'
+            out += whole
+            i += 1
+        elif c == 0x5C and i + 1 < n:                   # backslash
+            d = val[i + 1]
+            j = i + 1
+            if d == 0x67 and i + 2 < n and val[i + 2] == 0x7B:   # \g{N}
+                k = val.find(b"}", i + 3)
+                if k > i + 3 and val[i + 3:k].isdigit():
+                    out += whole if int(val[i + 3:k]) == 0 else b""
+                    i = k + 1
+                    continue
+            if d == 0x67:                               # \gN
+                j = i + 2
+            k = j
+            while k < n and 0x30 <= val[k] <= 0x39:
+                k += 1
+            if k > j:                                   # \N, \gN
+                out += whole if int(val[j:k]) == 0 else b""
+                i = k
+            else:                                       # \& \\ \x -> the byte
+                out.append(d)
+                i += 2
+        else:
+            out.append(c)
+            i += 1
+    return bytes(out)
+
+
 def match_regx(topic: bytes, mp, dest: bytes) -> bytes:
-    """match_regx/3 (src/emqx_mod_rewrite.erl:61-71)"""
+    """match_regx/3 (src/emqx_mod_rewrite.erl:61-71): for I = 1..n,
+    re:replace(Acc, "\\$I", Val_I, [global]) -- every "$I" of Acc (also the
+    "$1" inside "$10"), with Val_I's replacement metacharacters expanded"""
     m = mp.search(topic)
     if m is None:
         return topic
     acc = dest
     for i, val in enumerate(m.groups(), start=1):     # foldl over [{"\\$1", V1}, ...]
-        acc = acc.replace(b"$%d" % i, val if val is not None else b"")
+        var = b"$%d" % i
+        acc = acc.replace(var, _erl_replacement(val if val is not None else b"", var))
     return acc

@@ -30,3 +30,20 @@ def test_host_only_rewrite_refuses():
         rw.rule_index_batch(*pack([b"a/b"]))
     assert ex.value.code == L.TM_EDEVICE
     rw.close()
+
+
+def test_match_regx_replacement_metacharacters():
+    """re:replace/4's Replacement (emqx_mod_rewrite.erl:66-68): a captured level
+    holding '&' or a backslash is expanded, not copied (OTP re docs; worked by
+    hand, parity unpinned: the reference holds no vector for it)"""
+    mp = re.compile(rb"^a/(.+)/(.+)$")
+    # '&' = the whole match of "\$1", i.e. the text "$1"; the next fold step
+    # (I = 2) does not touch it again
+    assert match_regx(b"a/b&c/d", mp, b"x/$1/$2") == b"x/b$1c/d"
+    # \1: subexpression 1 of the pattern "\$1", which has none: nothing
+    assert match_regx(b"a/b\\1c/d", mp, b"x/$1/$2") == b"x/bc/d"
+    # \& and \\ are the literal characters
+    assert match_regx(b"a/b\\&c/d\\\\e", mp, b"$2+$1") == b"d\\e+b&c"
+    # "$1" also matches inside "$10" (the fold runs I = 1 first)
+    mp10 = re.compile(rb"^" + rb"/".join([rb"(.)"] * 10) + rb"$")
+    assert match_regx(b"a/b/c/d/e/f/g/h/i/j", mp10, b"$10|$1") == b"a0|a"
