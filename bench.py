@@ -129,6 +129,18 @@ def host_threads(a):
     return a.cpu_threads or len(os.sched_getaffinity(0))
 
 
+def insert_progress(eng, fb, fo, rank, chunk=10_000_000):
+    """insert_many in slices of `chunk` filters with a log line per slice
+    (a 100M-filter build takes minutes: the GPU job runner wants output)"""
+    n = len(fo) - 1
+    t0 = time.time()
+    for lo in range(0, n, chunk):
+        hi = min(n, lo + chunk)
+        eng.insert_many(fb[int(fo[lo]):int(fo[hi])], (fo[lo:hi + 1] - fo[lo]).astype(np.uint64))
+        if n > chunk:
+            log("rank %d: inserted %d / %d filters (%.0fs)" % (rank, hi, n, time.time() - t0))
+
+
 def make_batches(a, cfg, rank, world):
     """this rank's topic batches: strong = slice `rank` of each global batch,
     weak = batches of its own stream"""
@@ -190,8 +202,30 @@ def cpu_baseline(a, fb, fo, n_filters, tb, to):
     return res
 
 
+def o3_check(a, fb, fo, n_filters, batches, results):
+    """filter sets too large for O1's string-path tables (C4: 100M filters):
+    the check runs against O3, the same algorithm over interned ids"""
+    from oracle import O3   # checker only
+    t0 = time.time()
+    o3 = O3(n_filters)
+    o3.insert_many(fb, fo)
+    log("oracle O3 built in %.1fs" % (time.time() - t0))
+    ok = True
+    for (tb, to), (dc, doo, di) in zip(batches, results):
+        k = min(a.check, len(to) - 1)
+        oc, oo, oi = o3.match_ids(tb, to[: k + 1], threads=host_threads(a))
+        ok = ok and bool(np.array_equal(dc[:k], oc) and np.array_equal(doo[: k + 1], oo) and
+                         np.array_equal(di[: int(oo[-1])], oi))
+    log("bit-exact check of %d topics of each of %d batches vs O3: %s" % (min(a.check, len(batches[0][1]) - 1),
+                                                                          len(batches), ok))
+    o3.close()
+    return ok
+
+
 def o1_check_and_baseline(a, fb, fo, n_filters, batches, results, do_cpu):
     from oracle import O1   # checker / CPU baseline only
+    if n_filters > 20_000_000:
+        return o3_check(a, fb, fo, n_filters, batches, results), {}
     t0 = time.time()
     o1 = O1(n_filters)
     o1.insert_many(fb, fo)
@@ -257,7 +291,9 @@ def main():
         dist.init_process_group("nccl" if torch.cuda.is_available() and not share else "gloo")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if (a.mode or ("sharded" if a.config == 4 else "replicated")) == "sharded":
+    # replicated whenever the trie fits one GPU's HBM (north_star): C4's 100M
+    # filters (252M nodes) included; --mode sharded for filter sets beyond it
+    if (a.mode or "replicated") == "sharded":
         main_sharded(a, rank, world, local, dev)
         if world > 1:
             dist.destroy_process_group()
@@ -279,7 +315,7 @@ def main():
     for kv in a.opt:
         k, x = kv.split("=")
         eng.set_option(k, int(x))
-    eng.insert_many(fb, fo)
+    insert_progress(eng, fb, fo, rank)
     eng.commit()
     log("rank %d: trie built + committed in %.1fs: %d filters, %d nodes, image %.2f GB" % (
         rank, time.time() - t0, eng.filter_count, eng.node_count, eng.image_bytes / 1e9))

@@ -133,7 +133,7 @@ def test_c5_1m_filters_vs_o1(gpu_device, capsys):
     e.close()
 
 
-def test_c4_100m_filters_sharded_8_vs_replicated(gpu_device, capsys):
+def test_c4_100m_filters_sharded_8_vs_replicated_vs_o3(gpu_device, capsys):
     import torch
     from emqx_amd import Engine, shard
     from emqx_amd import workload as W
@@ -156,6 +156,14 @@ def test_c4_100m_filters_sharded_8_vs_replicated(gpu_device, capsys):
         e.commit()
         box["rep"] = e
 
+    def build_o3():
+        # the oracle side: O3 (oracle/o3_interned.c, emqx_trie's algorithm over
+        # interned ids) over all 100M filters
+        from oracle import O3
+        o = O3(n_f)
+        o.insert_many(fb, fo)
+        box["o3"] = o
+
     def build_shard(s):
         e = shard.ShardEngine(gpu_device, S, s, filters_hint=n_f // S + 1)
         e.set_option("stage_k", 128)
@@ -171,7 +179,7 @@ def test_c4_100m_filters_sharded_8_vs_replicated(gpu_device, capsys):
     tk = threading.Thread(target=ticker)
     tk.start()
     try:
-        _threads(build_rep, *[(lambda s=s: build_shard(s)) for s in range(S)])
+        _threads(build_rep, build_o3, *[(lambda s=s: build_shard(s)) for s in range(S)])
     finally:
         done.set()
         tk.join()
@@ -231,5 +239,13 @@ def test_c4_100m_filters_sharded_8_vs_replicated(gpu_device, capsys):
     assert np.array_equal(got, ids.astype(np.int64))
     assert offs[-1] > 60 * n
     say("20K topics: sharded (S=8) == replicated, %d matches" % int(offs[-1]))
+    # pinned to the oracle: O3's ordered lists of the first 10K topics equal
+    # the replicated engine's (and so the sharded merge's), id for id
+    k = 10_000
+    oc, oo, oi = box["o3"].match_ids(tb, to[: k + 1], threads=8)
+    assert np.array_equal(oc, counts[:k]) and np.array_equal(oo, offs[: k + 1])
+    assert np.array_equal(oi, ids[: int(oo[-1])])
+    say("10K topics: replicated == O3 over 100M filters, %d matches" % int(oo[-1]))
+    box["o3"].close()
     for e in engs + [rep]:
         e.close()

@@ -9,6 +9,7 @@
 #   pmc       PMC passes (tools/pmc_passes.sh)           -> pmc/summary.json
 #   traffic   per-launch walk traffic from those passes  -> profiles/traffic_c3.json (read by bench)
 #   cmd       an arbitrary python command in $CMD         -> cmd.log
+#   latency   open-loop batcher latency sweep             -> latency.jsonl
 # e.g. gpurun -- 'STEPS="tests bench prof" TAG=r02_head bash tools/gpu.sh'
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
@@ -25,8 +26,13 @@ for s in ${STEPS:-tests}; do
              python3 bench.py --steps 10 --warmup 2 --cpu-sample 0 --check 0 --streams 1 --no-extras ${BENCH_ARGS} \
              > "$OUT/prof_bench.json" 2> "$OUT/prof_bench.log" ;;
     pmc)   PMC_DIR=${TAG:-job}/pmc bash tools/pmc_passes.sh ;;
+    prof4) timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof4" -o run -- \
+             python3 bench.py --config 4 --steps 10 --warmup 2 --cpu-sample 0 --check 0 --streams 1 --no-extras \
+             > "$OUT/prof4_bench.json" 2> "$OUT/prof4_bench.log" ;;
     traffic) python3 tools/traffic.py "$OUT/pmc" profiles/traffic_c3.json > "$OUT/traffic_c3.json" ;;
     cmd)   timeout -k 10 ${T_CMD:-600} python -u -c "$CMD" > "$OUT/cmd.log" 2>&1 ;;
+    latency) timeout -k 10 ${T_LAT:-400} python -u tools/bench_batcher_latency.py ${LAT_ARGS} \
+             > "$OUT/latency.jsonl" 2> "$OUT/latency.log" ;;
     *)     echo "unknown step $s"; false ;;
   esac
   rc=$?

@@ -11,12 +11,21 @@ ARGS="--steps 3 --warmup 1 --roof-steps 0 --cpu-sample 0 --check 0 --streams 1 -
 run() {
   name=$1; shift
   mkdir -p $D/$name
-  timeout -s KILL 180 rocprofv3 --pmc "$@" --output-format csv -d $D/$name -o run -- python3 bench.py $ARGS > $D/$name/log.txt 2>&1
+  timeout -s KILL ${T_PMC:-180} rocprofv3 --pmc "$@" --output-format csv -d $D/$name -o run -- python3 bench.py $ARGS > $D/$name/log.txt 2>&1
 }
-run fetch FETCH_SIZE && \
-run write WRITE_SIZE && \
-run tcc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum && \
-run sq SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_BUSY_CYCLES && \
-run tcp TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCP_TCC_WRITE_REQ_sum TCP_TOTAL_READ_sum && \
-run ta TA_TA_BUSY_sum TA_BUFFER_READ_WAVEFRONTS_sum && \
+pass() {
+  case $1 in
+    fetch) run fetch FETCH_SIZE ;;
+    write) run write WRITE_SIZE ;;
+    tcc)   run tcc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum ;;
+    sq)    run sq SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_BUSY_CYCLES ;;
+    tcp)   run tcp TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCP_TCC_WRITE_REQ_sum TCP_TOTAL_READ_sum ;;
+    ta)    run ta TA_TA_BUSY_sum TA_BUFFER_READ_WAVEFRONTS_sum ;;
+    tlb)   run tlb TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_UTCL1_REQUEST_sum TCP_TCC_READ_REQ_sum ;;
+    *)     echo "unknown pass $1"; false ;;
+  esac
+}
+for p in ${PASSES:-fetch write tcc sq tcp ta}; do
+  pass $p || exit $?
+done
 python3 tools/pmc_summary.py $D > $D/summary.json

@@ -101,3 +101,106 @@ extern "C" int tm_bench_batcher(tm_engine* e, const uint8_t* tb, const uint64_t*
     out[7] = (double)ids;
     return TM_OK;
 }
+
+// ---- open loop: publishes arrive at a fixed rate ------------------------
+// P producers submit topic i at its scheduled time t0 + i / rate (the topic
+// batch is cycled); latency = callback time - scheduled time (not submit
+// time: a producer that falls behind its schedule is counted, as a publisher
+// kept waiting would be).  Every LAT_EVERY-th topic is timed.
+namespace {
+struct OLRec {
+    clk::time_point due;
+    int64_t lat_ns = -1;
+};
+std::atomic<uint64_t> g_ol_fail{0}, g_ol_done{0};
+void on_done_ol(void* ctx, uint64_t, int status, const uint32_t*, const uint32_t*, uint32_t) {
+    if (status != TM_OK) g_ol_fail.fetch_add(1, std::memory_order_relaxed);
+    if (ctx) {
+        OLRec* r = (OLRec*)ctx;
+        r->lat_ns = std::chrono::duration_cast<std::chrono::nanoseconds>(clk::now() - r->due).count();
+    }
+    g_ol_done.fetch_add(1, std::memory_order_relaxed);
+}
+}  // namespace
+
+// out[10]: seconds, achieved topics/s, batches, mean batch, p50 us, p99 us,
+//          p999 us, max us, failed, max producer lag us
+extern "C" int tm_bench_batcher_open_loop(tm_engine* e, const uint8_t* tb, const uint64_t* to, uint64_t nt,
+                                          int producers, double rate, uint64_t total, uint32_t deadline_us,
+                                          uint32_t max_topics, uint32_t lanes, uint32_t flags, uint32_t cb_threads,
+                                          double* out) {
+    tm_batcher_config bc{};
+    bc.callback_threads = cb_threads;
+    bc.max_topics = max_topics;
+    bc.deadline_us = deadline_us;
+    bc.lanes_per_replica = lanes;
+    bc.flags = flags;
+    tm_batcher* b;
+    int rc = tm_batcher_open(e, &bc, &b);
+    if (rc != TM_OK) return rc;
+    {   // warm-up: the lanes' buffers at their sizes
+        std::vector<std::thread> th;
+        const uint64_t w = std::min<uint64_t>(nt, 1u << 20);
+        for (int k = 0; k < producers; ++k)
+            th.emplace_back([&, k] {
+                for (uint64_t i = w * k / producers; i < w * (k + 1) / producers; ++i)
+                    tm_batcher_submit(b, tb + to[i], (uint32_t)(to[i + 1] - to[i]), on_done_ol, nullptr, nullptr);
+            });
+        for (auto& x : th) x.join();
+        tm_batcher_flush(b);
+    }
+    tm_batcher_stats st0;
+    tm_batcher_get_stats(b, &st0);
+    g_ol_fail = 0;
+    g_ol_done = 0;
+    std::vector<OLRec> recs(total / LAT_EVERY + 1);
+    std::vector<int64_t> lag(producers, 0);
+    const auto t0 = clk::now() + std::chrono::milliseconds(2);
+    const double ns_per = 1e9 / rate;
+    std::vector<std::thread> th;
+    for (int k = 0; k < producers; ++k)   // producer k: topics i = k, k + P, ... (interleaved schedule)
+        th.emplace_back([&, k] {
+            int64_t mylag = 0;
+            for (uint64_t i = (uint64_t)k; i < total; i += (uint64_t)producers) {
+                const auto due = t0 + std::chrono::nanoseconds((int64_t)(i * ns_per));
+                auto now = clk::now();
+                while (now < due) {   // spin to the schedule (sub-microsecond gaps)
+                    if (due - now > std::chrono::microseconds(50)) std::this_thread::sleep_for(due - now -
+                                                                                             std::chrono::microseconds(20));
+                    now = clk::now();
+                }
+                mylag = std::max<int64_t>(mylag, std::chrono::duration_cast<std::chrono::nanoseconds>(now - due).count());
+                const uint64_t j = i % nt;
+                OLRec* r = nullptr;
+                if (i % LAT_EVERY == 0) {
+                    r = &recs[i / LAT_EVERY];
+                    r->due = due;
+                }
+                tm_batcher_submit(b, tb + to[j], (uint32_t)(to[j + 1] - to[j]), on_done_ol, r, nullptr);
+            }
+            lag[k] = mylag;
+        });
+    for (auto& x : th) x.join();
+    tm_batcher_flush(b);
+    const double secs = std::chrono::duration<double>(clk::now() - t0).count();
+    tm_batcher_stats st;
+    tm_batcher_get_stats(b, &st);
+    tm_batcher_close(b);
+    std::vector<int64_t> lat;
+    for (const OLRec& r : recs)
+        if (r.lat_ns >= 0) lat.push_back(r.lat_ns);
+    std::sort(lat.begin(), lat.end());
+    if (lat.empty()) lat.push_back(0);
+    const size_t nl = lat.size();
+    out[0] = secs;
+    out[1] = total / secs;
+    out[2] = (double)(st.batches - st0.batches);
+    out[3] = (double)(st.topics - st0.topics) / std::max<double>(1, st.batches - st0.batches);
+    out[4] = lat[(size_t)(0.5 * (nl - 1))] / 1e3;
+    out[5] = lat[(size_t)(0.99 * (nl - 1))] / 1e3;
+    out[6] = lat[(size_t)(0.999 * (nl - 1))] / 1e3;
+    out[7] = lat[nl - 1] / 1e3;
+    out[8] = (double)g_ol_fail.load();
+    out[9] = *std::max_element(lag.begin(), lag.end()) / 1e3;
+    return TM_OK;
+}
