@@ -45,7 +45,8 @@ class TmBatcherConfig(ctypes.Structure):
 
 class TmBatcherStats(ctypes.Structure):
     _fields_ = [(k, ctypes.c_uint64) for k in ("batches", "topics", "results", "max_batch", "size_seals",
-                                               "deadline_seals", "failed_batches")]
+                                               "deadline_seals", "failed_batches", "wait_ns", "pack_ns",
+                                               "device_ns", "callback_ns")]
 
 
 class TmExchangeIn(ctypes.Structure):

@@ -143,6 +143,7 @@ struct Lane {
     Pinned h_bytes, h_off, h_counts, h_outoff, h_src, h_dest, h_total;
     Dev d_bytes, d_off, d_counts, d_outoff, d_src, d_dest, d_total;
     double ids_per_topic = 64.0;      // sizing estimate of the device result buffers
+    clk::time_point sealed;           // when the batch was handed over
 };
 
 std::atomic<uint32_t> g_stripe_rr{0};
@@ -436,18 +437,24 @@ struct tm_batcher {
             }
             const uint32_t n = L.n;
             uint64_t total = 0, results = 0;
+            const clk::time_point t_start = clk::now();
+            clk::time_point t_packed = t_start, t_dev = t_start;
             int rc = host_only ? TM_EDEVICE : TM_OK;   // host-only: the GPU path only
             // the batch's filter ids stay bound to their bytes until its
             // callbacks have gathered them (tm_lease_begin)
             uint64_t lease = 0;
             const bool leased = rc == TM_OK && n && tm_lease_begin(eng, &lease) == TM_OK;
             if (rc == TM_OK && n) {
-                rc = pack(L) ? run_device(L, routes, deliv, total) : TM_ENOMEM;
+                const bool packed = pack(L);
+                t_packed = clk::now();
+                rc = packed ? run_device(L, routes, deliv, total) : TM_ENOMEM;
+                t_dev = clk::now();
                 if (rc == TM_OK)   // deliveries sit at route offsets: count the entries
                     for (uint32_t i = 0; i < n; ++i) results += ((const uint32_t*)L.h_counts.p)[i];
             }
             const uint32_t m = n;
             run_callbacks(L, rc, routes, m);
+            const clk::time_point t_cb = clk::now();
             if (leased) tm_lease_end(eng, lease);
             recycle(L.chunks);
             {
@@ -455,6 +462,11 @@ struct tm_batcher {
                 L.full = false;
             }
             std::lock_guard<std::mutex> lk(mu);
+            auto ns = [](clk::duration d) { return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(d).count(); };
+            st.wait_ns += ns(t_start - L.sealed);
+            st.pack_ns += ns(t_packed - t_start);
+            st.device_ns += ns(t_dev - t_packed);
+            st.callback_ns += ns(t_cb - t_dev);
             st.batches++;
             st.topics += m;
             if (m > st.max_batch) st.max_batch = m;
@@ -485,6 +497,7 @@ struct tm_batcher {
                 {
                     std::lock_guard<std::mutex> l2(L.mu);
                     L.full = true;
+                    L.sealed = clk::now();
                 }
                 L.cv.notify_one();
                 lk.lock();

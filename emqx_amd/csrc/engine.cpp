@@ -216,7 +216,7 @@ struct Slot {
     uint64_t* h_maxc = nullptr;     // pinned copy of the slot's ws after its last walk (largest match count,
                                     // spill chunks taken per XCD)
     hipEvent_t maxc_ev = nullptr, done = nullptr;
-    bool maxc_pending = false, used = false, keyed = false;
+    bool maxc_pending = false, used = false, keyed = false, shaped = false;
     // the slot's last batch, for a re-copy into a larger output (no re-walk)
     uint32_t n = 0, K = 0, kw = 1;
     const uint8_t* bytes = nullptr;
@@ -238,6 +238,7 @@ struct Image {
     // trie: a batch's filter ids and the route lists it expands them with
     // always come from one commit
     DevBuf d_rslots, d_rarena, d_rdest, d_fr_meta, d_rank_src, d_dt, d_rank_tg;
+    DevBuf d_fshape;   // option "shape_keys": filter id -> order key
     size_t arena_uploaded = 0, woff_uploaded = 0;
     bool split_stale = true, written = false;
     uint64_t epoch = 0;
@@ -250,7 +251,7 @@ struct Image {
     AggreView av{};
     void release() {
         for (DevBuf* b : {&d_nodes, &d_edges, &d_hedges, &d_dict, &d_arena, &d_woff, &d_inner, &d_leaf, &d_rslots,
-                          &d_rarena, &d_rdest, &d_fr_meta, &d_rank_src, &d_dt, &d_rank_tg})
+                          &d_rarena, &d_rdest, &d_fr_meta, &d_rank_src, &d_dt, &d_rank_tg, &d_fshape})
             b->release();
         for (hipEvent_t ev : uses) (void)hipEventDestroy(ev);
         uses.clear();
@@ -585,6 +586,10 @@ struct tm_engine {
     int stage_auto = 1;                 // option "stage_auto": keyed walks grow K to the largest list seen
                                         // (no re-walks); unkeyed walks keep K and spill (kernels.h)
     int spill_on = 1;                   // option "spill": ids past K to spill chunks (0: re-walk, as keyed)
+    int shape_keys = 0;                 // option "shape_keys": keyed batches of <= 31 levels walk unkeyed and
+                                        // take each id's order key from fshape (image.h filter_shape)
+    std::vector<uint64_t> fshape;       // filter id -> filter_shape (kept always; uploaded with shape_keys)
+    Track t_fshape;
     static constexpr size_t SPILL_BUDGET = 8ull << 30;   // spill-area cap per slot (bytes)
     static constexpr size_t STAGE_BUDGET = 16ull << 30;  // stage-row footprint cap (bytes, of 288 GB HBM)
     bool stats_enabled = false, timing_enabled = false;
@@ -602,7 +607,7 @@ struct tm_engine {
                 stage_auto = 0;
             }
         }
-        dict.assign(1024, DictSlot{0, WORD_NONE, 0, {0, 0}});
+        dict.assign(1024, DictSlot{0, WORD_NONE, 0, 0, 0, 0});
         nodes.reserve(1024);
         cold.slots.assign(1024, kEmptySlot);
         hot.slots.assign(1024, kEmptySlot);
@@ -616,7 +621,7 @@ struct tm_engine {
         for (size_t s = h & mask;; s = (s + 1) & mask) {
             const DictSlot& d = dict[s];
             if (d.word == WORD_NONE) return WORD_NONE;
-            if (d.hash == h && d.len == len && std::memcmp(&word_arena[word_off[d.word]], p, len) == 0)
+            if (d.tag == dict_tag(h, len) && d.len == len && std::memcmp(&word_arena[word_off[d.word]], p, len) == 0)
                 return d.word;
         }
     }
@@ -624,17 +629,21 @@ struct tm_engine {
         size_t mask = dict.size() - 1;
         size_t s = h & mask;
         while (dict[s].word != WORD_NONE) s = (s + 1) & mask;
-        DictSlot d{h, id, len, {0, 0}};
-        std::memcpy(d.head, &word_arena[word_off[id]], std::min<size_t>(16, (len + 7) & ~size_t(7)));
+        DictSlot d{dict_tag(h, len), id, 0, 0, len, 0};
+        uint8_t head[16] = {0};
+        std::memcpy(head, &word_arena[word_off[id]], std::min<size_t>(16, len));
+        std::memcpy(&d.head0, head, 8);
+        std::memcpy(&d.head1, head + 8, 8);
         dict[s] = d;
         dict_dirty.mark(s);
     }
     void dict_grow() {
         std::vector<DictSlot> old;
         old.swap(dict);
-        dict.assign(old.size() * 2, DictSlot{0, WORD_NONE, 0, {0, 0}});
+        dict.assign(old.size() * 2, DictSlot{0, WORD_NONE, 0, 0, 0, 0});
         for (const DictSlot& d : old)
-            if (d.word != WORD_NONE) dict_place(d.hash, d.word, d.len);
+            if (d.word != WORD_NONE)
+                dict_place(word_hash(&word_arena[word_off[d.word]], d.len), d.word, d.len);
         dict_dirty.all = true;
     }
     // word id of a level (interning it when `intern`)
@@ -969,6 +978,13 @@ struct tm_engine {
         uint64_t off = filter_arena.size();
         filter_arena.insert(filter_arena.end(), p, p + len);
         filters[id] = FilterRec{off, len, node};
+        if (fshape.size() < filters.size()) {
+            const size_t old = fshape.size();
+            fshape.resize(filters.size(), 0);
+            t_fshape.mark_range(old, fshape.size());
+        }
+        fshape[id] = filter_shape(tmp_words.data(), (uint32_t)tmp_words.size());   // insert's split_words
+        t_fshape.cur.mark(id);
         ++live_filters;
         on_filter_new(p, len, id);
         return id;
@@ -1659,6 +1675,7 @@ struct tm_engine {
         im.dict_slot_mask = dict.size() - 1;
         im.word_arena = g.d_arena.as<const uint8_t>();
         im.word_off = g.d_woff.as<const uint32_t>();
+        im.fshape = shape_keys ? g.d_fshape.as<const uint64_t>() : nullptr;
         return im;
     }
 
@@ -1764,6 +1781,7 @@ struct tm_engine {
             upload_table(d, g, g.d_rank_src, rank_src, t_rank_src.cur, t_rank_src.prev);
             upload_table(d, g, g.d_dt, dt, t_dt.cur, t_dt.prev);
             upload_table(d, g, g.d_rank_tg, rank_tg, t_rank_tg.cur, t_rank_tg.prev);
+            if (shape_keys) upload_table(d, g, g.d_fshape, fshape, t_fshape.cur, t_fshape.prev);
             flush_stage(d);
             // append-only arrays: upload the new tail (or all after a realloc)
             {
@@ -1811,6 +1829,7 @@ struct tm_engine {
         t_rank_src.rotate(rank_src.size());
         t_dt.rotate(dt.size());
         t_rank_tg.rotate(rank_tg.size());
+        t_fshape.rotate(fshape.size());
         dev_dirty = false;
         ++epoch;
     }
@@ -1930,7 +1949,11 @@ struct tm_engine {
     void run_batch(DevState& d, const uint8_t* bytes, const uint64_t* off, uint32_t n, uint64_t nbytes,
                    uint32_t* counts, uint64_t* out_off, uint32_t* ids, uint64_t cap, uint64_t* total, hipStream_t st,
                    uint64_t* keys = nullptr, uint32_t key_words = 1) {
-        const uint32_t kw = keys ? key_words : 0u;
+        // shape keys: a keyed batch of one key word walks unkeyed (narrow
+        // rows, spill) and its copy-out takes each id's key from fshape; a
+        // topic with a literal '+' / '#' level re-walks keyed there
+        const bool shaped = keys && key_words == 1 && shape_keys;
+        const uint32_t kw = keys && !shaped ? key_words : 0u;
         adapt_stage_k(d, n, kw);
         const int si = d.next_slot;
         d.next_slot = (d.next_slot + 1) % nslots;
@@ -1958,10 +1981,11 @@ struct tm_engine {
         qb.meta = w.meta.as<uint32_t>();
         qb.path = w.path.as<uint32_t>();
         qb.stage = w.stage.as<uint32_t>();
-        qb.kstage = keys ? w.kstage.as<uint64_t>() : nullptr;
+        qb.kstage = kw ? w.kstage.as<uint64_t>() : nullptr;
+        qb.shaped = shaped;
         qb.scan_tmp = w.scan.as<uint64_t>();
         qb.ws = w.ws.as<unsigned long long>();
-        qb.perm = presort ? w.perm.as<uint32_t>() : nullptr;
+        qb.perm = presort && !shaped ? w.perm.as<uint32_t>() : nullptr;
         if (presort) {
             qb.sort_keys = w.skeys.as<uint32_t>();
             qb.sort_vals = w.svals.as<uint32_t>();
@@ -1981,7 +2005,8 @@ struct tm_engine {
                             cap, total, sp, st, timing_enabled ? marks : nullptr, walk_bpc, hist_enabled != 0,
                             keys ? key_words : 1u));
         d.note_use(st);   // the live image is read until this point of st
-        w.keyed = keys != nullptr;
+        w.keyed = kw != 0;
+        w.shaped = shaped;
         w.n = n;
         w.K = d.stage_k;
         w.kw = keys ? key_words : 1u;
@@ -2007,11 +2032,12 @@ struct tm_engine {
         qb.meta = w.meta.as<uint32_t>();
         qb.path = w.path.as<uint32_t>();
         qb.stage = w.stage.as<uint32_t>();
-        qb.kstage = keys ? w.kstage.as<uint64_t>() : nullptr;
+        qb.kstage = keys && w.keyed ? w.kstage.as<uint64_t>() : nullptr;
+        qb.shaped = keys && w.shaped;
         qb.scan_tmp = w.scan.as<uint64_t>();
         qb.ws = w.ws.as<unsigned long long>();
         qb.perm = w.sorted ? w.perm.as<uint32_t>() : nullptr;   // the rows of a presorted walk
-        if (w.spill_chunks && !keys) {   // the spill chunks of the same walk
+        if (w.spill_chunks && !w.keyed) {   // the spill chunks of the same walk
             qb.spill = w.spill.as<uint32_t>();
             qb.spill_head = w.spill_head.as<uint32_t>();
             qb.spill_chunks = w.spill_chunks;
@@ -3037,7 +3063,7 @@ int tm_key_levels(tm_engine* e, uint32_t* max_levels) {
         for (auto& dp : e->devs) {
             tm_engine::Guard g(dp->device);
             for (auto& w : dp->slots) {
-                if (!w.used || !w.keyed) continue;
+                if (!w.used || !(w.keyed || w.shaped)) continue;
                 HIPCHK(hipEventSynchronize(w.done));
                 uint64_t x = 0;
                 HIPCHK(hipMemcpy(&x, w.ws.as<uint64_t>() + QWS_MAXL, 8, hipMemcpyDeviceToHost));
@@ -3300,6 +3326,15 @@ int tm_set_option(tm_engine* e, const char* name, int64_t value) {
         if (!std::strcmp(name, "spill")) {
             if (value < 0 || value > 1) return TM_EINVAL;
             e->spill_on = (int)value;
+            return TM_OK;
+        }
+        if (!std::strcmp(name, "shape_keys")) {
+            if (value < 0 || value > 1) return TM_EINVAL;
+            if ((int)value != e->shape_keys) {
+                e->shape_keys = (int)value;
+                e->t_fshape.cur.all = true;   // both images take the whole table
+                e->dev_dirty = true;
+            }
             return TM_OK;
         }
         return TM_EINVAL;

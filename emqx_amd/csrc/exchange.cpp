@@ -261,8 +261,14 @@ int tm_shard_exchange(tm_comm* c, const tm_exchange_in* in, tm_exchange_out* out
     if (!c->recv_counts.ensure((size_t)S * m * 4 + 4)) return fail(c, "hipMalloc", TM_ENOMEM);
     // counts of slice p -> rank p, and the id count of each slice (all-to-all of one u64)
     XGROUP_START(c, std::vector<tm_comm*>{c});
+    // (a rank's own slice is a device copy: RCCL's send to self is slower)
     for (uint32_t p = 0; p < S; ++p) {
         const uint32_t lo = slice_lo(n, S, p), mp = slice_lo(n, S, p + 1) - lo;
+        if (p == me) {
+            XHIP(c, hipMemcpyAsync(c->recv_counts.as<uint32_t>() + (size_t)p * m, in->d_counts + lo, (size_t)mp * 4,
+                                   hipMemcpyDeviceToDevice, st));
+            continue;
+        }
         XNCCL(c, ncclSend(in->d_counts + lo, mp, ncclUint32, (int)p, c->nccl, st));
         XNCCL(c, ncclRecv(c->recv_counts.as<uint32_t>() + (size_t)p * m, m, ncclUint32, (int)p, c->nccl, st));
     }
@@ -278,6 +284,15 @@ int tm_shard_exchange(tm_comm* c, const tm_exchange_in* in, tm_exchange_out* out
     uint64_t base = 0;
     for (uint32_t p = 0; p < S; ++p) {
         const uint64_t items = c->h_send[p], from = c->h_send[S + p], ritems = c->h_recv[p];
+        if (p == me) {
+            XHIP(c, hipMemcpyAsync(c->recv_ids.as<uint32_t>() + base, in->d_ids + from, items * 4,
+                                   hipMemcpyDeviceToDevice, st));
+            for (uint32_t j = 0; j < in->key_words; ++j)
+                XHIP(c, hipMemcpyAsync(c->recv_keys.as<uint64_t>() + j * out->total + base,
+                                       in->d_keys + j * in->key_stride + from, items * 8, hipMemcpyDeviceToDevice, st));
+            base += ritems;
+            continue;
+        }
         XNCCL(c, ncclSend(in->d_ids + from, items, ncclUint32, (int)p, c->nccl, st));
         XNCCL(c, ncclRecv(c->recv_ids.as<uint32_t>() + base, ritems, ncclUint32, (int)p, c->nccl, st));
         for (uint32_t j = 0; j < in->key_words; ++j) {

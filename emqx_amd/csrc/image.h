@@ -100,14 +100,19 @@ struct alignas(SLOT_RECORD ? 32 : 16) EdgeSlot {
 };
 static_assert(sizeof(EdgeSlot) == (SLOT_RECORD ? 32 : 16), "edge slot is one or two 16 B halves");
 
+// Dictionary slot: the tokenizer's first 16 B load decides a word of <= 8
+// bytes on its own (tag, id and the bytes), a word of 9-16 bytes with the
+// second half (same 32 B, an L2 hit), a longer one against the arena.
 struct alignas(32) DictSlot {
-    uint64_t hash;         // 64-bit word hash (0 reserved for empty)
+    uint32_t tag;          // dict_tag(hash, len): hash bits 63..40 | min(len, 255)
     uint32_t word;         // word id, WORD_NONE when free
-    uint32_t len;          // word length in bytes
-    uint64_t head[2];      // the word's first 16 bytes, zero padded: the tokenizer verifies words of
-                           // <= 16 bytes from the slot itself (no dependent arena loads)
+    uint64_t head0;        // the word's bytes 0-7, zero padded
+    uint64_t head1;        // bytes 8-15, zero padded
+    uint32_t len;          // the exact length (read for words of 255 bytes or more)
+    uint32_t pad;
 };
 static_assert(sizeof(DictSlot) == 32, "dictionary slot is one 32 B half line");
+
 
 // device-side view of one committed image (plain pointers into HBM)
 struct ImageView {
@@ -123,7 +128,9 @@ struct ImageView {
     uint64_t        dict_slot_mask;
     const uint8_t*  word_arena;
     const uint32_t* word_off;          // word id -> arena offset
+    const uint64_t* fshape;            // filter id -> order key (filter_shape), or null (option "shape_keys" off)
 };
+
 
 // ---- route image (emqx_route bag, src/emqx_router.erl:52-59, 89-90) --------
 // Routes are (topic, dest) pairs; dests are interned to u32 ids.  Each topic
@@ -169,6 +176,29 @@ struct AggreView {
 #else
 #define TM_HD inline
 #endif
+
+// The order key of filter f for any topic it matches (sharded mode; the
+// walk's rank_sym keys, kernels.hip): per level i, '#' = 0, '+' = 2, a
+// literal = 1 (it can only have matched the topic's own word), then the end
+// mark 1 at position |f| unless f ends in '#' -- 2 bits per position from
+// the top of a u64, positions < 32.  A topic (without literal '+' / '#'
+// levels) has at most one matching filter per key, and its matches in
+// descending key order are emqx_trie:match/1's order:
+// the key is a property of the filter alone.
+TM_HD uint64_t filter_shape(const uint32_t* ws, uint32_t len) {
+    uint64_t k = 0;
+    for (uint32_t i = 0; i < len && i < 32; ++i) {
+        const uint64_t sym = ws[i] == 0xFFFFFFFDu ? 0u : ws[i] == 0xFFFFFFFEu ? 2u : 1u;   // WORD_HASH / WORD_PLUS
+        k |= sym << (62 - 2 * i);
+    }
+    if ((len == 0 || ws[len - 1] != 0xFFFFFFFDu) && len < 32) k |= 1ull << (62 - 2 * len);
+    return k;
+}
+
+// DictSlot::tag of a word: 24 hash bits and the length (capped at 255)
+TM_HD uint32_t dict_tag(uint64_t h, uint32_t len) {
+    return (uint32_t)(h >> 40) << 8 | (len < 255u ? len : 255u);
+}
 
 TM_HD bool sum_useful(uint32_t s, uint32_t k) {
     const uint32_t ends = k < 10 ? (s >> k) & 1u : (s >> 10) & 1u;

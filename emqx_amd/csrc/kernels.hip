@@ -69,7 +69,7 @@ __device__ __forceinline__ uint64_t load_chunk(const B& bytes, uint64_t p, uint3
 struct DictProbe {
     uint64_t p, h, s;
     uint32_t len, atom;   // atom: WORD_PLUS / WORD_HASH, or 0 (a dictionary word)
-    uint4 d0, d1;         // the home slot: hash, word, len | first 16 bytes
+    uint4 d0;             // the home slot's first half: tag, word, bytes 0-7
 };
 template <class B>
 __device__ __forceinline__ DictProbe dict_begin(const ImageView& im, const B& bytes, uint64_t p, uint32_t len) {
@@ -88,40 +88,42 @@ __device__ __forceinline__ DictProbe dict_begin(const ImageView& im, const B& by
     }
     q.h = word_hash_final(h, len);
     q.s = q.h & im.dict_slot_mask;
-    const uint4* slot = reinterpret_cast<const uint4*>(im.dict + q.s);
-    q.d0 = slot[0];
-    q.d1 = slot[1];
+    q.d0 = reinterpret_cast<const uint4*>(im.dict + q.s)[0];
     return q;
 }
+// a word of <= 8 bytes is decided by the slot's first 16 B alone (tag, id,
+// bytes); 9-16 bytes also read the second half (same 32 B), longer words the
+// zero-padded arena
 template <class B>
 __device__ __forceinline__ uint32_t dict_end(const ImageView& im, const B& bytes, DictProbe q) {
     if (q.atom) return q.atom;
-    const uint64_t p = q.p, h = q.h;
+    const uint64_t p = q.p;
     const uint32_t len = q.len;
+    const uint32_t tag = dict_tag(q.h, len);
     uint64_t s = q.s;
-    uint4 d0 = q.d0, d1 = q.d1;
+    uint4 d0 = q.d0;
     for (;;) {
-        const uint32_t word = d0.z;
+        const uint32_t word = d0.y;
         if (word == WORD_NONE) return WORD_NONE;
-        if ((((uint64_t)d0.y << 32) | d0.x) == h && d0.w == len) {
-            // byte-verify: the first 16 bytes against the slot's copy, the
-            // rest against the 8-aligned, zero-padded arena copy
-            const uint64_t head0 = ((uint64_t)d1.y << 32) | d1.x, head1 = ((uint64_t)d1.w << 32) | d1.z;
+        if (d0.x == tag) {
+            const uint64_t head0 = ((uint64_t)d0.w << 32) | d0.z;
             bool eq = len == 0 || load_chunk(bytes, p, len < 8 ? len : 8) == head0;
-            if (eq && len > 8) eq = load_chunk(bytes, p + 8, len < 16 ? len - 8 : 8) == head1;
-            if (eq && len > 16) {
-                const uint64_t* a = reinterpret_cast<const uint64_t*>(im.word_arena + im.word_off[word]);
-                for (uint32_t i = 16; i < len && eq; i += 8) {
-                    uint32_t k = len - i < 8 ? len - i : 8;
-                    eq = (load_chunk(bytes, p + i, k) == a[i >> 3]);
+            if (eq && len > 8) {
+                const uint4 d1 = reinterpret_cast<const uint4*>(im.dict + s)[1];   // head1, exact len
+                const uint64_t head1 = ((uint64_t)d1.y << 32) | d1.x;
+                eq = d1.z == len && load_chunk(bytes, p + 8, len < 16 ? len - 8 : 8) == head1;
+                if (eq && len > 16) {
+                    const uint64_t* a = reinterpret_cast<const uint64_t*>(im.word_arena + im.word_off[word]);
+                    for (uint32_t i = 16; i < len && eq; i += 8) {
+                        uint32_t k = len - i < 8 ? len - i : 8;
+                        eq = (load_chunk(bytes, p + i, k) == a[i >> 3]);
+                    }
                 }
             }
             if (eq) return word;
         }
         s = (s + 1) & im.dict_slot_mask;
-        const uint4* slot = reinterpret_cast<const uint4*>(im.dict + s);
-        d0 = slot[0];
-        d1 = slot[1];
+        d0 = reinterpret_cast<const uint4*>(im.dict + s)[0];
     }
 }
 
@@ -175,8 +177,9 @@ __device__ __forceinline__ uint64_t next_slash(const B& bytes, uint64_t q, uint6
 // dictionary slot requested before level k's slot is resolved.
 template <class B>
 __device__ __forceinline__ uint32_t tokenize_topic(const ImageView& im, const B& bytes, uint64_t b, uint64_t e,
-                                                   uint32_t (&tw)[WREG], uint32_t* lw) {
+                                                   uint32_t (&tw)[WREG], uint32_t* lw, bool& ood) {
     uint32_t lev = 0;
+    ood = false;
     bool found;
     uint64_t q = next_slash(bytes, b, e, found);
     DictProbe cur = dict_begin(im, bytes, b, (uint32_t)(q - b));
@@ -189,6 +192,7 @@ __device__ __forceinline__ uint32_t tokenize_topic(const ImageView& im, const B&
             nxt = dict_begin(im, bytes, s, (uint32_t)(q - s));
         }
         const uint32_t w = dict_end(im, bytes, cur);
+        ood |= w == WORD_PLUS || w == WORD_HASH;
         if (lev < WREG) {
 #pragma unroll
             for (uint32_t k = 0; k < WREG; ++k) tw[k] = lev == k ? w : tw[k];
@@ -201,7 +205,9 @@ __device__ __forceinline__ uint32_t tokenize_topic(const ImageView& im, const B&
     }
 }
 
-constexpr uint32_t MLONG = 1u << 30, MDOLLAR = 1u << 31, MN = (1u << 30) - 1;   // meta bits
+// meta bits: levels | MOOD (a level is the atom '+' or '#': out of the
+// publish domain, emqx_packet.erl:63) | MLONG (more than WREG levels) | MDOLLAR
+constexpr uint32_t MOOD = 1u << 29, MLONG = 1u << 30, MDOLLAR = 1u << 31, MN = (1u << 29) - 1;
 
 constexpr uint32_t TOK_WIN_WORDS = 512;   // LDS bytes window per wave: 4 KiB (64 topics of <= 64 B)
 
@@ -226,7 +232,8 @@ __device__ __forceinline__ void tokenize_one(const ImageView& im, const B& bytes
     uint32_t tw[WREG];
 #pragma unroll
     for (uint32_t k = 0; k < WREG; ++k) tw[k] = WORD_NONE;
-    const uint32_t lev = tokenize_topic(im, bytes, b, e, tw, words + (b - off[0]) + t);
+    bool ood;
+    const uint32_t lev = tokenize_topic(im, bytes, b, e, tw, words + (b - off[0]) + t, ood);
     // the row as four whole 16 B stores (per-level 4 B stores from 64 lanes
     // to 64 rows were partial-line writes: read-modify-write traffic)
     uint4* row = reinterpret_cast<uint4*>(twords + (uint64_t)t * WREG);
@@ -234,7 +241,7 @@ __device__ __forceinline__ void tokenize_one(const ImageView& im, const B& bytes
     for (uint32_t k = 0; k < WREG / 4; ++k)
         row[k] = make_uint4(tw[4 * k], tw[4 * k + 1], tw[4 * k + 2], tw[4 * k + 3]);
     const uint32_t dollar = (e > b && bytes.byte(b) == '$') ? 1u : 0u;
-    meta[t] = lev | (dollar << 31) | (lev > WREG ? MLONG : 0u);
+    meta[t] = lev | (dollar << 31) | (lev > WREG ? MLONG : 0u) | (ood ? MOOD : 0u);
     if (skeys) {   // option "presort": the walk-order key (presort.hip)
         skeys[t] = presort_key(tw, lev);
         svals[t] = t;
@@ -727,7 +734,7 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
     if (STATS) st.hist = hist;
     uint64_t lev_sum = 0, match_sum = 0;
     uint32_t maxc = 0;                 // largest list of this lane's topics (stage-row sizing)
-    uint32_t maxl = 0;                 // KEYS: most levels of this lane's topics (key width check)
+    uint32_t maxl = 0;                 // most levels of this lane's topics (key width check of keyed batches)
     for (;;) {
         const bool need = (my == NO_TOPIC) && !drained;
         const uint64_t m = __ballot(need);
@@ -783,7 +790,7 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
                     const uint32_t nl = mt & MN;
                     const bool dollar = (mt & MDOLLAR) != 0;
                     lev_sum += nl;
-                    if (KEYS) maxl = nl > maxl ? nl : maxl;
+                    maxl = nl > maxl ? nl : maxl;
                     is_long = (mt & MLONG) != 0;
                     em.row = stage + (uint64_t)i * K;
                     if (KEYS) em.krow = kstage + (uint64_t)i * K;
@@ -849,13 +856,11 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
         maxc = y > maxc ? y : maxc;
     }
     if (lane == 0 && maxc) atomicMax(ws + QWS_MAXC, (unsigned long long)maxc);
-    if (KEYS) {
-        for (int o = 32; o > 0; o >>= 1) {
-            const uint32_t y = (uint32_t)__shfl_xor((int)maxl, o, 64);
-            maxl = y > maxl ? y : maxl;
-        }
-        if (lane == 0 && maxl) atomicMax(ws + QWS_MAXL, (unsigned long long)maxl);
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint32_t y = (uint32_t)__shfl_xor((int)maxl, o, 64);
+        maxl = y > maxl ? y : maxl;
     }
+    if (lane == 0 && maxl) atomicMax(ws + QWS_MAXL, (unsigned long long)maxl);
     wave_stats_add<STATS>(stats, lev_sum, match_sum, st);
 }
 
@@ -870,7 +875,11 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
 #endif
 constexpr uint32_t COPY_WAVE_MIN = TM_COPY_WAVE_MIN;
 
-template <bool KEYS>
+// SHAPED (option "shape_keys"): a keyed batch walked unkeyed; each id's key
+// is its filter's order key im.fshape[id] (image.h filter_shape), and a
+// topic with a literal '+' / '#' level (MOOD: its walk repeats subtrees, so
+// keys by filter would tie) is re-walked keyed here, all of its outputs.
+template <bool KEYS, bool SHAPED>
 __global__ void __launch_bounds__(BLOCK)
 tm_copy_out(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const uint32_t* __restrict__ twords,
             const uint32_t* __restrict__ words, const uint32_t* __restrict__ meta, uint32_t* __restrict__ gpath,
@@ -891,6 +900,11 @@ tm_copy_out(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const ui
     lds_inc[threadIdx.x] = (uint32_t)(ex + c);
     __syncthreads();
     const uint64_t base = out_off[t0];
+    auto ood = [&](uint32_t lt) { return SHAPED && (meta[t0 + lt] & MOOD) != 0; };
+    auto put = [&](uint64_t p, uint32_t id) {
+        out[p] = id;
+        if (SHAPED) kout[p] = im.fshape[id];
+    };
     if (agg >= (uint64_t)COPY_WAVE_MIN * tn) {
         // high fan-out block: one wave per topic, its lanes stride the row
         // (no per-id search); output j of a topic with ct ids is row slot
@@ -899,11 +913,12 @@ tm_copy_out(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const ui
         for (uint32_t lt = w; lt < tn; lt += BLOCK / 64) {
             const uint32_t prev = lt ? lds_inc[lt - 1] : 0u;
             const uint32_t ct = lds_inc[lt] - prev;
+            if (ood(lt)) continue;
             const uint64_t ob = base + prev;
             const uint64_t row = (uint64_t)(t0 + lt) * K + K - ct;   // + j: slot of output j
             for (uint32_t j = (ct > K ? ct - K : 0u) + lane; j < ct; j += 64) {
                 if (ob + j < out_cap) {
-                    out[ob + j] = stage[row + j];
+                    put(ob + j, stage[row + j]);
                     if (KEYS)
                         for (uint32_t q = 0; q < KW; ++q) kout[q * out_cap + ob + j] = kstage[q * kplane + row + j];
                 }
@@ -919,8 +934,8 @@ tm_copy_out(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const ui
         const uint32_t k = (uint32_t)(j - prev);
         const uint32_t ct = lds_inc[lo] - prev;
         const int64_t slot = (int64_t)K - (int64_t)ct + (int64_t)k;
-        if (slot >= 0 && base + j < out_cap) {
-            out[base + j] = stage[(uint64_t)(t0 + lo) * K + (uint64_t)slot];
+        if (slot >= 0 && base + j < out_cap && !ood(lo)) {
+            put(base + j, stage[(uint64_t)(t0 + lo) * K + (uint64_t)slot]);
             if (KEYS)
                 for (uint32_t q = 0; q < KW; ++q)
                     kout[q * out_cap + base + j] = kstage[q * kplane + (uint64_t)(t0 + lo) * K + (uint64_t)slot];
@@ -933,7 +948,7 @@ tm_copy_out(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const ui
         for (uint32_t lt = w; lt < tn; lt += BLOCK / 64) {
             const uint32_t prev = lt ? lds_inc[lt - 1] : 0u;
             const uint32_t ct = lds_inc[lt] - prev;
-            if (ct <= K) continue;
+            if (ct <= K || ood(lt)) continue;
             uint32_t cur = spill_head[t0 + lt];
             if (cur == NO_SPILL) continue;   // re-walked below
             const uint32_t m = ct - K;
@@ -941,24 +956,27 @@ tm_copy_out(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const ui
             for (uint32_t o0 = 0; o0 < m; o0 += SPILL_CHUNK - 1) {
                 for (uint32_t j = lane; j < SPILL_CHUNK - 1 && o0 + j < m; j += 64) {
                     const uint64_t p = ob + m - 1 - (o0 + j);
-                    if (p < out_cap) out[p] = spill[(uint64_t)cur * SPILL_CHUNK + 1 + j];
+                    if (p < out_cap) put(p, spill[(uint64_t)cur * SPILL_CHUNK + 1 + j]);
                 }
                 if (o0 + SPILL_CHUNK - 1 < m) cur = spill[(uint64_t)cur * SPILL_CHUNK];
             }
         }
     }
-    if (threadIdx.x < tn && c > K && (KEYS || !spill || spill_head[t0 + threadIdx.x] == NO_SPILL)) {
-        // fan-out beyond the stage row and no spill: walk again, write the head
+    const bool tail = c > K && (KEYS || !spill || spill_head[t0 + threadIdx.x] == NO_SPILL);
+    if (threadIdx.x < tn && (tail || ood(threadIdx.x))) {
+        // fan-out beyond the stage row and no spill: walk again, write the
+        // head; SHAPED: keyed, and every output of an out-of-domain topic
         const uint32_t t = t0 + threadIdx.x;
         const uint32_t mt = meta[t];
         const uint64_t b = off[t] - off[0];
         const MemWords mw{twords + (uint64_t)t * WREG, words + b + t};
-        TailEmit<KEYS> em{out, kout, base + ex, out_cap, K, c, 0, KW, out_cap};
+        constexpr bool WK = KEYS || SHAPED;
+        TailEmit<WK> em{out, kout, base + ex, out_cap, ood(threadIdx.x) ? 0u : K, c, 0, KW, out_cap};
         WalkStats s2;
         if (mt & MLONG)
-            walk<false, KEYS>(im, mt & MN, (mt & MDOLLAR) != 0, GlobalPath{gpath + b + 2ull * t}, mw, em, s2);
+            walk<false, WK>(im, mt & MN, (mt & MDOLLAR) != 0, GlobalPath{gpath + b + 2ull * t}, mw, em, s2);
         else
-            walk<false, KEYS>(im, mt & MN, (mt & MDOLLAR) != 0, LdsPath{lds_path + threadIdx.x}, mw, em, s2);
+            walk<false, WK>(im, mt & MN, (mt & MDOLLAR) != 0, LdsPath{lds_path + threadIdx.x}, mw, em, s2);
     }
 }
 
@@ -1159,12 +1177,17 @@ hipError_t launch_copy(const ImageView& im, const uint8_t* bytes, const uint64_t
             hipLaunchKernelGGL(tm_copy_out_sorted<false>, g, blk, 0, st, im, off, n, qb.twords, qb.words, qb.meta,
                                qb.path, qb.stage, nullptr, K, 1u, counts, out_off, out, nullptr, out_cap, qb.perm);
     } else if (qb.kstage) {
-        hipLaunchKernelGGL(tm_copy_out<true>, g, blk, 0, st, im, off, n, qb.twords, qb.words, qb.meta, qb.path,
-                           qb.stage, qb.kstage, K, key_words, counts, out_off, out, out_keys, out_cap, nullptr,
-                           nullptr);
+        hipLaunchKernelGGL((tm_copy_out<true, false>), g, blk, 0, st, im, off, n, qb.twords, qb.words, qb.meta,
+                           qb.path, qb.stage, qb.kstage, K, key_words, counts, out_off, out, out_keys, out_cap,
+                           nullptr, nullptr);
+    } else if (qb.shaped) {
+        if (!out_keys || key_words != 1 || !im.fshape) return hipErrorInvalidValue;
+        hipLaunchKernelGGL((tm_copy_out<false, true>), g, blk, 0, st, im, off, n, qb.twords, qb.words, qb.meta,
+                           qb.path, qb.stage, nullptr, K, 1u, counts, out_off, out, out_keys, out_cap,
+                           qb.spill_chunks >= QRANGES ? qb.spill : nullptr, qb.spill_head);
     } else {
-        hipLaunchKernelGGL(tm_copy_out<false>, g, blk, 0, st, im, off, n, qb.twords, qb.words, qb.meta, qb.path,
-                           qb.stage, nullptr, K, 1u, counts, out_off, out, nullptr, out_cap,
+        hipLaunchKernelGGL((tm_copy_out<false, false>), g, blk, 0, st, im, off, n, qb.twords, qb.words, qb.meta,
+                           qb.path, qb.stage, nullptr, K, 1u, counts, out_off, out, nullptr, out_cap,
                            qb.spill_chunks >= QRANGES ? qb.spill : nullptr, qb.spill_head);
     }
     return hipGetLastError();

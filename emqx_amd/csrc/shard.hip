@@ -158,6 +158,17 @@ tm_shard_merge(uint32_t S, uint32_t m, const uint32_t* __restrict__ counts, cons
     }
 }
 
+// one shard: its list of every topic is already in order, and gid = id
+// (local * 1 + 0): the merge is a copy of the received block
+__global__ void __launch_bounds__(MBLOCK)
+tm_shard_copy1(const uint64_t* __restrict__ src_base, const uint32_t* __restrict__ ids,
+               const uint64_t* __restrict__ total, uint32_t* __restrict__ out_gid, uint64_t out_cap) {
+    const uint64_t nt = *total < out_cap ? *total : out_cap;
+    const uint32_t* src = ids + src_base[0];
+    for (uint64_t i = (uint64_t)blockIdx.x * MBLOCK + threadIdx.x; i < nt; i += (uint64_t)gridDim.x * MBLOCK)
+        out_gid[i] = src[i];
+}
+
 static inline uint32_t mdiv_up(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
 
 // exchange bookkeeping: out[d] = ids of topic slice d (offs[b[d+1]] -
@@ -208,6 +219,13 @@ hipError_t launch_shard_merge(uint32_t S, uint32_t m, const uint32_t* counts, co
     if (m == 0) {
         hipError_t err = hipMemsetAsync(out_off, 0, 8, st);
         return err == hipSuccess ? hipMemsetAsync(total, 0, 8, st) : err;
+    }
+    if (S == 1) {   // nothing to interleave: the counts, their scan, the ids as they came
+        hipError_t err = hipMemcpyAsync(out_count, counts, (size_t)m * 4, hipMemcpyDeviceToDevice, st);
+        if (err == hipSuccess) err = launch_scan(counts, m, out_off, total, tmp, st);
+        if (err != hipSuccess) return err;
+        hipLaunchKernelGGL(tm_shard_copy1, dim3(4096), dim3(MBLOCK), 0, st, src_base, ids, total, out_gid, out_cap);
+        return hipGetLastError();
     }
     // exclusive prefix of all S x m counts, source-major: within source s,
     // pre[s*m + t] - pre[s*m] is topic t's offset in s's block

@@ -98,6 +98,9 @@ class ShardEngine(Engine):
             raise ValueError("n_shards must be 1..8 and shard < n_shards")
         super().__init__(device=device, filters_hint=filters_hint)
         self.n_shards, self.shard = n_shards, shard
+        # keyed batches of <= 31 levels walk unkeyed; ids take their filter's
+        # order key (image.h filter_shape) in the copy-out
+        self.set_option("shape_keys", 1)
 
     def insert_many(self, buf, off):
         """insert the filters of [off[i], off[i+1]) that belong to this shard"""

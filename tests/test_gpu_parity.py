@@ -362,3 +362,43 @@ def test_commit_does_not_wait_for_walks_in_flight(gpu_device):
                         "--overlap"], env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     print(r.stdout.strip())
+
+
+def test_tokenizer_word_lengths_and_near_misses(gpu_device):
+    """emqx_topic:words/1 on the device against the dictionary slot layout
+    (image.h DictSlot: bytes 0-7 and the tag decide words of <= 8 bytes,
+    bytes 8-15 words of <= 16, the arena longer ones, the exact length words
+    of 255+): words of every length class, and topic levels that share a
+    word's prefix, its bytes minus or plus one, or its hash tag's length
+    byte (255 / 256 / 300 bytes), must resolve exactly as O1 does"""
+    rng = random.Random(11)
+    lens = [0, 1, 2, 7, 8, 9, 15, 16, 17, 24, 31, 32, 33, 100, 254, 255, 256, 257, 300, 1000]
+    words = []
+    for L in lens:
+        w = bytes(rng.choice(b"abcdefgh") for _ in range(L))
+        words += [w, w + b"x", w[:-1] if L else b"", b"a" * L]
+    words = sorted(set(words))
+    filters = set()
+    for w in words:
+        filters.add(b"p/" + w)
+        filters.add(w + b"/+")
+        filters.add(b"+/" + w + b"/#")
+    filters = sorted(filters)
+    near = []
+    for w in words:
+        near += [w, w + b"y", w[:-1] if w else b"z", w[:8] + b"!" + w[9:] if len(w) > 8 else w + b"!",
+                 w[:16] + b"?" + w[17:] if len(w) > 16 else w]
+    topics = []
+    for _ in range(4000):
+        topics.append(b"/".join(rng.choice([b"p", rng.choice(near), rng.choice(words)]) for _ in range(rng.randint(1, 3))))
+    e = Engine(device=gpu_device)
+    fb, fo = pack(filters)
+    e.insert_many(fb, fo)
+    o1 = O1(len(filters))
+    o1.insert_many(fb, fo)
+    tb, to = pack(topics)
+    c, o, ids = e.match_batch(tb, to)
+    oc, oo, oi = o1.match_ids(tb, to, threads=4)
+    assert np.array_equal(c, oc) and np.array_equal(o, oo) and np.array_equal(ids, oi)
+    assert int(oo[-1]) > len(topics)
+    e.close()

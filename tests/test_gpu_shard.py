@@ -103,7 +103,42 @@ def test_sharded_presorted_walk_equals_o1(gpu_device, S):
     from emqx_amd import workload as W
     filters = W.unpack(*W.filters(1))
     topics = W.unpack(*W.topics(1, n=20000))
-    got = _run_sharded(filters, topics, S, K=16, opts={"presort": 1, "stage_auto": 0})
+    got = _run_sharded(filters, topics, S, K=16, opts={"presort": 1, "stage_auto": 0, "shape_keys": 0})
+    assert got == _o1(filters, topics)
+
+
+@pytest.mark.parametrize("shape", [0, 1])
+def test_sharded_walk_keys_and_shape_keys_equal_o1(gpu_device, shape):
+    """both ways to key a shard's lists: the keyed walk (rank_sym) and the
+    unkeyed walk whose copy-out takes each filter's order key
+    (image.h filter_shape, option shape_keys, the ShardEngine default)"""
+    from emqx_amd import workload as W
+    filters = W.unpack(*W.filters(2, n=200_000))
+    topics = W.unpack(*W.topics(2, n=20000))
+    got = _run_sharded(filters, topics, 3, opts={"shape_keys": shape})
+    assert got == _o1(filters, topics)
+
+
+@pytest.mark.parametrize("S", [1, 3])
+def test_sharded_out_of_domain_topic_levels_equal_o1(gpu_device, S):
+    """publish topics with literal '+' / '#' levels (rejected by
+    emqx_packet.erl:63, so out of the domain, but emqx_trie:match/1 still
+    answers them: the fold over [W, '+'] follows the '+' edge twice and the
+    list repeats filters).  With shape keys such a topic's lists are keyed by
+    a keyed re-walk in the copy-out (filter keys would tie)"""
+    import random
+    rng = random.Random(5)
+    words = [b"a", b"b", b"+", b"#", b""]
+    filters = set()
+    while len(filters) < 3000:
+        ws = [rng.choice([b"a", b"b", b"+", b""]) for _ in range(rng.randint(1, 4))]
+        if rng.random() < 0.3:
+            ws[-1] = b"#"
+        filters.add(b"/".join(ws))
+    filters = sorted(filters)
+    topics = [b"/".join(rng.choice(words) for _ in range(rng.randint(1, 5))) for _ in range(3000)]
+    assert sum(1 for t in topics if b"+" in t.split(b"/") or b"#" in t.split(b"/")) > 500
+    got = _run_sharded(filters, topics, S, K=8)
     assert got == _o1(filters, topics)
 
 

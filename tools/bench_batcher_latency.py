@@ -37,7 +37,7 @@ def main():
     ap.add_argument("--max-topics", type=int, default=262144)
     ap.add_argument("--lanes", type=int, default=4)
     ap.add_argument("--cb-threads", type=int, default=8)
-    ap.add_argument("--producers", type=int, default=16)
+    ap.add_argument("--producers", type=int, default=4)
     a = ap.parse_args()
     fb, fo = W.filters(a.config)
     e = Engine(device=0)
@@ -56,7 +56,7 @@ def main():
         for dl in [int(x) for x in a.deadlines.split(",")]:
             total = max(100_000, int(rate * a.seconds))
             log("offered %.0fM publishes/s, deadline %d us, %d publishes ..." % (rate / 1e6, dl, total))
-            r = (ctypes.c_double * 10)()
+            r = (ctypes.c_double * 14)()
             rc = f(e.h, tb.ctypes.data, to.ctypes.data, len(to) - 1, a.producers, rate, total, dl, a.max_topics,
                    a.lanes, 0, a.cb_threads, r)
             print(json.dumps({"offered_per_s": rate, "deadline_us": dl, "max_topics": a.max_topics,
@@ -64,7 +64,9 @@ def main():
                               "rc": rc, "publishes": total, "secs": r[0], "achieved_per_s": r[1],
                               "batches": int(r[2]), "mean_batch": r[3], "lat_us_p50": r[4], "lat_us_p99": r[5],
                               "lat_us_p999": r[6], "lat_us_max": r[7], "failed": int(r[8]),
-                              "max_producer_lag_us": r[9]}), flush=True)
+                              "max_producer_lag_us": r[9],
+                              "per_batch_us": {"sealed_to_lane": r[10], "pack": r[11], "device": r[12],
+                                               "callbacks": r[13]}}), flush=True)
     e.close()
 
 

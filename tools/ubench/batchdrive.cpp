@@ -123,8 +123,9 @@ void on_done_ol(void* ctx, uint64_t, int status, const uint32_t*, const uint32_t
 }
 }  // namespace
 
-// out[10]: seconds, achieved topics/s, batches, mean batch, p50 us, p99 us,
-//          p999 us, max us, failed, max producer lag us
+// out[14]: seconds, achieved topics/s, batches, mean batch, p50 us, p99 us,
+//          p999 us, max us, failed, max producer lag us, and per batch (us):
+//          sealed -> lane, pack, device path, callbacks
 extern "C" int tm_bench_batcher_open_loop(tm_engine* e, const uint8_t* tb, const uint64_t* to, uint64_t nt,
                                           int producers, double rate, uint64_t total, uint32_t deadline_us,
                                           uint32_t max_topics, uint32_t lanes, uint32_t flags, uint32_t cb_threads,
@@ -160,14 +161,25 @@ extern "C" int tm_bench_batcher_open_loop(tm_engine* e, const uint8_t* tb, const
     std::vector<std::thread> th;
     for (int k = 0; k < producers; ++k)   // producer k: topics i = k, k + P, ... (interleaved schedule)
         th.emplace_back([&, k] {
+            // paced by sleeping, never spinning: a spinning producer burns the
+            // process's CPU quota (cgroup cpu.max) and the throttling then
+            // stalls every thread, the batcher's included, for the rest of the
+            // period.  A producer wakes at most every PACE_US and submits every
+            // publish that has come due; the wait counts in the latency (it
+            // runs from the scheduled time).
+            constexpr int64_t PACE_US = 20;
             int64_t mylag = 0;
+            auto now = clk::now();
             for (uint64_t i = (uint64_t)k; i < total; i += (uint64_t)producers) {
                 const auto due = t0 + std::chrono::nanoseconds((int64_t)(i * ns_per));
-                auto now = clk::now();
-                while (now < due) {   // spin to the schedule (sub-microsecond gaps)
-                    if (due - now > std::chrono::microseconds(50)) std::this_thread::sleep_for(due - now -
-                                                                                             std::chrono::microseconds(20));
+                if (now < due) {
                     now = clk::now();
+                    while (now < due) {
+                        const auto gap = std::chrono::duration_cast<std::chrono::microseconds>(due - now).count();
+                        std::this_thread::sleep_for(std::chrono::microseconds(std::min<int64_t>(std::max<int64_t>(gap, 1),
+                                                                                                PACE_US)));
+                        now = clk::now();
+                    }
                 }
                 mylag = std::max<int64_t>(mylag, std::chrono::duration_cast<std::chrono::nanoseconds>(now - due).count());
                 const uint64_t j = i % nt;
@@ -202,5 +214,10 @@ extern "C" int tm_bench_batcher_open_loop(tm_engine* e, const uint8_t* tb, const
     out[7] = lat[nl - 1] / 1e3;
     out[8] = (double)g_ol_fail.load();
     out[9] = *std::max_element(lag.begin(), lag.end()) / 1e3;
+    const double nb = std::max<double>(1, st.batches - st0.batches);
+    out[10] = (st.wait_ns - st0.wait_ns) / nb / 1e3;
+    out[11] = (st.pack_ns - st0.pack_ns) / nb / 1e3;
+    out[12] = (st.device_ns - st0.device_ns) / nb / 1e3;
+    out[13] = (st.callback_ns - st0.callback_ns) / nb / 1e3;
     return TM_OK;
 }
