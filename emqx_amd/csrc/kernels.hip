@@ -234,12 +234,13 @@ __device__ __forceinline__ void tokenize_one(const ImageView& im, const B& bytes
     for (uint32_t k = 0; k < WREG; ++k) tw[k] = WORD_NONE;
     bool ood;
     const uint32_t lev = tokenize_topic(im, bytes, b, e, tw, words + (b - off[0]) + t, ood);
-    // the row as four whole 16 B stores (per-level 4 B stores from 64 lanes
-    // to 64 rows were partial-line writes: read-modify-write traffic)
+    // the row as whole 16 B stores (per-level 4 B stores from 64 lanes to
+    // 64 rows were partial-line writes: read-modify-write traffic), only the
+    // quads the walk reads (4k < levels: 32 B for an 8-level topic)
     uint4* row = reinterpret_cast<uint4*>(twords + (uint64_t)t * WREG);
 #pragma unroll
     for (uint32_t k = 0; k < WREG / 4; ++k)
-        row[k] = make_uint4(tw[4 * k], tw[4 * k + 1], tw[4 * k + 2], tw[4 * k + 3]);
+        if (4 * k < lev || k == 0) row[k] = make_uint4(tw[4 * k], tw[4 * k + 1], tw[4 * k + 2], tw[4 * k + 3]);
     const uint32_t dollar = (e > b && bytes.byte(b) == '$') ? 1u : 0u;
     meta[t] = lev | (dollar << 31) | (lev > WREG ? MLONG : 0u) | (ood ? MOOD : 0u);
     if (skeys) {   // option "presort": the walk-order key (presort.hip)
@@ -316,10 +317,14 @@ __device__ __forceinline__ Hit probe_edge(const ImageView& im, uint32_t v, uint3
     for (;;) {
         const uint4* slot = reinterpret_cast<const uint4*>(tab + s);
         const uint4 e = (TM_NT_PROBE && !hot) ? nt_load16(slot) : slot[0];
+        // TM_SLOT_RECORD: the record half is loaded with the key half (same
+        // 32 B, one dependent step), so a found child is visited without a
+        // load of its own
+        uint4 d = make_uint4(0, 0, 0, 0);
+        if (SLOT_RECORD) d = slot[1];   // hash_filter, lw, lc, self_filter
         if (STATS) ++loads;
         if (e.x == v && e.y == w) {
             if (!SLOT_RECORD) return Hit{e.z, e.w, 0, 0, 0, 0, false};   // plus: the child's summary S(c)
-            const uint4 d = slot[1];   // same 32 B: hash_filter, lw, lc, self_filter
             return Hit{e.z, e.w, d.x, d.y, d.z, d.w, true};
         }
         if (e.x == EDGE_EMPTY) return Hit{NODE_NONE, 0, 0, 0, 0, 0, false};
@@ -384,9 +389,18 @@ struct WalkStats {
 };
 constexpr int HIST_OFF = 8;   // hist = stats + HIST_OFF
 
+// TM_PF1 (A/B builds): a step that visits v at level r also loads the half
+// of v's pending '+' sibling (path(r-1)) beside v's own, into one register
+// slot; when v turns out to be a dead end the pop to that sibling needs no
+// load of its own (one dependent step per topic saved each time)
+#ifndef TM_PF1
+#define TM_PF1 0
+#endif
 struct Cursor {
     uint32_t v, r, n, r0;   // node to visit next and its level; topic levels; start level
     uint64_t key;           // KEYS: fold branches taken above level r (rank_sym), key word 0
+    uint32_t pf_id;         // TM_PF1: node whose half is in pf (NODE_NONE: none)
+    uint4 pf;
 };
 
 // Order keys (sharded mode).  Every match of a topic is identified by the
@@ -458,6 +472,7 @@ __device__ __forceinline__ bool walk_begin(const ImageView& im, Cursor& c, uint3
                                            WalkStats& st) {
     c.n = n;
     c.key = 0;
+    c.pf_id = NODE_NONE;
     if (!dollar) {
         c.v = ROOT;
         c.r = c.r0 = 0;
@@ -483,7 +498,21 @@ __device__ __forceinline__ bool walk_step(const ImageView& im, Cursor& c, Path p
     uint32_t v = c.v, r = c.r;
     uint64_t key = KEYS ? c.key : 0ull;
     bool leaf = r == c.n;
-    const uint4 h = load_half(im, v, leaf, r);   // inner {plus, hf, lw, lc} / leaf {sf, hf, hash, pad}
+    uint4 h;
+    if (TM_PF1 && !STATS) {
+        const uint32_t sib = r > c.r0 ? (KEYS ? path(r - 1) & NODE_MASK : path(r - 1)) : NODE_NONE;
+        const bool cached = c.pf_id == v;
+        const bool pre = sib != NODE_NONE && sib != c.pf_id && sib != v;
+        uint4 ph = make_uint4(0, 0, 0, 0);
+        h = cached ? c.pf : load_half(im, v, leaf, r);   // the sibling's half is loaded beside v's
+        if (pre) ph = load_half(im, sib, leaf, r);
+        if (pre) {
+            c.pf_id = sib;
+            c.pf = ph;
+        }
+    } else {
+        h = load_half(im, v, leaf, r);   // inner {plus, hf, lw, lc} / leaf {sf, hf, hash, pad}
+    }
     uint32_t plus = h.x, hf = h.y, lw = h.z, lc = h.w, sf = h.x;
     for (;;) {
         if (STATS) {
@@ -699,8 +728,13 @@ constexpr uint32_t QCHUNK = 64;
 constexpr uint32_t QRANGES = 8;
 constexpr uint32_t NO_TOPIC = 0xFFFFFFFFu;
 
+#if TM_PF1
+#define TM_WALK_ATTR __attribute__((amdgpu_waves_per_eu(7, 8)))   // the prefetch slot within 7 waves/SIMD
+#else
+#define TM_WALK_ATTR
+#endif
 template <bool STATS, bool XCDQ, bool KEYS>
-__global__ void __launch_bounds__(BLOCK)
+__global__ void __launch_bounds__(BLOCK) TM_WALK_ATTR
 tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const uint32_t* __restrict__ twords,
               const uint32_t* __restrict__ words, const uint32_t* __restrict__ meta, uint32_t* __restrict__ gpath,
               uint32_t* __restrict__ stage, uint64_t* __restrict__ kstage, uint32_t K, uint32_t KW,
@@ -870,6 +904,9 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
 // K-c+j; a topic with c > K re-walks and writes its first c-K outputs.
 // blocks whose mean fan-out reaches COPY_WAVE_MIN ids per topic copy one
 // topic per wave (no per-id search)
+#ifndef TM_COPY_FLAT
+#define TM_COPY_FLAT 0   // A/B builds: the flat coalesced copy for every block
+#endif
 #ifndef TM_COPY_WAVE_MIN
 #define TM_COPY_WAVE_MIN 16   // A/B at C3: copy-out 0.322 (64) vs 0.283-0.293 ms (16, 0)
 #endif
@@ -905,7 +942,39 @@ tm_copy_out(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const ui
         out[p] = id;
         if (SHAPED) kout[p] = im.fshape[id];
     };
-    if (agg >= (uint64_t)COPY_WAVE_MIN * tn) {
+    if (TM_COPY_FLAT) {
+        // flat and coalesced: thread x copies outputs base + x, base + x +
+        // BLOCK, ... (U of them in flight); the topic of an output advances
+        // monotonically per thread over the block's inclusive prefix
+        constexpr int U = 4;
+        uint32_t lo = 0;
+        for (uint64_t j0 = threadIdx.x; j0 < agg; j0 += (uint64_t)BLOCK * U) {
+            uint32_t v[U];
+            uint64_t src[U];
+            bool ok[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint64_t j = j0 + (uint64_t)u * BLOCK;
+                ok[u] = false;
+                if (j >= agg) continue;
+                while ((uint64_t)lds_inc[lo] <= j) ++lo;
+                const uint32_t prev = lo ? lds_inc[lo - 1] : 0u;
+                const uint32_t ct = lds_inc[lo] - prev;
+                const int64_t slot = (int64_t)K - (int64_t)ct + (int64_t)(j - prev);   // < 0: head past K
+                ok[u] = slot >= 0 && base + j < out_cap && !ood(lo);
+                src[u] = (uint64_t)(t0 + lo) * K + (uint64_t)(slot < 0 ? 0 : slot);
+                if (ok[u]) v[u] = stage[src[u]];
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (!ok[u]) continue;
+                const uint64_t p = base + j0 + (uint64_t)u * BLOCK;
+                put(p, v[u]);
+                if (KEYS)
+                    for (uint32_t q = 0; q < KW; ++q) kout[q * out_cap + p] = kstage[q * kplane + src[u]];
+            }
+        }
+    } else if (agg >= (uint64_t)COPY_WAVE_MIN * tn) {
         // high fan-out block: one wave per topic, its lanes stride the row
         // (no per-id search); output j of a topic with ct ids is row slot
         // K-ct+j, staged for j >= ct-K

@@ -35,7 +35,7 @@ constexpr uint32_t PS_BLOCK = 256;
 constexpr uint32_t PS_ROUNDS = 16;                       // keys per thread per tile
 constexpr uint32_t PS_TILE = PS_BLOCK * PS_ROUNDS;       // 4096 keys per tile
 constexpr uint32_t PS_WAVES = PS_BLOCK / 64;
-constexpr uint32_t PS_META_N = (1u << 30) - 1;           // kernels.hip meta: level count bits
+constexpr uint32_t PS_META_N = (1u << 29) - 1;           // kernels.hip meta: level count bits (MN)
 
 uint32_t presort_counts(uint32_t n) { return 256u * ((n + PS_TILE - 1) / PS_TILE); }
 

@@ -388,7 +388,7 @@ def test_tokenizer_word_lengths_and_near_misses(gpu_device):
     for w in words:
         near += [w, w + b"y", w[:-1] if w else b"z", w[:8] + b"!" + w[9:] if len(w) > 8 else w + b"!",
                  w[:16] + b"?" + w[17:] if len(w) > 16 else w]
-    topics = []
+    topics = [b"p/" + w for w in near] + [w + b"/x" for w in near]   # every length class hits or near-misses
     for _ in range(4000):
         topics.append(b"/".join(rng.choice([b"p", rng.choice(near), rng.choice(words)]) for _ in range(rng.randint(1, 3))))
     e = Engine(device=gpu_device)
@@ -400,5 +400,5 @@ def test_tokenizer_word_lengths_and_near_misses(gpu_device):
     c, o, ids = e.match_batch(tb, to)
     oc, oo, oi = o1.match_ids(tb, to, threads=4)
     assert np.array_equal(c, oc) and np.array_equal(o, oo) and np.array_equal(ids, oi)
-    assert int(oo[-1]) > len(topics)
+    assert int(oo[-1]) > len(near)
     e.close()

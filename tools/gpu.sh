@@ -29,7 +29,7 @@ for s in ${STEPS:-tests}; do
     prof4) timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof4" -o run -- \
              python3 bench.py --config 4 --steps 10 --warmup 2 --cpu-sample 0 --check 0 --streams 1 --no-extras \
              > "$OUT/prof4_bench.json" 2> "$OUT/prof4_bench.log" ;;
-    traffic) python3 tools/traffic.py "$OUT/pmc" profiles/traffic_c3.json > "$OUT/traffic_c3.json" ;;
+    traffic) python3 tools/traffic.py "$OUT/pmc" ${TRAFFIC_OUT:-profiles/traffic_c3.json} > "$OUT/traffic.json" ;;
     cmd)   timeout -k 10 ${T_CMD:-600} python -u -c "$CMD" > "$OUT/cmd.log" 2>&1 ;;
     latency) timeout -k 10 ${T_LAT:-400} python -u tools/bench_batcher_latency.py ${LAT_ARGS} \
              > "$OUT/latency.jsonl" 2> "$OUT/latency.log" ;;

@@ -22,6 +22,10 @@ pass() {
     tcp)   run tcp TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCP_TCC_WRITE_REQ_sum TCP_TOTAL_READ_sum ;;
     ta)    run ta TA_TA_BUSY_sum TA_BUFFER_READ_WAVEFRONTS_sum ;;
     tlb)   run tlb TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_UTCL1_REQUEST_sum TCP_TCC_READ_REQ_sum ;;
+    # the L2 and translation groups in one pass (3 TCC + 4 TCP slots): for
+    # workloads whose build dominates a pass (C4: 100M filters)
+    tcctlb) run tcctlb TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCP_UTCL1_TRANSLATION_MISS_sum \
+              TCP_UTCL1_TRANSLATION_HIT_sum TCP_UTCL1_REQUEST_sum TCP_TCC_READ_REQ_sum ;;
     *)     echo "unknown pass $1"; false ;;
   esac
 }
