@@ -247,7 +247,10 @@ def load():
         raise ImportError("libtopicmatch.so not built at %s: run `make` (or __graft_entry__.build()); "
                           "the HIP match path has no CPU fallback" % LIB_PATH)
     lib = ctypes.CDLL(LIB_PATH)
+    in_tree = os.path.abspath(LIB_PATH) == os.path.join(_HERE, "libtopicmatch.so")
     for name, res, args in SIGNATURES:
+        if not in_tree and not hasattr(lib, name):
+            continue   # an older A/B build (bench.py --lib) without a newer entry point
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

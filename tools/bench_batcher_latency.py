@@ -37,7 +37,7 @@ def main():
     ap.add_argument("--max-topics", type=int, default=262144)
     ap.add_argument("--lanes", type=int, default=4)
     ap.add_argument("--cb-threads", type=int, default=8)
-    ap.add_argument("--producers", type=int, default=4)
+    ap.add_argument("--producers", type=int, default=16)
     a = ap.parse_args()
     fb, fo = W.filters(a.config)
     e = Engine(device=0)
