@@ -586,6 +586,8 @@ struct tm_engine {
     int stage_auto = 1;                 // option "stage_auto": keyed walks grow K to the largest list seen
                                         // (no re-walks); unkeyed walks keep K and spill (kernels.h)
     int spill_on = 1;                   // option "spill": ids past K to spill chunks (0: re-walk, as keyed)
+    uint32_t wave_walk_max = 0;         // option "wave_walk_max": batches of at most this many topics take the
+                                        // wave-per-topic walk (tm_walk_wave: latency, not throughput)
     int shape_keys = 0;                 // option "shape_keys": keyed batches of <= 31 levels walk unkeyed and
                                         // take each id's order key from fshape (image.h filter_shape)
     std::vector<uint64_t> fshape;       // filter id -> filter_shape (kept always; uploaded with shape_keys)
@@ -1983,6 +1985,7 @@ struct tm_engine {
         qb.stage = w.stage.as<uint32_t>();
         qb.kstage = kw ? w.kstage.as<uint64_t>() : nullptr;
         qb.shaped = shaped;
+        qb.wave_walk = n <= wave_walk_max && !kw && !presort;
         qb.scan_tmp = w.scan.as<uint64_t>();
         qb.ws = w.ws.as<unsigned long long>();
         qb.perm = presort && !shaped ? w.perm.as<uint32_t>() : nullptr;
@@ -3326,6 +3329,11 @@ int tm_set_option(tm_engine* e, const char* name, int64_t value) {
         if (!std::strcmp(name, "spill")) {
             if (value < 0 || value > 1) return TM_EINVAL;
             e->spill_on = (int)value;
+            return TM_OK;
+        }
+        if (!std::strcmp(name, "wave_walk_max")) {
+            if (value < 0 || value > 0xFFFFFFFFll) return TM_EINVAL;
+            e->wave_walk_max = (uint32_t)value;
             return TM_OK;
         }
         if (!std::strcmp(name, "shape_keys")) {

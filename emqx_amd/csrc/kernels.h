@@ -33,6 +33,7 @@ struct QueueBufs {
     uint32_t* stage;      // n x K: first K ids of each topic (written from the row's end)
     uint64_t* kstage;     // key_words planes of n x K order key words (sharded mode), or null
     bool shaped = false;  // keyed batch walked unkeyed: copy-out keys from ImageView::fshape (option "shape_keys")
+    bool wave_walk = false;   // small batch: tm_walk_wave, one wave per topic level by level (option "wave_walk_max")
     uint64_t* scan_tmp;   // scan_tmp_elems(n)
     unsigned long long* ws;   // QWS_BYTES of queue heads
     uint32_t* perm;       // option "presort": queue position -> topic (n), or null (arrival order)

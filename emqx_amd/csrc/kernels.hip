@@ -898,6 +898,198 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
     wave_stats_add<STATS>(stats, lev_sum, match_sum, st);
 }
 
+// ---------------------------------------------------------------------------
+// tm_walk_wave: the low-latency walk (small batches: engine option
+// "wave_walk_max").  One wave per topic, level by level: at level r the
+// lanes take the frontier's nodes (one load each, all in flight together),
+// emit, and push the children, so a topic costs about two dependent loads
+// per level instead of one per visited node (the per-lane walk above, which
+// is what a large batch wants: no idle lanes).  Every emission carries its
+// rank key (rank_sym: the fold's branch per level, emqx_trie.erl:127-145),
+// and sorting the topic's emissions by key restores the reference's
+// discovery order, whose first K go to the stage row as the
+// per-lane walk writes them (discovery k at slot K-1-k).  A topic beyond the
+// wave's frontier or emission capacity, or past WREG levels, takes the
+// per-lane walk on lane 0; lists past K are re-walked by the copy-out.
+constexpr uint32_t WV_F = 256;   // frontier entries per level, per wave
+constexpr uint32_t WV_E = 512;   // emissions per topic held for the sort
+struct WaveLds {
+    uint32_t fnode[2][WV_F];
+    uint64_t fkey[2][WV_F];
+    uint64_t ekey[WV_E];
+    uint32_t eid[WV_E];
+    uint32_t words[WREG];
+};
+
+__device__ __forceinline__ void wave_sync_lds() {
+    __threadfence_block();
+    __builtin_amdgcn_wave_barrier();
+}
+// lane-ordered append of this lane's item when `has`: returns the slot, adds
+// the wave's count to `n` (uniform)
+__device__ __forceinline__ uint32_t wave_append(bool has, uint32_t& n) {
+    const uint64_t m = __ballot(has);
+    const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    const uint32_t at = n + r;
+    n += (uint32_t)__popcll(m);
+    return at;
+}
+
+__global__ void __launch_bounds__(BLOCK)
+tm_walk_wave(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const uint32_t* __restrict__ twords,
+             const uint32_t* __restrict__ words, const uint32_t* __restrict__ meta, uint32_t* __restrict__ gpath,
+             uint32_t* __restrict__ stage, uint32_t K, uint32_t* __restrict__ counts,
+             uint32_t* __restrict__ spill_head) {
+    __shared__ WaveLds lds_all[BLOCK / 64];
+    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    WaveLds& L = lds_all[wv];
+    for (uint32_t t = blockIdx.x * (BLOCK / 64) + wv; t < n; t += gridDim.x * (BLOCK / 64)) {
+        const uint32_t mt = meta[t];
+        const uint32_t nl = mt & MN;
+        const bool dollar = (mt & MDOLLAR) != 0;
+        const uint32_t* row = twords + (uint64_t)t * WREG;
+        uint32_t* srow = stage + (uint64_t)t * K;
+        bool fallback = (mt & MLONG) != 0 || nl > 31;
+        uint32_t ec = 0;
+        if (!fallback) {
+            if (lane < WREG && lane < nl) L.words[lane] = row[lane];
+            wave_sync_lds();
+            // the start: root, or (the '$' rule, emqx_trie.erl:121-122) the
+            // root's literal child by the first word, skipping '#' and '+'
+            uint32_t fc = 0, p = 0, r = 0;
+            if (lane == 0) {
+                if (!dollar) {
+                    L.fnode[0][0] = ROOT;
+                    L.fkey[0][0] = 0;
+                    fc = 1;
+                } else {
+                    uint64_t ld = 0;
+                    const uint4 q = load_half(im, ROOT, false);
+                    const uint32_t c = lit_child<false>(im, ROOT, q.x, q.z, q.w, L.words[0], ld).child;
+                    if (c != NODE_NONE) {
+                        L.fnode[0][0] = c;
+                        L.fkey[0][0] = rank_sym(0, 1);
+                        fc = 1;
+                    }
+                }
+            }
+            fc = (uint32_t)__shfl((int)fc, 0, 64);
+            r = dollar ? 1u : 0u;
+            wave_sync_lds();
+            for (; fc && !fallback; ++r) {
+                const bool leaf = r == nl;
+                const uint32_t w = leaf ? 0u : L.words[r];
+                const uint32_t kleft = nl - r - 1;
+                uint32_t nf = 0;
+                for (uint32_t base = 0; base < fc; base += 64) {
+                    const uint32_t i = base + lane;
+                    const bool act = i < fc;
+                    const uint32_t v = act ? L.fnode[p][i] : NODE_NONE;
+                    const uint64_t key = act ? L.fkey[p][i] : 0ull;
+                    uint4 h = make_uint4(FILTER_NONE, FILTER_NONE, WORD_NONE, NODE_NONE);
+                    if (act) h = load_half(im, v, leaf, r);
+                    // 'match_#': the '#' child's filter, discovered first (rank 0 at r)
+                    uint32_t e1 = act && !(h.y & SUM_TAG) ? h.y : FILTER_NONE;
+                    uint32_t e2 = FILTER_NONE, c1 = NODE_NONE, c2 = NODE_NONE;
+                    if (act && leaf) {
+                        e2 = h.x;   // the node's own filter (emqx_trie.erl:128), end mark 1
+                    } else if (act) {
+                        const uint32_t plus = h.x, hf = h.y;
+                        bool lit_ok = true, plus_ok = true;
+                        if (hf & SUM_TAG) {
+                            plus_ok = sum_useful(hf & SUM_ALL, kleft);
+                            lit_ok = w < WORD_MAX ? sum_useful((hf >> 15) & SUM_ALL, kleft)
+                                                  : w == WORD_PLUS ? plus_ok : true;
+                        }
+                        uint64_t ld = 0;
+                        if (lit_ok) {
+                            const Hit g = lit_child<false>(im, v, plus, h.z, h.w, w, ld);
+                            if (g.child != NODE_NONE && (SLOT_RECORD || sum_useful(g.plus & SUM_ALL, kleft)))
+                                c1 = g.child;
+                        }
+                        if (plus_ok) c2 = plus & NODE_MASK;
+                    }
+                    // emissions (any order: the keys sort them)
+                    uint32_t a = wave_append(e1 != FILTER_NONE, ec);
+                    if (e1 != FILTER_NONE && a < WV_E) {
+                        L.ekey[a] = key;
+                        L.eid[a] = e1;
+                    }
+                    a = wave_append(e2 != FILTER_NONE, ec);
+                    if (e2 != FILTER_NONE && a < WV_E) {
+                        L.ekey[a] = key | rank_sym(r, 1);
+                        L.eid[a] = e2;
+                    }
+                    // children for level r + 1: the topic word's edge (1), the '+' edge (2)
+                    a = wave_append(c1 != NODE_NONE, nf);
+                    if (c1 != NODE_NONE && a < WV_F) {
+                        L.fnode[1 - p][a] = c1;
+                        L.fkey[1 - p][a] = key | rank_sym(r, 1);
+                    }
+                    a = wave_append(c2 != NODE_NONE, nf);
+                    if (c2 != NODE_NONE && a < WV_F) {
+                        L.fnode[1 - p][a] = c2;
+                        L.fkey[1 - p][a] = key | rank_sym(r, 2);
+                    }
+                }
+                wave_sync_lds();
+                if (nf > WV_F || ec > WV_E) fallback = true;   // uniform
+                if (leaf) break;
+                fc = nf;
+                p = 1 - p;
+            }
+        }
+        if (!fallback) {
+            // discovery order = ascending key: bitonic sort of the topic's
+            // emissions in LDS (padded with keys that sort last)
+            uint32_t P = 64;
+            while (P < ec) P <<= 1;
+            for (uint32_t i = ec + lane; i < P; i += 64) {
+                L.ekey[i] = ~0ull;
+                L.eid[i] = FILTER_NONE;
+            }
+            wave_sync_lds();
+            if (ec > 1) {
+                for (uint32_t k = 2; k <= P; k <<= 1) {
+                    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+                        for (uint32_t i = lane; i < P; i += 64) {
+                            const uint32_t l = i ^ j;
+                            if (l > i) {
+                                const uint64_t x = L.ekey[i], y = L.ekey[l];
+                                if ((x > y) == ((i & k) == 0)) {
+                                    const uint32_t xi = L.eid[i];
+                                    L.ekey[i] = y;
+                                    L.ekey[l] = x;
+                                    L.eid[i] = L.eid[l];
+                                    L.eid[l] = xi;
+                                }
+                            }
+                        }
+                        wave_sync_lds();
+                    }
+                }
+            }
+            const uint32_t m = ec < K ? ec : K;
+            for (uint32_t k = lane; k < m; k += 64) srow[K - 1 - k] = L.eid[k];
+            if (lane == 0) {
+                counts[t] = ec;
+                if (ec > K && spill_head) spill_head[t] = NO_SPILL;   // the copy-out re-walks the head
+            }
+        } else if (lane == 0) {
+            // beyond the wave's capacity: the per-lane walk, on one lane
+            const uint64_t b = off[t] - off[0];
+            const MemWords mw{row, words + b + t};
+            RowEmit<false> em{srow, nullptr, K, 0, make_uint4(0, 0, 0, 0), 0ull, 1u, 0ull};
+            WalkStats s2;
+            walk<false, false>(im, nl, dollar, GlobalPath{gpath + b + 2ull * t}, mw, em, s2);
+            em.flush();
+            counts[t] = em.cnt;
+            if (em.cnt > K && spill_head) spill_head[t] = NO_SPILL;
+        }
+        wave_sync_lds();
+    }
+}
+
 // tm_copy_out: per 256 topics, the block's output range is copied from the
 // stage rows with coalesced writes (output index -> topic by binary search of
 // the block's inclusive prefix); output j of a topic with c ids is row slot
@@ -1290,6 +1482,25 @@ hipError_t launch_queue(bool stats_mode, bool xcdq, const ImageView& im, const u
     mark(1);
     mark(2);
     const bool keys = qb.kstage != nullptr;
+    if (qb.wave_walk && !keys && !stats_mode && !qb.perm) {
+        // small batch: the wave-per-topic walk (latency); lists past K have
+        // spill_head = NO_SPILL, so the copy-out re-walks their heads
+        const uint32_t wb = div_up(n, BLOCK / 64);
+        hipLaunchKernelGGL(tm_walk_wave, dim3(wb < 65535 ? wb : 65535), blk, 0, st, im, off, n, qb.twords, qb.words,
+                           qb.meta, qb.path, qb.stage, K, counts, qb.spill_chunks >= QRANGES ? qb.spill_head : nullptr);
+        mark(3);
+        mark(4);
+        err = launch_scan(counts, n, out_off, total, qb.scan_tmp, st);
+        if (err != hipSuccess) return err;
+        mark(5);
+        mark(6);
+        if (out_cap) {
+            err = launch_copy(im, bytes, off, n, qb, K, key_words, counts, out_off, out, out_keys, out_cap, st);
+            if (err != hipSuccess) return err;
+        }
+        mark(7);
+        return hipGetLastError();
+    }
     // spill chunks: unkeyed walks in arrival order (presorted rows re-walk)
     uint32_t* const spill = (!keys && !qb.perm && qb.spill_chunks >= QRANGES) ? qb.spill : nullptr;
     const uint32_t wg = resident_grid(tm_walk_queue<false, false, false>, div_up(n, 64), walk_blocks_per_cu);

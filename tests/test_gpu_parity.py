@@ -237,7 +237,11 @@ VARIANTS = {"queue": {}, "queue_xcd": {}, "queue_xcd@nosplit@dfs": {"split": 0, 
             "queue_xcd@presort": {"presort": 1}, "queue@presort": {"presort": 1},
             "queue_xcd@presort@stagek16": {"presort": 1, "stage_k": 16, "stage_auto": 0},
             "queue_xcd@nospill": {"spill": 0}, "queue@stagek8": {"stage_k": 8},
-            "queue_xcd@stagek32@nospill": {"stage_k": 32, "spill": 0}}
+            "queue_xcd@stagek32@nospill": {"stage_k": 32, "spill": 0},
+            # the wave-per-topic walk (tm_walk_wave) on every batch size
+            "queue_xcd@wave": {"wave_walk_max": 1 << 30},
+            "queue_xcd@wave@nosummaries@nospill": {"wave_walk_max": 1 << 30, "summaries": 0, "spill": 0},
+            "queue_xcd@wave@nosplit@stagek8": {"wave_walk_max": 1 << 30, "split": 0, "stage_k": 8}}
 
 
 @pytest.mark.parametrize("variant", list(VARIANTS))
@@ -401,4 +405,19 @@ def test_tokenizer_word_lengths_and_near_misses(gpu_device):
     oc, oo, oi = o1.match_ids(tb, to, threads=4)
     assert np.array_equal(c, oc) and np.array_equal(o, oo) and np.array_equal(ids, oi)
     assert int(oo[-1]) > len(near)
+    e.close()
+
+
+def test_wave_walk_c5_overflow_falls_back_exact(gpu_device):
+    """C5 (16 levels, ~900 ids per topic): the wave walk's frontier and
+    emission buffers overflow, those topics take the per-lane walk on one
+    lane; the lists past K are re-walked by the copy-out -- all bit-exact"""
+    fb, fo = W.filters(5, n=200_000)
+    o1 = O1()
+    o1.insert_many(fb, fo)
+    e = Engine(device=gpu_device)
+    e.set_option("wave_walk_max", 1 << 30)
+    e.insert_many(fb, fo)
+    tb, to = W.topics(5, n=3000)
+    _by_id(o1, e, tb, to)
     e.close()

@@ -107,6 +107,15 @@ def test_sharded_presorted_walk_equals_o1(gpu_device, S):
     assert got == _o1(filters, topics)
 
 
+def test_sharded_shape_keys_with_wave_walk_equal_o1(gpu_device):
+    """shape keys over the wave-per-topic walk (small batches)"""
+    from emqx_amd import workload as W
+    filters = W.unpack(*W.filters(1))
+    topics = W.unpack(*W.topics(1, n=5000))
+    got = _run_sharded(filters, topics, 3, K=16, opts={"wave_walk_max": 1 << 30})
+    assert got == _o1(filters, topics)
+
+
 @pytest.mark.parametrize("shape", [0, 1])
 def test_sharded_walk_keys_and_shape_keys_equal_o1(gpu_device, shape):
     """both ways to key a shard's lists: the keyed walk (rank_sym) and the

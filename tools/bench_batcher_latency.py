@@ -38,9 +38,17 @@ def main():
     ap.add_argument("--lanes", type=int, default=4)
     ap.add_argument("--cb-threads", type=int, default=8)
     ap.add_argument("--producers", type=int, default=16)
+    ap.add_argument("--opt", action="append", default=[], help="engine option name=value (repeatable)")
+    ap.add_argument("--lib", default=None, help="EXPERIMENT: alternative build of libtopicmatch.so")
     a = ap.parse_args()
+    if a.lib:
+        from emqx_amd import _lib
+        _lib.LIB_PATH = os.path.abspath(a.lib)
     fb, fo = W.filters(a.config)
     e = Engine(device=0)
+    for kv in a.opt:
+        k, x = kv.split("=")
+        e.set_option(k, int(x))
     t0 = time.time()
     e.insert_many(fb, fo)
     e.commit()
@@ -59,7 +67,7 @@ def main():
             r = (ctypes.c_double * 14)()
             rc = f(e.h, tb.ctypes.data, to.ctypes.data, len(to) - 1, a.producers, rate, total, dl, a.max_topics,
                    a.lanes, 0, a.cb_threads, r)
-            print(json.dumps({"offered_per_s": rate, "deadline_us": dl, "max_topics": a.max_topics,
+            print(json.dumps({"opts": a.opt, "offered_per_s": rate, "deadline_us": dl, "max_topics": a.max_topics,
                               "lanes": a.lanes, "callback_threads": a.cb_threads, "producers": a.producers,
                               "rc": rc, "publishes": total, "secs": r[0], "achieved_per_s": r[1],
                               "batches": int(r[2]), "mean_batch": r[3], "lat_us_p50": r[4], "lat_us_p99": r[5],

@@ -32,7 +32,7 @@ for s in ${STEPS:-tests}; do
     traffic) python3 tools/traffic.py "$OUT/pmc" ${TRAFFIC_OUT:-profiles/traffic_c3.json} > "$OUT/traffic.json" ;;
     cmd)   timeout -k 10 ${T_CMD:-600} python -u -c "$CMD" > "$OUT/cmd.log" 2>&1 ;;
     latency) timeout -k 10 ${T_LAT:-400} python -u tools/bench_batcher_latency.py ${LAT_ARGS} \
-             > "$OUT/latency.jsonl" 2> "$OUT/latency.log" ;;
+             >> "$OUT/latency.jsonl" 2>> "$OUT/latency.log" ;;
     *)     echo "unknown step $s"; false ;;
   esac
   rc=$?
