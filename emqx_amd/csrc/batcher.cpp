@@ -311,6 +311,7 @@ struct tm_batcher {
     }
 
     // the lane's batch on its GPU; results in the lane's pinned buffers
+    static constexpr uint32_t EAGER_TOPICS = 32768;   // batches up to this size read their lists back with the counts
     int run_device(Lane& L, bool routes, bool deliv, uint64_t& total) {
         auto chk = [](hipError_t e) { return e == hipSuccess; };
         const uint32_t n = L.n;
@@ -338,15 +339,25 @@ struct tm_batcher {
                                                     nbytes, (uint32_t*)L.d_counts.p, (uint64_t*)L.d_outoff.p,
                                                     (uint32_t*)L.d_src.p, cap, (uint64_t*)L.d_total.p, s);
             if (rc != TM_OK) return rc;
-            // the total, counts and offsets first: the list read-back is sized by them
+            // the total, counts and offsets first: the list read-back is sized
+            // by them; a small batch also reads its lists back speculatively
+            // (up to the capacity) in the same round trip
+            const bool eager = n <= EAGER_TOPICS;
+            if (eager && (!L.h_src.ensure(cap * 4 + 4) || (routes && !L.h_dest.ensure(cap * 4 + 4))))
+                return TM_ENOMEM;
             if (!chk(hipMemcpyAsync(L.h_total.p, L.d_total.p, 8, hipMemcpyDeviceToHost, s)) ||
                 !chk(hipMemcpyAsync(L.h_counts.p, L.d_counts.p, n * 4, hipMemcpyDeviceToHost, s)) ||
                 !chk(hipMemcpyAsync(L.h_outoff.p, L.d_outoff.p, (n + 1) * 8, hipMemcpyDeviceToHost, s)) ||
+                (eager && !chk(hipMemcpyAsync(L.h_src.p, L.d_src.p, cap * 4, hipMemcpyDeviceToHost, s))) ||
+                (eager && routes && !chk(hipMemcpyAsync(L.h_dest.p, L.d_dest.p, cap * 4, hipMemcpyDeviceToHost, s))) ||
                 !chk(hipStreamSynchronize(s)))
                 return TM_EDEVICE;
             total = *(const uint64_t*)L.h_total.p;
             L.ids_per_topic = 0.9 * L.ids_per_topic + 0.1 * ((double)total / n);
-            if (total <= cap) break;
+            if (total <= cap) {
+                if (eager) return TM_OK;   // the lists came with the counts
+                break;
+            }
             cap = total + total / 4 + 1024;   // overflow: rerun with room (rare)
         }
         if (!L.h_src.ensure(total * 4 + 4) || (routes && !L.h_dest.ensure(total * 4 + 4))) return TM_ENOMEM;
