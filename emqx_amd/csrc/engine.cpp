@@ -586,8 +586,9 @@ struct tm_engine {
     int stage_auto = 1;                 // option "stage_auto": keyed walks grow K to the largest list seen
                                         // (no re-walks); unkeyed walks keep K and spill (kernels.h)
     int spill_on = 1;                   // option "spill": ids past K to spill chunks (0: re-walk, as keyed)
-    uint32_t wave_walk_max = 0;         // option "wave_walk_max": batches of at most this many topics take the
-                                        // wave-per-topic walk (tm_walk_wave: latency, not throughput)
+    uint32_t wave_walk_max = 32768;     // option "wave_walk_max": batches of at most this many topics take the
+                                        // wave-per-topic walk (tm_walk_wave: ~2 dependent loads per level);
+                                        // faster up to 16K topics, slower from 64K (profiles/r03_d)
     int shape_keys = 0;                 // option "shape_keys": keyed batches of <= 31 levels walk unkeyed and
                                         // take each id's order key from fshape (image.h filter_shape)
     std::vector<uint64_t> fshape;       // filter id -> filter_shape (kept always; uploaded with shape_keys)

@@ -251,6 +251,7 @@ def test_every_walk_variant_bit_exact(gpu_device, golden, variant):
 
     def configure(e):
         e.set_walk(walk)
+        e.set_option("wave_walk_max", 0)   # the per-lane walk unless the variant says otherwise
         for k, v in VARIANTS[variant].items():
             e.set_option(k, v)
     for vec in golden["o1_vectors"]:
