@@ -13,6 +13,9 @@
 // The host mirror IS the host copy of the device image (image.h): inserts and
 // deletes patch it in place and mark 64 KiB pages dirty; tm_commit uploads
 // the dirty pages (or the whole table after a resize) on the engine stream.
+#ifndef TM_CHUNK_ROWS
+#define TM_CHUNK_ROWS 0
+#endif
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
@@ -586,6 +589,7 @@ struct tm_engine {
     int stage_auto = 1;                 // option "stage_auto": keyed walks grow K to the largest list seen
                                         // (no re-walks); unkeyed walks keep K and spill (kernels.h)
     int spill_on = 1;                   // option "spill": ids past K to spill chunks (0: re-walk, as keyed)
+    int chunk_rows = TM_CHUNK_ROWS;     // option "chunk_rows" (kernels.h QueueBufs)
     uint32_t wave_walk_max = 32768;     // option "wave_walk_max": batches of at most this many topics take the
                                         // wave-per-topic walk (tm_walk_wave: ~2 dependent loads per level);
                                         // faster up to 16K topics, slower from 64K (profiles/r03_d)
@@ -1987,6 +1991,7 @@ struct tm_engine {
         qb.kstage = kw ? w.kstage.as<uint64_t>() : nullptr;
         qb.shaped = shaped;
         qb.wave_walk = n <= wave_walk_max && !kw && !presort;
+        qb.chunk_rows = chunk_rows;
         qb.scan_tmp = w.scan.as<uint64_t>();
         qb.ws = w.ws.as<unsigned long long>();
         qb.perm = presort && !shaped ? w.perm.as<uint32_t>() : nullptr;
@@ -3335,6 +3340,11 @@ int tm_set_option(tm_engine* e, const char* name, int64_t value) {
         if (!std::strcmp(name, "wave_walk_max")) {
             if (value < 0 || value > 0xFFFFFFFFll) return TM_EINVAL;
             e->wave_walk_max = (uint32_t)value;
+            return TM_OK;
+        }
+        if (!std::strcmp(name, "chunk_rows")) {
+            if (value < 0 || value > 2) return TM_EINVAL;
+            e->chunk_rows = (int)value;
             return TM_OK;
         }
         if (!std::strcmp(name, "shape_keys")) {
