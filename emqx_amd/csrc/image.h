@@ -229,14 +229,33 @@ TM_HD uint64_t edge_hash(uint32_t parent, uint32_t word) {
     return fmix64(((uint64_t)parent << 32) | word);
 }
 
-// Bloom bits of a literal word in a WIDE node's mask (2 of 64)
-TM_HD uint64_t word_bloom(uint32_t w) {
-    const uint64_t h = fmix64(0x9E3779B97F4A7C15ULL ^ w);
-    return (1ull << (h & 63)) | (1ull << ((h >> 6) & 63));
+TM_HD uint32_t fmix32(uint32_t h) {
+    h ^= h >> 16; h *= 0x85EBCA6Bu;
+    h ^= h >> 13; h *= 0xC2B2AE35u;
+    h ^= h >> 16;
+    return h;
 }
 
-// home slot of key (parent, word)
+// Bloom bits of a literal word in a WIDE node's mask (2 of 64): two 6-bit
+// fields of the word id's Fibonacci hash (one 32-bit multiply: the walk
+// computes this at every WIDE node it visits, and 64-bit multiplies are
+// several quarter-rate instructions each on CDNA)
+#ifndef TM_HASH32
+#define TM_HASH32 1   // A/B builds: 0 = the 64-bit mixes of round 2
+#endif
+TM_HD uint64_t word_bloom(uint32_t w) {
+    if (!TM_HASH32) {
+        const uint64_t h = fmix64(0x9E3779B97F4A7C15ULL ^ w);
+        return (1ull << (h & 63)) | (1ull << ((h >> 6) & 63));
+    }
+    const uint32_t h = w * 0x9E3779B1u;
+    return (1ull << (h >> 26)) | (1ull << ((h >> 20) & 63u));
+}
+
+// home slot of key (parent, word): a 32-bit mix (three 32-bit multiplies)
+// for tables of up to 2^32 slots, the 64-bit one beyond
 TM_HD uint64_t edge_home(uint32_t parent, uint32_t word, uint64_t slot_mask) {
+    if (TM_HASH32 && slot_mask <= 0xFFFFFFFFull) return fmix32(parent * 0x9E3779B1u + word) & slot_mask;
     return edge_hash(parent, word) & slot_mask;
 }
 

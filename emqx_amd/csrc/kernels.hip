@@ -475,12 +475,34 @@ __device__ __forceinline__ uint64_t key_word(const Path& path, uint32_t j, uint3
     return w;
 }
 
-// topic words in VGPRs (n <= WREG): dynamic index by AND-masks (a select
-// chain or tree over the array gets turned back into a private-memory array
-// indexed by r, i.e. scratch loads, by the compiler)
+// topic words in VGPRs (n <= WREG): dynamic index r < WREG by a select tree
+// on the bits of r (15 v_cndmask + 4 bit tests; the AND-mask form it
+// replaces took three VALU instructions per word, 48 per visit)
+#ifndef TM_WSEL_TREE
+#define TM_WSEL_TREE 1
+#endif
+// lane-wise m ? a : b, m a lane mask (v_cndmask_b32 picks src1 where the mask bit is set)
+__device__ __forceinline__ uint32_t sel(uint64_t m, uint32_t a, uint32_t b) {
+    uint32_t x;
+    asm volatile("v_cndmask_b32 %0, %1, %2, %3" : "=v"(x) : "v"(b), "v"(a), "s"(m));
+    return x;
+}
 struct RegWords {
     uint32_t w[WREG];
     __device__ __forceinline__ uint32_t operator()(uint32_t r) const {
+        static_assert(WREG == 16, "select tree over 16 words");
+        if (TM_WSEL_TREE) {
+            // the selects as opaque v_cndmask (plain ternaries get turned
+            // back into a scratch array indexed by r by the compiler)
+            const uint64_t b0 = __ballot((r & 1u) != 0), b1 = __ballot((r & 2u) != 0),
+                           b2 = __ballot((r & 4u) != 0), b3 = __ballot((r & 8u) != 0);
+            const uint32_t a0 = sel(b0, w[1], w[0]), a1 = sel(b0, w[3], w[2]), a2 = sel(b0, w[5], w[4]),
+                           a3 = sel(b0, w[7], w[6]), a4 = sel(b0, w[9], w[8]), a5 = sel(b0, w[11], w[10]),
+                           a6 = sel(b0, w[13], w[12]), a7 = sel(b0, w[15], w[14]);
+            const uint32_t c0 = sel(b1, a1, a0), c1 = sel(b1, a3, a2), c2 = sel(b1, a5, a4), c3 = sel(b1, a7, a6);
+            const uint32_t d0 = sel(b2, c1, c0), d1 = sel(b2, c3, c2);
+            return sel(b3, d1, d0);
+        }
         uint32_t x = 0;
 #pragma unroll
         for (uint32_t k = 0; k < WREG; ++k) x |= w[k] & (0u - (uint32_t)(r == k));
