@@ -14,7 +14,7 @@
 // deletes patch it in place and mark 64 KiB pages dirty; tm_commit uploads
 // the dirty pages (or the whole table after a resize) on the engine stream.
 #ifndef TM_CHUNK_ROWS
-#define TM_CHUNK_ROWS 0
+#define TM_CHUNK_ROWS 1
 #endif
 #include <hip/hip_runtime_api.h>
 
@@ -3343,7 +3343,7 @@ int tm_set_option(tm_engine* e, const char* name, int64_t value) {
             return TM_OK;
         }
         if (!std::strcmp(name, "chunk_rows")) {
-            if (value < 0 || value > 2) return TM_EINVAL;
+            if (value < 0 || value > 1) return TM_EINVAL;
             e->chunk_rows = (int)value;
             return TM_OK;
         }

@@ -34,8 +34,8 @@ struct QueueBufs {
     uint64_t* kstage;     // key_words planes of n x K order key words (sharded mode), or null
     bool shaped = false;  // keyed batch walked unkeyed: copy-out keys from ImageView::fshape (option "shape_keys")
     bool wave_walk = false;   // small batch: tm_walk_wave, one wave per topic level by level (option "wave_walk_max")
-    int chunk_rows = 0;       // option "chunk_rows": 0 rows from HBM per topic, 1 a chunk's rows staged in
-                              // LDS, 2 the walk tokenizes each chunk into LDS (no tm_tokenize launch)
+    int chunk_rows = 1;       // option "chunk_rows": 1 a taken chunk's rows staged in LDS, 0 each topic's row
+                              // read from HBM when a lane takes it
     uint64_t* scan_tmp;   // scan_tmp_elems(n)
     unsigned long long* ws;   // QWS_BYTES of queue heads
     uint32_t* perm;       // option "presort": queue position -> topic (n), or null (arrival order)

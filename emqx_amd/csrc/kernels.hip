@@ -205,45 +205,6 @@ __device__ __forceinline__ uint32_t tokenize_topic(const ImageView& im, const B&
     }
 }
 
-// the same split, each level's word id handed to sink(level, id) (the walk's
-// chunk tokenizer: LDS row, global row, long-topic words)
-template <bool PIPE, class B, class Sink>
-__device__ __forceinline__ uint32_t tokenize_to(const ImageView& im, const B& bytes, uint64_t b, uint64_t e,
-                                                Sink& sink, bool& ood) {
-    uint32_t lev = 0;
-    ood = false;
-    bool found;
-    if (!PIPE) {   // one level at a time (fewer live registers)
-        uint64_t s = b;
-        for (;;) {
-            const uint64_t q = next_slash(bytes, s, e, found);
-            const uint32_t w = dict_end(im, bytes, dict_begin(im, bytes, s, (uint32_t)(q - s)));
-            ood |= w == WORD_PLUS || w == WORD_HASH;
-            sink(lev, w);
-            ++lev;
-            if (!found) return lev;
-            s = q + 1;
-        }
-    }
-    uint64_t q = next_slash(bytes, b, e, found);
-    DictProbe cur = dict_begin(im, bytes, b, (uint32_t)(q - b));
-    for (;;) {
-        const bool more = found;
-        DictProbe nxt;
-        if (more) {
-            const uint64_t s = q + 1;
-            q = next_slash(bytes, s, e, found);
-            nxt = dict_begin(im, bytes, s, (uint32_t)(q - s));
-        }
-        const uint32_t w = dict_end(im, bytes, cur);
-        ood |= w == WORD_PLUS || w == WORD_HASH;
-        sink(lev, w);
-        ++lev;
-        if (!more) return lev;
-        cur = nxt;
-    }
-}
-
 // meta bits: levels | MOOD (a level is the atom '+' or '#': out of the
 // publish domain, emqx_packet.erl:63) | MLONG (more than WREG levels) | MDOLLAR
 constexpr uint32_t MOOD = 1u << 29, MLONG = 1u << 30, MDOLLAR = 1u << 31, MN = (1u << 29) - 1;
@@ -794,58 +755,27 @@ constexpr uint32_t NO_TOPIC = 0xFFFFFFFFu;
 #else
 #define TM_WALK_ATTR
 #endif
-// Chunk rows (CH != 0, unkeyed walks in arrival order): when a wave takes a
-// chunk, its 64 lanes fill the chunk's rows in LDS at once, lane j topic
-// g + j -- CH_ROWS copies the tokenizer's rows and meta (coalesced, one
-// round trip per chunk), CH_FUSED tokenizes the topics right there
-// (emqx_topic:words/1, no tm_tokenize launch and no row round trip through
-// HBM).  A lane that takes a topic then reads its words from LDS instead of
-// waiting on two dependent HBM loads (meta, row).  Topics of more than CW
-// levels read the global row (CH_FUSED writes it for them).
+// Chunk rows (CH_ROWS, unkeyed walks in arrival order): when a wave takes a
+// chunk, its 64 lanes copy the chunk's rows and meta to LDS at once (lane j
+// topic g + j: coalesced, one round trip per chunk), and a lane that takes a
+// topic reads its words from LDS instead of waiting on two dependent loads
+// (meta, then the row) in the middle of the walk: walk 10.87-10.88 vs
+// 11.10-11.13 ms at C3 (profiles/r03_ab/README.md).  Topics of more than CW
+// levels read their global row.  (A variant that tokenized the chunk in the
+// walk itself, dropping tm_tokenize, measured 13.15-15.89 ms: the tokenizer's
+// registers cut the walk's occupancy.)
 __device__ __forceinline__ void wave_sync_lds() {
     __threadfence_block();
     __builtin_amdgcn_wave_barrier();
 }
 constexpr uint32_t CW = 8;   // words per topic in the chunk's LDS rows
-#ifndef TM_FUSE_PIPE
-#define TM_FUSE_PIPE 0   // CH_FUSED: the software-pipelined tokenizer (more registers)
-#endif
-// CH_FUSED: tokenize topic t (emqx_topic:words/1) into its chunk row:
-// levels < CW to LDS, CW..WREG-1 to its global row, later ones to the long
-// topic's word area; a topic the copy-out may re-walk (more than CW levels,
-// or out of the publish domain: the shard copy-out re-walks those keyed)
-// gets its whole global row.  meta to LDS and to meta[t] (the copy-out's)
-__device__ __forceinline__ void fill_chunk_row(const ImageView& im, const uint8_t* bytes, const uint64_t* off,
-                                               uint32_t t, uint32_t* lrow, uint32_t* grow, uint32_t* words,
-                                               uint32_t* meta, uint32_t& lmeta) {
-    const uint64_t b = off[t], e = off[t + 1];
-    uint32_t* lw = words + (b - off[0]) + t;
-    auto sink = [&](uint32_t k, uint32_t w) {
-        if (k < CW) lrow[k] = w;
-        else if (k < WREG) grow[k] = w;
-        else lw[k] = w;
-    };
-    bool ood;
-    const GlobalBytes gb{bytes};
-    const uint32_t lev = tokenize_to<TM_FUSE_PIPE != 0>(im, gb, b, e, sink, ood);
-    const uint32_t dollar = (e > b && gb.byte(b) == '$') ? 1u : 0u;
-    const uint32_t mt = lev | (dollar << 31) | (lev > WREG ? MLONG : 0u) | (ood ? MOOD : 0u);
-    lmeta = mt;
-    meta[t] = mt;
-    if (lev > CW || ood)
-        for (uint32_t k = 0; k < CW && k < lev; ++k) grow[k] = lrow[k];
-}
-constexpr int CH_NONE = 0, CH_ROWS = 1, CH_FUSED = 2;
+constexpr int CH_NONE = 0, CH_ROWS = 1;
 struct ChunkRows {
     uint32_t w[QCHUNK][CW];
     uint32_t meta[QCHUNK];
 };
-#ifndef TM_FUSE_WAVES
-#define TM_FUSE_WAVES 6   // CH_FUSED: registers capped for this many waves per SIMD (the LDS allows 6)
-#endif
 template <bool STATS, bool XCDQ, bool KEYS, int CH = CH_NONE>
 __global__ void __launch_bounds__(BLOCK) TM_WALK_ATTR
-__attribute__((amdgpu_waves_per_eu(CH == CH_FUSED ? TM_FUSE_WAVES : 1, 8)))
 tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const uint32_t* __restrict__ twords,
               const uint32_t* __restrict__ words, const uint32_t* __restrict__ meta, uint32_t* __restrict__ gpath,
               uint32_t* __restrict__ stage, uint64_t* __restrict__ kstage, uint32_t K, uint32_t KW,
@@ -853,14 +783,12 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
               unsigned long long* __restrict__ ws, unsigned long long* __restrict__ stats,
               unsigned long long* __restrict__ hist, const uint32_t* __restrict__ perm,
               const uint32_t* __restrict__ twords_s, const uint32_t* __restrict__ meta_s,
-              uint32_t* __restrict__ spill, uint32_t* __restrict__ spill_head, uint32_t spill_chunks,
-              const uint8_t* __restrict__ bytes) {
+              uint32_t* __restrict__ spill, uint32_t* __restrict__ spill_head, uint32_t spill_chunks) {
     static_assert(CH == CH_NONE || (!STATS && !KEYS), "chunk rows: unkeyed walks in arrival order only");
     __shared__ uint32_t lds_path[WREG * BLOCK];
     __shared__ ChunkRows lds_chunk[CH != CH_NONE ? BLOCK / 64 : 1];
     const uint32_t lane = threadIdx.x & 63;
     ChunkRows& CR = lds_chunk[CH != CH_NONE ? threadIdx.x >> 6 : 0];
-    uint32_t* const twr = const_cast<uint32_t*>(twords);   // CH_FUSED writes the rows it needs later
     const LdsPath lp{lds_path + threadIdx.x};
     GlobalPath gp{nullptr};
     RegWords rw;
@@ -932,16 +860,11 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
                 // a new chunk: its rows to LDS, all lanes at once (uniform branch)
                 const uint32_t t = g + lane;
                 if (t < gend) {
-                    if (CH == CH_ROWS) {
-                        CR.meta[lane] = meta[t];
-                        const uint4* src = reinterpret_cast<const uint4*>(twords + (uint64_t)t * WREG);
-                        const uint4 a0 = src[0], a1 = src[1];
-                        *reinterpret_cast<uint4*>(&CR.w[lane][0]) = a0;
-                        *reinterpret_cast<uint4*>(&CR.w[lane][4]) = a1;
-                    } else {
-                        fill_chunk_row(im, bytes, off, t, CR.w[lane], twr + (uint64_t)t * WREG,
-                                       const_cast<uint32_t*>(words), const_cast<uint32_t*>(meta), CR.meta[lane]);
-                    }
+                    CR.meta[lane] = meta[t];
+                    const uint4* src = reinterpret_cast<const uint4*>(twords + (uint64_t)t * WREG);
+                    const uint4 a0 = src[0], a1 = src[1];   // quad 1 may be stale past the topic's levels: unread
+                    *reinterpret_cast<uint4*>(&CR.w[lane][0]) = a0;
+                    *reinterpret_cast<uint4*>(&CR.w[lane][4]) = a1;
                 }
                 cbase = g;
                 qnext = g;
@@ -1035,12 +958,6 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
             em.flush();
             counts[myt] = em.cnt;
             if (!KEYS && spill && em.cnt > K) spill_head[myt] = em.sfail ? NO_SPILL : em.shead;
-            if (CH == CH_FUSED && em.cnt > K && (!spill || em.sfail) && !is_long && cur.n <= CW) {
-                // the copy-out re-walks this topic from its global row
-                uint4* grow = reinterpret_cast<uint4*>(twr + (uint64_t)myt * WREG);
-                grow[0] = make_uint4(rw.w[0], rw.w[1], rw.w[2], rw.w[3]);
-                grow[1] = make_uint4(rw.w[4], rw.w[5], rw.w[6], rw.w[7]);
-            }
             match_sum += em.cnt;
             maxc = em.cnt > maxc ? em.cnt : maxc;
             my = NO_TOPIC;
@@ -1631,13 +1548,12 @@ hipError_t launch_queue(bool stats_mode, bool xcdq, const ImageView& im, const u
     dim3 blk(BLOCK), g(div_up(n, BLOCK));
     const bool keys = qb.kstage != nullptr;
     // chunk rows (option "chunk_rows"): the walk of an unkeyed batch in
-    // arrival order stages each chunk's rows in LDS; fused, it tokenizes
+    // arrival order stages each chunk's rows in LDS
     const bool lane_walk = !(qb.wave_walk && !keys && !stats_mode && !qb.perm);
-    const int ch = (lane_walk && !keys && !stats_mode && !qb.perm) ? qb.chunk_rows : CH_NONE;
+    const int ch = (lane_walk && !keys && !stats_mode && !qb.perm && qb.chunk_rows) ? CH_ROWS : CH_NONE;
     mark(0);
-    if (ch != CH_FUSED)
-        hipLaunchKernelGGL(tm_tokenize, g, blk, 0, st, im, bytes, off, n, qb.twords, qb.words, qb.meta,
-                           qb.perm ? qb.sort_keys : nullptr, qb.perm ? qb.perm : nullptr);
+    hipLaunchKernelGGL(tm_tokenize, g, blk, 0, st, im, bytes, off, n, qb.twords, qb.words, qb.meta,
+                       qb.perm ? qb.sort_keys : nullptr, qb.perm ? qb.perm : nullptr);
     if (qb.perm) {   // option "presort": perm and the rows in walk order (presort.hip)
         err = launch_presort(qb.twords, qb.meta, n, qb, st);
         if (err != hipSuccess) return err;
@@ -1665,21 +1581,17 @@ hipError_t launch_queue(bool stats_mode, bool xcdq, const ImageView& im, const u
     }
     // spill chunks: unkeyed walks in arrival order (presorted rows re-walk)
     uint32_t* const spill = (!keys && !qb.perm && qb.spill_chunks >= QRANGES) ? qb.spill : nullptr;
-    const uint32_t wg = ch == CH_FUSED ? resident_grid(tm_walk_queue<false, true, false, CH_FUSED>, div_up(n, 64),
-                                                       walk_blocks_per_cu)
-                      : ch == CH_ROWS  ? resident_grid(tm_walk_queue<false, true, false, CH_ROWS>, div_up(n, 64),
-                                                       walk_blocks_per_cu)
-                                       : resident_grid(tm_walk_queue<false, false, false>, div_up(n, 64),
-                                                       walk_blocks_per_cu);
+    const uint32_t wg = ch == CH_ROWS ? resident_grid(tm_walk_queue<false, true, false, CH_ROWS>, div_up(n, 64),
+                                                      walk_blocks_per_cu)
+                                      : resident_grid(tm_walk_queue<false, false, false>, div_up(n, 64),
+                                                      walk_blocks_per_cu);
 #define TM_Q(S, X, Y, C)                                                                                           \
     hipLaunchKernelGGL((tm_walk_queue<S, X, Y, C>), dim3(wg), blk, 0, st, im, off, n, qb.twords, qb.words,       \
                        qb.meta, qb.path, qb.stage, qb.kstage, K, key_words, counts, qb.ws, stats,                \
                        hist ? stats + HIST_OFF : nullptr, qb.perm, qb.twords_s, qb.meta_s, spill, qb.spill_head,   \
-                       qb.spill_chunks, bytes)
+                       qb.spill_chunks)
     if (ch == CH_ROWS) {
         if (xcdq) TM_Q(false, true, false, CH_ROWS); else TM_Q(false, false, false, CH_ROWS);
-    } else if (ch == CH_FUSED) {
-        if (xcdq) TM_Q(false, true, false, CH_FUSED); else TM_Q(false, false, false, CH_FUSED);
     } else if (keys) {
         if (stats_mode) TM_Q(true, true, true, CH_NONE); else TM_Q(false, true, true, CH_NONE);
     } else if (stats_mode) {
