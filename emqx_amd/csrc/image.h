@@ -261,11 +261,29 @@ TM_HD uint64_t edge_home(uint32_t parent, uint32_t word, uint64_t slot_mask) {
 
 // word hash: 8-byte little-endian chunks folded with a multiply-xorshift; the
 // value never decides identity (the dictionary verifies bytes), only placement.
+// TM_WHASH32: the same with 32-bit multiplies only (two lanes of state,
+// cross-mixed), for the VALU-bound tokenizer
+#ifndef TM_WHASH32
+#define TM_WHASH32 1
+#endif
 TM_HD uint64_t word_hash_step(uint64_t h, uint64_t chunk) {
+    if (TM_WHASH32) {
+        uint32_t a = ((uint32_t)h ^ (uint32_t)chunk) * 0x9E3779B1u;
+        uint32_t b = ((uint32_t)(h >> 32) ^ (uint32_t)(chunk >> 32)) * 0x85EBCA77u;
+        a ^= b >> 15;
+        b ^= a >> 13;
+        return ((uint64_t)b << 32) | a;
+    }
     h ^= chunk; h *= 0x9E3779B97F4A7C15ULL; h ^= h >> 29;
     return h;
 }
 TM_HD uint64_t word_hash_final(uint64_t h, uint32_t len) {
+    if (TM_WHASH32) {
+        const uint32_t a = fmix32((uint32_t)h ^ (len * 0x27D4EB2Fu) ^ ((uint32_t)(h >> 32) * 0x165667B1u));
+        const uint32_t b = fmix32((uint32_t)(h >> 32) ^ a);
+        const uint64_t r = ((uint64_t)b << 32) | a;
+        return r ? r : 1;
+    }
     h = fmix64(h ^ ((uint64_t)len * 0xD6E8FEB86659FD93ULL));
     return h ? h : 1;   // 0 marks an empty dict slot
 }

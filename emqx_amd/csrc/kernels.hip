@@ -1177,6 +1177,10 @@ tm_walk_wave(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const u
 #define TM_COPY_WAVE_MIN 16   // A/B at C3: copy-out 0.322 (64) vs 0.283-0.293 ms (16, 0)
 #endif
 constexpr uint32_t COPY_WAVE_MIN = TM_COPY_WAVE_MIN;
+#ifndef TM_COPY_U
+#define TM_COPY_U 8   // unkeyed copy-out: topics per wave with their row loads in flight together (1: one at a time)
+#endif
+constexpr uint32_t COPY_U = TM_COPY_U;
 
 // SHAPED (option "shape_keys"): a keyed batch walked unkeyed; each id's key
 // is its filter's order key im.fshape[id] (image.h filter_shape), and a
@@ -1238,6 +1242,44 @@ tm_copy_out(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const ui
                 put(p, v[u]);
                 if (KEYS)
                     for (uint32_t q = 0; q < KW; ++q) kout[q * out_cap + p] = kstage[q * kplane + src[u]];
+            }
+        }
+    } else if (!KEYS && COPY_U > 1 && agg >= (uint64_t)COPY_WAVE_MIN * tn) {
+        // high fan-out block, unkeyed: each wave copies a contiguous quarter
+        // of the block's topics, COPY_U topics at a time with all their row
+        // loads (two per lane: 128 ids) issued before the first store, so a
+        // wave has 2 x COPY_U loads in flight instead of one topic's; ids of
+        // a row past 128 (widened rows) in a loop after
+        const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+        const uint32_t q = (tn + 3) / 4, la = w * q, lz = la + q < tn ? la + q : tn;
+        for (uint32_t l0 = la; l0 < lz; l0 += COPY_U) {
+            uint32_t v0[COPY_U], v1[COPY_U];
+#pragma unroll
+            for (uint32_t u = 0; u < COPY_U; ++u) {
+                const uint32_t lt = l0 + u;
+                v0[u] = v1[u] = 0;
+                if (lt < lz) {
+                    const uint32_t prev = lt ? lds_inc[lt - 1] : 0u;
+                    const uint32_t ct = lds_inc[lt] - prev;
+                    const uint32_t j = (ct > K ? ct - K : 0u) + lane;
+                    const uint64_t row = (uint64_t)(t0 + lt) * K + K - ct;
+                    if (j < ct) v0[u] = stage[row + j];
+                    if (j + 64 < ct) v1[u] = stage[row + j + 64];
+                }
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < COPY_U; ++u) {
+                const uint32_t lt = l0 + u;
+                if (lt >= lz || ood(lt)) continue;
+                const uint32_t prev = lt ? lds_inc[lt - 1] : 0u;
+                const uint32_t ct = lds_inc[lt] - prev;
+                const uint64_t ob = base + prev;
+                const uint64_t row = (uint64_t)(t0 + lt) * K + K - ct;
+                const uint32_t j = (ct > K ? ct - K : 0u) + lane;
+                if (j < ct && ob + j < out_cap) put(ob + j, v0[u]);
+                if (j + 64 < ct && ob + j + 64 < out_cap) put(ob + j + 64, v1[u]);
+                for (uint32_t jj = j + 128; jj < ct; jj += 64)
+                    if (ob + jj < out_cap) put(ob + jj, stage[row + jj]);
             }
         }
     } else if (agg >= (uint64_t)COPY_WAVE_MIN * tn) {
