@@ -175,12 +175,32 @@ __device__ __forceinline__ uint64_t next_slash(const B& bytes, uint64_t q, uint6
 // returns the number of levels (N slashes -> N+1 levels, empty levels kept).
 // Software-pipelined by one level: level k+1 is scanned, hashed and its
 // dictionary slot requested before level k's slot is resolved.
+#ifndef TM_TOK_LEAN
+#define TM_TOK_LEAN 0   // A/B builds: tokenizer without LDS staging or pipelining (fewer registers, no LDS)
+#endif
 template <class B>
 __device__ __forceinline__ uint32_t tokenize_topic(const ImageView& im, const B& bytes, uint64_t b, uint64_t e,
                                                    uint32_t (&tw)[WREG], uint32_t* lw, bool& ood) {
     uint32_t lev = 0;
     ood = false;
     bool found;
+    if (TM_TOK_LEAN) {   // one level at a time
+        uint64_t s = b;
+        for (;;) {
+            const uint64_t q = next_slash(bytes, s, e, found);
+            const uint32_t w = dict_end(im, bytes, dict_begin(im, bytes, s, (uint32_t)(q - s)));
+            ood |= w == WORD_PLUS || w == WORD_HASH;
+            if (lev < WREG) {
+#pragma unroll
+                for (uint32_t k = 0; k < WREG; ++k) tw[k] = lev == k ? w : tw[k];
+            } else {
+                lw[lev] = w;
+            }
+            ++lev;
+            if (!found) return lev;
+            s = q + 1;
+        }
+    }
     uint64_t q = next_slash(bytes, b, e, found);
     DictProbe cur = dict_begin(im, bytes, b, (uint32_t)(q - b));
     for (;;) {
@@ -253,8 +273,12 @@ __global__ void __launch_bounds__(BLOCK)
 tm_tokenize(ImageView im, const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint32_t n,
             uint32_t* __restrict__ twords, uint32_t* __restrict__ words, uint32_t* __restrict__ meta,
             uint32_t* __restrict__ skeys, uint32_t* __restrict__ svals) {
-    __shared__ uint64_t win[BLOCK / 64][TOK_WIN_WORDS];
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (TM_TOK_LEAN) {
+        if (t < n) tokenize_one(im, GlobalBytes{bytes}, off, t, twords, words, meta, skeys, svals);
+        return;
+    }
+    __shared__ uint64_t win[BLOCK / 64][TOK_WIN_WORDS];
     const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     // the wave's 64 topics are contiguous bytes: stage them in LDS with
     // coalesced loads (per-lane 8 B loads of 64 different topics touch 64
@@ -1178,7 +1202,7 @@ tm_walk_wave(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const u
 #endif
 constexpr uint32_t COPY_WAVE_MIN = TM_COPY_WAVE_MIN;
 #ifndef TM_COPY_U
-#define TM_COPY_U 8   // unkeyed copy-out: topics per wave with their row loads in flight together (1: one at a time)
+#define TM_COPY_U 4   // unkeyed copy-out: topics per wave with their row loads in flight together (1: one at a time)
 #endif
 constexpr uint32_t COPY_U = TM_COPY_U;
 
@@ -1196,7 +1220,6 @@ tm_copy_out(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const ui
             const uint32_t* __restrict__ spill_head) {
     const uint64_t kplane = (uint64_t)n * K;   // KEYS: key word j of stage slot x at kstage[j * kplane + x],
                                                // of output p at kout[j * out_cap + p]
-    __shared__ uint32_t lds_path[WREG * BLOCK];
     __shared__ uint32_t lds_inc[BLOCK];
     __shared__ uint64_t lds_scan[BLOCK / 64];
     const uint32_t t0 = blockIdx.x * BLOCK;
@@ -1350,10 +1373,9 @@ tm_copy_out(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const ui
         constexpr bool WK = KEYS || SHAPED;
         TailEmit<WK> em{out, kout, base + ex, out_cap, ood(threadIdx.x) ? 0u : K, c, 0, KW, out_cap};
         WalkStats s2;
-        if (mt & MLONG)
-            walk<false, WK>(im, mt & MN, (mt & MDOLLAR) != 0, GlobalPath{gpath + b + 2ull * t}, mw, em, s2);
-        else
-            walk<false, WK>(im, mt & MN, (mt & MDOLLAR) != 0, LdsPath{lds_path + threadIdx.x}, mw, em, s2);
+        // the topic's global path area (the walk's, for long topics): no LDS
+        // path here, so the copy-out's blocks stay small (1.3 KB of LDS)
+        walk<false, WK>(im, mt & MN, (mt & MDOLLAR) != 0, GlobalPath{gpath + b + 2ull * t}, mw, em, s2);
     }
 }
 
@@ -1371,7 +1393,6 @@ tm_copy_out_sorted(ImageView im, const uint64_t* __restrict__ off, uint32_t n, c
                    const uint64_t* __restrict__ kstage, uint32_t K, uint32_t KW, const uint32_t* __restrict__ counts,
                    const uint64_t* __restrict__ out_off, uint32_t* __restrict__ out, uint64_t* __restrict__ kout,
                    uint64_t out_cap, const uint32_t* __restrict__ perm) {
-    __shared__ uint32_t lds_path[WREG * BLOCK];
     __shared__ uint32_t s_c[BLOCK];
     __shared__ uint64_t s_o[BLOCK];
     const uint64_t kplane = (uint64_t)n * K;
@@ -1405,10 +1426,7 @@ tm_copy_out_sorted(ImageView im, const uint64_t* __restrict__ off, uint32_t n, c
         const MemWords mw{twords + (uint64_t)t * WREG, words + b + t};
         TailEmit<KEYS> em{out, kout, ob, out_cap, K, c, 0, KW, out_cap};
         WalkStats s2;
-        if (mt & MLONG)
-            walk<false, KEYS>(im, mt & MN, (mt & MDOLLAR) != 0, GlobalPath{gpath + b + 2ull * t}, mw, em, s2);
-        else
-            walk<false, KEYS>(im, mt & MN, (mt & MDOLLAR) != 0, LdsPath{lds_path + threadIdx.x}, mw, em, s2);
+        walk<false, KEYS>(im, mt & MN, (mt & MDOLLAR) != 0, GlobalPath{gpath + b + 2ull * t}, mw, em, s2);
     }
 }
 

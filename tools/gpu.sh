@@ -6,6 +6,7 @@
 #   smoke     __graft_entry__.smoke()
 #   bench     python bench.py $BENCH_ARGS                -> bench.json / bench.log
 #   prof      rocprofv3 --kernel-trace --stats of the bench -> prof/ (kernel_stats.csv)
+#   prof3     the same over 3 streams, with the kernel overlap (tools/overlap.py) -> overlap.json
 #   pmc       PMC passes (tools/pmc_passes.sh)           -> pmc/summary.json
 #   traffic   per-launch walk traffic from those passes  -> profiles/traffic_c3.json (read by bench)
 #   cmd       an arbitrary python command in $CMD         -> cmd.log
@@ -26,6 +27,10 @@ for s in ${STEPS:-tests}; do
              python3 bench.py --steps 10 --warmup 2 --cpu-sample 0 --check 0 --streams 1 --no-extras ${BENCH_ARGS} \
              > "$OUT/prof_bench.json" 2> "$OUT/prof_bench.log" ;;
     pmc)   PMC_DIR=${TAG:-job}/pmc bash tools/pmc_passes.sh ;;
+    prof3) timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof3" -o run -- \
+             python3 bench.py --steps 20 --warmup 3 --cpu-sample 0 --check 0 --streams 3 --no-extras ${BENCH_ARGS} \
+             > "$OUT/prof3_bench.json" 2> "$OUT/prof3_bench.log" && \
+           python3 tools/overlap.py "$OUT/prof3/run_kernel_trace.csv" 20 > "$OUT/overlap.json" ;;
     prof4) timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof4" -o run -- \
              python3 bench.py --config 4 --steps 10 --warmup 2 --cpu-sample 0 --check 0 --streams 1 --no-extras \
              > "$OUT/prof4_bench.json" 2> "$OUT/prof4_bench.log" ;;
