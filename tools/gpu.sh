@@ -30,7 +30,7 @@ for s in ${STEPS:-tests}; do
     prof3) timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof3" -o run -- \
              python3 bench.py --steps 20 --warmup 3 --cpu-sample 0 --check 0 --streams 3 --no-extras ${BENCH_ARGS} \
              > "$OUT/prof3_bench.json" 2> "$OUT/prof3_bench.log" && \
-           python3 tools/overlap.py "$OUT/prof3/run_kernel_trace.csv" 20 > "$OUT/overlap.json" ;;
+           python3 tools/overlap.py "$OUT/prof3/run_kernel_trace.csv" 23 2 > "$OUT/overlap.json" ;;
     prof4) timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof4" -o run -- \
              python3 bench.py --config 4 --steps 10 --warmup 2 --cpu-sample 0 --check 0 --streams 1 --no-extras \
              > "$OUT/prof4_bench.json" 2> "$OUT/prof4_bench.log" ;;

@@ -2,10 +2,12 @@
 last N walk launches, how long the other match-pipeline kernels ran beside a
 walk (on another queue) versus serially.
 
-    python tools/overlap.py gpurun_out/<tag>/prof3/run_kernel_trace.csv [N]
+    python tools/overlap.py gpurun_out/<tag>/prof3/run_kernel_trace.csv [N] [SKIP]
 
+N walks after the first SKIP (default 2: bench.py's two untimed sizing
+passes), i.e. the warm-up and timed steps (the serial roof steps follow).
 Prints one JSON object: per kernel family the summed duration, the part of
-it that overlapped a walk, and the wall time the pipeline spanned.
+it that overlapped another walk, and the wall time the pipeline spanned.
 """
 import csv
 import json
@@ -19,7 +21,7 @@ def family(name):
     return None
 
 
-def main(path, last=20):
+def main(path, last=20, skip=2):
     rows = []
     with open(path) as f:
         for r in csv.DictReader(f):
@@ -27,7 +29,7 @@ def main(path, last=20):
             if fam:
                 rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), fam, r["Queue_Id"]))
     rows.sort()
-    walks = [r for r in rows if r[2] == "tm_walk_queue"][-last:]
+    walks = [r for r in rows if r[2] == "tm_walk_queue"][skip:skip + last]
     if not walks:
         print(json.dumps({"error": "no walks"}))
         return
@@ -40,8 +42,8 @@ def main(path, last=20):
             if f != fam:
                 continue
             tot += e - s
-            if fam != "tm_walk_queue":
-                for ws, we, _, wq in walks:
+            for ws, we, _, wq in walks:
+                if (ws, we) != (s, e):
                     ov += max(0, min(e, we) - max(s, ws))
         out["families"][fam] = {"sum_ms": tot / 1e6, "beside_walk_ms": ov / 1e6}
     # busy union of all pipeline kernels
@@ -59,4 +61,4 @@ def main(path, last=20):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 20)
+    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 20, int(sys.argv[3]) if len(sys.argv) > 3 else 2)
