@@ -1873,7 +1873,7 @@ struct tm_engine {
         w.stage.ensure(((size_t)n * d.stage_k + 4) * 4);
         if (key_words) w.kstage.ensure(((size_t)n * d.stage_k * key_words + 4) * 8);
         w.spill_chunks = 0;
-        if (!key_words && spill_on && !presort && d.spill_chunks >= 8) {
+        if (!key_words && spill_on && (!presort || chunk_rows) && d.spill_chunks >= 8) {
             w.spill.ensure((size_t)d.spill_chunks * SPILL_CHUNK * 4);
             w.spill_head.ensure((size_t)n * 4 + 4);
             w.spill_chunks = (uint32_t)d.spill_chunks;
@@ -2009,7 +2009,7 @@ struct tm_engine {
             qb.spill_head = w.spill_head.as<uint32_t>();
             qb.spill_chunks = w.spill_chunks;
         }
-        w.sorted = presort != 0;
+        w.sorted = queue_rows_by_position(qb, stats_enabled);   // the copy-out moves rows by perm
         HIPCHK(launch_queue(stats_enabled, xcdq != 0, im, bytes, off, n, qb, d.stage_k, counts, out_off, ids, keys,
                             cap, total, sp, st, timing_enabled ? marks : nullptr, walk_bpc, hist_enabled != 0,
                             keys ? key_words : 1u));

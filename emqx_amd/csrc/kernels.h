@@ -64,7 +64,13 @@ struct QueueBufs {
 // digit counters of the presort of n topics (256 per 4096-topic tile)
 uint32_t presort_counts(uint32_t n);
 hipError_t launch_presort(const uint32_t* twords, const uint32_t* meta, uint32_t n, const QueueBufs& qb,
-                          hipStream_t st);
+                          hipStream_t st, bool gather = true);
+// true when launch_queue's walk of a presorted batch writes stage row p for
+// queue position p (the copy-out then moves row p to topic perm[p]): without
+// chunk rows, or keyed / stats walks.  With chunk rows the walk reads each
+// chunk's rows through perm and writes stage rows, counts and spill heads by
+// topic, so the ordinary copy-out (and spill) applies.
+bool queue_rows_by_position(const QueueBufs& qb, bool stats_mode);
 
 // tokenize -> NFA walk -> scan -> copy-out, all on st.  marks: 8 events,
 // [2i] before / [2i+1] after stage i, or null.  out_cap == 0: counts and

@@ -912,6 +912,7 @@ constexpr int CH_NONE = 0, CH_ROWS = 1;
 struct ChunkRows {
     uint32_t w[QCHUNK][CW];
     uint32_t meta[QCHUNK];
+    uint32_t topic[QCHUNK];   // the topic at each queue position (presorted batches: perm)
 };
 template <bool STATS, bool XCDQ, bool KEYS, int CH = CH_NONE>
 __global__ void __launch_bounds__(BLOCK) TM_WALK_ATTR
@@ -999,8 +1000,12 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
                 // a new chunk: its rows to LDS, all lanes at once (uniform branch)
                 const uint32_t t = g + lane;
                 if (t < gend) {
-                    CR.meta[lane] = meta[t];
-                    const uint4* src = reinterpret_cast<const uint4*>(twords + (uint64_t)t * WREG);
+                    // a presorted batch: queue position t walks topic perm[t], whose row
+                    // is read here (the rows are not gathered into walk order)
+                    const uint32_t tt = perm ? perm[t] : t;
+                    CR.topic[lane] = tt;
+                    CR.meta[lane] = meta[tt];
+                    const uint4* src = reinterpret_cast<const uint4*>(twords + (uint64_t)tt * WREG);
                     const uint4 a0 = src[0], a1 = src[1];   // quad 1 may be stale past the topic's levels: unread
                     *reinterpret_cast<uint4*>(&CR.w[lane][0]) = a0;
                     *reinterpret_cast<uint4*>(&CR.w[lane][4]) = a1;
@@ -1020,7 +1025,9 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
                 else if (g + (rank - avail) < gend) i = g + (rank - avail);
                 if (i != NO_TOPIC) {
                     // i: queue position = stage row; ti: the topic
-                    const uint32_t ti = CH != CH_NONE ? i : perm ? perm[i] : i;
+                    // CH: stage rows, counts and spill heads by topic (a presorted
+                    // batch then needs no position-ordered copy-out)
+                    const uint32_t ti = CH != CH_NONE ? CR.topic[i - cbase] : perm ? perm[i] : i;
                     const uint32_t* tws = CH == CH_NONE && perm ? twords_s : twords;
                     const uint32_t mt = CH != CH_NONE ? CR.meta[i - cbase] : perm ? meta_s[i] : meta[i];
                     const uint32_t nl = mt & MN;
@@ -1028,11 +1035,11 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
                     lev_sum += nl;
                     maxl = nl > maxl ? nl : maxl;
                     is_long = (mt & MLONG) != 0;
-                    em.row = stage + (uint64_t)i * K;
+                    em.row = stage + (uint64_t)(CH != CH_NONE ? ti : i) * K;
                     if (KEYS) em.krow = kstage + (uint64_t)i * K;
                     em.cnt = 0;
                     em.sfail = false;
-                    const uint32_t* tw = tws + (uint64_t)i * WREG;
+                    const uint32_t* tw = tws + (uint64_t)(CH != CH_NONE ? ti : i) * WREG;
                     bool go;
                     if (!is_long && CH != CH_NONE && nl <= CW) {
                         const uint32_t* cw = CR.w[i - cbase];
@@ -1725,7 +1732,8 @@ hipError_t launch_queue(bool stats_mode, bool xcdq, const ImageView& im, const u
     // chunk rows (option "chunk_rows"): the walk of an unkeyed batch in
     // arrival order stages each chunk's rows in LDS
     const bool lane_walk = !(qb.wave_walk && !keys && !stats_mode && !qb.perm);
-    const int ch = (lane_walk && !keys && !stats_mode && !qb.perm && qb.chunk_rows) ? CH_ROWS : CH_NONE;
+    const int ch = (lane_walk && !keys && !stats_mode && qb.chunk_rows) ? CH_ROWS : CH_NONE;
+    const bool by_pos = queue_rows_by_position(qb, stats_mode);   // presorted without chunk rows
     mark(0);
     if (TM_TOK2)
         hipLaunchKernelGGL(tm_tokenize2, dim3(div_up(n, 64)), dim3(64), 0, st, im, bytes, off, n, qb.twords, qb.words,
@@ -1733,8 +1741,8 @@ hipError_t launch_queue(bool stats_mode, bool xcdq, const ImageView& im, const u
     else
         hipLaunchKernelGGL(tm_tokenize, g, blk, 0, st, im, bytes, off, n, qb.twords, qb.words, qb.meta,
                            qb.perm ? qb.sort_keys : nullptr, qb.perm ? qb.perm : nullptr);
-    if (qb.perm) {   // option "presort": perm and the rows in walk order (presort.hip)
-        err = launch_presort(qb.twords, qb.meta, n, qb, st);
+    if (qb.perm) {   // option "presort": perm (and the rows in walk order unless chunk rows read them by perm)
+        err = launch_presort(qb.twords, qb.meta, n, qb, st, by_pos);
         if (err != hipSuccess) return err;
     }
     mark(1);
@@ -1759,7 +1767,7 @@ hipError_t launch_queue(bool stats_mode, bool xcdq, const ImageView& im, const u
         return hipGetLastError();
     }
     // spill chunks: unkeyed walks in arrival order (presorted rows re-walk)
-    uint32_t* const spill = (!keys && !qb.perm && qb.spill_chunks >= QRANGES) ? qb.spill : nullptr;
+    uint32_t* const spill = (!keys && !by_pos && qb.spill_chunks >= QRANGES) ? qb.spill : nullptr;
     const uint32_t wg = ch == CH_ROWS ? resident_grid(tm_walk_queue<false, true, false, CH_ROWS>, div_up(n, 64),
                                                       walk_blocks_per_cu)
                                       : resident_grid(tm_walk_queue<false, false, false>, div_up(n, 64),
@@ -1786,11 +1794,18 @@ hipError_t launch_queue(bool stats_mode, bool xcdq, const ImageView& im, const u
     mark(5);
     mark(6);
     if (out_cap) {
-        err = launch_copy(im, bytes, off, n, qb, K, key_words, counts, out_off, out, out_keys, out_cap, st);
+        QueueBufs qc = qb;
+        if (!by_pos) qc.perm = nullptr;   // stage rows by topic
+        err = launch_copy(im, bytes, off, n, qc, K, key_words, counts, out_off, out, out_keys, out_cap, st);
         if (err != hipSuccess) return err;
     }
     mark(7);
     return hipGetLastError();
+}
+
+bool queue_rows_by_position(const QueueBufs& qb, bool stats_mode) {
+    const bool keys = qb.kstage != nullptr;
+    return qb.perm != nullptr && (keys || stats_mode || !qb.chunk_rows);
 }
 
 }  // namespace tmx

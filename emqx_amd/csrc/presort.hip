@@ -119,7 +119,7 @@ tm_presort_gather(const uint32_t* __restrict__ perm, const uint32_t* __restrict_
 }
 
 hipError_t launch_presort(const uint32_t* twords, const uint32_t* meta, uint32_t n, const QueueBufs& qb,
-                          hipStream_t st) {
+                          hipStream_t st, bool gather) {
     if (n == 0) return hipSuccess;
     const uint32_t tiles = (n + PS_TILE - 1) / PS_TILE, nc = 256u * tiles;
     // ping-pong: keys A = sort_keys, B = sort_keys + n; values A = perm, B = sort_vals;
@@ -140,8 +140,9 @@ hipError_t launch_presort(const uint32_t* twords, const uint32_t* meta, uint32_t
         va = vb;
         vb = t;
     }
-    hipLaunchKernelGGL(tm_presort_gather, dim3((n + PS_BLOCK - 1) / PS_BLOCK), dim3(PS_BLOCK), 0, st, qb.perm,
-                       twords, meta, n, qb.twords_s, qb.meta_s);
+    if (gather)   // rows into walk order (a walk with chunk rows reads them through perm instead)
+        hipLaunchKernelGGL(tm_presort_gather, dim3((n + PS_BLOCK - 1) / PS_BLOCK), dim3(PS_BLOCK), 0, st, qb.perm,
+                           twords, meta, n, qb.twords_s, qb.meta_s);
     return hipGetLastError();
 }
 
