@@ -307,122 +307,9 @@ tm_tokenize(ImageView im, const uint8_t* __restrict__ bytes, const uint64_t* __r
 
 
 
-// ---------------------------------------------------------------------------
-// tm_tokenize2: the same output, in two phases per wave of 64 topics (lane j
-// = topic t0 + j, bytes staged in LDS as above):
-//   A  each lane finds its topic's level starts (exact per-byte '/' masks of
-//      aligned 8-byte words, every slash of a word in one pass) -> LDS;
-//   B  level-major, four levels at a time: every lane hashes its topic's
-//      levels k..k+3 and issues their four dictionary-slot loads before it
-//      resolves the first, ids to an LDS row, then 16 B row stores.
-// No level is scanned twice and no per-level register shuffle is needed
-// (tm_tokenize: ~274 VALU instructions per level, profiles/r03_head).
-// Topics of more than WREG levels take the per-lane path.
-#ifndef TM_TOK2
-#define TM_TOK2 1
-#endif
 __device__ __forceinline__ void wave_sync_lds() {
     __threadfence_block();
     __builtin_amdgcn_wave_barrier();
-}
-constexpr uint32_t T2_U = 4;   // levels whose slot loads are in flight together
-struct Tok2Lds {
-    uint64_t win[TOK_WIN_WORDS];      // the wave's topic bytes
-    uint16_t lst[64][WREG + 1];       // level starts, window-relative ([lev]: end + 1)
-};
-__device__ __forceinline__ uint64_t slash_bytes(uint64_t w) {   // 0x80 in every byte that is '/'
-    const uint64_t x = w ^ 0x2F2F2F2F2F2F2F2FULL, m = 0x7F7F7F7F7F7F7F7FULL;
-    return ~(((x & m) + m) | x | m);
-}
-__global__ void __launch_bounds__(64)
-tm_tokenize2(ImageView im, const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint32_t n,
-             uint32_t* __restrict__ twords, uint32_t* __restrict__ words, uint32_t* __restrict__ meta,
-             uint32_t* __restrict__ skeys, uint32_t* __restrict__ svals) {
-    __shared__ Tok2Lds L;   // one wave per block: 10 KB of LDS
-    const uint32_t lane = threadIdx.x;
-    const uint32_t t0 = blockIdx.x * 64, t = t0 + lane;
-    if (t0 >= n) return;   // the whole wave
-    const uint32_t t1 = t0 + 64 < n ? t0 + 64 : n;
-    const uint64_t wbase = off[t0] & ~7ull;
-    const uint64_t nw = (off[t1] - wbase + 7) >> 3;
-    if (nw > TOK_WIN_WORDS) {   // uniform: a window that does not fit, per lane from global memory
-        if (t < n) tokenize_one(im, GlobalBytes{bytes}, off, t, twords, words, meta, skeys, svals);
-        return;
-    }
-    for (uint64_t k = lane; k < nw; k += 64) L.win[k] = *reinterpret_cast<const uint64_t*>(bytes + wbase + 8 * k);
-    wave_sync_lds();
-    const LdsBytes lb{L.win, wbase};
-    // A: level starts
-    uint64_t b = 0, e = 0;
-    uint32_t lev = 0;
-    if (t < n) {
-        b = off[t];
-        e = off[t + 1];
-        L.lst[lane][0] = (uint16_t)(b - wbase);
-        lev = 1;
-        for (uint64_t a = b & ~7ull; a < e; a += 8) {
-            uint64_t z = slash_bytes(lb.word(a));
-            if (a < b) z &= ~0ull << (8 * (b - a));
-            if (e - a < 8) z &= ~0ull >> (64 - 8 * (e - a));
-            while (z) {
-                const uint64_t pos = a + (__builtin_ctzll(z) >> 3);
-                if (lev <= WREG) L.lst[lane][lev] = (uint16_t)(pos + 1 - wbase);
-                ++lev;
-                z &= z - 1;
-            }
-        }
-        if (lev <= WREG) L.lst[lane][lev] = (uint16_t)(e + 1 - wbase);   // end sentinel: "next start"
-    }
-    const bool longt = lev > WREG;
-    // B: words, level-major
-    uint32_t nlev = longt ? 0u : lev;
-    for (int o = 32; o > 0; o >>= 1) {
-        const uint32_t y = (uint32_t)__shfl_xor((int)nlev, o, 64);
-        nlev = y > nlev ? y : nlev;
-    }
-    bool ood = false;
-    uint32_t pkey = 0;   // option "presort": presort_key, built level by level
-    uint4* row = reinterpret_cast<uint4*>(twords + (uint64_t)(t < n ? t : 0) * WREG);
-    static_assert(T2_U == 4, "a row quad per pass");
-    for (uint32_t k0 = 0; k0 < nlev; k0 += T2_U) {
-        DictProbe pr[T2_U];
-#pragma unroll
-        for (uint32_t u = 0; u < T2_U; ++u) {
-            const uint32_t k = k0 + u;
-            if (!longt && k < lev) {
-                const uint64_t s0 = wbase + L.lst[lane][k], s1 = wbase + L.lst[lane][k + 1] - 1;
-                pr[u] = dict_begin(im, lb, s0, (uint32_t)(s1 - s0));
-            }
-        }
-        uint32_t wq[T2_U];
-#pragma unroll
-        for (uint32_t u = 0; u < T2_U; ++u) {
-            const uint32_t k = k0 + u;
-            wq[u] = WORD_NONE;
-            if (!longt && k < lev) {
-                wq[u] = dict_end(im, lb, pr[u]);
-                ood |= wq[u] == WORD_PLUS || wq[u] == WORD_HASH;
-            }
-            if (k < 8) {
-                constexpr uint32_t bits[8] = {6, 5, 5, 4, 4, 3, 3, 2};
-                pkey = (pkey << bits[k]) | (k < lev ? (wq[u] * 0x9E3779B1u) >> (32 - bits[k]) : 0u);
-            }
-        }
-        if (t < n && !longt && k0 < lev) row[k0 / 4] = make_uint4(wq[0], wq[1], wq[2], wq[3]);
-    }
-    for (uint32_t k0 = (nlev + 3) & ~3u; k0 < 8; k0 += T2_U)   // presort key: levels past the wave's deepest topic are 0
-        pkey <<= (k0 == 0 ? 6 + 5 + 5 + 4 : 4 + 3 + 3 + 2);
-    if (t >= n) return;
-    if (longt) {   // more than WREG levels: the per-lane tokenizer over the same LDS bytes
-        tokenize_one(im, lb, off, t, twords, words, meta, skeys, svals);
-        return;
-    }
-    const uint32_t dollar = (e > b && lb.byte(b) == '$') ? 1u : 0u;
-    meta[t] = lev | (dollar << 31) | (ood ? MOOD : 0u);
-    if (skeys) {   // option "presort"
-        skeys[t] = pkey;
-        svals[t] = t;
-    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1735,12 +1622,8 @@ hipError_t launch_queue(bool stats_mode, bool xcdq, const ImageView& im, const u
     const int ch = (lane_walk && !keys && !stats_mode && qb.chunk_rows) ? CH_ROWS : CH_NONE;
     const bool by_pos = queue_rows_by_position(qb, stats_mode);   // presorted without chunk rows
     mark(0);
-    if (TM_TOK2)
-        hipLaunchKernelGGL(tm_tokenize2, dim3(div_up(n, 64)), dim3(64), 0, st, im, bytes, off, n, qb.twords, qb.words,
-                           qb.meta, qb.perm ? qb.sort_keys : nullptr, qb.perm ? qb.perm : nullptr);
-    else
-        hipLaunchKernelGGL(tm_tokenize, g, blk, 0, st, im, bytes, off, n, qb.twords, qb.words, qb.meta,
-                           qb.perm ? qb.sort_keys : nullptr, qb.perm ? qb.perm : nullptr);
+    hipLaunchKernelGGL(tm_tokenize, g, blk, 0, st, im, bytes, off, n, qb.twords, qb.words, qb.meta,
+                       qb.perm ? qb.sort_keys : nullptr, qb.perm ? qb.perm : nullptr);
     if (qb.perm) {   // option "presort": perm (and the rows in walk order unless chunk rows read them by perm)
         err = launch_presort(qb.twords, qb.meta, n, qb, st, by_pos);
         if (err != hipSuccess) return err;
