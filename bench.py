@@ -6,9 +6,11 @@ through the whole hot path of emqx_trie:match/1: device tokenizer
 
 Workload: 10M distinct wildcard filters (8 levels max,
 p+ 0.20, p# 0.05, Zipf(1.0) words over 16/64/256/1024/4096x4), replicated on
-every GPU.  Strong scaling (default, as §8(d) defines C3): one batch of 8M
-8-level topics per step, split 1/2/4/8 ways over the ranks; `--scaling weak`
-gives every rank its own batch instead.  Steps rotate over `--batches`
+every GPU.  Weak scaling (default): every rank walks its own batch of 8M
+8-level topics per step (rank r's topic stream r; rank 0's batches are the
+N = 1 batches), since topics are independent units and the replicated path
+has no data-path collective; `--scaling strong` splits one 8M-topic batch
+1/2/4/8 ways over the ranks instead.  Steps rotate over `--batches`
 distinct batches (no batch is replayed back to back, so L2 / MALL never hold
 the previous step's topics).  No collective on the data path.  `value` =
 topics matched per second over all ranks (max-over-ranks step time).
@@ -59,9 +61,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", type=int, default=3, help="SURVEY §8(d) config (3 = the metric's)")
     ap.add_argument("--filters", type=int, default=None, help="override filter count")
-    ap.add_argument("--scaling", choices=["strong", "weak"], default="strong",
-                    help="strong: one batch per step split over the ranks (C3 as §8(d) defines it); "
-                         "weak: a batch per rank")
+    ap.add_argument("--scaling", choices=["strong", "weak"], default="weak",
+                    help="weak (default): a batch of --topics per rank per step; "
+                         "strong: one batch per step split over the ranks")
     ap.add_argument("--topics", type=int, default=None,
                     help="topics per batch (strong, default the config's: 8M at C3) or per GPU (weak, default 1M)")
     ap.add_argument("--batches", type=int, default=2, help="distinct batches the steps rotate over")
@@ -299,7 +301,7 @@ def main():
             dist.destroy_process_group()
         return
     cfg = W.CONFIGS[a.config]
-    a.topics = a.topics or (cfg["topics"] if a.scaling == "strong" else 1_000_000)
+    a.topics = a.topics or cfg["topics"]   # per step: the whole batch (strong) or each rank's (weak)
     n_filters = a.filters or cfg["filters"]
     t0 = time.time()
     fb, fo = W.filters(a.config, n=n_filters)
@@ -469,7 +471,8 @@ def main():
                                        a.batches, a.streams),
                        "filters": n_filters, "topics_per_step": int(topics_per_step),
                        "topics_per_gpu_step": n0, "levels": cfg["levels"],
-                       "parallelism": "replicated trie x %d, topic batch split by rank" % world},
+                       "parallelism": "replicated trie x %d, %s" % (
+                           world, "topic batch split by rank" if a.scaling == "strong" else "a topic batch per rank")},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
                          "traffic_frac": (traffic / HBM_PEAK_GBS) if traffic else None,
