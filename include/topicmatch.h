@@ -552,6 +552,24 @@ int  tm_rewrite_match_batch_device(tm_rewrite* r, const uint8_t* d_topics, const
  *              default 4; 0 = DFS preorder throughout); forces a relayout
  *   "presort"  1 = walk each batch in the order of a key of its first words
  *              (device radix sort; default 0)
+ *   "chunk_rows" 1 = a wave copies each taken chunk's 64 tokenized rows to
+ *              LDS at once (default), 0 = each lane reads its topic's row
+ *   "spill"    1 = ids past a stage row go to per-XCD spill chunks (default),
+ *              0 = the copy-out re-walks such topics
+ *   "wave_walk_max" batches of at most this many topics take the
+ *              wave-per-topic level-synchronous walk (default 32768, 0 = never)
+ *   "summaries" 1 = subtree summaries prune dead '+' / literal subtrees (default)
+ *   "order"    relayout order bits (default 15: '+' child after its parent,
+ *              '#' nodes last, heat order, heat from filter counts)
+ *   "edge_load" edge tables kept at load <= 1/edge_load (2..16, default 4)
+ *   "hot_edges" parents of depth < D probe a separate small table (0 = off)
+ *   "slots"    per-batch workspace slots rotated over by consecutive batches
+ *   "double_buffer" 1 = two image epochs per replica (commits never wait on
+ *              walks; default), 0 = one
+ *   "shape_keys" 1 = keyed batches of <= 31 levels walk unkeyed and key each
+ *              id by its filter's shape (the shard engines set it), 0 = keyed
+ *              walk (default)
+ *   "route_gc" garbage dest entries before a route-pool compaction is considered
  * TM_EINVAL for unknown names / values. */
 int tm_set_option(tm_engine* e, const char* name, int64_t value);
 
