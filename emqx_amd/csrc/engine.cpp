@@ -13,9 +13,6 @@
 // The host mirror IS the host copy of the device image (image.h): inserts and
 // deletes patch it in place and mark 64 KiB pages dirty; tm_commit uploads
 // the dirty pages (or the whole table after a resize) on the engine stream.
-#ifndef TM_IMG_MALLOC
-#define TM_IMG_MALLOC 0   // A/B: image tables >= 256 MB via hipMalloc (1) / contiguous (2)
-#endif
 #ifndef TM_CHUNK_ROWS
 #define TM_CHUNK_ROWS 1
 #endif
@@ -156,19 +153,6 @@ struct DevBuf {
         p = nullptr;
         bytes = 0;
         size_t want = std::max<size_t>(256, (size_t)(need * slack));
-        if (TM_IMG_MALLOC && want >= (256ull << 20)) {
-            // A/B: large tables outside the stream-ordered pool (1: hipMalloc,
-            // 2: physically contiguous), for larger translation fragments
-            hipError_t e = hipErrorUnknown;
-            if (TM_IMG_MALLOC == 2) e = hipExtMallocWithFlags(&p, want, hipDeviceMallocContiguous);
-            if (e != hipSuccess) e = hipMalloc(&p, want);
-            if (e == hipSuccess) {
-                bytes = want;
-                pooled = false;
-                return true;
-            }
-            p = nullptr;
-        }
         hipError_t e = hipMallocAsync(&p, want, st);
         if (e != hipSuccess) {
             p = nullptr;
