@@ -426,8 +426,15 @@ constexpr int HIST_OFF = 8;   // hist = stats + HIST_OFF
 #ifndef TM_PF1
 #define TM_PF1 0
 #endif
+// TM_PEND_MASK: levels with a pending '+' child as a bit mask in the cursor
+// (LDS paths, levels < 32), so a pop reads one path entry (the highest set
+// bit below r) instead of scanning the levels down one LDS read at a time
+#ifndef TM_PEND_MASK
+#define TM_PEND_MASK 0
+#endif
 struct Cursor {
     uint32_t v, r, n, r0;   // node to visit next and its level; topic levels; start level
+    uint32_t pend;          // TM_PEND_MASK: bit k = path(k) holds a '+' child still to visit (k < r)
     uint64_t key;           // KEYS: fold branches taken above level r (rank_sym), key word 0
     uint32_t pf_id;         // TM_PF1: node whose half is in pf (NODE_NONE: none)
     uint4 pf;
@@ -508,10 +515,12 @@ struct MemWords {
 };
 
 struct LdsPath {
+    static constexpr bool kMask = TM_PEND_MASK != 0;   // levels < WREG: the cursor's pending mask applies
     uint32_t* base;   // [level][BLOCK]
     __device__ __forceinline__ uint32_t& operator()(uint32_t r) const { return base[r * BLOCK]; }
 };
 struct GlobalPath {
+    static constexpr bool kMask = false;
     uint32_t* base;
     __device__ __forceinline__ uint32_t& operator()(uint32_t r) const { return base[r]; }
 };
@@ -524,6 +533,7 @@ __device__ __forceinline__ bool walk_begin(const ImageView& im, Cursor& c, uint3
                                            WalkStats& st) {
     c.n = n;
     c.key = 0;
+    c.pend = 0;
     c.pf_id = NODE_NONE;
     if (!dollar) {
         c.v = ROOT;
@@ -612,6 +622,7 @@ __device__ __forceinline__ bool walk_step(const ImageView& im, Cursor& c, Path p
         }
         if (g.child != NODE_NONE) {   // literal subtree first, '+' child pending at level r
             path(r) = KEYS ? (pc | SYM_LIT) : pc;
+            if (Path::kMask) c.pend = pc != NODE_NONE ? (c.pend | (1u << r)) : (c.pend & ~(1u << r));
             v = g.child;
             if (KEYS) key |= rank_sym(r, 1);
             ++r;
@@ -631,12 +642,26 @@ __device__ __forceinline__ bool walk_step(const ImageView& im, Cursor& c, Path p
         }
         if (pc != NODE_NONE) {        // no literal child: straight into the '+' subtree
             path(r) = KEYS ? (NODE_NONE | SYM_PLUS) : NODE_NONE;
+            if (Path::kMask) c.pend &= ~(1u << r);
             c.v = pc;
             c.r = r + 1;
             if (KEYS) c.key = key | rank_sym(r, 2);
             return false;
         }
         break;
+    }
+    if (Path::kMask) {   // pop: the deepest pending level below r, one path read
+        const uint32_t m = c.pend & ((1u << r) - 1u);
+        if (!m) return true;
+        const uint32_t k = 31u - (uint32_t)__builtin_clz(m);
+        const uint32_t p = KEYS ? path(k) & NODE_MASK : path(k);
+        if (STATS && st.hist) atomicAdd(st.hist + 50, 1ull);
+        if (KEYS) path(k) = NODE_NONE | SYM_PLUS;
+        c.pend &= ~(1u << k);
+        c.v = p;
+        c.r = k + 1;
+        if (KEYS) c.key = rank_prefix(key, k) | rank_sym(k, 2);
+        return false;
     }
     for (uint32_t k = r; k > c.r0;) {   // pop to the deepest pending '+' child
         --k;
