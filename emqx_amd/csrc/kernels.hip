@@ -430,7 +430,7 @@ constexpr int HIST_OFF = 8;   // hist = stats + HIST_OFF
 // (LDS paths, levels < 32), so a pop reads one path entry (the highest set
 // bit below r) instead of scanning the levels down one LDS read at a time
 #ifndef TM_PEND_MASK
-#define TM_PEND_MASK 0
+#define TM_PEND_MASK 1   // A/B at C3: walk 9.78 vs 10.08-10.09 ms (profiles/r03_ab)
 #endif
 struct Cursor {
     uint32_t v, r, n, r0;   // node to visit next and its level; topic levels; start level
