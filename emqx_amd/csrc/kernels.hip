@@ -429,6 +429,9 @@ constexpr int HIST_OFF = 8;   // hist = stats + HIST_OFF
 // TM_PEND_MASK: levels with a pending '+' child as a bit mask in the cursor
 // (LDS paths, levels < 32), so a pop reads one path entry (the highest set
 // bit below r) instead of scanning the levels down one LDS read at a time
+#ifndef TM_REFILL_EARLY
+#define TM_REFILL_EARLY 0
+#endif
 #ifndef TM_PEND_MASK
 #define TM_PEND_MASK 1   // A/B at C3: walk 9.78 vs 10.08-10.09 ms (profiles/r03_ab)
 #endif
@@ -939,6 +942,13 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
                     // i: queue position = stage row; ti: the topic
                     // CH: stage rows, counts and spill heads by topic (a presorted
                     // batch then needs no position-ordered copy-out)
+                    // TM_REFILL_EARLY: the chunk row's words are read with its meta and
+                    // topic (one LDS round trip), not after the level count is known
+                    uint4 cw0 = make_uint4(0, 0, 0, 0), cw1 = make_uint4(0, 0, 0, 0);
+                    if (CH != CH_NONE && TM_REFILL_EARLY) {
+                        cw0 = *reinterpret_cast<const uint4*>(CR.w[i - cbase]);
+                        cw1 = *reinterpret_cast<const uint4*>(CR.w[i - cbase] + 4);
+                    }
                     const uint32_t ti = CH != CH_NONE ? CR.topic[i - cbase] : perm ? perm[i] : i;
                     const uint32_t* tws = CH == CH_NONE && perm ? twords_s : twords;
                     const uint32_t mt = CH != CH_NONE ? CR.meta[i - cbase] : perm ? meta_s[i] : meta[i];
@@ -955,8 +965,8 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
                     bool go;
                     if (!is_long && CH != CH_NONE && nl <= CW) {
                         const uint32_t* cw = CR.w[i - cbase];
-                        const uint4 a0 = *reinterpret_cast<const uint4*>(cw);
-                        const uint4 a1 = *reinterpret_cast<const uint4*>(cw + 4);
+                        const uint4 a0 = TM_REFILL_EARLY ? cw0 : *reinterpret_cast<const uint4*>(cw);
+                        const uint4 a1 = TM_REFILL_EARLY ? cw1 : *reinterpret_cast<const uint4*>(cw + 4);
                         rw.w[0] = a0.x;
                         rw.w[1] = a0.y;
                         rw.w[2] = a0.z;
