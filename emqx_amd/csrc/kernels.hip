@@ -429,15 +429,13 @@ constexpr int HIST_OFF = 8;   // hist = stats + HIST_OFF
 // TM_PEND_MASK: levels with a pending '+' child as a bit mask in the cursor
 // (LDS paths, levels < 32), so a pop reads one path entry (the highest set
 // bit below r) instead of scanning the levels down one LDS read at a time
-#ifndef TM_REFILL_EARLY
-#define TM_REFILL_EARLY 0
-#endif
 #ifndef TM_PEND_MASK
 #define TM_PEND_MASK 1   // A/B at C3: walk 9.78 vs 10.08-10.09 ms (profiles/r03_ab)
 #endif
 struct Cursor {
     uint32_t v, r, n, r0;   // node to visit next and its level; topic levels; start level
     uint32_t pend;          // TM_PEND_MASK: bit k = path(k) holds a '+' child still to visit (k < r)
+    uint32_t pp, ppc;       // TM_SPLIT_PROBE: v's edge probe is the next step's load; v's pending '+' child
     uint64_t key;           // KEYS: fold branches taken above level r (rank_sym), key word 0
     uint32_t pf_id;         // TM_PF1: node whose half is in pf (NODE_NONE: none)
     uint4 pf;
@@ -537,6 +535,7 @@ __device__ __forceinline__ bool walk_begin(const ImageView& im, Cursor& c, uint3
     c.n = n;
     c.key = 0;
     c.pend = 0;
+    c.pp = 0;
     c.pf_id = NODE_NONE;
     if (!dollar) {
         c.v = ROOT;
@@ -557,11 +556,73 @@ __device__ __forceinline__ bool walk_begin(const ImageView& im, Cursor& c, uint3
 // the walk pops.  (A variant that resolved edge probes one slot per step,
 // walk_step1, measured 4.10 vs 3.59 ms at C3 and was removed:
 // profiles/r01_v12_heat/walk1_ab.json.)
+// pop from level r to the deepest pending '+' child; true when the walk is complete
+template <bool STATS, bool KEYS, class Path>
+__device__ __forceinline__ bool walk_pop(Cursor& c, Path path, uint32_t r, uint64_t key, WalkStats& st) {
+    if (Path::kMask) {   // the deepest pending level below r, one path read
+        const uint32_t m = c.pend & ((1u << r) - 1u);
+        if (!m) return true;
+        const uint32_t k = 31u - (uint32_t)__builtin_clz(m);
+        const uint32_t p = KEYS ? path(k) & NODE_MASK : path(k);
+        if (STATS && st.hist) atomicAdd(st.hist + 50, 1ull);
+        if (KEYS) path(k) = NODE_NONE | SYM_PLUS;
+        c.pend &= ~(1u << k);
+        c.v = p;
+        c.r = k + 1;
+        if (KEYS) c.key = rank_prefix(key, k) | rank_sym(k, 2);
+        return false;
+    }
+    for (uint32_t k = r; k > c.r0;) {   // scan the path down
+        --k;
+        const uint32_t p = KEYS ? path(k) & NODE_MASK : path(k);
+        if (p != NODE_NONE) {
+            if (STATS && st.hist) atomicAdd(st.hist + 50, 1ull);
+            path(k) = KEYS ? (NODE_NONE | SYM_PLUS) : NODE_NONE;
+            c.v = p;
+            c.r = k + 1;
+            if (KEYS) c.key = rank_prefix(key, k) | rank_sym(k, 2);
+            return false;
+        }
+    }
+    return true;
+}
+
+// TM_SPLIT_PROBE: a WIDE node whose Bloom admits the word defers its edge
+// probe to the next step, so no step chains two dependent global loads (the
+// wave waits for its slowest lane: one lane's probe after its node load
+// stretched the whole step)
+#ifndef TM_SPLIT_PROBE
+#define TM_SPLIT_PROBE 0
+#endif
+
 template <bool STATS, bool KEYS, class Path, class Words, class Emit>
 __device__ __forceinline__ bool walk_step(const ImageView& im, Cursor& c, Path path, const Words& W, Emit& emit,
                                           WalkStats& st) {
     uint32_t v = c.v, r = c.r;
     uint64_t key = KEYS ? c.key : 0ull;
+    if (TM_SPLIT_PROBE && !STATS && !SLOT_RECORD && c.pp) {   // resume v's visit: its probe is this step's load
+        c.pp = 0;
+        Hit g = probe_edge<false>(im, v, W(r), st.probe_loads);
+        if (g.child != NODE_NONE && !sum_useful(g.plus & SUM_ALL, c.n - r - 1)) g.child = NODE_NONE;
+        const uint32_t pc = c.ppc;
+        if (g.child != NODE_NONE) {
+            path(r) = KEYS ? (pc | SYM_LIT) : pc;
+            if (Path::kMask) c.pend = pc != NODE_NONE ? (c.pend | (1u << r)) : (c.pend & ~(1u << r));
+            c.v = g.child;
+            c.r = r + 1;
+            if (KEYS) c.key = key | rank_sym(r, 1);
+            return false;
+        }
+        if (pc != NODE_NONE) {
+            path(r) = KEYS ? (NODE_NONE | SYM_PLUS) : NODE_NONE;
+            if (Path::kMask) c.pend &= ~(1u << r);
+            c.v = pc;
+            c.r = r + 1;
+            if (KEYS) c.key = key | rank_sym(r, 2);
+            return false;
+        }
+        return walk_pop<STATS, KEYS>(c, path, r, key, st);
+    }
     bool leaf = r == c.n;
     uint4 h;
     if (TM_PF1 && !STATS) {
@@ -601,6 +662,17 @@ __device__ __forceinline__ bool walk_step(const ImageView& im, Cursor& c, Path p
             const uint32_t k = c.n - r - 1;
             plus_ok = sum_useful(hf & SUM_ALL, k);
             lit_ok = w < WORD_MAX ? sum_useful((hf >> 15) & SUM_ALL, k) : w == WORD_PLUS ? plus_ok : true;
+        }
+        if (TM_SPLIT_PROBE && !STATS && !SLOT_RECORD && lit_ok && w < WORD_MAX && (plus & WIDE)) {
+            const uint64_t b = word_bloom(w);
+            if (((((uint64_t)lc << 32) | lw) & b) == b) {   // probe at the next step
+                c.pp = 1;
+                c.ppc = plus_ok ? (plus & NODE_MASK) : NODE_NONE;
+                c.v = v;
+                c.r = r;
+                return false;
+            }
+            lit_ok = false;   // the Bloom rejects the word: no literal child
         }
         Hit g = (!STATS && !lit_ok) ? Hit{NODE_NONE, 0, 0, 0, 0, 0, false}
                                     : lit_child<STATS>(im, v, plus, lw, lc, w, st.probe_loads);
@@ -653,32 +725,7 @@ __device__ __forceinline__ bool walk_step(const ImageView& im, Cursor& c, Path p
         }
         break;
     }
-    if (Path::kMask) {   // pop: the deepest pending level below r, one path read
-        const uint32_t m = c.pend & ((1u << r) - 1u);
-        if (!m) return true;
-        const uint32_t k = 31u - (uint32_t)__builtin_clz(m);
-        const uint32_t p = KEYS ? path(k) & NODE_MASK : path(k);
-        if (STATS && st.hist) atomicAdd(st.hist + 50, 1ull);
-        if (KEYS) path(k) = NODE_NONE | SYM_PLUS;
-        c.pend &= ~(1u << k);
-        c.v = p;
-        c.r = k + 1;
-        if (KEYS) c.key = rank_prefix(key, k) | rank_sym(k, 2);
-        return false;
-    }
-    for (uint32_t k = r; k > c.r0;) {   // pop to the deepest pending '+' child
-        --k;
-        const uint32_t p = KEYS ? path(k) & NODE_MASK : path(k);
-        if (p != NODE_NONE) {
-            if (STATS && st.hist) atomicAdd(st.hist + 50, 1ull);
-            path(k) = KEYS ? (NODE_NONE | SYM_PLUS) : NODE_NONE;
-            c.v = p;
-            c.r = k + 1;
-            if (KEYS) c.key = rank_prefix(key, k) | rank_sym(k, 2);
-            return false;
-        }
-    }
-    return true;
+    return walk_pop<STATS, KEYS>(c, path, r, key, st);   // pop to the deepest pending '+' child
 }
 
 template <bool STATS, bool KEYS, class Path, class Words, class Emit>
@@ -942,13 +989,6 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
                     // i: queue position = stage row; ti: the topic
                     // CH: stage rows, counts and spill heads by topic (a presorted
                     // batch then needs no position-ordered copy-out)
-                    // TM_REFILL_EARLY: the chunk row's words are read with its meta and
-                    // topic (one LDS round trip), not after the level count is known
-                    uint4 cw0 = make_uint4(0, 0, 0, 0), cw1 = make_uint4(0, 0, 0, 0);
-                    if (CH != CH_NONE && TM_REFILL_EARLY) {
-                        cw0 = *reinterpret_cast<const uint4*>(CR.w[i - cbase]);
-                        cw1 = *reinterpret_cast<const uint4*>(CR.w[i - cbase] + 4);
-                    }
                     const uint32_t ti = CH != CH_NONE ? CR.topic[i - cbase] : perm ? perm[i] : i;
                     const uint32_t* tws = CH == CH_NONE && perm ? twords_s : twords;
                     const uint32_t mt = CH != CH_NONE ? CR.meta[i - cbase] : perm ? meta_s[i] : meta[i];
@@ -965,8 +1005,8 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
                     bool go;
                     if (!is_long && CH != CH_NONE && nl <= CW) {
                         const uint32_t* cw = CR.w[i - cbase];
-                        const uint4 a0 = TM_REFILL_EARLY ? cw0 : *reinterpret_cast<const uint4*>(cw);
-                        const uint4 a1 = TM_REFILL_EARLY ? cw1 : *reinterpret_cast<const uint4*>(cw + 4);
+                        const uint4 a0 = *reinterpret_cast<const uint4*>(cw);
+                        const uint4 a1 = *reinterpret_cast<const uint4*>(cw + 4);
                         rw.w[0] = a0.x;
                         rw.w[1] = a0.y;
                         rw.w[2] = a0.z;
