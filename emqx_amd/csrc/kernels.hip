@@ -435,7 +435,6 @@ constexpr int HIST_OFF = 8;   // hist = stats + HIST_OFF
 struct Cursor {
     uint32_t v, r, n, r0;   // node to visit next and its level; topic levels; start level
     uint32_t pend;          // TM_PEND_MASK: bit k = path(k) holds a '+' child still to visit (k < r)
-    uint32_t pp, ppc;       // TM_SPLIT_PROBE: v's edge probe is the next step's load; v's pending '+' child
     uint64_t key;           // KEYS: fold branches taken above level r (rank_sym), key word 0
     uint32_t pf_id;         // TM_PF1: node whose half is in pf (NODE_NONE: none)
     uint4 pf;
@@ -535,7 +534,6 @@ __device__ __forceinline__ bool walk_begin(const ImageView& im, Cursor& c, uint3
     c.n = n;
     c.key = 0;
     c.pend = 0;
-    c.pp = 0;
     c.pf_id = NODE_NONE;
     if (!dollar) {
         c.v = ROOT;
@@ -587,42 +585,11 @@ __device__ __forceinline__ bool walk_pop(Cursor& c, Path path, uint32_t r, uint6
     return true;
 }
 
-// TM_SPLIT_PROBE: a WIDE node whose Bloom admits the word defers its edge
-// probe to the next step, so no step chains two dependent global loads (the
-// wave waits for its slowest lane: one lane's probe after its node load
-// stretched the whole step)
-#ifndef TM_SPLIT_PROBE
-#define TM_SPLIT_PROBE 0
-#endif
-
 template <bool STATS, bool KEYS, class Path, class Words, class Emit>
 __device__ __forceinline__ bool walk_step(const ImageView& im, Cursor& c, Path path, const Words& W, Emit& emit,
                                           WalkStats& st) {
     uint32_t v = c.v, r = c.r;
     uint64_t key = KEYS ? c.key : 0ull;
-    if (TM_SPLIT_PROBE && !STATS && !SLOT_RECORD && c.pp) {   // resume v's visit: its probe is this step's load
-        c.pp = 0;
-        Hit g = probe_edge<false>(im, v, W(r), st.probe_loads);
-        if (g.child != NODE_NONE && !sum_useful(g.plus & SUM_ALL, c.n - r - 1)) g.child = NODE_NONE;
-        const uint32_t pc = c.ppc;
-        if (g.child != NODE_NONE) {
-            path(r) = KEYS ? (pc | SYM_LIT) : pc;
-            if (Path::kMask) c.pend = pc != NODE_NONE ? (c.pend | (1u << r)) : (c.pend & ~(1u << r));
-            c.v = g.child;
-            c.r = r + 1;
-            if (KEYS) c.key = key | rank_sym(r, 1);
-            return false;
-        }
-        if (pc != NODE_NONE) {
-            path(r) = KEYS ? (NODE_NONE | SYM_PLUS) : NODE_NONE;
-            if (Path::kMask) c.pend &= ~(1u << r);
-            c.v = pc;
-            c.r = r + 1;
-            if (KEYS) c.key = key | rank_sym(r, 2);
-            return false;
-        }
-        return walk_pop<STATS, KEYS>(c, path, r, key, st);
-    }
     bool leaf = r == c.n;
     uint4 h;
     if (TM_PF1 && !STATS) {
@@ -662,17 +629,6 @@ __device__ __forceinline__ bool walk_step(const ImageView& im, Cursor& c, Path p
             const uint32_t k = c.n - r - 1;
             plus_ok = sum_useful(hf & SUM_ALL, k);
             lit_ok = w < WORD_MAX ? sum_useful((hf >> 15) & SUM_ALL, k) : w == WORD_PLUS ? plus_ok : true;
-        }
-        if (TM_SPLIT_PROBE && !STATS && !SLOT_RECORD && lit_ok && w < WORD_MAX && (plus & WIDE)) {
-            const uint64_t b = word_bloom(w);
-            if (((((uint64_t)lc << 32) | lw) & b) == b) {   // probe at the next step
-                c.pp = 1;
-                c.ppc = plus_ok ? (plus & NODE_MASK) : NODE_NONE;
-                c.v = v;
-                c.r = r;
-                return false;
-            }
-            lit_ok = false;   // the Bloom rejects the word: no literal child
         }
         Hit g = (!STATS && !lit_ok) ? Hit{NODE_NONE, 0, 0, 0, 0, 0, false}
                                     : lit_child<STATS>(im, v, plus, lw, lc, w, st.probe_loads);
