@@ -326,3 +326,62 @@ class ShardSet:
             c.close()
         for e in self.engines:
             e.close()
+
+
+# ---------------------------------------------------------------------------
+# Topic routing by first words (design step for a scaling sharded mode; host
+# logic, checked against O1 on the CPU: tests/test_shard_routing.py).
+#
+# Today every shard walks every topic.  Instead, route topic T to the shard
+# of its first `depth` levels, and place filter F on the shard of its first
+# `depth` levels when those are all literal, on EVERY shard otherwise (a '+'
+# or '#' among them, which can match topics of any route).  A filter with
+# literal first levels can only match topics that start with the same words
+# (or, shorter than `depth`, exactly its own levels), so the owner shard holds
+# every filter that can match T, and its walk alone yields emqx_trie:match/1's
+# complete list in order: the order of two matching filters is a property of
+# the filters (image.h filter_shape), not of the rest of the trie.  No merge,
+# only a topic exchange; the price is the replicated wildcard-led filters.
+
+def _route_key(levels, depth):
+    return b"/".join(levels[:depth])
+
+
+def _route_hash(key: bytes, n_shards: int) -> int:
+    h = 0xCBF29CE484222325
+    for c in key:
+        h = ((h ^ c) * 0x100000001B3) & 0xFFFFFFFFFFFFFFFF
+    h ^= h >> 33
+    h = (h * 0xFF51AFD7ED558CCD) & 0xFFFFFFFFFFFFFFFF
+    h ^= h >> 33
+    return h % n_shards
+
+
+def filter_route(filt: bytes, n_shards: int, depth: int = 2) -> int:
+    """shard of an (inner, emqx_topic:parse/1-stripped) filter, or -1 = every shard"""
+    levels = filt.split(b"/")
+    if any(w in (b"+", b"#") for w in levels[:depth]):
+        return -1
+    return _route_hash(_route_key(levels, depth), n_shards)
+
+
+def topic_route(topic: bytes, n_shards: int, depth: int = 2) -> int:
+    """the shard that owns a publish topic's walk"""
+    return _route_hash(_route_key(topic.split(b"/"), depth), n_shards)
+
+
+def routed_partition(filters, topics, n_shards: int, depth: int = 2):
+    """per-shard filter lists (replicated ones on every shard), topic owners
+    and the balance figures: replication factor (filters held over filters),
+    topic skew (busiest shard's topics over the mean)"""
+    per = [[] for _ in range(n_shards)]
+    for f in filters:
+        s = filter_route(f, n_shards, depth)
+        for d in (range(n_shards) if s < 0 else (s,)):
+            per[d].append(f)
+    owner = [topic_route(t, n_shards, depth) for t in topics]
+    counts = np.bincount(np.asarray(owner, dtype=np.int64), minlength=n_shards)
+    stats = {"replication": sum(len(p) for p in per) / max(len(filters), 1),
+             "topic_skew": float(counts.max() / max(counts.mean(), 1e-9)),
+             "max_shard_filters": max(len(p) for p in per) / max(len(filters), 1)}
+    return per, owner, stats
