@@ -274,3 +274,33 @@ def test_rccl_one_rank_exchange_equals_o1(gpu_device):
     assert np.array_equal(og[: int(wo[-1])].cpu().numpy().view(np.uint32), wi)
     comm.close()
     e.close()
+
+
+@pytest.mark.parametrize("S,depth", [(4, 2), (8, 1)])
+def test_routed_shards_on_device_equal_o1(gpu_device, S, depth):
+    """topic routing by first words (shard.py routed_partition): each shard
+    engine holds its literal-led filters plus every wildcard-led one and
+    walks only the topics it owns; its device lists equal O1 over the whole
+    filter set, filter for filter and in order"""
+    from emqx_amd import shard
+    from emqx_amd import workload as W
+    from emqx_amd.engine import Engine
+    from oracle import O1
+    fb, fo = W.filters(1)
+    tb, to = W.topics(1, n=20000)
+    filters = [bytes(x) for x in W.unpack(fb, fo)]
+    topics = [bytes(x) for x in W.unpack(tb, to)]
+    full = O1()
+    full.insert_many(fb, fo)
+    per, owner, _ = shard.routed_partition(filters, topics, S, depth)
+    for s in range(S):
+        mine = [t for t, o in zip(topics, owner) if o == s]
+        if not mine:
+            continue
+        e = Engine(device=gpu_device)
+        for f in per[s]:
+            e.insert(f)
+        got = e.match(mine)
+        for t, g in zip(mine, got):
+            assert list(g) == full.match(t), (s, t)
+        e.close()
