@@ -38,6 +38,7 @@ def main():
     a = ap.parse_args()
     import torch
     dev = torch.device("cuda", 0)
+    st = torch.cuda.Stream(device=dev)   # explicit: handle 0 would select the engine's own stream
     cfg = W.CONFIGS[a.config]
     n_topics = a.topics or cfg["topics"]
     t0 = time.time()
@@ -62,19 +63,18 @@ def main():
         c = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
         o = torch.empty(n + 1, dtype=torch.int64, device=dev)
         tot = torch.zeros(1, dtype=torch.int64, device=dev)
-        e.match_batch_device(d_b, d_o, n, int(qo[-1]), c, o, None, 0, tot)   # sizing pass
+        e.match_batch_device(d_b, d_o, n, int(qo[-1]), c, o, None, 0, tot, stream=st)   # sizing pass
         torch.cuda.synchronize(dev)
         cap = int(tot.item()) + 1024
         ids = torch.empty(cap, dtype=torch.int32, device=dev)
-        e.match_batch_device(d_b, d_o, n, int(qo[-1]), c, o, ids, cap, tot)   # warm-up
+        e.match_batch_device(d_b, d_o, n, int(qo[-1]), c, o, ids, cap, tot, stream=st)   # warm-up
         torch.cuda.synchronize(dev)
         ts = []
         for _ in range(a.reps):
             ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            ev0.record()
-            e.match_batch_device(d_b, d_o, n, int(qo[-1]), c, o, ids, cap, tot,
-                                 stream=torch.cuda.current_stream(dev))
-            ev1.record()
+            ev0.record(st)
+            e.match_batch_device(d_b, d_o, n, int(qo[-1]), c, o, ids, cap, tot, stream=st)
+            ev1.record(st)
             torch.cuda.synchronize(dev)
             ts.append(ev0.elapsed_time(ev1))
         ms = float(np.median(ts))
