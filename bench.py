@@ -6,14 +6,16 @@ through the whole hot path of emqx_trie:match/1: device tokenizer
 
 Workload: 10M distinct wildcard filters (8 levels max,
 p+ 0.20, p# 0.05, Zipf(1.0) words over 16/64/256/1024/4096x4), replicated on
-every GPU.  Weak scaling (default): every rank walks its own batch of 8M
-8-level topics per step (rank r's topic stream r; rank 0's batches are the
-N = 1 batches), since topics are independent units and the replicated path
-has no data-path collective; `--scaling strong` splits one 8M-topic batch
-1/2/4/8 ways over the ranks instead.  Steps rotate over `--batches`
-distinct batches (no batch is replayed back to back, so L2 / MALL never hold
-the previous step's topics).  No collective on the data path.  `value` =
-topics matched per second over all ranks (max-over-ranks step time).
+every GPU.  Strong scaling (default; SURVEY §8(d) C3, BASELINE configs[2]
+"publish batches sharded across 2/4/8 MI355X"): one 8M-topic batch per step
+split 1/2/4/8 ways over the ranks (rank r walks slice r).  The weak-scaling
+figure (every rank walks its own 1M-topic batch per step, SURVEY's "also
+1M/GPU") is reported beside it under "weak"; `--scaling weak` makes it the
+headline.  Steps rotate over `--batches` distinct batches (no batch is
+replayed back to back, so L2 / MALL never hold the previous step's topics).
+No collective on the data path.  `value` = topics matched per second over
+all ranks (max-over-ranks step time).  Every rank checks its own lists
+against the oracle; `parity_check` is the AND over ranks.
 
 Extra legs at N = 1 (not `value`): the CPU baseline (O1 = C restatement of
 emqx_trie, on all host threads and on one; O3 = the same algorithm over
@@ -61,11 +63,16 @@ def parse():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", type=int, default=3, help="SURVEY §8(d) config (3 = the metric's)")
     ap.add_argument("--filters", type=int, default=None, help="override filter count")
-    ap.add_argument("--scaling", choices=["strong", "weak"], default="weak",
-                    help="weak (default): a batch of --topics per rank per step; "
-                         "strong: one batch per step split over the ranks")
+    ap.add_argument("--scaling", choices=["strong", "weak"], default="strong",
+                    help="strong (default, SURVEY §8(d) C3 / BASELINE configs[2]): one batch per step split over "
+                         "the ranks; weak: a batch of --topics per rank per step")
     ap.add_argument("--topics", type=int, default=None,
-                    help="topics per batch (strong, default the config's: 8M at C3) or per GPU (weak, default 1M)")
+                    help="topics per batch (strong, default the config's: 8M at C3) or per GPU (weak, default "
+                         "--weak-topics)")
+    ap.add_argument("--weak-topics", type=int, default=1_000_000,
+                    help="topics per GPU of the weak-scaling figure reported beside the strong one (0 = skip)")
+    ap.add_argument("--check-rank", type=int, default=2_000,
+                    help="topics of each batch every rank > 0 checks bit-exactly vs O3")
     ap.add_argument("--batches", type=int, default=2, help="distinct batches the steps rotate over")
     ap.add_argument("--mode", choices=["replicated", "sharded"], default=None,
                     help="replicated trie per GPU (default) or filter shards per GPU (default for --config 4)")
@@ -204,43 +211,53 @@ def cpu_baseline(a, fb, fo, n_filters, tb, to):
     return res
 
 
-def o3_check(a, fb, fo, n_filters, batches, results):
-    """filter sets too large for O1's string-path tables (C4: 100M filters):
-    the check runs against O3, the same algorithm over interned ids"""
+def check_lists(oracle, a, k, batches, results):
+    """the first k topics of each batch: device counts, offsets and ids
+    equal the oracle's, id for id"""
+    ok = True
+    for (tb, to), (dc, doo, di) in zip(batches, results):
+        kk = min(k, len(to) - 1)
+        oc, oo, oi = oracle.match_ids(tb, to[: kk + 1], threads=host_threads(a))
+        ok = ok and bool(np.array_equal(dc[:kk], oc) and np.array_equal(doo[: kk + 1], oo) and
+                         np.array_equal(di[: int(oo[-1])], oi))
+    return ok
+
+
+def o3_check(a, fb, fo, n_filters, batches, results, k=None, extra=None):
+    """filter sets too large for O1's string-path tables (C4: 100M filters),
+    and the ranks > 0 of a multi-GPU run: the check runs against O3, the
+    same algorithm over interned ids"""
     from oracle import O3   # checker only
+    k = a.check if k is None else k
     t0 = time.time()
     o3 = O3(n_filters)
     o3.insert_many(fb, fo)
     log("oracle O3 built in %.1fs" % (time.time() - t0))
-    ok = True
-    for (tb, to), (dc, doo, di) in zip(batches, results):
-        k = min(a.check, len(to) - 1)
-        oc, oo, oi = o3.match_ids(tb, to[: k + 1], threads=host_threads(a))
-        ok = ok and bool(np.array_equal(dc[:k], oc) and np.array_equal(doo[: k + 1], oo) and
-                         np.array_equal(di[: int(oo[-1])], oi))
-    log("bit-exact check of %d topics of each of %d batches vs O3: %s" % (min(a.check, len(batches[0][1]) - 1),
-                                                                          len(batches), ok))
+    ok = check_lists(o3, a, k, batches, results)
+    if extra:
+        ok = ok and check_lists(o3, a, k, *extra)
+    log("bit-exact check of %d topics of each of %d batches vs O3: %s" % (min(k, len(batches[0][1]) - 1),
+                                                                          len(batches) + (len(extra[0]) if extra
+                                                                                          else 0), ok))
     o3.close()
     return ok
 
 
-def o1_check_and_baseline(a, fb, fo, n_filters, batches, results, do_cpu):
+def o1_check_and_baseline(a, fb, fo, n_filters, batches, results, do_cpu, extra=None):
     from oracle import O1   # checker / CPU baseline only
     if n_filters > 20_000_000:
-        return o3_check(a, fb, fo, n_filters, batches, results), {}
+        return o3_check(a, fb, fo, n_filters, batches, results, extra=extra), {}
     t0 = time.time()
     o1 = O1(n_filters)
     o1.insert_many(fb, fo)
     log("oracle O1 built in %.1fs (%d nodes)" % (time.time() - t0, o1.node_count))
     threads = host_threads(a)
-    ok = True
-    for (tb, to), (dc, doo, di) in zip(batches, results):
-        k = min(a.check, len(to) - 1)
-        oc, oo, oi = o1.match_ids(tb, to[: k + 1], threads=threads)
-        ok = ok and bool(np.array_equal(dc[:k], oc) and np.array_equal(doo[: k + 1], oo) and
-                         np.array_equal(di[: int(oo[-1])], oi))
+    ok = check_lists(o1, a, a.check, batches, results)
+    if extra:
+        ok = ok and check_lists(o1, a, a.check, *extra)
     log("bit-exact check of %d topics of each of %d batches vs O1: %s" % (min(a.check, len(batches[0][1]) - 1),
-                                                                          len(batches), ok))
+                                                                          len(batches) + (len(extra[0]) if extra
+                                                                                          else 0), ok))
     legs = {}
     if do_cpu:
         tb, to = batches[0]
@@ -254,6 +271,30 @@ def o1_check_and_baseline(a, fb, fo, n_filters, batches, results, do_cpu):
             log("cpu %s: %.0f topics/s (%d topics, %d threads)" % (name, legs[name]["value"], k, th))
     o1.close()
     return ok, legs
+
+
+def effective_cores(hc):
+    """the CPUs' worth of time the CPU legs can use: the cgroup quota when one
+    is set (the GPU box: 256 CPUs in the affinity mask, 16 CPUs of cpu.max),
+    else the affinity count"""
+    q = hc.get("cgroup_cpu_max_cpus")
+    return max(1, int(round(q))) if q else hc["affinity_cpus"]
+
+
+def cpu_line(a, legs, n_filters):
+    th = host_threads(a)
+    hc = host_cpus()
+    return {"value": legs["o1_all"]["value"], "unit": "topics/s", "cores": effective_cores(hc), "kind": "port",
+            "sample": "%d topics of the bench batch against the same %d-filter trie: O1, the C "
+                      "restatement of emqx_trie (string-path node ids, ETS-like {trie_edge, NodeId, "
+                      "Word} tables), %d pthreads over %d CPUs of the affinity mask sharing %s CPUs of cgroup "
+                      "time, 1 warm-up then the median of 5 runs of %d topics"
+                      % (legs["o1_all"]["topics"], n_filters, th, hc["affinity_cpus"],
+                         hc["cgroup_cpu_max_cpus"] if hc["cgroup_cpu_max_cpus"] else "all",
+                         legs["o1_all"]["topics"] // 5),
+            "cores_source": "cgroup cpu.max quota" if hc["cgroup_cpu_max_cpus"] else "affinity mask",
+            "affinity_cpus": hc["affinity_cpus"], "threads_used": th,
+            "cpu_model": cpu_model(), "nproc": os.cpu_count(), "host_cpus": hc, "legs": legs}
 
 
 # The one JSON line goes to the process's original stdout; everything else
@@ -301,7 +342,8 @@ def main():
             dist.destroy_process_group()
         return
     cfg = W.CONFIGS[a.config]
-    a.topics = a.topics or cfg["topics"]   # per step: the whole batch (strong) or each rank's (weak)
+    # per step: the whole batch (strong) or each rank's (weak)
+    a.topics = a.topics or (cfg["topics"] if a.scaling == "strong" else a.weak_topics)
     n_filters = a.filters or cfg["filters"]
     t0 = time.time()
     fb, fo = W.filters(a.config, n=n_filters)
@@ -321,118 +363,75 @@ def main():
     eng.commit()
     log("rank %d: trie built + committed in %.1fs: %d filters, %d nodes, image %.2f GB" % (
         rank, time.time() - t0, eng.filter_count, eng.node_count, eng.image_bytes / 1e9))
+    eng.set_option("slots", min(4, max(2, a.streams)))
 
+    # the headline region: strong = this rank's slice of each global batch,
+    # weak = this rank's own batches (--scaling weak)
     t0 = time.time()
     batches = make_batches(a, cfg, rank, world)
     log("rank %d: %d batches of %d topics generated in %.1fs" % (rank, len(batches), len(batches[0][1]) - 1,
                                                                  time.time() - t0))
-    st = torch.cuda.Stream(device=dev)   # explicit (handle 0 would select the engine's own stream)
-    dbat = []
-    for tb, to in batches:
-        n = len(to) - 1
-        d_b = torch.from_numpy(tb).to(dev)
-        d_o = torch.from_numpy(to.view(np.int64)).to(dev)
-        dbat.append((d_b, d_o, n, int(to[-1])))
-    # size the outputs from one counting pass per batch (untimed), exact stats of batch 0
-    totals = []
-    for i, (d_b, d_o, n, nb) in enumerate(dbat):
-        c = torch.empty(n, dtype=torch.int32, device=dev)
-        oo = torch.empty(n + 1, dtype=torch.int64, device=dev)
-        t = torch.zeros(1, dtype=torch.int64, device=dev)
-        eng.set_stats(i == 0)
-        if i == 0 and a.hist:
-            eng.set_option("hist", 1)
-        eng.match_batch_device(d_b, d_o, n, nb, c, oo, None, 0, t, stream=st)
-        torch.cuda.synchronize(dev)
-        if i == 0:
-            stats = eng.last_stats()
-            fan = np.sort(c.cpu().numpy().view(np.uint32))
-            if a.hist:   # the stats batch's slot, before the next batch takes another
-                h = (ctypes.c_uint64 * 56)()
-                eng.lib.tm_debug_hist(eng.h, h, 56)
-                for k, name in enumerate(["visits", "probe_loads", "failed_probes"]):
-                    log("per-level %s per topic: %s" % (name, [round(h[16 * k + l] / n, 2) for l in range(16)]))
-                eng.set_option("hist", 0)
-        totals.append(int(t.item()))
-    eng.set_stats(False)
-    fanout = {"mean": float(fan.mean()), "p50": int(fan[len(fan) // 2]), "p90": int(fan[int(len(fan) * 0.9)]),
-              "p99": int(fan[int(len(fan) * 0.99)]), "max": int(fan[-1])}
+    reg = Region(eng, dev, batches, a.streams, stats=True, hist=a.hist)
+    stats, fanout = reg.stats, reg.fanout
     log("fan-out per topic: %s" % fanout)
-    cap = max(totals) + 1024
-    # consecutive steps alternate over a.streams streams (each with its own
-    # output buffers: a batch's tokenizer / copy-out overlap its neighbours'
-    # walks; the engine rotates its per-batch workspace slots likewise) and
-    # rotate over the distinct batches
-    nmax = max(x[2] for x in dbat)
-    lanes = []
-    for k in range(a.streams):
-        s_ = st if k == 0 else torch.cuda.Stream(device=dev)
-        lanes.append((s_, torch.empty(nmax, dtype=torch.int32, device=dev),
-                      torch.empty(nmax + 1, dtype=torch.int64, device=dev),
-                      torch.empty(cap, dtype=torch.int32, device=dev), torch.zeros(1, dtype=torch.int64, device=dev)))
-    eng.set_option("slots", min(4, max(2, a.streams)))
-    k_step = [0]
-    last = {}
-
-    def step():
-        j = k_step[0]
-        k_step[0] += 1
-        s_, c_, oo_, i_, t_ = lanes[j % len(lanes)]
-        bi = j % len(dbat)
-        d_b, d_o, n, nb = dbat[bi]
-        eng.match_batch_device(d_b, d_o, n, nb, c_, oo_, i_, cap, t_, stream=s_)
-        last[j % len(lanes)] = bi   # a lane's outputs hold its latest batch
-
-    for _ in range(a.warmup):
-        step()
-    torch.cuda.synchronize(dev)
-
+    reg.warm(a.warmup)
     # ---- timed region: K steps; barrier + sync on both sides, max over ranks
-    dt = multi.timed_region(step, a.steps, lambda: torch.cuda.synchronize(dev))
-    for li, bi in last.items():   # every lane's last result is complete and exact
-        assert int(lanes[li][4].item()) == totals[bi], "match total changed between steps"
-    # per-kernel durations for the roofline: with batches overlapping, a
-    # kernel's event interval also holds its neighbours' work, so the kernels
-    # are timed over a.roof_steps extra serial steps of batch 0 on one stream
-    d_b, d_o, n0, nb0 = dbat[0]
-    s0, c0, oo0, i0, t0_ = lanes[0]
-    torch.cuda.synchronize(dev)
-    eng.set_timing(True)
-    for _ in range(a.roof_steps):
-        eng.match_batch_device(d_b, d_o, n0, nb0, c0, oo0, i0, cap, t0_, stream=s0)
-    torch.cuda.synchronize(dev)
-    kms = eng.last_kernel_times()
-    eng.set_timing(False)
-    # every batch's full result (the bit-exact check reads them back)
-    results = []
-    for bi, (d_b, d_o, n, nb) in enumerate(dbat):
-        eng.match_batch_device(d_b, d_o, n, nb, c0, oo0, i0, cap, t0_, stream=s0)
-        torch.cuda.synchronize(dev)
-        results.append((c0[:n].cpu().numpy().view(np.uint32).copy(), oo0[: n + 1].cpu().numpy().view(np.uint64).copy(),
-                        i0[: totals[bi]].cpu().numpy().view(np.uint32).copy()))
+    dt = reg.timed(a.steps)
+    kms = reg.kernel_times(a.roof_steps)
+    results = reg.results()
+    n0 = reg.dbat[0][2]
+
+    # the other scaling figure beside it (not `value`): weak scaling at
+    # SURVEY §8(d)'s 1M topics per GPU when the headline is strong
+    weak = None
+    wres, wbatches = None, None
+    if a.scaling == "strong" and a.weak_topics > 0:
+        wbatches = [W.topics(a.config, n=a.weak_topics, stream=multi.topic_stream(rank) * 64 + b)
+                    for b in range(a.batches)]
+        wreg = Region(eng, dev, wbatches, a.streams)
+        wreg.warm(a.warmup)
+        wdt = wreg.timed(a.steps)
+        wres = wreg.results()
+        weak = {"value": a.weak_topics * world * a.steps / wdt, "unit": "topics/s", "topics_per_gpu": a.weak_topics,
+                "ms_per_step": wdt / a.steps * 1e3, "steps": a.steps,
+                "scaling": "weak: each rank walks its own %d-topic batch per step" % a.weak_topics}
+        log("weak scaling (%d topics per GPU): %.0f topics/s, %.3f ms per step" % (a.weak_topics, weak["value"],
+                                                                                  weak["ms_per_step"]))
+        wreg.free()
+    reg.free()
 
     extras = {}
     if world == 1 and not a.no_extras:
-        extras = host_legs(a, eng, batches[0], totals[0])
+        extras = host_legs(a, eng, batches[0], reg.totals[0])
 
-    check_ok, cpu = None, None
-    if rank == 0 and (a.check > 0 or (world == 1 and a.cpu_sample > 0)):
-        check_ok, legs = o1_check_and_baseline(a, fb, fo, n_filters, batches, results, world == 1 and a.cpu_sample > 0)
-        if legs:
-            legs.update(cpu_baseline(a, fb, fo, n_filters, *batches[0]))
-            th = host_threads(a)
-            cpu = {"value": legs["o1_all"]["value"], "unit": "topics/s", "cores": th, "kind": "port",
-                   "sample": "%d topics of the bench batch against the same %d-filter trie: O1, the C "
-                             "restatement of emqx_trie (string-path node ids, ETS-like {trie_edge, NodeId, "
-                             "Word} tables), %d pthreads, 1 warm-up then the median of 5 runs of %d topics"
-                             % (legs["o1_all"]["topics"], n_filters, th, legs["o1_all"]["topics"] // 5),
-                   "cpu_model": cpu_model(), "nproc": os.cpu_count(), "threads_used": th,
-                   "host_cpus": host_cpus(), "legs": legs}
+    # parity on EVERY rank: rank 0 against O1 (a.check topics of each batch;
+    # at N = 1 also the CPU baseline), every other rank against O3 (the same
+    # algorithm over interned ids, a.check_rank topics); the line's
+    # parity_check is the AND over ranks
+    check_ok, cpu, check_desc = None, None, None
+    do_cpu = world == 1 and a.cpu_sample > 0
+    if a.check > 0 or do_cpu:
+        if rank == 0:
+            check_ok, legs = o1_check_and_baseline(a, fb, fo, n_filters, batches, results, do_cpu,
+                                                   extra=(wbatches, wres) if wres else None)
+            if legs:
+                legs.update(cpu_baseline(a, fb, fo, n_filters, *batches[0]))
+                cpu = cpu_line(a, legs, n_filters)
+        else:
+            check_ok = o3_check(a, fb, fo, n_filters, batches, results, k=a.check_rank,
+                                extra=(wbatches, wres) if wres else None)
+        if world > 1:
+            check_ok = multi.all_true(check_ok)
+        check_desc = ("rank 0: first %d topics of each batch vs O1%s; ranks 1..%d: first %d topics of each "
+                      "batch vs O3; AND over ranks" % (a.check, " (O3 past 20M filters)" if n_filters > 20_000_000
+                                                       else "", world - 1, a.check_rank)) if world > 1 else \
+            "first %d topics of each batch vs O1%s" % (a.check, " (O3 past 20M filters)"
+                                                        if n_filters > 20_000_000 else "")
+        if wres:
+            check_desc += ", the weak-scaling batches likewise"
 
     if rank == 0:
-        topics_per_step = sum(x[2] for x in dbat) / len(dbat) * (world if a.scaling == "weak" else 1)
-        if a.scaling == "strong":
-            topics_per_step = a.topics
+        topics_per_step = a.topics if a.scaling == "strong" else n0 * world
         topics_per_s = topics_per_step * a.steps / dt
         levels = stats["levels"]
         B = 8 * levels + 16 * stats["edge_reads"] + 4 * stats["matches"]   # SURVEY §8(d), per launch of batch 0
@@ -495,12 +494,124 @@ def main():
             "filter_hits_per_s": stats["matches"] / n0 * topics_per_s,
             "fanout": fanout,
             "parity_check": check_ok,
+            "parity_scope": check_desc,
         }
+        if weak:
+            out["weak"] = weak
         out.update(extras)
         emit(out)
     eng.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+class Region:
+    """HBM-resident topic batches stepped over `streams` lanes: consecutive
+    steps alternate over the lanes (each with its own output buffers, so a
+    batch's tokenizer / copy-out overlap its neighbours' walks; the engine
+    rotates its per-batch workspace slots likewise) and rotate over the
+    distinct batches.  Outputs are sized by one untimed counting pass per
+    batch (exact stats of batch 0 when `stats`)."""
+
+    def __init__(self, eng, dev, batches, streams, stats=False, hist=False):
+        self.eng, self.dev = eng, dev
+        self.st = torch.cuda.Stream(device=dev)   # explicit (handle 0 would select the engine's own stream)
+        self.dbat = []
+        for tb, to in batches:
+            n = len(to) - 1
+            self.dbat.append((torch.from_numpy(tb).to(dev), torch.from_numpy(to.view(np.int64)).to(dev), n,
+                              int(to[-1])))
+        self.totals = []
+        self.stats = None
+        for i, (d_b, d_o, n, nb) in enumerate(self.dbat):
+            c = torch.empty(n, dtype=torch.int32, device=dev)
+            oo = torch.empty(n + 1, dtype=torch.int64, device=dev)
+            t = torch.zeros(1, dtype=torch.int64, device=dev)
+            eng.set_stats(stats and i == 0)
+            if stats and i == 0 and hist:
+                eng.set_option("hist", 1)
+            eng.match_batch_device(d_b, d_o, n, nb, c, oo, None, 0, t, stream=self.st)
+            torch.cuda.synchronize(dev)
+            if stats and i == 0:
+                self.stats = eng.last_stats()
+                fan = np.sort(c.cpu().numpy().view(np.uint32))
+                self.fanout = {"mean": float(fan.mean()), "p50": int(fan[len(fan) // 2]),
+                               "p90": int(fan[int(len(fan) * 0.9)]), "p99": int(fan[int(len(fan) * 0.99)]),
+                               "max": int(fan[-1])}
+                if hist:   # the stats batch's slot, before the next batch takes another
+                    h = (ctypes.c_uint64 * 56)()
+                    eng.lib.tm_debug_hist(eng.h, h, 56)
+                    for k, name in enumerate(["visits", "probe_loads", "failed_probes"]):
+                        log("per-level %s per topic: %s" % (name, [round(h[16 * k + lv] / n, 2) for lv in range(16)]))
+                    eng.set_option("hist", 0)
+            self.totals.append(int(t.item()))
+        eng.set_stats(False)
+        self.cap = max(self.totals) + 1024
+        nmax = max(x[2] for x in self.dbat)
+        self.lanes = []
+        for k in range(streams):
+            s_ = self.st if k == 0 else torch.cuda.Stream(device=dev)
+            self.lanes.append((s_, torch.empty(nmax, dtype=torch.int32, device=dev),
+                               torch.empty(nmax + 1, dtype=torch.int64, device=dev),
+                               torch.empty(self.cap, dtype=torch.int32, device=dev),
+                               torch.zeros(1, dtype=torch.int64, device=dev)))
+        self.k = 0
+        self.last = {}
+
+    def step(self):
+        j = self.k
+        self.k += 1
+        s_, c_, oo_, i_, t_ = self.lanes[j % len(self.lanes)]
+        bi = j % len(self.dbat)
+        d_b, d_o, n, nb = self.dbat[bi]
+        self.eng.match_batch_device(d_b, d_o, n, nb, c_, oo_, i_, self.cap, t_, stream=s_)
+        self.last[j % len(self.lanes)] = bi   # a lane's outputs hold its latest batch
+
+    def sync(self):
+        torch.cuda.synchronize(self.dev)
+
+    def warm(self, steps):
+        for _ in range(steps):
+            self.step()
+        self.sync()
+
+    def timed(self, steps):
+        """K steps bracketed by barrier + device sync on both sides; max over ranks"""
+        dt = multi.timed_region(self.step, steps, self.sync)
+        for li, bi in self.last.items():   # every lane's last result is complete and exact
+            assert int(self.lanes[li][4].item()) == self.totals[bi], "match total changed between steps"
+        return dt
+
+    def kernel_times(self, steps):
+        """per-kernel durations for the roofline: with batches overlapping, a
+        kernel's event interval also holds its neighbours' work, so the
+        kernels are timed over `steps` extra serial steps of batch 0 on one
+        stream"""
+        d_b, d_o, n0, nb0 = self.dbat[0]
+        s0, c0, oo0, i0, t0_ = self.lanes[0]
+        self.sync()
+        self.eng.set_timing(True)
+        for _ in range(steps):
+            self.eng.match_batch_device(d_b, d_o, n0, nb0, c0, oo0, i0, self.cap, t0_, stream=s0)
+        self.sync()
+        kms = self.eng.last_kernel_times()
+        self.eng.set_timing(False)
+        return kms
+
+    def results(self):
+        """every batch's full result (host arrays: counts, offsets, ids)"""
+        s0, c0, oo0, i0, t0_ = self.lanes[0]
+        out = []
+        for bi, (d_b, d_o, n, nb) in enumerate(self.dbat):
+            self.eng.match_batch_device(d_b, d_o, n, nb, c0, oo0, i0, self.cap, t0_, stream=s0)
+            self.sync()
+            out.append((c0[:n].cpu().numpy().view(np.uint32).copy(), oo0[: n + 1].cpu().numpy().view(np.uint64).copy(),
+                        i0[: self.totals[bi]].cpu().numpy().view(np.uint32).copy()))
+        return out
+
+    def free(self):
+        self.dbat, self.lanes = [], []
+        torch.cuda.empty_cache()
 
 
 def host_legs(a, eng, batch, total):

@@ -231,7 +231,11 @@ static ERL_NIF_TERM nif_lookup(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv
          * :72): the argument binary, with no second engine call that a
          * concurrent delete could race */
         ERL_NIF_TERM topic = info.filter_id == TM_NO_FILTER ? atom(env, "undefined") : argv[1];
-        res = enif_make_list1(env, enif_make_tuple2(env, enif_make_uint(env, info.edge_count), topic));
+        /* #trie_node{node_id, edge_count, topic, flags} (include/emqx.hrl:95-100):
+         * the record as its tuple, flags never set by emqx_trie (undefined) */
+        res = enif_make_list1(env, enif_make_tuple5(env, atom(env, "trie_node"), argv[1],
+                                                    enif_make_uint(env, info.edge_count), topic,
+                                                    atom(env, "undefined")));
     }
     return res;
 }

@@ -89,19 +89,25 @@ struct tm_comm {
 };
 
 namespace {
+// abort the communicators of this thread's RCCL group (their peers can no
+// longer complete the group's operations)
+void abort_group(tm_comm* c, const std::string& what) {
+    for (tm_comm* g : t_group_comms)
+        if (g && g->nccl && !g->aborted) {
+            (void)ncclCommAbort(g->nccl);
+            g->nccl = nullptr;
+            g->aborted = true;
+            if (g != c) g->last_error = "aborted with its RCCL group: " + what;
+        }
+    t_group_comms.clear();
+}
+
 int fail(tm_comm* c, const std::string& what, int code) {
     if (c) c->last_error = what;
     if (t_group_depth > 0) {
         t_group_depth = 0;
         (void)ncclGroupEnd();
-        for (tm_comm* g : t_group_comms)
-            if (g && g->nccl && !g->aborted) {
-                (void)ncclCommAbort(g->nccl);
-                g->nccl = nullptr;
-                g->aborted = true;
-                if (g != c) g->last_error = "aborted with its RCCL group: " + what;
-            }
-        t_group_comms.clear();
+        abort_group(c, what);
     }
     return code;
 }
@@ -122,11 +128,19 @@ int fail(tm_comm* c, const std::string& what, int code) {
         ++t_group_depth;                       \
         t_group_comms = (comms);               \
     } while (0)
-#define XGROUP_END(c)                          \
-    do {                                       \
-        t_group_depth = 0;                     \
-        t_group_comms.clear();                 \
-        XNCCL(c, ncclGroupEnd());              \
+// ncclGroupEnd first, with the group state still set: when it fails, fail()
+// aborts the group's communicators (the group is already closed, so fail()
+// must not end it again: t_group_depth is cleared before the call)
+#define XGROUP_END(c)                                                                    \
+    do {                                                                                 \
+        const ncclResult_t _g = ncclGroupEnd();                                          \
+        if (_g != ncclSuccess) {                                                         \
+            t_group_depth = 0;                                                           \
+            abort_group(c, std::string("ncclGroupEnd: ") + ncclGetErrorString(_g));     \
+            return fail(c, std::string("ncclGroupEnd: ") + ncclGetErrorString(_g));     \
+        }                                                                                \
+        t_group_depth = 0;                                                               \
+        t_group_comms.clear();                                                           \
     } while (0)
 
 hipStream_t stream_of(tm_comm* c, const tm_exchange_in& in) {
@@ -314,6 +328,10 @@ int tm_shard_exchange_group(tm_comm** comms, uint32_t S, const tm_exchange_in* i
         if (!comms[r] || comms[r]->nranks != S || comms[r]->rank != r || !valid_in(ins[r]) || ins[r].n != ins[0].n ||
             ins[r].key_words != ins[0].key_words)
             return TM_EINVAL;
+    // a group whose communicators were aborted stays failed: it must not fall
+    // back to device copies (comm->nccl is null after an abort)
+    for (uint32_t r = 0; r < S; ++r)
+        if (comms[r]->aborted) return fail(comms[r], "communicator aborted after a failed RCCL group");
     const uint32_t n = ins[0].n;
     const bool rccl = comms[0]->nccl != nullptr;
     for (uint32_t r = 0; r < S; ++r) {   // sizes of every rank's sends, on the host

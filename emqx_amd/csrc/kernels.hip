@@ -1077,13 +1077,15 @@ __global__ void __launch_bounds__(BLOCK)
 tm_walk_wave(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const uint32_t* __restrict__ twords,
              const uint32_t* __restrict__ words, const uint32_t* __restrict__ meta, uint32_t* __restrict__ gpath,
              uint32_t* __restrict__ stage, uint32_t K, uint32_t* __restrict__ counts,
-             uint32_t* __restrict__ spill_head) {
+             uint32_t* __restrict__ spill_head, unsigned long long* __restrict__ ws) {
     __shared__ WaveLds lds_all[BLOCK / 64];
     const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     WaveLds& L = lds_all[wv];
+    uint32_t maxl = 0;   // most levels of the wave's topics (QWS_MAXL: key width check of keyed batches)
     for (uint32_t t = blockIdx.x * (BLOCK / 64) + wv; t < n; t += gridDim.x * (BLOCK / 64)) {
         const uint32_t mt = meta[t];
         const uint32_t nl = mt & MN;
+        maxl = nl > maxl ? nl : maxl;   // uniform: one topic per wave
         const bool dollar = (mt & MDOLLAR) != 0;
         const uint32_t* row = twords + (uint64_t)t * WREG;
         uint32_t* srow = stage + (uint64_t)t * K;
@@ -1226,6 +1228,7 @@ tm_walk_wave(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const u
         }
         wave_sync_lds();
     }
+    if (lane == 0 && maxl && ws) atomicMax(ws + QWS_MAXL, (unsigned long long)maxl);
 }
 
 // tm_copy_out: per 256 topics, the block's output range is copied from the
@@ -1666,7 +1669,8 @@ hipError_t launch_queue(bool stats_mode, bool xcdq, const ImageView& im, const u
         // spill_head = NO_SPILL, so the copy-out re-walks their heads
         const uint32_t wb = div_up(n, BLOCK / 64);
         hipLaunchKernelGGL(tm_walk_wave, dim3(wb < 65535 ? wb : 65535), blk, 0, st, im, off, n, qb.twords, qb.words,
-                           qb.meta, qb.path, qb.stage, K, counts, qb.spill_chunks >= QRANGES ? qb.spill_head : nullptr);
+                           qb.meta, qb.path, qb.stage, K, counts, qb.spill_chunks >= QRANGES ? qb.spill_head : nullptr,
+                           qb.ws);
         mark(3);
         mark(4);
         err = launch_scan(counts, n, out_off, total, qb.scan_tmp, st);

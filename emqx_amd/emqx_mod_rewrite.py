@@ -83,9 +83,11 @@ class Rewrite:
 
 def _erl_replacement(val: bytes, whole: bytes) -> bytes:
     """the Replacement argument of re:replace/4 expanded for a pattern with
-    no subexpressions (OTP re docs: '&' inserts the whole match, \\N /
-    \\gN / \\g{N} subexpression N -- 0 the whole match, none other exists
-    here, so nothing -- and \\& / \\\\ a literal '&' / backslash; a
+    no subexpressions (OTP re docs: '&' inserts the whole match, \\N
+    (N starting 1-9) / \\gN / \\g{N} subexpression N -- none exists here, so
+    nothing, except \\g0 / \\g{0}: the whole match; \\0 is an escaped '0'
+    (re.erl precomp_repl takes a backslash before a byte outside 1-9 as an
+    escape) -- and \\& / \\\\ a literal '&' / backslash; a
     backslash before any other byte keeps that byte).  Parity unpinned: the
     reference holds no vector for it (tests/test_rewrite.py works cases by
     hand)."""
@@ -106,6 +108,10 @@ def _erl_replacement(val: bytes, whole: bytes) -> bytes:
                     continue
             if d == 0x67:                               # \gN
                 j = i + 2
+            elif d == 0x30:                             # \0: an escaped '0' (precomp_repl: X < $1 ; X > $9)
+                out.append(d)
+                i += 2
+                continue
             k = j
             while k < n and 0x30 <= val[k] <= 0x39:
                 k += 1

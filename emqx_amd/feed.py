@@ -27,7 +27,9 @@ subscription over the snapshot ends in the committed state.
 
 Event tuples are those oracle/pytrie.py records: ("write", "emqx_trie_node",
 node_id, edge_count, topic), ("delete", "emqx_trie_node", node_id),
-("write" | "delete_object", "emqx_route", topic, dest).
+("write" | "delete_object", "emqx_route", topic, dest), and the whole-key
+delete ("delete", "emqx_route", topic, old_dests) with the Old list mnesia's
+detailed event carries.
 """
 from .emqx_router import _enc, _key
 from .engine import Engine
@@ -83,6 +85,9 @@ class TrieFeed:
                 self._add_route(topic, dest)
             elif op == "delete_object":
                 self.engine.route_delete_object(topic, _enc(dest))
+            elif op == "delete":   # the whole key: every old object (erl:97-99); dest = the Old list
+                for d in dest:
+                    self.engine.route_delete_object(topic, _enc(d))
             else:
                 return
         else:

@@ -2,6 +2,7 @@
 %% reference's names, arities and return shapes:
 %%
 %%   match/1           = emqx_trie:match/1           (src/emqx_trie.erl:77-79)
+%%   lookup/1          = emqx_trie:lookup/1          (src/emqx_trie.erl:83-84)
 %%   match_routes/1    = emqx_router:match_routes/1  (src/emqx_router.erl:116-118)
 %%   match_deliveries/1 = emqx_broker:aggre(emqx_router:match_routes(T))
 %%                                                  (src/emqx_broker.erl:152, 194-206)
@@ -20,10 +21,11 @@
 
 -include_lib("emqx/include/emqx.hrl").
 
--export([engine/0, match/1, match_routes/1, match_deliveries/1, match_many/1]).
+-export([engine/0, match/1, lookup/1, match_routes/1, match_deliveries/1, match_many/1]).
 
 -define(TAB, emqx_trie_gpu).
 -define(TIMEOUT, 5000).
+-define(LATE, emqx_trie_gpu_late).   %% process dictionary: refs of replies that timed out
 
 engine() ->
     [{engine, E}] = ets:lookup(?TAB, engine),
@@ -32,6 +34,14 @@ engine() ->
 %% emqx_trie:match/1: [Filter] in the reference's order
 match(Topic) when is_binary(Topic) ->
     wait(emqx_trie_nif:match_async(engine(), Topic)).
+
+%% emqx_trie:lookup/1: [] | [#trie_node{}] from the engine's host mirror
+%% (edge_count and topic kept exactly as emqx_trie:insert/1, delete/1 keep them)
+lookup(NodeId) when is_binary(NodeId) ->
+    case emqx_trie_nif:lookup(engine(), NodeId) of
+        {error, _} = E -> error(E);
+        Nodes -> Nodes
+    end.
 
 %% many topics in one device batch (print_routes, tests, bulk callers)
 match_many(Topics) when is_list(Topics) ->
@@ -53,9 +63,43 @@ match_deliveries(Topic) when is_binary(Topic) ->
 wait({error, _} = E) ->
     error(E);
 wait(Ref) when is_reference(Ref) ->
+    flush_late(),
     receive
         {Ref, {error, _} = E} -> error(E);
         {Ref, Result} -> Result
     after ?TIMEOUT ->
+        %% the batcher still answers this Ref later: drop the reply if it
+        %% came in the meantime, else remember the Ref so that the caller's
+        %% next wait/1 drops it (OTP 21 has no aliases to cancel a reply)
+        receive
+            {Ref, _} -> ok
+        after 0 ->
+            put(?LATE, [Ref | late()])
+        end,
         error({emqx_trie_gpu, timeout})
+    end.
+
+late() ->
+    case get(?LATE) of
+        undefined -> [];
+        L -> L
+    end.
+
+%% drop the late replies that have arrived; keep waiting for the others
+flush_late() ->
+    case late() of
+        [] -> ok;
+        L ->
+            case [R || R <- L, not drop(R)] of
+                [] -> erase(?LATE);
+                Rest -> put(?LATE, Rest)
+            end,
+            ok
+    end.
+
+drop(Ref) ->
+    receive
+        {Ref, _} -> true
+    after 0 ->
+        false
     end.

@@ -24,7 +24,8 @@ open(_Devices) -> erlang:nif_error(nif_not_loaded).
 %% emqx_trie:insert/1, delete/1 (src/emqx_trie.erl:62-73, 88-96)
 insert(_Engine, _Filter) -> erlang:nif_error(nif_not_loaded).
 delete(_Engine, _Filter) -> erlang:nif_error(nif_not_loaded).
-%% emqx_trie:lookup/1 (src/emqx_trie.erl:83-84): [] | [{EdgeCount, Topic | undefined}]
+%% emqx_trie:lookup/1 (src/emqx_trie.erl:83-84): [] | [#trie_node{}], i.e.
+%% [{trie_node, NodeId, EdgeCount, Topic | undefined, undefined}] (include/emqx.hrl:95-100)
 lookup(_Engine, _NodeId) -> erlang:nif_error(nif_not_loaded).
 commit(_Engine) -> erlang:nif_error(nif_not_loaded).
 %% emqx_trie:match/1 (src/emqx_trie.erl:77-79), synchronous on a dirty IO scheduler

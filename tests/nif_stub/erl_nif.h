@@ -38,6 +38,7 @@ int enif_make_existing_atom(ErlNifEnv*, const char*, ERL_NIF_TERM*, ErlNifCharEn
 ERL_NIF_TERM enif_make_atom(ErlNifEnv*, const char*);
 ERL_NIF_TERM enif_make_atom_len(ErlNifEnv*, const char*, size_t);
 ERL_NIF_TERM enif_make_tuple2(ErlNifEnv*, ERL_NIF_TERM, ERL_NIF_TERM);
+ERL_NIF_TERM enif_make_tuple5(ErlNifEnv*, ERL_NIF_TERM, ERL_NIF_TERM, ERL_NIF_TERM, ERL_NIF_TERM, ERL_NIF_TERM);
 ERL_NIF_TERM enif_make_badarg(ErlNifEnv*);
 ErlNifResourceType* enif_open_resource_type(ErlNifEnv*, const char*, const char*, ErlNifResourceDtor*,
                                             ErlNifResourceFlags, ErlNifResourceFlags*);

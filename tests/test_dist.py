@@ -5,10 +5,12 @@ import os
 import socket
 import sys
 
-import numpy as np
+import numpy as np  # noqa: F401
 import torch.multiprocessing as mp
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from emqx_amd import workload as W  # noqa: E402
 
 
 def _free_port():
@@ -34,7 +36,16 @@ def _worker(rank, world, port, q):
     delay = 0.02 * (rank + 1)
     dt = multi.timed_region(lambda: time.sleep(delay), 3, lambda: None)
     tb, to = W.topics(1, n=500, stream=multi.topic_stream(r))
-    q.put((rank, r, w, dt, tb[:int(to[-1])].tobytes()))
+    # parity_check is the AND over ranks: one failing rank fails the line
+    and_all = multi.all_true(True)
+    and_one = multi.all_true(rank == 0)
+    # strong scaling (bench.py's default): rank r walks slice r of the batch
+    import argparse
+    sys.path.insert(0, ROOT)
+    import bench
+    a = argparse.Namespace(batches=2, scaling="strong", topics=1001, config=1, presort=None)
+    sl = [(tb_.tobytes()[:int(to_[-1])], to_.tolist()) for tb_, to_ in bench.make_batches(a, None, r, w)]
+    q.put((rank, r, w, dt, tb[:int(to[-1])].tobytes(), and_all, and_one, sl))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -50,8 +61,17 @@ def test_two_rank_timed_region_and_streams():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    (r0, rr0, w0, dt0, b0), (r1, rr1, w1, dt1, b1) = res
+    (r0, rr0, w0, dt0, b0, aa0, ao0, sl0), (r1, rr1, w1, dt1, b1, aa1, ao1, sl1) = res
     assert (rr0, rr1, w0, w1) == (0, 1, 2, 2)
+    assert aa0 and aa1 and not ao0 and not ao1   # AND over ranks
+    # the two ranks' strong slices are the whole batch, in order
+    for b in range(2):
+        tb, to = W.topics(1, n=1001, stream=b)
+        whole = [bytes(tb[int(to[i]):int(to[i + 1])]) for i in range(1001)]
+        got = []
+        for bb, oo in (sl0[b], sl1[b]):
+            got += [bb[oo[i]:oo[i + 1]] for i in range(len(oo) - 1)]
+        assert got == whole and len(sl0[b][1]) - 1 == 500
     assert abs(dt0 - dt1) < 1e-9            # both ranks report the same max
     assert dt0 >= 3 * 0.04                  # the slower rank's time
     assert b0 != b1                         # independent topic streams

@@ -194,6 +194,24 @@ def test_route_table_events_never_touch_the_trie():
     eng.close()
 
 
+def test_whole_key_route_delete_event():
+    """mnesia:delete({emqx_route, T}) (not issued by emqx_router, but a
+    table operation the feed must follow: erlang/emqx_trie_gpu_feed.erl:97-99)
+    arrives as ("delete", "emqx_route", T, Old): every old object goes, the
+    trie keeps the filter, other topics' routes stay"""
+    eng = Engine(device=-1)
+    feed = TrieFeed(eng)
+    for e in [("write", "emqx_trie_node", b"a/+", 0, b"a/+"), ("write", "emqx_route", b"a/+", b"n1"),
+              ("write", "emqx_route", b"a/+", (b"g1", b"n2")), ("write", "emqx_route", b"b/#", b"n1"),
+              ("delete", "emqx_route", b"a/+", [b"n1", (b"g1", b"n2")])]:
+        feed.handle(e)
+    feed.commit()
+    assert eng.get_routes(b"a/+") == [] and eng.lookup(b"a/+") == [(0, b"a/+")]
+    assert [eng.dest_bytes(d) for d in eng.get_routes(b"b/#")] == [_enc(b"n1")]
+    assert eng.route_count == 1
+    eng.close()
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("seed", [1, 2, 3])
 def test_gpu_replay_match_and_match_routes_node_down(gpu_device, seed):

@@ -116,6 +116,37 @@ def test_sharded_shape_keys_with_wave_walk_equal_o1(gpu_device):
     assert got == _o1(filters, topics)
 
 
+@pytest.mark.parametrize("wave", [0, 1])
+def test_key_levels_reported_by_every_walk(gpu_device, wave):
+    """tm_key_levels after a shaped batch of <= 31-level key width that holds
+    a 40-level topic: both the per-lane walk and the wave-per-topic walk
+    (small batches) report its 40 levels, so the caller's key-width guard
+    (ShardSet.match_batch) fires instead of merging with truncated keys"""
+    import torch
+    from emqx_amd import shard
+    from emqx_amd.engine import pack
+    dev = torch.device("cuda", 0)
+    long_t = b"/".join(b"l%d" % i for i in range(40))
+    filters = [b"l0/#", b"+/l1/#", b"#", long_t, b"a/+"]
+    topics = [b"a/b", long_t, b"x/y/z"] * 20
+    fb, fo = pack(filters)
+    tb, to = pack(topics)
+    n = len(topics)
+    e = shard.ShardEngine(0, 1, 0, filters_hint=len(filters))
+    e.set_option("wave_walk_max", (1 << 30) if wave else 0)
+    e.insert_many(fb, fo)
+    d_b = torch.from_numpy(tb).to(dev)
+    d_o = torch.from_numpy(to.view(np.int64)).to(dev)
+    c = torch.empty(n, dtype=torch.int32, device=dev)
+    o = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    tot = torch.zeros(1, dtype=torch.int64, device=dev)
+    e.match_keys_device(d_b, d_o, n, int(to[-1]), c, o, None, None, 0, tot, key_words=1)
+    torch.cuda.synchronize()
+    assert e.key_levels() == 40
+    assert shard.key_words_for(tb, to) == 2   # what ShardSet would have chosen
+    e.close()
+
+
 @pytest.mark.parametrize("shape", [0, 1])
 def test_sharded_walk_keys_and_shape_keys_equal_o1(gpu_device, shape):
     """both ways to key a shard's lists: the keyed walk (rank_sym) and the

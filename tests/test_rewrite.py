@@ -42,6 +42,11 @@ def test_match_regx_replacement_metacharacters():
     assert match_regx(b"a/b&c/d", mp, b"x/$1/$2") == b"x/b$1c/d"
     # \1: subexpression 1 of the pattern "\$1", which has none: nothing
     assert match_regx(b"a/b\\1c/d", mp, b"x/$1/$2") == b"x/bc/d"
+    # \0 is an escaped '0' (re.erl precomp_repl: a backslash before a byte
+    # outside 1-9); \g0 and \g{0} are the whole match
+    assert match_regx(b"a/b\\0c/d", mp, b"x/$1/$2") == b"x/b0c/d"
+    assert match_regx(b"a/b\\g0c/d", mp, b"x/$1/$2") == b"x/b$1c/d"
+    assert match_regx(b"a/b\\g{0}c/d", mp, b"x/$1/$2") == b"x/b$1c/d"
     # \& and \\ are the literal characters
     assert match_regx(b"a/b\\&c/d\\\\e", mp, b"$2+$1") == b"d\\e+b&c"
     # "$1" also matches inside "$10" (the fold runs I = 1 first)
