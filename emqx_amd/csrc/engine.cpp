@@ -1631,6 +1631,10 @@ struct tm_engine {
         for (FilterRec& f : filters)
             if (f.node != NODE_NONE) f.node = newid[f.node];
         for (uint32_t v = 0; v < nodes.size(); ++v) nodes[v].hash_filter = hf_value(v);
+        if (SLOT_RECORD)   // the slots carry their children's records: those of the final hash_filter values
+            for (EdgeTable* t : {&cold, &hot})
+                for (EdgeSlot& e : t->slots)
+                    if (e.parent != EDGE_EMPTY) e = slot_for(e.parent, e.word, e.child);
         free_nodes.clear();
         created_since_layout = 0;
         force_relayout = false;
@@ -3153,6 +3157,62 @@ extern "C" int tm_debug_hist(tm_engine* e, uint64_t* out, int n) {
         const DevBuf& ws = e->devs[0]->slots[e->devs[0]->last_slot].stats;
         if (!ws.p) return TM_EINVAL;
         HIPCHK(hipMemcpy(out, ws.as<uint64_t>() + 8, (size_t)n * 8, hipMemcpyDeviceToHost));
+        return TM_OK;
+    });
+}
+
+// diagnostics (not part of include/topicmatch.h): the host mirror of the
+// trie image as the last commit laid it out, for the walk simulator
+// (tools/sim/walksim.cpp): node records, edge tables, per-node parent and
+// word; pointers stay valid until the next delta or commit
+struct tm_debug_image_view {
+    const void* nodes;       // Node[n_nodes], 32 B each (image.h)
+    uint64_t n_nodes;
+    const void* cold;        // EdgeSlot[cold_slots]
+    uint64_t cold_slots;
+    const void* hot;         // EdgeSlot[hot_slots]
+    uint64_t hot_slots;
+    uint32_t hot_limit;
+    uint32_t aux_stride;     // bytes per aux record
+    const void* aux;         // per node: {parent u32, word u32, edge_count u32, lit_count u32, ...}
+};
+extern "C" int tm_debug_image(tm_engine* e, tm_debug_image_view* out) {
+    if (!e || !out) return TM_EINVAL;
+    return guarded(e, [&]() -> int {
+        out->nodes = e->nodes.data();
+        out->n_nodes = e->nodes.size();
+        out->cold = e->cold.slots.data();
+        out->cold_slots = e->cold.slots.size();
+        out->hot = e->hot.slots.data();
+        out->hot_slots = e->hot.slots.size();
+        out->hot_limit = e->hot_limit;
+        out->aux_stride = (uint32_t)sizeof(NodeAux);
+        out->aux = e->aux.data();
+        return TM_OK;
+    });
+}
+// diagnostics: the word ids of n topics as the device tokenizer makes them
+// (WORD_NONE for bytes no filter contains, WORD_PLUS / WORD_HASH for the
+// atoms), levels[t] per topic, ids packed in topic order (cap ids at most)
+extern "C" int tm_debug_words(tm_engine* e, const uint8_t* bytes, const uint64_t* off, uint32_t n, uint32_t* levels,
+                              uint32_t* ids, uint64_t cap) {
+    if (!e || (n && (!bytes || !off || !levels || !ids))) return TM_EINVAL;
+    return guarded(e, [&]() -> int {
+        uint64_t k = 0;
+        for (uint32_t t = 0; t < n; ++t) {
+            const uint8_t* p = bytes + off[t];
+            const uint32_t len = (uint32_t)(off[t + 1] - off[t]);
+            uint32_t s = 0, lv = 0;
+            for (uint32_t i = 0; i <= len; ++i) {
+                if (i == len || p[i] == '/') {
+                    if (k >= cap) return TM_ENOSPC;
+                    ids[k++] = e->word_id(p + s, i - s, false);
+                    ++lv;
+                    s = i + 1;
+                }
+            }
+            levels[t] = lv;
+        }
         return TM_OK;
     });
 }

@@ -142,6 +142,11 @@ def test_key_levels_reported_by_every_walk(gpu_device, wave):
     tot = torch.zeros(1, dtype=torch.int64, device=dev)
     e.match_keys_device(d_b, d_o, n, int(to[-1]), c, o, None, None, 0, tot, key_words=1)
     torch.cuda.synchronize()
+    cap = int(tot.item()) + 16
+    ids = torch.empty(cap, dtype=torch.int32, device=dev)
+    keys = torch.empty(cap, dtype=torch.int64, device=dev)
+    e.match_keys_device(d_b, d_o, n, int(to[-1]), c, o, ids, keys, cap, tot, key_words=1)   # the keyed batch
+    torch.cuda.synchronize()
     assert e.key_levels() == 40
     assert shard.key_words_for(tb, to) == 2   # what ShardSet would have chosen
     e.close()

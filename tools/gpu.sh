@@ -11,6 +11,8 @@
 #   traffic   per-launch walk traffic from those passes  -> profiles/traffic_c3.json (read by bench)
 #   cmd       an arbitrary python command in $CMD         -> cmd.log
 #   latency   open-loop batcher latency sweep             -> latency.jsonl
+#   slices    rocprofv3 stats of one-GPU batches of $SLICES topics (the per-rank slices of strong scaling)
+#   rehearse  the driver's N > 1 launch with $NPROC ranks sharing GPU 0 (control plane over gloo)
 # e.g. gpurun -- 'STEPS="tests bench prof" TAG=r02_head bash tools/gpu.sh'
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
@@ -35,6 +37,15 @@ for s in ${STEPS:-tests}; do
              python3 bench.py --config 4 --steps 10 --warmup 2 --cpu-sample 0 --check 0 --streams 1 --no-extras \
              > "$OUT/prof4_bench.json" 2> "$OUT/prof4_bench.log" ;;
     traffic) python3 tools/traffic.py "$OUT/pmc" ${TRAFFIC_OUT:-profiles/traffic_c3.json} > "$OUT/traffic.json" ;;
+    slices) for T in ${SLICES:-1000000 2000000 4000000 8000000}; do
+             timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/slice_$T" -o run -- \
+               python3 bench.py --topics $T --steps 40 --warmup 5 --cpu-sample 0 --check 2000 --weak-topics 0 \
+               --no-extras ${BENCH_ARGS} > "$OUT/slice_$T.json" 2> "$OUT/slice_$T.log" || exit $?
+           done ;;
+    rehearse) TM_BENCH_SHARE_GPU=1 timeout -k 10 600 python3 -m torch.distributed.run --nnodes=1 \
+               --nproc-per-node ${NPROC:-2} --master-addr 127.0.0.1 --master-port ${PORT:-29533} bench.py \
+               --gpus ${NPROC:-2} --steps 20 --warmup 3 --no-extras ${BENCH_ARGS} \
+               > "$OUT/rehearse_${NPROC:-2}.json" 2> "$OUT/rehearse_${NPROC:-2}.log" ;;
     cmd)   timeout -k 10 ${T_CMD:-600} python -u -c "$CMD" > "$OUT/cmd.log" 2>&1 ;;
     latency) timeout -k 10 ${T_LAT:-400} python -u tools/bench_batcher_latency.py ${LAT_ARGS} \
              >> "$OUT/latency.jsonl" 2>> "$OUT/latency.log" ;;
