@@ -46,13 +46,16 @@ $(BUILD)/exchange.o: emqx_amd/csrc/exchange.cpp emqx_amd/csrc/kernels.h include/
 $(BUILD)/batcher.o: emqx_amd/csrc/batcher.cpp include/topicmatch.h | $(BUILD)
 	$(HIPCC) -O2 -fPIC -std=c++17 -Wall -pthread -c $< -o $@
 
+$(BUILD)/route.o: emqx_amd/csrc/route.hip emqx_amd/csrc/kernels.h emqx_amd/csrc/image.h | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
 $(BUILD)/acl.o: emqx_amd/csrc/acl.hip include/topicmatch.h | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(BUILD)/rewrite.o: emqx_amd/csrc/rewrite.hip include/topicmatch.h | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(LIBOUT): $(BUILD)/kernels.o $(BUILD)/shard.o $(BUILD)/routes.o $(BUILD)/presort.o $(BUILD)/aggre.o $(BUILD)/engine.o $(BUILD)/batcher.o $(BUILD)/acl.o $(BUILD)/rewrite.o $(BUILD)/exchange.o
+$(LIBOUT): $(BUILD)/kernels.o $(BUILD)/shard.o $(BUILD)/route.o $(BUILD)/routes.o $(BUILD)/presort.o $(BUILD)/aggre.o $(BUILD)/engine.o $(BUILD)/batcher.o $(BUILD)/acl.o $(BUILD)/rewrite.o $(BUILD)/exchange.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -pthread $^ -L/opt/rocm/lib -lrccl -o $@
 
 emqx_amd/libtmwork.so: emqx_amd/csrc/workload.c

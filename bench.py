@@ -74,8 +74,12 @@ def parse():
     ap.add_argument("--check-rank", type=int, default=2_000,
                     help="topics of each batch every rank > 0 checks bit-exactly vs O3")
     ap.add_argument("--batches", type=int, default=2, help="distinct batches the steps rotate over")
-    ap.add_argument("--mode", choices=["replicated", "sharded"], default=None,
-                    help="replicated trie per GPU (default) or filter shards per GPU (default for --config 4)")
+    ap.add_argument("--mode", choices=["replicated", "sharded", "routed"], default=None,
+                    help="replicated trie per GPU (default), filter shards per GPU with a list exchange (sharded), "
+                         "or routed shards: topics exchanged to the shard owning their first --depth levels")
+    ap.add_argument("--depth", type=int, default=2, help="routed mode: routing depth (levels of the key)")
+    ap.add_argument("--shards", type=int, default=None,
+                    help="routed mode in one process (--single-process): shards on GPU 0 (a one-GPU rehearsal)")
     ap.add_argument("--single-process", action="store_true",
                     help="one process drives --gpus GPUs through ONE engine (tm_open_devices)")
     ap.add_argument("--replicas", default=None,
@@ -323,6 +327,8 @@ def main():
         from emqx_amd import _lib
         _lib.LIB_PATH = os.path.abspath(a.lib)
     rank, world, local = multi.env_rank()
+    if a.single_process and a.mode == "routed":
+        return main_routed_single(a)
     if a.single_process:
         return main_single_process(a)
     # TM_BENCH_SHARE_GPU=1 (rehearsal on a one-GPU box): every rank on GPU 0,
@@ -338,6 +344,11 @@ def main():
     # filters (252M nodes) included; --mode sharded for filter sets beyond it
     if (a.mode or "replicated") == "sharded":
         main_sharded(a, rank, world, local, dev)
+        if world > 1:
+            dist.destroy_process_group()
+        return
+    if a.mode == "routed":
+        main_routed(a, rank, world, local, dev)
         if world > 1:
             dist.destroy_process_group()
         return
@@ -727,6 +738,307 @@ def main_single_process(a):
                                  "parallelism": "one process, tm_open_devices x %d" % N},
                       "replicas_consistent": True})
     eng.close()
+
+
+def routed_line(a, cfg, n_filters, S, topics_per_step, dt, kms, stats, n0, eng_info, check_ok, phases, transport):
+    levels = stats["levels"]
+    B = 8 * levels + 16 * stats["edge_reads"] + 4 * stats["matches"]   # rank 0's owned batch, one launch
+    walk_ms = kms.get("walk", 0.0)
+    achieved = B / (walk_ms * 1e-3) / 1e9 if walk_ms > 0 else None
+    return {
+        "metric": METRIC, "value": topics_per_step * a.steps / dt, "unit": "topics/s", "n_gpus": S,
+        "steps": a.steps, "warmup": a.warmup, "ms_per_step": dt / a.steps * 1e3, "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+        "config": {"workload": "C%d: %d distinct wildcard filters routed over %d shard(s) by their first %d levels "
+                               "(wildcard-led ones on every shard), %d-level topics, one %d-topic batch per step "
+                               "split over the ranks; each topic walked on its owner shard only" % (
+                                   a.config, n_filters, S, a.depth, cfg["levels"], topics_per_step),
+                   "filters": n_filters, "topics_per_step": topics_per_step, "levels": cfg["levels"],
+                   "depth": a.depth,
+                   "parallelism": "routed shards x %d: topic all-to-all to the owner (%s), walk, lists back" % (
+                       S, transport)},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": None,
+                     "kernel": "tm_walk_queue on rank 0's owned topics", "kernel_ms": walk_ms,
+                     "algorithmic_bytes_per_launch": B, "topics_per_launch": n0},
+        "cpu_baseline": None, "kernel_ms": kms, "phases_ms_rank0": phases, "shard0": eng_info,
+        "parity_check": check_ok,
+    }
+
+
+def routed_check(a, fb, fo, n_filters, batches, results, rank):
+    """every rank: its own batches' lists (returned to it, in its topic
+    order) against O1 over the WHOLE filter set (O3 past 20M filters)"""
+    from oracle import O1, O3   # checker only
+    o = (O1 if n_filters <= 20_000_000 else O3)(n_filters)
+    o.insert_many(fb, fo)
+    k = a.check if rank == 0 else a.check_rank
+    ok = check_lists(o, a, k, batches, results)
+    o.close()
+    log("rank %d: bit-exact check of %d topics of each batch vs %s over all filters: %s" % (
+        rank, k, "O1" if n_filters <= 20_000_000 else "O3", ok))
+    return ok
+
+
+def main_routed(a, rank, world, local, dev):
+    """Routed sharded mode, one process per GPU (RCCL): each rank holds the
+    filters routed to it plus the wildcard-led ones (global ids), walks only
+    the topics it owns, and returns their lists to the ranks that sent them."""
+    from emqx_amd import shard
+    S = world
+    cfg = W.CONFIGS[a.config]
+    n_filters = a.filters or cfg["filters"]
+    a.topics = a.topics or cfg["topics"]
+    fb, fo = W.filters(a.config, n=n_filters)
+    t0 = time.time()
+    eng = shard.RoutedEngine(local, S, rank, depth=a.depth, filters_hint=n_filters)
+    eng.insert_many(fb, fo)
+    eng.commit()
+    info = {"filters": eng.filter_count, "nodes": eng.node_count, "image_gb": eng.image_bytes / 1e9,
+            "filter_share": eng.filter_count / n_filters}
+    log("rank %d: routed shard built in %.1fs: %s" % (rank, time.time() - t0, info))
+    uid = [shard.Comm.unique_id() if rank == 0 else None]
+    if world > 1:
+        dist.broadcast_object_list(uid, src=0)
+    comm = shard.Comm.init_rank(uid[0], S, rank, local)
+    batches = make_batches(a, cfg, rank, world)   # strong: slice `rank` of each global batch
+    st = torch.cuda.Stream(device=dev)
+    dbat = []
+    for tb, to in batches:
+        pad = np.zeros(len(tb) + 16, dtype=np.uint8)
+        pad[:len(tb)] = tb
+        dbat.append((torch.from_numpy(pad).to(dev), torch.from_numpy(to.view(np.int64)).to(dev), len(to) - 1,
+                     int(to[-1])))
+    caps, mmax = [], 1
+    for d_b, d_o, n, nb in dbat:   # sizes of the owned batches' lists (untimed)
+        o = shard.route_exchange(comm, shard.route_in(n, nb, d_b, d_o, a.depth, st))
+        c = torch.empty(max(o.m, 1), dtype=torch.int32, device=dev)
+        oo = torch.empty(o.m + 1, dtype=torch.int64, device=dev)
+        t = torch.zeros(1, dtype=torch.int64, device=dev)
+        eng.match_batch_device(o.d_bytes, o.d_off, o.m, o.bytes, c, oo, None, 0, t, stream=st)
+        torch.cuda.synchronize(dev)
+        caps.append(int(t.item()) + 1024)
+        mmax = max(mmax, o.m)
+    cap = max(caps)
+    d_c = torch.empty(mmax + 1, dtype=torch.int32, device=dev)
+    d_oo = torch.empty(mmax + 2, dtype=torch.int64, device=dev)
+    d_i = torch.empty(cap, dtype=torch.int32, device=dev)
+    d_t = torch.zeros(1, dtype=torch.int64, device=dev)
+    k_step = [0]
+    last = {}
+
+    def exchange(bi):
+        d_b, d_o, n, nb = dbat[bi]
+        return shard.route_exchange(comm, shard.route_in(n, nb, d_b, d_o, a.depth, st))
+
+    def walk(o):
+        eng.match_batch_device(o.d_bytes, o.d_off, o.m, o.bytes, d_c, d_oo, d_i, cap, d_t, stream=st)
+
+    def back():
+        return shard.route_return(comm, d_c, d_oo, d_i, stream=st)
+
+    def step():
+        bi = k_step[0] % len(dbat)
+        k_step[0] += 1
+        o = exchange(bi)
+        walk(o)
+        last["res"] = back()
+        last["bi"] = bi
+
+    for _ in range(max(a.warmup, 1)):
+        step()
+    torch.cuda.synchronize(dev)
+    dt = multi.timed_region(step, a.steps, lambda: torch.cuda.synchronize(dev))
+    # stats and kernel times of rank 0's owned batch 0 (serial, untimed)
+    o = exchange(0)
+    eng.set_stats(True)
+    walk(o)
+    torch.cuda.synchronize(dev)
+    stats = eng.last_stats()
+    eng.set_stats(False)
+    n0 = o.m
+    eng.set_timing(True)
+    for _ in range(a.roof_steps):
+        walk(o)
+    torch.cuda.synchronize(dev)
+    kms = eng.last_kernel_times()
+    eng.set_timing(False)
+    back()
+    torch.cuda.synchronize(dev)
+
+    def phase(fn, k=3):
+        multi.timed_region(lambda: None, 1, lambda: torch.cuda.synchronize(dev))
+        t1 = time.perf_counter()
+        for _ in range(k):
+            fn()
+        torch.cuda.synchronize(dev)
+        return (time.perf_counter() - t1) / k * 1e3
+    oo_ = exchange(0)
+    phases = {"exchange_ms": phase(lambda: exchange(0)), "walk_ms": phase(lambda: walk(oo_)),
+              "return_ms": phase(back)}
+    # every batch's lists on this rank, in its topic order
+    results = []
+    for bi in range(len(dbat)):
+        walk(exchange(bi))
+        r = back()
+        torch.cuda.synchronize(dev)
+        results.append((shard._dev_array(r.d_counts, r.n, np.uint32, local),
+                        shard._dev_array(r.d_offs, r.n + 1, np.uint64, local),
+                        shard._dev_array(r.d_ids, r.total, np.uint32, local)))
+    check_ok = None
+    if a.check > 0:
+        check_ok = routed_check(a, fb, fo, n_filters, batches, results, rank)
+        if world > 1:
+            check_ok = multi.all_true(check_ok)
+    if rank == 0:
+        emit(routed_line(a, cfg, n_filters, S, a.topics, dt, kms, stats, n0, info, check_ok, phases,
+                         "RCCL" if comm.rccl else "device copies"))
+    comm.close()
+    eng.close()
+
+
+def main_routed_single(a):
+    """Routed mode in ONE process: --shards S shard engines (on GPU 0 by
+    default, or on --replicas) exchanging by device copies / RCCL group calls
+    (tm_route_exchange_group): the launch rehearsal of the routed mode on a
+    one-GPU box.  One step = every shard's slice of the batch routed, each
+    shard's owned topics walked, the lists returned."""
+    from emqx_amd import shard
+    devs = [int(x) for x in a.replicas.split(",")] if a.replicas else [0] * (a.shards or a.gpus)
+    S = len(devs)
+    cfg = W.CONFIGS[a.config]
+    n_filters = a.filters or cfg["filters"]
+    a.topics = a.topics or cfg["topics"]
+    fb, fo = W.filters(a.config, n=n_filters)
+    t0 = time.time()
+    rs = shard.RoutedSet(devs, depth=a.depth, filters_hint=n_filters)
+    rs.insert_many(fb, fo)
+    info = [{"filters": e.filter_count, "nodes": e.node_count, "image_gb": round(e.image_bytes / 1e9, 3),
+             "filter_share": round(e.filter_count / n_filters, 4)} for e in rs.engines]
+    log("%d routed shards built in %.1fs: %s" % (S, time.time() - t0, info))
+    per_rank = [make_batches(a, cfg, r, S) for r in range(S)]   # [rank][batch]
+    batches = [[per_rank[r][b] for r in range(S)] for b in range(a.batches)]
+    # one step through RoutedSet's machinery, with HBM-resident inputs
+    import ctypes as C
+    from emqx_amd import _lib as L
+    lib = rs.comms[0].lib
+    hs = (C.c_void_p * S)(*[c.h.value for c in rs.comms])
+    streams = [torch.cuda.Stream(device=torch.device("cuda", d)) for d in devs]
+    dins = []
+    for b in range(a.batches):
+        ins = []
+        keep = []
+        for r, (tb, to) in enumerate(batches[b]):
+            dev = torch.device("cuda", devs[r])
+            pad = np.zeros(len(tb) + 16, dtype=np.uint8)
+            pad[:len(tb)] = tb
+            d_b, d_o = torch.from_numpy(pad).to(dev), torch.from_numpy(to.view(np.int64)).to(dev)
+            keep.append((d_b, d_o))
+            ins.append(shard.route_in(len(to) - 1, int(to[-1]), d_b, d_o, a.depth, streams[r]))
+        dins.append(((L.TmRouteIn * S)(*ins), keep))
+    state = {}
+
+    def exchange(b):
+        outs = (L.TmRouteOut * S)()
+        rc = lib.tm_route_exchange_group(hs, S, dins[b][0], outs)
+        if rc != L.TM_OK:
+            raise L.TopicMatchError(rc, "tm_route_exchange_group")
+        return outs
+
+    def lists_for(outs, sized=True):
+        ls = []
+        for r, e in enumerate(rs.engines):
+            o = outs[r]
+            buf = state.setdefault(r, {})
+            dev = torch.device("cuda", devs[r])
+            if buf.get("m", -1) < o.m:
+                buf["m"] = o.m + 1024
+                buf["c"] = torch.empty(buf["m"], dtype=torch.int32, device=dev)
+                buf["o"] = torch.empty(buf["m"] + 1, dtype=torch.int64, device=dev)
+                buf["t"] = torch.zeros(1, dtype=torch.int64, device=dev)
+            if not sized or "cap" not in buf:
+                e.match_batch_device(o.d_bytes, o.d_off, o.m, o.bytes, buf["c"], buf["o"], None, 0, buf["t"],
+                                     stream=streams[r])
+                streams[r].synchronize()
+                need = int(buf["t"].item()) + 1024
+                if buf.get("cap", 0) < need:
+                    buf["cap"] = need * 2
+                    buf["i"] = torch.empty(buf["cap"], dtype=torch.int32, device=dev)
+            e.match_batch_device(o.d_bytes, o.d_off, o.m, o.bytes, buf["c"], buf["o"], buf["i"], buf["cap"],
+                                 buf["t"], stream=streams[r])
+            ls.append(L.TmRouteLists(buf["c"].data_ptr(), buf["o"].data_ptr(), buf["i"].data_ptr(),
+                                     streams[r].cuda_stream))
+        return (L.TmRouteLists * S)(*ls)
+
+    def back(ls):
+        res = (L.TmRouteResult * S)()
+        rc = lib.tm_route_return_group(hs, S, ls, res)
+        if rc != L.TM_OK:
+            raise L.TopicMatchError(rc, "tm_route_return_group")
+        return res
+
+    for b in range(a.batches):   # size every shard's output for every batch (untimed)
+        back(lists_for(exchange(b), sized=False))
+    k_step = [0]
+
+    def step():
+        b = k_step[0] % a.batches
+        k_step[0] += 1
+        state["res"] = back(lists_for(exchange(b)))
+
+    def sync():
+        for d in sorted(set(devs)):
+            torch.cuda.synchronize(torch.device("cuda", d))
+    for _ in range(max(a.warmup, 1)):
+        step()
+    sync()
+    dt = multi.timed_region(step, a.steps, sync)
+    # rank 0's owned batch 0: stats and kernel times
+    outs = exchange(0)
+    ls = lists_for(outs)
+    sync()
+    e0, o0 = rs.engines[0], outs[0]
+    buf = state[0]
+    e0.set_stats(True)
+    e0.match_batch_device(o0.d_bytes, o0.d_off, o0.m, o0.bytes, buf["c"], buf["o"], buf["i"], buf["cap"], buf["t"],
+                          stream=streams[0])
+    sync()
+    stats = e0.last_stats()
+    e0.set_stats(False)
+    e0.set_timing(True)
+    for _ in range(a.roof_steps):
+        e0.match_batch_device(o0.d_bytes, o0.d_off, o0.m, o0.bytes, buf["c"], buf["o"], buf["i"], buf["cap"],
+                              buf["t"], stream=streams[0])
+    sync()
+    kms = e0.last_kernel_times()
+    e0.set_timing(False)
+    back(ls)
+    sync()
+    check_ok = True
+    for b in range(a.batches):
+        res = back(lists_for(exchange(b)))
+        sync()
+        for r in range(S):
+            x = res[r]
+            got = (shard._dev_array(x.d_counts, x.n, np.uint32, devs[r]),
+                   shard._dev_array(x.d_offs, x.n + 1, np.uint64, devs[r]),
+                   shard._dev_array(x.d_ids, x.total, np.uint32, devs[r]))
+            state.setdefault("results", {})[(r, b)] = got
+    if a.check > 0:
+        from oracle import O1, O3   # checker only
+        o = (O1 if n_filters <= 20_000_000 else O3)(n_filters)
+        o.insert_many(fb, fo)
+        for (r, b), got in state["results"].items():
+            check_ok = check_ok and check_lists(o, a, a.check_rank if r else a.check, [batches[b][r]], [got])
+        o.close()
+        log("bit-exact check of every shard's batches vs the whole filter set: %s" % check_ok)
+    line = routed_line(a, cfg, n_filters, S, a.topics, dt, kms, stats, o0.m, info[0], check_ok if a.check else None,
+                       None, "device copies" if not rs.comms[0].rccl else "RCCL group")
+    line["n_gpus"] = len(set(devs))
+    line["config"]["parallelism"] += ", one process, shards on GPUs %s" % devs
+    line["shards"] = info
+    emit(line)
+    rs.close()
 
 
 def main_sharded(a, rank, world, local, dev):

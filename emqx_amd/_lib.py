@@ -61,6 +61,27 @@ class TmExchangeOut(ctypes.Structure):
                 ("d_keys", ctypes.c_void_p)]
 
 
+class TmRouteIn(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_uint32), ("depth", ctypes.c_uint32), ("bytes", ctypes.c_uint64),
+                ("d_bytes", ctypes.c_void_p), ("d_off", ctypes.c_void_p), ("hip_stream", ctypes.c_void_p)]
+
+
+class TmRouteOut(ctypes.Structure):
+    _fields_ = [("m", ctypes.c_uint32), ("reserved", ctypes.c_uint32), ("bytes", ctypes.c_uint64),
+                ("d_bytes", ctypes.c_void_p), ("d_off", ctypes.c_void_p)]
+
+
+class TmRouteLists(ctypes.Structure):
+    _fields_ = [("d_counts", ctypes.c_void_p), ("d_offs", ctypes.c_void_p), ("d_ids", ctypes.c_void_p),
+                ("hip_stream", ctypes.c_void_p)]
+
+
+class TmRouteResult(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_uint32), ("reserved", ctypes.c_uint32), ("total", ctypes.c_uint64),
+                ("d_counts", ctypes.c_void_p), ("d_offs", ctypes.c_void_p), ("d_ids", ctypes.c_void_p)]
+
+
+TM_ROUTE_ALL = 0xFFFFFFFF
 TM_COMM_ID_BYTES = 128
 TM_BATCHER_ROUTES = 1
 TM_BATCHER_DELIVERIES = 2
@@ -138,6 +159,19 @@ SIGNATURES = [
                                          ctypes.POINTER(TmExchangeOut)]),
     ("tm_shard_exchange_group", ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint32,
                                                ctypes.POINTER(TmExchangeIn), ctypes.POINTER(TmExchangeOut)]),
+    ("tm_route_of", ctypes.c_uint32, [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                      ctypes.c_int]),
+    ("tm_insert_batch_ids", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                           ctypes.c_void_p]),
+    ("tm_insert_batch_routed", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                              ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]),
+    ("tm_route_exchange", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(TmRouteIn), ctypes.POINTER(TmRouteOut)]),
+    ("tm_route_exchange_group", ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint32,
+                                               ctypes.POINTER(TmRouteIn), ctypes.POINTER(TmRouteOut)]),
+    ("tm_route_return", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(TmRouteLists),
+                                       ctypes.POINTER(TmRouteResult)]),
+    ("tm_route_return_group", ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint32,
+                                             ctypes.POINTER(TmRouteLists), ctypes.POINTER(TmRouteResult)]),
     ("tm_route_add", ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p,
                                     ctypes.c_uint32]),
     ("tm_route_add_batch", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
@@ -256,3 +290,14 @@ def load():
         fn.argtypes = args
     _lib = lib
     return lib
+
+
+def hip_memcpy_d2h(dst, src, nbytes, device):
+    """synchronous device -> host copy of a raw device pointer (comm-owned
+    buffers of the routed exchange), through the HIP runtime the library is
+    bound to"""
+    lib = load()
+    lib.hipSetDevice.argtypes = [ctypes.c_int]
+    lib.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    if lib.hipSetDevice(device) != 0 or lib.hipMemcpy(dst, src, nbytes, 2) != 0:   # hipMemcpyDeviceToHost
+        raise TopicMatchError(TM_EDEVICE, "hipMemcpy device -> host")

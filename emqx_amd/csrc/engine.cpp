@@ -971,10 +971,25 @@ struct tm_engine {
 
     // ------------------------------------------------------------------
     // filters
+    // the id the next new filter takes (tm_insert_batch_ids), FILTER_NONE: allocate one
+    uint32_t forced_fid = FILTER_NONE;
     uint32_t new_filter(const uint8_t* p, uint32_t len, uint32_t node) {
         uint32_t id;
-        if (free_filters.empty()) release_quarantine();
-        if (!free_filters.empty()) {
+        if (forced_fid != FILTER_NONE) {   // a caller-chosen (global) id: holes below it stay unused
+            id = forced_fid;
+            if (id >= 0x7FFFFFF0u) throw RangeError("filter id past 2^31 - 16");
+            if (id >= filters.size()) filters.resize((size_t)id + 1, FilterRec{0, 0, NODE_NONE});
+            else if (filters[id].node != NODE_NONE) throw ArgError("filter id " + std::to_string(id) + " in use");
+            for (auto it = quarantine.begin(); it != quarantine.end(); ++it)   // a re-inserted id leaves quarantine
+                if (it->second == id) {
+                    quarantine.erase(it);
+                    break;
+                }
+        } else if (free_filters.empty()) {
+            release_quarantine();
+        }
+        if (forced_fid != FILTER_NONE) {
+        } else if (!free_filters.empty()) {
             id = free_filters.back();
             free_filters.pop_back();
         } else {
@@ -2582,6 +2597,63 @@ int tm_insert_batch_shard(tm_engine* e, const uint8_t* bytes, const uint64_t* of
             if (off[i + 1] < off[i] || off[i + 1] - off[i] > 0xFFFFFFFFull) throw ArgError("bad offsets");
             const uint32_t len = (uint32_t)(off[i + 1] - off[i]);
             if (tm_shard_of(bytes + off[i], len, n_shards) == shard) e->insert(bytes + off[i], len);
+        }
+        return TM_OK;
+    });
+}
+
+// routed sharded mode (topicmatch.h): the key is the first min(depth, levels)
+// levels' bytes, hashed as the device hashes words (route.hip does the same)
+uint32_t tm_route_of(const uint8_t* topic, uint32_t len, uint32_t n_shards, uint32_t depth, int is_filter) {
+    if ((!topic && len) || n_shards == 0) return 0;
+    uint32_t lev = 0, start = 0, cut = len;
+    for (uint32_t i = 0; i <= len; ++i) {
+        if (i == len || topic[i] == '/') {
+            if (lev < depth && is_filter && i - start == 1 && (topic[start] == '+' || topic[start] == '#'))
+                return TM_ROUTE_ALL;
+            if (++lev == depth) {
+                cut = i;
+                break;
+            }
+            start = i + 1;
+        }
+    }
+    if (n_shards == 1) return 0;
+    return route_shard(word_hash(topic, cut), n_shards);
+}
+
+int tm_insert_batch_ids(tm_engine* e, const uint8_t* bytes, const uint64_t* off, uint32_t n, const uint32_t* ids) {
+    if (n && (!bytes || !off || !ids)) return TM_EINVAL;
+    return guarded(e, [&] {
+        struct Reset {
+            tm_engine* e;
+            ~Reset() { e->forced_fid = FILTER_NONE; }
+        } reset{e};
+        for (uint32_t i = 0; i < n; ++i) {
+            if (off[i + 1] < off[i] || off[i + 1] - off[i] > 0xFFFFFFFFull) throw ArgError("bad offsets");
+            if (ids[i] == FILTER_NONE) throw ArgError("filter id FILTER_NONE");
+            e->forced_fid = ids[i];
+            e->insert(bytes + off[i], (uint32_t)(off[i + 1] - off[i]));
+        }
+        return TM_OK;
+    });
+}
+
+int tm_insert_batch_routed(tm_engine* e, const uint8_t* bytes, const uint64_t* off, uint32_t n, uint32_t n_shards,
+                           uint32_t shard, uint32_t depth, uint32_t gid_base) {
+    if ((n && (!bytes || !off)) || n_shards == 0 || shard >= n_shards || depth == 0) return TM_EINVAL;
+    return guarded(e, [&] {
+        struct Reset {
+            tm_engine* e;
+            ~Reset() { e->forced_fid = FILTER_NONE; }
+        } reset{e};
+        for (uint32_t i = 0; i < n; ++i) {
+            if (off[i + 1] < off[i] || off[i + 1] - off[i] > 0xFFFFFFFFull) throw ArgError("bad offsets");
+            const uint32_t len = (uint32_t)(off[i + 1] - off[i]);
+            const uint32_t r = tm_route_of(bytes + off[i], len, n_shards, depth, 1);
+            if (r != TM_ROUTE_ALL && r != shard) continue;
+            e->forced_fid = gid_base + i;
+            e->insert(bytes + off[i], len);
         }
         return TM_OK;
     });

@@ -195,6 +195,13 @@ TM_HD uint64_t filter_shape(const uint32_t* ws, uint32_t len) {
     return k;
 }
 
+// Routed sharded mode (topicmatch.h tm_route_of): the owner shard of a topic
+// (or literal-led filter) from the word hash of its routing key (the bytes
+// of its first `depth` levels), identical on host and device
+TM_HD uint32_t route_shard(uint64_t key_hash, uint32_t n_shards) {
+    return n_shards <= 1 ? 0u : (uint32_t)((key_hash >> 32) % n_shards);
+}
+
 // DictSlot::tag of a word: 24 hash bits and the length (capped at 255)
 TM_HD uint32_t dict_tag(uint64_t h, uint32_t len) {
     return (uint32_t)(h >> 40) << 8 | (len < 255u ? len : 255u);

@@ -137,4 +137,33 @@ hipError_t launch_shard_merge(uint32_t S, uint32_t m, const uint32_t* counts, co
 hipError_t launch_slice_sizes(const uint64_t* offs, uint32_t n, uint32_t S, uint64_t* out, hipStream_t st);
 hipError_t launch_source_totals(const uint32_t* counts, uint32_t m, uint32_t S, uint64_t* out, hipStream_t st);
 
+// Routed sharded mode (route.hip): each rank's batch into owner buckets.
+// owner n u8, blk_cnt / blk_base ceil(n/256) x S u32, bucket S+1 u32 (topic
+// base of each owner's bucket), perm / slen n u32, soff n+1 u64, scan_tmp
+// scan_tmp_elems(n), sbuf the batch's bytes + 8, cuts S+1 u64 (byte base of
+// each bucket).  The bucket order is stable (a source's topics keep their
+// order within each owner's bucket).
+constexpr uint32_t MAX_ROUTE_SHARDS = 64;
+struct RoutePlanBufs {
+    uint8_t* owner;
+    uint32_t* blk_cnt;
+    uint32_t* blk_base;
+    uint32_t* bucket;
+    uint32_t* perm;
+    uint32_t* slen;
+    uint64_t* soff;
+    uint64_t* scan_tmp;
+    uint8_t* sbuf;
+    uint64_t* cuts;
+};
+hipError_t launch_route_plan(const uint8_t* bytes, const uint64_t* off, uint32_t n, uint32_t depth, uint32_t S,
+                             const RoutePlanBufs& w, hipStream_t st);
+// out[k] = in[idx[k]], k < count
+hipError_t launch_gather_u64(const uint64_t* in, const uint32_t* idx, uint32_t k, uint64_t* out, hipStream_t st);
+// lists returned in bucket order (rcount n, roff CSR, rids) -> the batch's own
+// topic order: out_count[perm[p]] = rcount[p], out_off = scan, ids copied
+hipError_t launch_route_unpermute(const uint32_t* rcount, const uint64_t* roff, const uint32_t* rids,
+                                  const uint32_t* perm, uint32_t n, uint32_t* out_count, uint64_t* out_off,
+                                  uint32_t* out_ids, uint64_t* total, uint64_t* scan_tmp, hipStream_t st);
+
 }  // namespace tmx

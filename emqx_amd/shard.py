@@ -329,45 +329,30 @@ class ShardSet:
 
 
 # ---------------------------------------------------------------------------
-# Topic routing by first words (design step for a scaling sharded mode; host
-# logic, checked against O1 on the CPU: tests/test_shard_routing.py).
+# Routed sharded mode (topicmatch.h tm_route_*; exchange.cpp, route.hip).
 #
-# Today every shard walks every topic.  Instead, route topic T to the shard
-# of its first `depth` levels, and place filter F on the shard of its first
-# `depth` levels when those are all literal, on EVERY shard otherwise (a '+'
-# or '#' among them, which can match topics of any route).  A filter with
-# literal first levels can only match topics that start with the same words
-# (or, shorter than `depth`, exactly its own levels), so the owner shard holds
-# every filter that can match T, and its walk alone yields emqx_trie:match/1's
-# complete list in order: the order of two matching filters is a property of
-# the filters (image.h filter_shape), not of the rest of the trie.  No merge,
-# only a topic exchange; the price is the replicated wildcard-led filters.
-
-def _route_key(levels, depth):
-    return b"/".join(levels[:depth])
-
-
-def _route_hash(key: bytes, n_shards: int) -> int:
-    h = 0xCBF29CE484222325
-    for c in key:
-        h = ((h ^ c) * 0x100000001B3) & 0xFFFFFFFFFFFFFFFF
-    h ^= h >> 33
-    h = (h * 0xFF51AFD7ED558CCD) & 0xFFFFFFFFFFFFFFFF
-    h ^= h >> 33
-    return h % n_shards
-
+# Route topic T to the shard of its first `depth` levels, and place filter F
+# on the shard of its first `depth` levels when those are all literal, on
+# EVERY shard otherwise (a '+' or '#' among them, which can match topics of
+# any route).  A filter with literal first levels can only match topics that
+# start with the same words (or, shorter than `depth`, exactly its own
+# levels), so the owner shard holds every filter that can match T, and its
+# walk alone yields emqx_trie:match/1's complete list in order: the order of
+# two matching filters is a property of the filters (image.h filter_shape),
+# not of the rest of the trie.  No merge, only a topic exchange; filters keep
+# global ids on every shard (tm_insert_batch_routed), so the lists need no
+# id translation.  The price is the replicated wildcard-led filters.
+# tm_route_of hashes the routing key exactly as the device does (route.hip).
 
 def filter_route(filt: bytes, n_shards: int, depth: int = 2) -> int:
     """shard of an (inner, emqx_topic:parse/1-stripped) filter, or -1 = every shard"""
-    levels = filt.split(b"/")
-    if any(w in (b"+", b"#") for w in levels[:depth]):
-        return -1
-    return _route_hash(_route_key(levels, depth), n_shards)
+    r = L.load().tm_route_of(filt, len(filt), n_shards, depth, 1)
+    return -1 if r == L.TM_ROUTE_ALL else r
 
 
 def topic_route(topic: bytes, n_shards: int, depth: int = 2) -> int:
     """the shard that owns a publish topic's walk"""
-    return _route_hash(_route_key(topic.split(b"/"), depth), n_shards)
+    return L.load().tm_route_of(topic, len(topic), n_shards, depth, 0)
 
 
 def routed_partition(filters, topics, n_shards: int, depth: int = 2):
@@ -385,3 +370,140 @@ def routed_partition(filters, topics, n_shards: int, depth: int = 2):
              "topic_skew": float(counts.max() / max(counts.mean(), 1e-9)),
              "max_shard_filters": max(len(p) for p in per) / max(len(filters), 1)}
     return per, owner, stats
+
+
+class RoutedEngine(Engine):
+    """The engine of routed shard `shard` of `n_shards`: the filters routed to
+    it and the replicated ones, under their global ids."""
+
+    def __init__(self, device, n_shards, shard, depth=2, filters_hint=0):
+        if not 1 <= n_shards <= 64 or not 0 <= shard < n_shards or depth < 1:
+            raise ValueError("n_shards must be 1..64, shard < n_shards, depth >= 1")
+        super().__init__(device=device, filters_hint=filters_hint)
+        self.n_shards, self.shard, self.depth = n_shards, shard, depth
+
+    def insert_many(self, buf, off, gid_base=0):
+        """insert the filters of [off[i], off[i+1]) that live on this shard,
+        filter i under global id gid_base + i"""
+        n = len(off) - 1
+        buf = np.ascontiguousarray(buf, dtype=np.uint8)
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        return self._check(self.lib.tm_insert_batch_routed(self.h, buf.ctypes.data, off.ctypes.data, n,
+                                                           self.n_shards, self.shard, self.depth, gid_base),
+                           "tm_insert_batch_routed")
+
+
+def _sp(stream):
+    return None if stream is None else (stream if isinstance(stream, int) else stream.cuda_stream)
+
+
+def route_in(n, nbytes, d_bytes, d_off, depth, stream=None):
+    return L.TmRouteIn(n, depth, nbytes, _p(d_bytes).value, _p(d_off).value, _sp(stream))
+
+
+def route_exchange(comm, rin):
+    """this rank's topic exchange over RCCL: returns the TmRouteOut of the
+    batch it owns (comm-owned device buffers)"""
+    out = L.TmRouteOut()
+    rc = comm.lib.tm_route_exchange(comm.h, ctypes.byref(rin), ctypes.byref(out))
+    if rc != L.TM_OK:
+        raise L.TopicMatchError(rc, "tm_route_exchange: " + comm.lib.tm_comm_last_error(comm.h).decode())
+    return out
+
+
+def route_return(comm, counts, offs, ids, stream=None):
+    """the owner's lists back to their sources: returns the TmRouteResult of
+    this rank's own batch, in its topic order"""
+    lists = L.TmRouteLists(_p(counts).value, _p(offs).value, _p(ids).value, _sp(stream))
+    res = L.TmRouteResult()
+    rc = comm.lib.tm_route_return(comm.h, ctypes.byref(lists), ctypes.byref(res))
+    if rc != L.TM_OK:
+        raise L.TopicMatchError(rc, "tm_route_return: " + comm.lib.tm_comm_last_error(comm.h).decode())
+    return res
+
+
+class RoutedSet:
+    """All S routed shards of one process (one per device in `devices`,
+    repeats allowed: shards sharing a GPU exchange by device copies).
+    match_batches takes one host batch per shard (each rank's own publishes)
+    and returns each batch's lists in its own topic order, with global ids."""
+
+    def __init__(self, devices, depth=2, filters_hint=0):
+        import torch
+        self.torch = torch
+        self.devices = list(devices)
+        self.S = len(self.devices)
+        self.depth = depth
+        self.engines = [RoutedEngine(d, self.S, s, depth=depth, filters_hint=filters_hint)
+                        for s, d in enumerate(self.devices)]
+        self.comms = Comm.init_all(self.devices)
+
+    def insert_many(self, buf, off, gid_base=0):
+        for e in self.engines:
+            e.insert_many(buf, off, gid_base)
+            e.commit()
+
+    def match_batches(self, batches):
+        """batches: S host batches (tb, to); returns S (counts, offsets, gids)"""
+        torch = self.torch
+        S = self.S
+        lib = self.comms[0].lib
+        streams = [torch.cuda.Stream(device=torch.device("cuda", d)) for d in self.devices]
+        keep, ins = [], []
+        for s, (tb, to) in enumerate(batches):
+            dev = torch.device("cuda", self.devices[s])
+            pad = np.zeros(len(tb) + 16, dtype=np.uint8)
+            pad[:len(tb)] = tb
+            d_b = torch.from_numpy(pad).to(dev)
+            d_o = torch.from_numpy(np.ascontiguousarray(to).view(np.int64).copy()).to(dev)
+            keep.append((d_b, d_o))
+            ins.append(route_in(len(to) - 1, int(to[-1] - to[0]), d_b, d_o, self.depth, streams[s]))
+        hs = (ctypes.c_void_p * S)(*[c.h.value for c in self.comms])
+        outs = (L.TmRouteOut * S)()
+        rc = lib.tm_route_exchange_group(hs, S, (L.TmRouteIn * S)(*ins), outs)
+        if rc != L.TM_OK:
+            raise L.TopicMatchError(rc, "tm_route_exchange_group: " + lib.tm_comm_last_error(self.comms[0].h).decode())
+        lists = []
+        for s, e in enumerate(self.engines):
+            dev = torch.device("cuda", self.devices[s])
+            o = outs[s]
+            m = o.m
+            c = torch.empty(max(m, 1), dtype=torch.int32, device=dev)
+            oo = torch.empty(m + 1, dtype=torch.int64, device=dev)
+            t = torch.zeros(1, dtype=torch.int64, device=dev)
+            e.match_batch_device(o.d_bytes, o.d_off, m, o.bytes, c, oo, None, 0, t, stream=streams[s])
+            streams[s].synchronize()
+            cap = int(t.item()) + 1
+            ids = torch.empty(cap, dtype=torch.int32, device=dev)
+            e.match_batch_device(o.d_bytes, o.d_off, m, o.bytes, c, oo, ids, cap, t, stream=streams[s])
+            lists.append((c, oo, ids))
+        ls = (L.TmRouteLists * S)(*[L.TmRouteLists(_p(c).value, _p(oo).value, _p(ids).value, _sp(streams[s]))
+                                    for s, (c, oo, ids) in enumerate(lists)])
+        res = (L.TmRouteResult * S)()
+        rc = lib.tm_route_return_group(hs, S, ls, res)
+        if rc != L.TM_OK:
+            raise L.TopicMatchError(rc, "tm_route_return_group: " + lib.tm_comm_last_error(self.comms[0].h).decode())
+        out = []
+        for s in range(S):
+            streams[s].synchronize()
+            r = res[s]
+            n = r.n
+            out.append((_dev_array(r.d_counts, n, np.uint32, self.devices[s]),
+                        _dev_array(r.d_offs, n + 1, np.uint64, self.devices[s]),
+                        _dev_array(r.d_ids, r.total, np.uint32, self.devices[s])))
+        return out
+
+    def close(self):
+        for c in self.comms:
+            c.close()
+        for e in self.engines:
+            e.close()
+
+
+def _dev_array(ptr, n, dtype, device):
+    """copy n elements of a device buffer (a raw pointer) to the host"""
+    out = np.empty(n, dtype=dtype)
+    if n:
+        from ._lib import hip_memcpy_d2h
+        hip_memcpy_d2h(out.ctypes.data, ptr, out.nbytes, device)
+    return out

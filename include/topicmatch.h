@@ -289,6 +289,82 @@ int  tm_shard_exchange(tm_comm* c, const tm_exchange_in* in, tm_exchange_out* ou
 /* all S ranks of one process at once (comms from tm_comm_init_all) */
 int  tm_shard_exchange_group(tm_comm** comms, uint32_t S, const tm_exchange_in* ins, tm_exchange_out* outs);
 
+/* ---- routed sharded mode (SURVEY §8(e) sharded, C4: filter capacity beyond
+ * one GPU with per-topic work on ONE shard; exchange.cpp, route.hip) ---------
+ * Topic T is owned by shard tm_route_of(T's first `depth` levels); filter F
+ * lives on the shard of its first `depth` levels when those are all literal
+ * (it can match only topics that begin with them), on EVERY shard otherwise
+ * (a '+' / '#' among them).  The owner shard then holds every filter that can
+ * match T, and its walk alone yields emqx_trie:match/1's complete list in
+ * order (src/emqx_trie.erl:121-145): the relative order of two matching
+ * filters is a property of the filters, so no merge is
+ * needed, only a topic exchange.  Filters keep GLOBAL ids on every shard
+ * (tm_insert_batch_ids), so every rank's lists name filters alike.
+ *
+ * tm_route_of: the owner shard (0 .. n_shards-1) of a publish topic, or of a
+ * filter (is_filter = 1; TM_ROUTE_ALL when one of its first depth levels is
+ * '+' or '#').  The key is the bytes of the first min(depth, levels) levels,
+ * hashed exactly as the device does it. */
+#define TM_ROUTE_ALL 0xFFFFFFFFu
+uint32_t tm_route_of(const uint8_t* topic, uint32_t len, uint32_t n_shards, uint32_t depth, int is_filter);
+
+/* emqx_trie:insert/1 of n filters under caller-chosen filter ids (ids[i],
+ * unique, < 2^31 - 16): a sharded or routed engine holds its part of a global
+ * filter set under the global ids, so its walks emit them directly.  An engine
+ * filled this way must not also take tm_insert / tm_insert_batch (their ids
+ * would collide).  TM_EINVAL when ids[i] names another live filter. */
+int tm_insert_batch_ids(tm_engine* e, const uint8_t* bytes, const uint64_t* off, uint32_t n, const uint32_t* ids);
+
+/* tm_insert_batch_ids of the filters tm_route_of places on `shard` (routed to
+ * it, or to every shard), filter i of the batch under global id gid_base + i. */
+int tm_insert_batch_routed(tm_engine* e, const uint8_t* bytes, const uint64_t* off, uint32_t n, uint32_t n_shards,
+                           uint32_t shard, uint32_t depth, uint32_t gid_base);
+
+/* Topic exchange: every rank routes its own batch (HBM, stream-ordered) and
+ * sends each topic to its owner; *out receives the topics this rank owns —
+ * concatenated by source rank, in each source's order — as a batch for
+ * tm_match_batch_device (bytes + n+1 offsets, comm-owned, valid until the
+ * comm's next route call).  One host sync sizes the receives. */
+typedef struct tm_route_in {
+    uint32_t n;                 /* topics of this rank's batch                              */
+    uint32_t depth;             /* routing depth (levels of the key)                        */
+    uint64_t bytes;             /* d_off[n] - d_off[0] (sizes the sends without a device read) */
+    const uint8_t* d_bytes;     /* topic bytes (+ 8 readable bytes past the end)            */
+    const uint64_t* d_off;      /* n + 1 offsets                                            */
+    void* hip_stream;           /* NULL: the comm's stream                                  */
+} tm_route_in;
+typedef struct tm_route_out {
+    uint32_t m;                 /* topics this rank owns                                    */
+    uint32_t reserved;
+    uint64_t bytes;             /* their bytes                                              */
+    const uint8_t* d_bytes;     /* m topics back to back (+ 8 padding bytes)                */
+    const uint64_t* d_off;      /* m + 1 offsets                                            */
+} tm_route_out;
+int tm_route_exchange(tm_comm* c, const tm_route_in* in, tm_route_out* out);
+int tm_route_exchange_group(tm_comm** comms, uint32_t S, const tm_route_in* ins, tm_route_out* outs);
+
+/* The way back: the owner's lists of its m topics (CSR from
+ * tm_match_batch_device on the batch tm_route_exchange delivered) return to
+ * the ranks the topics came from; *res is each rank's own batch's lists in its
+ * original topic order (counts n, offsets n+1, ids total; comm-owned, valid
+ * until the comm's next route call). */
+typedef struct tm_route_lists {
+    const uint32_t* d_counts;   /* m                                                        */
+    const uint64_t* d_offs;     /* m + 1                                                    */
+    const uint32_t* d_ids;
+    void* hip_stream;
+} tm_route_lists;
+typedef struct tm_route_result {
+    uint32_t n;
+    uint32_t reserved;
+    uint64_t total;
+    const uint32_t* d_counts;   /* n                                                        */
+    const uint64_t* d_offs;     /* n + 1                                                    */
+    const uint32_t* d_ids;      /* total                                                    */
+} tm_route_result;
+int tm_route_return(tm_comm* c, const tm_route_lists* lists, tm_route_result* res);
+int tm_route_return_group(tm_comm** comms, uint32_t S, const tm_route_lists* lists, tm_route_result* res);
+
 /* ---- routes: the emqx_route bag and emqx_router:match_routes/1 -------------
  * A route is (topic, dest) (#route{topic, dest}, include/emqx.hrl:84-87); dest
  * is opaque bytes (the NIF passes term_to_binary(node() | {Group, node()})),

@@ -1,0 +1,81 @@
+"""Routed sharded mode on the GPU (topicmatch.h tm_route_*):
+S routed shard engines sharing GPU 0 in one process (tm_route_exchange_group
+/ tm_route_return_group move the topics and lists by device copies, the RCCL
+path's same transfers).  Every rank hands in its own publish batch; each
+topic is walked only on the shard that owns its first `depth` levels, and the
+lists come back to the rank that sent it.  They must equal emqx_trie:match/1
+over the WHOLE filter set (O1), id for id (global ids = the filter's index)
+and in order, on every rank."""
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+pytestmark = pytest.mark.gpu
+L1 = "latin-1"
+
+
+def _run(filters_b, filters_o, batches, S, depth):
+    from emqx_amd import shard
+    rs = shard.RoutedSet([0] * S, depth=depth, filters_hint=len(filters_o))
+    try:
+        rs.insert_many(filters_b, filters_o)
+        return rs.match_batches(batches)
+    finally:
+        rs.close()
+
+
+def _check(fb, fo, batches, got):
+    from oracle import O1
+    o1 = O1(len(fo))
+    o1.insert_many(fb, fo)
+    for (tb, to), (c, oo, ids) in zip(batches, got):
+        oc, ooo, oi = o1.match_ids(tb, to, threads=8)
+        assert np.array_equal(c, oc)
+        assert np.array_equal(oo, ooo)
+        assert np.array_equal(ids, oi)
+    o1.close()
+
+
+@pytest.mark.parametrize("S,depth", [(2, 1), (3, 2), (4, 2)])
+def test_routed_c1_every_rank_equals_o1(gpu_device, S, depth):
+    from emqx_amd import workload as W
+    fb, fo = W.filters(1)
+    batches = [W.topics(1, n=6000 + 777 * r, stream=r) for r in range(S)]
+    got = _run(fb, fo, batches, S, depth)
+    _check(fb, fo, batches, got)
+
+
+def test_routed_golden_vectors(gpu_device):
+    """the committed O1 vectors: '$' topics vs root wildcards, '#' parents,
+    empty levels, literal '+' / '#' topic levels, long topics"""
+    from emqx_amd.engine import pack
+    g = json.load(open(os.path.join(ROOT, "tests", "golden", "o1_vectors.json")))
+    for vec in g:
+        fb, fo = pack([f.encode(L1) for f in vec["filters"]])
+        topics = [r["topic"].encode(L1) for r in vec["topics"]]
+        for S, depth in ((2, 1), (3, 2)):
+            batches = [pack(topics[r::S]) for r in range(S)]
+            got = _run(fb, fo, batches, S, depth)
+            for r in range(S):
+                c, oo, ids = got[r]
+                rows = vec["topics"][r::S]
+                for t, row in enumerate(rows):
+                    want = row["match"]
+                    have = [vec["filters"][int(i)] for i in ids[oo[t]:oo[t + 1]]]
+                    assert have == want, (vec["name"], row["topic"], S, depth)
+
+
+def test_routed_c2_sample_and_empty_rank(gpu_device):
+    """a larger trie (C2: 1M filters), ranks of unequal batch sizes, one rank
+    with an empty batch"""
+    from emqx_amd import workload as W
+    fb, fo = W.filters(2, n=300_000)
+    batches = [W.topics(2, n=20000, stream=7), W.topics(2, n=0, stream=8), W.topics(2, n=5000, stream=9)]
+    got = _run(fb, fo, batches, 3, 2)
+    _check(fb, fo, batches, got)

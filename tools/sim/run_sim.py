@@ -26,7 +26,7 @@ from emqx_amd import Engine  # noqa: E402
 from emqx_amd import workload as W  # noqa: E402
 
 KINDS = ["inner", "leaf", "cold", "hot", "pair"]
-MODES = {"cur": 0, "slotrec": 1, "pair": 2, "spec": 4}
+MODES = {"cur": 0, "slotrec": 1, "pair": 2, "spec": 4, "blocks": 8}
 
 
 class View(ctypes.Structure):
@@ -40,7 +40,8 @@ class SimOut(ctypes.Structure):
                 ("topics", ctypes.c_uint64), ("steps", ctypes.c_uint64), ("matches", ctypes.c_uint64),
                 ("rounds", ctypes.c_uint64), ("probes_ok", ctypes.c_uint64), ("probes_fail", ctypes.c_uint64),
                 ("table_visits", ctypes.c_uint64), ("plus_now", ctypes.c_uint64), ("plus_pop", ctypes.c_uint64),
-                ("lit_inline", ctypes.c_uint64), ("wave_time", ctypes.c_double), ("wave_rounds", ctypes.c_double),
+                ("lit_inline", ctypes.c_uint64), ("reach_req", ctypes.c_uint64 * 5), ("reach_l2m", ctypes.c_uint64 * 5),
+                ("wave_time", ctypes.c_double), ("wave_rounds", ctypes.c_double),
                 ("waves", ctypes.c_uint64)]
 
 
@@ -93,6 +94,8 @@ def report(name, o, extra=None):
     d["plus_now"] = round(o.plus_now / t, 2)
     d["plus_pop"] = round(o.plus_pop / t, 2)
     d["lit_inline"] = round(o.lit_inline / t, 2)
+    d["node_loads_by_reach"] = {nm: [round(o.reach_req[k] / t, 2), round(o.reach_l2m[k] / t, 2)]
+                                for k, nm in enumerate(["root", "plus_now", "plus_pop", "lit_inline", "lit_table"])}
     d["wave_rounds_per_topic"] = round(o.wave_rounds * o.waves / t, 3)
     d["model_cycles_per_topic"] = round(o.wave_time * o.waves / t, 1)
     if extra:
@@ -150,6 +153,8 @@ def main():
         for part in name.split("+"):
             if part.startswith("occ"):
                 occ = int(part[3:])
+            elif part.startswith("div"):   # per-node block load: size >= div x edges
+                mode |= int(part[3:]) << 8
             else:
                 mode |= MODES[part]
         lanes = 32 * 4 * occ * 64

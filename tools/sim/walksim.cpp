@@ -50,7 +50,9 @@ struct Acc {
     uint32_t idx;   // node id / slot index (bit 31: second 16 B half of a 32 B slot)
     uint8_t kind;
     uint8_t round;
+    uint8_t reach;  // node loads: how the walk got there (R_*)
 };
+enum Reach : uint8_t { R_ROOT = 0, R_PLUS_NOW = 1, R_PLUS_POP = 2, R_LIT_INLINE = 3, R_LIT_TABLE = 4, R_NREACH = 5 };
 
 // set-associative LRU cache of 2^shift-byte lines
 struct Cache {
@@ -84,11 +86,61 @@ enum Mode : int {
     M_SLOTREC = 1,   // TM_SLOT_RECORD: 32 B slots carry the child's record, the walk goes on in the same step
     M_PAIR = 2,      // a node's '+' child at id + 1, both halves loaded in one round; an immediate '+' step is free
     M_SPECPROBE = 4, // the parent's reference says "WIDE": the home slot is loaded with the node (no Bloom)
+    M_BLOCKS = 8,    // per-node child blocks: a WIDE node's literal / '#' edges in a contiguous open-addressing
+                     // block of its own (blocks in node order = heat order), not one shared table
+};
+
+// per-node child blocks (M_BLOCKS): 16 B slots {word, child, S(child), -}
+struct Blocks {
+    std::vector<uint64_t> base;    // per node: first slot (cells), ~0 = none
+    std::vector<uint32_t> size;    // per node: slots (power of two)
+    std::vector<uint32_t> word, child, sum;
+    uint32_t div = 2;              // block size >= div * edges
+    static uint32_t home(uint32_t w, uint32_t mask) { return (w * 0x9E3779B1u >> 7) & mask; }
+    void build(const View& v, uint32_t d) {
+        div = d;
+        const uint64_t n = v.n_nodes;
+        std::vector<uint32_t> cnt(n, 0);
+        auto each = [&](auto f) {
+            for (const EdgeSlot* t : {v.cold, v.hot}) {
+                const uint64_t ns = t == v.cold ? v.cold_slots : v.hot_slots;
+                for (uint64_t s = 0; s < ns; ++s)
+                    if (t[s].parent != EDGE_EMPTY) f(t[s]);
+            }
+        };
+        each([&](const EdgeSlot& e) { ++cnt[e.parent]; });
+        base.assign(n, ~0ull);
+        size.assign(n, 0);
+        uint64_t cur = 0;
+        for (uint64_t x = 0; x < n; ++x) {
+            if (!cnt[x]) continue;
+            uint32_t sz = 1;
+            while (sz < cnt[x] * div) sz <<= 1;
+            if (sz < 4) sz = 4;
+            // a block of <= 4 slots never crosses a 64 B line
+            if (sz <= 4 && ((cur & 3) + sz > 4)) cur = (cur + 3) & ~3ull;
+            base[x] = cur;
+            size[x] = sz;
+            cur += sz;
+        }
+        word.assign(cur, EDGE_EMPTY);
+        child.assign(cur, NODE_NONE);
+        sum.assign(cur, 0);
+        each([&](const EdgeSlot& e) {
+            const uint32_t m = size[e.parent] - 1;
+            uint32_t p = home(e.word, m);
+            while (word[base[e.parent] + p] != EDGE_EMPTY) p = (p + 1) & m;
+            word[base[e.parent] + p] = e.word;
+            child[base[e.parent] + p] = e.child;
+            sum[base[e.parent] + p] = e.plus;
+        });
+    }
 };
 
 struct Walker {
     const View& v;
     int mode = 0;
+    const Blocks* blk = nullptr;
     mutable uint64_t probes_ok = 0, probes_fail = 0, table_visits = 0, plus_now = 0, plus_pop = 0, lit_inline = 0;
     mutable uint64_t wide_hist[48] = {0};   // WIDE lookups by log2(children): lookups, bloom passes, hits
     explicit Walker(const View& vw, int m) : v(vw), mode(m) {}
@@ -103,6 +155,29 @@ struct Walker {
     // probe_edge<false> (kernels.hip): linear probing from the home slot,
     // one dependent round per slot (from round rd0 on)
     Hit probe(uint32_t node, uint32_t w, std::vector<Acc>& acc, uint32_t& rd) const {
+        if (mode & M_BLOCKS) {
+            const uint64_t b = blk->base[node];
+            if (b == ~0ull) {
+                ++probes_fail;
+                return Hit{NODE_NONE, 0, false};
+            }
+            const uint32_t m = blk->size[node] - 1;
+            uint32_t p = Blocks::home(w, m);
+            for (;;) {
+                acc.push_back(Acc{(uint32_t)(b + p), K_COLD, (uint8_t)std::min<uint32_t>(rd, 255)});
+                ++rd;
+                const uint32_t ww = blk->word[b + p];
+                if (ww == w) {
+                    ++probes_ok;
+                    return Hit{blk->child[b + p], blk->sum[b + p], false};
+                }
+                if (ww == EDGE_EMPTY) {
+                    ++probes_fail;
+                    return Hit{NODE_NONE, 0, false};
+                }
+                p = (p + 1) & m;
+            }
+        }
         const bool hot = node < v.hot_limit;
         const EdgeSlot* tab = hot ? v.hot : v.cold;
         const uint64_t mask = (hot ? v.hot_slots : v.cold_slots) - 1;
@@ -175,6 +250,7 @@ struct Walker {
             if (cv == NODE_NONE) return;
         }
         bool have = false;          // slotrec: the node's record came with the previous probe
+        uint8_t reach = R_ROOT;
         uint32_t pair_id = NODE_NONE;   // pair: the half already in registers
         for (;;) {
             const uint32_t node = cv, r = cr;
@@ -190,8 +266,8 @@ struct Walker {
                 pair_id = NODE_NONE;
             } else {
                 const bool pair = (mode & M_PAIR) && !leaf && (x.plus & NODE_MASK) == node + 1;
-                acc.push_back(Acc{node, leaf ? K_LEAF : K_INNER, 0});
-                if (pair) acc.push_back(Acc{node + 1, K_PAIR, 0});
+                acc.push_back(Acc{node, leaf ? K_LEAF : K_INNER, 0, reach});
+                if (pair) acc.push_back(Acc{node + 1, K_PAIR, 0, reach});
                 rd = 1;
                 pair_id = pair ? node + 1 : NODE_NONE;
             }
@@ -219,6 +295,7 @@ struct Walker {
                     cv = g.child;
                     cr = r + 1;
                     have = g.delivered;
+                    reach = (x.plus & WIDE) ? R_LIT_TABLE : R_LIT_INLINE;
                     if (pair_id != NODE_NONE) pair_id = NODE_NONE;   // the '+' half is not kept past a descent
                     next = true;
                 } else if (pc != NODE_NONE) {
@@ -226,6 +303,7 @@ struct Walker {
                     cv = pc;
                     cr = r + 1;
                     ++plus_now;
+                    reach = R_PLUS_NOW;
                     next = true;
                 }
             }
@@ -237,6 +315,7 @@ struct Walker {
                 cv = path[k];
                 cr = k + 1;
                 ++plus_pop;
+                reach = R_PLUS_POP;
                 pair_id = NODE_NONE;
             }
         }
@@ -251,6 +330,7 @@ struct SimOut {
     uint64_t req[K_NKIND], l1m[K_NKIND], l2m[K_NKIND];
     uint64_t topics, steps, matches, rounds;
     uint64_t probes_ok, probes_fail, table_visits, plus_now, plus_pop, lit_inline;
+    uint64_t reach_req[R_NREACH], reach_l2m[R_NREACH];   // node loads by how the node was reached
     double wave_time;        // mean over waves of the summed per-round max latency (cycles)
     double wave_rounds;      // mean over waves of the dependent rounds executed
     uint64_t waves;
@@ -264,6 +344,11 @@ int sim_run(const void* view, const uint32_t* levels, const uint32_t* words, con
             SimOut* out) {
     const View& vw = *reinterpret_cast<const View*>(view);
     Walker wk(vw, mode);
+    Blocks blocks;
+    if (mode & M_BLOCKS) {
+        blocks.build(vw, (uint32_t)((mode >> 8) & 0xFF) ? (uint32_t)((mode >> 8) & 0xFF) : 2u);
+        wk.blk = &blocks;
+    }
     std::memset(out, 0, sizeof(SimOut));
     std::vector<uint64_t> woff(n_topics + 1, 0);
     for (uint32_t t = 0; t < n_topics; ++t) woff[t + 1] = woff[t] + levels[t];
@@ -329,12 +414,15 @@ int sim_run(const void* view, const uint32_t* levels, const uint32_t* words, con
                     const Acc& a = ln.acc[k];
                     const uint64_t ad = addr(a);
                     ++out->req[a.kind];
+                    const bool nodeload = a.kind == K_INNER || a.kind == K_LEAF;
+                    if (nodeload) ++out->reach_req[a.reach];
                     double lt = lat[0];
                     if (!c1.access(ad)) {
                         ++out->l1m[a.kind];
                         lt = lat[1];
                         if (!l2.access(ad)) {
                             ++out->l2m[a.kind];
+                            if (nodeload) ++out->reach_l2m[a.reach];
                             lt = lat[2];
                         }
                     }
