@@ -99,6 +99,9 @@ def parse():
     ap.add_argument("--layout", type=int, default=None, help="1 = DFS relayout on commit (default), 0 = off")
     ap.add_argument("--opt", action="append", default=[], help="EXPERIMENT: engine option name=value (repeatable)")
     ap.add_argument("--presort", default=None, help="EXPERIMENT: batches sorted on the host: bytes | hN (N-bit word hashes)")
+    ap.add_argument("--ab-opt", action="append", default=[],
+                    help="EXPERIMENT: after the headline region, time the same batches again with these engine options "
+                         "(name=value[,name=value]; repeatable; one trie build for every variant), reported under ab")
     return ap.parse_args()
 
 
@@ -392,6 +395,22 @@ def main():
     results = reg.results()
     n0 = reg.dbat[0][2]
 
+    # in-process A/B of engine options over the same trie and batches
+    ab = []
+    for spec in a.ab_opt:
+        kv = [x.split("=") for x in spec.split(",") if x]
+        for k, x in kv:
+            eng.set_option(k, int(x))
+        reg.warm(a.warmup)
+        adt = reg.timed(a.steps)
+        akms = reg.kernel_times(a.roof_steps)
+        ares = reg.results()
+        same = all(np.array_equal(x[0], y[0]) and np.array_equal(x[1], y[1]) and np.array_equal(x[2], y[2])
+                   for x, y in zip(ares, results))
+        ab.append({"opts": spec, "ms_per_step": adt / a.steps * 1e3, "kernel_ms": akms,
+                   "value": (a.topics if a.scaling == "strong" else n0 * world) * a.steps / adt,
+                   "lists_equal_headline": bool(same)})
+        log("A/B %s: %.3f ms per step, kernels %s, lists equal: %s" % (spec, adt / a.steps * 1e3, akms, same))
     # the other scaling figure beside it (not `value`): weak scaling at
     # SURVEY §8(d)'s 1M topics per GPU when the headline is strong
     weak = None
@@ -509,6 +528,8 @@ def main():
         }
         if weak:
             out["weak"] = weak
+        if ab:
+            out["ab"] = ab
         out.update(extras)
         emit(out)
     eng.close()
@@ -663,13 +684,15 @@ def host_legs(a, eng, batch, total):
                                          ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                          ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_double)]
         k = n   # the whole batch, after a warm-up run inside the driver
-        res = (ctypes.c_double * 8)()
+        res = (ctypes.c_double * 12)()
         bc = BATCHER
         rc = drv.tm_bench_batcher(eng.h, tb.ctypes.data, to.ctypes.data, k, bc["producers"], bc["deadline_us"],
                                   bc["max_topics"], bc["lanes_per_replica"], 0, bc["callback_threads"], res)
         if rc == 0:
             out["batcher"] = dict(bc, topics_per_s=res[1], topics=k, batches=int(res[2]), mean_batch=res[3],
                                   lat_us_p50=res[4], lat_us_p99=res[5], failed=int(res[6]), matches=int(res[7]),
+                                  per_batch_us={"sealed_to_lane": res[8], "pack": res[9], "device": res[10],
+                                                "callbacks": res[11]},
                                   path="tm_batcher_submit per publish from %d threads, per-topic callbacks "
                                        "(NIF path), PCIe both ways included" % bc["producers"])
             log("batcher: %.0f topics/s, mean batch %.0f, p50 %.0f us, p99 %.0f us" % (res[1], res[3], res[4],

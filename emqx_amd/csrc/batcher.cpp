@@ -234,6 +234,8 @@ struct tm_batcher {
         const uint64_t n = pending(&b, &o);
         if (n == 0) return false;
         if (n >= cfg.max_topics || b >= cfg.max_bytes || force.load(std::memory_order_acquire)) return true;
+        // TM_BATCHER_EAGER: a free lane takes whatever is pending (under mu)
+        if ((cfg.flags & TM_BATCHER_EAGER) && !free_lanes.empty()) return true;
         return now_ns() - o >= (int64_t)cfg.deadline_us * 1000;
     }
 
@@ -487,6 +489,7 @@ struct tm_batcher {
             --in_flight;
             cv_lane.notify_all();
             cv_idle.notify_all();
+            if (cfg.flags & TM_BATCHER_EAGER) cv_work.notify_one();   // the sealer may seal at once now
         }
     }
 

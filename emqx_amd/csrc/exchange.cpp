@@ -260,7 +260,7 @@ int route_alloc_recv(tm_comm* c) {
 int route_finish(tm_comm* c, hipStream_t st, tm_route_out* out) {
     tm_comm::Route& r = c->rt;
     XHIP(c, hipMemsetAsync(r.rbuf.as<uint8_t>() + r.rb_base[c->nranks], 0, 16, st));
-    XHIP(c, launch_scan(r.rlen.as<uint32_t>(), r.m, r.roff.as<uint64_t>(), r.roff.as<uint64_t>() + r.m,
+    XHIP(c, launch_scan0(r.rlen.as<uint32_t>(), r.m, r.roff.as<uint64_t>(), r.roff.as<uint64_t>() + r.m,
                         r.rscan.as<uint64_t>(), st));
     out->m = r.m;
     out->reserved = 0;
@@ -303,7 +303,7 @@ int return_alloc(tm_comm* c) {
 // return step 3 (one rank): the lists in the batch's own topic order
 int return_finish(tm_comm* c, hipStream_t st, tm_route_result* res) {
     tm_comm::Route& r = c->rt;
-    XHIP(c, launch_scan(r.rcount.as<uint32_t>(), r.n, r.rroff.as<uint64_t>(), r.rroff.as<uint64_t>() + r.n,
+    XHIP(c, launch_scan0(r.rcount.as<uint32_t>(), r.n, r.rroff.as<uint64_t>(), r.rroff.as<uint64_t>() + r.n,
                         r.uscan.as<uint64_t>(), st));
     XHIP(c, launch_route_unpermute(r.rcount.as<uint32_t>(), r.rroff.as<uint64_t>(), r.rids.as<uint32_t>(),
                                    r.perm.as<uint32_t>(), r.n, r.out_count.as<uint32_t>(), r.out_off.as<uint64_t>(),

@@ -158,6 +158,9 @@ struct RoutePlanBufs {
 };
 hipError_t launch_route_plan(const uint8_t* bytes, const uint64_t* off, uint32_t n, uint32_t depth, uint32_t S,
                              const RoutePlanBufs& w, hipStream_t st);
+// launch_scan, and for n = 0 out_off[0] = *total = 0
+hipError_t launch_scan0(const uint32_t* counts, uint32_t n, uint64_t* out_off, uint64_t* total, uint64_t* tmp,
+                        hipStream_t st);
 // out[k] = in[idx[k]], k < count
 hipError_t launch_gather_u64(const uint64_t* in, const uint32_t* idx, uint32_t k, uint64_t* out, hipStream_t st);
 // lists returned in bucket order (rcount n, roff CSR, rids) -> the batch's own

@@ -432,19 +432,12 @@ constexpr int HIST_OFF = 8;   // hist = stats + HIST_OFF
 #ifndef TM_PEND_MASK
 #define TM_PEND_MASK 1   // A/B at C3: walk 9.78 vs 10.08-10.09 ms (profiles/r03_ab)
 #endif
-// TM_SLOT_RECORD=2 (A/B builds, "stash"): the 32 B edge slots carry the
-// child's record as in TM_SLOT_RECORD=1, but a probe that finds the child
-// ends the step with the record kept in the cursor; the next step visits
-// the child from those registers instead of loading its half (one dependent
-// round per step, as without slot records)
-constexpr bool SLOT_STASH = TM_SLOT_RECORD == 2;
 struct Cursor {
     uint32_t v, r, n, r0;   // node to visit next and its level; topic levels; start level
     uint32_t pend;          // TM_PEND_MASK: bit k = path(k) holds a '+' child still to visit (k < r)
     uint64_t key;           // KEYS: fold branches taken above level r (rank_sym), key word 0
-    uint32_t pf_id;         // TM_PF1 / SLOT_STASH: node whose half is in pf (NODE_NONE: none)
+    uint32_t pf_id;         // TM_PF1: node whose half is in pf (NODE_NONE: none)
     uint4 pf;
-    uint32_t pf_sf;         // SLOT_STASH: that node's own filter (its leaf half's first word)
 };
 
 // Order keys (sharded mode).  Every match of a topic is identified by the
@@ -610,9 +603,6 @@ __device__ __forceinline__ bool walk_step(const ImageView& im, Cursor& c, Path p
             c.pf_id = sib;
             c.pf = ph;
         }
-    } else if (SLOT_STASH && c.pf_id == v) {   // the record came with the probe that found v
-        h = leaf ? make_uint4(c.pf_sf, c.pf.y, 0u, 0u) : c.pf;
-        c.pf_id = NODE_NONE;
     } else {
         h = load_half(im, v, leaf, r);   // inner {plus, hf, lw, lc} / leaf {sf, hf, hash, pad}
     }
@@ -667,15 +657,10 @@ __device__ __forceinline__ bool walk_step(const ImageView& im, Cursor& c, Path p
             v = g.child;
             if (KEYS) key |= rank_sym(r, 1);
             ++r;
-            if (!g.have || SLOT_STASH) {
+            if (!g.have) {
                 c.v = v;
                 c.r = r;
                 if (KEYS) c.key = key;
-                if (SLOT_STASH && g.have) {
-                    c.pf_id = v;
-                    c.pf = make_uint4(g.plus, g.hf, g.lw, g.lc);
-                    c.pf_sf = g.sf;
-                }
                 return false;
             }
             plus = g.plus;
@@ -828,8 +813,6 @@ constexpr uint32_t NO_TOPIC = 0xFFFFFFFFu;
 
 #if TM_PF1
 #define TM_WALK_ATTR __attribute__((amdgpu_waves_per_eu(7, 8)))   // the prefetch slot within 7 waves/SIMD
-#elif TM_SLOT_RECORD == 2
-#define TM_WALK_ATTR __attribute__((amdgpu_waves_per_eu(6, 8)))   // the stashed record within 6 waves/SIMD
 #else
 #define TM_WALK_ATTR
 #endif

@@ -103,17 +103,20 @@ tm_route_bases(const uint32_t* __restrict__ blk_cnt, uint32_t nb, uint32_t S, ui
         }
         __syncthreads();
     }
+    __shared__ uint32_t sb[MAX_ROUTE_SHARDS + 1];
     if (threadIdx.x == 0) {
         uint32_t run = 0;
         for (uint32_t o = 0; o < S; ++o) {
-            bucket[o] = run;
+            sb[o] = run;
             run += tot[o];
         }
-        bucket[S] = run;
+        sb[S] = run;
     }
     __syncthreads();
-    // bucket bases folded into the block bases
-    for (uint64_t i = threadIdx.x; i < (uint64_t)nb * S; i += RB) blk_base[i] += bucket[i % S];
+    // bucket bases folded into the block bases (each thread into the entries it wrote)
+    for (uint32_t b = lo; b < hi; ++b)
+        for (uint32_t o = 0; o < S; ++o) blk_base[(uint64_t)b * S + o] += sb[o];
+    if (threadIdx.x <= S) bucket[threadIdx.x] = sb[threadIdx.x];
 }
 
 // stable positions: block base + the topic's rank among the block's earlier
@@ -188,6 +191,14 @@ inline uint32_t blocks_of(uint64_t n, uint32_t per) { return (uint32_t)((n + per
 
 }  // namespace
 
+hipError_t launch_scan0(const uint32_t* counts, uint32_t n, uint64_t* out_off, uint64_t* total, uint64_t* tmp,
+                        hipStream_t st) {
+    if (n) return launch_scan(counts, n, out_off, total, tmp, st);
+    hipError_t err = hipMemsetAsync(out_off, 0, 8, st);   // an empty batch: offsets {0}, total 0
+    if (err == hipSuccess && total != out_off) err = hipMemsetAsync(total, 0, 8, st);
+    return err;
+}
+
 hipError_t launch_route_plan(const uint8_t* bytes, const uint64_t* off, uint32_t n, uint32_t depth, uint32_t S,
                              const RoutePlanBufs& w, hipStream_t st) {
     if (S == 0 || S > MAX_ROUTE_SHARDS) return hipErrorInvalidValue;
@@ -200,7 +211,7 @@ hipError_t launch_route_plan(const uint8_t* bytes, const uint64_t* off, uint32_t
         hipLaunchKernelGGL(tm_route_scatter, dim3(nb), dim3(RB), 0, st, off, n, S, w.owner, w.blk_base, w.perm,
                            w.slen);
     }
-    hipError_t err = launch_scan(w.slen, n, w.soff, w.soff + n, w.scan_tmp, st);
+    hipError_t err = launch_scan0(w.slen, n, w.soff, w.soff + n, w.scan_tmp, st);
     if (err != hipSuccess) return err;
     if (n) hipLaunchKernelGGL(tm_route_bytes, dim3(nb), dim3(RB), 0, st, bytes, off, n, w.perm, w.soff, w.sbuf);
     // byte cut of every bucket: soff[bucket[o]], o = 0..S
@@ -217,7 +228,7 @@ hipError_t launch_route_unpermute(const uint32_t* rcount, const uint64_t* roff, 
                                   const uint32_t* perm, uint32_t n, uint32_t* out_count, uint64_t* out_off,
                                   uint32_t* out_ids, uint64_t* total, uint64_t* scan_tmp, hipStream_t st) {
     if (n) hipLaunchKernelGGL(tm_route_unpermute, dim3(blocks_of(n, RB)), dim3(RB), 0, st, rcount, perm, n, out_count);
-    hipError_t err = launch_scan(out_count, n, out_off, total, scan_tmp, st);
+    hipError_t err = launch_scan0(out_count, n, out_off, total, scan_tmp, st);
     if (err != hipSuccess) return err;
     if (n && out_ids)
         hipLaunchKernelGGL(tm_route_lists, dim3(blocks_of(n, RB / 64)), dim3(RB), 0, st, rcount, roff, rids, perm, n,

@@ -500,6 +500,8 @@ int tm_match_deliveries_batch_device(tm_engine* e, const uint8_t* d_topic_bytes,
  * term and enif_send()s it).  status != TM_OK: ids are null. */
 #define TM_BATCHER_ROUTES 1u   /* results are match_routes/1 (src ids + dest ids) */
 #define TM_BATCHER_DELIVERIES 2u   /* results are aggre(match_routes/1) (To ids + target ids) */
+#define TM_BATCHER_EAGER 4u   /* seal as soon as a lane is free (deadline_us stays the upper bound): low
+                                 load runs small batches at once, high load batches up while lanes are busy */
 
 typedef struct tm_batcher tm_batcher;
 typedef struct tm_batcher_config {

@@ -31,7 +31,9 @@ void on_done(void* ctx, uint64_t, int status, const uint32_t*, const uint32_t*, 
 }
 }  // namespace
 
-// out[8]: seconds, topics/s, batches, mean batch, p50 us, p99 us, failed, matches
+// out[12]: seconds, topics/s, batches, mean batch, p50 us, p99 us, failed,
+// matches, then per batch (us): sealed -> lane, pack, device path (H2D,
+// kernels, D2H), callbacks
 extern "C" int tm_bench_batcher(tm_engine* e, const uint8_t* tb, const uint64_t* to, uint64_t nt, int producers,
                                 uint32_t deadline_us, uint32_t max_topics, uint32_t lanes, uint32_t flags,
                                 uint32_t cb_threads, double* out) {
@@ -80,6 +82,11 @@ extern "C" int tm_bench_batcher(tm_engine* e, const uint8_t* tb, const uint64_t*
     tm_batcher_close(b);
     st.batches -= st0.batches;
     st.topics -= st0.topics;
+    const double nb = st.batches ? (double)st.batches : 1.0;
+    out[8] = (st.wait_ns - st0.wait_ns) / nb / 1e3;
+    out[9] = (st.pack_ns - st0.pack_ns) / nb / 1e3;
+    out[10] = (st.device_ns - st0.device_ns) / nb / 1e3;
+    out[11] = (st.callback_ns - st0.callback_ns) / nb / 1e3;
     std::vector<int64_t> lat;
     lat.reserve(nt / LAT_EVERY + 1);
     uint64_t fails = 0, ids = 0;
