@@ -172,6 +172,24 @@ def make_batches(a, cfg, rank, world):
     if a.presort:   # EXPERIMENT: the batch in topic byte order (lanes of a wave walk shared prefixes)
         from emqx_amd.engine import pack
         import zlib
+        if a.presort == "lpt":   # the predicted-heavy topics first within each XCD range (tail experiment)
+            import math
+
+            def cost(t):   # hot words (low Zipf rank k of w<level>_<k>) lead to more filters below
+                c = 0.0
+                for w in t.split(b"/"):
+                    k = w.rsplit(b"_", 1)[-1]
+                    c += -math.log2(int(k) + 2) if k.isdigit() else -32
+                return c
+            res = []
+            for tb, to in out:
+                ts = W.unpack(tb, to)
+                n = len(ts)
+                srt = []
+                for r in range(8):
+                    srt += sorted(ts[n * r // 8: n * (r + 1) // 8], key=cost, reverse=True)
+                res.append(pack(srt))
+            return res
         if a.presort == "bytes":
             key = None
         else:   # "hN": each level's word hashed to N bits, level-major (what a device radix sort could use)

@@ -13,6 +13,8 @@
 #   latency   open-loop batcher latency sweep             -> latency.jsonl
 #   slices    rocprofv3 stats of one-GPU batches of $SLICES topics (the per-rank slices of strong scaling)
 #   rehearse  the driver's N > 1 launch with $NPROC ranks sharing GPU 0 (control plane over gloo)
+#   routed    bench --mode routed in one process: $SHARDS routed shards on GPU 0 (device-copy exchange)
+#   batcher   tools/bench_batcher.py $BATCHER_ARGS (flood: per-stage split, eager sealing, replicas)
 # e.g. gpurun -- 'STEPS="tests bench prof" TAG=r02_head bash tools/gpu.sh'
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
@@ -46,6 +48,11 @@ for s in ${STEPS:-tests}; do
                --nproc-per-node ${NPROC:-2} --master-addr 127.0.0.1 --master-port ${PORT:-29533} bench.py \
                --gpus ${NPROC:-2} --steps 20 --warmup 3 --no-extras ${BENCH_ARGS} \
                > "$OUT/rehearse_${NPROC:-2}.json" 2> "$OUT/rehearse_${NPROC:-2}.log" ;;
+    routed) timeout -k 10 600 python3 -u bench.py --mode routed --single-process --shards ${SHARDS:-4} \
+               --steps 20 --warmup 3 --depth ${DEPTH:-2} ${BENCH_ARGS} > "$OUT/routed_${SHARDS:-4}.json" \
+               2> "$OUT/routed_${SHARDS:-4}.log" ;;
+    batcher) timeout -k 10 ${T_BATCHER:-600} python3 -u tools/bench_batcher.py ${BATCHER_ARGS} \
+               >> "$OUT/batcher.jsonl" 2>> "$OUT/batcher.log" ;;
     cmd)   timeout -k 10 ${T_CMD:-600} python -u -c "$CMD" > "$OUT/cmd.log" 2>&1 ;;
     latency) timeout -k 10 ${T_LAT:-400} python -u tools/bench_batcher_latency.py ${LAT_ARGS} \
              >> "$OUT/latency.jsonl" 2>> "$OUT/latency.log" ;;

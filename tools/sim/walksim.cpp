@@ -458,6 +458,26 @@ int sim_run(const void* view, const uint32_t* levels, const uint32_t* words, con
     return 0;
 }
 
+// per-topic walk steps (node visits) and loads, no caches
+int sim_per_topic(const void* view, const uint32_t* levels, const uint32_t* words, const uint8_t* dollar,
+                  uint32_t n_topics, uint32_t* steps_out, uint32_t* loads_out) {
+    const View& vw = *reinterpret_cast<const View*>(view);
+    Walker wk(vw, 0);
+    std::vector<Acc> acc;
+    std::vector<uint32_t> steps;
+    uint64_t wo = 0;
+    for (uint32_t t = 0; t < n_topics; ++t) {
+        acc.clear();
+        steps.clear();
+        uint64_t m = 0;
+        wk.walk(words + wo, levels[t], dollar[t] != 0, acc, steps, m);
+        wo += levels[t];
+        steps_out[t] = (uint32_t)steps.size();
+        loads_out[t] = (uint32_t)acc.size();
+    }
+    return 0;
+}
+
 // the walk alone (no caches): WIDE lookups by children count
 int sim_count(const void* view, const uint32_t* levels, const uint32_t* words, const uint8_t* dollar,
               uint32_t n_topics, SimOut* out, uint64_t* hist48) {
