@@ -142,6 +142,15 @@ struct Lane {
     uint32_t cb_left = 0;
     Pinned h_bytes, h_off, h_counts, h_outoff, h_src, h_dest, h_total;
     Dev d_bytes, d_off, d_counts, d_outoff, d_src, d_dest, d_total;
+    // small match/1 batches (fused transfers): offsets + bytes up in one copy,
+    // total + offsets + counts + ids down in one copy
+    Pinned h_io, h_out;
+    Dev d_io, d_out;
+    // the batch's results as the callbacks read them (into h_out, or the separate buffers)
+    const uint32_t* r_counts = nullptr;
+    const uint64_t* r_off = nullptr;
+    const uint32_t* r_src = nullptr;
+    const uint32_t* r_dst = nullptr;
     double ids_per_topic = 64.0;      // sizing estimate of the device result buffers
     clk::time_point sealed;           // when the batch was handed over
 };
@@ -294,12 +303,22 @@ struct tm_batcher {
 
     // the lane packs its chunks into pinned memory (bytes, offsets); false:
     // staging memory ran out
-    bool pack(Lane& L) {
+    static bool fused(const Lane& L, bool routes) { return !routes && L.n <= EAGER_TOPICS; }
+    bool pack(Lane& L, bool routes) {
         uint64_t nb = 0;
         for (const Chunk& c : L.chunks) nb += c.nbytes();
-        if (!L.h_bytes.ensure(nb + 16) || !L.h_off.ensure(((uint64_t)L.n + 1) * 8)) return false;
-        uint8_t* hb = (uint8_t*)L.h_bytes.p;
-        uint64_t* ho = (uint64_t*)L.h_off.p;
+        uint8_t* hb;
+        uint64_t* ho;
+        if (fused(L, routes)) {   // [offsets (n+1) u64][bytes] in one pinned block
+            const uint64_t offb = ((uint64_t)L.n + 1) * 8;
+            if (!L.h_io.ensure(offb + nb + 16)) return false;
+            ho = (uint64_t*)L.h_io.p;
+            hb = (uint8_t*)L.h_io.p + offb;
+        } else {
+            if (!L.h_bytes.ensure(nb + 16) || !L.h_off.ensure(((uint64_t)L.n + 1) * 8)) return false;
+            hb = (uint8_t*)L.h_bytes.p;
+            ho = (uint64_t*)L.h_off.p;
+        }
         uint64_t o = 0, k = 0;
         ho[0] = 0;
         for (const Chunk& c : L.chunks) {
@@ -314,7 +333,47 @@ struct tm_batcher {
 
     // the lane's batch on its GPU; results in the lane's pinned buffers
     static constexpr uint32_t EAGER_TOPICS = 32768;   // batches up to this size read their lists back with the counts
+    // a small match/1 batch: one copy up, the walk, one copy down (a small
+    // batch's device time is mostly per-operation latency, not bytes)
+    int run_fused(Lane& L, uint64_t& total) {
+        auto chk = [](hipError_t e) { return e == hipSuccess; };
+        const uint32_t n = L.n;
+        const uint64_t offb = ((uint64_t)n + 1) * 8;
+        const uint64_t nbytes = ((const uint64_t*)L.h_io.p)[n];
+        const uint64_t cntb = ((uint64_t)n * 4 + 7) & ~7ull;
+        if (!L.d_io.ensure(offb + nbytes + 16)) return TM_ENOMEM;
+        hipStream_t s = L.stream;
+        if (!chk(hipMemcpyAsync(L.d_io.p, L.h_io.p, offb + nbytes + 8, hipMemcpyHostToDevice, s))) return TM_EDEVICE;
+        uint64_t cap = (uint64_t)(L.ids_per_topic * n * 1.25) + 1024;
+        for (int pass = 0; pass < 2; ++pass) {
+            const uint64_t outb = 8 + offb + cntb + cap * 4;
+            if (!L.d_out.ensure(outb) || !L.h_out.ensure(outb)) return TM_ENOMEM;
+            uint8_t* d = (uint8_t*)L.d_out.p;
+            int rc = tm_match_batch_device(eng, (const uint8_t*)L.d_io.p + offb, (const uint64_t*)L.d_io.p, n, nbytes,
+                                           (uint32_t*)(d + 8 + offb), (uint64_t*)(d + 8), (uint32_t*)(d + 8 + offb + cntb),
+                                           cap, (uint64_t*)d, s);
+            if (rc != TM_OK) return rc;
+            if (!chk(hipMemcpyAsync(L.h_out.p, L.d_out.p, outb, hipMemcpyDeviceToHost, s)) ||
+                !chk(hipStreamSynchronize(s)))
+                return TM_EDEVICE;
+            const uint8_t* h = (const uint8_t*)L.h_out.p;
+            total = *(const uint64_t*)h;
+            L.ids_per_topic = 0.9 * L.ids_per_topic + 0.1 * ((double)total / n);
+            L.r_off = (const uint64_t*)(h + 8);
+            L.r_counts = (const uint32_t*)(h + 8 + offb);
+            L.r_src = (const uint32_t*)(h + 8 + offb + cntb);
+            L.r_dst = nullptr;
+            if (total <= cap) return TM_OK;
+            cap = total + total / 4 + 1024;   // overflow: rerun with room (rare)
+        }
+        return TM_EDEVICE;
+    }
     int run_device(Lane& L, bool routes, bool deliv, uint64_t& total) {
+        if (fused(L, routes)) return run_fused(L, total);
+        L.r_counts = (const uint32_t*)L.h_counts.p;
+        L.r_off = (const uint64_t*)L.h_outoff.p;
+        L.r_src = (const uint32_t*)L.h_src.p;
+        L.r_dst = (const uint32_t*)L.h_dest.p;
         auto chk = [](hipError_t e) { return e == hipSuccess; };
         const uint32_t n = L.n;
         const uint64_t nbytes = ((const uint64_t*)L.h_off.p)[n];
@@ -357,7 +416,13 @@ struct tm_batcher {
             total = *(const uint64_t*)L.h_total.p;
             L.ids_per_topic = 0.9 * L.ids_per_topic + 0.1 * ((double)total / n);
             if (total <= cap) {
-                if (eager) return TM_OK;   // the lists came with the counts
+                if (eager) {   // the lists came with the counts
+                    L.r_src = (const uint32_t*)L.h_src.p;
+                    L.r_dst = (const uint32_t*)L.h_dest.p;
+                    L.r_counts = (const uint32_t*)L.h_counts.p;
+                    L.r_off = (const uint64_t*)L.h_outoff.p;
+                    return TM_OK;
+                }
                 break;
             }
             cap = total + total / 4 + 1024;   // overflow: rerun with room (rare)
@@ -367,15 +432,19 @@ struct tm_batcher {
             (total && routes && !chk(hipMemcpyAsync(L.h_dest.p, L.d_dest.p, total * 4, hipMemcpyDeviceToHost, s))) ||
             !chk(hipStreamSynchronize(s)))
             return TM_EDEVICE;
+        L.r_counts = (const uint32_t*)L.h_counts.p;
+        L.r_off = (const uint64_t*)L.h_outoff.p;
+        L.r_src = (const uint32_t*)L.h_src.p;
+        L.r_dst = (const uint32_t*)L.h_dest.p;
         return TM_OK;
     }
 
     // callbacks of topics [lo, hi) of lane L's batch (gather order)
     void callbacks(const Lane& L, int rc, bool routes, uint32_t lo, uint32_t hi) {
-        const uint32_t* cnt = (const uint32_t*)L.h_counts.p;
-        const uint64_t* off = (const uint64_t*)L.h_outoff.p;
-        const uint32_t* src = (const uint32_t*)L.h_src.p;
-        const uint32_t* dst = (const uint32_t*)L.h_dest.p;
+        const uint32_t* cnt = L.r_counts;
+        const uint64_t* off = L.r_off;
+        const uint32_t* src = L.r_src;
+        const uint32_t* dst = L.r_dst;
         uint32_t i = 0;
         for (const Chunk& c : L.chunks) {
             const uint32_t cn = (uint32_t)c.size();
@@ -458,12 +527,12 @@ struct tm_batcher {
             uint64_t lease = 0;
             const bool leased = rc == TM_OK && n && tm_lease_begin(eng, &lease) == TM_OK;
             if (rc == TM_OK && n) {
-                const bool packed = pack(L);
+                const bool packed = pack(L, routes);
                 t_packed = clk::now();
                 rc = packed ? run_device(L, routes, deliv, total) : TM_ENOMEM;
                 t_dev = clk::now();
                 if (rc == TM_OK)   // deliveries sit at route offsets: count the entries
-                    for (uint32_t i = 0; i < n; ++i) results += ((const uint32_t*)L.h_counts.p)[i];
+                    for (uint32_t i = 0; i < n; ++i) results += L.r_counts[i];
             }
             const uint32_t m = n;
             run_callbacks(L, rc, routes, m);

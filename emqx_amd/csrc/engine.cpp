@@ -242,7 +242,9 @@ struct Image {
     // always come from one commit
     DevBuf d_rslots, d_rarena, d_rdest, d_fr_meta, d_rank_src, d_dt, d_rank_tg;
     DevBuf d_fshape;   // option "shape_keys": filter id -> order key
+    DevBuf d_wheat;    // word id -> heat (option "presort" 2: the tail order's cost estimate)
     size_t arena_uploaded = 0, woff_uploaded = 0;
+    uint64_t heat_uploaded = ~0ull;   // word_heat version in d_wheat
     bool split_stale = true, written = false;
     uint64_t epoch = 0;
     std::vector<hipEvent_t> uses;
@@ -254,7 +256,7 @@ struct Image {
     AggreView av{};
     void release() {
         for (DevBuf* b : {&d_nodes, &d_edges, &d_hedges, &d_dict, &d_arena, &d_woff, &d_inner, &d_leaf, &d_rslots,
-                          &d_rarena, &d_rdest, &d_fr_meta, &d_rank_src, &d_dt, &d_rank_tg, &d_fshape})
+                          &d_rarena, &d_rdest, &d_fr_meta, &d_rank_src, &d_dt, &d_rank_tg, &d_fshape, &d_wheat})
             b->release();
         for (hipEvent_t ev : uses) (void)hipEventDestroy(ev);
         uses.clear();
@@ -413,6 +415,21 @@ struct tm_engine {
     size_t dict_used = 0;
     std::vector<uint8_t> word_arena;   // 8-aligned, zero-padded words
     std::vector<uint32_t> word_off;
+    // word heat: floor(log2(1 + trie nodes a word labels)), the tail order's
+    // per-level cost estimate (a word on many edges leads into many filters)
+    std::vector<uint32_t> word_nodes;
+    std::vector<uint8_t> word_heat;
+    uint64_t heat_version = 0;
+    void heat_bump(uint32_t w, int d) {
+        if (w >= word_nodes.size()) return;
+        word_nodes[w] = (uint32_t)((int64_t)word_nodes[w] + d);
+        const uint32_t x = word_nodes[w] + 1;
+        const uint8_t h = (uint8_t)(31 - __builtin_clz(x));
+        if (h != word_heat[w]) {
+            word_heat[w] = h;
+            ++heat_version;
+        }
+    }
     Dirty dict_dirty;
 
     // ---- trie mirror / image ----
@@ -669,6 +686,9 @@ struct tm_engine {
         word_arena.resize(off + padded, 0);
         if (len) std::memcpy(&word_arena[off], p, len);
         word_off.push_back((uint32_t)off);
+        word_nodes.push_back(0);
+        word_heat.push_back(0);
+        ++heat_version;
         if ((dict_used + 1) * 2 > dict.size()) dict_grow();
         dict_place(h, id, len);
         ++dict_used;
@@ -808,6 +828,7 @@ struct tm_engine {
         }
         nodes[id] = empty_node();
         aux[id] = NodeAux{parent, word, 0, 0, (uint16_t)SUM_NONE, (uint16_t)SUM_NONE};
+        if (word < WORD_MAX) heat_bump(word, +1);
         node_dirty.mark(id);
         ++live_nodes;
         ++created_since_layout;
@@ -908,6 +929,7 @@ struct tm_engine {
         }
         aux[v].edge_count--;
         touched(v);
+        if (w < WORD_MAX) heat_bump(w, -1);
         nodes[c] = empty_node();
         aux[c] = NodeAux{NODE_NONE, 0, 0, 0, (uint16_t)SUM_NONE, (uint16_t)SUM_NONE};
         node_dirty.mark(c);
@@ -1702,6 +1724,8 @@ struct tm_engine {
         im.word_arena = g.d_arena.as<const uint8_t>();
         im.word_off = g.d_woff.as<const uint32_t>();
         im.fshape = shape_keys ? g.d_fshape.as<const uint64_t>() : nullptr;
+        im.word_heat = g.d_wheat.as<const uint8_t>();
+        im.n_words = (uint32_t)word_heat.size();
         return im;
     }
 
@@ -1825,6 +1849,13 @@ struct tm_engine {
                     HIPCHK(hipMemcpyAsync(g.d_woff.as<uint32_t>() + from, word_off.data() + from,
                                           (word_off.size() - from) * 4, hipMemcpyHostToDevice, d.ustream));
                 g.woff_uploaded = word_off.size();
+            }
+            if (g.heat_uploaded != heat_version) {   // small: the whole table
+                g.d_wheat.ensure_async(std::max<size_t>(word_heat.size(), 1) + 16, d.ustream);
+                if (!word_heat.empty())
+                    HIPCHK(hipMemcpyAsync(g.d_wheat.p, word_heat.data(), word_heat.size(), hipMemcpyHostToDevice,
+                                          d.ustream));
+                g.heat_uploaded = heat_version;
             }
             g.split_stale = true;
             if (split_halves) split_image(d, g);
@@ -2009,11 +2040,13 @@ struct tm_engine {
         qb.stage = w.stage.as<uint32_t>();
         qb.kstage = kw ? w.kstage.as<uint64_t>() : nullptr;
         qb.shaped = shaped;
-        qb.wave_walk = n <= wave_walk_max && !kw && !presort;
+        // the tail order (presort 2) leaves small batches to the wave walk
+        qb.wave_walk = n <= wave_walk_max && !kw && presort != 1;
         qb.chunk_rows = chunk_rows;
         qb.scan_tmp = w.scan.as<uint64_t>();
         qb.ws = w.ws.as<unsigned long long>();
-        qb.perm = presort && !shaped ? w.perm.as<uint32_t>() : nullptr;
+        qb.perm = presort && !shaped && !(qb.wave_walk && presort == 2) ? w.perm.as<uint32_t>() : nullptr;
+        qb.presort_mode = presort == 2 ? 2u : 1u;
         if (presort) {
             qb.sort_keys = w.skeys.as<uint32_t>();
             qb.sort_vals = w.svals.as<uint32_t>();
@@ -3374,8 +3407,8 @@ int tm_set_option(tm_engine* e, const char* name, int64_t value) {
             e->layout_mode = (int)value;
             return TM_OK;
         }
-        if (!std::strcmp(name, "presort")) {
-            if (value < 0 || value > 1) return TM_EINVAL;
+        if (!std::strcmp(name, "presort")) {   // 0 arrival order, 1 word-hash key, 2 the tail order
+            if (value < 0 || value > 2) return TM_EINVAL;
             e->presort = (int)value;
             return TM_OK;
         }

@@ -129,6 +129,8 @@ struct ImageView {
     const uint8_t*  word_arena;
     const uint32_t* word_off;          // word id -> arena offset
     const uint64_t* fshape;            // filter id -> order key (filter_shape), or null (option "shape_keys" off)
+    const uint8_t*  word_heat;         // word id -> floor(log2(1 + nodes it labels)) (presort mode 2)
+    uint32_t        n_words;
 };
 
 

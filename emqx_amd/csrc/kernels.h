@@ -39,6 +39,8 @@ struct QueueBufs {
     uint64_t* scan_tmp;   // scan_tmp_elems(n)
     unsigned long long* ws;   // QWS_BYTES of queue heads
     uint32_t* perm;       // option "presort": queue position -> topic (n), or null (arrival order)
+    uint32_t presort_mode = 1;   // 1: key of the first eight words (4 radix passes); 2: the tail order
+                                 // (kernels.hip tail_key: heavy topics first in each XCD range, 1 pass)
     // option "presort": the batch walked in the order of a 32-bit key of
     // its first eight words (each hashed, level-major: 6,5,5,4,4,3,3,2 bits),
     // so a wave's 64 lanes walk shared prefixes -- their loads of one node

@@ -243,12 +243,33 @@ __device__ __forceinline__ uint32_t presort_key(const uint32_t (&tw)[WREG], uint
     return k;
 }
 
+// option "presort" 2, the tail order: within each of the walk's 8 XCD ranges
+// (QRANGES, by topic index), the topics whose words label the most trie
+// nodes first -- they lead into the most filters and take the longest walks,
+// so the lanes that finish last are the ones on light topics.  Key: the
+// range (3 bits) over 31 - the summed heat of the first eight levels / 4
+// (5 bits), one radix pass (presort.hip).
+__device__ __forceinline__ uint32_t tail_key(const ImageView& im, const uint32_t (&tw)[WREG], uint32_t lev,
+                                             uint32_t t, uint32_t n) {
+    uint32_t cost = 0;
+#pragma unroll
+    for (uint32_t l = 0; l < 8; ++l) {
+        const uint32_t w = tw[l];
+        if (l < lev && w < im.n_words) cost += im.word_heat[w];
+    }
+    uint32_t r = (uint32_t)(((uint64_t)t * 8) / n);   // range r = [n r / 8, n (r+1) / 8)
+    while (r > 0 && (uint64_t)n * r / 8 > t) --r;
+    while (r < 7 && (uint64_t)n * (r + 1) / 8 <= t) ++r;
+    const uint32_t c = cost >> 2 < 31 ? cost >> 2 : 31u;
+    return (r << 5) | (31u - c);
+}
+
 template <class B>
 __device__ __forceinline__ void tokenize_one(const ImageView& im, const B& bytes,
-                                             const uint64_t* __restrict__ off, uint32_t t,
+                                             const uint64_t* __restrict__ off, uint32_t t, uint32_t n,
                                              uint32_t* __restrict__ twords, uint32_t* __restrict__ words,
                                              uint32_t* __restrict__ meta, uint32_t* __restrict__ skeys,
-                                             uint32_t* __restrict__ svals) {
+                                             uint32_t* __restrict__ svals, uint32_t key_mode) {
     const uint64_t b = off[t], e = off[t + 1];
     uint32_t tw[WREG];
 #pragma unroll
@@ -265,7 +286,7 @@ __device__ __forceinline__ void tokenize_one(const ImageView& im, const B& bytes
     const uint32_t dollar = (e > b && bytes.byte(b) == '$') ? 1u : 0u;
     meta[t] = lev | (dollar << 31) | (lev > WREG ? MLONG : 0u) | (ood ? MOOD : 0u);
     if (skeys) {   // option "presort": the walk-order key (presort.hip)
-        skeys[t] = presort_key(tw, lev);
+        skeys[t] = key_mode == 2 ? tail_key(im, tw, lev, t, n) : presort_key(tw, lev);
         svals[t] = t;
     }
 }
@@ -273,10 +294,10 @@ __device__ __forceinline__ void tokenize_one(const ImageView& im, const B& bytes
 __global__ void __launch_bounds__(BLOCK)
 tm_tokenize(ImageView im, const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint32_t n,
             uint32_t* __restrict__ twords, uint32_t* __restrict__ words, uint32_t* __restrict__ meta,
-            uint32_t* __restrict__ skeys, uint32_t* __restrict__ svals) {
+            uint32_t* __restrict__ skeys, uint32_t* __restrict__ svals, uint32_t key_mode) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (TM_TOK_LEAN) {
-        if (t < n) tokenize_one(im, GlobalBytes{bytes}, off, t, twords, words, meta, skeys, svals);
+        if (t < n) tokenize_one(im, GlobalBytes{bytes}, off, t, n, twords, words, meta, skeys, svals, key_mode);
         return;
     }
     __shared__ uint64_t win[BLOCK / 64][TOK_WIN_WORDS];
@@ -299,9 +320,9 @@ tm_tokenize(ImageView im, const uint8_t* __restrict__ bytes, const uint64_t* __r
     __syncthreads();
     if (t < n) {
         if (lds)
-            tokenize_one(im, LdsBytes{win[wv], wbase}, off, t, twords, words, meta, skeys, svals);
+            tokenize_one(im, LdsBytes{win[wv], wbase}, off, t, n, twords, words, meta, skeys, svals, key_mode);
         else
-            tokenize_one(im, GlobalBytes{bytes}, off, t, twords, words, meta, skeys, svals);
+            tokenize_one(im, GlobalBytes{bytes}, off, t, n, twords, words, meta, skeys, svals, key_mode);
     }
 }
 
@@ -1656,8 +1677,12 @@ hipError_t launch_queue(bool stats_mode, bool xcdq, const ImageView& im, const u
     const int ch = (lane_walk && !keys && !stats_mode && qb.chunk_rows) ? CH_ROWS : CH_NONE;
     const bool by_pos = queue_rows_by_position(qb, stats_mode);   // presorted without chunk rows
     mark(0);
+    // presort keys / values where launch_presort's first pass reads them (the
+    // tail order's single pass reads the second halves and ends in perm)
+    const bool tail = qb.presort_mode == 2;
     hipLaunchKernelGGL(tm_tokenize, g, blk, 0, st, im, bytes, off, n, qb.twords, qb.words, qb.meta,
-                       qb.perm ? qb.sort_keys : nullptr, qb.perm ? qb.perm : nullptr);
+                       qb.perm ? qb.sort_keys + (tail ? n : 0u) : nullptr,
+                       qb.perm ? (tail ? qb.sort_vals : qb.perm) : nullptr, qb.presort_mode);
     if (qb.perm) {   // option "presort": perm (and the rows in walk order unless chunk rows read them by perm)
         err = launch_presort(qb.twords, qb.meta, n, qb, st, by_pos);
         if (err != hipSuccess) return err;

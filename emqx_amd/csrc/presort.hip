@@ -126,7 +126,15 @@ hipError_t launch_presort(const uint32_t* twords, const uint32_t* meta, uint32_t
     // four passes end in A, so perm holds the order
     // (the tokenizer wrote the keys and values t: kernels.hip presort_key)
     uint32_t *ka = qb.sort_keys, *kb = qb.sort_keys + n, *va = qb.perm, *vb = qb.sort_vals;
-    for (uint32_t pass = 0; pass < 4; ++pass) {
+    uint32_t passes = 4;
+    if (qb.presort_mode == 2) {   // the tail order: one pass of an 8-bit key, B -> A (perm)
+        ka = qb.sort_keys + n;
+        kb = qb.sort_keys;
+        va = qb.sort_vals;
+        vb = qb.perm;
+        passes = 1;
+    }
+    for (uint32_t pass = 0; pass < passes; ++pass) {
         const uint32_t shift = 8 * pass;
         hipLaunchKernelGGL(tm_presort_count, dim3(tiles), dim3(PS_BLOCK), 0, st, ka, n, shift, qb.sort_counts);
         hipError_t err = launch_scan(qb.sort_counts, nc, qb.sort_off, qb.sort_off + nc, qb.sort_scan, st);

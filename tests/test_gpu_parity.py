@@ -248,7 +248,10 @@ VARIANTS = {"queue": {}, "queue_xcd": {}, "queue_xcd@nosplit@dfs": {"split": 0, 
             # chunk rows in LDS (option chunk_rows): copied from the tokenizer's rows, or tokenized by the walk
             "queue_xcd@norows": {"chunk_rows": 0}, "queue@norows@nospill": {"chunk_rows": 0, "spill": 0},
             "queue_xcd@rows@stagek8@nosummaries": {"stage_k": 8, "summaries": 0},
-            "queue_xcd@rows@presort": {"presort": 1}}
+            "queue_xcd@rows@presort": {"presort": 1},
+            # the tail order (presort 2: heavy topics first in each XCD range, one radix pass)
+            "queue_xcd@tail": {"presort": 2}, "queue@tail@stagek8": {"presort": 2, "stage_k": 8},
+            "queue_xcd@tail@norows@nospill": {"presort": 2, "chunk_rows": 0, "spill": 0}}
 
 
 @pytest.mark.parametrize("variant", list(VARIANTS))
