@@ -1610,8 +1610,46 @@ hipError_t launch_scatter(void* table, const uint32_t* pkt, uint64_t n, uint32_t
 
 size_t scan_tmp_elems(uint32_t n) { return div_up(n ? n : 1, SCAN_TILE); }
 
+// a small batch's scan in one launch: one block over the tiles in turn,
+// carrying the running total (a small batch's time is per-launch latency)
+__global__ void __launch_bounds__(BLOCK)
+tm_scan_single(const uint32_t* __restrict__ in, uint32_t n, uint64_t* __restrict__ out_off,
+               uint64_t* __restrict__ total) {
+    __shared__ uint64_t lds[BLOCK / 64];
+    uint64_t carry = 0;
+    for (uint64_t t0 = 0; t0 < n; t0 += SCAN_TILE) {
+        const uint64_t base = t0 + (uint64_t)threadIdx.x * SCAN_ITEMS;
+        uint32_t v[SCAN_ITEMS];
+        uint64_t s = 0;
+#pragma unroll
+        for (int i = 0; i < SCAN_ITEMS; ++i) {
+            const uint64_t k = base + i;
+            v[i] = k < n ? in[k] : 0;
+            s += v[i];
+        }
+        uint64_t tot;
+        uint64_t ex = block_exclusive_scan(s, lds, tot) + carry;
+#pragma unroll
+        for (int i = 0; i < SCAN_ITEMS; ++i) {
+            const uint64_t k = base + i;
+            if (k < n) out_off[k] = ex;
+            ex += v[i];
+        }
+        carry += tot;
+    }
+    if (threadIdx.x == 0) {
+        out_off[n] = carry;
+        *total = carry;
+    }
+}
+constexpr uint32_t SCAN_SINGLE_MAX = 32768;   // batches up to this size scan in one launch
+
 hipError_t launch_scan(const uint32_t* counts, uint32_t n, uint64_t* out_off, uint64_t* total, uint64_t* tmp,
                        hipStream_t st) {
+    if (n <= SCAN_SINGLE_MAX) {
+        hipLaunchKernelGGL(tm_scan_single, dim3(1), dim3(BLOCK), 0, st, counts, n, out_off, total);
+        return hipGetLastError();
+    }
     uint32_t tiles = div_up(n, SCAN_TILE);
     hipLaunchKernelGGL(tm_scan_reduce, dim3(tiles), dim3(BLOCK), 0, st, counts, n, tmp);
     hipLaunchKernelGGL(tm_scan_tiles, dim3(1), dim3(BLOCK), 0, st, tmp, tiles);
