@@ -629,10 +629,13 @@ int  tm_rewrite_match_batch_device(tm_rewrite* r, const uint8_t* d_topics, const
  *   "hot_levels" depths laid out level by level first at relayout (0..16,
  *              default 4; 0 = DFS preorder throughout); forces a relayout
  *   "presort"  1 = walk each batch in the order of a key of its first words
- *              (device radix sort; default 0); 2 = the tail order: within
- *              each XCD range the topics whose words label the most trie
- *              nodes first (one radix pass), so the walk's last lanes finish
- *              on light topics (batches above wave_walk_max)
+ *              (device radix sort); 2 = the tail order: within each XCD
+ *              range the topics whose words label the most trie nodes first
+ *              (one radix pass), so the walk's last lanes finish on light
+ *              topics (batches above wave_walk_max); 3 = the tail order for
+ *              batches of at most "tail_max" topics, arrival order above
+ *              (default); 0 = arrival order
+ *   "tail_max" presort 3's largest tail-ordered batch (default 2097152)
  *   "chunk_rows" 1 = a wave copies each taken chunk's 64 tokenized rows to
  *              LDS at once (default), 0 = each lane reads its topic's row
  *   "spill"    1 = ids past a stage row go to per-XCD spill chunks (default),

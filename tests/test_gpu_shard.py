@@ -95,15 +95,16 @@ def test_sharded_c1_equals_o1(gpu_device, S):
     assert got == _o1(filters, topics)
 
 
-@pytest.mark.parametrize("S", [1, 3])
-def test_sharded_presorted_walk_equals_o1(gpu_device, S):
-    """option presort on the keyed walk: stage rows in walk order, keys and
-    ids copied out by position (tm_copy_out_sorted<KEYS>), merged by key;
-    with a small stage row, so topics past K re-walk their heads"""
+@pytest.mark.parametrize("S,presort", [(1, 1), (3, 1), (3, 2)])
+def test_sharded_presorted_walk_equals_o1(gpu_device, S, presort):
+    """option presort (1 word-hash key, 2 the tail order) on the keyed walk:
+    stage rows in walk order, keys and ids copied out by position
+    (tm_copy_out_sorted<KEYS>), merged by key; with a small stage row, so
+    topics past K re-walk their heads"""
     from emqx_amd import workload as W
     filters = W.unpack(*W.filters(1))
     topics = W.unpack(*W.topics(1, n=20000))
-    got = _run_sharded(filters, topics, S, K=16, opts={"presort": 1, "stage_auto": 0, "shape_keys": 0})
+    got = _run_sharded(filters, topics, S, K=16, opts={"presort": presort, "stage_auto": 0, "shape_keys": 0})
     assert got == _o1(filters, topics)
 
 
