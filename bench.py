@@ -702,7 +702,7 @@ def host_legs(a, eng, batch, total):
                                          ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                          ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_double)]
         k = n   # the whole batch, after a warm-up run inside the driver
-        res = (ctypes.c_double * 12)()
+        res = (ctypes.c_double * 14)()
         bc = BATCHER
         rc = drv.tm_bench_batcher(eng.h, tb.ctypes.data, to.ctypes.data, k, bc["producers"], bc["deadline_us"],
                                   bc["max_topics"], bc["lanes_per_replica"], 0, bc["callback_threads"], res)
@@ -710,7 +710,8 @@ def host_legs(a, eng, batch, total):
             out["batcher"] = dict(bc, topics_per_s=res[1], topics=k, batches=int(res[2]), mean_batch=res[3],
                                   lat_us_p50=res[4], lat_us_p99=res[5], failed=int(res[6]), matches=int(res[7]),
                                   per_batch_us={"sealed_to_lane": res[8], "pack": res[9], "device": res[10],
-                                                "callbacks": res[11]},
+                                                "callbacks": res[11], "device_launch": res[12],
+                                                "device_wait": res[13]},
                                   path="tm_batcher_submit per publish from %d threads, per-topic callbacks "
                                        "(NIF path), PCIe both ways included" % bc["producers"])
             log("batcher: %.0f topics/s, mean batch %.0f, p50 %.0f us, p99 %.0f us" % (res[1], res[3], res[4],

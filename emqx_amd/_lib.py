@@ -46,7 +46,7 @@ class TmBatcherConfig(ctypes.Structure):
 class TmBatcherStats(ctypes.Structure):
     _fields_ = [(k, ctypes.c_uint64) for k in ("batches", "topics", "results", "max_batch", "size_seals",
                                                "deadline_seals", "failed_batches", "wait_ns", "pack_ns",
-                                               "device_ns", "callback_ns")]
+                                               "device_ns", "callback_ns", "launch_ns", "sync_ns")]
 
 
 class TmExchangeIn(ctypes.Structure):
@@ -301,3 +301,19 @@ def hip_memcpy_d2h(dst, src, nbytes, device):
     lib.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
     if lib.hipSetDevice(device) != 0 or lib.hipMemcpy(dst, src, nbytes, 2) != 0:   # hipMemcpyDeviceToHost
         raise TopicMatchError(TM_EDEVICE, "hipMemcpy device -> host")
+
+
+def stream_handle(stream):
+    """The HIP stream handle of `stream` (a torch stream, an int handle or
+    None).  A torch stream first waits for the work already queued on its
+    device's current stream -- the fills and copies of the tensors the caller
+    just made for this call: torch's side streams are non-blocking, so
+    without the wait a zero-fill of an output total could land after the
+    engine has written it."""
+    if stream is None or isinstance(stream, int):
+        return stream
+    import torch
+    cur = torch.cuda.current_stream(stream.device)
+    if cur.cuda_stream != stream.cuda_stream:
+        stream.wait_stream(cur)
+    return stream.cuda_stream

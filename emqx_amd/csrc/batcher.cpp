@@ -153,7 +153,11 @@ struct Lane {
     const uint32_t* r_dst = nullptr;
     double ids_per_topic = 64.0;      // sizing estimate of the device result buffers
     clk::time_point sealed;           // when the batch was handed over
+    uint64_t launch_ns = 0, sync_ns = 0;   // this batch: host time enqueueing the device work, waiting on it
 };
+inline uint64_t ns_since(clk::time_point a) {
+    return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(clk::now() - a).count();
+}
 
 std::atomic<uint32_t> g_stripe_rr{0};
 thread_local int t_stripe = -1;
@@ -343,9 +347,11 @@ struct tm_batcher {
         const uint64_t cntb = ((uint64_t)n * 4 + 7) & ~7ull;
         if (!L.d_io.ensure(offb + nbytes + 16)) return TM_ENOMEM;
         hipStream_t s = L.stream;
+        clk::time_point t0 = clk::now();
         if (!chk(hipMemcpyAsync(L.d_io.p, L.h_io.p, offb + nbytes + 8, hipMemcpyHostToDevice, s))) return TM_EDEVICE;
         uint64_t cap = (uint64_t)(L.ids_per_topic * n * 1.25) + 1024;
         for (int pass = 0; pass < 2; ++pass) {
+            if (pass) t0 = clk::now();
             const uint64_t outb = 8 + offb + cntb + cap * 4;
             if (!L.d_out.ensure(outb) || !L.h_out.ensure(outb)) return TM_ENOMEM;
             uint8_t* d = (uint8_t*)L.d_out.p;
@@ -353,9 +359,11 @@ struct tm_batcher {
                                            (uint32_t*)(d + 8 + offb), (uint64_t*)(d + 8), (uint32_t*)(d + 8 + offb + cntb),
                                            cap, (uint64_t*)d, s);
             if (rc != TM_OK) return rc;
-            if (!chk(hipMemcpyAsync(L.h_out.p, L.d_out.p, outb, hipMemcpyDeviceToHost, s)) ||
-                !chk(hipStreamSynchronize(s)))
-                return TM_EDEVICE;
+            if (!chk(hipMemcpyAsync(L.h_out.p, L.d_out.p, outb, hipMemcpyDeviceToHost, s))) return TM_EDEVICE;
+            L.launch_ns += ns_since(t0);
+            t0 = clk::now();
+            if (!chk(hipStreamSynchronize(s))) return TM_EDEVICE;
+            L.sync_ns += ns_since(t0);
             const uint8_t* h = (const uint8_t*)L.h_out.p;
             total = *(const uint64_t*)h;
             L.ids_per_topic = 0.9 * L.ids_per_topic + 0.1 * ((double)total / n);
@@ -382,11 +390,13 @@ struct tm_batcher {
             !L.h_outoff.ensure((n + 1) * 8) || !L.h_total.ensure(64))
             return TM_ENOMEM;
         hipStream_t s = L.stream;
+        clk::time_point t0 = clk::now();
         if (!chk(hipMemcpyAsync(L.d_bytes.p, L.h_bytes.p, nbytes, hipMemcpyHostToDevice, s)) ||
             !chk(hipMemcpyAsync(L.d_off.p, L.h_off.p, (n + 1) * 8, hipMemcpyHostToDevice, s)))
             return TM_EDEVICE;
         uint64_t cap = (uint64_t)(L.ids_per_topic * n * 1.25) + 1024;
         for (int pass = 0; pass < 2; ++pass) {
+            if (pass) t0 = clk::now();
             if (!L.d_src.ensure(cap * 4) || (routes && !L.d_dest.ensure(cap * 4))) return TM_ENOMEM;
             int rc = deliv ? tm_match_deliveries_batch_device(eng, (const uint8_t*)L.d_bytes.p, (const uint64_t*)L.d_off.p,
                                                               n, nbytes, (uint32_t*)L.d_counts.p, (uint64_t*)L.d_outoff.p,
@@ -410,9 +420,12 @@ struct tm_batcher {
                 !chk(hipMemcpyAsync(L.h_counts.p, L.d_counts.p, n * 4, hipMemcpyDeviceToHost, s)) ||
                 !chk(hipMemcpyAsync(L.h_outoff.p, L.d_outoff.p, (n + 1) * 8, hipMemcpyDeviceToHost, s)) ||
                 (eager && !chk(hipMemcpyAsync(L.h_src.p, L.d_src.p, cap * 4, hipMemcpyDeviceToHost, s))) ||
-                (eager && routes && !chk(hipMemcpyAsync(L.h_dest.p, L.d_dest.p, cap * 4, hipMemcpyDeviceToHost, s))) ||
-                !chk(hipStreamSynchronize(s)))
+                (eager && routes && !chk(hipMemcpyAsync(L.h_dest.p, L.d_dest.p, cap * 4, hipMemcpyDeviceToHost, s))))
                 return TM_EDEVICE;
+            L.launch_ns += ns_since(t0);
+            t0 = clk::now();
+            if (!chk(hipStreamSynchronize(s))) return TM_EDEVICE;
+            L.sync_ns += ns_since(t0);
             total = *(const uint64_t*)L.h_total.p;
             L.ids_per_topic = 0.9 * L.ids_per_topic + 0.1 * ((double)total / n);
             if (total <= cap) {
@@ -428,10 +441,12 @@ struct tm_batcher {
             cap = total + total / 4 + 1024;   // overflow: rerun with room (rare)
         }
         if (!L.h_src.ensure(total * 4 + 4) || (routes && !L.h_dest.ensure(total * 4 + 4))) return TM_ENOMEM;
+        t0 = clk::now();
         if ((total && !chk(hipMemcpyAsync(L.h_src.p, L.d_src.p, total * 4, hipMemcpyDeviceToHost, s))) ||
             (total && routes && !chk(hipMemcpyAsync(L.h_dest.p, L.d_dest.p, total * 4, hipMemcpyDeviceToHost, s))) ||
             !chk(hipStreamSynchronize(s)))
             return TM_EDEVICE;
+        L.sync_ns += ns_since(t0);
         L.r_counts = (const uint32_t*)L.h_counts.p;
         L.r_off = (const uint64_t*)L.h_outoff.p;
         L.r_src = (const uint32_t*)L.h_src.p;
@@ -519,6 +534,7 @@ struct tm_batcher {
             }
             const uint32_t n = L.n;
             uint64_t total = 0, results = 0;
+            L.launch_ns = L.sync_ns = 0;
             const clk::time_point t_start = clk::now();
             clk::time_point t_packed = t_start, t_dev = t_start;
             int rc = host_only ? TM_EDEVICE : TM_OK;   // host-only: the GPU path only
@@ -549,6 +565,8 @@ struct tm_batcher {
             st.pack_ns += ns(t_packed - t_start);
             st.device_ns += ns(t_dev - t_packed);
             st.callback_ns += ns(t_cb - t_dev);
+            st.launch_ns += L.launch_ns;
+            st.sync_ns += L.sync_ns;
             st.batches++;
             st.topics += m;
             if (m > st.max_batch) st.max_batch = m;

@@ -245,6 +245,7 @@ struct Image {
     DevBuf d_wheat;    // word id -> heat (option "presort" 2: the tail order's cost estimate)
     size_t arena_uploaded = 0, woff_uploaded = 0;
     uint64_t heat_uploaded = ~0ull;   // word_heat version in d_wheat
+    uint32_t heat_words = 0;          // words in d_wheat (the host table may have grown since)
     bool split_stale = true, written = false;
     uint64_t epoch = 0;
     std::vector<hipEvent_t> uses;
@@ -1727,7 +1728,7 @@ struct tm_engine {
         im.word_off = g.d_woff.as<const uint32_t>();
         im.fshape = shape_keys ? g.d_fshape.as<const uint64_t>() : nullptr;
         im.word_heat = g.d_wheat.as<const uint8_t>();
-        im.n_words = (uint32_t)word_heat.size();
+        im.n_words = g.heat_words;
         return im;
     }
 
@@ -1858,6 +1859,7 @@ struct tm_engine {
                     HIPCHK(hipMemcpyAsync(g.d_wheat.p, word_heat.data(), word_heat.size(), hipMemcpyHostToDevice,
                                           d.ustream));
                 g.heat_uploaded = heat_version;
+                g.heat_words = (uint32_t)word_heat.size();
             }
             g.split_stale = true;
             if (split_halves) split_image(d, g);

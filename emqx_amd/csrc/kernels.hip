@@ -420,6 +420,9 @@ __device__ __forceinline__ uint4 load_half(const ImageView& im, uint32_t v, bool
     if (TM_NT_LEVEL > 0 && (leaf || r >= (uint32_t)TM_NT_LEVEL)) return nt_load16(p);
     return *p;
 }
+#ifndef TM_STAGE_PAIR
+#define TM_STAGE_PAIR 1
+#endif
 __device__ __forceinline__ void store_stage(uint32_t* p, uint4 x) {
     if (TM_NT_STAGE) nt_store16(p, x);
     else *reinterpret_cast<uint4*>(p) = x;
@@ -714,8 +717,12 @@ __device__ __forceinline__ void walk(const ImageView& im, uint32_t n, bool dolla
     }
 }
 
-// discovery k of a topic goes to stage row slot K-1-k (k < K), 4 ids per
-// 16 B store; the row's last `count` slots are then the output in order.
+// discovery k of a topic goes to stage row slot K-1-k (k < K); the row's
+// last `count` slots are then the output in order.  TM_STAGE_PAIR: 8 ids
+// per pair of back-to-back 16 B stores (one 32 B sector, so the L2 writes
+// one whole sector to HBM instead of two half-filled ones: round 3's walk
+// wrote 2.2x its id bytes); 0: one 16 B store per 4 ids.
+// A row whose K is not a multiple of 8 stores its last 4 slots alone.
 // KEYS: key word 0 to the same slot of the topic's key row; words j >= 1
 // (KW > 1) to key plane j, kplane u64 further on.
 template <bool KEYS>
@@ -723,7 +730,8 @@ struct RowEmit {
     uint32_t* row;
     uint64_t* krow;
     uint32_t K, cnt;
-    uint4 buf;
+    uint4 buf;     // slots K-4-g .. K-1-g of the current group g
+    uint4 buf2;    // TM_STAGE_PAIR: slots K-8-g .. K-5-g
     uint64_t kb;   // KEYS: key of the last even discovery, stored with the next one (16 B)
     uint32_t KW;
     uint64_t kplane;
@@ -744,7 +752,23 @@ struct RowEmit {
             }
             for (uint32_t j = 1; j < KW; ++j) krow[j * kplane + K - 1 - cnt] = key_word(path, j, r, sym);
         }
-        if (cnt < K) {
+        if (cnt < K && TM_STAGE_PAIR) {
+            const uint32_t s = cnt & 7u, g = cnt & ~7u;
+            buf.w = s == 0 ? f : buf.w;
+            buf.z = s == 1 ? f : buf.z;
+            buf.y = s == 2 ? f : buf.y;
+            buf.x = s == 3 ? f : buf.x;
+            buf2.w = s == 4 ? f : buf2.w;
+            buf2.z = s == 5 ? f : buf2.z;
+            buf2.y = s == 6 ? f : buf2.y;
+            buf2.x = s == 7 ? f : buf2.x;
+            if (s == 7) {
+                store_stage(row + K - 8 - g, buf2);
+                store_stage(row + K - 4 - g, buf);
+            } else if (s == 3 && g + 8 > K) {   // K % 8 == 4: the row's last 4 slots
+                store_stage(row + K - 4 - g, buf);
+            }
+        } else if (cnt < K) {
             const uint32_t s = cnt & 3u;
             buf.w = s == 0 ? f : buf.w;
             buf.z = s == 1 ? f : buf.z;
@@ -768,7 +792,15 @@ struct RowEmit {
         ++cnt;
     }
     __device__ __forceinline__ void flush() {
-        if ((cnt & 3u) && cnt < K) store_stage(row + K - 4 - (cnt & ~3u), buf);
+        if (TM_STAGE_PAIR) {
+            const uint32_t s = cnt & 7u, g = cnt & ~7u;
+            if (s && cnt < K) {   // s <= 4: the first quad of the group only (s == 4 with K % 8 == 4 is stored)
+                if (s > 4) store_stage(row + K - 8 - g, buf2);
+                store_stage(row + K - 4 - g, buf);
+            }
+        } else if ((cnt & 3u) && cnt < K) {
+            store_stage(row + K - 4 - (cnt & ~3u), buf);
+        }
         if (KEYS && (cnt & 1u) && cnt <= K) krow[K - cnt] = kb;   // the unpaired last even discovery
     }
 };
@@ -880,7 +912,7 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
     uint32_t my = NO_TOPIC, myt = 0;   // the lane's queue position and its topic
     bool is_long = false, drained = false;
     Cursor cur;
-    RowEmit<KEYS> em{nullptr, nullptr, K, 0, make_uint4(0, 0, 0, 0), 0ull, KW, (uint64_t)n * K};
+    RowEmit<KEYS> em{nullptr, nullptr, K, 0, make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0), 0ull, KW, (uint64_t)n * K};
     if (!KEYS && spill) {   // this XCD's spill area and counter (placement only: any XCD id is valid)
         const uint32_t x = xcc_id();
         em.spill = spill;
@@ -1240,7 +1272,7 @@ tm_walk_wave(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const u
             // beyond the wave's capacity: the per-lane walk, on one lane
             const uint64_t b = off[t] - off[0];
             const MemWords mw{row, words + b + t};
-            RowEmit<false> em{srow, nullptr, K, 0, make_uint4(0, 0, 0, 0), 0ull, 1u, 0ull};
+            RowEmit<false> em{srow, nullptr, K, 0, make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0), 0ull, 1u, 0ull};
             WalkStats s2;
             walk<false, false>(im, nl, dollar, GlobalPath{gpath + b + 2ull * t}, mw, em, s2);
             em.flush();

@@ -141,7 +141,7 @@ class AclRules:
         P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
         st = None
         if stream is not None:
-            st = ctypes.c_void_p(stream if isinstance(stream, int) else stream.cuda_stream)
+            st = ctypes.c_void_p(L.stream_handle(stream))
         self._ck(self.lib.tm_acl_check_batch_device(self.h, n, *[P(d[k]) for k in self.ARGS], P(d_out), P(d_rule),
                                                     st), "tm_acl_check_batch_device")
 

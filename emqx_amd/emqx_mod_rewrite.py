@@ -66,7 +66,7 @@ class Rewrite:
     def rule_index_device(self, d_topics, d_off, n, d_out, stream=None):
         def p(x):
             return None if x is None else ctypes.c_void_p(x.data_ptr() if hasattr(x, "data_ptr") else int(x))
-        st = None if stream is None else ctypes.c_void_p(stream if isinstance(stream, int) else stream.cuda_stream)
+        st = None if stream is None else ctypes.c_void_p(L.stream_handle(stream))
         rc = self.lib.tm_rewrite_match_batch_device(self.h, p(d_topics), p(d_off), n, p(d_out), st)
         if rc != L.TM_OK:
             raise L.TopicMatchError(rc, "tm_rewrite_match_batch_device")

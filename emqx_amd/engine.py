@@ -221,7 +221,7 @@ class Engine:
             return ctypes.c_void_p(int(x))
         st = None
         if stream is not None:
-            st = ctypes.c_void_p(stream if isinstance(stream, int) else stream.cuda_stream)
+            st = ctypes.c_void_p(L.stream_handle(stream))
         rc = self.lib.tm_match_batch_device(self.h, p(d_bytes), p(d_off), n, topic_bytes, p(d_counts), p(d_offs),
                                             p(d_ids), out_cap, p(d_total), st)
         return self._check(rc, "tm_match_batch_device")
@@ -331,7 +331,7 @@ class Engine:
             return ctypes.c_void_p(x.data_ptr() if hasattr(x, "data_ptr") else int(x))
         st = None
         if stream is not None:
-            st = ctypes.c_void_p(stream if isinstance(stream, int) else stream.cuda_stream)
+            st = ctypes.c_void_p(L.stream_handle(stream))
         rc = self.lib.tm_match_routes_batch_device(self.h, p(d_bytes), p(d_off), n, topic_bytes, p(d_counts),
                                                    p(d_offs), p(d_src), p(d_dest), out_cap, p(d_total), st)
         return self._check(rc, "tm_match_routes_batch_device")
@@ -391,7 +391,7 @@ class Engine:
             return ctypes.c_void_p(x.data_ptr() if hasattr(x, "data_ptr") else int(x))
         st = None
         if stream is not None:
-            st = ctypes.c_void_p(stream if isinstance(stream, int) else stream.cuda_stream)
+            st = ctypes.c_void_p(L.stream_handle(stream))
         rc = self.lib.tm_match_deliveries_batch_device(self.h, p(d_bytes), p(d_off), n, topic_bytes, p(d_counts),
                                                        p(d_offs), p(d_to), p(d_target), out_cap, p(d_total), st)
         return self._check(rc, "tm_match_deliveries_batch_device")

@@ -114,7 +114,7 @@ class ShardEngine(Engine):
                           stream=None, key_words=1):
         """keyed walk; d_keys holds key_words planes of out_cap u64 (word j of
         id i at d_keys[j * out_cap + i])"""
-        st = None if stream is None else ctypes.c_void_p(stream if isinstance(stream, int) else stream.cuda_stream)
+        st = None if stream is None else ctypes.c_void_p(L.stream_handle(stream))
         rc = self.lib.tm_match_batch_device_keys_w(self.h, _p(d_bytes), _p(d_off), n, topic_bytes, _p(d_counts),
                                                    _p(d_offs), _p(d_ids), _p(d_keys), key_words, out_cap,
                                                    _p(d_total), st)
@@ -128,7 +128,7 @@ class ShardEngine(Engine):
 
     def merge_device(self, m, d_counts, d_src_base, d_ids, d_keys, d_out_count, d_out_off, d_out_gid, out_cap,
                      d_total, stream=None, key_words=1, key_stride=0):
-        st = None if stream is None else ctypes.c_void_p(stream if isinstance(stream, int) else stream.cuda_stream)
+        st = None if stream is None else ctypes.c_void_p(L.stream_handle(stream))
         rc = self.lib.tm_shard_merge_w(self.h, self.n_shards, m, _p(d_counts), _p(d_src_base), _p(d_ids),
                                        _p(d_keys), key_words, key_stride, _p(d_out_count), _p(d_out_off),
                                        _p(d_out_gid), out_cap, _p(d_total), st)
@@ -226,7 +226,7 @@ class Comm:
 
 def _xin(n, counts, offs, ids, keys, key_words, key_stride, stream):
     p = lambda x: None if x is None else (x.data_ptr() if hasattr(x, "data_ptr") else int(x))  # noqa: E731
-    st = None if stream is None else (stream if isinstance(stream, int) else stream.cuda_stream)
+    st = None if stream is None else L.stream_handle(stream)
     return L.TmExchangeIn(n, key_words, p(counts), p(offs), p(ids), p(keys), key_stride, st)
 
 
@@ -394,7 +394,7 @@ class RoutedEngine(Engine):
 
 
 def _sp(stream):
-    return None if stream is None else (stream if isinstance(stream, int) else stream.cuda_stream)
+    return None if stream is None else L.stream_handle(stream)
 
 
 def route_in(n, nbytes, d_bytes, d_off, depth, stream=None):

@@ -519,8 +519,10 @@ typedef struct tm_batcher_stats {
     uint64_t size_seals, deadline_seals, failed_batches;
     /* where a batch's time goes, summed over batches (ns): sealed -> its lane
      * starts, packing into pinned memory, the device path with both
-     * read-backs, the callbacks */
+     * read-backs, the callbacks; within the device path, the host time
+     * spent enqueueing the copies and kernels and waiting on the stream */
     uint64_t wait_ns, pack_ns, device_ns, callback_ns;
+    uint64_t launch_ns, sync_ns;
 } tm_batcher_stats;
 /* ids: filter ids (match/1), route sources (match_routes/1) or To ids
  * (deliveries); dests: route dest ids, target ids (deliveries) or null; n:

@@ -34,11 +34,18 @@ def _check(fb, fo, batches, got):
     from oracle import O1
     o1 = O1(len(fo))
     o1.insert_many(fb, fo)
-    for (tb, to), (c, oo, ids) in zip(batches, got):
+    for r, ((tb, to), (c, oo, ids)) in enumerate(zip(batches, got)):
         oc, ooo, oi = o1.match_ids(tb, to, threads=8)
-        assert np.array_equal(c, oc)
-        assert np.array_equal(oo, ooo)
-        assert np.array_equal(ids, oi)
+        assert np.array_equal(c, oc), r
+        assert np.array_equal(oo, ooo), r
+        if not np.array_equal(ids, oi):   # name the first topic whose list differs
+            j = int(np.flatnonzero(ids != oi)[0])
+            t = int(np.searchsorted(ooo, j, side="right")) - 1
+            bad = [int(x) for x in np.flatnonzero([not np.array_equal(ids[ooo[u]:ooo[u + 1]], oi[ooo[u]:ooo[u + 1]])
+                                                   for u in range(len(oc))])]
+            raise AssertionError(f"rank {r}: {len(bad)} topics differ, first {t} "
+                                 f"{bytes(tb[to[t]:to[t + 1]])!r}: got {ids[ooo[t]:ooo[t + 1]].tolist()} "
+                                 f"want {oi[ooo[t]:ooo[t + 1]].tolist()}; topics {bad[:20]}")
     o1.close()
 
 

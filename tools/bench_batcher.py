@@ -49,7 +49,7 @@ def main():
                                                              ints(a.producers), ints(a.cb_threads), ints(a.eager)):
         print("[batcher] lanes %d, max_topics %d, deadline %d us, producers %d, callback threads %d ..." % (
             lanes, mt, dl, prod, cbt), file=sys.stderr, flush=True)
-        res = (ctypes.c_double * 12)()
+        res = (ctypes.c_double * 14)()
         rc = drv.tm_bench_batcher(e.h, tb.ctypes.data, to.ctypes.data, len(to) - 1, prod, dl, mt, lanes,
                                   4 if eager else 0, cbt, res)
         print(json.dumps({"replicas": devs, "eager": eager, "lanes": lanes, "max_topics": mt, "deadline_us": dl,
@@ -59,7 +59,8 @@ def main():
                           "mean_batch": res[3], "lat_us_p50": res[4], "lat_us_p99": res[5], "failed": int(res[6]),
                           "matches": int(res[7]),
                           "per_batch_us": {"sealed_to_lane": res[8], "pack": res[9], "device": res[10],
-                                           "callbacks": res[11]}}), flush=True)
+                                           "callbacks": res[11], "device_launch": res[12],
+                                           "device_wait": res[13]}}), flush=True)
     e.close()
 
 

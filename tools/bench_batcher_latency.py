@@ -65,7 +65,7 @@ def main():
         for dl in [int(x) for x in a.deadlines.split(",")]:
             total = max(100_000, int(rate * a.seconds))
             log("offered %.0fM publishes/s, deadline %d us, %d publishes ..." % (rate / 1e6, dl, total))
-            r = (ctypes.c_double * 14)()
+            r = (ctypes.c_double * 16)()
             rc = f(e.h, tb.ctypes.data, to.ctypes.data, len(to) - 1, a.producers, rate, total, dl, a.max_topics,
                    a.lanes, 4 if eager else 0, a.cb_threads, r)
             print(json.dumps({"opts": a.opt, "eager": eager, "offered_per_s": rate, "deadline_us": dl, "max_topics": a.max_topics,
@@ -75,7 +75,8 @@ def main():
                               "lat_us_p999": r[6], "lat_us_max": r[7], "failed": int(r[8]),
                               "max_producer_lag_us": r[9],
                               "per_batch_us": {"sealed_to_lane": r[10], "pack": r[11], "device": r[12],
-                                               "callbacks": r[13]}}), flush=True)
+                                               "callbacks": r[13], "device_launch": r[14],
+                                               "device_wait": r[15]}}), flush=True)
     e.close()
 
 

@@ -17,6 +17,7 @@ pass() {
   case $1 in
     fetch) run fetch FETCH_SIZE ;;
     write) run write WRITE_SIZE ;;
+    wr)    run wr WRITE_SIZE TCC_EA0_WRREQ_sum TCP_TCC_WRITE_REQ_sum ;;
     tcc)   run tcc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum ;;
     sq)    run sq SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_BUSY_CYCLES ;;
     tcp)   run tcp TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCP_TCC_WRITE_REQ_sum TCP_TOTAL_READ_sum ;;

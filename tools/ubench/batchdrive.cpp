@@ -31,9 +31,10 @@ void on_done(void* ctx, uint64_t, int status, const uint32_t*, const uint32_t*, 
 }
 }  // namespace
 
-// out[12]: seconds, topics/s, batches, mean batch, p50 us, p99 us, failed,
+// out[14]: seconds, topics/s, batches, mean batch, p50 us, p99 us, failed,
 // matches, then per batch (us): sealed -> lane, pack, device path (H2D,
-// kernels, D2H), callbacks
+// kernels, D2H), callbacks, and within the device path the host time
+// enqueueing it and waiting on the stream
 extern "C" int tm_bench_batcher(tm_engine* e, const uint8_t* tb, const uint64_t* to, uint64_t nt, int producers,
                                 uint32_t deadline_us, uint32_t max_topics, uint32_t lanes, uint32_t flags,
                                 uint32_t cb_threads, double* out) {
@@ -87,6 +88,8 @@ extern "C" int tm_bench_batcher(tm_engine* e, const uint8_t* tb, const uint64_t*
     out[9] = (st.pack_ns - st0.pack_ns) / nb / 1e3;
     out[10] = (st.device_ns - st0.device_ns) / nb / 1e3;
     out[11] = (st.callback_ns - st0.callback_ns) / nb / 1e3;
+    out[12] = (st.launch_ns - st0.launch_ns) / nb / 1e3;
+    out[13] = (st.sync_ns - st0.sync_ns) / nb / 1e3;
     std::vector<int64_t> lat;
     lat.reserve(nt / LAT_EVERY + 1);
     uint64_t fails = 0, ids = 0;
@@ -130,9 +133,9 @@ void on_done_ol(void* ctx, uint64_t, int status, const uint32_t*, const uint32_t
 }
 }  // namespace
 
-// out[14]: seconds, achieved topics/s, batches, mean batch, p50 us, p99 us,
+// out[16]: seconds, achieved topics/s, batches, mean batch, p50 us, p99 us,
 //          p999 us, max us, failed, max producer lag us, and per batch (us):
-//          sealed -> lane, pack, device path, callbacks
+//          sealed -> lane, pack, device path, callbacks, device enqueue, device wait
 extern "C" int tm_bench_batcher_open_loop(tm_engine* e, const uint8_t* tb, const uint64_t* to, uint64_t nt,
                                           int producers, double rate, uint64_t total, uint32_t deadline_us,
                                           uint32_t max_topics, uint32_t lanes, uint32_t flags, uint32_t cb_threads,
@@ -226,5 +229,7 @@ extern "C" int tm_bench_batcher_open_loop(tm_engine* e, const uint8_t* tb, const
     out[11] = (st.pack_ns - st0.pack_ns) / nb / 1e3;
     out[12] = (st.device_ns - st0.device_ns) / nb / 1e3;
     out[13] = (st.callback_ns - st0.callback_ns) / nb / 1e3;
+    out[14] = (st.launch_ns - st0.launch_ns) / nb / 1e3;
+    out[15] = (st.sync_ns - st0.sync_ns) / nb / 1e3;
     return TM_OK;
 }
