@@ -503,7 +503,7 @@ struct tm_engine {
     int presort = 3;                  // option "presort": walk the batch in the order of a key of its first
                                       // eight words (presort.hip; 0 = arrival order, 2 the tail order,
                                       // 3 the tail order for batches up to tail_max topics)
-    uint32_t tail_max = 2u << 20;     // option "tail_max": presort 3's largest tail-ordered batch
+    uint32_t tail_max = 4u << 20;     // option "tail_max": presort 3's largest tail-ordered batch
     int layout_mode = 1;              // option "layout": 0 off, 1 auto, 2 every commit (tests)
     size_t created_since_layout = 0;  // nodes created since the last relayout
     uint32_t hot_levels = 4;          // option "hot_levels": relayout puts depths <= H level by level (BFS)
@@ -1920,8 +1920,8 @@ struct tm_engine {
     // the walk order of an n-topic batch: option "presort" 3 tail-orders the
     // batches whose walk tail (the last lanes of each XCD range, ~0.4 ms a
     // launch) is a visible share of the walk -- 1M topics: walk -6 %, the
-    // key and one radix pass +0.045 ms; 8M: walk unchanged, +0.15 ms
-    // (profiles/r04_tail)
+    // key and one radix pass +0.045 ms; 2M: +1.5 % topics/s, 4M: +0.6 %;
+    // 8M: walk unchanged, +0.15 ms (profiles/r04_tail, r04_i)
     int presort_of(uint32_t n) const { return presort == 3 ? (n <= tail_max ? 2 : 0) : presort; }
     void ensure_slot(DevState& d, Slot& w, uint32_t n, uint64_t nbytes, uint32_t key_words, int presort) {
         w.twords.ensure((size_t)(n + 1) * WREG * 4);

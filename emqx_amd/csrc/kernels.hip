@@ -420,9 +420,11 @@ __device__ __forceinline__ uint4 load_half(const ImageView& im, uint32_t v, bool
     if (TM_NT_LEVEL > 0 && (leaf || r >= (uint32_t)TM_NT_LEVEL)) return nt_load16(p);
     return *p;
 }
-#ifndef TM_STAGE_PAIR
-#define TM_STAGE_PAIR 1
+#ifndef TM_STAGE_IDS
+#define TM_STAGE_IDS 8   // ids per stage-row store group (4, 8 or 16): RowEmit
 #endif
+constexpr uint32_t STAGE_IDS = TM_STAGE_IDS, STAGE_Q = TM_STAGE_IDS / 4;
+static_assert(STAGE_IDS == 4 || STAGE_IDS == 8 || STAGE_IDS == 16, "TM_STAGE_IDS: 4, 8 or 16");
 __device__ __forceinline__ void store_stage(uint32_t* p, uint4 x) {
     if (TM_NT_STAGE) nt_store16(p, x);
     else *reinterpret_cast<uint4*>(p) = x;
@@ -718,11 +720,15 @@ __device__ __forceinline__ void walk(const ImageView& im, uint32_t n, bool dolla
 }
 
 // discovery k of a topic goes to stage row slot K-1-k (k < K); the row's
-// last `count` slots are then the output in order.  TM_STAGE_PAIR: 8 ids
-// per pair of back-to-back 16 B stores (one 32 B sector, so the L2 writes
-// one whole sector to HBM instead of two half-filled ones: round 3's walk
-// wrote 2.2x its id bytes); 0: one 16 B store per 4 ids.
-// A row whose K is not a multiple of 8 stores its last 4 slots alone.
+// last `count` slots are then the output in order.  The ids of a group of
+// STAGE_IDS slots are held in registers and stored by back-to-back 16 B
+// stores once the group is full: 8 ids = one whole 32 B sector, so the L2
+// writes whole sectors to HBM instead of half-filled ones (round 3's one
+// store per 4 ids wrote 2.2x the id bytes; at C3 8 ids
+// per group cut the walk's fabric write requests from 64.5M to 36.9M per
+// launch and the walk from 10.07-10.38 to 9.24-9.40 ms, profiles/r04_g).
+// A row ending inside a group (K not a multiple of STAGE_IDS) stores its
+// last quads when the row fills.
 // KEYS: key word 0 to the same slot of the topic's key row; words j >= 1
 // (KW > 1) to key plane j, kplane u64 further on.
 template <bool KEYS>
@@ -730,8 +736,7 @@ struct RowEmit {
     uint32_t* row;
     uint64_t* krow;
     uint32_t K, cnt;
-    uint4 buf;     // slots K-4-g .. K-1-g of the current group g
-    uint4 buf2;    // TM_STAGE_PAIR: slots K-8-g .. K-5-g
+    uint4 bq[STAGE_Q];   // quad q: slots K-4(q+1)-g .. K-1-4q-g of the current group g (.w highest)
     uint64_t kb;   // KEYS: key of the last even discovery, stored with the next one (16 B)
     uint32_t KW;
     uint64_t kplane;
@@ -752,29 +757,16 @@ struct RowEmit {
             }
             for (uint32_t j = 1; j < KW; ++j) krow[j * kplane + K - 1 - cnt] = key_word(path, j, r, sym);
         }
-        if (cnt < K && TM_STAGE_PAIR) {
-            const uint32_t s = cnt & 7u, g = cnt & ~7u;
-            buf.w = s == 0 ? f : buf.w;
-            buf.z = s == 1 ? f : buf.z;
-            buf.y = s == 2 ? f : buf.y;
-            buf.x = s == 3 ? f : buf.x;
-            buf2.w = s == 4 ? f : buf2.w;
-            buf2.z = s == 5 ? f : buf2.z;
-            buf2.y = s == 6 ? f : buf2.y;
-            buf2.x = s == 7 ? f : buf2.x;
-            if (s == 7) {
-                store_stage(row + K - 8 - g, buf2);
-                store_stage(row + K - 4 - g, buf);
-            } else if (s == 3 && g + 8 > K) {   // K % 8 == 4: the row's last 4 slots
-                store_stage(row + K - 4 - g, buf);
+        if (cnt < K) {
+            const uint32_t s = cnt & (STAGE_IDS - 1), g = cnt - s;
+#pragma unroll
+            for (uint32_t q = 0; q < STAGE_Q; ++q) {
+                bq[q].w = s == 4 * q ? f : bq[q].w;
+                bq[q].z = s == 4 * q + 1 ? f : bq[q].z;
+                bq[q].y = s == 4 * q + 2 ? f : bq[q].y;
+                bq[q].x = s == 4 * q + 3 ? f : bq[q].x;
             }
-        } else if (cnt < K) {
-            const uint32_t s = cnt & 3u;
-            buf.w = s == 0 ? f : buf.w;
-            buf.z = s == 1 ? f : buf.z;
-            buf.y = s == 2 ? f : buf.y;
-            buf.x = s == 3 ? f : buf.x;
-            if (s == 3) store_stage(row + K - 4 - (cnt & ~3u), buf);
+            if (s == STAGE_IDS - 1 || cnt + 1 == K) store_group(s + 1, g);
         } else if (!KEYS && spill && !sfail) {
             const uint32_t o = cnt - K, j = o % (SPILL_CHUNK - 1);
             if (j == 0) {   // a new chunk, linked from the previous one
@@ -791,16 +783,15 @@ struct RowEmit {
         }
         ++cnt;
     }
+    // the quads holding the group's first m slots, lowest address first
+    __device__ __forceinline__ void store_group(uint32_t m, uint32_t g) {
+#pragma unroll
+        for (int q = (int)STAGE_Q - 1; q >= 0; --q)
+            if (4u * (uint32_t)q < m) store_stage(row + K - 4 * (q + 1) - g, bq[q]);
+    }
     __device__ __forceinline__ void flush() {
-        if (TM_STAGE_PAIR) {
-            const uint32_t s = cnt & 7u, g = cnt & ~7u;
-            if (s && cnt < K) {   // s <= 4: the first quad of the group only (s == 4 with K % 8 == 4 is stored)
-                if (s > 4) store_stage(row + K - 8 - g, buf2);
-                store_stage(row + K - 4 - g, buf);
-            }
-        } else if ((cnt & 3u) && cnt < K) {
-            store_stage(row + K - 4 - (cnt & ~3u), buf);
-        }
+        const uint32_t s = cnt & (STAGE_IDS - 1);
+        if (s && cnt < K) store_group(s, cnt - s);   // a part-filled group (a filled row stored itself)
         if (KEYS && (cnt & 1u) && cnt <= K) krow[K - cnt] = kb;   // the unpaired last even discovery
     }
 };
@@ -866,6 +857,8 @@ constexpr uint32_t NO_TOPIC = 0xFFFFFFFFu;
 
 #if TM_PF1
 #define TM_WALK_ATTR __attribute__((amdgpu_waves_per_eu(7, 8)))   // the prefetch slot within 7 waves/SIMD
+#elif TM_WALK_WAVES
+#define TM_WALK_ATTR __attribute__((amdgpu_waves_per_eu(TM_WALK_WAVES, 8)))   // A/B builds: a register cap
 #else
 #define TM_WALK_ATTR
 #endif
@@ -912,7 +905,7 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
     uint32_t my = NO_TOPIC, myt = 0;   // the lane's queue position and its topic
     bool is_long = false, drained = false;
     Cursor cur;
-    RowEmit<KEYS> em{nullptr, nullptr, K, 0, make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0), 0ull, KW, (uint64_t)n * K};
+    RowEmit<KEYS> em{nullptr, nullptr, K, 0, {}, 0ull, KW, (uint64_t)n * K};
     if (!KEYS && spill) {   // this XCD's spill area and counter (placement only: any XCD id is valid)
         const uint32_t x = xcc_id();
         em.spill = spill;
@@ -1272,7 +1265,7 @@ tm_walk_wave(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const u
             // beyond the wave's capacity: the per-lane walk, on one lane
             const uint64_t b = off[t] - off[0];
             const MemWords mw{row, words + b + t};
-            RowEmit<false> em{srow, nullptr, K, 0, make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0), 0ull, 1u, 0ull};
+            RowEmit<false> em{srow, nullptr, K, 0, {}, 0ull, 1u, 0ull};
             WalkStats s2;
             walk<false, false>(im, nl, dollar, GlobalPath{gpath + b + 2ull * t}, mw, em, s2);
             em.flush();

@@ -637,7 +637,7 @@ int  tm_rewrite_match_batch_device(tm_rewrite* r, const uint8_t* d_topics, const
  *              topics (batches above wave_walk_max); 3 = the tail order for
  *              batches of at most "tail_max" topics, arrival order above
  *              (default); 0 = arrival order
- *   "tail_max" presort 3's largest tail-ordered batch (default 2097152)
+ *   "tail_max" presort 3's largest tail-ordered batch (default 4194304)
  *   "chunk_rows" 1 = a wave copies each taken chunk's 64 tokenized rows to
  *              LDS at once (default), 0 = each lane reads its topic's row
  *   "spill"    1 = ids past a stage row go to per-XCD spill chunks (default),
