@@ -85,6 +85,8 @@ TM_ROUTE_ALL = 0xFFFFFFFF
 TM_COMM_ID_BYTES = 128
 TM_BATCHER_ROUTES = 1
 TM_BATCHER_DELIVERIES = 2
+TM_BATCHER_EAGER = 4
+TM_BATCHER_CSR = 8
 DONE_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, c_u32p, c_u32p, ctypes.c_uint32)
 
 # (name, restype, argtypes) — every symbol include/topicmatch.h declares
@@ -125,6 +127,9 @@ SIGNATURES = [
                                             c_u64p]),
     ("tm_free", None, [ctypes.c_void_p]),
     ("tm_match_batch_device", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                             ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                             ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]),
+    ("tm_match_small_device", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
                                              ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                              ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]),
     ("tm_set_option", ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int64]),

@@ -355,9 +355,12 @@ struct tm_batcher {
             const uint64_t outb = 8 + offb + cntb + cap * 4;
             if (!L.d_out.ensure(outb) || !L.h_out.ensure(outb)) return TM_ENOMEM;
             uint8_t* d = (uint8_t*)L.d_out.p;
-            int rc = tm_match_batch_device(eng, (const uint8_t*)L.d_io.p + offb, (const uint64_t*)L.d_io.p, n, nbytes,
-                                           (uint32_t*)(d + 8 + offb), (uint64_t*)(d + 8), (uint32_t*)(d + 8 + offb + cntb),
-                                           cap, (uint64_t*)d, s);
+            // one launch (tm_match_small_device: lists in completion order,
+            // read by (offset, count) per topic), or the CSR path (A/B)
+            auto* const match = (cfg.flags & TM_BATCHER_CSR) ? tm_match_batch_device : tm_match_small_device;
+            int rc = match(eng, (const uint8_t*)L.d_io.p + offb, (const uint64_t*)L.d_io.p, n, nbytes,
+                           (uint32_t*)(d + 8 + offb), (uint64_t*)(d + 8), (uint32_t*)(d + 8 + offb + cntb), cap,
+                           (uint64_t*)d, s);
             if (rc != TM_OK) return rc;
             if (!chk(hipMemcpyAsync(L.h_out.p, L.d_out.p, outb, hipMemcpyDeviceToHost, s))) return TM_EDEVICE;
             L.launch_ns += ns_since(t0);

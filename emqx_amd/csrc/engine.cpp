@@ -214,6 +214,7 @@ constexpr int N_KERNEL_SLOTS = 4;   // tokenize, walk, scan, copy_out
 struct Slot {
     DevBuf twords, words, path, meta, scan, stage, kstage, ws, stats, perm, skeys, svals, scount, soff, sscan,
         twords_s, meta_s, spill, spill_head;
+    DevBuf sctl;                    // tm_match_small's placement / completion counters (left zeroed by it)
     uint32_t spill_chunks = 0;      // spill capacity of the slot's last batch (0: none)
     bool sorted = false;            // the slot's last batch walked in presort order (perm valid)
     uint64_t* h_maxc = nullptr;     // pinned copy of the slot's ws after its last walk (largest match count,
@@ -2092,6 +2093,33 @@ struct tm_engine {
         if (timing_enabled)
             for (int i = 0; i < 4; ++i) d.ev_pending.push_back(d.ev_cur[i]);
     }
+    // a small batch in one launch (tm_match_small_device): tokenize, walk a
+    // wave per topic, place each list with one atomic -- no stage rows, no
+    // scan, no copy-out kernel.  Uses the next slot's row / word / path
+    // buffers like run_batch; the slot's last CSR batch is not re-copied
+    // after this (re-copies happen inside one call, under the batch lock).
+    void run_small(DevState& d, const uint8_t* bytes, const uint64_t* off, uint32_t n, uint64_t nbytes,
+                   uint32_t* counts, uint64_t* out_off, uint32_t* ids, uint64_t cap, uint64_t* total, hipStream_t st) {
+        const int si = d.next_slot;
+        d.next_slot = (d.next_slot + 1) % nslots;
+        Slot& w = d.slots[si];
+        if (w.used) HIPCHK(hipStreamWaitEvent(st, w.done, 0));   // its previous batch, maybe on another stream
+        w.twords.ensure((size_t)(n + 1) * WREG * 4);
+        w.words.ensure((nbytes + n + 1) * 4);
+        w.path.ensure((nbytes + 2ull * n + 2) * 4);
+        w.meta.ensure((size_t)(n + 1) * 4);
+        if (!w.sctl.p) {
+            w.sctl.ensure(64);
+            HIPCHK(hipMemsetAsync(w.sctl.p, 0, 64, st));
+        }
+        if (!w.done) HIPCHK(hipEventCreateWithFlags(&w.done, hipEventDisableTiming));
+        HIPCHK(launch_small(view(d), bytes, off, n, w.twords.as<uint32_t>(), w.words.as<uint32_t>(),
+                            w.meta.as<uint32_t>(), w.path.as<uint32_t>(), counts, out_off, ids, cap, total,
+                            w.sctl.as<unsigned long long>(), st));
+        d.note_use(st);
+        HIPCHK(hipEventRecord(w.done, st));
+        w.used = true;
+    }
     // emqx_router:match_routes/1 over a device batch (stream-ordered except
     // for one read of the match total that sizes the ids workspace)
     // the ids of replica d's last batch again, into a larger output: only
@@ -3261,6 +3289,21 @@ static int match_device(tm_engine* e, const uint8_t* d_bytes, const uint64_t* d_
         }
         return TM_OK;
     }, [&] { e->last_stats = stats; });
+}
+
+int tm_match_small_device(tm_engine* e, const uint8_t* d_bytes, const uint64_t* d_off, uint32_t n,
+                          uint64_t topic_bytes, uint32_t* d_count, uint64_t* d_out_off, uint32_t* d_ids,
+                          uint64_t out_cap, uint64_t* d_total, void* hip_stream) {
+    if (!d_off || !d_out_off || !d_total || (n && !d_count) || (out_cap && !d_ids)) return TM_EINVAL;
+    if (!e) return TM_EINVAL;
+    if (e->devs.empty()) return no_device(e, "the match path");
+    DevState& d = *e->replica_for(d_off);
+    return batch_call(e, {&d}, [&]() -> int {
+        tm_engine::Guard g(d.device);
+        hipStream_t st = hip_stream ? (hipStream_t)hip_stream : d.stream;
+        e->run_small(d, d_bytes, d_off, n, topic_bytes, d_count, d_out_off, d_ids, out_cap, d_total, st);
+        return TM_OK;
+    }, [&] { e->finish_batch(n); });
 }
 
 // diagnostics (not part of include/topicmatch.h): the last stats-mode

@@ -88,6 +88,12 @@ hipError_t launch_queue(bool stats_mode, bool xcdq, const ImageView& im, const u
                         bool hist = false, uint32_t key_words = 1);
 // tm_copy_out again over a finished launch_queue's workspace (qb, same n /
 // K / key_words) into a larger output: no second walk
+// a small batch in one launch (kernels.hip tm_match_small): lists placed in
+// completion order, out_off[t] = topic t's start; ctl: two u64 the kernel
+// leaves zeroed (zero them once when allocated)
+hipError_t launch_small(const ImageView& im, const uint8_t* bytes, const uint64_t* off, uint32_t n, uint32_t* twords,
+                        uint32_t* words, uint32_t* meta, uint32_t* gpath, uint32_t* counts, uint64_t* out_off,
+                        uint32_t* out, uint64_t cap, uint64_t* total, unsigned long long* ctl, hipStream_t st);
 hipError_t launch_copy(const ImageView& im, const uint8_t* bytes, const uint64_t* off, uint32_t n, const QueueBufs& qb,
                        uint32_t K, uint32_t key_words, const uint32_t* counts, const uint64_t* out_off, uint32_t* out,
                        uint64_t* out_keys, uint64_t out_cap, hipStream_t st);

@@ -1119,6 +1119,132 @@ __device__ __forceinline__ uint32_t wave_append(bool has, uint32_t& n) {
     return at;
 }
 
+// one topic's level-synchronous walk by one wave: the topic's words are in
+// L.words; on return the emissions are in L.eid[0, ec) in discovery order
+// (ascending key), or the result is false: the frontier or the emissions
+// outgrew the wave's LDS (the caller walks the topic per lane instead)
+__device__ __forceinline__ bool wave_walk_topic(const ImageView& im, WaveLds& L, uint32_t nl, bool dollar,
+                                                uint32_t lane, uint32_t& ec_out) {
+    uint32_t ec = 0;
+    bool fallback = false;
+    // the start: root, or (the '$' rule, emqx_trie.erl:121-122) the root's
+    // literal child by the first word, skipping '#' and '+'
+    uint32_t fc = 0, p = 0, r = 0;
+    if (lane == 0) {
+        if (!dollar) {
+            L.fnode[0][0] = ROOT;
+            L.fkey[0][0] = 0;
+            fc = 1;
+        } else {
+            uint64_t ld = 0;
+            const uint4 q = load_half(im, ROOT, false);
+            const uint32_t c = lit_child<false>(im, ROOT, q.x, q.z, q.w, L.words[0], ld).child;
+            if (c != NODE_NONE) {
+                L.fnode[0][0] = c;
+                L.fkey[0][0] = rank_sym(0, 1);
+                fc = 1;
+            }
+        }
+    }
+    fc = (uint32_t)__shfl((int)fc, 0, 64);
+    r = dollar ? 1u : 0u;
+    wave_sync_lds();
+    for (; fc && !fallback; ++r) {
+        const bool leaf = r == nl;
+        const uint32_t w = leaf ? 0u : L.words[r];
+        const uint32_t kleft = nl - r - 1;
+        uint32_t nf = 0;
+        for (uint32_t base = 0; base < fc; base += 64) {
+            const uint32_t i = base + lane;
+            const bool act = i < fc;
+            const uint32_t v = act ? L.fnode[p][i] : NODE_NONE;
+            const uint64_t key = act ? L.fkey[p][i] : 0ull;
+            uint4 h = make_uint4(FILTER_NONE, FILTER_NONE, WORD_NONE, NODE_NONE);
+            if (act) h = load_half(im, v, leaf, r);
+            // 'match_#': the '#' child's filter, discovered first (rank 0 at r)
+            uint32_t e1 = act && !(h.y & SUM_TAG) ? h.y : FILTER_NONE;
+            uint32_t e2 = FILTER_NONE, c1 = NODE_NONE, c2 = NODE_NONE;
+            if (act && leaf) {
+                e2 = h.x;   // the node's own filter (emqx_trie.erl:128), end mark 1
+            } else if (act) {
+                const uint32_t plus = h.x, hf = h.y;
+                bool lit_ok = true, plus_ok = true;
+                if (hf & SUM_TAG) {
+                    plus_ok = sum_useful(hf & SUM_ALL, kleft);
+                    lit_ok = w < WORD_MAX ? sum_useful((hf >> 15) & SUM_ALL, kleft)
+                                          : w == WORD_PLUS ? plus_ok : true;
+                }
+                uint64_t ld = 0;
+                if (lit_ok) {
+                    const Hit g = lit_child<false>(im, v, plus, h.z, h.w, w, ld);
+                    if (g.child != NODE_NONE && (SLOT_RECORD || sum_useful(g.plus & SUM_ALL, kleft)))
+                        c1 = g.child;
+                }
+                if (plus_ok) c2 = plus & NODE_MASK;
+            }
+            // emissions (any order: the keys sort them)
+            uint32_t a = wave_append(e1 != FILTER_NONE, ec);
+            if (e1 != FILTER_NONE && a < WV_E) {
+                L.ekey[a] = key;
+                L.eid[a] = e1;
+            }
+            a = wave_append(e2 != FILTER_NONE, ec);
+            if (e2 != FILTER_NONE && a < WV_E) {
+                L.ekey[a] = key | rank_sym(r, 1);
+                L.eid[a] = e2;
+            }
+            // children for level r + 1: the topic word's edge (1), the '+' edge (2)
+            a = wave_append(c1 != NODE_NONE, nf);
+            if (c1 != NODE_NONE && a < WV_F) {
+                L.fnode[1 - p][a] = c1;
+                L.fkey[1 - p][a] = key | rank_sym(r, 1);
+            }
+            a = wave_append(c2 != NODE_NONE, nf);
+            if (c2 != NODE_NONE && a < WV_F) {
+                L.fnode[1 - p][a] = c2;
+                L.fkey[1 - p][a] = key | rank_sym(r, 2);
+            }
+        }
+        wave_sync_lds();
+        if (nf > WV_F || ec > WV_E) fallback = true;   // uniform
+        if (leaf) break;
+        fc = nf;
+        p = 1 - p;
+    }
+    if (fallback) return false;
+    // discovery order = ascending key: bitonic sort of the topic's emissions
+    // in LDS (padded with keys that sort last)
+    uint32_t P = 64;
+    while (P < ec) P <<= 1;
+    for (uint32_t i = ec + lane; i < P; i += 64) {
+        L.ekey[i] = ~0ull;
+        L.eid[i] = FILTER_NONE;
+    }
+    wave_sync_lds();
+    if (ec > 1) {
+        for (uint32_t k = 2; k <= P; k <<= 1) {
+            for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+                for (uint32_t i = lane; i < P; i += 64) {
+                    const uint32_t l = i ^ j;
+                    if (l > i) {
+                        const uint64_t x = L.ekey[i], y = L.ekey[l];
+                        if ((x > y) == ((i & k) == 0)) {
+                            const uint32_t xi = L.eid[i];
+                            L.ekey[i] = y;
+                            L.ekey[l] = x;
+                            L.eid[i] = L.eid[l];
+                            L.eid[l] = xi;
+                        }
+                    }
+                }
+                wave_sync_lds();
+            }
+        }
+    }
+    ec_out = ec;
+    return true;
+}
+
 __global__ void __launch_bounds__(BLOCK)
 tm_walk_wave(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const uint32_t* __restrict__ twords,
              const uint32_t* __restrict__ words, const uint32_t* __restrict__ meta, uint32_t* __restrict__ gpath,
@@ -1140,121 +1266,9 @@ tm_walk_wave(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const u
         if (!fallback) {
             if (lane < WREG && lane < nl) L.words[lane] = row[lane];
             wave_sync_lds();
-            // the start: root, or (the '$' rule, emqx_trie.erl:121-122) the
-            // root's literal child by the first word, skipping '#' and '+'
-            uint32_t fc = 0, p = 0, r = 0;
-            if (lane == 0) {
-                if (!dollar) {
-                    L.fnode[0][0] = ROOT;
-                    L.fkey[0][0] = 0;
-                    fc = 1;
-                } else {
-                    uint64_t ld = 0;
-                    const uint4 q = load_half(im, ROOT, false);
-                    const uint32_t c = lit_child<false>(im, ROOT, q.x, q.z, q.w, L.words[0], ld).child;
-                    if (c != NODE_NONE) {
-                        L.fnode[0][0] = c;
-                        L.fkey[0][0] = rank_sym(0, 1);
-                        fc = 1;
-                    }
-                }
-            }
-            fc = (uint32_t)__shfl((int)fc, 0, 64);
-            r = dollar ? 1u : 0u;
-            wave_sync_lds();
-            for (; fc && !fallback; ++r) {
-                const bool leaf = r == nl;
-                const uint32_t w = leaf ? 0u : L.words[r];
-                const uint32_t kleft = nl - r - 1;
-                uint32_t nf = 0;
-                for (uint32_t base = 0; base < fc; base += 64) {
-                    const uint32_t i = base + lane;
-                    const bool act = i < fc;
-                    const uint32_t v = act ? L.fnode[p][i] : NODE_NONE;
-                    const uint64_t key = act ? L.fkey[p][i] : 0ull;
-                    uint4 h = make_uint4(FILTER_NONE, FILTER_NONE, WORD_NONE, NODE_NONE);
-                    if (act) h = load_half(im, v, leaf, r);
-                    // 'match_#': the '#' child's filter, discovered first (rank 0 at r)
-                    uint32_t e1 = act && !(h.y & SUM_TAG) ? h.y : FILTER_NONE;
-                    uint32_t e2 = FILTER_NONE, c1 = NODE_NONE, c2 = NODE_NONE;
-                    if (act && leaf) {
-                        e2 = h.x;   // the node's own filter (emqx_trie.erl:128), end mark 1
-                    } else if (act) {
-                        const uint32_t plus = h.x, hf = h.y;
-                        bool lit_ok = true, plus_ok = true;
-                        if (hf & SUM_TAG) {
-                            plus_ok = sum_useful(hf & SUM_ALL, kleft);
-                            lit_ok = w < WORD_MAX ? sum_useful((hf >> 15) & SUM_ALL, kleft)
-                                                  : w == WORD_PLUS ? plus_ok : true;
-                        }
-                        uint64_t ld = 0;
-                        if (lit_ok) {
-                            const Hit g = lit_child<false>(im, v, plus, h.z, h.w, w, ld);
-                            if (g.child != NODE_NONE && (SLOT_RECORD || sum_useful(g.plus & SUM_ALL, kleft)))
-                                c1 = g.child;
-                        }
-                        if (plus_ok) c2 = plus & NODE_MASK;
-                    }
-                    // emissions (any order: the keys sort them)
-                    uint32_t a = wave_append(e1 != FILTER_NONE, ec);
-                    if (e1 != FILTER_NONE && a < WV_E) {
-                        L.ekey[a] = key;
-                        L.eid[a] = e1;
-                    }
-                    a = wave_append(e2 != FILTER_NONE, ec);
-                    if (e2 != FILTER_NONE && a < WV_E) {
-                        L.ekey[a] = key | rank_sym(r, 1);
-                        L.eid[a] = e2;
-                    }
-                    // children for level r + 1: the topic word's edge (1), the '+' edge (2)
-                    a = wave_append(c1 != NODE_NONE, nf);
-                    if (c1 != NODE_NONE && a < WV_F) {
-                        L.fnode[1 - p][a] = c1;
-                        L.fkey[1 - p][a] = key | rank_sym(r, 1);
-                    }
-                    a = wave_append(c2 != NODE_NONE, nf);
-                    if (c2 != NODE_NONE && a < WV_F) {
-                        L.fnode[1 - p][a] = c2;
-                        L.fkey[1 - p][a] = key | rank_sym(r, 2);
-                    }
-                }
-                wave_sync_lds();
-                if (nf > WV_F || ec > WV_E) fallback = true;   // uniform
-                if (leaf) break;
-                fc = nf;
-                p = 1 - p;
-            }
+            fallback = !wave_walk_topic(im, L, nl, dollar, lane, ec);
         }
         if (!fallback) {
-            // discovery order = ascending key: bitonic sort of the topic's
-            // emissions in LDS (padded with keys that sort last)
-            uint32_t P = 64;
-            while (P < ec) P <<= 1;
-            for (uint32_t i = ec + lane; i < P; i += 64) {
-                L.ekey[i] = ~0ull;
-                L.eid[i] = FILTER_NONE;
-            }
-            wave_sync_lds();
-            if (ec > 1) {
-                for (uint32_t k = 2; k <= P; k <<= 1) {
-                    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-                        for (uint32_t i = lane; i < P; i += 64) {
-                            const uint32_t l = i ^ j;
-                            if (l > i) {
-                                const uint64_t x = L.ekey[i], y = L.ekey[l];
-                                if ((x > y) == ((i & k) == 0)) {
-                                    const uint32_t xi = L.eid[i];
-                                    L.ekey[i] = y;
-                                    L.ekey[l] = x;
-                                    L.eid[i] = L.eid[l];
-                                    L.eid[l] = xi;
-                                }
-                            }
-                        }
-                        wave_sync_lds();
-                    }
-                }
-            }
             const uint32_t m = ec < K ? ec : K;
             for (uint32_t k = lane; k < m; k += 64) srow[K - 1 - k] = L.eid[k];
             if (lane == 0) {
@@ -1275,6 +1289,83 @@ tm_walk_wave(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const u
         wave_sync_lds();
     }
     if (lane == 0 && maxl && ws) atomicMax(ws + QWS_MAXL, (unsigned long long)maxl);
+}
+
+// tm_match_small: a small batch in ONE launch (the micro-batcher's path,
+// engine.cpp match_small; a small batch's time is per-operation latency).
+// One wave per topic: lane 0 tokenizes it (tokenize_one: the row, words and
+// meta as tm_tokenize writes them), the wave walks it level by level
+// (wave_walk_topic), reserves its list's range with one atomic and writes
+// the list in emqx_trie:match/1 order (reverse discovery order) straight to
+// the output.  Lists are contiguous per topic but placed in completion
+// order: out_off[t] is topic t's start, not an exclusive scan.  Topics past
+// the wave's capacity walk per lane on lane 0, twice (count, then emit).
+// ctl[0] = ids placed, ctl[1] = waves done: the last wave to finish writes
+// *total and zeroes both for the next launch on the same ctl (the engine
+// keeps one per batch slot, zeroed when it is allocated).
+__global__ void __launch_bounds__(BLOCK)
+tm_match_small(ImageView im, const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint32_t n,
+               uint32_t* __restrict__ twords, uint32_t* __restrict__ words, uint32_t* __restrict__ meta,
+               uint32_t* __restrict__ gpath, uint32_t* __restrict__ counts, uint64_t* __restrict__ out_off,
+               uint32_t* __restrict__ out, uint64_t cap, uint64_t* __restrict__ total,
+               unsigned long long* __restrict__ ctl) {
+    __shared__ WaveLds lds_all[BLOCK / 64];
+    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    WaveLds& L = lds_all[wv];
+    for (uint32_t t = blockIdx.x * (BLOCK / 64) + wv; t < n; t += gridDim.x * (BLOCK / 64)) {
+        const uint64_t b = off[t] - off[0];
+        uint32_t mt = 0;
+        if (lane == 0) {
+            tokenize_one(im, GlobalBytes{bytes}, off, t, n, twords, words, meta, nullptr, nullptr, 0u);
+            mt = meta[t];   // this lane's own store
+            const uint32_t* row = twords + (uint64_t)t * WREG;
+#pragma unroll
+            for (uint32_t k = 0; k < WREG; ++k) L.words[k] = row[k];
+        }
+        mt = (uint32_t)__shfl((int)mt, 0, 64);
+        wave_sync_lds();
+        const uint32_t nl = mt & MN;
+        const bool dollar = (mt & MDOLLAR) != 0;
+        uint32_t ec = 0;
+        bool fallback = (mt & MLONG) != 0 || nl > 31;
+        if (!fallback) fallback = !wave_walk_topic(im, L, nl, dollar, lane, ec);
+        if (!fallback) {
+            uint64_t base = 0;
+            if (lane == 0) base = atomicAdd(ctl, (unsigned long long)ec);
+            base = __shfl(base, 0, 64);
+            if (base + ec <= cap)
+                for (uint32_t j = lane; j < ec; j += 64) out[base + j] = L.eid[ec - 1 - j];
+            if (lane == 0) {
+                counts[t] = ec;
+                out_off[t] = base;
+            }
+        } else if (lane == 0) {
+            // the per-lane walk: count, reserve, then emit at base + (c-1-k)
+            const MemWords mw{twords + (uint64_t)t * WREG, words + b + t};
+            const GlobalPath gp{gpath + b + 2ull * t};
+            RowEmit<false> cnt{nullptr, nullptr, 0u, 0, {}, 0ull, 1u, 0ull};
+            WalkStats s2;
+            walk<false, false>(im, nl, dollar, gp, mw, cnt, s2);
+            const uint64_t base = atomicAdd(ctl, (unsigned long long)cnt.cnt);
+            if (base + cnt.cnt <= cap) {
+                TailEmit<false> em{out, nullptr, base, cap, 0u, cnt.cnt, 0, 1u, 0ull};
+                walk<false, false>(im, nl, dollar, gp, mw, em, s2);
+            }
+            counts[t] = cnt.cnt;
+            out_off[t] = base;
+        }
+        wave_sync_lds();
+    }
+    // the last wave out publishes the total and re-arms ctl
+    if (lane == 0) {
+        __threadfence();
+        const unsigned long long waves = (unsigned long long)gridDim.x * (BLOCK / 64);
+        if (atomicAdd(ctl + 1, 1ull) == waves - 1) {
+            *total = atomicAdd(ctl, 0ull);
+            atomicExch(ctl, 0ull);
+            atomicExch(ctl + 1, 0ull);
+        }
+    }
 }
 
 // tm_copy_out: per 256 topics, the block's output range is copied from the
@@ -1679,6 +1770,16 @@ hipError_t launch_scan(const uint32_t* counts, uint32_t n, uint64_t* out_off, ui
     hipLaunchKernelGGL(tm_scan_reduce, dim3(tiles), dim3(BLOCK), 0, st, counts, n, tmp);
     hipLaunchKernelGGL(tm_scan_tiles, dim3(1), dim3(BLOCK), 0, st, tmp, tiles);
     hipLaunchKernelGGL(tm_scan_final, dim3(tiles), dim3(BLOCK), 0, st, counts, n, tmp, out_off, total);
+    return hipGetLastError();
+}
+
+hipError_t launch_small(const ImageView& im, const uint8_t* bytes, const uint64_t* off, uint32_t n, uint32_t* twords,
+                        uint32_t* words, uint32_t* meta, uint32_t* gpath, uint32_t* counts, uint64_t* out_off,
+                        uint32_t* out, uint64_t cap, uint64_t* total, unsigned long long* ctl, hipStream_t st) {
+    if (n == 0) return hipMemsetAsync(total, 0, 8, st);
+    const uint32_t wb = div_up(n, BLOCK / 64);
+    hipLaunchKernelGGL(tm_match_small, dim3(wb < 65535 ? wb : 65535), dim3(BLOCK), 0, st, im, bytes, off, n, twords,
+                       words, meta, gpath, counts, out_off, out, cap, total, ctl);
     return hipGetLastError();
 }
 

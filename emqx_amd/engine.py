@@ -226,6 +226,22 @@ class Engine:
                                             p(d_ids), out_cap, p(d_total), st)
         return self._check(rc, "tm_match_batch_device")
 
+    def match_small_device(self, d_bytes, d_off, n, topic_bytes, d_counts, d_offs, d_ids, out_cap, d_total,
+                           stream=None):
+        """tm_match_small_device: the lists of a small batch in one launch;
+        topic t's list is d_ids[d_offs[t] : d_offs[t] + d_counts[t]] (lists
+        in completion order, d_offs has n entries)"""
+        def p(x):
+            if x is None:
+                return None
+            if hasattr(x, "data_ptr"):
+                return ctypes.c_void_p(x.data_ptr())
+            return ctypes.c_void_p(int(x))
+        st = None if stream is None else ctypes.c_void_p(L.stream_handle(stream))
+        rc = self.lib.tm_match_small_device(self.h, p(d_bytes), p(d_off), n, topic_bytes, p(d_counts), p(d_offs),
+                                            p(d_ids), out_cap, p(d_total), st)
+        return self._check(rc, "tm_match_small_device")
+
     # -- emqx_router: the route bag and match_routes/1 ----------------------
     TOPIC_ROUTE = 0xFFFFFFFF    # route source = the publish topic itself
 

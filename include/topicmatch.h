@@ -200,6 +200,21 @@ int tm_match_batch_device(tm_engine* e, const uint8_t* d_topic_bytes, const uint
                           uint64_t* d_out_off, uint32_t* d_out_filter_id, uint64_t out_cap,
                           uint64_t* d_total, void* hip_stream);
 
+/* The same lists for a small batch in ONE kernel launch (tokenize, a wave per
+ * topic, each list placed with one atomic): for latency-bound batches (the
+ * micro-batcher's, up to a few tens of thousands of topics), where the four
+ * launches and the scan of tm_match_batch_device cost more than the walk.
+ * Each topic's list is contiguous and in emqx_trie:match/1 order at
+ * d_out_off[t] .. + d_out_count[t], but topics' lists are laid out in
+ * completion order (d_out_off is not an exclusive scan; there is no
+ * d_out_off[n]).  *d_total = ids of all lists; when it exceeds out_cap, no
+ * list past the capacity was written: run again with out_cap >= *d_total.
+ * Same arguments and stream semantics as tm_match_batch_device. */
+int tm_match_small_device(tm_engine* e, const uint8_t* d_topic_bytes, const uint64_t* d_topic_off,
+                          uint32_t n, uint64_t topic_bytes, uint32_t* d_out_count,
+                          uint64_t* d_out_off, uint32_t* d_out_filter_id, uint64_t out_cap,
+                          uint64_t* d_total, void* hip_stream);
+
 /* Sharded mode (the filter set partitioned over GPUs, see
  * emqx_amd/shard.py).  Same as tm_match_batch_device on this engine's shard,
  * plus d_out_key[i]: the order key of id i (2 bits per level for the branch
@@ -500,6 +515,8 @@ int tm_match_deliveries_batch_device(tm_engine* e, const uint8_t* d_topic_bytes,
  * term and enif_send()s it).  status != TM_OK: ids are null. */
 #define TM_BATCHER_ROUTES 1u   /* results are match_routes/1 (src ids + dest ids) */
 #define TM_BATCHER_DELIVERIES 2u   /* results are aggre(match_routes/1) (To ids + target ids) */
+#define TM_BATCHER_CSR 8u   /* small match/1 batches through tm_match_batch_device (four launches and a
+                              scan) instead of the one-launch tm_match_small_device (A/B) */
 #define TM_BATCHER_EAGER 4u   /* seal as soon as a lane is free (deadline_us stays the upper bound): low
                                  load runs small batches at once, high load batches up while lanes are busy */
 
