@@ -98,6 +98,105 @@ tm_presort_scatter(const uint32_t* __restrict__ keys_in, const uint32_t* __restr
     }
 }
 
+// the same stable scatter through LDS (TM_PS_LOCAL): each wave ranks a
+// contiguous quarter of the tile (1024 keys, 16 rounds of 64) with its own
+// running per-digit counts -- no block barrier per round --, the block
+// combines the waves' counts, places the tile sorted by digit in LDS, and
+// writes each digit's run out with consecutive threads on consecutive
+// addresses (the per-round form scatters 4 B stores one lane at a time).
+#ifndef TM_PS_LOCAL
+#define TM_PS_LOCAL 1
+#endif
+__device__ __forceinline__ uint32_t block_excl_scan256(uint32_t x, uint32_t* tmp) {
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t inc = x;
+#pragma unroll
+    for (uint32_t o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)inc, o, 64);
+        if (lane >= o) inc += y;
+    }
+    if (lane == 63) tmp[wave] = inc;
+    __syncthreads();
+    uint32_t pre = 0;
+    for (uint32_t w = 0; w < wave; ++w) pre += tmp[w];
+    return pre + inc - x;
+}
+__global__ void __launch_bounds__(PS_BLOCK)
+tm_presort_scatter_ls(const uint32_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in, uint32_t n,
+                      uint32_t shift, const uint64_t* __restrict__ off, uint32_t* __restrict__ keys_out,
+                      uint32_t* __restrict__ vals_out) {
+    __shared__ uint32_t skey[PS_TILE];
+    __shared__ uint32_t sval[PS_TILE];
+    __shared__ uint32_t wcnt[PS_WAVES][256];   // keys per digit in each wave, then that wave's base per digit
+    __shared__ uint32_t lstart[256];           // tile-local start of each digit
+    __shared__ uint32_t gstart[256];           // global start of this tile's run of each digit
+    __shared__ uint32_t tmp[PS_WAVES];
+    const uint32_t tile = blockIdx.x, base = tile * PS_TILE;
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (uint32_t w = 0; w < PS_WAVES; ++w) wcnt[w][threadIdx.x] = 0;
+    gstart[threadIdx.x] = (uint32_t)off[(size_t)threadIdx.x * gridDim.x + tile];
+    __syncthreads();
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;   // lanes below this one
+    uint32_t k[PS_ROUNDS], v[PS_ROUNDS], rk[PS_ROUNDS];
+    const uint32_t seg = base + wave * (PS_TILE / PS_WAVES);
+#pragma unroll
+    for (uint32_t r = 0; r < PS_ROUNDS; ++r) {
+        const uint32_t i = seg + r * 64 + lane;
+        const bool valid = i < n;
+        k[r] = valid ? keys_in[i] : 0u;
+        v[r] = valid ? vals_in[i] : 0u;
+    }
+#pragma unroll
+    for (uint32_t r = 0; r < PS_ROUNDS; ++r) {
+        const bool valid = seg + r * 64 + lane < n;
+        const uint32_t d = (k[r] >> shift) & 255u;
+        uint64_t m = __ballot(valid);
+#pragma unroll
+        for (uint32_t bit = 0; bit < 8; ++bit) {
+            const uint64_t bb = __ballot(valid && ((d >> bit) & 1u));
+            m &= ((d >> bit) & 1u) ? bb : ~bb;
+        }
+        const uint32_t rank = __popcll(m & lt);
+        const uint32_t prior = wcnt[wave][d];   // read by every lane of the digit before its leader adds
+        rk[r] = prior + rank;
+        __builtin_amdgcn_wave_barrier();
+        if (valid && rank == 0) wcnt[wave][d] = prior + (uint32_t)__popcll(m);
+        __builtin_amdgcn_wave_barrier();
+    }
+    __syncthreads();
+    {   // thread = digit: the waves' bases and the digit's tile-local start
+        const uint32_t d = threadIdx.x;
+        uint32_t t = 0;
+#pragma unroll
+        for (uint32_t w = 0; w < PS_WAVES; ++w) {
+            const uint32_t c = wcnt[w][d];
+            wcnt[w][d] = t;
+            t += c;
+        }
+        lstart[d] = block_excl_scan256(t, tmp);
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t r = 0; r < PS_ROUNDS; ++r) {
+        if (seg + r * 64 + lane < n) {
+            const uint32_t d = (k[r] >> shift) & 255u;
+            const uint32_t pos = lstart[d] + wcnt[wave][d] + rk[r];
+            skey[pos] = k[r];
+            sval[pos] = v[r];
+        }
+    }
+    __syncthreads();
+    const uint32_t cnt = n - base < PS_TILE ? n - base : PS_TILE;
+    for (uint32_t j = threadIdx.x; j < cnt; j += PS_BLOCK) {
+        const uint32_t key = skey[j];
+        const uint32_t d = (key >> shift) & 255u;
+        const uint32_t g = gstart[d] + (j - lstart[d]);
+        keys_out[g] = key;
+        vals_out[g] = sval[j];
+    }
+}
+
 // the rows in walk order: the 16 B chunks of words the walk reads (all of a
 // long topic's row, whose later levels it reads as memory words)
 __global__ void __launch_bounds__(PS_BLOCK)
@@ -139,8 +238,12 @@ hipError_t launch_presort(const uint32_t* twords, const uint32_t* meta, uint32_t
         hipLaunchKernelGGL(tm_presort_count, dim3(tiles), dim3(PS_BLOCK), 0, st, ka, n, shift, qb.sort_counts);
         hipError_t err = launch_scan(qb.sort_counts, nc, qb.sort_off, qb.sort_off + nc, qb.sort_scan, st);
         if (err != hipSuccess) return err;
-        hipLaunchKernelGGL(tm_presort_scatter, dim3(tiles), dim3(PS_BLOCK), 0, st, ka, va, n, shift, qb.sort_off,
-                           kb, vb);
+        if (TM_PS_LOCAL)
+            hipLaunchKernelGGL(tm_presort_scatter_ls, dim3(tiles), dim3(PS_BLOCK), 0, st, ka, va, n, shift,
+                               qb.sort_off, kb, vb);
+        else
+            hipLaunchKernelGGL(tm_presort_scatter, dim3(tiles), dim3(PS_BLOCK), 0, st, ka, va, n, shift,
+                               qb.sort_off, kb, vb);
         uint32_t* t = ka;
         ka = kb;
         kb = t;
