@@ -314,11 +314,17 @@ def stream_handle(stream):
     device's current stream -- the fills and copies of the tensors the caller
     just made for this call: torch's side streams are non-blocking, so
     without the wait a zero-fill of an output total could land after the
-    engine has written it."""
+    engine has written it.  Torch's default stream has handle 0, which the
+    C-ABI reads as "the engine's own (non-blocking) stream": that stream
+    cannot wait on it, so its queued work is finished on the host first (the
+    caller then synchronizes the device before reading the results)."""
     if stream is None or isinstance(stream, int):
         return stream
     import torch
     cur = torch.cuda.current_stream(stream.device)
-    if cur.cuda_stream != stream.cuda_stream:
+    if stream.cuda_stream == 0:
+        cur.synchronize()
+        stream.synchronize()
+    elif cur.cuda_stream != stream.cuda_stream:
         stream.wait_stream(cur)
     return stream.cuda_stream

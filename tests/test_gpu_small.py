@@ -32,6 +32,7 @@ def _small(e, tb, to, cap=None, stream=None, dev=0):
     cap = 64 * n + 1024 if cap is None else cap
     d_i = torch.full((max(cap, 1),), -1, dtype=torch.int32, device=d)
     d_t = torch.full((1,), -1, dtype=torch.int64, device=d)
+    torch.cuda.synchronize(d)   # the fills above are on torch's stream; stream=None runs on the engine's
     e.match_small_device(d_b, d_o, n, int(to[-1] - to[0]), d_c, d_oo, d_i, cap, d_t, stream=stream)
     # the whole device: with no stream (or torch's default stream, handle 0)
     # the call runs on the engine's own stream
