@@ -7,7 +7,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
 D=gpurun_out/${PMC_DIR:-pmc}
-ARGS="--steps 3 --warmup 1 --roof-steps 0 --cpu-sample 0 --check 0 --streams 1 --batches 1 --no-extras ${BENCH_ARGS}"
+ARGS="--steps 3 --warmup 1 --roof-steps 0 --cpu-sample 0 --check 0 --streams 1 --batches 1 --no-extras --weak-topics 0 ${BENCH_ARGS}"
 run() {
   name=$1; shift
   mkdir -p $D/$name
