@@ -502,9 +502,9 @@ struct tm_engine {
     uint32_t walk_bpc = 0;            // option "walk_bpc": walk blocks per CU (0 = full occupancy)
     int xcdq = 1;                     // option "xcdq": per-XCD dequeue ranges in the queue walk (default on)
     int presort = 3;                  // option "presort": walk the batch in the order of a key of its first
-                                      // eight words (presort.hip; 0 = arrival order, 2 the tail order,
-                                      // 3 the tail order for batches up to tail_max topics)
-    uint32_t tail_max = 4u << 20;     // option "tail_max": presort 3's largest tail-ordered batch
+                                      // eight words (presort.hip; 0 = arrival order, 1 the word-hash key,
+                                      // 2 the tail order, 3 by batch size: 1 from sort_min topics, else 2)
+    uint32_t sort_min = 3000000;      // option "sort_min": presort 3's smallest batch in word-hash order
     int layout_mode = 1;              // option "layout": 0 off, 1 auto, 2 every commit (tests)
     size_t created_since_layout = 0;  // nodes created since the last relayout
     uint32_t hot_levels = 4;          // option "hot_levels": relayout puts depths <= H level by level (BFS)
@@ -1918,12 +1918,14 @@ struct tm_engine {
         }
         return k;
     }
-    // the walk order of an n-topic batch: option "presort" 3 tail-orders the
-    // batches whose walk tail (the last lanes of each XCD range, ~0.4 ms a
-    // launch) is a visible share of the walk -- 1M topics: walk -6 %, the
-    // key and one radix pass +0.045 ms; 2M: +1.5 % topics/s, 4M: +0.6 %;
-    // 8M: walk unchanged, +0.15 ms (profiles/r04_tail, r04_i)
-    int presort_of(uint32_t n) const { return presort == 3 ? (n <= tail_max ? 2 : 0) : presort; }
+    // the walk order of an n-topic batch (option "presort" 3; C3, topics/s
+    // against arrival order, profiles/r04_o): the word-hash order shares the
+    // trie's lines between neighbouring lanes and XCD-mates (walk -6 % at 8M)
+    // for four radix passes (+0.30 ms at 8M): 8M +4.8 %, 4M +3.3 %, but 2M
+    // +0.6 % and 1M -5 %; the tail order (heaviest topics first in each XCD
+    // range, one pass) shortens the walk's tail, a fixed ~0.4 ms a launch:
+    // 1M +4 %, 2M +4.5 %, 4M +1.7 %, 8M +0.9 %
+    int presort_of(uint32_t n) const { return presort == 3 ? (n >= sort_min ? 1 : 2) : presort; }
     void ensure_slot(DevState& d, Slot& w, uint32_t n, uint64_t nbytes, uint32_t key_words, int presort) {
         w.twords.ensure((size_t)(n + 1) * WREG * 4);
         w.words.ensure((nbytes + n + 1) * 4);
@@ -1942,8 +1944,10 @@ struct tm_engine {
         w.ws.ensure(QWS_BYTES);
         if (presort) {
             w.perm.ensure((size_t)n * 4 + 4);
-            w.twords_s.ensure((size_t)(n + 1) * WREG * 4);
-            w.meta_s.ensure((size_t)n * 4 + 4);
+            if (key_words || !chunk_rows || stats_enabled) {   // the rows gathered into walk order (by_pos)
+                w.twords_s.ensure((size_t)(n + 1) * WREG * 4);
+                w.meta_s.ensure((size_t)n * 4 + 4);
+            }
             const uint32_t nc = presort_counts(n);
             w.skeys.ensure((size_t)n * 8 + 8);
             w.svals.ensure((size_t)n * 4 + 4);
@@ -3466,9 +3470,9 @@ int tm_set_option(tm_engine* e, const char* name, int64_t value) {
             e->presort = (int)value;
             return TM_OK;
         }
-        if (!std::strcmp(name, "tail_max")) {
+        if (!std::strcmp(name, "sort_min")) {
             if (value < 0 || value > 0xffffffffll) return TM_EINVAL;
-            e->tail_max = (uint32_t)value;
+            e->sort_min = (uint32_t)value;
             return TM_OK;
         }
         if (!std::strcmp(name, "route_gc")) {

@@ -651,10 +651,11 @@ int  tm_rewrite_match_batch_device(tm_rewrite* r, const uint8_t* d_topics, const
  *              (device radix sort); 2 = the tail order: within each XCD
  *              range the topics whose words label the most trie nodes first
  *              (one radix pass), so the walk's last lanes finish on light
- *              topics (batches above wave_walk_max); 3 = the tail order for
- *              batches of at most "tail_max" topics, arrival order above
- *              (default); 0 = arrival order
- *   "tail_max" presort 3's largest tail-ordered batch (default 4194304)
+ *              topics (batches above wave_walk_max); 3 = by batch size:
+ *              1 from "sort_min" topics on, 2 below (default); 0 = arrival
+ *              order
+ *   "sort_min" presort 3's smallest batch walked in word-hash order
+ *              (default 3000000)
  *   "chunk_rows" 1 = a wave copies each taken chunk's 64 tokenized rows to
  *              LDS at once (default), 0 = each lane reads its topic's row
  *   "spill"    1 = ids past a stage row go to per-XCD spill chunks (default),
