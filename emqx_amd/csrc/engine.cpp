@@ -505,6 +505,7 @@ struct tm_engine {
                                       // eight words (presort.hip; 0 = arrival order, 1 the word-hash key,
                                       // 2 the tail order, 3 by batch size: 1 from sort_min topics, else 2)
     uint32_t sort_min = 3000000;      // option "sort_min": presort 3's smallest batch in word-hash order
+    uint32_t sort_bits = 32;          // option "sort_bits": top bits of the word-hash key sorted (8..32, % 8)
     int layout_mode = 1;              // option "layout": 0 off, 1 auto, 2 every commit (tests)
     size_t created_since_layout = 0;  // nodes created since the last relayout
     uint32_t hot_levels = 4;          // option "hot_levels": relayout puts depths <= H level by level (BFS)
@@ -2063,6 +2064,7 @@ struct tm_engine {
         qb.ws = w.ws.as<unsigned long long>();
         qb.perm = presort && !shaped && !(qb.wave_walk && presort == 2) ? w.perm.as<uint32_t>() : nullptr;
         qb.presort_mode = presort == 2 ? 2u : 1u;
+        qb.sort_passes = sort_bits / 8;
         if (presort) {
             qb.sort_keys = w.skeys.as<uint32_t>();
             qb.sort_vals = w.svals.as<uint32_t>();
@@ -3468,6 +3470,11 @@ int tm_set_option(tm_engine* e, const char* name, int64_t value) {
         if (!std::strcmp(name, "presort")) {   // 0 arrival order, 1 word-hash key, 2 the tail order, 3 auto
             if (value < 0 || value > 3) return TM_EINVAL;
             e->presort = (int)value;
+            return TM_OK;
+        }
+        if (!std::strcmp(name, "sort_bits")) {
+            if (value < 8 || value > 32 || value % 8) return TM_EINVAL;
+            e->sort_bits = (uint32_t)value;
             return TM_OK;
         }
         if (!std::strcmp(name, "sort_min")) {

@@ -39,7 +39,11 @@ struct QueueBufs {
     uint64_t* scan_tmp;   // scan_tmp_elems(n)
     unsigned long long* ws;   // QWS_BYTES of queue heads
     uint32_t* perm;       // option "presort": queue position -> topic (n), or null (arrival order)
-    uint32_t presort_mode = 1;   // 1: key of the first eight words (4 radix passes); 2: the tail order
+    uint32_t presort_mode = 1;   // 1: key of the first eight words; 2: the tail order (one radix pass)
+    uint32_t sort_passes = 4;    // mode 1: radix passes over the key's top 8 * sort_passes bits (1..4)
+    // the radix passes of the batch's presort: the tokenizer writes the keys
+    // and values where the first pass reads them, so the last ends in perm
+    uint32_t presort_passes() const { return presort_mode == 2 ? 1u : sort_passes; }
                                  // (kernels.hip tail_key: heavy topics first in each XCD range, 1 pass)
     // option "presort": the batch walked in the order of a 32-bit key of
     // its first eight words (each hashed, level-major: 6,5,5,4,4,3,3,2 bits),

@@ -1841,12 +1841,12 @@ hipError_t launch_queue(bool stats_mode, bool xcdq, const ImageView& im, const u
     const int ch = (lane_walk && !keys && !stats_mode && qb.chunk_rows) ? CH_ROWS : CH_NONE;
     const bool by_pos = queue_rows_by_position(qb, stats_mode);   // presorted without chunk rows
     mark(0);
-    // presort keys / values where launch_presort's first pass reads them (the
-    // tail order's single pass reads the second halves and ends in perm)
-    const bool tail = qb.presort_mode == 2;
+    // presort keys / values where launch_presort's first pass reads them (an
+    // odd number of passes starts from the second halves, so it ends in perm)
+    const bool odd = (qb.presort_passes() & 1u) != 0;
     hipLaunchKernelGGL(tm_tokenize, g, blk, 0, st, im, bytes, off, n, qb.twords, qb.words, qb.meta,
-                       qb.perm ? qb.sort_keys + (tail ? n : 0u) : nullptr,
-                       qb.perm ? (tail ? qb.sort_vals : qb.perm) : nullptr, qb.presort_mode);
+                       qb.perm ? qb.sort_keys + (odd ? n : 0u) : nullptr,
+                       qb.perm ? (odd ? qb.sort_vals : qb.perm) : nullptr, qb.presort_mode);
     if (qb.perm) {   // option "presort": perm (and the rows in walk order unless chunk rows read them by perm)
         err = launch_presort(qb.twords, qb.meta, n, qb, st, by_pos);
         if (err != hipSuccess) return err;

@@ -222,19 +222,22 @@ hipError_t launch_presort(const uint32_t* twords, const uint32_t* meta, uint32_t
     if (n == 0) return hipSuccess;
     const uint32_t tiles = (n + PS_TILE - 1) / PS_TILE, nc = 256u * tiles;
     // ping-pong: keys A = sort_keys, B = sort_keys + n; values A = perm, B = sort_vals;
-    // four passes end in A, so perm holds the order
-    // (the tokenizer wrote the keys and values t: kernels.hip presort_key)
+    // an even number of passes starts in A, an odd one in B, so the last ends
+    // in A and perm holds the order (the tokenizer wrote the keys and values
+    // t there: kernels.hip presort_key / tail_key).  Passes sort the key's
+    // top 8 * passes bits (the tail order's key is 8 bits: one pass).
+    const uint32_t passes = qb.presort_passes();
+    if (passes < 1 || passes > 4) return hipErrorInvalidValue;
     uint32_t *ka = qb.sort_keys, *kb = qb.sort_keys + n, *va = qb.perm, *vb = qb.sort_vals;
-    uint32_t passes = 4;
-    if (qb.presort_mode == 2) {   // the tail order: one pass of an 8-bit key, B -> A (perm)
+    if (passes & 1u) {
         ka = qb.sort_keys + n;
         kb = qb.sort_keys;
         va = qb.sort_vals;
         vb = qb.perm;
-        passes = 1;
     }
+    const uint32_t low = qb.presort_mode == 2 ? 0u : 32u - 8u * passes;   // the lowest key bit sorted
     for (uint32_t pass = 0; pass < passes; ++pass) {
-        const uint32_t shift = 8 * pass;
+        const uint32_t shift = low + 8 * pass;
         hipLaunchKernelGGL(tm_presort_count, dim3(tiles), dim3(PS_BLOCK), 0, st, ka, n, shift, qb.sort_counts);
         hipError_t err = launch_scan(qb.sort_counts, nc, qb.sort_off, qb.sort_off + nc, qb.sort_scan, st);
         if (err != hipSuccess) return err;

@@ -251,7 +251,10 @@ VARIANTS = {"queue": {}, "queue_xcd": {}, "queue_xcd@nosplit@dfs": {"split": 0, 
             "queue_xcd@rows@presort": {"presort": 1},
             # the tail order (presort 2: heavy topics first in each XCD range, one radix pass)
             "queue_xcd@tail": {"presort": 2}, "queue@tail@stagek8": {"presort": 2, "stage_k": 8},
-            "queue_xcd@tail@norows@nospill": {"presort": 2, "chunk_rows": 0, "spill": 0}}
+            "queue_xcd@tail@norows@nospill": {"presort": 2, "chunk_rows": 0, "spill": 0},
+            # presort 1 over the key's top 24 / 16 bits (3 / 2 radix passes: odd and even)
+            "queue_xcd@presort@bits24": {"presort": 1, "sort_bits": 24},
+            "queue_xcd@presort@bits16@norows": {"presort": 1, "sort_bits": 16, "chunk_rows": 0}}
 
 
 @pytest.mark.parametrize("variant", list(VARIANTS))
