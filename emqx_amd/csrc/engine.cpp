@@ -505,7 +505,9 @@ struct tm_engine {
                                       // eight words (presort.hip; 0 = arrival order, 1 the word-hash key,
                                       // 2 the tail order, 3 by batch size: 1 from sort_min topics, else 2)
     uint32_t sort_min = 3000000;      // option "sort_min": presort 3's smallest batch in word-hash order
-    uint32_t sort_bits = 32;          // option "sort_bits": top bits of the word-hash key sorted (8..32, % 8)
+    uint32_t sort_bits = 16;          // option "sort_bits": top bits of the word-hash key sorted (8..32, % 8;
+                                      // 16 = two radix passes: the walk as fast as with 32, 0.15 ms less
+                                      // sort at 8M topics, profiles/r04_p)
     int layout_mode = 1;              // option "layout": 0 off, 1 auto, 2 every commit (tests)
     size_t created_since_layout = 0;  // nodes created since the last relayout
     uint32_t hot_levels = 4;          // option "hot_levels": relayout puts depths <= H level by level (BFS)

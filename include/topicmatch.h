@@ -657,7 +657,7 @@ int  tm_rewrite_match_batch_device(tm_rewrite* r, const uint8_t* d_topics, const
  *   "sort_min" presort 3's smallest batch walked in word-hash order
  *              (default 3000000)
  *   "sort_bits" the word-hash key's top bits that presort 1 sorts, one radix
- *              pass per 8 (8..32, default 32)
+ *              pass per 8 (8..32, default 16)
  *   "chunk_rows" 1 = a wave copies each taken chunk's 64 tokenized rows to
  *              LDS at once (default), 0 = each lane reads its topic's row
  *   "spill"    1 = ids past a stage row go to per-XCD spill chunks (default),
