@@ -28,7 +28,7 @@ for s in ${STEPS:-tests}; do
     smoke) timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 ;;
     bench) timeout -k 10 ${T_BENCH:-600} python -u bench.py ${BENCH_ARGS} > "$OUT/bench.json" 2> "$OUT/bench.log" ;;
     prof)  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
-             python3 bench.py --steps 10 --warmup 2 --cpu-sample 0 --check 0 --streams 1 --no-extras ${BENCH_ARGS} \
+             python3 bench.py --steps 10 --warmup 2 --cpu-sample 0 --check 0 --streams 1 --no-extras --weak-topics 0 ${BENCH_ARGS} \
              > "$OUT/prof_bench.json" 2> "$OUT/prof_bench.log" ;;
     pmc)   PMC_DIR=${TAG:-job}/pmc bash tools/pmc_passes.sh ;;
     prof3) timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof3" -o run -- \
