@@ -220,6 +220,7 @@ struct Slot {
     uint64_t* h_maxc = nullptr;     // pinned copy of the slot's ws after its last walk (largest match count,
                                     // spill chunks taken per XCD)
     hipEvent_t maxc_ev = nullptr, done = nullptr;
+    hipEvent_t tail_fork = nullptr, tail_join = nullptr;   // option "tail_wave": the tail walk's stream fork / join
     bool maxc_pending = false, used = false, keyed = false, shaped = false;
     // the slot's last batch, for a re-copy into a larger output (no re-walk)
     uint32_t n = 0, K = 0, kw = 1;
@@ -273,6 +274,7 @@ struct DevState {
     int device = -1;
     hipStream_t stream = nullptr;
     hipStream_t ustream = nullptr;   // commits: image uploads and scatters (never behind a batch on `stream`)
+    hipStream_t tstream = nullptr;   // option "tail_wave": tm_walk_tail beside the persistent walk (made on first use)
     // trie image + dictionary, two epochs (Image)
     Image img[2];
     int cur = 0;                          // the image new batches pin (switched by commit, under the engine lock)
@@ -374,6 +376,7 @@ struct DevState {
         (void)hipSetDevice(device);
         if (stream) (void)hipStreamSynchronize(stream);
         if (ustream) (void)hipStreamSynchronize(ustream);
+        if (tstream) (void)hipStreamSynchronize(tstream);
         if (rw_done) (void)hipEventDestroy(rw_done);
         img[0].release();
         img[1].release();
@@ -385,9 +388,11 @@ struct DevState {
         for (auto& w : slots) {
             for (DevBuf* b : {&w.twords, &w.words, &w.path, &w.meta, &w.scan, &w.stage, &w.kstage, &w.ws, &w.stats,
                               &w.perm, &w.skeys, &w.svals, &w.scount, &w.soff, &w.sscan, &w.twords_s, &w.meta_s,
-                              &w.spill, &w.spill_head})
+                              &w.spill, &w.spill_head, &w.sctl})
                 b->release();
             if (w.done) (void)hipEventDestroy(w.done);
+            if (w.tail_fork) (void)hipEventDestroy(w.tail_fork);
+            if (w.tail_join) (void)hipEventDestroy(w.tail_join);
             if (w.maxc_ev) (void)hipEventDestroy(w.maxc_ev);
             if (w.h_maxc) (void)hipHostFree(w.h_maxc);
         }
@@ -398,7 +403,8 @@ struct DevState {
             }
         if (stream) (void)hipStreamDestroy(stream);
         if (ustream) (void)hipStreamDestroy(ustream);
-        stream = ustream = nullptr;
+        if (tstream) (void)hipStreamDestroy(tstream);
+        stream = ustream = tstream = nullptr;
     }
 };
 
@@ -505,6 +511,7 @@ struct tm_engine {
                                       // eight words (presort.hip; 0 = arrival order, 1 the word-hash key,
                                       // 2 the tail order, 3 by batch size: 1 from sort_min topics, else 2)
     uint32_t sort_min = 3000000;      // option "sort_min": presort 3's smallest batch in word-hash order
+    uint32_t tail_wave = 0;           // option "tail_wave": queue positions per XCD range walked by tm_walk_tail
     uint32_t sort_bits = 16;          // option "sort_bits": top bits of the word-hash key sorted (8..32, % 8;
                                       // 16 = two radix passes: the walk as fast as with 32, 0.15 ms less
                                       // sort at 8M topics, profiles/r04_p)
@@ -2081,6 +2088,15 @@ struct tm_engine {
             qb.spill_head = w.spill_head.as<uint32_t>();
             qb.spill_chunks = w.spill_chunks;
         }
+        if (tail_wave && !kw && !stats_enabled && n / 8 > 4u * tail_wave) {   // 8 XCD ranges
+            if (!d.tstream) HIPCHK(hipStreamCreateWithFlags(&d.tstream, hipStreamNonBlocking));
+            if (!w.tail_fork) HIPCHK(hipEventCreateWithFlags(&w.tail_fork, hipEventDisableTiming));
+            if (!w.tail_join) HIPCHK(hipEventCreateWithFlags(&w.tail_join, hipEventDisableTiming));
+            qb.tail_wave = tail_wave;
+            qb.tail_stream = d.tstream;
+            qb.tail_fork = w.tail_fork;
+            qb.tail_join = w.tail_join;
+        }
         w.sorted = queue_rows_by_position(qb, stats_enabled);   // the copy-out moves rows by perm
         HIPCHK(launch_queue(stats_enabled, xcdq != 0, im, bytes, off, n, qb, d.stage_k, counts, out_off, ids, keys,
                             cap, total, sp, st, timing_enabled ? marks : nullptr, walk_bpc, hist_enabled != 0,
@@ -3472,6 +3488,11 @@ int tm_set_option(tm_engine* e, const char* name, int64_t value) {
         if (!std::strcmp(name, "presort")) {   // 0 arrival order, 1 word-hash key, 2 the tail order, 3 auto
             if (value < 0 || value > 3) return TM_EINVAL;
             e->presort = (int)value;
+            return TM_OK;
+        }
+        if (!std::strcmp(name, "tail_wave")) {
+            if (value < 0 || value > (1 << 24)) return TM_EINVAL;
+            e->tail_wave = (uint32_t)value;
             return TM_OK;
         }
         if (!std::strcmp(name, "sort_bits")) {

@@ -39,22 +39,23 @@ struct QueueBufs {
     uint64_t* scan_tmp;   // scan_tmp_elems(n)
     unsigned long long* ws;   // QWS_BYTES of queue heads
     uint32_t* perm;       // option "presort": queue position -> topic (n), or null (arrival order)
-    uint32_t presort_mode = 1;   // 1: key of the first eight words; 2: the tail order (one radix pass)
+    uint32_t presort_mode = 1;   // 1: key of the first eight words; 2: the tail order (kernels.hip
+                                 // tail_key: heavy topics first in each XCD range, one radix pass)
     uint32_t sort_passes = 4;    // mode 1: radix passes over the key's top 8 * sort_passes bits (1..4)
     // the radix passes of the batch's presort: the tokenizer writes the keys
     // and values where the first pass reads them, so the last ends in perm
     uint32_t presort_passes() const { return presort_mode == 2 ? 1u : sort_passes; }
-                                 // (kernels.hip tail_key: heavy topics first in each XCD range, 1 pass)
     // option "presort": the batch walked in the order of a 32-bit key of
     // its first eight words (each hashed, level-major: 6,5,5,4,4,3,3,2 bits),
     // so a wave's 64 lanes walk shared prefixes -- their loads of one node
     // are one request, and a prefix's nodes are hot in L2 while its topics
-    // run.  An LSD radix sort, 4 passes of 8 bits (presort.hip): 2n u32 keys
+    // run.  An LSD radix sort of the key's top bits (presort.hip): 2n u32 keys
     // (the first n written by the tokenizer), n u32 values (ping-pong with
     // perm), presort_counts(n) u32 and
     // presort_counts(n) + 1 u64 offsets, scan_tmp_elems(presort_counts(n))
-    // The walk then reads twords_s / meta_s (the rows in walk order) and
-    // writes stage row p for position p; copy-out moves row p to topic
+    // With chunk rows the walk reads each chunk's rows through perm; without,
+    // it reads twords_s / meta_s (the rows gathered into walk order) and
+    // writes stage row p for position p, and copy-out moves row p to topic
     // perm[p] (launch_copy: the perm of the batch's walk, or null).
     uint32_t* sort_keys = nullptr;
     uint32_t* sort_vals = nullptr;
@@ -66,6 +67,15 @@ struct QueueBufs {
     uint32_t* spill = nullptr;      // spill_chunks x SPILL_CHUNK (null: fan-out beyond K re-walks)
     uint32_t* spill_head = nullptr; // n
     uint32_t spill_chunks = 0;      // a multiple of 8
+    // option "tail_wave": the last tail_wave queue positions of each XCD
+    // range are walked by tm_walk_tail (a wave per topic, level by level) on
+    // tail_stream, concurrently: its blocks take the CU slots the persistent
+    // walk's waves give up when its queue runs dry, so the launch's tail is
+    // cut into short per-topic wave walks instead of waiting on the last
+    // lanes' whole topics (unkeyed chunk-row walks with per-XCD ranges only)
+    uint32_t tail_wave = 0;
+    hipStream_t tail_stream = nullptr;
+    hipEvent_t tail_fork = nullptr, tail_join = nullptr;
 };
 // digit counters of the presort of n topics (256 per 4096-topic tile)
 uint32_t presort_counts(uint32_t n);

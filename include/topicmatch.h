@@ -656,6 +656,10 @@ int  tm_rewrite_match_batch_device(tm_rewrite* r, const uint8_t* d_topics, const
  *              order
  *   "sort_min" presort 3's smallest batch walked in word-hash order
  *              (default 3000000)
+ *   "tail_wave" the last tail_wave positions of each of the walk's 8 XCD
+ *              ranges are walked a wave per topic (tm_walk_tail) on a second
+ *              stream beside the persistent walk, in the slots its waves give
+ *              up as its queue runs dry (0 = off)
  *   "sort_bits" the word-hash key's top bits that presort 1 sorts, one radix
  *              pass per 8 (8..32, default 16)
  *   "chunk_rows" 1 = a wave copies each taken chunk's 64 tokenized rows to

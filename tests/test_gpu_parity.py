@@ -254,7 +254,11 @@ VARIANTS = {"queue": {}, "queue_xcd": {}, "queue_xcd@nosplit@dfs": {"split": 0, 
             "queue_xcd@tail@norows@nospill": {"presort": 2, "chunk_rows": 0, "spill": 0},
             # presort 1 over the key's top 24 / 16 bits (3 / 2 radix passes: odd and even)
             "queue_xcd@presort@bits24": {"presort": 1, "sort_bits": 24},
-            "queue_xcd@presort@bits16@norows": {"presort": 1, "sort_bits": 16, "chunk_rows": 0}}
+            "queue_xcd@presort@bits16@norows": {"presort": 1, "sort_bits": 16, "chunk_rows": 0},
+            # the last positions of each XCD range walked a wave per topic on a second stream
+            "queue_xcd@tailwave": {"tail_wave": 256},
+            "queue_xcd@tailwave@presort@stagek8": {"tail_wave": 512, "presort": 1, "stage_k": 8, "stage_auto": 0},
+            "queue_xcd@tailwave@tail@nospill": {"tail_wave": 256, "presort": 2, "spill": 0}}
 
 
 @pytest.mark.parametrize("variant", list(VARIANTS))
