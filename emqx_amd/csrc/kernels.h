@@ -13,6 +13,7 @@ constexpr size_t QWS_BYTES = 2048;   // queue heads: 8 ranges x 128 B, then 8 sp
 constexpr size_t QWS_MAXC = 120;     // u64 slot of ws: the batch's largest match count
 constexpr size_t QWS_MAXL = 121;     // u64 slot of ws: most levels of a topic in a keyed batch
 constexpr size_t QWS_SPILL = 128;    // u64 slots 128 + 16 x: spill chunks taken by XCD x's waves
+constexpr size_t QWS_TAIL = 4;       // u64 slots 4 + 16 r: tm_walk_tail's next position of range r's tail
 // Spill chunks (unkeyed walks): ids of a topic past its K-slot stage row go
 // to chunks of SPILL_CHUNK u32 -- slot 0 the next chunk of the topic, slots
 // 1.. ids in discovery order -- taken from the walking XCD's area (capacity

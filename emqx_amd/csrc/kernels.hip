@@ -1297,7 +1297,7 @@ tm_walk_wave(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const u
 // tm_walk_tail (option "tail_wave", QueueBufs): the last tailz queue
 // positions of each XCD range, one wave per topic level by level, launched
 // beside tm_walk_queue on its own stream.  A wave takes positions of its own
-// XCD's range from a per-range counter (ws + 16 r + 8), then the other
+// XCD's range from a per-range counter (ws + QWS_TAIL + 16 r), then the other
 // ranges'.  Stage rows, counts and spill heads by topic, as the chunk-row
 // walk writes them (lists past K: spill_head NO_SPILL, the copy-out re-walks).
 __global__ void __launch_bounds__(BLOCK)
@@ -1315,7 +1315,7 @@ tm_walk_tail(ImageView im, const uint64_t* __restrict__ off, uint32_t n, uint32_
         const uint32_t re = (uint32_t)((uint64_t)n * (r + 1) / QRANGES);
         const uint32_t z = tailz < re - rb ? tailz : re - rb;
         uint32_t k = 0;
-        if (lane == 0) k = (uint32_t)atomicAdd(ws + 16 * r + 8, 1ull);
+        if (lane == 0) k = (uint32_t)atomicAdd(ws + QWS_TAIL + 16 * r, 1ull);
         k = (uint32_t)__shfl((int)k, 0, 64);
         if (k >= z) {   // this range's tail is taken: the next range's (uniform)
             if (++tried == QRANGES) break;

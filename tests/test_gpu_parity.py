@@ -101,7 +101,12 @@ def _by_id(o1, eng, tb, to, threads=16):
     oc, oo, oi = o1.match_ids(tb, to, threads=threads)
     assert np.array_equal(ec, oc)
     assert np.array_equal(eo, oo)
-    assert np.array_equal(ei, oi)
+    if not np.array_equal(ei, oi):   # name the topics whose lists differ
+        bad = [t for t in range(len(oc)) if not np.array_equal(ei[oo[t]:oo[t + 1]], oi[oo[t]:oo[t + 1]])]
+        t = bad[0]
+        raise AssertionError(f"{len(bad)} of {len(oc)} topics differ, first {t} "
+                             f"{bytes(tb[to[t]:to[t + 1]])!r}: got {ei[oo[t]:oo[t + 1]].tolist()} "
+                             f"want {oi[oo[t]:oo[t + 1]].tolist()}; topics {bad[:12]}")
     return ec
 
 
