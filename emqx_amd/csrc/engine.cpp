@@ -1936,6 +1936,8 @@ struct tm_engine {
     // range, one pass) shortens the walk's tail, a fixed ~0.4 ms a launch:
     // 1M +4 %, 2M +4.5 %, 4M +1.7 %, 8M +0.9 %
     int presort_of(uint32_t n) const { return presort == 3 ? (n >= sort_min ? 1 : 2) : presort; }
+    // (presort 4: the tail order, then the word-hash key within each heat
+    // class; 5: the word-hash key within each XCD range -- A/B orders)
     void ensure_slot(DevState& d, Slot& w, uint32_t n, uint64_t nbytes, uint32_t key_words, int presort) {
         w.twords.ensure((size_t)(n + 1) * WREG * 4);
         w.words.ensure((nbytes + n + 1) * 4);
@@ -2067,12 +2069,12 @@ struct tm_engine {
         qb.kstage = kw ? w.kstage.as<uint64_t>() : nullptr;
         qb.shaped = shaped;
         // the tail order (presort 2) leaves small batches to the wave walk
-        qb.wave_walk = n <= wave_walk_max && !kw && presort != 1;
+        qb.wave_walk = n <= wave_walk_max && !kw && presort != 1;   // (the range-keyed orders: 2, 4, 5)
         qb.chunk_rows = chunk_rows;
         qb.scan_tmp = w.scan.as<uint64_t>();
         qb.ws = w.ws.as<unsigned long long>();
-        qb.perm = presort && !shaped && !(qb.wave_walk && presort == 2) ? w.perm.as<uint32_t>() : nullptr;
-        qb.presort_mode = presort == 2 ? 2u : 1u;
+        qb.perm = presort && !shaped && !(qb.wave_walk && presort >= 2) ? w.perm.as<uint32_t>() : nullptr;
+        qb.presort_mode = presort >= 2 ? (uint32_t)presort : 1u;
         qb.sort_passes = sort_bits / 8;
         if (presort) {
             qb.sort_keys = w.skeys.as<uint32_t>();
@@ -3486,7 +3488,7 @@ int tm_set_option(tm_engine* e, const char* name, int64_t value) {
             return TM_OK;
         }
         if (!std::strcmp(name, "presort")) {   // 0 arrival order, 1 word-hash key, 2 the tail order, 3 auto
-            if (value < 0 || value > 3) return TM_EINVAL;
+            if (value < 0 || value > 5) return TM_EINVAL;
             e->presort = (int)value;
             return TM_OK;
         }

@@ -286,7 +286,13 @@ __device__ __forceinline__ void tokenize_one(const ImageView& im, const B& bytes
     const uint32_t dollar = (e > b && bytes.byte(b) == '$') ? 1u : 0u;
     meta[t] = lev | (dollar << 31) | (lev > WREG ? MLONG : 0u) | (ood ? MOOD : 0u);
     if (skeys) {   // option "presort": the walk-order key (presort.hip)
-        skeys[t] = key_mode == 2 ? tail_key(im, tw, lev, t, n) : presort_key(tw, lev);
+        // 2: the tail order (8 bits); 4: the tail order, then the word-hash
+        // key's top 8 bits within a heat class (16); 5: the XCD range, then
+        // the word-hash key's top 13 bits (16); 1: the word-hash key (32)
+        skeys[t] = key_mode == 2   ? tail_key(im, tw, lev, t, n)
+                   : key_mode == 4 ? tail_key(im, tw, lev, t, n) << 8 | presort_key(tw, lev) >> 24
+                   : key_mode == 5 ? (tail_key(im, tw, lev, t, n) >> 5) << 13 | presort_key(tw, lev) >> 19
+                                   : presort_key(tw, lev);
         svals[t] = t;
     }
 }

@@ -235,7 +235,9 @@ hipError_t launch_presort(const uint32_t* twords, const uint32_t* meta, uint32_t
         va = qb.sort_vals;
         vb = qb.perm;
     }
-    const uint32_t low = qb.presort_mode == 2 ? 0u : 32u - 8u * passes;   // the lowest key bit sorted
+    // the lowest key bit sorted: the range-keyed orders (2, 4, 5) sort their
+    // whole 8 / 16-bit key, the word-hash key (1) its top 8 x passes bits
+    const uint32_t low = qb.presort_mode >= 2 ? 0u : 32u - 8u * passes;
     for (uint32_t pass = 0; pass < passes; ++pass) {
         const uint32_t shift = low + 8 * pass;
         hipLaunchKernelGGL(tm_presort_count, dim3(tiles), dim3(PS_BLOCK), 0, st, ka, n, shift, qb.sort_counts);

@@ -263,7 +263,9 @@ VARIANTS = {"queue": {}, "queue_xcd": {}, "queue_xcd@nosplit@dfs": {"split": 0, 
             # the last positions of each XCD range walked a wave per topic on a second stream
             "queue_xcd@tailwave": {"tail_wave": 256},
             "queue_xcd@tailwave@presort@stagek8": {"tail_wave": 512, "presort": 1, "stage_k": 8, "stage_auto": 0},
-            "queue_xcd@tailwave@tail@nospill": {"tail_wave": 256, "presort": 2, "spill": 0}}
+            "queue_xcd@tailwave@tail@nospill": {"tail_wave": 256, "presort": 2, "spill": 0},
+            # range-keyed orders with a word-hash part (two radix passes)
+            "queue_xcd@order4": {"presort": 4}, "queue_xcd@order5@stagek8": {"presort": 5, "stage_k": 8}}
 
 
 @pytest.mark.parametrize("variant", list(VARIANTS))
