@@ -509,8 +509,9 @@ struct tm_engine {
     int xcdq = 1;                     // option "xcdq": per-XCD dequeue ranges in the queue walk (default on)
     int presort = 3;                  // option "presort": walk the batch in the order of a key of its first
                                       // eight words (presort.hip; 0 = arrival order, 1 the word-hash key,
-                                      // 2 the tail order, 3 by batch size: 1 from sort_min topics, else 2)
-    uint32_t sort_min = 3000000;      // option "sort_min": presort 3's smallest batch in word-hash order
+                                      // 2 the tail order, 5 the word-hash key within each XCD range, 3 by
+                                      // batch size: 5 from sort_min topics, else 2)
+    uint32_t sort_min = 3000000;      // option "sort_min": presort 3's smallest batch in range-local word-hash order
     uint32_t tail_wave = 0;           // option "tail_wave": queue positions per XCD range walked by tm_walk_tail
     uint32_t sort_bits = 16;          // option "sort_bits": top bits of the word-hash key sorted (8..32, % 8;
                                       // 16 = two radix passes: the walk as fast as with 32, 0.15 ms less
@@ -1928,14 +1929,16 @@ struct tm_engine {
         }
         return k;
     }
-    // the walk order of an n-topic batch (option "presort" 3; C3, topics/s
-    // against arrival order, profiles/r04_o): the word-hash order shares the
-    // trie's lines between neighbouring lanes and XCD-mates (walk -6 % at 8M)
-    // for four radix passes (+0.30 ms at 8M): 8M +4.8 %, 4M +3.3 %, but 2M
-    // +0.6 % and 1M -5 %; the tail order (heaviest topics first in each XCD
-    // range, one pass) shortens the walk's tail, a fixed ~0.4 ms a launch:
-    // 1M +4 %, 2M +4.5 %, 4M +1.7 %, 8M +0.9 %
-    int presort_of(uint32_t n) const { return presort == 3 ? (n >= sort_min ? 1 : 2) : presort; }
+    // the walk order of an n-topic batch (option "presort" 3; C3, topics/s,
+    // profiles/r04_o, r04_s): the word-hash order shares the trie's lines
+    // between neighbouring lanes; sorted within each XCD range (5: every
+    // prefix spread over all XCDs, each XCD's lanes grouped by prefix) it
+    // beats the global sort (1: a key slice per XCD, so the hot prefixes
+    // crowd one XCD): 8M 795-797M vs 767M (1) vs 741M (2), 4M 744-748M vs
+    // 730M vs 711M; the tail order (2: heaviest topics first in each range,
+    // one radix pass) shortens the walk's fixed ~0.4 ms tail and wins below
+    // ~3M: 1M 622-624M vs 597-603M (5)
+    int presort_of(uint32_t n) const { return presort == 3 ? (n >= sort_min ? 5 : 2) : presort; }
     // (presort 4: the tail order, then the word-hash key within each heat
     // class; 5: the word-hash key within each XCD range -- A/B orders)
     void ensure_slot(DevState& d, Slot& w, uint32_t n, uint64_t nbytes, uint32_t key_words, int presort) {

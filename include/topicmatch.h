@@ -651,12 +651,12 @@ int  tm_rewrite_match_batch_device(tm_rewrite* r, const uint8_t* d_topics, const
  *              (device radix sort); 2 = the tail order: within each XCD
  *              range the topics whose words label the most trie nodes first
  *              (one radix pass), so the walk's last lanes finish on light
- *              topics (batches above wave_walk_max); 3 = by batch size:
- *              1 from "sort_min" topics on, 2 below (default); 0 = arrival
+ *              topics (batches above wave_walk_max); 5 = the word-hash key
+ *              within each XCD range (two radix passes); 3 = by batch size:
+ *              5 from "sort_min" topics on, 2 below (default); 0 = arrival
  *              order; 4 = the tail order, then the word-hash key within a
- *              heat class, 5 = the word-hash key within each XCD range
- *              (both two radix passes; A/B orders)
- *   "sort_min" presort 3's smallest batch walked in word-hash order
+ *              heat class (A/B)
+ *   "sort_min" presort 3's smallest batch walked in range-local word-hash order
  *              (default 3000000)
  *   "tail_wave" the last tail_wave positions of each of the walk's 8 XCD
  *              ranges are walked a wave per topic (tm_walk_tail) on a second
