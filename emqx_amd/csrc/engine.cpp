@@ -513,9 +513,10 @@ struct tm_engine {
                                       // batch size: 5 from sort_min topics, else 2)
     uint32_t sort_min = 3000000;      // option "sort_min": presort 3's smallest batch in range-local word-hash order
     uint32_t tail_wave = 0;           // option "tail_wave": queue positions per XCD range walked by tm_walk_tail
-    uint32_t sort_bits = 16;          // option "sort_bits": top bits of the word-hash key sorted (8..32, % 8;
-                                      // 16 = two radix passes: the walk as fast as with 32, 0.15 ms less
-                                      // sort at 8M topics, profiles/r04_p)
+    uint32_t sort_bits = 24;          // option "sort_bits": key bits sorted (8..32, % 8; one radix pass per
+                                      // 8): presort 1 sorts the word-hash key's top bits (16 walk as fast as
+                                      // 32, profiles/r04_p), presort 5 the range's 3 bits over the key's top
+                                      // sort_bits - 3 (24: 8M +0.6 % over 16, profiles/r04_t)
     int layout_mode = 1;              // option "layout": 0 off, 1 auto, 2 every commit (tests)
     size_t created_since_layout = 0;  // nodes created since the last relayout
     uint32_t hot_levels = 4;          // option "hot_levels": relayout puts depths <= H level by level (BFS)

@@ -45,7 +45,7 @@ struct QueueBufs {
     uint32_t sort_passes = 4;    // mode 1: radix passes over the key's top 8 * sort_passes bits (1..4)
     // the radix passes of the batch's presort: the tokenizer writes the keys
     // and values where the first pass reads them, so the last ends in perm
-    uint32_t presort_passes() const { return presort_mode == 2 ? 1u : presort_mode >= 4 ? 2u : sort_passes; }
+    uint32_t presort_passes() const { return presort_mode == 2 ? 1u : presort_mode == 4 ? 2u : sort_passes; }
     // option "presort": the batch walked in the order of a 32-bit key of
     // its first eight words (each hashed, level-major: 6,5,5,4,4,3,3,2 bits),
     // so a wave's 64 lanes walk shared prefixes -- their loads of one node

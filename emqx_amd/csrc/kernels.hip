@@ -289,10 +289,13 @@ __device__ __forceinline__ void tokenize_one(const ImageView& im, const B& bytes
         // 2: the tail order (8 bits); 4: the tail order, then the word-hash
         // key's top 8 bits within a heat class (16); 5: the XCD range, then
         // the word-hash key's top 13 bits (16); 1: the word-hash key (32)
-        skeys[t] = key_mode == 2   ? tail_key(im, tw, lev, t, n)
-                   : key_mode == 4 ? tail_key(im, tw, lev, t, n) << 8 | presort_key(tw, lev) >> 24
-                   : key_mode == 5 ? (tail_key(im, tw, lev, t, n) >> 5) << 13 | presort_key(tw, lev) >> 19
-                                   : presort_key(tw, lev);
+        // (key_mode: the order | its key bits << 8; 5 takes the range's 3
+        // bits over the word-hash key's top bits - 3)
+        const uint32_t mode = key_mode & 255u, bits = key_mode >> 8;
+        skeys[t] = mode == 2   ? tail_key(im, tw, lev, t, n)
+                   : mode == 4 ? tail_key(im, tw, lev, t, n) << 8 | presort_key(tw, lev) >> 24
+                   : mode == 5 ? (tail_key(im, tw, lev, t, n) >> 5) << (bits - 3) | presort_key(tw, lev) >> (35 - bits)
+                               : presort_key(tw, lev);
         svals[t] = t;
     }
 }
@@ -1922,7 +1925,8 @@ hipError_t launch_queue(bool stats_mode, bool xcdq, const ImageView& im, const u
     const bool odd = (qb.presort_passes() & 1u) != 0;
     hipLaunchKernelGGL(tm_tokenize, g, blk, 0, st, im, bytes, off, n, qb.twords, qb.words, qb.meta,
                        qb.perm ? qb.sort_keys + (odd ? n : 0u) : nullptr,
-                       qb.perm ? (odd ? qb.sort_vals : qb.perm) : nullptr, qb.presort_mode);
+                       qb.perm ? (odd ? qb.sort_vals : qb.perm) : nullptr,
+                       qb.presort_mode | (8u * qb.presort_passes()) << 8);
     if (qb.perm) {   // option "presort": perm (and the rows in walk order unless chunk rows read them by perm)
         err = launch_presort(qb.twords, qb.meta, n, qb, st, by_pos);
         if (err != hipSuccess) return err;

@@ -662,8 +662,9 @@ int  tm_rewrite_match_batch_device(tm_rewrite* r, const uint8_t* d_topics, const
  *              ranges are walked a wave per topic (tm_walk_tail) on a second
  *              stream beside the persistent walk, in the slots its waves give
  *              up as its queue runs dry (0 = off)
- *   "sort_bits" the word-hash key's top bits that presort 1 sorts, one radix
- *              pass per 8 (8..32, default 16)
+ *   "sort_bits" the key bits presort 1 and 5 sort, one radix pass per 8
+ *              (8..32, default 24; presort 5: the XCD range over the
+ *              word-hash key's top sort_bits - 3 bits)
  *   "chunk_rows" 1 = a wave copies each taken chunk's 64 tokenized rows to
  *              LDS at once (default), 0 = each lane reads its topic's row
  *   "spill"    1 = ids past a stage row go to per-XCD spill chunks (default),
