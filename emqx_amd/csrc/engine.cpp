@@ -275,6 +275,12 @@ struct DevState {
     hipStream_t stream = nullptr;
     hipStream_t ustream = nullptr;   // commits: image uploads and scatters (never behind a batch on `stream`)
     hipStream_t tstream = nullptr;   // option "tail_wave": tm_walk_tail beside the persistent walk (made on first use)
+    // the pipelined host-buffer match (host_batch_pipelined): two chunk
+    // workspaces, the read-back stream and the events between them
+    hipStream_t hstream = nullptr;
+    DevBuf hp_bytes[2], hp_off[2], hp_ids[2], hp_outoff[2], hp_total[2];
+    hipEvent_t hp_comp[2] = {nullptr, nullptr}, hp_copy[2] = {nullptr, nullptr};
+    uint64_t* hp_htot = nullptr;     // pinned: the chunk totals
     // trie image + dictionary, two epochs (Image)
     Image img[2];
     int cur = 0;                          // the image new batches pin (switched by commit, under the engine lock)
@@ -383,7 +389,9 @@ struct DevState {
         for (hipEvent_t ev : ev_spare) (void)hipEventDestroy(ev);
         ev_spare.clear();
         for (DevBuf* b : {&stage_dev, &w_rexact, &w_rscan, &w_rids, &w_rcounts, &w_roff, &w_dsrc, &w_dcount, &w_akey,
-                          &w_alarge, &w_mpre, &w_mscan, &w_bytes, &w_off, &w_counts, &w_outoff, &w_ids, &w_total})
+                          &w_alarge, &w_mpre, &w_mscan, &w_bytes, &w_off, &w_counts, &w_outoff, &w_ids, &w_total,
+                          &hp_bytes[0], &hp_bytes[1], &hp_off[0], &hp_off[1], &hp_ids[0], &hp_ids[1], &hp_outoff[0],
+                          &hp_outoff[1], &hp_total[0], &hp_total[1]})
             b->release();
         for (auto& w : slots) {
             for (DevBuf* b : {&w.twords, &w.words, &w.path, &w.meta, &w.scan, &w.stage, &w.kstage, &w.ws, &w.stats,
@@ -404,6 +412,18 @@ struct DevState {
         if (stream) (void)hipStreamDestroy(stream);
         if (ustream) (void)hipStreamDestroy(ustream);
         if (tstream) (void)hipStreamDestroy(tstream);
+        if (hstream) {
+            (void)hipStreamSynchronize(hstream);
+            (void)hipStreamDestroy(hstream);
+        }
+        for (int j = 0; j < 2; ++j) {
+            if (hp_comp[j]) (void)hipEventDestroy(hp_comp[j]);
+            if (hp_copy[j]) (void)hipEventDestroy(hp_copy[j]);
+            hp_comp[j] = hp_copy[j] = nullptr;
+        }
+        if (hp_htot) (void)hipHostFree(hp_htot);
+        hp_htot = nullptr;
+        hstream = nullptr;
         stream = ustream = tstream = nullptr;
     }
 };
@@ -513,6 +533,8 @@ struct tm_engine {
                                       // batch size: 5 from sort_min topics, else 2)
     uint32_t sort_min = 3000000;      // option "sort_min": presort 3's smallest batch in range-local word-hash order
     uint32_t tail_wave = 0;           // option "tail_wave": queue positions per XCD range walked by tm_walk_tail
+    int host_pipeline = 1;            // option "host_pipeline": host-buffer match/1 batches of >= 2M topics on
+                                      // one replica go up, walk and come back in 1M-topic chunks, overlapped
     uint32_t sort_bits = 24;          // option "sort_bits": key bits sorted (8..32, % 8; one radix pass per
                                       // 8): presort 1 sorts the word-hash key's top bits (16 walk as fast as
                                       // 32, profiles/r04_p), presort 5 the range's 3 bits over the key's top
@@ -2875,6 +2897,108 @@ enum BatchKind { K_MATCH = 0, K_ROUTES = 1, K_DELIVERIES = 2 };
 // one replica running the whole batch.
 // the body of a host-buffer batch, inside batch_call over every replica
 // (the batch is cut across them); *stats_out gets the merged counters
+// match/1 of a host batch on ONE replica, pipelined: chunks of HP_CHUNK
+// topics go up, walk and come back on two streams, so the read-back of a
+// chunk's ids (PCIe: 4 B per match, most of a host batch's time) overlaps the
+// upload and walk of the next.  A chunk's ids land at the running total in
+// the output (offsets rebased on the host at the end); an owned output is
+// sized from the first chunk's fan-out and grown (host copy of what is there)
+// if a later chunk outruns it.  Same results and errors as the one-shot path.
+constexpr uint32_t HP_CHUNK = 1u << 20;
+int host_batch_pipelined(tm_engine* e, const uint8_t* topic_bytes, const uint64_t* topic_off, uint32_t n,
+                         uint32_t* out_count, uint64_t* out_off, uint32_t* out_a, uint64_t out_cap,
+                         uint64_t* out_needed, uint32_t** out_alloc) {
+    DevState& d = *e->devs[0];
+    hipStream_t s = d.stream;
+    d.rw_drain();
+    if (!d.hstream) HIPCHK(hipStreamCreateWithFlags(&d.hstream, hipStreamNonBlocking));
+    for (int j = 0; j < 2; ++j) {
+        if (!d.hp_comp[j]) HIPCHK(hipEventCreateWithFlags(&d.hp_comp[j], hipEventDisableTiming));
+        if (!d.hp_copy[j]) HIPCHK(hipEventCreateWithFlags(&d.hp_copy[j], hipEventDisableTiming));
+    }
+    if (!d.hp_htot) HIPCHK(hipHostMalloc((void**)&d.hp_htot, 64, hipHostMallocDefault));
+    d.w_counts.ensure((size_t)n * 4 + 4);
+    const uint32_t nch = (n + HP_CHUNK - 1) / HP_CHUNK;
+    std::vector<uint64_t> place(nch + 1, 0);
+    std::vector<uint64_t> rel;
+    uint32_t* out = out_alloc ? nullptr : out_a;
+    uint64_t ocap = out_alloc ? 0 : out_cap;
+    bool used[2] = {false, false};
+    for (uint32_t k = 0; k < nch; ++k) {
+        const int j = (int)(k & 1u);
+        const uint32_t lo = k * HP_CHUNK, hi = std::min<uint32_t>(n, lo + HP_CHUNK), c = hi - lo;
+        const uint64_t base = topic_off[lo], nb = topic_off[hi] - base;
+        if (used[j]) HIPCHK(hipEventSynchronize(d.hp_copy[j]));   // chunk k-2's read-back left set j
+        d.hp_bytes[j].ensure(nb + 16);
+        d.hp_off[j].ensure((size_t)(c + 1) * 8);
+        d.hp_outoff[j].ensure((size_t)(c + 1) * 8);
+        d.hp_total[j].ensure(64);
+        const uint64_t per = k ? place[k] / std::max<uint64_t>(lo, 1) + 1 : 16;   // ids per topic so far
+        d.hp_ids[j].ensure(((uint64_t)c * per * 5 / 4 + 1024) * 4, 1.0);
+        rel.assign(topic_off + lo, topic_off + hi + 1);
+        for (auto& x : rel) x -= base;
+        if (nb) HIPCHK(hipMemcpyAsync(d.hp_bytes[j].p, topic_bytes + base, nb, hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(d.hp_off[j].p, rel.data(), (size_t)(c + 1) * 8, hipMemcpyHostToDevice, s));
+        uint64_t cap = d.hp_ids[j].bytes / 4;
+        uint64_t* d_total = d.hp_total[j].as<uint64_t>();
+        e->run_batch(d, d.hp_bytes[j].as<uint8_t>(), d.hp_off[j].as<uint64_t>(), c, nb, d.w_counts.as<uint32_t>() + lo,
+                     d.hp_outoff[j].as<uint64_t>(), d.hp_ids[j].as<uint32_t>(), cap, d_total, s);
+        HIPCHK(hipMemcpyAsync(d.hp_htot + j, d_total, 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        const uint64_t total = d.hp_htot[j];
+        if (total > cap) {   // the lists outgrew the chunk workspace: copy-out again, no re-walk
+            d.hp_ids[j].ensure(total * 4, 1.25);
+            cap = d.hp_ids[j].bytes / 4;
+            e->recopy(d, d.hp_ids[j].as<uint32_t>(), nullptr, cap, s);
+        }
+        place[k + 1] = place[k] + total;
+        if (out_alloc && place[k + 1] > ocap) {   // owned output: size it (first chunk) or grow it
+            const uint64_t want = std::max<uint64_t>(place[k + 1] * 5 / 4,
+                                                     (uint64_t)((double)place[k + 1] / hi * n * 1.15) + 1024);
+            uint32_t* grown = (uint32_t*)g_pinned.get(want * 4);
+            if (!grown) throw std::bad_alloc();
+            if (out) {
+                HIPCHK(hipStreamSynchronize(d.hstream));
+                std::memcpy(grown, out, place[k] * 4);
+                tm_free(out);
+            }
+            out = grown;
+            ocap = want;
+            *out_alloc = out;
+        }
+        // counts and chunk-local offsets on the walk's stream (small; the
+        // caller's arrays may be pageable, which makes a copy wait on the
+        // host: behind a previous chunk's ids on the read-back stream it would
+        // stall the pipeline), then the ids that fit the output (past out_cap
+        // the call reports TM_ENOSPC) on the read-back stream
+        HIPCHK(hipMemcpyAsync(out_count + lo, d.w_counts.as<uint32_t>() + lo, (size_t)c * 4, hipMemcpyDeviceToHost,
+                              s));
+        HIPCHK(hipMemcpyAsync(out_off + lo, d.hp_outoff[j].p, (size_t)c * 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipEventRecord(d.hp_comp[j], s));
+        HIPCHK(hipStreamWaitEvent(d.hstream, d.hp_comp[j], 0));
+        const uint64_t room = ocap > place[k] ? ocap - place[k] : 0;
+        const uint64_t cp = std::min(total, room);
+        if (cp) HIPCHK(hipMemcpyAsync(out + place[k], d.hp_ids[j].p, cp * 4, hipMemcpyDeviceToHost, d.hstream));
+        HIPCHK(hipEventRecord(d.hp_copy[j], d.hstream));
+        used[j] = true;
+    }
+    HIPCHK(hipStreamSynchronize(s));
+    HIPCHK(hipStreamSynchronize(d.hstream));
+    if (out_alloc && !out) {   // no ids at all: still a valid (empty) allocation for tm_free
+        out = (uint32_t*)g_pinned.get(4);
+        if (!out) throw std::bad_alloc();
+        *out_alloc = out;
+    }
+    for (uint32_t k = 1; k < nch; ++k) {
+        const uint32_t lo = k * HP_CHUNK, hi = std::min<uint32_t>(n, lo + HP_CHUNK);
+        for (uint32_t t = lo; t < hi; ++t) out_off[t] += place[k];
+    }
+    const uint64_t total = place[nch];
+    out_off[n] = total;
+    if (out_needed) *out_needed = total;
+    return total > ocap ? TM_ENOSPC : TM_OK;
+}
+
 int host_batch_work(tm_engine* e, BatchKind kind, const uint8_t* topic_bytes, const uint64_t* topic_off, uint32_t n,
                     uint32_t* out_count, uint64_t* out_off, uint32_t* out_a, uint32_t* out_b, uint64_t out_cap,
                     uint64_t* out_needed, uint32_t** out_alloc, tm_batch_stats* stats_out) {
@@ -2889,6 +3013,9 @@ int host_batch_work(tm_engine* e, BatchKind kind, const uint8_t* topic_bytes, co
         if (out_alloc && !(*out_alloc = (uint32_t*)std::malloc(4))) throw std::bad_alloc();
         return TM_OK;
     }
+    if (kind == K_MATCH && e->devs.size() == 1 && n >= 2 * HP_CHUNK && !e->stats_enabled && e->host_pipeline)
+        return host_batch_pipelined(e, topic_bytes, topic_off, n, out_count, out_off, out_a, out_cap, out_needed,
+                                    out_alloc);
     if (out_alloc) out_cap = UINT64_MAX;   // sized below at the exact total
     const size_t R = std::min<size_t>(e->devs.size(), n);
     const uint32_t planes = kind == K_MATCH ? 1u : 2u;
@@ -3494,6 +3621,11 @@ int tm_set_option(tm_engine* e, const char* name, int64_t value) {
         if (!std::strcmp(name, "presort")) {   // 0 arrival order, 1 word-hash key, 2 the tail order, 3 auto
             if (value < 0 || value > 5) return TM_EINVAL;
             e->presort = (int)value;
+            return TM_OK;
+        }
+        if (!std::strcmp(name, "host_pipeline")) {
+            if (value < 0 || value > 1) return TM_EINVAL;
+            e->host_pipeline = (int)value;
             return TM_OK;
         }
         if (!std::strcmp(name, "tail_wave")) {

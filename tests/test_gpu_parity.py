@@ -446,3 +446,33 @@ def test_wave_walk_c5_overflow_falls_back_exact(gpu_device):
     tb, to = W.topics(5, n=3000)
     _by_id(o1, e, tb, to)
     e.close()
+
+
+def test_pipelined_host_batch_equals_one_shot_and_o1(gpu_device):
+    """host-buffer batches of >= 2M topics on one replica go up, walk and come
+    back in 1M-topic chunks on two streams (option host_pipeline): owned and
+    caller-sized outputs equal the one-shot path and O1 (on a sample), and a
+    too-small caller output reports TM_ENOSPC with the exact total"""
+    fb, fo = W.filters(1)
+    tb, to = W.topics(1, n=2_600_000, stream=5)
+    e = Engine(device=gpu_device)
+    e.insert_many(fb, fo)
+    c1, o1_, i1 = e.match_batch(tb, to)                       # pipelined, owned output
+    need = len(i1)
+    c2, o2, i2 = e.match_batch(tb, to, out_cap=need + 7)      # pipelined, caller output
+    e.set_option("host_pipeline", 0)
+    c0, o0, i0 = e.match_batch(tb, to)                        # one shot
+    assert np.array_equal(c1, c0) and np.array_equal(o1_, o0) and np.array_equal(i1, i0)
+    assert np.array_equal(c2, c0) and np.array_equal(o2, o0) and np.array_equal(i2[:need], i0)
+    e.set_option("host_pipeline", 1)
+    with pytest.raises(_lib.TopicMatchError):
+        e.match_batch(tb, to, out_cap=need // 2)
+    e.close()
+    o1 = O1()
+    o1.insert_many(fb, fo)
+    for lo in (0, 1_048_570, 2_599_000):   # across chunk boundaries
+        sb, so = tb[to[lo]:to[lo + 1000]], to[lo:lo + 1001] - to[lo]
+        oc, oo, oi = o1.match_ids(sb, so, threads=8)
+        assert np.array_equal(c0[lo:lo + 1000], oc)
+        assert np.array_equal(i0[o0[lo]:o0[lo + 1000]], oi)
+    o1.close()
