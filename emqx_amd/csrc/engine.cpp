@@ -2909,6 +2909,7 @@ int host_batch_pipelined(tm_engine* e, const uint8_t* topic_bytes, const uint64_
                          uint32_t* out_count, uint64_t* out_off, uint32_t* out_a, uint64_t out_cap,
                          uint64_t* out_needed, uint32_t** out_alloc) {
     DevState& d = *e->devs[0];
+    tm_engine::Guard g(d.device);
     hipStream_t s = d.stream;
     d.rw_drain();
     if (!d.hstream) HIPCHK(hipStreamCreateWithFlags(&d.hstream, hipStreamNonBlocking));
