@@ -457,6 +457,7 @@ def test_pipelined_host_batch_equals_one_shot_and_o1(gpu_device):
     tb, to = W.topics(1, n=2_600_000, stream=5)
     e = Engine(device=gpu_device)
     e.insert_many(fb, fo)
+    e.set_option("host_pipeline", 1)
     c1, o1_, i1 = e.match_batch(tb, to)                       # pipelined, owned output
     need = len(i1)
     c2, o2, i2 = e.match_batch(tb, to, out_cap=need + 7)      # pipelined, caller output
