@@ -690,7 +690,7 @@ def host_legs(a, eng, batch, total):
     moved = int(to[-1]) + 8 * (n + 1) + 4 * n + 8 * (n + 1) + 4 * total
     out["host_path"] = {"topics_per_s": n / secs, "ms_per_batch": secs * 1e3, "topics": n,
                         "pcie_bytes": moved, "pcie_gbs": moved / secs / 1e9,
-                        "path": "tm_match_batch_owned: pinned host topics -> HBM -> walk -> counts, offsets and ids "
+                        "path": "tm_match_batch_owned (1M-topic chunks pipelined on two streams): pinned host topics -> HBM -> walk -> counts, offsets and ids "
                                 "back to pinned host memory (one library-sized read-back), PCIe both ways included"}
     log("host path: %.0f topics/s, %.2f ms per %d-topic batch, %.1f GB/s over PCIe" % (
         n / secs, secs * 1e3, n, moved / secs / 1e9))

@@ -533,7 +533,7 @@ struct tm_engine {
                                       // batch size: 5 from sort_min topics, else 2)
     uint32_t sort_min = 3000000;      // option "sort_min": presort 3's smallest batch in range-local word-hash order
     uint32_t tail_wave = 0;           // option "tail_wave": queue positions per XCD range walked by tm_walk_tail
-    int host_pipeline = 0;            // option "host_pipeline": host-buffer match/1 batches of >= 2M topics on
+    int host_pipeline = 1;            // option "host_pipeline": host-buffer match/1 batches of >= 2M topics on
                                       // one replica go up, walk and come back in 1M-topic chunks, overlapped
     uint32_t sort_bits = 24;          // option "sort_bits": key bits sorted (8..32, % 8; one radix pass per
                                       // 8): presort 1 sorts the word-hash key's top bits (16 walk as fast as
