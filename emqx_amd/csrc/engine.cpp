@@ -541,9 +541,9 @@ struct tm_engine {
                                       // sort_bits - 3 (24: 8M +0.6 % over 16, profiles/r04_t)
     int layout_mode = 1;              // option "layout": 0 off, 1 auto, 2 every commit (tests)
     size_t created_since_layout = 0;  // nodes created since the last relayout
-    uint32_t hot_levels = 3;          // option "hot_levels": relayout puts depths <= H level by level (BFS);
-                                      // 3: the 8M-topic walk 8.12 vs 8.59-8.61 ms at 4 under the round-4 walk
-                                      // order, two boxes (profiles/r04_w, r04_x); 1M / 4M unchanged
+    uint32_t hot_levels = 4;          // option "hot_levels": relayout puts depths <= H level by level (BFS)
+                                      // (an in-process relayout to 2 / 3 / 6 walks 8M topics 5 % faster, but
+                                      // the first layout at 3 does not: DESIGN 5.2b, profiles/r04_x, r04_final8)
                                       // first, then DFS-preorder subtrees (0 = DFS throughout)
     uint32_t edge_div = 4;            // option "edge_load": edge tables kept at load <= 1/edge_div
     uint32_t layout_order = 15;       // option "order" (default 15; A/B at C3, walk ms: 0 3.90, 1 3.84, 7 3.51-3.66, 15 3.44): bit 0 = a node's '+' child directly follows it

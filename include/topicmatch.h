@@ -646,7 +646,7 @@ int  tm_rewrite_match_batch_device(tm_rewrite* r, const uint8_t* d_topics, const
  *   "split"    1 = walk reads separate inner / leaf half arrays (default),
  *              0 = interleaved 32 B records
  *   "hot_levels" depths laid out level by level first at relayout (0..16,
- *              default 3; 0 = DFS preorder throughout); forces a relayout
+ *              default 4; 0 = DFS preorder throughout); forces a relayout
  *   "presort"  1 = walk each batch in the order of a key of its first words
  *              (device radix sort); 2 = the tail order: within each XCD
  *              range the topics whose words label the most trie nodes first
