@@ -43,6 +43,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from emqx_amd import Engine  # noqa: E402
+from emqx_amd.engine import check_total  # noqa: E402
 from emqx_amd import multi  # noqa: E402
 from emqx_amd import workload as W  # noqa: E402
 
@@ -78,6 +79,9 @@ def parse():
                     help="replicated trie per GPU (default), filter shards per GPU with a list exchange (sharded), "
                          "or routed shards: topics exchanged to the shard owning their first --depth levels")
     ap.add_argument("--depth", type=int, default=2, help="routed mode: routing depth (levels of the key)")
+    ap.add_argument("--self-rccl", action="store_true",
+                    help="routed / sharded modes: a rank's own part of every exchange over RCCL too (at world 1 "
+                         "the launch then runs the RCCL transfers the ranks of a multi-GPU node run)")
     ap.add_argument("--shards", type=int, default=None,
                     help="routed mode in one process (--single-process): shards on GPU 0 (a one-GPU rehearsal)")
     ap.add_argument("--single-process", action="store_true",
@@ -655,6 +659,8 @@ class Region:
         for bi, (d_b, d_o, n, nb) in enumerate(self.dbat):
             self.eng.match_batch_device(d_b, d_o, n, nb, c0, oo0, i0, self.cap, t0_, stream=s0)
             self.sync()
+            if check_total(t0_, self.cap, "batch %d" % bi) != self.totals[bi]:
+                raise RuntimeError("batch %d: total changed between passes" % bi)
             out.append((c0[:n].cpu().numpy().view(np.uint32).copy(), oo0[: n + 1].cpu().numpy().view(np.uint64).copy(),
                         i0[: self.totals[bi]].cpu().numpy().view(np.uint32).copy()))
         return out
@@ -843,6 +849,8 @@ def main_routed(a, rank, world, local, dev):
     if world > 1:
         dist.broadcast_object_list(uid, src=0)
     comm = shard.Comm.init_rank(uid[0], S, rank, local)
+    if a.self_rccl:
+        comm.set_self_rccl(True)
     batches = make_batches(a, cfg, rank, world)   # strong: slice `rank` of each global batch
     st = torch.cuda.Stream(device=dev)
     dbat = []
@@ -922,6 +930,8 @@ def main_routed(a, rank, world, local, dev):
     results = []
     for bi in range(len(dbat)):
         walk(exchange(bi))
+        torch.cuda.synchronize(dev)
+        check_total(d_t, cap, "routed owned batch %d" % bi)
         r = back()
         torch.cuda.synchronize(dev)
         results.append((shard._dev_array(r.d_counts, r.n, np.uint32, local),
@@ -934,7 +944,7 @@ def main_routed(a, rank, world, local, dev):
             check_ok = multi.all_true(check_ok)
     if rank == 0:
         emit(routed_line(a, cfg, n_filters, S, a.topics, dt, kms, stats, n0, info, check_ok, phases,
-                         "RCCL" if comm.rccl else "device copies"))
+                         ("RCCL (own buckets too)" if a.self_rccl else "RCCL") if comm.rccl else "device copies"))
     comm.close()
     eng.close()
 
@@ -1112,6 +1122,8 @@ def main_sharded(a, rank, world, local, dev):
     if world > 1:
         dist.broadcast_object_list(uid, src=0)
     comm = shard.Comm.init_rank(uid[0], S, rank, local)
+    if a.self_rccl:
+        comm.set_self_rccl(True)
 
     n_topics = a.topics if a.topics else cfg["topics"]
     tb, to = W.topics(a.config, n=n_topics, stream=0)     # the same batch on every shard

@@ -160,6 +160,7 @@ SIGNATURES = [
     ("tm_comm_destroy", None, [ctypes.c_void_p]),
     ("tm_comm_uses_rccl", ctypes.c_int, [ctypes.c_void_p]),
     ("tm_comm_last_error", ctypes.c_char_p, [ctypes.c_void_p]),
+    ("tm_comm_set_self_rccl", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     ("tm_shard_exchange", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(TmExchangeIn),
                                          ctypes.POINTER(TmExchangeOut)]),
     ("tm_shard_exchange_group", ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint32,

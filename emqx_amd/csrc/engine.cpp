@@ -220,7 +220,6 @@ struct Slot {
     uint64_t* h_maxc = nullptr;     // pinned copy of the slot's ws after its last walk (largest match count,
                                     // spill chunks taken per XCD)
     hipEvent_t maxc_ev = nullptr, done = nullptr;
-    hipEvent_t tail_fork = nullptr, tail_join = nullptr;   // option "tail_wave": the tail walk's stream fork / join
     bool maxc_pending = false, used = false, keyed = false, shaped = false;
     // the slot's last batch, for a re-copy into a larger output (no re-walk)
     uint32_t n = 0, K = 0, kw = 1;
@@ -274,7 +273,6 @@ struct DevState {
     int device = -1;
     hipStream_t stream = nullptr;
     hipStream_t ustream = nullptr;   // commits: image uploads and scatters (never behind a batch on `stream`)
-    hipStream_t tstream = nullptr;   // option "tail_wave": tm_walk_tail beside the persistent walk (made on first use)
     // the pipelined host-buffer match (host_batch_pipelined): two chunk
     // workspaces, the read-back stream and the events between them
     hipStream_t hstream = nullptr;
@@ -382,7 +380,6 @@ struct DevState {
         (void)hipSetDevice(device);
         if (stream) (void)hipStreamSynchronize(stream);
         if (ustream) (void)hipStreamSynchronize(ustream);
-        if (tstream) (void)hipStreamSynchronize(tstream);
         if (rw_done) (void)hipEventDestroy(rw_done);
         img[0].release();
         img[1].release();
@@ -399,8 +396,6 @@ struct DevState {
                               &w.spill, &w.spill_head, &w.sctl})
                 b->release();
             if (w.done) (void)hipEventDestroy(w.done);
-            if (w.tail_fork) (void)hipEventDestroy(w.tail_fork);
-            if (w.tail_join) (void)hipEventDestroy(w.tail_join);
             if (w.maxc_ev) (void)hipEventDestroy(w.maxc_ev);
             if (w.h_maxc) (void)hipHostFree(w.h_maxc);
         }
@@ -411,7 +406,6 @@ struct DevState {
             }
         if (stream) (void)hipStreamDestroy(stream);
         if (ustream) (void)hipStreamDestroy(ustream);
-        if (tstream) (void)hipStreamDestroy(tstream);
         if (hstream) {
             (void)hipStreamSynchronize(hstream);
             (void)hipStreamDestroy(hstream);
@@ -424,7 +418,7 @@ struct DevState {
         if (hp_htot) (void)hipHostFree(hp_htot);
         hp_htot = nullptr;
         hstream = nullptr;
-        stream = ustream = tstream = nullptr;
+        stream = ustream = nullptr;
     }
 };
 
@@ -495,6 +489,11 @@ struct tm_engine {
     // and its last gather) predates the commit that dropped it.  Until then
     // the id keeps its bytes, and the gather keeps serving them.
     std::deque<std::pair<uint64_t, uint32_t>> quarantine;   // (epoch from which images lack the id, id)
+    // id -> the epoch of its live quarantine entry: a forced (caller-chosen)
+    // re-insert takes an id out of quarantine in O(1) and leaves its deque
+    // entry stale (skipped on release), as free_listed does for free_filters
+    std::unordered_map<uint32_t, uint64_t> quarantined;
+    std::vector<uint8_t> free_listed;                        // id has a live entry in free_filters
     std::mutex lease_mu;                                     // leaf lock
     std::multiset<uint64_t> leases;                          // epochs of the open leases
     uint64_t lease_begin() {
@@ -508,15 +507,29 @@ struct tm_engine {
         auto it = leases.find(x);
         if (it != leases.end()) leases.erase(it);
     }
+    // an id that left the images at epoch `vis` names nothing any more once
+    // both epochs are rewritten (now >= vis + 1) and no lease predates vis
+    bool quarantine_over(uint64_t vis, uint64_t now, uint64_t oldest) const { return now >= vis + 1 && oldest >= vis; }
+    uint64_t oldest_lease() {   // under lease_mu
+        return leases.empty() ? UINT64_MAX : *leases.begin();
+    }
     void release_quarantine() {
         if (quarantine.empty()) return;
         std::lock_guard<std::mutex> lk(lease_mu);
         const uint64_t now = epoch.load();
-        const uint64_t oldest = leases.empty() ? UINT64_MAX : *leases.begin();
+        const uint64_t oldest = oldest_lease();
         while (!quarantine.empty()) {
             const uint64_t vis = quarantine.front().first;
-            if (now < vis + 1 || oldest < vis) break;
-            free_filters.push_back(quarantine.front().second);
+            const uint32_t id = quarantine.front().second;
+            auto it = quarantined.find(id);
+            if (it == quarantined.end() || it->second != vis) {   // stale: re-inserted under its id meanwhile
+                quarantine.pop_front();
+                continue;
+            }
+            if (!quarantine_over(vis, now, oldest)) break;
+            quarantined.erase(it);
+            free_filters.push_back(id);
+            free_listed[id] = 1;
             quarantine.pop_front();
         }
     }
@@ -532,7 +545,7 @@ struct tm_engine {
                                       // 2 the tail order, 5 the word-hash key within each XCD range, 3 by
                                       // batch size: 5 from sort_min topics, else 2)
     uint32_t sort_min = 3000000;      // option "sort_min": presort 3's smallest batch in range-local word-hash order
-    uint32_t tail_wave = 0;           // option "tail_wave": queue positions per XCD range walked by tm_walk_tail
+    std::atomic<int> last_order{-1};  // the walk order (presort mode) of the last device batch (tm_debug_last_order)
     int host_pipeline = 1;            // option "host_pipeline": host-buffer match/1 batches of >= 2M topics on
                                       // one replica go up, walk and come back in 1M-topic chunks, overlapped
     uint32_t sort_bits = 24;          // option "sort_bits": key bits sorted (8..32, % 8; one radix pass per
@@ -1036,28 +1049,50 @@ struct tm_engine {
     // the id the next new filter takes (tm_insert_batch_ids), FILTER_NONE: allocate one
     uint32_t forced_fid = FILTER_NONE;
     uint32_t new_filter(const uint8_t* p, uint32_t len, uint32_t node) {
-        uint32_t id;
+        uint32_t id = FILTER_NONE;
         if (forced_fid != FILTER_NONE) {   // a caller-chosen (global) id: holes below it stay unused
             id = forced_fid;
             if (id >= 0x7FFFFFF0u) throw RangeError("filter id past 2^31 - 16");
-            if (id >= filters.size()) filters.resize((size_t)id + 1, FilterRec{0, 0, NODE_NONE});
-            else if (filters[id].node != NODE_NONE) throw ArgError("filter id " + std::to_string(id) + " in use");
-            for (auto it = quarantine.begin(); it != quarantine.end(); ++it)   // a re-inserted id leaves quarantine
-                if (it->second == id) {
-                    quarantine.erase(it);
+            if (id >= filters.size()) {
+                filters.resize((size_t)id + 1, FilterRec{0, 0, NODE_NONE});
+                free_listed.resize(filters.size(), 0);
+            } else if (filters[id].node != NODE_NONE) {
+                throw ArgError("filter id " + std::to_string(id) + " in use");
+            }
+            auto q = quarantined.find(id);
+            if (q != quarantined.end()) {
+                // a deleted id batches in flight may still emit: taken again
+                // at once only for the same filter (whatever those batches
+                // name, it is still this filter) or once its quarantine is over
+                const FilterRec& old = filters[id];
+                const bool same = old.len == len && (len == 0 || std::memcmp(&filter_arena[old.off], p, len) == 0);
+                if (!same) {
+                    std::lock_guard<std::mutex> lk(lease_mu);
+                    if (!quarantine_over(q->second, epoch.load(), oldest_lease()))
+                        throw ArgError("filter id " + std::to_string(id) + " was deleted and may still be named by "
+                                       "batches in flight: reusable for another filter after two commits and the "
+                                       "leases open at its delete");
+                }
+                quarantined.erase(q);   // its deque entry goes stale
+            }
+            free_listed[id] = 0;        // a free_filters entry of it goes stale
+        } else {
+            if (free_filters.empty()) release_quarantine();
+            while (!free_filters.empty()) {
+                const uint32_t f = free_filters.back();
+                free_filters.pop_back();
+                if (free_listed[f]) {   // else stale: taken by a forced insert
+                    free_listed[f] = 0;
+                    id = f;
                     break;
                 }
-        } else if (free_filters.empty()) {
-            release_quarantine();
-        }
-        if (forced_fid != FILTER_NONE) {
-        } else if (!free_filters.empty()) {
-            id = free_filters.back();
-            free_filters.pop_back();
-        } else {
-            if (filters.size() >= 0x7FFFFFF0ull) throw RangeError("filter ids exhausted (2^31: the image tags summaries with bit 31)");
-            id = (uint32_t)filters.size();
-            filters.push_back(FilterRec{});
+            }
+            if (id == FILTER_NONE) {
+                if (filters.size() >= 0x7FFFFFF0ull) throw RangeError("filter ids exhausted (2^31: the image tags summaries with bit 31)");
+                id = (uint32_t)filters.size();
+                filters.push_back(FilterRec{});
+                free_listed.push_back(0);
+            }
         }
         uint64_t off = filter_arena.size();
         filter_arena.insert(filter_arena.end(), p, p + len);
@@ -1077,6 +1112,7 @@ struct tm_engine {
         on_filter_free(id);
         filters[id].node = NODE_NONE;   // off / len stay: the gather serves the id until it is reused
         quarantine.emplace_back(epoch.load() + 1, id);   // the next commit drops it from the images
+        quarantined[id] = epoch.load() + 1;
         --live_filters;
     }
 
@@ -1092,6 +1128,11 @@ struct tm_engine {
         if (nodes[v].self_filter == FILTER_NONE) {
             set_topic(v, new_filter(p, len, v));
             add_summaries(!tmp_words.empty() && tmp_words.back() == WORD_HASH);
+        } else if (forced_fid != FILTER_NONE && nodes[v].self_filter != forced_fid) {
+            // the filter is in the trie under another id: a caller that
+            // believes it now has forced_fid would mis-name its matches
+            throw ArgError("filter already present under id " + std::to_string(nodes[v].self_filter) +
+                           ", not " + std::to_string(forced_fid));
         }
         dev_dirty = true;
     }
@@ -1839,6 +1880,7 @@ struct tm_engine {
         if (devs.empty()) {
             ++epoch;
             dev_dirty = false;
+            release_quarantine();
             return;
         }
         if (!dev_dirty && devs[0]->img[devs[0]->cur].written) {
@@ -1930,6 +1972,7 @@ struct tm_engine {
         t_fshape.rotate(fshape.size());
         dev_dirty = false;
         ++epoch;
+        release_quarantine();   // also for engines that only take forced ids (never reach new_filter's release)
     }
 
     // option "split": de-interleave the uploaded records into inner / leaf arrays
@@ -2068,6 +2111,7 @@ struct tm_engine {
         const uint32_t kw = keys && !shaped ? key_words : 0u;
         adapt_stage_k(d, n, kw);
         const int presort = presort_of(n);
+        last_order = presort;
         const int si = d.next_slot;
         d.next_slot = (d.next_slot + 1) % nslots;
         Slot& w = d.slots[si];
@@ -2117,15 +2161,6 @@ struct tm_engine {
             qb.spill = w.spill.as<uint32_t>();
             qb.spill_head = w.spill_head.as<uint32_t>();
             qb.spill_chunks = w.spill_chunks;
-        }
-        if (tail_wave && !kw && !stats_enabled && n / 8 > 4u * tail_wave) {   // 8 XCD ranges
-            if (!d.tstream) HIPCHK(hipStreamCreateWithFlags(&d.tstream, hipStreamNonBlocking));
-            if (!w.tail_fork) HIPCHK(hipEventCreateWithFlags(&w.tail_fork, hipEventDisableTiming));
-            if (!w.tail_join) HIPCHK(hipEventCreateWithFlags(&w.tail_join, hipEventDisableTiming));
-            qb.tail_wave = tail_wave;
-            qb.tail_stream = d.tstream;
-            qb.tail_fork = w.tail_fork;
-            qb.tail_join = w.tail_join;
         }
         w.sorted = queue_rows_by_position(qb, stats_enabled);   // the copy-out moves rows by perm
         HIPCHK(launch_queue(stats_enabled, xcdq != 0, im, bytes, off, n, qb, d.stage_k, counts, out_off, ids, keys,
@@ -2907,9 +2942,39 @@ enum BatchKind { K_MATCH = 0, K_ROUTES = 1, K_DELIVERIES = 2 };
 // sized from the first chunk's fan-out and grown (host copy of what is there)
 // if a later chunk outruns it.  Same results and errors as the one-shot path.
 constexpr uint32_t HP_CHUNK = 1u << 20;
+int host_batch_pipelined_body(tm_engine* e, const uint8_t* topic_bytes, const uint64_t* topic_off, uint32_t n,
+                              uint32_t* out_count, uint64_t* out_off, uint32_t* out_a, uint64_t out_cap,
+                              uint64_t* out_needed, uint32_t** out_alloc);
+// an owned output: pinned (DMA target) when the pool has it, else pageable
+// (as the one-shot path); freed by tm_free either way
+uint32_t* owned_ids(uint64_t n) {
+    void* p = g_pinned.get(n * 4);
+    if (!p) p = std::malloc(n * 4);
+    if (!p) throw std::bad_alloc();
+    return (uint32_t*)p;
+}
 int host_batch_pipelined(tm_engine* e, const uint8_t* topic_bytes, const uint64_t* topic_off, uint32_t n,
                          uint32_t* out_count, uint64_t* out_off, uint32_t* out_a, uint64_t out_cap,
                          uint64_t* out_needed, uint32_t** out_alloc) {
+    try {
+        return host_batch_pipelined_body(e, topic_bytes, topic_off, n, out_count, out_off, out_a, out_cap, out_needed,
+                                         out_alloc);
+    } catch (...) {
+        // an owned output handed out before a later chunk failed: no DMA may
+        // still target it, and the caller gets no pointer (nothing to free)
+        if (out_alloc && *out_alloc) {
+            DevState& d = *e->devs[0];
+            (void)hipStreamSynchronize(d.stream);
+            if (d.hstream) (void)hipStreamSynchronize(d.hstream);
+            tm_free(*out_alloc);
+            *out_alloc = nullptr;
+        }
+        throw;
+    }
+}
+int host_batch_pipelined_body(tm_engine* e, const uint8_t* topic_bytes, const uint64_t* topic_off, uint32_t n,
+                              uint32_t* out_count, uint64_t* out_off, uint32_t* out_a, uint64_t out_cap,
+                              uint64_t* out_needed, uint32_t** out_alloc) {
     DevState& d = *e->devs[0];
     tm_engine::Guard g(d.device);
     hipStream_t s = d.stream;
@@ -2958,8 +3023,7 @@ int host_batch_pipelined(tm_engine* e, const uint8_t* topic_bytes, const uint64_
         if (out_alloc && place[k + 1] > ocap) {   // owned output: size it (first chunk) or grow it
             const uint64_t want = std::max<uint64_t>(place[k + 1] * 5 / 4,
                                                      (uint64_t)((double)place[k + 1] / hi * n * 1.15) + 1024);
-            uint32_t* grown = (uint32_t*)g_pinned.get(want * 4);
-            if (!grown) throw std::bad_alloc();
+            uint32_t* grown = owned_ids(want);
             if (out) {
                 HIPCHK(hipStreamSynchronize(d.hstream));
                 std::memcpy(grown, out, place[k] * 4);
@@ -2967,7 +3031,7 @@ int host_batch_pipelined(tm_engine* e, const uint8_t* topic_bytes, const uint64_
             }
             out = grown;
             ocap = want;
-            *out_alloc = out;
+            *out_alloc = out;   // (the old block was freed above: *out_alloc never names a freed block)
         }
         // counts and chunk-local offsets on the walk's stream (small; the
         // caller's arrays may be pageable, which makes a copy wait on the
@@ -2988,8 +3052,7 @@ int host_batch_pipelined(tm_engine* e, const uint8_t* topic_bytes, const uint64_
     HIPCHK(hipStreamSynchronize(s));
     HIPCHK(hipStreamSynchronize(d.hstream));
     if (out_alloc && !out) {   // no ids at all: still a valid (empty) allocation for tm_free
-        out = (uint32_t*)g_pinned.get(4);
-        if (!out) throw std::bad_alloc();
+        out = owned_ids(1);
         *out_alloc = out;
     }
     for (uint32_t k = 1; k < nch; ++k) {
@@ -3466,6 +3529,11 @@ int tm_match_small_device(tm_engine* e, const uint8_t* d_bytes, const uint64_t* 
     }, [&] { e->finish_batch(n); });
 }
 
+// diagnostics (not part of include/topicmatch.h): the walk order of the
+// last device batch (option "presort" resolved by batch size: 5 the
+// range-local word-hash order, 2 the tail order, 0 arrival order ...)
+extern "C" int tm_debug_last_order(tm_engine* e) { return e ? e->last_order.load() : TM_EINVAL; }
+
 // diagnostics (not part of include/topicmatch.h): the last stats-mode
 // batch's per-level histogram [visits, probe loads, failed probes] x 16
 extern "C" int tm_debug_hist(tm_engine* e, uint64_t* out, int n) {
@@ -3629,11 +3697,6 @@ int tm_set_option(tm_engine* e, const char* name, int64_t value) {
         if (!std::strcmp(name, "host_pipeline")) {
             if (value < 0 || value > 1) return TM_EINVAL;
             e->host_pipeline = (int)value;
-            return TM_OK;
-        }
-        if (!std::strcmp(name, "tail_wave")) {
-            if (value < 0 || value > (1 << 24)) return TM_EINVAL;
-            e->tail_wave = (uint32_t)value;
             return TM_OK;
         }
         if (!std::strcmp(name, "sort_bits")) {

@@ -80,6 +80,7 @@ struct tm_comm {
     uint32_t nranks = 1, rank = 0;
     ncclComm_t nccl = nullptr;    // RCCL backend (null: device copies within one process)
     bool aborted = false;         // aborted after a failure inside an RCCL group
+    bool self_rccl = false;       // tm_comm_set_self_rccl: the rank's own part over RCCL too
     hipStream_t stream = nullptr;
     Buf sizes;                    // 2S u64: send counts per destination, then their first ids
     Buf rsizes;                   // S u64: ids to receive from each source
@@ -339,7 +340,8 @@ int run_xfers(tm_comm** comms, uint32_t k, const std::vector<Xfer>& xs, const st
     for (const Xfer& x : xs) {
         if (!x.bytes) continue;
         const int is = of(x.src), id = of(x.dst);
-        if (x.src == x.dst || !rccl) {   // a device copy (same rank, or ranks of one process without RCCL)
+        const bool self_copy = x.src == x.dst && !(rccl && is >= 0 && comms[is]->self_rccl);
+        if (self_copy || !rccl) {   // a device copy (same rank, or ranks of one process without RCCL)
             if (is < 0 || id < 0) return fail(c0, "routed exchange: copy between ranks of different processes");
             XHIP(comms[id], hipMemcpyPeerAsync(x.dp, comms[id]->device, x.sp, comms[is]->device, x.bytes, st[id]));
             continue;
@@ -427,6 +429,11 @@ void tm_comm_destroy(tm_comm* c) {
 }
 
 int tm_comm_uses_rccl(tm_comm* c) { return c && c->nccl ? 1 : 0; }
+int tm_comm_set_self_rccl(tm_comm* c, int on) {
+    if (!c || !c->nccl) return TM_EINVAL;
+    c->self_rccl = on != 0;
+    return TM_OK;
+}
 const char* tm_comm_last_error(tm_comm* c) { return c ? c->last_error.c_str() : "null comm"; }
 
 // one rank of a multi-process (or one-rank) RCCL exchange
@@ -447,7 +454,7 @@ int tm_shard_exchange(tm_comm* c, const tm_exchange_in* in, tm_exchange_out* out
     // (a rank's own slice is a device copy: RCCL's send to self is slower)
     for (uint32_t p = 0; p < S; ++p) {
         const uint32_t lo = slice_lo(n, S, p), mp = slice_lo(n, S, p + 1) - lo;
-        if (p == me) {
+        if (p == me && !c->self_rccl) {
             XHIP(c, hipMemcpyAsync(c->recv_counts.as<uint32_t>() + (size_t)p * m, in->d_counts + lo, (size_t)mp * 4,
                                    hipMemcpyDeviceToDevice, st));
             continue;
@@ -467,7 +474,7 @@ int tm_shard_exchange(tm_comm* c, const tm_exchange_in* in, tm_exchange_out* out
     uint64_t base = 0;
     for (uint32_t p = 0; p < S; ++p) {
         const uint64_t items = c->h_send[p], from = c->h_send[S + p], ritems = c->h_recv[p];
-        if (p == me) {
+        if (p == me && !c->self_rccl) {
             XHIP(c, hipMemcpyAsync(c->recv_ids.as<uint32_t>() + base, in->d_ids + from, items * 4,
                                    hipMemcpyDeviceToDevice, st));
             for (uint32_t j = 0; j < in->key_words; ++j)
@@ -580,7 +587,8 @@ int tm_route_exchange(tm_comm* c, const tm_route_in* in, tm_route_out* out) {
     // [topics, bytes] per peer: an all-to-all of two u64
     if (!c->sizes.ensure(2 * S * 8) || !c->rsizes.ensure(2 * S * 8)) return fail(c, "hipMalloc", TM_ENOMEM);
     XHIP(c, hipMemcpyAsync(c->sizes.p, r.h_sz.data(), 2 * S * 8, hipMemcpyHostToDevice, st));
-    if (S > 1) {
+    const bool over_rccl = S > 1 || c->self_rccl;
+    if (over_rccl) {
         XGROUP_START(c, std::vector<tm_comm*>{c});
         XNCCL(c, ncclAllToAll(c->sizes.p, c->rsizes.p, 2, ncclUint64, c->nccl, st));
         XGROUP_END(c);
@@ -606,7 +614,7 @@ int tm_route_exchange(tm_comm* c, const tm_route_in* in, tm_route_out* out) {
         run.push_back(Xfer{p, me, nullptr, r.rlen.as<uint32_t>() + r.rt_base[p], r.h_rsz[2 * p] * 4});
         run.push_back(Xfer{p, me, nullptr, r.rbuf.as<uint8_t>() + r.rb_base[p], r.h_rsz[2 * p + 1]});
     }
-    rc = run_xfers(&c, 1, run, {st}, S > 1);
+    rc = run_xfers(&c, 1, run, {st}, over_rccl);
     if (rc != TM_OK) return rc;
     return route_finish(c, st, out);
 }
@@ -675,7 +683,8 @@ int tm_route_return(tm_comm* c, const tm_route_lists* l, tm_route_result* res) {
     for (uint32_t s = 0; s < S; ++s) send[s] = r.h_seg_cut[s + 1] - r.h_seg_cut[s];
     if (!r.ret_sz.ensure(S * 8) || !r.ret_rsz.ensure(S * 8)) return fail(c, "hipMalloc", TM_ENOMEM);
     XHIP(c, hipMemcpyAsync(r.ret_sz.p, send.data(), S * 8, hipMemcpyHostToDevice, st));
-    if (S > 1) {
+    const bool over_rccl = S > 1 || c->self_rccl;
+    if (over_rccl) {
         XGROUP_START(c, std::vector<tm_comm*>{c});
         XNCCL(c, ncclAllToAll(r.ret_sz.p, r.ret_rsz.p, 1, ncclUint64, c->nccl, st));
         XGROUP_END(c);
@@ -704,7 +713,7 @@ int tm_route_return(tm_comm* c, const tm_route_lists* l, tm_route_result* res) {
             xs.insert(xs.end(), {cnt_out, ids_out, cnt_in, ids_in});
         }
     }
-    rc = run_xfers(&c, 1, xs, {st}, S > 1);
+    rc = run_xfers(&c, 1, xs, {st}, over_rccl);
     if (rc != TM_OK) return rc;
     return return_finish(c, st, res);
 }

@@ -13,7 +13,6 @@ constexpr size_t QWS_BYTES = 2048;   // queue heads: 8 ranges x 128 B, then 8 sp
 constexpr size_t QWS_MAXC = 120;     // u64 slot of ws: the batch's largest match count
 constexpr size_t QWS_MAXL = 121;     // u64 slot of ws: most levels of a topic in a keyed batch
 constexpr size_t QWS_SPILL = 128;    // u64 slots 128 + 16 x: spill chunks taken by XCD x's waves
-constexpr size_t QWS_TAIL = 4;       // u64 slots 4 + 16 r: tm_walk_tail's next position of range r's tail
 // Spill chunks (unkeyed walks): ids of a topic past its K-slot stage row go
 // to chunks of SPILL_CHUNK u32 -- slot 0 the next chunk of the topic, slots
 // 1.. ids in discovery order -- taken from the walking XCD's area (capacity
@@ -68,15 +67,6 @@ struct QueueBufs {
     uint32_t* spill = nullptr;      // spill_chunks x SPILL_CHUNK (null: fan-out beyond K re-walks)
     uint32_t* spill_head = nullptr; // n
     uint32_t spill_chunks = 0;      // a multiple of 8
-    // option "tail_wave": the last tail_wave queue positions of each XCD
-    // range are walked by tm_walk_tail (a wave per topic, level by level) on
-    // tail_stream, concurrently: its blocks take the CU slots the persistent
-    // walk's waves give up when its queue runs dry, so the launch's tail is
-    // cut into short per-topic wave walks instead of waiting on the last
-    // lanes' whole topics (unkeyed chunk-row walks with per-XCD ranges only)
-    uint32_t tail_wave = 0;
-    hipStream_t tail_stream = nullptr;
-    hipEvent_t tail_fork = nullptr, tail_join = nullptr;
 };
 // digit counters of the presort of n topics (256 per 4096-topic tile)
 uint32_t presort_counts(uint32_t n);

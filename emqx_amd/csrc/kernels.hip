@@ -896,8 +896,7 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
               unsigned long long* __restrict__ ws, unsigned long long* __restrict__ stats,
               unsigned long long* __restrict__ hist, const uint32_t* __restrict__ perm,
               const uint32_t* __restrict__ twords_s, const uint32_t* __restrict__ meta_s,
-              uint32_t* __restrict__ spill, uint32_t* __restrict__ spill_head, uint32_t spill_chunks,
-              uint32_t tailz) {
+              uint32_t* __restrict__ spill, uint32_t* __restrict__ spill_head, uint32_t spill_chunks) {
     static_assert(CH == CH_NONE || (!STATS && !KEYS), "chunk rows: unkeyed walks in arrival order only");
     __shared__ uint32_t lds_path[WREG * BLOCK];
     __shared__ ChunkRows lds_chunk[CH != CH_NONE ? BLOCK / 64 : 1];
@@ -942,9 +941,7 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
                     while (qr < QRANGES) {
                         const uint32_t r = (home + qr) & (QRANGES - 1);
                         const uint32_t rb = (uint32_t)((uint64_t)n * r / QRANGES);
-                        const uint32_t re0 = (uint32_t)((uint64_t)n * (r + 1) / QRANGES);
-                        // the range's last tailz positions are tm_walk_tail's (option "tail_wave")
-                        const uint32_t re = re0 - (tailz < re0 - rb ? tailz : re0 - rb);
+                        const uint32_t re = (uint32_t)((uint64_t)n * (r + 1) / QRANGES);
                         uint32_t x = 0;
                         if (lane == leader)
                             x = (uint32_t)__hip_atomic_fetch_add(ws + 16 * r, (unsigned long long)QCHUNK,
@@ -1301,73 +1298,6 @@ tm_walk_wave(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const u
         wave_sync_lds();
     }
     if (lane == 0 && maxl && ws) atomicMax(ws + QWS_MAXL, (unsigned long long)maxl);
-}
-
-// tm_walk_tail (option "tail_wave", QueueBufs): the last tailz queue
-// positions of each XCD range, one wave per topic level by level, launched
-// beside tm_walk_queue on its own stream.  A wave takes positions of its own
-// XCD's range from a per-range counter (ws + QWS_TAIL + 16 r), then the other
-// ranges'.  Stage rows, counts and spill heads by topic, as the chunk-row
-// walk writes them (lists past K: spill_head NO_SPILL, the copy-out re-walks).
-__global__ void __launch_bounds__(BLOCK)
-tm_walk_tail(ImageView im, const uint64_t* __restrict__ off, uint32_t n, uint32_t tailz,
-             const uint32_t* __restrict__ twords, const uint32_t* __restrict__ words,
-             const uint32_t* __restrict__ meta, uint32_t* __restrict__ gpath, uint32_t* __restrict__ stage,
-             uint32_t K, uint32_t* __restrict__ counts, uint32_t* __restrict__ spill_head,
-             const uint32_t* __restrict__ perm, unsigned long long* __restrict__ ws) {
-    __shared__ WaveLds lds_all[BLOCK / 64];
-    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    WaveLds& L = lds_all[wv];
-    uint32_t r = xcc_id(), tried = 0, maxc = 0;
-    for (;;) {
-        const uint32_t rb = (uint32_t)((uint64_t)n * r / QRANGES);
-        const uint32_t re = (uint32_t)((uint64_t)n * (r + 1) / QRANGES);
-        const uint32_t z = tailz < re - rb ? tailz : re - rb;
-        uint32_t k = 0;
-        if (lane == 0) k = (uint32_t)atomicAdd(ws + QWS_TAIL + 16 * r, 1ull);
-        k = (uint32_t)__shfl((int)k, 0, 64);
-        if (k >= z) {   // this range's tail is taken: the next range's (uniform)
-            if (++tried == QRANGES) break;
-            r = (r + 1) & (QRANGES - 1);
-            continue;
-        }
-        const uint32_t pos = re - z + k;
-        const uint32_t t = perm ? perm[pos] : pos;
-        const uint32_t mt = meta[t];
-        const uint32_t nl = mt & MN;
-        const bool dollar = (mt & MDOLLAR) != 0;
-        const uint32_t* row = twords + (uint64_t)t * WREG;
-        uint32_t* srow = stage + (uint64_t)t * K;
-        bool fallback = (mt & MLONG) != 0 || nl > 31;
-        uint32_t ec = 0;
-        if (!fallback) {
-            if (lane < WREG && lane < nl) L.words[lane] = row[lane];
-            wave_sync_lds();
-            fallback = !wave_walk_topic(im, L, nl, dollar, lane, ec);
-        }
-        if (!fallback) {
-            const uint32_t m = ec < K ? ec : K;
-            for (uint32_t j = lane; j < m; j += 64) srow[K - 1 - j] = L.eid[j];
-            if (lane == 0) {
-                counts[t] = ec;
-                if (ec > K && spill_head) spill_head[t] = NO_SPILL;
-            }
-        } else if (lane == 0) {
-            const uint64_t b = off[t] - off[0];
-            const MemWords mw{row, words + b + t};
-            RowEmit<false> em{srow, nullptr, K, 0, {}, 0ull, 1u, 0ull};
-            WalkStats s2;
-            walk<false, false>(im, nl, dollar, GlobalPath{gpath + b + 2ull * t}, mw, em, s2);
-            em.flush();
-            ec = em.cnt;
-            counts[t] = ec;
-            if (ec > K && spill_head) spill_head[t] = NO_SPILL;
-        }
-        ec = (uint32_t)__shfl((int)ec, 0, 64);
-        maxc = ec > maxc ? ec : maxc;
-        wave_sync_lds();
-    }
-    if (lane == 0 && maxc) atomicMax(ws + QWS_MAXC, (unsigned long long)maxc);
 }
 
 // tm_match_small: a small batch in ONE launch (the micro-batcher's path,
@@ -1955,10 +1885,6 @@ hipError_t launch_queue(bool stats_mode, bool xcdq, const ImageView& im, const u
     }
     // spill chunks: unkeyed walks in arrival order (presorted rows re-walk)
     uint32_t* const spill = (!keys && !by_pos && qb.spill_chunks >= QRANGES) ? qb.spill : nullptr;
-    // option "tail_wave": the last positions of each XCD range go to
-    // tm_walk_tail on the second stream (chunk-row walks with per-XCD ranges)
-    const bool tail_on = qb.tail_wave && ch == CH_ROWS && xcdq && qb.tail_stream && qb.tail_fork && qb.tail_join;
-    const uint32_t tz = tail_on ? qb.tail_wave : 0u;
     const uint32_t wg = ch == CH_ROWS ? resident_grid(tm_walk_queue<false, true, false, CH_ROWS>, div_up(n, 64),
                                                       walk_blocks_per_cu)
                                       : resident_grid(tm_walk_queue<false, false, false>, div_up(n, 64),
@@ -1967,24 +1893,9 @@ hipError_t launch_queue(bool stats_mode, bool xcdq, const ImageView& im, const u
     hipLaunchKernelGGL((tm_walk_queue<S, X, Y, C>), dim3(wg), blk, 0, st, im, off, n, qb.twords, qb.words,       \
                        qb.meta, qb.path, qb.stage, qb.kstage, K, key_words, counts, qb.ws, stats,                \
                        hist ? stats + HIST_OFF : nullptr, qb.perm, qb.twords_s, qb.meta_s, spill, qb.spill_head,   \
-                       qb.spill_chunks, tz)
+                       qb.spill_chunks)
     if (ch == CH_ROWS) {
-        if (tail_on) {   // the tail walk may start with the persistent walk (both after the presort)
-            err = hipEventRecord(qb.tail_fork, st);
-            if (err != hipSuccess) return err;
-        }
         if (xcdq) TM_Q(false, true, false, CH_ROWS); else TM_Q(false, false, false, CH_ROWS);
-        if (tail_on) {   // enqueued after the persistent walk, so its waves take the CUs first
-            err = hipStreamWaitEvent(qb.tail_stream, qb.tail_fork, 0);
-            if (err != hipSuccess) return err;
-            const uint32_t tb = div_up(tz * QRANGES, BLOCK / 64);
-            hipLaunchKernelGGL(tm_walk_tail, dim3(tb < 65535 ? tb : 65535), blk, 0, qb.tail_stream, im, off, n, tz,
-                               qb.twords, qb.words, qb.meta, qb.path, qb.stage, K, counts,
-                               spill ? qb.spill_head : nullptr, qb.perm, qb.ws);
-            err = hipEventRecord(qb.tail_join, qb.tail_stream);
-            if (err == hipSuccess) err = hipStreamWaitEvent(st, qb.tail_join, 0);
-            if (err != hipSuccess) return err;
-        }
     } else if (keys) {
         if (stats_mode) TM_Q(true, true, true, CH_NONE); else TM_Q(false, true, true, CH_NONE);
     } else if (stats_mode) {

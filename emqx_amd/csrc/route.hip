@@ -214,9 +214,9 @@ hipError_t launch_route_plan(const uint8_t* bytes, const uint64_t* off, uint32_t
     hipError_t err = launch_scan0(w.slen, n, w.soff, w.soff + n, w.scan_tmp, st);
     if (err != hipSuccess) return err;
     if (n) hipLaunchKernelGGL(tm_route_bytes, dim3(nb), dim3(RB), 0, st, bytes, off, n, w.perm, w.soff, w.sbuf);
-    // byte cut of every bucket: soff[bucket[o]], o = 0..S
-    hipLaunchKernelGGL(tm_gather_u64, dim3(1), dim3(64), 0, st, w.soff, w.bucket, S + 1, w.cuts);
-    return hipGetLastError();
+    // byte cut of every bucket: soff[bucket[o]], o = 0..S (S + 1 = 65 entries
+    // at MAX_ROUTE_SHARDS: more than one 64-lane block)
+    return launch_gather_u64(w.soff, w.bucket, S + 1, w.cuts, st);
 }
 
 hipError_t launch_gather_u64(const uint64_t* in, const uint32_t* idx, uint32_t k, uint64_t* out, hipStream_t st) {

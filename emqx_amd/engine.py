@@ -21,6 +21,19 @@ def pack(strings):
     return buf, off
 
 
+def check_total(d_total, cap, what="match"):
+    """the exact total a two-pass device call wrote (a 1-element device tensor
+    whose stream the caller has synchronised) against the capacity of the
+    output it sized from the first pass: the device API drops ids past cap and
+    reports the exact total, so a total past cap means lists were cut (e.g. a
+    first-pass total overwritten by a late fill) -- raise instead of
+    returning them"""
+    total = int(d_total.item()) if hasattr(d_total, "item") else int(d_total)
+    if total > cap:
+        raise RuntimeError("%s: %d ids past an output of %d (lists would be cut)" % (what, total, cap))
+    return total
+
+
 def _ptr(a):
     return ctypes.c_void_p(a.ctypes.data) if a is not None else None
 
@@ -84,6 +97,15 @@ class Engine:
         buf = np.ascontiguousarray(buf, dtype=np.uint8)
         off = np.ascontiguousarray(off, dtype=np.uint64)
         return self._check(self.lib.tm_insert_batch(self.h, _ptr(buf), _ptr(off), n), "tm_insert_batch")
+
+    def insert_many_ids(self, buf, off, ids):
+        """tm_insert_batch_ids: filter i under the caller's (global) id ids[i]"""
+        n = len(off) - 1
+        buf = np.ascontiguousarray(buf, dtype=np.uint8)
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        ids = np.ascontiguousarray(ids, dtype=np.uint32)
+        return self._check(self.lib.tm_insert_batch_ids(self.h, _ptr(buf), _ptr(off), n, _ptr(ids)),
+                           "tm_insert_batch_ids")
 
     def delete(self, filt: bytes):
         return self._check(self.lib.tm_delete(self.h, filt, len(filt)), "tm_delete")

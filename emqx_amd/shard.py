@@ -32,7 +32,7 @@ import ctypes
 import numpy as np
 
 from . import _lib as L
-from .engine import Engine
+from .engine import Engine, check_total
 
 
 def shard_of(filt: bytes, n_shards: int) -> int:
@@ -218,6 +218,13 @@ class Comm:
     def rccl(self):
         return bool(self.lib.tm_comm_uses_rccl(self.h))
 
+    def set_self_rccl(self, on=True):
+        """the rank's own part of every exchange over RCCL too (a one-rank
+        communicator then runs the RCCL code paths of the multi-GPU ranks)"""
+        rc = self.lib.tm_comm_set_self_rccl(self.h, 1 if on else 0)
+        if rc != L.TM_OK:
+            raise L.TopicMatchError(rc, "tm_comm_set_self_rccl")
+
     def close(self):
         if self.h:
             self.lib.tm_comm_destroy(self.h)
@@ -250,13 +257,20 @@ class ShardSet:
     on the slice's GPU.  match_batch returns the merged lists with global ids
     (local * S + shard), in emqx_trie:match/1 order."""
 
-    def __init__(self, devices, filters_hint=0):
+    def __init__(self, devices, filters_hint=0, engines=None):
+        """engines: already built ShardEngines (shard s of S on devices[s]),
+        e.g. filled in parallel threads; the set takes them over"""
         import torch
         self.torch = torch
         self.devices = list(devices)
         self.S = len(self.devices)
-        self.engines = [ShardEngine(d, self.S, s, filters_hint=filters_hint // max(self.S, 1) + 1)
-                        for s, d in enumerate(self.devices)]
+        if engines is not None:
+            if len(engines) != self.S or any(e.n_shards != self.S or e.shard != s for s, e in enumerate(engines)):
+                raise ValueError("engines must be shards 0..S-1 of S")
+            self.engines = list(engines)
+        else:
+            self.engines = [ShardEngine(d, self.S, s, filters_hint=filters_hint // max(self.S, 1) + 1)
+                            for s, d in enumerate(self.devices)]
         self.comms = Comm.init_all(self.devices)
 
     def insert_many(self, buf, off):
@@ -291,6 +305,7 @@ class ShardSet:
             keys = torch.empty(cap * KW, dtype=torch.int64, device=dev)
             e.match_keys_device(d_b, d_o, n, int(to[-1]), c, o, ids, keys, cap, t, key_words=KW, stream=st)
             st.synchronize()
+            check_total(t, cap, "shard %d keyed walk" % s)
             if e.key_levels() > 32 * KW - 1:
                 raise RuntimeError("order keys too narrow for the batch")
             lists.append((c, o, ids, keys, cap, d_b, d_o))
@@ -315,6 +330,8 @@ class ShardSet:
             self.engines[r].merge_device(m, x.d_counts, x.d_src_base, x.d_ids, x.d_keys, oc, oo, og, x.total + 1,
                                          tot, stream=streams[r], key_words=KW, key_stride=x.total)
             streams[r].synchronize()
+            if check_total(tot, x.total + 1, "merge of slice %d" % r) != x.total:
+                raise RuntimeError("merge of slice %d: %d ids merged, %d received" % (r, int(tot.item()), x.total))
             counts.append(oc[:m].cpu().numpy().view(np.uint32))
             offs.extend((oo[1:].cpu().numpy() + offs[-1]).tolist())
             gids.append(og[: x.total].cpu().numpy().view(np.uint32))
@@ -476,6 +493,8 @@ class RoutedSet:
             cap = int(t.item()) + 1
             ids = torch.empty(cap, dtype=torch.int32, device=dev)
             e.match_batch_device(o.d_bytes, o.d_off, m, o.bytes, c, oo, ids, cap, t, stream=streams[s])
+            streams[s].synchronize()
+            check_total(t, cap, "routed shard %d walk" % s)
             lists.append((c, oo, ids))
         ls = (L.TmRouteLists * S)(*[L.TmRouteLists(_p(c).value, _p(oo).value, _p(ids).value, _sp(streams[s]))
                                     for s, (c, oo, ids) in enumerate(lists)])

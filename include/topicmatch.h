@@ -298,6 +298,12 @@ int  tm_comm_init_all(const int32_t* devices, uint32_t n, tm_comm** comms);
 void tm_comm_destroy(tm_comm* c);
 int  tm_comm_uses_rccl(tm_comm* c);   /* 1: RCCL, 0: device copies */
 const char* tm_comm_last_error(tm_comm* c);
+/* A rank's own part of every exchange (tm_shard_exchange, tm_route_exchange,
+ * tm_route_return) through RCCL too -- ncclSend / ncclRecv to itself inside
+ * the group, and the size all-to-alls over RCCL at one rank -- instead of a
+ * device copy.  Slower; it exists so that a one-GPU box (one rank) executes
+ * the RCCL code paths the multi-GPU ranks take.  TM_EINVAL without RCCL. */
+int  tm_comm_set_self_rccl(tm_comm* c, int on);
 /* one rank (RCCL communicator) of a multi-process exchange; stream-ordered
  * after two small host syncs that size the sends and receives */
 int  tm_shard_exchange(tm_comm* c, const tm_exchange_in* in, tm_exchange_out* out);
@@ -658,10 +664,6 @@ int  tm_rewrite_match_batch_device(tm_rewrite* r, const uint8_t* d_topics, const
  *              heat class (A/B)
  *   "sort_min" presort 3's smallest batch walked in range-local word-hash order
  *              (default 3000000)
- *   "tail_wave" the last tail_wave positions of each of the walk's 8 XCD
- *              ranges are walked a wave per topic (tm_walk_tail) on a second
- *              stream beside the persistent walk, in the slots its waves give
- *              up as its queue runs dry (0 = off)
  *   "sort_bits" the key bits presort 1 and 5 sort, one radix pass per 8
  *              (8..32, default 24; presort 5: the XCD range over the
  *              word-hash key's top sort_bits - 3 bits)

@@ -134,7 +134,6 @@ def test_c5_1m_filters_vs_o1(gpu_device, capsys):
 
 
 def test_c4_100m_filters_sharded_8_vs_replicated_vs_o3(gpu_device, capsys):
-    import torch
     from emqx_amd import Engine, shard
     from emqx_amd import workload as W
     say = _Progress(capsys, "C4")
@@ -188,48 +187,18 @@ def test_c4_100m_filters_sharded_8_vs_replicated_vs_o3(gpu_device, capsys):
     say("built: replicated %d nodes, shards %s filters" % (rep.node_count, [x.filter_count for x in engs]))
     tb, to = W.topics(4, n=20_000)
     n = len(to) - 1
-    dev = torch.device("cuda", gpu_device)
-    d_b = torch.from_numpy(tb.copy()).to(dev)
-    d_o = torch.from_numpy(to.view(np.int64).copy()).to(dev)
-    KW = shard.key_words_for(tb, to)
-    res = []
-    for e in engs:
-        c = torch.empty(n, dtype=torch.int32, device=dev)
-        o = torch.empty(n + 1, dtype=torch.int64, device=dev)
-        tot = torch.zeros(1, dtype=torch.int64, device=dev)
-        e.match_keys_device(d_b, d_o, n, int(to[-1]), c, o, None, None, 0, tot, key_words=KW)
-        torch.cuda.synchronize()
-        cap = int(tot.item()) + 16
-        ids = torch.empty(cap, dtype=torch.int32, device=dev)
-        keys = torch.empty(cap * KW, dtype=torch.int64, device=dev)
-        e.match_keys_device(d_b, d_o, n, int(to[-1]), c, o, ids, keys, cap, tot, key_words=KW)
-        torch.cuda.synchronize()
-        res.append((c, o, ids, keys.view(KW, cap)))
-    b = shard.slices(n, S)
-    merged_off, merged_gid = [0], []
-    for r in range(S):       # rank r's receive + merge, as shard.exchange delivers it
-        m = b[r + 1] - b[r]
-        rc = torch.cat([res[s][0][b[r]:b[r + 1]] for s in range(S)])
-        cuts = [(int(res[s][1][b[r]].item()), int(res[s][1][b[r + 1]].item())) for s in range(S)]
-        sizes = [hi - lo for lo, hi in cuts]
-        tot_r = sum(sizes)
-        rid = torch.cat([res[s][2][lo:hi] for s, (lo, hi) in enumerate(cuts)] +
-                        [torch.zeros(1, dtype=torch.int32, device=dev)])
-        rk = torch.cat([torch.cat([res[s][3][j, lo:hi] for s, (lo, hi) in enumerate(cuts)]) for j in range(KW)] +
-                       [torch.zeros(1, dtype=torch.int64, device=dev)])
-        base = torch.tensor(np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.int64), device=dev)
-        oc = torch.empty(max(m, 1), dtype=torch.int32, device=dev)
-        oo = torch.empty(m + 1, dtype=torch.int64, device=dev)
-        tot = torch.zeros(1, dtype=torch.int64, device=dev)
-        og = torch.empty(tot_r + 1, dtype=torch.int32, device=dev)
-        engs[r].merge_device(m, rc, base, rid, rk, oc, oo, og, tot_r + 1, tot, key_words=KW, key_stride=tot_r)
-        torch.cuda.synchronize()
-        assert int(tot.item()) == tot_r
-        oo_h = oo.cpu().numpy()
-        merged_off.extend((oo_h[1:] + merged_off[-1]).tolist())
-        merged_gid.append(og[:tot_r].cpu().numpy().view(np.uint32))
-    say("sharded walk + merge done")
+    # the product path of the sharded mode in one process: every shard's keyed
+    # walk, tm_shard_exchange_group (the 8 shards share this GPU, so the
+    # exchange moves each slice by device copies where ranks on 8 GPUs use
+    # RCCL), then each slice's device merge (shard.ShardSet.match_batch)
+    ss = shard.ShardSet([gpu_device] * S, engines=engs)
+    assert not any(c.rccl for c in ss.comms)
+    m_counts, m_offs, m_gids = ss.match_batch(tb, to)
+    merged_off = m_offs
+    merged_gid = [m_gids]
+    say("sharded walk + exchange (tm_shard_exchange_group) + merge done")
     counts, offs, ids = rep.match_batch(tb, to)
+    assert np.array_equal(m_counts, counts)
     assert np.array_equal(np.asarray(merged_off, dtype=np.uint64), offs)
     # both id spaces -> the filter's index in the generated list: the
     # replicated engine numbers distinct filters in insertion order, a shard
@@ -247,5 +216,5 @@ def test_c4_100m_filters_sharded_8_vs_replicated_vs_o3(gpu_device, capsys):
     assert np.array_equal(oi, ids[: int(oo[-1])])
     say("10K topics: replicated == O3 over 100M filters, %d matches" % int(oo[-1]))
     box["o3"].close()
-    for e in engs + [rep]:
-        e.close()
+    ss.close()
+    rep.close()

@@ -261,9 +261,6 @@ VARIANTS = {"queue": {}, "queue_xcd": {}, "queue_xcd@nosplit@dfs": {"split": 0, 
             "queue_xcd@presort@bits24": {"presort": 1, "sort_bits": 24},
             "queue_xcd@presort@bits16@norows": {"presort": 1, "sort_bits": 16, "chunk_rows": 0},
             # the last positions of each XCD range walked a wave per topic on a second stream
-            "queue_xcd@tailwave": {"tail_wave": 256},
-            "queue_xcd@tailwave@presort@stagek8": {"tail_wave": 512, "presort": 1, "stage_k": 8, "stage_auto": 0},
-            "queue_xcd@tailwave@tail@nospill": {"tail_wave": 256, "presort": 2, "spill": 0},
             # range-keyed orders with a word-hash part (two radix passes)
             "queue_xcd@order4": {"presort": 4}, "queue_xcd@order5@stagek8": {"presort": 5, "stage_k": 8}}
 
@@ -477,3 +474,84 @@ def test_pipelined_host_batch_equals_one_shot_and_o1(gpu_device):
         assert np.array_equal(c0[lo:lo + 1000], oc)
         assert np.array_equal(i0[o0[lo]:o0[lo + 1000]], oi)
     o1.close()
+
+
+def test_pipelined_host_owned_output_grows_exact(gpu_device):
+    """the pipelined path sizes an owned output from its first
+    chunk's fan-out (x 1.15 over the batch) and grows it when a later chunk
+    outruns that.  Here the first 1M-topic chunk matches few filters (words no
+    filter holds below the root: only root '+' / '#' filters fire) and the
+    rest are C1 topics (~10x the fan-out), so the grow-and-copy branch runs;
+    the lists equal the one-shot path and O1 on every topic"""
+    from emqx_amd.engine import pack
+    fb, fo = W.filters(1)
+    low = [b"zz%d/q%d/r/s/t" % (i % 997, i) for i in range(1_100_000)]
+    hb, ho = W.topics(1, n=1_300_000, stream=9)
+    topics = low + [bytes(x) for x in W.unpack(hb, ho)]
+    tb, to = pack(topics)
+    o1 = O1()
+    o1.insert_many(fb, fo)
+    wc, wo, wi = o1.match_ids(tb, to, threads=16)
+    o1.close()
+    first = int(wo[1 << 20]) / (1 << 20)
+    rest = (int(wo[-1]) - int(wo[1 << 20])) / (len(topics) - (1 << 20))
+    assert rest > 1.5 * first * 1.15, (first, rest)   # a later chunk outruns the first one's estimate
+    e = Engine(device=gpu_device)
+    e.insert_many(fb, fo)
+    e.set_option("host_pipeline", 1)
+    c1, o1_, i1 = e.match_batch(tb, to)                  # pipelined, owned: grows
+    assert np.array_equal(c1, wc) and np.array_equal(o1_, wo) and np.array_equal(i1, wi)
+    e.set_option("host_pipeline", 0)
+    c0, o0, i0 = e.match_batch(tb, to)
+    assert np.array_equal(c0, wc) and np.array_equal(i0, wi)
+    e.close()
+
+
+def test_side_stream_call_waits_for_fills_on_the_current_stream(gpu_device):
+    """VERDICT r4 (the r04_f routed mismatch): outputs made on torch's current
+    stream (a zero-filled total, an id buffer) are filled behind a long
+    kernel; the engine is then called on a side stream.  _lib.stream_handle
+    makes the side stream wait for the current one, so the engine writes
+    after the fills: exact total and lists every time.  Without that wait the
+    engine would run first and the late fills would overwrite its total and
+    ids (counts and offsets intact): the failure mode the round-4 log showed."""
+    import torch
+    fb, fo = W.filters(1)
+    tb, to = W.topics(1, n=30_000, stream=3)
+    o1 = O1()
+    o1.insert_many(fb, fo)
+    wc, wo, wi = o1.match_ids(tb, to, threads=8)
+    o1.close()
+    e = Engine(device=gpu_device)
+    e.insert_many(fb, fo)
+    e.commit()
+    dev = torch.device("cuda", gpu_device)
+    n = len(to) - 1
+    d_b = torch.from_numpy(np.ascontiguousarray(tb)).to(dev)
+    d_o = torch.from_numpy(np.ascontiguousarray(to).view(np.int64)).to(dev)
+    cap = int(wo[-1]) + 16
+    side = torch.cuda.Stream(device=dev)
+    cur = torch.cuda.current_stream(dev)
+    big = torch.randn(4096, 4096, device=dev)
+
+    def long_kernel():   # ~tens of ms on the current stream
+        if hasattr(torch.cuda, "_sleep"):
+            torch.cuda._sleep(200_000_000)
+        else:
+            x = big
+            for _ in range(40):
+                x = x @ big
+    for trial in range(3):
+        long_kernel()
+        c = torch.full((n,), 7, dtype=torch.int32, device=dev)
+        oo = torch.full((n + 1,), 7, dtype=torch.int64, device=dev)
+        ids = torch.full((cap,), -1, dtype=torch.int32, device=dev)
+        t = torch.zeros(1, dtype=torch.int64, device=dev)
+        e.match_batch_device(d_b, d_o, n, int(to[-1]), c, oo, ids, cap, t, stream=side)
+        side.synchronize()
+        cur.synchronize()
+        assert int(t.item()) == int(wo[-1]), trial
+        assert np.array_equal(c.cpu().numpy().view(np.uint32), wc)
+        assert np.array_equal(oo.cpu().numpy().view(np.uint64), wo)
+        assert np.array_equal(ids[: int(wo[-1])].cpu().numpy().view(np.uint32), wi)
+    e.close()

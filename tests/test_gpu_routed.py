@@ -86,3 +86,66 @@ def test_routed_c2_sample_and_empty_rank(gpu_device):
     batches = [W.topics(2, n=20000, stream=7), W.topics(2, n=0, stream=8), W.topics(2, n=5000, stream=9)]
     got = _run(fb, fo, batches, 3, 2)
     _check(fb, fo, batches, got)
+
+
+@pytest.mark.parametrize("self_rccl", [False, True])
+def test_route_exchange_one_rank_rccl_equals_o1(gpu_device, self_rccl):
+    """the multi-process entry points tm_route_exchange / tm_route_return (one
+    rank per process, as bench.py --mode routed runs them) on a one-rank RCCL
+    communicator: plan, size all-to-all, transfers, receive scan, the owner's
+    walk, the return and the unpermute.  self_rccl: the rank's own buckets go
+    through ncclSend / ncclRecv to itself and the size exchanges through
+    ncclAllToAll, i.e. the RCCL code the ranks of a multi-GPU node run."""
+    import torch
+    from emqx_amd import shard
+    from emqx_amd import workload as W
+    from emqx_amd.engine import check_total
+    fb, fo = W.filters(1)
+    tb, to = W.topics(1, n=9000, stream=4)
+    comm = shard.Comm.init_rank(shard.Comm.unique_id(), 1, 0, gpu_device)
+    assert comm.rccl
+    if self_rccl:
+        comm.set_self_rccl(True)
+    e = shard.RoutedEngine(gpu_device, 1, 0, depth=2)
+    e.insert_many(fb, fo)
+    e.commit()
+    dev = torch.device("cuda", gpu_device)
+    st = torch.cuda.Stream(device=dev)
+    pad = np.zeros(len(tb) + 16, dtype=np.uint8)
+    pad[:len(tb)] = tb
+    d_b = torch.from_numpy(pad).to(dev)
+    d_o = torch.from_numpy(np.ascontiguousarray(to).view(np.int64).copy()).to(dev)
+    n = len(to) - 1
+    for rep in range(2):
+        o = shard.route_exchange(comm, shard.route_in(n, int(to[-1]), d_b, d_o, 2, st))
+        assert o.m == n and o.bytes == int(to[-1])
+        c = torch.empty(o.m, dtype=torch.int32, device=dev)
+        oo = torch.empty(o.m + 1, dtype=torch.int64, device=dev)
+        t = torch.zeros(1, dtype=torch.int64, device=dev)
+        e.match_batch_device(o.d_bytes, o.d_off, o.m, o.bytes, c, oo, None, 0, t, stream=st)
+        st.synchronize()
+        cap = int(t.item()) + 1
+        ids = torch.empty(cap, dtype=torch.int32, device=dev)
+        e.match_batch_device(o.d_bytes, o.d_off, o.m, o.bytes, c, oo, ids, cap, t, stream=st)
+        st.synchronize()
+        check_total(t, cap)
+        r = shard.route_return(comm, c, oo, ids, stream=st)
+        st.synchronize()
+        got = (shard._dev_array(r.d_counts, r.n, np.uint32, gpu_device),
+               shard._dev_array(r.d_offs, r.n + 1, np.uint64, gpu_device),
+               shard._dev_array(r.d_ids, r.total, np.uint32, gpu_device))
+        _check(fb, fo, [(tb, to)], [got])
+    comm.close()
+    e.close()
+
+
+def test_routed_64_shards_one_gpu_equals_o1(gpu_device):
+    """MAX_ROUTE_SHARDS = 64 shards (the plan's S + 1 = 65 bucket
+    cuts used to be gathered by one 64-lane block, leaving the last cut
+    unwritten): every rank's lists equal O1; most shards own few or no topics"""
+    from emqx_amd import workload as W
+    fb, fo = W.filters(1)
+    S = 64
+    batches = [W.topics(1, n=(300 if r % 7 else 0) + 11 * r, stream=100 + r) for r in range(S)]
+    got = _run(fb, fo, batches, S, 2)
+    _check(fb, fo, batches, got)

@@ -264,10 +264,12 @@ def test_shardset_native_exchange_equals_o1(gpu_device, S):
     ss.close()
 
 
-def test_rccl_one_rank_exchange_equals_o1(gpu_device):
+@pytest.mark.parametrize("self_rccl", [False, True])
+def test_rccl_one_rank_exchange_equals_o1(gpu_device, self_rccl):
     """the RCCL path of tm_shard_exchange on the one GPU of the box: a
-    one-rank communicator (send / receive to itself inside ncclGroup), then
-    the merge"""
+    one-rank communicator (the size all-to-all over RCCL; with self_rccl the
+    counts, ids and keys too, by send / receive to itself inside the group),
+    then the merge"""
     import torch
     from emqx_amd import shard
     from emqx_amd import workload as W
@@ -278,6 +280,8 @@ def test_rccl_one_rank_exchange_equals_o1(gpu_device):
     tb, to = pack(topics)
     comm = shard.Comm.init_rank(shard.Comm.unique_id(), 1, 0, gpu_device)
     assert comm.rccl
+    if self_rccl:
+        comm.set_self_rccl(True)
     e = shard.ShardEngine(gpu_device, 1, 0)
     e.insert_many(fb, fo)
     dev = torch.device("cuda", gpu_device)

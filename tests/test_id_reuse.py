@@ -135,3 +135,90 @@ def test_gpu_batcher_callbacks_under_delete_reinsert_churn(gpu_device):
     assert not missing, missing[:5]
     assert not bad, bad[:5]
     eng.close()
+
+
+# ---- caller-chosen (global) ids: tm_insert_batch_ids (sharded / routed engines)
+
+def _ins_ids(eng, filters, ids):
+    from emqx_amd.engine import pack
+    b, o = pack(filters)
+    eng.insert_many_ids(b, o, ids)
+
+
+def test_forced_id_of_another_filter_waits_out_the_quarantine():
+    """a deleted id taken at once by a forced insert skipped the
+    epoch / lease guard.  Now another filter gets it only once both images
+    dropped it and no older lease is open; the same filter may take it back
+    at once (whatever a batch in flight names, it is still that filter)."""
+    from emqx_amd import _lib as L
+    eng = Engine(device=-1)
+    _ins_ids(eng, [b"a/+", b"b/#"], [7, 9])
+    eng.commit()
+    assert fid(eng, b"a/+") == 7 and fid(eng, b"b/#") == 9
+    eng.delete(b"a/+")
+    with pytest.raises(L.TopicMatchError):
+        _ins_ids(eng, [b"z/+"], [7])                      # another filter, before any commit
+    eng.commit()
+    with pytest.raises(L.TopicMatchError):
+        _ins_ids(eng, [b"z/+"], [7])                      # one image still holds 7
+    assert eng.filters_bytes([7]) == [b"a/+"]
+    eng.commit()
+    _ins_ids(eng, [b"z/+"], [7])                          # both images dropped it, no lease: reusable
+    assert fid(eng, b"z/+") == 7 and eng.filters_bytes([7]) == [b"z/+"]
+    # the same filter back under its own id: at once
+    eng.delete(b"b/#")
+    _ins_ids(eng, [b"b/#"], [9])
+    assert fid(eng, b"b/#") == 9
+    eng.close()
+
+
+def test_forced_id_respects_open_leases():
+    from emqx_amd import _lib as L
+    eng = Engine(device=-1)
+    _ins_ids(eng, [b"a/+"], [3])
+    eng.commit()
+    lease = eng.lease()
+    lease.__enter__()
+    eng.delete(b"a/+")
+    for _ in range(3):
+        eng.commit()
+        with pytest.raises(L.TopicMatchError):
+            _ins_ids(eng, [b"q/+"], [3])
+    lease.__exit__(None, None, None)
+    eng.commit()
+    _ins_ids(eng, [b"q/+"], [3])
+    assert fid(eng, b"q/+") == 3
+    eng.close()
+
+
+def test_forced_ids_duplicate_filter_and_live_id():
+    """a filter already present under another id was silently
+    kept under the old id; a live id is refused as before"""
+    from emqx_amd import _lib as L
+    eng = Engine(device=-1)
+    _ins_ids(eng, [b"s/+/x"], [5])
+    _ins_ids(eng, [b"s/+/x"], [5])                        # same filter, same id: idempotent
+    with pytest.raises(L.TopicMatchError):
+        _ins_ids(eng, [b"s/+/x"], [6])                    # same filter, another id
+    with pytest.raises(L.TopicMatchError):
+        _ins_ids(eng, [b"t/#"], [5])                      # another filter, a live id
+    assert eng.filter_count == 1 and fid(eng, b"s/+/x") == 5
+    eng.close()
+
+
+def test_forced_only_engine_drains_its_quarantine_at_commit():
+    """a forced-only engine (routed shards) never calls the id allocator, so
+    the quarantine must drain at commit: many delete / re-insert rounds of
+    distinct filters under recycled ids all succeed after two commits"""
+    eng = Engine(device=-1)
+    ids = list(range(100, 164))
+    _ins_ids(eng, [b"r0/%d/+" % i for i in ids], ids)
+    eng.commit()
+    for rnd in range(1, 6):
+        for i in ids:
+            eng.delete(b"r%d/%d/+" % (rnd - 1, i))
+        eng.commit()
+        eng.commit()
+        _ins_ids(eng, [b"r%d/%d/+" % (rnd, i) for i in ids], ids)
+        assert all(fid(eng, b"r%d/%d/+" % (rnd, i)) == i for i in ids)
+    eng.close()

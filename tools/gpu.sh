@@ -14,6 +14,8 @@
 #   slices    rocprofv3 stats of one-GPU batches of $SLICES topics (the per-rank slices of strong scaling)
 #   rehearse  the driver's N > 1 launch with $NPROC ranks sharing GPU 0 (control plane over gloo)
 #   routed    bench --mode routed in one process: $SHARDS routed shards on GPU 0 (device-copy exchange)
+#   routed1   bench --mode routed through the driver's torchrun launch at world 1, own buckets over RCCL
+#   sharded1  bench --mode sharded likewise (tm_shard_exchange over a one-rank RCCL communicator)
 #   batcher   tools/bench_batcher.py $BATCHER_ARGS (flood: per-stage split, eager sealing, replicas)
 # e.g. gpurun -- 'STEPS="tests bench prof" TAG=r02_head bash tools/gpu.sh'
 set -o pipefail
@@ -51,6 +53,12 @@ for s in ${STEPS:-tests}; do
     routed) timeout -k 10 600 python3 -u bench.py --mode routed --single-process --shards ${SHARDS:-4} \
                --steps 20 --warmup 3 --depth ${DEPTH:-2} ${BENCH_ARGS} > "$OUT/routed_${SHARDS:-4}.json" \
                2> "$OUT/routed_${SHARDS:-4}.log" ;;
+    routed1) timeout -k 10 600 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
+               --master-port ${PORT:-29534} bench.py --mode routed --self-rccl --steps 20 --warmup 3 \
+               --depth ${DEPTH:-2} ${BENCH_ARGS} > "$OUT/routed_torchrun_w1.json" 2> "$OUT/routed_torchrun_w1.log" ;;
+    sharded1) timeout -k 10 600 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
+               --master-port ${PORT:-29535} bench.py --mode sharded --self-rccl --steps 10 --warmup 2 \
+               ${BENCH_ARGS} > "$OUT/sharded_torchrun_w1.json" 2> "$OUT/sharded_torchrun_w1.log" ;;
     batcher) timeout -k 10 ${T_BATCHER:-600} python3 -u tools/bench_batcher.py ${BATCHER_ARGS} \
                >> "$OUT/batcher.jsonl" 2>> "$OUT/batcher.log" ;;
     cmd)   timeout -k 10 ${T_CMD:-600} python -u -c "$CMD" > "$OUT/cmd.log" 2>&1 ;;
