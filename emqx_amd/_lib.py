@@ -40,7 +40,7 @@ class TmBatchStats(ctypes.Structure):
 class TmBatcherConfig(ctypes.Structure):
     _fields_ = [("max_topics", ctypes.c_uint32), ("deadline_us", ctypes.c_uint32), ("max_bytes", ctypes.c_uint64),
                 ("flags", ctypes.c_uint32), ("lanes_per_replica", ctypes.c_uint32),
-                ("callback_threads", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+                ("callback_threads", ctypes.c_uint32), ("eager_us", ctypes.c_uint32)]
 
 
 class TmBatcherStats(ctypes.Structure):

@@ -247,10 +247,13 @@ struct tm_batcher {
         const uint64_t n = pending(&b, &o);
         if (n == 0) return false;
         if (n >= cfg.max_topics || b >= cfg.max_bytes || force.load(std::memory_order_acquire)) return true;
-        // TM_BATCHER_EAGER: a free lane takes whatever is pending (under mu)
-        if ((cfg.flags & TM_BATCHER_EAGER) && !free_lanes.empty()) return true;
-        return now_ns() - o >= (int64_t)cfg.deadline_us * 1000;
+        const int64_t age = now_ns() - o;
+        // TM_BATCHER_EAGER: a free lane takes what is pending once the oldest
+        // topic has waited eager_us or a fair batch is there (under mu)
+        if (eager_ready() && (age >= (int64_t)cfg.eager_us * 1000 || n >= TM_BATCHER_EAGER_TOPICS)) return true;
+        return age >= (int64_t)cfg.deadline_us * 1000;
     }
+    bool eager_ready() const { return (cfg.flags & TM_BATCHER_EAGER) && !free_lanes.empty(); }
 
     // move stripes' topics (oldest first, up to max_topics) into lane L's
     // chunk list: a stripe that fits whole is swapped out, one holding more
@@ -620,7 +623,10 @@ struct tm_batcher {
                 if (pending() == 0) sleep_for(lk, std::chrono::milliseconds(50));
                 sealer_idle.store(false, std::memory_order_release);
             } else {
-                const int64_t left = oldest + (int64_t)cfg.deadline_us * 1000 - now_ns();
+                // until the deadline, or the eager age when a lane is free
+                // (a lane freed or a batch's worth arriving meanwhile wakes it)
+                const uint32_t us = eager_ready() ? std::min(cfg.eager_us, cfg.deadline_us) : cfg.deadline_us;
+                const int64_t left = oldest + (int64_t)us * 1000 - now_ns();
                 if (left > 0) sleep_for(lk, std::chrono::nanoseconds(std::min<int64_t>(left, 1000000)));
             }
         }
@@ -673,6 +679,7 @@ int tm_batcher_open(tm_engine* e, const tm_batcher_config* cfg, tm_batcher** out
     if (b->cfg.max_topics == 0) b->cfg.max_topics = 65536;
     if (b->cfg.max_bytes == 0) b->cfg.max_bytes = 64ull << 20;
     if (b->cfg.deadline_us == 0) b->cfg.deadline_us = 200;
+    if (b->cfg.eager_us == 0) b->cfg.eager_us = 60;
     const uint32_t per = b->cfg.lanes_per_replica ? b->cfg.lanes_per_replica : 2u;
     const int R = tm_engine_replicas(e);
     b->host_only = R == 0;
@@ -739,7 +746,8 @@ int tm_batcher_submit(tm_batcher* b, const uint8_t* topic, uint32_t len, tm_batc
     // wake the sealer only when it sleeps with nothing pending (it times the
     // deadline itself), or when this stripe alone could fill a batch
     if ((was == 0 && b->sealer_idle.exchange(false, std::memory_order_seq_cst)) ||
-        was + 1 == b->cfg.max_topics / NSTRIPE)
+        was + 1 == b->cfg.max_topics / NSTRIPE ||
+        ((b->cfg.flags & TM_BATCHER_EAGER) && was + 1 == TM_BATCHER_EAGER_TOPICS / NSTRIPE))
         b->kick();
     if (ticket_out) *ticket_out = t;
     return TM_OK;

@@ -1048,6 +1048,7 @@ struct tm_engine {
     // filters
     // the id the next new filter takes (tm_insert_batch_ids), FILTER_NONE: allocate one
     uint32_t forced_fid = FILTER_NONE;
+    bool forced_dup_first = false;   // a filter already present keeps its id (tm_insert_batch_routed)
     uint32_t new_filter(const uint8_t* p, uint32_t len, uint32_t node) {
         uint32_t id = FILTER_NONE;
         if (forced_fid != FILTER_NONE) {   // a caller-chosen (global) id: holes below it stay unused
@@ -1128,9 +1129,10 @@ struct tm_engine {
         if (nodes[v].self_filter == FILTER_NONE) {
             set_topic(v, new_filter(p, len, v));
             add_summaries(!tmp_words.empty() && tmp_words.back() == WORD_HASH);
-        } else if (forced_fid != FILTER_NONE && nodes[v].self_filter != forced_fid) {
+        } else if (forced_fid != FILTER_NONE && nodes[v].self_filter != forced_fid && !forced_dup_first) {
             // the filter is in the trie under another id: a caller that
             // believes it now has forced_fid would mis-name its matches
+            // (tm_insert_batch_routed instead keeps the first occurrence's id)
             throw ArgError("filter already present under id " + std::to_string(nodes[v].self_filter) +
                            ", not " + std::to_string(forced_fid));
         }
@@ -2806,8 +2808,12 @@ int tm_insert_batch_routed(tm_engine* e, const uint8_t* bytes, const uint64_t* o
     return guarded(e, [&] {
         struct Reset {
             tm_engine* e;
-            ~Reset() { e->forced_fid = FILTER_NONE; }
+            ~Reset() {
+                e->forced_fid = FILTER_NONE;
+                e->forced_dup_first = false;
+            }
         } reset{e};
+        e->forced_dup_first = true;
         for (uint32_t i = 0; i < n; ++i) {
             if (off[i + 1] < off[i] || off[i + 1] - off[i] > 0xFFFFFFFFull) throw ArgError("bad offsets");
             const uint32_t len = (uint32_t)(off[i + 1] - off[i]);
@@ -3687,6 +3693,12 @@ int tm_set_option(tm_engine* e, const char* name, int64_t value) {
         if (!std::strcmp(name, "layout")) {
             if (value < 0 || value > 2) return TM_EINVAL;
             e->layout_mode = (int)value;
+            return TM_OK;
+        }
+        if (!std::strcmp(name, "relayout")) {   // 1: relayout at the next commit (layout A/Bs)
+            if (value != 1) return TM_EINVAL;
+            e->force_relayout = true;
+            e->dev_dirty = true;
             return TM_OK;
         }
         if (!std::strcmp(name, "presort")) {   // 0 arrival order, 1 word-hash key, 2 the tail order, 3 auto

@@ -333,11 +333,20 @@ uint32_t tm_route_of(const uint8_t* topic, uint32_t len, uint32_t n_shards, uint
  * unique, < 2^31 - 16): a sharded or routed engine holds its part of a global
  * filter set under the global ids, so its walks emit them directly.  An engine
  * filled this way must not also take tm_insert / tm_insert_batch (their ids
- * would collide).  TM_EINVAL when ids[i] names another live filter. */
+ * would collide).  TM_EINVAL when ids[i] names another live filter, when the
+ * filter is present under another id, or when ids[i] was deleted from another
+ * filter and batches in flight may still name it (it is reusable for another
+ * filter after two commits and once the leases open at the delete end; the
+ * same filter may take it back at once). */
 int tm_insert_batch_ids(tm_engine* e, const uint8_t* bytes, const uint64_t* off, uint32_t n, const uint32_t* ids);
 
 /* tm_insert_batch_ids of the filters tm_route_of places on `shard` (routed to
- * it, or to every shard), filter i of the batch under global id gid_base + i. */
+ * it, or to every shard), filter i of the batch under global id gid_base + i.
+ * A filter repeated in the batch (or already present) keeps the id of its
+ * first insertion: emqx_trie:insert/1 is idempotent (src/emqx_trie.erl:62-73),
+ * so a list with repeats names each filter by its first index.  (tm_insert_
+ * batch_ids, whose caller states every id, refuses a filter present under
+ * another id with TM_EINVAL.) */
 int tm_insert_batch_routed(tm_engine* e, const uint8_t* bytes, const uint64_t* off, uint32_t n, uint32_t n_shards,
                            uint32_t shard, uint32_t depth, uint32_t gid_base);
 
@@ -523,8 +532,14 @@ int tm_match_deliveries_batch_device(tm_engine* e, const uint8_t* d_topic_bytes,
 #define TM_BATCHER_DELIVERIES 2u   /* results are aggre(match_routes/1) (To ids + target ids) */
 #define TM_BATCHER_CSR 8u   /* small match/1 batches through tm_match_batch_device (four launches and a
                               scan) instead of the one-launch tm_match_small_device (A/B) */
-#define TM_BATCHER_EAGER 4u   /* seal as soon as a lane is free (deadline_us stays the upper bound): low
-                                 load runs small batches at once, high load batches up while lanes are busy */
+#define TM_BATCHER_EAGER 4u   /* seal as soon as a lane is free AND the oldest pending topic has waited
+                                 eager_us or TM_BATCHER_EAGER_TOPICS are pending (deadline_us stays the
+                                 upper bound): low load runs small batches early, high load batches up
+                                 while lanes are busy, and no load makes batches of a handful of topics
+                                 (a sealed batch costs ~100 us of host and PCIe latency, and tens of
+                                 thousands of them a second crowd the host: the p99 of sealing at every
+                                 free lane was 4 ms at 1M publishes/s) */
+#define TM_BATCHER_EAGER_TOPICS 256u
 
 typedef struct tm_batcher tm_batcher;
 typedef struct tm_batcher_config {
@@ -535,7 +550,8 @@ typedef struct tm_batcher_config {
     uint32_t lanes_per_replica; /* batches in flight per GPU (0 = 2)            */
     uint32_t callback_threads;  /* threads that share a batch's callbacks with its lane
                                    (parts of >= 8192 topics; 0 = the lane alone) */
-    uint32_t reserved;
+    uint32_t eager_us;        /* TM_BATCHER_EAGER: least age of the oldest pending topic for a seal at a
+                                 free lane (0 = 60; >= deadline_us: deadline sealing) */
 } tm_batcher_config;
 typedef struct tm_batcher_stats {
     uint64_t batches, topics, results, max_batch;

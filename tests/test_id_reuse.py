@@ -222,3 +222,17 @@ def test_forced_only_engine_drains_its_quarantine_at_commit():
         _ins_ids(eng, [b"r%d/%d/+" % (rnd, i) for i in ids], ids)
         assert all(fid(eng, b"r%d/%d/+" % (rnd, i)) == i for i in ids)
     eng.close()
+
+
+def test_routed_insert_repeated_filter_keeps_first_id():
+    """tm_insert_batch_routed over a list with repeats: emqx_trie:insert/1 is
+    idempotent, so the repeat keeps its first index (a list's filter i is
+    named by the first i holding it)"""
+    from emqx_amd import shard
+    from emqx_amd.engine import pack
+    eng = shard.RoutedEngine(-1, 1, 0, depth=1)
+    b, o = pack([b"x/+", b"y/#", b"x/+", b"z"])
+    eng.insert_many(b, o)
+    assert fid(eng, b"x/+") == 0 and fid(eng, b"y/#") == 1 and fid(eng, b"z") == 3
+    assert eng.filter_count == 3
+    eng.close()

@@ -41,6 +41,8 @@ def main():
     ap.add_argument("--opt", action="append", default=[], help="engine option name=value (repeatable)")
     ap.add_argument("--lib", default=None, help="EXPERIMENT: alternative build of libtopicmatch.so")
     ap.add_argument("--eager", default="0", help="comma list of 0/1: TM_BATCHER_EAGER (seal when a lane is free)")
+    ap.add_argument("--eager-us", default="0", help="comma list: tm_batcher_config.eager_us (0 = the library's "
+                    "default) for the eager points")
     ap.add_argument("--csr", default="0", help="comma list of 0/1: TM_BATCHER_CSR (small batches through the "
                     "four-launch CSR path instead of the one-launch tm_match_small_device)")
     a = ap.parse_args()
@@ -63,15 +65,16 @@ def main():
     f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_double,
                   ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                   ctypes.c_uint32, ctypes.POINTER(ctypes.c_double)]
-    for rate, eager, csr in [(float(x), int(g), int(c)) for x in a.rates.split(",") for g in a.eager.split(",")
-                             for c in a.csr.split(",")]:
+    for rate, eager, csr, eus in [(float(x), int(g), int(c), int(u)) for x in a.rates.split(",")
+                                  for g in a.eager.split(",") for c in a.csr.split(",")
+                                  for u in (a.eager_us.split(",") if int(g) else ["0"])]:
         for dl in [int(x) for x in a.deadlines.split(",")]:
             total = max(100_000, int(rate * a.seconds))
             log("offered %.0fM publishes/s, deadline %d us, %d publishes ..." % (rate / 1e6, dl, total))
             r = (ctypes.c_double * 16)()
             rc = f(e.h, tb.ctypes.data, to.ctypes.data, len(to) - 1, a.producers, rate, total, dl, a.max_topics,
-                   a.lanes, (4 if eager else 0) | (8 if csr else 0), a.cb_threads, r)
-            print(json.dumps({"opts": a.opt, "eager": eager, "csr": csr, "offered_per_s": rate, "deadline_us": dl, "max_topics": a.max_topics,
+                   a.lanes, (4 if eager else 0) | (8 if csr else 0) | (eus << 16), a.cb_threads, r)
+            print(json.dumps({"opts": a.opt, "eager": eager, "eager_us": eus, "csr": csr, "offered_per_s": rate, "deadline_us": dl, "max_topics": a.max_topics,
                               "lanes": a.lanes, "callback_threads": a.cb_threads, "producers": a.producers,
                               "rc": rc, "publishes": total, "secs": r[0], "achieved_per_s": r[1],
                               "batches": int(r[2]), "mean_batch": r[3], "lat_us_p50": r[4], "lat_us_p99": r[5],

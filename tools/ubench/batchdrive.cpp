@@ -145,7 +145,8 @@ extern "C" int tm_bench_batcher_open_loop(tm_engine* e, const uint8_t* tb, const
     bc.max_topics = max_topics;
     bc.deadline_us = deadline_us;
     bc.lanes_per_replica = lanes;
-    bc.flags = flags;
+    bc.flags = flags & 0xFFFFu;
+    bc.eager_us = flags >> 16;   // (this driver's convention: eager_us in the flags' high half)
     tm_batcher* b;
     int rc = tm_batcher_open(e, &bc, &b);
     if (rc != TM_OK) return rc;
