@@ -414,6 +414,10 @@ def main():
     # ---- timed region: K steps; barrier + sync on both sides, max over ranks
     dt = reg.timed(a.steps)
     kms = reg.kernel_times(a.roof_steps)
+    xcd = reg.walk_clocks()
+    if xcd:
+        log("walk per XCD (ms): " + " | ".join("%d: %.3f %.3f %.3f %d" % (i, x["start"], x["home_done"], x["end"],
+                                                                          x["stolen_chunks"]) for i, x in enumerate(xcd)))
     results = reg.results()
     n0 = reg.dbat[0][2]
 
@@ -426,10 +430,11 @@ def main():
         reg.warm(a.warmup)
         adt = reg.timed(a.steps)
         akms = reg.kernel_times(a.roof_steps)
+        axcd = reg.walk_clocks()
         ares = reg.results()
         same = all(np.array_equal(x[0], y[0]) and np.array_equal(x[1], y[1]) and np.array_equal(x[2], y[2])
                    for x, y in zip(ares, results))
-        ab.append({"opts": spec, "ms_per_step": adt / a.steps * 1e3, "kernel_ms": akms,
+        ab.append({"opts": spec, "ms_per_step": adt / a.steps * 1e3, "kernel_ms": akms, "walk_xcd_ms": axcd,
                    "value": (a.topics if a.scaling == "strong" else n0 * world) * a.steps / adt,
                    "lists_equal_headline": bool(same)})
         log("A/B %s: %.3f ms per step, kernels %s, lists equal: %s" % (spec, adt / a.steps * 1e3, akms, same))
@@ -543,6 +548,7 @@ def main():
                                        "prunable_visits": stats.get("prunable_visits", 0) / n0}},
             "cpu_baseline": cpu,
             "kernel_ms": kms,
+            "walk_xcd_ms": xcd,
             "filter_hits_per_s": stats["matches"] / n0 * topics_per_s,
             "fanout": fanout,
             "parity_check": check_ok,
@@ -651,6 +657,19 @@ class Region:
         kms = self.eng.last_kernel_times()
         self.eng.set_timing(False)
         return kms
+
+    def walk_clocks(self):
+        """per XCD of the last walk (batch 0 after kernel_times): ms from the
+        walk's first wave start to the XCD's first start, to its home range's
+        exhaustion (from then on its waves steal or drain) and to its last
+        wave's end, and the chunks it stole (engine diagnostic)"""
+        out = (ctypes.c_double * 32)()
+        f = self.eng.lib.tm_debug_walk_clocks
+        f.restype = ctypes.c_int
+        if f(self.eng.h, out) != 0:
+            return None
+        return [{"start": round(out[4 * x], 4), "home_done": round(out[4 * x + 1], 4), "end": round(out[4 * x + 2], 4),
+                 "stolen_chunks": int(out[4 * x + 3])} for x in range(8)]
 
     def results(self):
         """every batch's full result (host arrays: counts, offsets, ids)"""

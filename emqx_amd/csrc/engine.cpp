@@ -3540,6 +3540,40 @@ int tm_match_small_device(tm_engine* e, const uint8_t* d_bytes, const uint64_t* 
 // range-local word-hash order, 2 the tail order, 0 arrival order ...)
 extern "C" int tm_debug_last_order(tm_engine* e) { return e ? e->last_order.load() : TM_EINVAL; }
 
+// diagnostics (not part of include/topicmatch.h): the phases of the last
+// per-lane queue walk on replica 0, per XCD x (kernels.h QWS_CLOCK):
+// out[4x..4x+3] = ms from the walk's first wave start to XCD x's first wave
+// start, to the first exhaustion of its home range, to its last wave's end,
+// and the chunks its waves stole (-1 where not recorded)
+extern "C" int tm_debug_walk_clocks(tm_engine* e, double* out) {
+    if (!e || !out) return TM_EINVAL;
+    auto held = lock_batches(e);
+    return guarded(e, [&]() -> int {
+        if (e->devs.empty()) return TM_EINVAL;
+        DevState& d = *e->devs[0];
+        tm_engine::Guard g(d.device);
+        const DevBuf& ws = d.slots[d.last_slot].ws;
+        if (!ws.p) return TM_EINVAL;
+        HIPCHK(hipDeviceSynchronize());
+        std::vector<uint64_t> h(QWS_BYTES / 8);
+        HIPCHK(hipMemcpy(h.data(), ws.p, QWS_BYTES, hipMemcpyDeviceToHost));
+        int khz = 0;
+        HIPCHK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, d.device));
+        uint64_t t0 = UINT64_MAX;
+        for (int x = 0; x < 8; ++x)
+            if (h[QWS_CLOCK + 16 * x]) t0 = std::min<uint64_t>(t0, ~h[QWS_CLOCK + 16 * x]);
+        for (int x = 0; x < 8; ++x) {
+            const uint64_t* c = &h[QWS_CLOCK + 16 * x];
+            auto ms = [&](uint64_t t) { return khz > 0 ? (double)(t - t0) / (double)khz : -1.0; };
+            out[4 * x] = c[0] ? ms(~c[0]) : -1.0;
+            out[4 * x + 1] = c[1] ? ms(~c[1]) : -1.0;
+            out[4 * x + 2] = c[2] ? ms(c[2]) : -1.0;
+            out[4 * x + 3] = (double)c[3];
+        }
+        return TM_OK;
+    });
+}
+
 // diagnostics (not part of include/topicmatch.h): the last stats-mode
 // batch's per-level histogram [visits, probe loads, failed probes] x 16
 extern "C" int tm_debug_hist(tm_engine* e, uint64_t* out, int n) {

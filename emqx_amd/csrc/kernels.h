@@ -9,10 +9,15 @@ namespace tmx {
 
 constexpr uint32_t WREG = 16;        // topic levels kept in VGPRs / LDS path slots; longer
                                      // topics keep their path in global scratch
-constexpr size_t QWS_BYTES = 2048;   // queue heads: 8 ranges x 128 B, then 8 spill counters x 128 B
+constexpr size_t QWS_BYTES = 3072;   // queue heads: 8 ranges x 128 B, 8 spill counters x 128 B, 8 XCD clocks x 128 B
 constexpr size_t QWS_MAXC = 120;     // u64 slot of ws: the batch's largest match count
 constexpr size_t QWS_MAXL = 121;     // u64 slot of ws: most levels of a topic in a keyed batch
 constexpr size_t QWS_SPILL = 128;    // u64 slots 128 + 16 x: spill chunks taken by XCD x's waves
+// u64 slots 256 + 16 x (per-lane queue walks with XCD ranges; diagnostics,
+// tm_debug_walk_clocks): wall clock of XCD x's first wave start (stored
+// inverted: max of ~t), of its home range's first exhaustion (inverted), of
+// its last wave's end, and the chunks its waves stole from other ranges
+constexpr size_t QWS_CLOCK = 256;
 // Spill chunks (unkeyed walks): ids of a topic past its K-slot stage row go
 // to chunks of SPILL_CHUNK u32 -- slot 0 the next chunk of the topic, slots
 // 1.. ids in discovery order -- taken from the walking XCD's area (capacity

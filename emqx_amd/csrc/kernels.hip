@@ -927,6 +927,9 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
     uint64_t lev_sum = 0, match_sum = 0;
     uint32_t maxc = 0;                 // largest list of this lane's topics (stage-row sizing)
     uint32_t maxl = 0;                 // most levels of this lane's topics (key width check of keyed batches)
+    const uint64_t t_begin = wall_clock64();   // clocks of the walk's phases per XCD (QWS_CLOCK)
+    uint64_t t_home = 0;
+    uint32_t stolen = 0;
     for (;;) {
         const bool need = (my == NO_TOPIC) && !drained;
         const uint64_t m = __ballot(need);
@@ -950,8 +953,10 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
                         if (x < re - rb) {
                             g = rb + x;
                             gend = g + QCHUNK < re ? g + QCHUNK : re;
+                            stolen += qr != 0 ? 1u : 0u;
                             break;
                         }
+                        if (qr == 0) t_home = wall_clock64();
                         ++qr;
                     }
                     if (qr == QRANGES) exhausted = true;
@@ -1092,6 +1097,13 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
         maxl = y > maxl ? y : maxl;
     }
     if (lane == 0 && maxl) atomicMax(ws + QWS_MAXL, (unsigned long long)maxl);
+    if (XCDQ && lane == 0) {
+        unsigned long long* ck = ws + QWS_CLOCK + 16 * home;
+        atomicMax(ck, (unsigned long long)~t_begin);
+        if (t_home) atomicMax(ck + 1, (unsigned long long)~t_home);
+        atomicMax(ck + 2, (unsigned long long)wall_clock64());
+        if (stolen) atomicAdd(ck + 3, (unsigned long long)stolen);
+    }
     wave_stats_add<STATS>(stats, lev_sum, match_sum, st);
 }
 

@@ -116,6 +116,9 @@ def main():
     ap.add_argument("--layouts", default="cur")
     ap.add_argument("--opt", action="append", default=[])
     ap.add_argument("--bloom-hist", action="store_true", help="WIDE lookups by children count (no cache model)")
+    ap.add_argument("--sorted", action="store_true",
+                    help="topics in prefix order (lexicographic by word ids: the grouping of the walk's "
+                         "word-hash order, presort 5)")
     a = ap.parse_args()
     cfg = W.CONFIGS[a.config]
     nf = a.filters or cfg["filters"]
@@ -131,6 +134,13 @@ def main():
           file=sys.stderr, flush=True)
     tb, to = W.topics(a.config, n=a.topics, stream=0)
     lv, ids, dollar = words(eng, tb, to)
+    if a.sorted:
+        woff = np.zeros(len(lv) + 1, dtype=np.int64)
+        woff[1:] = np.cumsum(lv)
+        keys = [tuple(ids[woff[t]:woff[t + 1]][:8]) for t in range(len(lv))]
+        order = sorted(range(len(lv)), key=lambda t: keys[t])
+        ids = np.concatenate([ids[woff[t]:woff[t + 1]] for t in order]).astype(np.uint32)
+        lv, dollar = lv[order].copy(), dollar[order].copy()
     v = image(eng)
     lib = load_sim()
 
