@@ -237,7 +237,7 @@ constexpr int MAX_SLOTS = 4;
 // written, and only the next write to it waits for them (by then they are
 // long done).
 struct Image {
-    DevBuf d_nodes, d_edges, d_hedges, d_dict, d_arena, d_woff, d_inner, d_leaf;
+    DevBuf d_nodes, d_edges, d_hedges, d_dict, d_arena, d_woff, d_inner, d_leaf, d_bpool;
     // route image (routes.hip) and aggre tables (aggre.hip), same epoch as the
     // trie: a batch's filter ids and the route lists it expands them with
     // always come from one commit
@@ -257,7 +257,7 @@ struct Image {
     RouteView rv{};
     AggreView av{};
     void release() {
-        for (DevBuf* b : {&d_nodes, &d_edges, &d_hedges, &d_dict, &d_arena, &d_woff, &d_inner, &d_leaf, &d_rslots,
+        for (DevBuf* b : {&d_nodes, &d_edges, &d_hedges, &d_dict, &d_arena, &d_woff, &d_inner, &d_leaf, &d_bpool, &d_rslots,
                           &d_rarena, &d_rdest, &d_fr_meta, &d_rank_src, &d_dt, &d_rank_tg, &d_fshape, &d_wheat})
             b->release();
         for (hipEvent_t ev : uses) (void)hipEventDestroy(ev);
@@ -476,6 +476,20 @@ struct tm_engine {
     Dirty prev_node_dirty, prev_cold_dirty, prev_hot_dirty, prev_dict_dirty;
     EdgeTable& tab(uint32_t parent) { return parent < hot_limit ? hot : cold; }
     const EdgeTable& tab(uint32_t parent) const { return parent < hot_limit ? hot : cold; }
+    // per-node child blocks (option "blocks", image.h BlockSlot): with
+    // blocks_live, a WIDE node's literal children live in its own block of
+    // bpool (lw = first slot, lc = log2 slots << 27 | 27-bit Bloom) and the
+    // edge tables keep only '#' edges.  A block holds at most 1/block_div of
+    // its slots; a full one moves to a block twice the size at the pool's end
+    // (the old one is garbage until compaction or relayout, which lays the
+    // blocks out in node order)
+    std::vector<BlockSlot> bpool;
+    Dirty bpool_dirty, prev_bpool_dirty;
+    size_t bpool_garbage = 0;
+    int blocks_want = 1;              // option "blocks"
+    bool blocks_live = false;         // the representation the host mirror is in (switched by relayout)
+    uint32_t block_div = 4;           // option "block_load": blocks kept at load <= 1/block_div
+    size_t block_gc_min = 1u << 20;   // option "block_gc": garbage slots before a compaction is considered
 
     // ---- filter registry ----
     std::vector<uint8_t> filter_arena;
@@ -685,6 +699,8 @@ struct tm_engine {
             }
         }
         dict.assign(1024, DictSlot{0, WORD_NONE, 0, 0, 0, 0});
+        if (const char* v = std::getenv("TM_BLOCKS")) blocks_want = std::atoi(v) ? 1 : 0;
+        blocks_live = blocks_want != 0 && !SLOT_RECORD;
         nodes.reserve(1024);
         cold.slots.assign(1024, kEmptySlot);
         hot.slots.assign(1024, kEmptySlot);
@@ -814,6 +830,14 @@ struct tm_engine {
         const uint32_t p = aux[x].parent, w = aux[x].word;
         if (p == NODE_NONE || w == WORD_PLUS) return;
         if (w != WORD_HASH && !(nodes[p].plus & WIDE)) return;
+        if (w != WORD_HASH && blocks_live) {
+            const size_t s = blk_find(p, w);
+            if (s != SIZE_MAX && bpool[s].sum != child_sum(x)) {
+                bpool[s].sum = child_sum(x);
+                bpool_dirty.mark(s);
+            }
+            return;
+        }
         const size_t s = edge_find_slot(p, w);
         if (s == SIZE_MAX) return;
         EdgeSlot& e = tab(p).slots[s];
@@ -867,6 +891,118 @@ struct tm_engine {
     }
 
     // ------------------------------------------------------------------
+    // child blocks (blocks_live): a WIDE node's literal children
+    static BlockSlot empty_block_slot() { return BlockSlot{WORD_NONE, NODE_NONE, 0, 0}; }
+    static uint32_t blk_log2(const Node& x) { return x.lc >> BLOCK_LOG2_SHIFT; }
+    // the smallest block for c children: at least 2 x 4 slots' worth of room
+    uint32_t blk_log2_for(uint32_t c) const {
+        uint32_t k = 2;
+        while ((1ull << k) < (uint64_t)c * block_div) ++k;
+        return k;
+    }
+    // slots of a new block of 2^k slots at the pool's end (blocks of up to
+    // 8 slots aligned to their size: never across a 128 B line)
+    uint64_t blk_alloc(uint32_t k) {
+        const uint64_t sz = 1ull << k, al = sz < 8 ? sz : 8;
+        uint64_t base = (bpool.size() + al - 1) & ~(al - 1);
+        if (base + sz > 0xFFFFFFF0ull) throw RangeError("child block pool past 2^32 slots");
+        const size_t old = bpool.size();
+        bpool.resize(base + sz, empty_block_slot());
+        bpool_garbage += base - old;   // alignment padding
+        for (size_t i = old; i < bpool.size() && !bpool_dirty.all; ++i) bpool_dirty.mark(i);
+        return base;
+    }
+    size_t blk_find(uint32_t v, uint32_t w) const {
+        const Node& x = nodes[v];
+        const uint32_t k = blk_log2(x), m = (1u << k) - 1;
+        for (uint32_t p = block_home(w, k);; p = (p + 1) & m) {
+            const BlockSlot& e = bpool[(size_t)x.lw + p];
+            if (e.word == w) return (size_t)x.lw + p;
+            if (e.word == WORD_NONE) return SIZE_MAX;
+        }
+    }
+    // place (w, c) in v's block, which has room
+    void blk_put(uint32_t v, uint32_t w, uint32_t c) {
+        Node& x = nodes[v];
+        const uint32_t k = blk_log2(x), m = (1u << k) - 1;
+        uint32_t p = block_home(w, k);
+        while (bpool[(size_t)x.lw + p].word != WORD_NONE) p = (p + 1) & m;
+        bpool[(size_t)x.lw + p] = BlockSlot{w, c, child_sum(c), 0};
+        bpool_dirty.mark((size_t)x.lw + p);
+        x.lc |= block_bloom(w);
+    }
+    // v's block moved to one of 2^k slots (its children re-placed)
+    void blk_resize(uint32_t v, uint32_t k) {
+        std::vector<BlockSlot> keep;
+        const Node& x0 = nodes[v];
+        const uint64_t ob = x0.lw, on = 1ull << blk_log2(x0);
+        for (uint64_t i = 0; i < on; ++i)
+            if (bpool[ob + i].word != WORD_NONE) keep.push_back(bpool[ob + i]);
+        const uint64_t nb = blk_alloc(k);   // (may reallocate bpool: no references held across it)
+        for (uint64_t i = 0; i < on; ++i) {
+            bpool[ob + i] = empty_block_slot();
+            bpool_dirty.mark(ob + i);
+        }
+        bpool_garbage += on;
+        Node& x = nodes[v];
+        x.lw = (uint32_t)nb;
+        x.lc = k << BLOCK_LOG2_SHIFT;   // Bloom rebuilt from the children kept
+        for (const BlockSlot& e : keep) blk_put(v, e.word, e.child);
+    }
+    // backward-shift deletion within the block (no tombstones)
+    void blk_erase(uint32_t v, uint32_t w) {
+        const size_t at = blk_find(v, w);
+        if (at == SIZE_MAX) return;
+        const Node& x = nodes[v];
+        const uint64_t b = x.lw;
+        const uint32_t m = (1u << blk_log2(x)) - 1;
+        uint32_t i = (uint32_t)(at - b), j = i;
+        for (;;) {
+            j = (j + 1) & m;
+            if (bpool[b + j].word == WORD_NONE) break;
+            const uint32_t h = block_home(bpool[b + j].word, blk_log2(x));
+            const bool move = (i <= j) ? (h <= i || h > j) : (h <= i && h > j);
+            if (move) {
+                bpool[b + i] = bpool[b + j];
+                bpool_dirty.mark(b + i);
+                i = j;
+            }
+        }
+        bpool[b + i] = empty_block_slot();
+        bpool_dirty.mark(b + i);
+    }
+    void blk_free(uint32_t v) {
+        bpool_garbage += 1ull << blk_log2(nodes[v]);
+        const uint64_t b = nodes[v].lw, n = 1ull << blk_log2(nodes[v]);
+        for (uint64_t i = 0; i < n; ++i) {
+            bpool[b + i] = empty_block_slot();
+            bpool_dirty.mark(b + i);
+        }
+    }
+    // the pool rewritten without garbage, blocks in node order (positions
+    // inside a block unchanged); every slot re-uploaded
+    void blk_compact() {
+        std::vector<BlockSlot> np;
+        np.reserve(bpool.size() - bpool_garbage + 64);
+        for (size_t v = 0; v < nodes.size(); ++v) {
+            Node& x = nodes[v];
+            if (!(x.plus & WIDE) || (aux[v].parent == NODE_NONE && v != ROOT)) continue;
+            const uint64_t sz = 1ull << blk_log2(x), al = sz < 8 ? sz : 8;
+            const uint64_t base = (np.size() + al - 1) & ~(al - 1);
+            np.resize(base, empty_block_slot());
+            np.insert(np.end(), bpool.begin() + x.lw, bpool.begin() + x.lw + sz);
+            x.lw = (uint32_t)base;
+            node_dirty.mark(v);
+        }
+        bpool.swap(np);
+        bpool_garbage = 0;
+        bpool_dirty.all = true;
+    }
+    void maybe_compact_blocks() {
+        if (blocks_live && bpool_garbage > block_gc_min && bpool_garbage * 2 > bpool.size()) blk_compact();
+    }
+
+    // ------------------------------------------------------------------
     // nodes
     uint32_t new_node(uint32_t parent, uint32_t word) {
         uint32_t id;
@@ -904,6 +1040,10 @@ struct tm_engine {
         if (w == WORD_PLUS) return x.plus & NODE_MASK;
         if (w == WORD_HASH) return x.hash;
         if (!(x.plus & WIDE)) return x.lw == w ? x.lc : NODE_NONE;
+        if (blocks_live) {
+            const size_t s = blk_find(v, w);
+            return s == SIZE_MAX ? NODE_NONE : bpool[s].child;
+        }
         size_t s = edge_find_slot(v, w);
         return s == SIZE_MAX ? NODE_NONE : tab(v).slots[s].child;
     }
@@ -918,6 +1058,26 @@ struct tm_engine {
     }
     void lit_add(uint32_t v, uint32_t w, uint32_t c) {
         Node& x = nodes[v];
+        if (blocks_live) {   // (aux[v].lit_count: the children before this one)
+            if (!(x.plus & WIDE)) {
+                if (x.lw == WORD_NONE) {
+                    x.lw = w;
+                    x.lc = c;
+                    return;
+                }
+                const uint32_t w0 = x.lw, c0 = x.lc, k = blk_log2_for(2);
+                const uint64_t base = blk_alloc(k);
+                Node& y = nodes[v];
+                y.plus |= WIDE;
+                y.lw = (uint32_t)base;
+                y.lc = k << BLOCK_LOG2_SHIFT;
+                blk_put(v, w0, c0);
+            } else if ((uint64_t)(aux[v].lit_count + 1) * block_div > (1ull << blk_log2(x))) {
+                blk_resize(v, blk_log2_for(aux[v].lit_count + 1));
+            }
+            blk_put(v, w, c);
+            return;
+        }
         if (!(x.plus & WIDE)) {
             if (x.lw == WORD_NONE) {
                 x.lw = w;
@@ -938,12 +1098,14 @@ struct tm_engine {
     void lit_remove(uint32_t v, uint32_t w) {
         Node& x = nodes[v];
         if (x.plus & WIDE) {
-            edge_erase(v, w);
+            if (blocks_live) blk_erase(v, w);
+            else edge_erase(v, w);
         } else if (x.lw == w) {
             x.lw = WORD_NONE;
             x.lc = NODE_NONE;
         }
         if (--aux[v].lit_count == 0) {
+            if (blocks_live && (nodes[v].plus & WIDE)) blk_free(v);
             nodes[v].plus &= ~WIDE;
             nodes[v].lw = WORD_NONE;
             nodes[v].lc = NODE_NONE;
@@ -1608,6 +1770,26 @@ struct tm_engine {
     // discovery order) directly follows it, two 32 B records to a 64 B line;
     // topics with a common prefix walk a compact region.  Deleted ids are
     // dropped (compaction).  Filter ids are unchanged.
+    // f(parent, word, child) for every literal edge of a WIDE node (in its
+    // block, or in the edge tables)
+    template <class F>
+    void table_literals(F&& f) const {
+        if (blocks_live) {
+            for (size_t v = 0; v < nodes.size(); ++v) {
+                const Node& x = nodes[v];
+                if (!(x.plus & WIDE) || (aux[v].parent == NODE_NONE && v != ROOT)) continue;
+                const uint64_t n = 1ull << blk_log2(x);
+                for (uint64_t i = 0; i < n; ++i) {
+                    const BlockSlot& e = bpool[(size_t)x.lw + i];
+                    if (e.word != WORD_NONE) f((uint32_t)v, e.word, e.child);
+                }
+            }
+            return;
+        }
+        for (const EdgeTable* t : {&cold, &hot})
+            for (const EdgeSlot& e : t->slots)
+                if (e.parent != EDGE_EMPTY && e.word != WORD_HASH) f(e.parent, e.word, e.child);
+    }
     void relayout() {
         const size_t N = nodes.size();
         // literal children per node (inline or table edges), CSR
@@ -1616,9 +1798,7 @@ struct tm_engine {
             if (aux[v].parent == NODE_NONE && v != ROOT) continue;  // free slot
             if (!(nodes[v].plus & WIDE) && nodes[v].lw != WORD_NONE) start[v + 1]++;
         }
-        for (const EdgeTable* t : {&cold, &hot})
-            for (const EdgeSlot& e : t->slots)
-                if (e.parent != EDGE_EMPTY && e.word != WORD_HASH) start[e.parent + 1]++;
+        table_literals([&](uint32_t p, uint32_t, uint32_t) { start[p + 1]++; });
         for (size_t v = 0; v < N; ++v) start[v + 1] += start[v];
         std::vector<uint32_t> kids(start[N]);
         {
@@ -1627,9 +1807,7 @@ struct tm_engine {
                 if (aux[v].parent == NODE_NONE && v != ROOT) continue;
                 if (!(nodes[v].plus & WIDE) && nodes[v].lw != WORD_NONE) kids[fill[v]++] = nodes[v].lc;
             }
-            for (const EdgeTable* t : {&cold, &hot})
-                for (const EdgeSlot& e : t->slots)
-                    if (e.parent != EDGE_EMPTY && e.word != WORD_HASH) kids[fill[e.parent]++] = e.child;
+            table_literals([&](uint32_t p, uint32_t, uint32_t c) { kids[fill[p]++] = c; });
         }
         // preorder: v, literal subtrees, '+' subtree, '#' subtree; with
         // hot_levels = H, depths 0..H first, level by level (each node's
@@ -1725,16 +1903,60 @@ struct tm_engine {
         // edge tables with the new ids: parents below the new hot limit in `hot`
         std::vector<EdgeSlot> old;
         old.reserve(cold.used + hot.used);
+        table_literals([&](uint32_t p, uint32_t w, uint32_t c) {
+            EdgeSlot e{};
+            e.parent = p;
+            e.word = w;
+            e.child = c;
+            old.push_back(e);
+        });
         for (EdgeTable* t : {&cold, &hot}) {
             for (const EdgeSlot& e : t->slots)
-                if (e.parent != EDGE_EMPTY) old.push_back(e);
+                if (e.parent != EDGE_EMPTY && e.word == WORD_HASH) old.push_back(e);
             std::vector<EdgeSlot>().swap(t->slots);
             t->used = 0;
         }
-        for (const EdgeSlot& e : old)
-            if (e.word != WORD_HASH) bloom_add(nn[newid[e.parent]], e.word);
+        std::vector<BlockSlot>().swap(bpool);
+        bpool_garbage = 0;
+        blocks_live = blocks_want != 0 && !SLOT_RECORD;
+        if (!blocks_live)
+            for (const EdgeSlot& e : old)
+                if (e.word != WORD_HASH) bloom_add(nn[newid[e.parent]], e.word);
         nodes.swap(nn);
         aux.swap(na);   // before the edges are placed: slot_for reads the children's new summaries
+        if (blocks_live) {
+            // one block per WIDE node, in node order; the literal edges leave `old`
+            std::vector<EdgeSlot> lit;
+            size_t k = 0;
+            for (const EdgeSlot& e : old) {
+                if (e.word == WORD_HASH) old[k++] = e;
+                else lit.push_back(e);
+            }
+            old.resize(k);
+            std::sort(lit.begin(), lit.end(), [&](const EdgeSlot& a, const EdgeSlot& b) {
+                return newid[a.parent] != newid[b.parent] ? newid[a.parent] < newid[b.parent]
+                                                          : newid[a.child] < newid[b.child];
+            });
+            size_t total = 0;
+            for (size_t i = 0; i < lit.size();) {
+                size_t j = i;
+                while (j < lit.size() && lit[j].parent == lit[i].parent) ++j;
+                total += (size_t)1 << blk_log2_for((uint32_t)(j - i));
+                i = j;
+            }
+            bpool.reserve(total + total / 8 + 64);
+            for (size_t i = 0; i < lit.size();) {
+                size_t j = i;
+                while (j < lit.size() && lit[j].parent == lit[i].parent) ++j;
+                const uint32_t p = newid[lit[i].parent], kk = blk_log2_for((uint32_t)(j - i));
+                const uint64_t base = blk_alloc(kk);
+                nodes[p].lw = (uint32_t)base;
+                nodes[p].lc = kk << BLOCK_LOG2_SHIFT;
+                for (size_t q = i; q < j; ++q) blk_put(p, lit[q].word, newid[lit[q].child]);
+                i = j;
+            }
+            bpool_dirty.all = true;
+        }
         hot_limit = new_hot_limit;
         size_t nhot = 0;
         for (const EdgeSlot& e : old) nhot += newid[e.parent] < hot_limit;
@@ -1800,6 +2022,7 @@ struct tm_engine {
         im.edges = g.d_edges.as<const EdgeSlot>();
         im.edge_slot_mask = cold.slots.size() - 1;
         im.hot_edges = g.d_hedges.as<const EdgeSlot>();
+        im.blocks = blocks_live ? g.d_bpool.as<const BlockSlot>() : nullptr;
         im.hot_slot_mask = hot.slots.size() - 1;
         im.hot_limit = hot_limit;
         im.dict = g.d_dict.as<const DictSlot>();
@@ -1878,6 +2101,7 @@ struct tm_engine {
     // were launched on, consistent and untouched.
     void commit() {
         if (dev_dirty || devs.empty() || !devs[0]->img[devs[0]->cur].written) maybe_relayout();
+        maybe_compact_blocks();
         if (targets_dirty && !devs.empty()) rank_targets();
         if (devs.empty()) {
             ++epoch;
@@ -1907,6 +2131,7 @@ struct tm_engine {
             upload_table(d, g, g.d_nodes, nodes, node_dirty, prev_node_dirty);
             upload_table(d, g, g.d_edges, cold.slots, cold.dirty, prev_cold_dirty);
             upload_table(d, g, g.d_hedges, hot.slots, hot.dirty, prev_hot_dirty);
+            if (blocks_live) upload_table(d, g, g.d_bpool, bpool, bpool_dirty, prev_bpool_dirty);
             upload_table(d, g, g.d_dict, dict, dict_dirty, prev_dict_dirty);
             upload_table(d, g, g.d_rslots, rt_slots, t_slots.cur, t_slots.prev);
             upload_table(d, g, g.d_rarena, rt_arena, t_rarena.cur, t_rarena.prev);
@@ -1959,6 +2184,7 @@ struct tm_engine {
         for (const Rot& r : {Rot{&node_dirty, &prev_node_dirty, nodes.size()},
                              Rot{&cold.dirty, &prev_cold_dirty, cold.slots.size()},
                              Rot{&hot.dirty, &prev_hot_dirty, hot.slots.size()},
+                             Rot{&bpool_dirty, &prev_bpool_dirty, bpool.size()},
                              Rot{&dict_dirty, &prev_dict_dirty, dict.size()}}) {
             *r.prev = *r.cur;
             r.cur->clear();
@@ -2879,7 +3105,7 @@ int tm_engine_device(tm_engine* e) { return e ? e->device : -1; }
 uint64_t tm_image_bytes(tm_engine* e) {
     if (!e) return 0;
     return e->nodes.size() * sizeof(Node) + (e->cold.slots.size() + e->hot.slots.size()) * sizeof(EdgeSlot) +
-           e->dict.size() * sizeof(DictSlot) +
+           (e->blocks_live ? e->bpool.size() * sizeof(BlockSlot) : 0) + e->dict.size() * sizeof(DictSlot) +
            e->word_arena.size() + e->word_off.size() * 4;
 }
 
@@ -3535,6 +3761,45 @@ int tm_match_small_device(tm_engine* e, const uint8_t* d_bytes, const uint64_t* 
     }, [&] { e->finish_batch(n); });
 }
 
+// diagnostics (not part of include/topicmatch.h): host-side consistency of
+// the child blocks (option "blocks"): every WIDE node's block holds exactly
+// its literal children (each found from its home slot, with its word, its
+// current summary and a Bloom bit pattern the node carries), no other node
+// owns a slot of it.  TM_OK, or TM_EINVAL naming the first defect.
+extern "C" int tm_debug_check_blocks(tm_engine* e) {
+    if (!e) return TM_EINVAL;
+    return guarded(e, [&]() -> int {
+        if (!e->blocks_live) return TM_OK;
+        std::vector<uint8_t> owned(e->bpool.size(), 0);
+        for (size_t v = 0; v < e->nodes.size(); ++v) {
+            const Node& x = e->nodes[v];
+            if (!(x.plus & WIDE) || (e->aux[v].parent == NODE_NONE && v != ROOT)) continue;
+            const uint64_t n = 1ull << (x.lc >> BLOCK_LOG2_SHIFT);
+            if ((uint64_t)x.lw + n > e->bpool.size()) throw ArgError("node " + std::to_string(v) + ": block past the pool");
+            uint32_t cnt = 0;
+            for (uint64_t i = 0; i < n; ++i) {
+                if (owned[x.lw + i]) throw ArgError("slot " + std::to_string(x.lw + i) + " in two blocks");
+                owned[x.lw + i] = 1;
+                const BlockSlot& b = e->bpool[x.lw + i];
+                if (b.word == WORD_NONE) continue;
+                ++cnt;
+                if (b.child >= e->nodes.size() || e->aux[b.child].parent != v || e->aux[b.child].word != b.word)
+                    throw ArgError("node " + std::to_string(v) + ": slot " + std::to_string(i) + " names a stranger");
+                if (e->blk_find((uint32_t)v, b.word) != x.lw + i)
+                    throw ArgError("node " + std::to_string(v) + ": word " + std::to_string(b.word) + " unreachable");
+                if (b.sum != e->child_sum(b.child)) throw ArgError("node " + std::to_string(v) + ": stale summary");
+                const uint32_t bb = block_bloom(b.word);
+                if ((x.lc & bb) != bb) throw ArgError("node " + std::to_string(v) + ": Bloom misses a child");
+            }
+            if (cnt != e->aux[v].lit_count)
+                throw ArgError("node " + std::to_string(v) + ": " + std::to_string(cnt) + " block children, lit_count " +
+                               std::to_string(e->aux[v].lit_count));
+            if ((uint64_t)cnt * e->block_div > n) throw ArgError("node " + std::to_string(v) + ": block over its load");
+        }
+        return TM_OK;
+    });
+}
+
 // diagnostics (not part of include/topicmatch.h): the walk order of the
 // last device batch (option "presort" resolved by batch size: 5 the
 // range-local word-hash order, 2 the tail order, 0 arrival order ...)
@@ -3602,6 +3867,10 @@ struct tm_debug_image_view {
     uint32_t hot_limit;
     uint32_t aux_stride;     // bytes per aux record
     const void* aux;         // per node: {parent u32, word u32, edge_count u32, lit_count u32, ...}
+    const void* blocks;      // BlockSlot[block_slots] (option "blocks"; WIDE nodes: lw = first slot, lc = log2 | Bloom)
+    uint64_t block_slots;
+    uint32_t blocks_live;
+    uint32_t pad;
 };
 extern "C" int tm_debug_image(tm_engine* e, tm_debug_image_view* out) {
     if (!e || !out) return TM_EINVAL;
@@ -3615,6 +3884,10 @@ extern "C" int tm_debug_image(tm_engine* e, tm_debug_image_view* out) {
         out->hot_limit = e->hot_limit;
         out->aux_stride = (uint32_t)sizeof(NodeAux);
         out->aux = e->aux.data();
+        out->blocks = e->bpool.data();
+        out->block_slots = e->bpool.size();
+        out->blocks_live = e->blocks_live ? 1u : 0u;
+        out->pad = 0;
         return TM_OK;
     });
 }
@@ -3727,6 +4000,33 @@ int tm_set_option(tm_engine* e, const char* name, int64_t value) {
         if (!std::strcmp(name, "layout")) {
             if (value < 0 || value > 2) return TM_EINVAL;
             e->layout_mode = (int)value;
+            return TM_OK;
+        }
+        if (!std::strcmp(name, "blocks")) {   // 1: WIDE nodes' children in per-node blocks, 0: the shared table
+            if (value < 0 || value > 1 || (value && SLOT_RECORD)) return TM_EINVAL;
+            e->blocks_want = (int)value;
+            if ((value != 0) != e->blocks_live) {
+                if (e->live_nodes <= 1 && e->bpool.empty() && e->cold.used == 0 && e->hot.used == 0) {
+                    e->blocks_live = value != 0;   // an empty trie: switch now
+                } else {
+                    e->force_relayout = true;      // the next commit converts
+                    e->dev_dirty = true;
+                }
+            }
+            return TM_OK;
+        }
+        if (!std::strcmp(name, "block_gc")) {
+            if (value < 0) return TM_EINVAL;
+            e->block_gc_min = (size_t)value;
+            return TM_OK;
+        }
+        if (!std::strcmp(name, "block_load")) {   // blocks kept at load <= 1/value (the next relayout resizes)
+            if (value < 2 || value > 16) return TM_EINVAL;
+            if ((uint32_t)value != e->block_div) {
+                e->block_div = (uint32_t)value;
+                e->force_relayout = true;
+                e->dev_dirty = true;
+            }
             return TM_OK;
         }
         if (!std::strcmp(name, "relayout")) {   // 1: relayout at the next commit (layout A/Bs)

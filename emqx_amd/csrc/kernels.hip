@@ -402,6 +402,18 @@ __device__ __forceinline__ Hit lit_child(const ImageView& im, uint32_t v, uint32
     const Hit none{NODE_NONE, 0, 0, 0, 0, 0, false};
     if (w < WORD_MAX) {
         if (!(plus & WIDE)) return Hit{lw == w ? lc : NODE_NONE, SUM_ALL, 0, 0, 0, 0, false};
+        if (im.blocks) {   // option "blocks": the node's own block (lw = first slot, lc = log2 size | Bloom)
+            const uint32_t bb = block_bloom(w);
+            if ((lc & bb) != bb) return none;
+            const uint32_t k = lc >> BLOCK_LOG2_SHIFT, m = (1u << k) - 1u;
+            const BlockSlot* blk = im.blocks + lw;
+            for (uint32_t p = block_home(w, k);; p = (p + 1) & m) {
+                const uint4 e = reinterpret_cast<const uint4*>(blk + p)[0];
+                if (STATS) ++loads;
+                if (e.x == w) return Hit{e.y, e.z, 0, 0, 0, 0, false};   // e.z: S(child)
+                if (e.x == WORD_NONE) return none;
+            }
+        }
         const uint64_t b = word_bloom(w);
         const uint64_t mask = ((uint64_t)lc << 32) | lw;
         return (mask & b) == b ? probe_edge<STATS>(im, v, w, loads) : none;

@@ -32,7 +32,9 @@ MODES = {"cur": 0, "slotrec": 1, "pair": 2, "spec": 4, "blocks": 8}
 class View(ctypes.Structure):
     _fields_ = [("nodes", ctypes.c_void_p), ("n_nodes", ctypes.c_uint64), ("cold", ctypes.c_void_p),
                 ("cold_slots", ctypes.c_uint64), ("hot", ctypes.c_void_p), ("hot_slots", ctypes.c_uint64),
-                ("hot_limit", ctypes.c_uint32), ("aux_stride", ctypes.c_uint32), ("aux", ctypes.c_void_p)]
+                ("hot_limit", ctypes.c_uint32), ("aux_stride", ctypes.c_uint32), ("aux", ctypes.c_void_p),
+                ("blocks", ctypes.c_void_p), ("block_slots", ctypes.c_uint64), ("blocks_live", ctypes.c_uint32),
+                ("pad", ctypes.c_uint32)]
 
 
 class SimOut(ctypes.Structure):
@@ -116,6 +118,9 @@ def main():
     ap.add_argument("--layouts", default="cur")
     ap.add_argument("--opt", action="append", default=[])
     ap.add_argument("--bloom-hist", action="store_true", help="WIDE lookups by children count (no cache model)")
+    ap.add_argument("--slice", type=int, default=-1,
+                    help="with --sorted: 8 x --topics topics sorted as ONE batch (the global word-hash order), and "
+                         "the walk of XCD range SLICE of them (the global sort hands each XCD a key-space slice)")
     ap.add_argument("--sorted", action="store_true",
                     help="topics in prefix order (lexicographic by word ids: the grouping of the walk's "
                          "word-hash order, presort 5)")
@@ -132,13 +137,16 @@ def main():
     eng.commit()
     print("# built %d filters, %d nodes in %.1fs" % (eng.filter_count, eng.node_count, time.time() - t0),
           file=sys.stderr, flush=True)
-    tb, to = W.topics(a.config, n=a.topics, stream=0)
+    tb, to = W.topics(a.config, n=a.topics * (8 if a.slice >= 0 else 1), stream=0)
     lv, ids, dollar = words(eng, tb, to)
     if a.sorted:
         woff = np.zeros(len(lv) + 1, dtype=np.int64)
         woff[1:] = np.cumsum(lv)
         keys = [tuple(ids[woff[t]:woff[t + 1]][:8]) for t in range(len(lv))]
         order = sorted(range(len(lv)), key=lambda t: keys[t])
+        if a.slice >= 0:
+            n8 = len(order)
+            order = order[n8 * a.slice // 8: n8 * (a.slice + 1) // 8]
         ids = np.concatenate([ids[woff[t]:woff[t + 1]] for t in order]).astype(np.uint32)
         lv, dollar = lv[order].copy(), dollar[order].copy()
     v = image(eng)

@@ -41,6 +41,10 @@ struct View {
     uint32_t hot_limit;
     uint32_t aux_stride;
     const uint8_t* aux;
+    const BlockSlot* blocks;   // the engine's own child blocks (blocks_live)
+    uint64_t block_slots;
+    uint32_t blocks_live;
+    uint32_t pad;
 };
 
 enum Kind : uint8_t { K_INNER = 0, K_LEAF = 1, K_COLD = 2, K_HOT = 3, K_PAIR = 4, K_NKIND = 5 };
@@ -155,6 +159,23 @@ struct Walker {
     // probe_edge<false> (kernels.hip): linear probing from the home slot,
     // one dependent round per slot (from round rd0 on)
     Hit probe(uint32_t node, uint32_t w, std::vector<Acc>& acc, uint32_t& rd) const {
+        if (v.blocks_live && w != WORD_HASH) {   // the engine's blocks (lw = first slot, lc = log2 | Bloom)
+            const Node& x = v.nodes[node];
+            const uint32_t k = x.lc >> BLOCK_LOG2_SHIFT, m = (1u << k) - 1;
+            for (uint32_t p = block_home(w, k);; p = (p + 1) & m) {
+                const BlockSlot& e = v.blocks[(uint64_t)x.lw + p];
+                acc.push_back(Acc{x.lw + p, K_COLD, (uint8_t)std::min<uint32_t>(rd, 255)});
+                ++rd;
+                if (e.word == w) {
+                    ++probes_ok;
+                    return Hit{e.child, e.sum, false};
+                }
+                if (e.word == WORD_NONE) {
+                    ++probes_fail;
+                    return Hit{NODE_NONE, 0, false};
+                }
+            }
+        }
         if (mode & M_BLOCKS) {
             const uint64_t b = blk->base[node];
             if (b == ~0ull) {
@@ -217,9 +238,14 @@ struct Walker {
                 if (h.child != NODE_NONE) ++wide_hist[32 + bk];
                 return h;
             }
-            const uint64_t b = word_bloom(w);
-            const uint64_t mask = ((uint64_t)lc << 32) | lw;
-            if ((mask & b) != b) return Hit{NODE_NONE, 0, false};
+            if (v.blocks_live) {
+                const uint32_t bb = block_bloom(w);
+                if ((lc & bb) != bb) return Hit{NODE_NONE, 0, false};
+            } else {
+                const uint64_t b = word_bloom(w);
+                const uint64_t mask = ((uint64_t)lc << 32) | lw;
+                if ((mask & b) != b) return Hit{NODE_NONE, 0, false};
+            }
             ++wide_hist[16 + bk];
             const Hit h = probe(node, w, acc, rd);
             if (h.child != NODE_NONE) ++wide_hist[32 + bk];
