@@ -667,6 +667,12 @@ int  tm_rewrite_match_batch_device(tm_rewrite* r, const uint8_t* d_topics, const
  *              a 16 GiB stage footprint (default), 0 = fixed K
  *   "split"    1 = walk reads separate inner / leaf half arrays (default),
  *              0 = interleaved 32 B records
+ *   "blocks"   1 = a WIDE node's literal children in a block of its own
+ *              (per-node open addressing, blocks in node order), 0 = the
+ *              shared edge table (default; converted at the next commit)
+ *   "block_load" blocks kept at load <= 1/value (2..16, default 4)
+ *   "block_gc" garbage block slots before a compaction (default 2^20)
+ *   "relayout" 1 = relayout the image at the next commit
  *   "hot_levels" depths laid out level by level first at relayout (0..16,
  *              default 4; 0 = DFS preorder throughout); forces a relayout
  *   "presort"  1 = walk each batch in the order of a key of its first words

@@ -101,6 +101,7 @@ def test_blocks_grow_and_compact():
     """a node with thousands of children: its block doubles again and again
     (each move leaves garbage), then mass deletes; commits compact the pool"""
     eng = Engine(device=-1)
+    eng.set_option("blocks", 1)               # an empty trie: blocks from the first insert
     eng.set_option("layout", 0)               # no relayout: growth and compaction only
     eng.set_option("block_gc", 1024)
     o1 = O1()

@@ -260,9 +260,13 @@ VARIANTS = {"queue": {}, "queue_xcd": {}, "queue_xcd@nosplit@dfs": {"split": 0, 
             # presort 1 over the key's top 24 / 16 bits (3 / 2 radix passes: odd and even)
             "queue_xcd@presort@bits24": {"presort": 1, "sort_bits": 24},
             "queue_xcd@presort@bits16@norows": {"presort": 1, "sort_bits": 16, "chunk_rows": 0},
-            # the last positions of each XCD range walked a wave per topic on a second stream
             # range-keyed orders with a word-hash part (two radix passes)
-            "queue_xcd@order4": {"presort": 4}, "queue_xcd@order5@stagek8": {"presort": 5, "stage_k": 8}}
+            "queue_xcd@order4": {"presort": 4}, "queue_xcd@order5@stagek8": {"presort": 5, "stage_k": 8},
+            # per-node child blocks (option blocks): every walk over them, and a relayout into them
+            "queue_xcd@blocks": {"blocks": 1}, "queue_xcd@blocks@relayout@load2": {"blocks": 1, "layout": 2,
+                                                                                  "block_load": 2},
+            "queue_xcd@blocks@wave": {"blocks": 1, "wave_walk_max": 1 << 30},
+            "queue_xcd@blocks@order5@nosummaries": {"blocks": 1, "presort": 5, "summaries": 0}}
 
 
 @pytest.mark.parametrize("variant", list(VARIANTS))

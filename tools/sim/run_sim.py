@@ -26,7 +26,7 @@ from emqx_amd import Engine  # noqa: E402
 from emqx_amd import workload as W  # noqa: E402
 
 KINDS = ["inner", "leaf", "cold", "hot", "pair"]
-MODES = {"cur": 0, "slotrec": 1, "pair": 2, "spec": 4, "blocks": 8}
+MODES = {"cur": 0, "slotrec": 1, "pair": 2, "spec": 4, "blocks": 8, "bloom64": 16}
 
 
 class View(ctypes.Structure):
@@ -173,6 +173,8 @@ def main():
                 occ = int(part[3:])
             elif part.startswith("div"):   # per-node block load: size >= div x edges
                 mode |= int(part[3:]) << 8
+            elif part.startswith("bloomw"):   # the engine's blocks under a W-bit mask (0: none)
+                mode |= 32 | int(part[6:]) << 16
             else:
                 mode |= MODES[part]
         lanes = 32 * 4 * occ * 64

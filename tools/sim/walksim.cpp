@@ -90,6 +90,8 @@ enum Mode : int {
     M_SLOTREC = 1,   // TM_SLOT_RECORD: 32 B slots carry the child's record, the walk goes on in the same step
     M_PAIR = 2,      // a node's '+' child at id + 1, both halves loaded in one round; an immediate '+' step is free
     M_SPECPROBE = 4, // the parent's reference says "WIDE": the home slot is loaded with the node (no Bloom)
+    M_BLOOM64 = 16,  // the engine's blocks, Bloom test by a 64-bit mask of the block's words (word_bloom)
+    M_BLOOMW = 32,   // the engine's blocks, Bloom test by a (mode >> 16)-bit mask, k = 2 (0 = no Bloom)
     M_BLOCKS = 8,    // per-node child blocks: a WIDE node's literal / '#' edges in a contiguous open-addressing
                      // block of its own (blocks in node order = heat order), not one shared table
 };
@@ -238,7 +240,21 @@ struct Walker {
                 if (h.child != NODE_NONE) ++wide_hist[32 + bk];
                 return h;
             }
-            if (v.blocks_live) {
+            if (v.blocks_live && (mode & (M_BLOOM64 | M_BLOOMW))) {   // emulated masks of the block's words
+                const uint32_t k = lc >> BLOCK_LOG2_SHIFT;
+                const uint32_t bits = (mode & M_BLOOM64) ? 64u : (uint32_t)(mode >> 16);
+                auto bl = [&](uint32_t x) -> uint64_t {
+                    if (bits == 64) return word_bloom(x);
+                    const uint32_t h = x * 0x85EBCA77u;
+                    return (1ull << (((h & 0xFFFFu) * bits) >> 16)) | (1ull << (((h >> 16) * bits) >> 16));
+                };
+                if (bits) {
+                    uint64_t m = 0;
+                    for (uint64_t i = 0; i < (1ull << k); ++i)
+                        if (v.blocks[(uint64_t)lw + i].word != WORD_NONE) m |= bl(v.blocks[(uint64_t)lw + i].word);
+                    if ((m & bl(w)) != bl(w)) return Hit{NODE_NONE, 0, false};
+                }
+            } else if (v.blocks_live) {
                 const uint32_t bb = block_bloom(w);
                 if ((lc & bb) != bb) return Hit{NODE_NONE, 0, false};
             } else {
