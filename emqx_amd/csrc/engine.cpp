@@ -362,6 +362,7 @@ struct DevState {
     uint32_t keyed_k = 0;     // K of keyed walks (grown by stage_auto)
     uint32_t unkeyed_k = 0;   // K of unkeyed walks once their lists mostly spilled (grown by stage_auto)
     uint64_t spill_chunks = 0;   // spill area of unkeyed walks (adapted per batch)
+    uint32_t light_max = 31;     // presort 6: the light-tail cost-class bound (adapted per batch; 31 = none yet)
     // per-batch event records, accumulated until tm_last_kernel_times()
     std::vector<KTimes> ev_pool;          // recycled events
     std::vector<KTimes> ev_pending;       // recorded, not yet read
@@ -560,6 +561,8 @@ struct tm_engine {
                                       // 2 the tail order, 5 the word-hash key within each XCD range, 3 by
                                       // batch size: 5 from sort_min topics, else 2)
     uint32_t sort_min = 3000000;      // option "sort_min": presort 3's smallest batch in range-local word-hash order
+    uint32_t light_tail = 60;         // option "light_tail": presort 6 walks the lightest ~light_tail per mille of
+                                      // each XCD range last (the cost classes that cover it in the previous batch)
     std::atomic<int> last_order{-1};  // the walk order (presort mode) of the last device batch (tm_debug_last_order)
     int host_pipeline = 1;            // option "host_pipeline": host-buffer match/1 batches of >= 2M topics on
                                       // one replica go up, walk and come back in 1M-topic chunks, overlapped
@@ -2277,6 +2280,17 @@ struct tm_engine {
         for (Slot& w : d.slots) {
             if (!w.maxc_pending || hipEventQuery(w.maxc_ev) != hipSuccess) continue;
             w.maxc_pending = false;
+            uint64_t ht = 0;   // presort 6: the cost classes that hold the lightest light_tail per mille
+            for (int c = 0; c < 32; ++c) ht += w.h_maxc[QWS_CHIST + c];
+            if (ht) {
+                uint64_t run = 0;
+                uint32_t T = 0;
+                for (; T < 31; ++T) {
+                    run += w.h_maxc[QWS_CHIST + T];
+                    if (run * 1000 >= ht * light_tail) break;
+                }
+                d.light_max = T;
+            }
             mc = std::max<uint64_t>(mc, w.h_maxc[QWS_MAXC]);
             uint64_t t = 0;
             for (uint32_t x = 0; x < 8; ++x) {
@@ -2377,6 +2391,7 @@ struct tm_engine {
         qb.perm = presort && !shaped && !(qb.wave_walk && presort >= 2) ? w.perm.as<uint32_t>() : nullptr;
         qb.presort_mode = presort >= 2 ? (uint32_t)presort : 1u;
         qb.sort_passes = sort_bits / 8;
+        qb.light_max = light_tail ? d.light_max : 31u;
         if (presort) {
             qb.sort_keys = w.skeys.as<uint32_t>();
             qb.sort_vals = w.svals.as<uint32_t>();
@@ -4016,6 +4031,11 @@ int tm_set_option(tm_engine* e, const char* name, int64_t value) {
             }
             return TM_OK;
         }
+        if (!std::strcmp(name, "light_tail")) {   // per mille of each range walked last by presort 6
+            if (value < 0 || value > 500) return TM_EINVAL;
+            e->light_tail = (uint32_t)value;
+            return TM_OK;
+        }
         if (!std::strcmp(name, "block_gc")) {
             if (value < 0) return TM_EINVAL;
             e->block_gc_min = (size_t)value;
@@ -4037,7 +4057,7 @@ int tm_set_option(tm_engine* e, const char* name, int64_t value) {
             return TM_OK;
         }
         if (!std::strcmp(name, "presort")) {   // 0 arrival order, 1 word-hash key, 2 the tail order, 3 auto
-            if (value < 0 || value > 5) return TM_EINVAL;
+            if (value < 0 || value > 6) return TM_EINVAL;
             e->presort = (int)value;
             return TM_OK;
         }

@@ -9,7 +9,8 @@ namespace tmx {
 
 constexpr uint32_t WREG = 16;        // topic levels kept in VGPRs / LDS path slots; longer
                                      // topics keep their path in global scratch
-constexpr size_t QWS_BYTES = 3072;   // queue heads: 8 ranges x 128 B, 8 spill counters x 128 B, 8 XCD clocks x 128 B
+constexpr size_t QWS_BYTES = 3328;   // queue heads: 8 ranges x 128 B, 8 spill counters x 128 B, 8 XCD clocks x 128 B,
+                                     // the batch's cost histogram
 constexpr size_t QWS_MAXC = 120;     // u64 slot of ws: the batch's largest match count
 constexpr size_t QWS_MAXL = 121;     // u64 slot of ws: most levels of a topic in a keyed batch
 constexpr size_t QWS_SPILL = 128;    // u64 slots 128 + 16 x: spill chunks taken by XCD x's waves
@@ -18,6 +19,9 @@ constexpr size_t QWS_SPILL = 128;    // u64 slots 128 + 16 x: spill chunks taken
 // inverted: max of ~t), of its home range's first exhaustion (inverted), of
 // its last wave's end, and the chunks its waves stole from other ranges
 constexpr size_t QWS_CLOCK = 256;
+// u64 slots 384 + c (presort 6): topics of predicted cost class c (kernels.hip
+// tail_key), for the next batch's light-tail threshold
+constexpr size_t QWS_CHIST = 384;
 // Spill chunks (unkeyed walks): ids of a topic past its K-slot stage row go
 // to chunks of SPILL_CHUNK u32 -- slot 0 the next chunk of the topic, slots
 // 1.. ids in discovery order -- taken from the walking XCD's area (capacity
@@ -47,6 +51,7 @@ struct QueueBufs {
     uint32_t presort_mode = 1;   // 1: key of the first eight words; 2: the tail order (kernels.hip
                                  // tail_key: heavy topics first in each XCD range, one radix pass)
     uint32_t sort_passes = 4;    // mode 1: radix passes over the key's top 8 * sort_passes bits (1..4)
+    uint32_t light_max = 31;     // mode 6: cost classes <= light_max are walked last in their XCD range
     // the radix passes of the batch's presort: the tokenizer writes the keys
     // and values where the first pass reads them, so the last ends in perm
     uint32_t presort_passes() const { return presort_mode == 2 ? 1u : presort_mode == 4 ? 2u : sort_passes; }

@@ -265,7 +265,7 @@ __device__ __forceinline__ uint32_t tail_key(const ImageView& im, const uint32_t
 }
 
 template <class B>
-__device__ __forceinline__ void tokenize_one(const ImageView& im, const B& bytes,
+__device__ __forceinline__ uint32_t tokenize_one(const ImageView& im, const B& bytes,
                                              const uint64_t* __restrict__ off, uint32_t t, uint32_t n,
                                              uint32_t* __restrict__ twords, uint32_t* __restrict__ words,
                                              uint32_t* __restrict__ meta, uint32_t* __restrict__ skeys,
@@ -289,27 +289,41 @@ __device__ __forceinline__ void tokenize_one(const ImageView& im, const B& bytes
         // 2: the tail order (8 bits); 4: the tail order, then the word-hash
         // key's top 8 bits within a heat class (16); 5: the XCD range, then
         // the word-hash key's top 13 bits (16); 1: the word-hash key (32)
-        // (key_mode: the order | its key bits << 8; 5 takes the range's 3
-        // bits over the word-hash key's top bits - 3)
-        const uint32_t mode = key_mode & 255u, bits = key_mode >> 8;
+        // (key_mode: the order | its key bits << 8 | the light-tail class
+        // bound << 16; 5 takes the range's 3 bits over the word-hash key's
+        // top bits - 3; 6 the range's 3 bits, a light-tail bit, then the
+        // word-hash key's top bits - 4)
+        const uint32_t mode = key_mode & 255u, bits = (key_mode >> 8) & 255u;
+        if (mode == 6) {
+            const uint32_t tk = tail_key(im, tw, lev, t, n), c = 31u - (tk & 31u);
+            const uint32_t light = c <= ((key_mode >> 16) & 255u) ? 1u : 0u;
+            skeys[t] = (tk >> 5) << (bits - 3) | light << (bits - 4) | presort_key(tw, lev) >> (36 - bits);
+            svals[t] = t;
+            return c;
+        }
         skeys[t] = mode == 2   ? tail_key(im, tw, lev, t, n)
                    : mode == 4 ? tail_key(im, tw, lev, t, n) << 8 | presort_key(tw, lev) >> 24
                    : mode == 5 ? (tail_key(im, tw, lev, t, n) >> 5) << (bits - 3) | presort_key(tw, lev) >> (35 - bits)
                                : presort_key(tw, lev);
         svals[t] = t;
     }
+    return 32u;   // (presort 6: the topic's cost class)
 }
 
 __global__ void __launch_bounds__(BLOCK)
 tm_tokenize(ImageView im, const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint32_t n,
             uint32_t* __restrict__ twords, uint32_t* __restrict__ words, uint32_t* __restrict__ meta,
-            uint32_t* __restrict__ skeys, uint32_t* __restrict__ svals, uint32_t key_mode) {
+            uint32_t* __restrict__ skeys, uint32_t* __restrict__ svals, uint32_t key_mode,
+            unsigned long long* __restrict__ ws_hist) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (TM_TOK_LEAN) {
         if (t < n) tokenize_one(im, GlobalBytes{bytes}, off, t, n, twords, words, meta, skeys, svals, key_mode);
         return;
     }
     __shared__ uint64_t win[BLOCK / 64][TOK_WIN_WORDS];
+    __shared__ uint32_t chist[32];   // presort 6: the block's cost-class histogram (QWS_CHIST)
+    const bool hist = skeys && (key_mode & 255u) == 6u;
+    if (hist && threadIdx.x < 32) chist[threadIdx.x] = 0;
     const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     // the wave's 64 topics are contiguous bytes: stage them in LDS with
     // coalesced loads (per-lane 8 B loads of 64 different topics touch 64
@@ -327,11 +341,18 @@ tm_tokenize(ImageView im, const uint8_t* __restrict__ bytes, const uint64_t* __r
                 win[wv][k] = *reinterpret_cast<const uint64_t*>(bytes + wbase + 8 * k);
     }
     __syncthreads();
+    uint32_t c = 32u;
     if (t < n) {
         if (lds)
-            tokenize_one(im, LdsBytes{win[wv], wbase}, off, t, n, twords, words, meta, skeys, svals, key_mode);
+            c = tokenize_one(im, LdsBytes{win[wv], wbase}, off, t, n, twords, words, meta, skeys, svals, key_mode);
         else
-            tokenize_one(im, GlobalBytes{bytes}, off, t, n, twords, words, meta, skeys, svals, key_mode);
+            c = tokenize_one(im, GlobalBytes{bytes}, off, t, n, twords, words, meta, skeys, svals, key_mode);
+    }
+    if (hist) {   // (uniform per block: the key mode is one for the launch)
+        if (c < 32u) atomicAdd(&chist[c], 1u);
+        __syncthreads();
+        if (threadIdx.x < 32 && chist[threadIdx.x])
+            atomicAdd(ws_hist + threadIdx.x, (unsigned long long)chist[threadIdx.x]);
     }
 }
 
@@ -1880,7 +1901,8 @@ hipError_t launch_queue(bool stats_mode, bool xcdq, const ImageView& im, const u
     hipLaunchKernelGGL(tm_tokenize, g, blk, 0, st, im, bytes, off, n, qb.twords, qb.words, qb.meta,
                        qb.perm ? qb.sort_keys + (odd ? n : 0u) : nullptr,
                        qb.perm ? (odd ? qb.sort_vals : qb.perm) : nullptr,
-                       qb.presort_mode | (8u * qb.presort_passes()) << 8);
+                       qb.presort_mode | (8u * qb.presort_passes()) << 8 | (qb.light_max & 255u) << 16,
+                       qb.ws + QWS_CHIST);
     if (qb.perm) {   // option "presort": perm (and the rows in walk order unless chunk rows read them by perm)
         err = launch_presort(qb.twords, qb.meta, n, qb, st, by_pos);
         if (err != hipSuccess) return err;

@@ -262,6 +262,9 @@ VARIANTS = {"queue": {}, "queue_xcd": {}, "queue_xcd@nosplit@dfs": {"split": 0, 
             "queue_xcd@presort@bits16@norows": {"presort": 1, "sort_bits": 16, "chunk_rows": 0},
             # range-keyed orders with a word-hash part (two radix passes)
             "queue_xcd@order4": {"presort": 4}, "queue_xcd@order5@stagek8": {"presort": 5, "stage_k": 8},
+            # the range-local word-hash order with the lightest topics of each range last (three radix passes)
+            "queue_xcd@order6": {"presort": 6}, "queue_xcd@order6@bits16@tail300": {"presort": 6, "sort_bits": 16,
+                                                                                    "light_tail": 300},
             # per-node child blocks (option blocks): every walk over them, and a relayout into them
             "queue_xcd@blocks": {"blocks": 1}, "queue_xcd@blocks@relayout@load2": {"blocks": 1, "layout": 2,
                                                                                   "block_load": 2},
