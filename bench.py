@@ -666,8 +666,8 @@ class Region:
         out = (ctypes.c_double * 32)()
         f = self.eng.lib.tm_debug_walk_clocks
         f.restype = ctypes.c_int
-        if f(self.eng.h, out) != 0:
-            return None
+        if f(self.eng.h, out) != 0 or all(out[4 * x] < 0 for x in range(8)):
+            return None   # (a build without the walk's clocks: TM_WALK_CLOCKS)
         return [{"start": round(out[4 * x], 4), "home_done": round(out[4 * x + 1], 4), "end": round(out[4 * x + 2], 4),
                  "stolen_chunks": int(out[4 * x + 3])} for x in range(8)]
 

@@ -703,7 +703,7 @@ struct tm_engine {
             }
         }
         dict.assign(1024, DictSlot{0, WORD_NONE, 0, 0, 0, 0});
-        if (const char* v = std::getenv("TM_BLOCKS")) blocks_want = std::atoi(v) ? 1 : 0;
+        if (const char* v = std::getenv("TM_BLOCKS")) blocks_want = std::atoi(v) && kernels_have_blocks() ? 1 : 0;
         blocks_live = blocks_want != 0 && !SLOT_RECORD;
         nodes.reserve(1024);
         cold.slots.assign(1024, kEmptySlot);
@@ -4020,6 +4020,8 @@ int tm_set_option(tm_engine* e, const char* name, int64_t value) {
         }
         if (!std::strcmp(name, "blocks")) {   // 1: WIDE nodes' children in per-node blocks, 0: the shared table
             if (value < 0 || value > 1 || (value && SLOT_RECORD)) return TM_EINVAL;
+            // a device engine needs walks that read blocks (a TM_BLOCKS_PATH build)
+            if (value && !e->devs.empty() && !kernels_have_blocks()) return TM_EINVAL;
             e->blocks_want = (int)value;
             if ((value != 0) != e->blocks_live) {
                 if (e->live_nodes <= 1 && e->bpool.empty() && e->cold.used == 0 && e->hot.used == 0) {

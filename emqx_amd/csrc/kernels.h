@@ -88,6 +88,8 @@ hipError_t launch_presort(const uint32_t* twords, const uint32_t* meta, uint32_t
 // chunk's rows through perm and writes stage rows, counts and spill heads by
 // topic, so the ordinary copy-out (and spill) applies.
 bool queue_rows_by_position(const QueueBufs& qb, bool stats_mode);
+// the walk kernels of this build read per-node child blocks (TM_BLOCKS_PATH)
+bool kernels_have_blocks();
 
 // tokenize -> NFA walk -> scan -> copy-out, all on st.  marks: 8 events,
 // [2i] before / [2i+1] after stage i, or null.  out_cap == 0: counts and

@@ -386,6 +386,14 @@ __device__ __forceinline__ void nt_store16(void* p, uint4 v) {
     u32x4_nt x = {v.x, v.y, v.z, v.w};
     __builtin_nontemporal_store(x, reinterpret_cast<u32x4_nt*>(p));
 }
+#ifndef TM_WALK_CLOCKS
+#define TM_WALK_CLOCKS 0   // diagnostic builds: the queue walk's per-XCD phase clocks (QWS_CLOCK,
+                           // tm_debug_walk_clocks); 4 VGPRs of the walk, so off in the product build
+#endif
+#ifndef TM_BLOCKS_PATH
+#define TM_BLOCKS_PATH 0   // A/B builds: the walks' child-block lookups (option "blocks": measured slower,
+                           // DESIGN 5.2c; 3 VGPRs of the walk), 0: the shared edge table only
+#endif
 // literal (or '#') edge (v, w) in the edge table: linear probing, one 16 B
 // key half per slot (load factor <= 1/4: ~1.2 loads per hit); on a hit the
 // slot's second half completes the child's record
@@ -423,7 +431,7 @@ __device__ __forceinline__ Hit lit_child(const ImageView& im, uint32_t v, uint32
     const Hit none{NODE_NONE, 0, 0, 0, 0, 0, false};
     if (w < WORD_MAX) {
         if (!(plus & WIDE)) return Hit{lw == w ? lc : NODE_NONE, SUM_ALL, 0, 0, 0, 0, false};
-        if (im.blocks) {   // option "blocks": the node's own block (lw = first slot, lc = log2 size | Bloom)
+        if (TM_BLOCKS_PATH && im.blocks) {   // option "blocks": the node's own block (lw = first slot, lc = log2 size | Bloom)
             const uint32_t bb = block_bloom(w);
             if ((lc & bb) != bb) return none;
             const uint32_t k = lc >> BLOCK_LOG2_SHIFT, m = (1u << k) - 1u;
@@ -960,9 +968,9 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
     uint64_t lev_sum = 0, match_sum = 0;
     uint32_t maxc = 0;                 // largest list of this lane's topics (stage-row sizing)
     uint32_t maxl = 0;                 // most levels of this lane's topics (key width check of keyed batches)
-    const uint64_t t_begin = wall_clock64();   // clocks of the walk's phases per XCD (QWS_CLOCK)
-    uint64_t t_home = 0;
-    uint32_t stolen = 0;
+    // clocks of the walk's phases per XCD (QWS_CLOCK), written as they happen
+    // (no registers held across the loop)
+    if (TM_WALK_CLOCKS && XCDQ && lane == 0) atomicMax(ws + QWS_CLOCK + 16 * home, (unsigned long long)~wall_clock64());
     for (;;) {
         const bool need = (my == NO_TOPIC) && !drained;
         const uint64_t m = __ballot(need);
@@ -986,10 +994,11 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
                         if (x < re - rb) {
                             g = rb + x;
                             gend = g + QCHUNK < re ? g + QCHUNK : re;
-                            stolen += qr != 0 ? 1u : 0u;
+                            if (TM_WALK_CLOCKS && qr != 0 && lane == leader) atomicAdd(ws + QWS_CLOCK + 16 * home + 3, 1ull);
                             break;
                         }
-                        if (qr == 0) t_home = wall_clock64();
+                        if (TM_WALK_CLOCKS && qr == 0 && lane == leader)
+                            atomicMax(ws + QWS_CLOCK + 16 * home + 1, (unsigned long long)~wall_clock64());
                         ++qr;
                     }
                     if (qr == QRANGES) exhausted = true;
@@ -1130,13 +1139,7 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
         maxl = y > maxl ? y : maxl;
     }
     if (lane == 0 && maxl) atomicMax(ws + QWS_MAXL, (unsigned long long)maxl);
-    if (XCDQ && lane == 0) {
-        unsigned long long* ck = ws + QWS_CLOCK + 16 * home;
-        atomicMax(ck, (unsigned long long)~t_begin);
-        if (t_home) atomicMax(ck + 1, (unsigned long long)~t_home);
-        atomicMax(ck + 2, (unsigned long long)wall_clock64());
-        if (stolen) atomicAdd(ck + 3, (unsigned long long)stolen);
-    }
+    if (TM_WALK_CLOCKS && XCDQ && lane == 0) atomicMax(ws + QWS_CLOCK + 16 * home + 2, (unsigned long long)wall_clock64());
     wave_stats_add<STATS>(stats, lev_sum, match_sum, st);
 }
 
@@ -1435,6 +1438,9 @@ tm_match_small(ImageView im, const uint8_t* __restrict__ bytes, const uint64_t* 
 #define TM_COPY_WAVE_MIN 16   // A/B at C3: copy-out 0.322 (64) vs 0.283-0.293 ms (16, 0)
 #endif
 constexpr uint32_t COPY_WAVE_MIN = TM_COPY_WAVE_MIN;
+#ifndef TM_COPY_NT
+#define TM_COPY_NT 0   // A/B builds: the unkeyed copy-out's stage reads and output stores non-temporal
+#endif
 #ifndef TM_COPY_U
 #define TM_COPY_U 4   // unkeyed copy-out: topics per wave with their row loads in flight together (1: one at a time)
 #endif
@@ -1466,7 +1472,8 @@ tm_copy_out(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const ui
     const uint64_t base = out_off[t0];
     auto ood = [&](uint32_t lt) { return SHAPED && (meta[t0 + lt] & MOOD) != 0; };
     auto put = [&](uint64_t p, uint32_t id) {
-        out[p] = id;
+        if (TM_COPY_NT) __builtin_nontemporal_store(id, out + p);
+        else out[p] = id;
         if (SHAPED) kout[p] = im.fshape[id];
     };
     if (TM_COPY_FLAT) {
@@ -1520,8 +1527,9 @@ tm_copy_out(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const ui
                     const uint32_t ct = lds_inc[lt] - prev;
                     const uint32_t j = (ct > K ? ct - K : 0u) + lane;
                     const uint64_t row = (uint64_t)(t0 + lt) * K + K - ct;
-                    if (j < ct) v0[u] = stage[row + j];
-                    if (j + 64 < ct) v1[u] = stage[row + j + 64];
+                    if (j < ct) v0[u] = TM_COPY_NT ? __builtin_nontemporal_load(stage + row + j) : stage[row + j];
+                    if (j + 64 < ct)
+                        v1[u] = TM_COPY_NT ? __builtin_nontemporal_load(stage + row + j + 64) : stage[row + j + 64];
                 }
             }
 #pragma unroll
@@ -1748,6 +1756,8 @@ tm_split_nodes(const uint4* __restrict__ nodes, uint64_t n, uint4* __restrict__ 
         leaf[v] = nodes[2 * v + 1];
     }
 }
+
+bool kernels_have_blocks() { return TM_BLOCKS_PATH != 0; }
 
 hipError_t launch_split_nodes(const void* nodes, uint64_t n, void* inner, void* leaf, hipStream_t st) {
     if (n == 0) return hipSuccess;

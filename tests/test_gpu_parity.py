@@ -265,11 +265,7 @@ VARIANTS = {"queue": {}, "queue_xcd": {}, "queue_xcd@nosplit@dfs": {"split": 0, 
             # the range-local word-hash order with the lightest topics of each range last (three radix passes)
             "queue_xcd@order6": {"presort": 6}, "queue_xcd@order6@bits16@tail300": {"presort": 6, "sort_bits": 16,
                                                                                     "light_tail": 300},
-            # per-node child blocks (option blocks): every walk over them, and a relayout into them
-            "queue_xcd@blocks": {"blocks": 1}, "queue_xcd@blocks@relayout@load2": {"blocks": 1, "layout": 2,
-                                                                                  "block_load": 2},
-            "queue_xcd@blocks@wave": {"blocks": 1, "wave_walk_max": 1 << 30},
-            "queue_xcd@blocks@order5@nosummaries": {"blocks": 1, "presort": 5, "summaries": 0}}
+}
 
 
 @pytest.mark.parametrize("variant", list(VARIANTS))
