@@ -30,6 +30,43 @@ namespace tmx {
 
 constexpr int BLOCK = 256;
 
+// Non-temporal loads and stores.  TM_NT_STREAM (A/B builds): the once-read
+// and once-written streams of the pipeline -- the tokenizer's topic bytes
+// and rows, the walk's chunk-row fill, the copy-out's stage reads -- marked
+// non-temporal, so they do not push the trie's lines out of the caches
+// between walks (the Infinity Cache keeps a line only while everything any
+// kernel touches between two of its uses fits in its 256 MiB)
+#ifndef TM_NT_STREAM
+#define TM_NT_STREAM 0
+#endif
+typedef uint32_t u32x4_nt __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 nt_load16(const void* p) {
+    const u32x4_nt x = __builtin_nontemporal_load(reinterpret_cast<const u32x4_nt*>(p));
+    return make_uint4(x.x, x.y, x.z, x.w);
+}
+__device__ __forceinline__ void nt_store16(void* p, uint4 v) {
+    u32x4_nt x = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(x, reinterpret_cast<u32x4_nt*>(p));
+}
+template <class T>
+__device__ __forceinline__ T stream_load(const T* p) {
+    if (TM_NT_STREAM) return __builtin_nontemporal_load(p);
+    return *p;
+}
+template <class T>
+__device__ __forceinline__ void stream_store(T* p, T v) {
+    if (TM_NT_STREAM) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+__device__ __forceinline__ uint4 stream_load16(const void* p) {
+    if (TM_NT_STREAM) return nt_load16(p);
+    return *reinterpret_cast<const uint4*>(p);
+}
+__device__ __forceinline__ void stream_store16(void* p, uint4 v) {
+    if (TM_NT_STREAM) nt_store16(p, v);
+    else *reinterpret_cast<uint4*>(p) = v;
+}
+
 // ---------------------------------------------------------------------------
 // byte access: aligned 8-byte words (an aligned word holding a valid byte
 // never crosses a page), little-endian extraction.  Topic bytes are read
@@ -282,9 +319,9 @@ __device__ __forceinline__ uint32_t tokenize_one(const ImageView& im, const B& b
     uint4* row = reinterpret_cast<uint4*>(twords + (uint64_t)t * WREG);
 #pragma unroll
     for (uint32_t k = 0; k < WREG / 4; ++k)
-        if (4 * k < lev || k == 0) row[k] = make_uint4(tw[4 * k], tw[4 * k + 1], tw[4 * k + 2], tw[4 * k + 3]);
+        if (4 * k < lev || k == 0) stream_store16(row + k, make_uint4(tw[4 * k], tw[4 * k + 1], tw[4 * k + 2], tw[4 * k + 3]));
     const uint32_t dollar = (e > b && bytes.byte(b) == '$') ? 1u : 0u;
-    meta[t] = lev | (dollar << 31) | (lev > WREG ? MLONG : 0u) | (ood ? MOOD : 0u);
+    stream_store(meta + t, lev | (dollar << 31) | (lev > WREG ? MLONG : 0u) | (ood ? MOOD : 0u));
     if (skeys) {   // option "presort": the walk-order key (presort.hip)
         // 2: the tail order (8 bits); 4: the tail order, then the word-hash
         // key's top 8 bits within a heat class (16); 5: the XCD range, then
@@ -338,7 +375,7 @@ tm_tokenize(ImageView im, const uint8_t* __restrict__ bytes, const uint64_t* __r
         lds = nw <= TOK_WIN_WORDS;
         if (lds)
             for (uint64_t k = lane; k < nw; k += 64)
-                win[wv][k] = *reinterpret_cast<const uint64_t*>(bytes + wbase + 8 * k);
+                win[wv][k] = stream_load(reinterpret_cast<const uint64_t*>(bytes + wbase + 8 * k));
     }
     __syncthreads();
     uint32_t c = 32u;
@@ -377,15 +414,6 @@ struct Hit {
 #ifndef TM_NT_PROBE
 #define TM_NT_PROBE 0
 #endif
-typedef uint32_t u32x4_nt __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ uint4 nt_load16(const void* p) {
-    const u32x4_nt x = __builtin_nontemporal_load(reinterpret_cast<const u32x4_nt*>(p));
-    return make_uint4(x.x, x.y, x.z, x.w);
-}
-__device__ __forceinline__ void nt_store16(void* p, uint4 v) {
-    u32x4_nt x = {v.x, v.y, v.z, v.w};
-    __builtin_nontemporal_store(x, reinterpret_cast<u32x4_nt*>(p));
-}
 #ifndef TM_WALK_CLOCKS
 #define TM_WALK_CLOCKS 0   // diagnostic builds: the queue walk's per-XCD phase clocks (QWS_CLOCK,
                            // tm_debug_walk_clocks); 4 VGPRs of the walk, so off in the product build
@@ -1022,11 +1050,11 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
                 if (t < gend) {
                     // a presorted batch: queue position t walks topic perm[t], whose row
                     // is read here (the rows are not gathered into walk order)
-                    const uint32_t tt = perm ? perm[t] : t;
+                    const uint32_t tt = perm ? stream_load(perm + t) : t;
                     CR.topic[lane] = tt;
-                    CR.meta[lane] = meta[tt];
+                    CR.meta[lane] = stream_load(meta + tt);
                     const uint4* src = reinterpret_cast<const uint4*>(twords + (uint64_t)tt * WREG);
-                    const uint4 a0 = src[0], a1 = src[1];   // quad 1 may be stale past the topic's levels: unread
+                    const uint4 a0 = stream_load16(src), a1 = stream_load16(src + 1);   // quad 1 may be stale: unread
                     *reinterpret_cast<uint4*>(&CR.w[lane][0]) = a0;
                     *reinterpret_cast<uint4*>(&CR.w[lane][4]) = a1;
                 }
@@ -1527,9 +1555,10 @@ tm_copy_out(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const ui
                     const uint32_t ct = lds_inc[lt] - prev;
                     const uint32_t j = (ct > K ? ct - K : 0u) + lane;
                     const uint64_t row = (uint64_t)(t0 + lt) * K + K - ct;
-                    if (j < ct) v0[u] = TM_COPY_NT ? __builtin_nontemporal_load(stage + row + j) : stage[row + j];
+                    if (j < ct) v0[u] = TM_COPY_NT || TM_NT_STREAM ? __builtin_nontemporal_load(stage + row + j) : stage[row + j];
                     if (j + 64 < ct)
-                        v1[u] = TM_COPY_NT ? __builtin_nontemporal_load(stage + row + j + 64) : stage[row + j + 64];
+                        v1[u] = TM_COPY_NT || TM_NT_STREAM ? __builtin_nontemporal_load(stage + row + j + 64)
+                                                          : stage[row + j + 64];
                 }
             }
 #pragma unroll
