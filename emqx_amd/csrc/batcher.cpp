@@ -679,7 +679,7 @@ int tm_batcher_open(tm_engine* e, const tm_batcher_config* cfg, tm_batcher** out
     if (b->cfg.max_topics == 0) b->cfg.max_topics = 65536;
     if (b->cfg.max_bytes == 0) b->cfg.max_bytes = 64ull << 20;
     if (b->cfg.deadline_us == 0) b->cfg.deadline_us = 200;
-    if (b->cfg.eager_us == 0) b->cfg.eager_us = 60;
+    if (b->cfg.eager_us == 0) b->cfg.eager_us = 40;   // profiles/r05_f/latency.jsonl
     const uint32_t per = b->cfg.lanes_per_replica ? b->cfg.lanes_per_replica : 2u;
     const int R = tm_engine_replicas(e);
     b->host_only = R == 0;

@@ -551,7 +551,7 @@ typedef struct tm_batcher_config {
     uint32_t callback_threads;  /* threads that share a batch's callbacks with its lane
                                    (parts of >= 8192 topics; 0 = the lane alone) */
     uint32_t eager_us;        /* TM_BATCHER_EAGER: least age of the oldest pending topic for a seal at a
-                                 free lane (0 = 60; >= deadline_us: deadline sealing) */
+                                 free lane (0 = 40; >= deadline_us: deadline sealing) */
 } tm_batcher_config;
 typedef struct tm_batcher_stats {
     uint64_t batches, topics, results, max_batch;
