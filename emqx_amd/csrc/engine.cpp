@@ -2238,7 +2238,16 @@ struct tm_engine {
     // 730M vs 711M; the tail order (2: heaviest topics first in each range,
     // one radix pass) shortens the walk's fixed ~0.4 ms tail and wins below
     // ~3M: 1M 622-624M vs 597-603M (5)
-    int presort_of(uint32_t n) const { return presort == 3 ? (n >= sort_min ? 5 : 2) : presort; }
+    // Heavy batches (lists mostly past the stage row, so the rows were
+    // widened: C5, ~880 ids per topic) walk thousands of nodes per topic,
+    // where lanes sharing prefixes matter more than the drain: the
+    // range-local word-hash order with the light tail (6) at any size (C5
+    // 1M topics: step 35.7 vs 38.9 ms in the tail order, profiles/r05_e)
+    int presort_of(uint32_t n, const DevState& d) const {
+        if (presort != 3) return presort;
+        if (d.unkeyed_k > stage_k_min) return 6;
+        return n >= sort_min ? 5 : 2;
+    }
     // (presort 4: the tail order, then the word-hash key within each heat
     // class; 5: the word-hash key within each XCD range -- A/B orders)
     void ensure_slot(DevState& d, Slot& w, uint32_t n, uint64_t nbytes, uint32_t key_words, int presort) {
@@ -2353,7 +2362,7 @@ struct tm_engine {
         const bool shaped = keys && key_words == 1 && shape_keys;
         const uint32_t kw = keys && !shaped ? key_words : 0u;
         adapt_stage_k(d, n, kw);
-        const int presort = presort_of(n);
+        const int presort = presort_of(n, d);
         last_order = presort;
         const int si = d.next_slot;
         d.next_slot = (d.next_slot + 1) % nslots;

@@ -680,10 +680,12 @@ int  tm_rewrite_match_batch_device(tm_rewrite* r, const uint8_t* d_topics, const
  *              range the topics whose words label the most trie nodes first
  *              (one radix pass), so the walk's last lanes finish on light
  *              topics (batches above wave_walk_max); 5 = the word-hash key
- *              within each XCD range (two radix passes); 3 = by batch size:
- *              5 from "sort_min" topics on, 2 below (default); 0 = arrival
- *              order; 4 = the tail order, then the word-hash key within a
- *              heat class (A/B)
+ *              within each XCD range (two radix passes); 6 = order 5 with
+ *              each range's lightest topics last ("light_tail" per mille,
+ *              default 60); 3 = by batch: 6 for heavy batches (lists mostly
+ *              past the stage row), else 5 from "sort_min" topics on, 2
+ *              below (default); 0 = arrival order; 4 = the tail order, then
+ *              the word-hash key within a heat class (A/B)
  *   "sort_min" presort 3's smallest batch walked in range-local word-hash order
  *              (default 3000000)
  *   "sort_bits" the key bits presort 1 and 5 sort, one radix pass per 8
