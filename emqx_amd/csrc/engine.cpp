@@ -214,9 +214,11 @@ constexpr int N_KERNEL_SLOTS = 4;   // tokenize, walk, scan, copy_out
 struct Slot {
     DevBuf twords, words, path, meta, scan, stage, kstage, ws, stats, perm, skeys, svals, scount, soff, sscan,
         twords_s, meta_s, spill, spill_head;
+    DevBuf icounts, ioff;           // option "root_split": the 2n items' counts and offsets
     DevBuf sctl;                    // tm_match_small's placement / completion counters (left zeroed by it)
     uint32_t spill_chunks = 0;      // spill capacity of the slot's last batch (0: none)
     bool sorted = false;            // the slot's last batch walked in presort order (perm valid)
+    bool split = false;             // ... walked as 2n root-split items (icounts / ioff valid)
     uint64_t* h_maxc = nullptr;     // pinned copy of the slot's ws after its last walk (largest match count,
                                     // spill chunks taken per XCD)
     hipEvent_t maxc_ev = nullptr, done = nullptr;
@@ -678,6 +680,7 @@ struct tm_engine {
                                         // (no re-walks); unkeyed walks keep K and spill (kernels.h)
     int spill_on = 1;                   // option "spill": ids past K to spill chunks (0: re-walk, as keyed)
     int chunk_rows = TM_CHUNK_ROWS;     // option "chunk_rows" (kernels.h QueueBufs)
+    int root_split = 0;                 // option "root_split" (kernels.h QueueBufs)
     uint32_t wave_walk_max = 32768;     // option "wave_walk_max": batches of at most this many topics take the
                                         // wave-per-topic walk (tm_walk_wave: ~2 dependent loads per level);
                                         // faster up to 16K topics, slower from 64K (profiles/r03_d)
@@ -2250,19 +2253,27 @@ struct tm_engine {
     }
     // (presort 4: the tail order, then the word-hash key within each heat
     // class; 5: the word-hash key within each XCD range -- A/B orders)
-    void ensure_slot(DevState& d, Slot& w, uint32_t n, uint64_t nbytes, uint32_t key_words, int presort) {
+    void ensure_slot(DevState& d, Slot& w, uint32_t n, uint64_t nbytes, uint32_t key_words, int presort,
+                     bool split) {
+        // split: rows, counts, spill heads and scan by item (2n); a second
+        // path area for the copy-out's re-walks of items 2t
+        const uint32_t nq = split ? 2 * n : n;
         w.twords.ensure((size_t)(n + 1) * WREG * 4);
         w.words.ensure((nbytes + n + 1) * 4);
-        w.path.ensure((nbytes + 2ull * n + 2) * 4);
+        w.path.ensure((nbytes + 2ull * n + 2) * 4 * (split ? 2 : 1));
         w.stats.ensure(STATS_BYTES);
         w.meta.ensure((size_t)(n + 1) * 4);
-        w.scan.ensure(scan_tmp_elems(n) * 8 + 8);
-        w.stage.ensure(((size_t)n * d.stage_k + 4) * 4);
+        w.scan.ensure(scan_tmp_elems(nq) * 8 + 8);
+        w.stage.ensure(((size_t)nq * d.stage_k + 4) * 4);
+        if (split) {
+            w.icounts.ensure((size_t)nq * 4 + 8);
+            w.ioff.ensure(((size_t)nq + 2) * 8);
+        }
         if (key_words) w.kstage.ensure(((size_t)n * d.stage_k * key_words + 4) * 8);
         w.spill_chunks = 0;
         if (!key_words && spill_on && (!presort || chunk_rows) && d.spill_chunks >= 8) {
             w.spill.ensure((size_t)d.spill_chunks * SPILL_CHUNK * 4);
-            w.spill_head.ensure((size_t)n * 4 + 4);
+            w.spill_head.ensure((size_t)nq * 4 + 4);
             w.spill_chunks = (uint32_t)d.spill_chunks;
         }
         w.ws.ensure(QWS_BYTES);
@@ -2364,6 +2375,10 @@ struct tm_engine {
         adapt_stage_k(d, n, kw);
         const int presort = presort_of(n, d);
         last_order = presort;
+        // option "root_split": exactly the batches launch_queue walks in chunk
+        // rows (unkeyed, lane walk -- a wave-walk batch has no perm -- no stats)
+        const bool wave = n <= wave_walk_max && !kw && presort != 1;
+        const bool split = root_split && !kw && !shaped && !stats_enabled && chunk_rows && !wave && n <= (1u << 30);
         const int si = d.next_slot;
         d.next_slot = (d.next_slot + 1) % nslots;
         Slot& w = d.slots[si];
@@ -2371,7 +2386,7 @@ struct tm_engine {
         // every slot sized for this batch now: a slot first used later would
         // allocate (hipMalloc of GBs of stage rows) in the middle of a stream
         // of batches
-        for (int k = 0; k < nslots; ++k) ensure_slot(d, d.slots[(si + k) % nslots], n, nbytes, kw, presort);
+        for (int k = 0; k < nslots; ++k) ensure_slot(d, d.slots[(si + k) % nslots], n, nbytes, kw, presort, split);
         d.last_slot = si;
         ImageView im = view(d);
         unsigned long long* sp = w.stats.as<unsigned long long>();
@@ -2393,7 +2408,7 @@ struct tm_engine {
         qb.kstage = kw ? w.kstage.as<uint64_t>() : nullptr;
         qb.shaped = shaped;
         // the tail order (presort 2) leaves small batches to the wave walk
-        qb.wave_walk = n <= wave_walk_max && !kw && presort != 1;   // (the range-keyed orders: 2, 4, 5)
+        qb.wave_walk = wave;   // (the range-keyed orders: 2, 4, 5, 6)
         qb.chunk_rows = chunk_rows;
         qb.scan_tmp = w.scan.as<uint64_t>();
         qb.ws = w.ws.as<unsigned long long>();
@@ -2415,7 +2430,13 @@ struct tm_engine {
             qb.spill_head = w.spill_head.as<uint32_t>();
             qb.spill_chunks = w.spill_chunks;
         }
+        qb.root_split = split;
+        if (split) {
+            qb.icounts = w.icounts.as<uint32_t>();
+            qb.ioff = w.ioff.as<uint64_t>();
+        }
         w.sorted = queue_rows_by_position(qb, stats_enabled);   // the copy-out moves rows by perm
+        w.split = split;
         HIPCHK(launch_queue(stats_enabled, xcdq != 0, im, bytes, off, n, qb, d.stage_k, counts, out_off, ids, keys,
                             cap, total, sp, st, timing_enabled ? marks : nullptr, walk_bpc, hist_enabled != 0,
                             keys ? key_words : 1u));
@@ -2479,6 +2500,11 @@ struct tm_engine {
         qb.scan_tmp = w.scan.as<uint64_t>();
         qb.ws = w.ws.as<unsigned long long>();
         qb.perm = w.sorted ? w.perm.as<uint32_t>() : nullptr;   // the rows of a presorted walk
+        if (w.split) {   // the item rows, counts and offsets of a root-split walk
+            qb.root_split = true;
+            qb.icounts = w.icounts.as<uint32_t>();
+            qb.ioff = w.ioff.as<uint64_t>();
+        }
         if (w.spill_chunks && !w.keyed) {   // the spill chunks of the same walk
             qb.spill = w.spill.as<uint32_t>();
             qb.spill_head = w.spill_head.as<uint32_t>();
@@ -4185,6 +4211,11 @@ int tm_set_option(tm_engine* e, const char* name, int64_t value) {
         if (!std::strcmp(name, "chunk_rows")) {
             if (value < 0 || value > 1) return TM_EINVAL;
             e->chunk_rows = (int)value;
+            return TM_OK;
+        }
+        if (!std::strcmp(name, "root_split")) {   // each topic walked as two queue items (kernels.h QueueBufs)
+            if (value < 0 || value > 1) return TM_EINVAL;
+            e->root_split = (int)value;
             return TM_OK;
         }
         if (!std::strcmp(name, "shape_keys")) {

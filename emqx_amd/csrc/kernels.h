@@ -52,6 +52,19 @@ struct QueueBufs {
                                  // tail_key: heavy topics first in each XCD range, one radix pass)
     uint32_t sort_passes = 4;    // mode 1: radix passes over the key's top 8 * sort_passes bits (1..4)
     uint32_t light_max = 31;     // mode 6: cost classes <= light_max are walked last in their XCD range
+    // option "root_split": every topic is two queue items, 2t = the root's
+    // '+' subtree and 2t + 1 = the rest (the root's '#' filter and literal
+    // subtree), each with its own stage row (K slots), count (icounts) and
+    // spill head; their concatenation in item order IS the topic's list in
+    // emqx_trie:match/1 order (the '+' subtree is discovered last, so it is
+    // output first).  The item CSR (ioff, over 2n) is scanned and copied as
+    // usual, then folded into the topics' counts and offsets.  Halves the
+    // longest work item, so the walk's drain (lanes finishing their last
+    // topic while the queue is dry) shortens.  Unkeyed chunk-row walks only;
+    // long topics (> WREG levels) stay one item (2t + 1; 2t empty).
+    bool root_split = false;
+    uint32_t* icounts = nullptr;   // 2n
+    uint64_t* ioff = nullptr;      // 2n + 1
     // the radix passes of the batch's presort: the tokenizer writes the keys
     // and values where the first pass reads them, so the last ends in perm
     uint32_t presort_passes() const { return presort_mode == 2 ? 1u : presort_mode == 4 ? 2u : sort_passes; }

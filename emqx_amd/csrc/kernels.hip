@@ -536,6 +536,9 @@ constexpr int HIST_OFF = 8;   // hist = stats + HIST_OFF
 #ifndef TM_PEND_MASK
 #define TM_PEND_MASK 1   // A/B at C3: walk 9.78 vs 10.08-10.09 ms (profiles/r03_ab)
 #endif
+// Cursor::pend bit 31 (option "root_split", item 2t + 1): the root's '+'
+// child is not visited (item 2t walks that subtree)
+constexpr uint32_t ROOT_NOPLUS = 1u << 31;
 struct Cursor {
     uint32_t v, r, n, r0;   // node to visit next and its level; topic levels; start level
     uint32_t pend;          // TM_PEND_MASK: bit k = path(k) holds a '+' child still to visit (k < r)
@@ -749,7 +752,8 @@ __device__ __forceinline__ bool walk_step(const ImageView& im, Cursor& c, Path p
         }
         if (STATS) st.prunable += (g.child != NODE_NONE && !lit_ok ? 1u : 0u) +
                                   ((plus & NODE_MASK) != NODE_NONE && !plus_ok ? 1u : 0u);
-        const uint32_t pc = (STATS || plus_ok) ? (plus & NODE_MASK) : NODE_NONE;
+        const uint32_t pc = ((STATS || plus_ok) && !(r == 0 && (c.pend & ROOT_NOPLUS))) ? (plus & NODE_MASK)
+                                                                                          : NODE_NONE;
         if (STATS && st.hist) {   // how the next visit is reached: [48] inline literal, [49] table literal,
                                   // [50] '+' (here or by a later pop: counted at the pop)
             if (g.child != NODE_NONE) atomicAdd(st.hist + ((plus & WIDE) ? 49 : 48), 1ull);
@@ -794,6 +798,42 @@ __device__ __forceinline__ void walk(const ImageView& im, uint32_t n, bool dolla
     Cursor c;
     if (!walk_begin(im, c, n, dollar, W, st)) return;
     while (!walk_step<STATS, KEYS>(im, c, path, W, emit, st)) {
+    }
+}
+
+// option "root_split": the start of item `part` of a topic.  Part 0 walks
+// the root's '+' subtree (from level 1; nothing for '$' topics, whose walk
+// skips the root's '+' and '#', emqx_trie.erl:121-122); part 1 the rest,
+// the root's '+' child left out.  Discovery order: the root's '#' filter,
+// its literal subtree (part 1), then its '+' subtree (part 0), so the
+// reversed lists concatenate as part 0's then part 1's.
+template <class Words>
+__device__ __forceinline__ bool walk_begin_part(const ImageView& im, Cursor& c, uint32_t n, bool dollar,
+                                                const Words& W, WalkStats& st, uint32_t part) {
+    if (part) {
+        const bool go = walk_begin(im, c, n, dollar, W, st);
+        if (!dollar) c.pend |= ROOT_NOPLUS;
+        return go;
+    }
+    c.n = n;
+    c.key = 0;
+    c.pend = 0;
+    c.pf_id = NODE_NONE;
+    if (dollar) return false;
+    const uint4 q = load_half(im, ROOT, false);
+    const uint32_t pc = q.x & NODE_MASK;
+    if (pc == NODE_NONE || ((q.y & SUM_TAG) && !sum_useful(q.y & SUM_ALL, n - 1))) return false;
+    c.v = pc;
+    c.r = c.r0 = 1;
+    return true;
+}
+// a whole walk of one item (part < 2) or topic (part = 2), global path
+template <class Words, class Emit>
+__device__ __forceinline__ void walk_item(const ImageView& im, uint32_t n, bool dollar, GlobalPath path,
+                                          const Words& W, Emit& emit, WalkStats& st, uint32_t part) {
+    Cursor c;
+    if (part < 2 ? !walk_begin_part(im, c, n, dollar, W, st, part) : !walk_begin(im, c, n, dollar, W, st)) return;
+    while (!walk_step<false, false>(im, c, path, W, emit, st)) {
     }
 }
 
@@ -965,8 +1005,13 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
               unsigned long long* __restrict__ ws, unsigned long long* __restrict__ stats,
               unsigned long long* __restrict__ hist, const uint32_t* __restrict__ perm,
               const uint32_t* __restrict__ twords_s, const uint32_t* __restrict__ meta_s,
-              uint32_t* __restrict__ spill, uint32_t* __restrict__ spill_head, uint32_t spill_chunks) {
+              uint32_t* __restrict__ spill, uint32_t* __restrict__ spill_head, uint32_t spill_chunks, uint32_t split) {
     static_assert(CH == CH_NONE || (!STATS && !KEYS), "chunk rows: unkeyed walks in arrival order only");
+    // queue positions: n topics, or 2n items (option "root_split": chunk-row
+    // walks only; position p is item p & 1 of topic p >> 1, stage row,
+    // count and spill head by item 2 x topic + part)
+    if (CH == CH_NONE) split = 0;
+    const uint32_t nq = n << split;
     __shared__ uint32_t lds_path[WREG * BLOCK];
     __shared__ ChunkRows lds_chunk[CH != CH_NONE ? BLOCK / 64 : 1];
     const uint32_t lane = threadIdx.x & 63;
@@ -1012,8 +1057,8 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
                 if (XCDQ) {
                     while (qr < QRANGES) {
                         const uint32_t r = (home + qr) & (QRANGES - 1);
-                        const uint32_t rb = (uint32_t)((uint64_t)n * r / QRANGES);
-                        const uint32_t re = (uint32_t)((uint64_t)n * (r + 1) / QRANGES);
+                        const uint32_t rb = (uint32_t)((uint64_t)nq * r / QRANGES);
+                        const uint32_t re = (uint32_t)((uint64_t)nq * (r + 1) / QRANGES);
                         uint32_t x = 0;
                         if (lane == leader)
                             x = (uint32_t)__hip_atomic_fetch_add(ws + 16 * r, (unsigned long long)QCHUNK,
@@ -1036,9 +1081,9 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
                         x = (uint32_t)__hip_atomic_fetch_add(ws, (unsigned long long)QCHUNK, __ATOMIC_RELAXED,
                                                              __HIP_MEMORY_SCOPE_AGENT);
                     x = __shfl(x, leader, 64);
-                    if (x < n) {
+                    if (x < nq) {
                         g = x;
-                        gend = g + QCHUNK < n ? g + QCHUNK : n;
+                        gend = g + QCHUNK < nq ? g + QCHUNK : nq;
                     } else {
                         exhausted = true;
                     }
@@ -1050,8 +1095,9 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
                 if (t < gend) {
                     // a presorted batch: queue position t walks topic perm[t], whose row
                     // is read here (the rows are not gathered into walk order)
-                    const uint32_t tt = perm ? stream_load(perm + t) : t;
-                    CR.topic[lane] = tt;
+                    const uint32_t tq = t >> split;
+                    const uint32_t tt = perm ? stream_load(perm + tq) : tq;
+                    CR.topic[lane] = (tt << split) | (t & split);   // the item (= the topic without split)
                     CR.meta[lane] = stream_load(meta + tt);
                     const uint4* src = reinterpret_cast<const uint4*>(twords + (uint64_t)tt * WREG);
                     const uint4 a0 = stream_load16(src), a1 = stream_load16(src + 1);   // quad 1 may be stale: unread
@@ -1072,10 +1118,11 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
                 if (rank < avail) i = qnext + rank;
                 else if (g + (rank - avail) < gend) i = g + (rank - avail);
                 if (i != NO_TOPIC) {
-                    // i: queue position = stage row; ti: the topic
-                    // CH: stage rows, counts and spill heads by topic (a presorted
-                    // batch then needs no position-ordered copy-out)
-                    const uint32_t ti = CH != CH_NONE ? CR.topic[i - cbase] : perm ? perm[i] : i;
+                    // i: queue position = stage row; ti: the topic; item: the
+                    // stage row / count / spill head (CH: by topic or item, so a
+                    // presorted batch needs no position-ordered copy-out)
+                    const uint32_t item = CH != CH_NONE ? CR.topic[i - cbase] : perm ? perm[i] : i;
+                    const uint32_t ti = item >> split, part = item & split;
                     const uint32_t* tws = CH == CH_NONE && perm ? twords_s : twords;
                     const uint32_t mt = CH != CH_NONE ? CR.meta[i - cbase] : perm ? meta_s[i] : meta[i];
                     const uint32_t nl = mt & MN;
@@ -1083,7 +1130,7 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
                     lev_sum += nl;
                     maxl = nl > maxl ? nl : maxl;
                     is_long = (mt & MLONG) != 0;
-                    em.row = stage + (uint64_t)(CH != CH_NONE ? ti : i) * K;
+                    em.row = stage + (uint64_t)(CH != CH_NONE ? item : i) * K;
                     if (KEYS) em.krow = kstage + (uint64_t)i * K;
                     em.cnt = 0;
                     em.sfail = false;
@@ -1101,7 +1148,8 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
                         rw.w[5] = a1.y;
                         rw.w[6] = a1.z;
                         rw.w[7] = a1.w;
-                        go = walk_begin(im, cur, nl, dollar, rw, st);
+                        go = split ? walk_begin_part(im, cur, nl, dollar, rw, st, part)
+                                   : walk_begin(im, cur, nl, dollar, rw, st);
                     } else if (!is_long) {
 #pragma unroll
                         for (uint32_t k = 0; k < WREG / 4; ++k) {
@@ -1114,18 +1162,21 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
                                 rw.w[4 * k + 3] = x.w;
                             }
                         }
-                        go = walk_begin(im, cur, nl, dollar, rw, st);
+                        go = split ? walk_begin_part(im, cur, nl, dollar, rw, st, part)
+                                   : walk_begin(im, cur, nl, dollar, rw, st);
                     } else {
                         const uint64_t b = off[ti] - off[0];
                         mw = MemWords{tw, words + b + ti};
                         gp.base = gpath + b + 2ull * ti;
-                        go = walk_begin(im, cur, nl, dollar, mw, st);
+                        // a long topic is one item (2t + 1: the whole walk; 2t empty):
+                        // its global path area is the topic's
+                        go = (split && !part) ? false : walk_begin(im, cur, nl, dollar, mw, st);
                     }
                     if (go) {
                         my = i;
-                        myt = ti;
+                        myt = item;
                     } else {
-                        counts[ti] = 0;
+                        counts[item] = 0;
                     }
                 } else if (exhausted) {
                     drained = true;
@@ -1485,7 +1536,9 @@ tm_copy_out(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const ui
             const uint32_t* __restrict__ stage, const uint64_t* __restrict__ kstage, uint32_t K, uint32_t KW,
             const uint32_t* __restrict__ counts, const uint64_t* __restrict__ out_off, uint32_t* __restrict__ out,
             uint64_t* __restrict__ kout, uint64_t out_cap, const uint32_t* __restrict__ spill,
-            const uint32_t* __restrict__ spill_head) {
+            const uint32_t* __restrict__ spill_head, uint32_t split) {
+    // split (option "root_split", unkeyed): n counts 2x the topics' items;
+    // item x is part x & 1 of topic x >> 1 (its rows, words and path area)
     const uint64_t kplane = (uint64_t)n * K;   // KEYS: key word j of stage slot x at kstage[j * kplane + x],
                                                // of output p at kout[j * out_cap + p]
     __shared__ uint32_t lds_inc[BLOCK];
@@ -1637,7 +1690,7 @@ tm_copy_out(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const ui
     if (threadIdx.x < tn && (tail || ood(threadIdx.x))) {
         // fan-out beyond the stage row and no spill: walk again, write the
         // head; SHAPED: keyed, and every output of an out-of-domain topic
-        const uint32_t t = t0 + threadIdx.x;
+        const uint32_t x = t0 + threadIdx.x, t = x >> split;   // item, topic
         const uint32_t mt = meta[t];
         const uint64_t b = off[t] - off[0];
         const MemWords mw{twords + (uint64_t)t * WREG, words + b + t};
@@ -1645,8 +1698,18 @@ tm_copy_out(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const ui
         TailEmit<WK> em{out, kout, base + ex, out_cap, ood(threadIdx.x) ? 0u : K, c, 0, KW, out_cap};
         WalkStats s2;
         // the topic's global path area (the walk's, for long topics): no LDS
-        // path here, so the copy-out's blocks stay small (1.3 KB of LDS)
-        walk<false, WK>(im, mt & MN, (mt & MDOLLAR) != 0, GlobalPath{gpath + b + 2ull * t}, mw, em, s2);
+        // path here, so the copy-out's blocks stay small (1.3 KB of LDS);
+        // split: item 2t re-walks in a second area past the first (the
+        // engine sizes the path buffer twice over), item 2t + 1 in the topic's
+        if (!WK && split) {
+            const uint32_t nt = n >> 1;
+            const uint64_t second = (x & 1u) ? 0 : (off[nt] - off[0]) + 2ull * nt + 2;
+            // a long topic is item 2t + 1 alone (its walk is the whole topic)
+            const uint32_t part = (mt & MLONG) ? 2u : (x & 1u);
+            walk_item(im, mt & MN, (mt & MDOLLAR) != 0, GlobalPath{gpath + second + b + 2ull * t}, mw, em, s2, part);
+        } else {
+            walk<false, WK>(im, mt & MN, (mt & MDOLLAR) != 0, GlobalPath{gpath + b + 2ull * t}, mw, em, s2);
+        }
     }
 }
 
@@ -1699,6 +1762,21 @@ tm_copy_out_sorted(ImageView im, const uint64_t* __restrict__ off, uint32_t n, c
         WalkStats s2;
         walk<false, KEYS>(im, mt & MN, (mt & MDOLLAR) != 0, GlobalPath{gpath + b + 2ull * t}, mw, em, s2);
     }
+}
+
+// option "root_split": the item CSR (2n counts, 2n + 1 offsets) folded into
+// the topics' (items 2t and 2t + 1 are adjacent, so a topic's list starts at
+// its first item's offset)
+__global__ void __launch_bounds__(BLOCK)
+tm_fold_items(const uint32_t* __restrict__ icounts, const uint64_t* __restrict__ ioff, uint32_t n,
+              uint32_t* __restrict__ counts, uint64_t* __restrict__ out_off) {
+    const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
+    if (t < n) {
+        const uint2 c = reinterpret_cast<const uint2*>(icounts)[t];
+        counts[t] = c.x + c.y;
+        out_off[t] = ioff[2ull * t];
+    }
+    if (t == n) out_off[n] = ioff[2ull * n];
 }
 
 constexpr int SCAN_ITEMS = 8;
@@ -1883,8 +1961,17 @@ hipError_t launch_copy(const ImageView& im, const uint8_t* bytes, const uint64_t
                        uint32_t K, uint32_t key_words, const uint32_t* counts, const uint64_t* out_off, uint32_t* out,
                        uint64_t* out_keys, uint64_t out_cap, hipStream_t st) {
     if (n == 0 || out_cap == 0) return hipSuccess;
-    dim3 blk(BLOCK), g(div_up(n, BLOCK));
-    if (qb.perm) {   // a presorted walk: stage row p is topic perm[p]
+    // option "root_split": the 2n items' rows, counts and offsets (counts /
+    // out_off here are the topics', folded from them)
+    const bool split = qb.root_split && !qb.kstage && !qb.shaped;
+    if (qb.root_split && !split) return hipErrorInvalidValue;
+    if (split) {
+        counts = qb.icounts;
+        out_off = qb.ioff;
+    }
+    const uint32_t nq = split ? 2 * n : n;
+    dim3 blk(BLOCK), g(div_up(nq, BLOCK));
+    if (qb.perm && !split) {   // a presorted walk: stage row p is topic perm[p]
         if (qb.kstage)
             hipLaunchKernelGGL(tm_copy_out_sorted<true>, g, blk, 0, st, im, off, n, qb.twords, qb.words, qb.meta,
                                qb.path, qb.stage, qb.kstage, K, key_words, counts, out_off, out, out_keys, out_cap,
@@ -1895,16 +1982,16 @@ hipError_t launch_copy(const ImageView& im, const uint8_t* bytes, const uint64_t
     } else if (qb.kstage) {
         hipLaunchKernelGGL((tm_copy_out<true, false>), g, blk, 0, st, im, off, n, qb.twords, qb.words, qb.meta,
                            qb.path, qb.stage, qb.kstage, K, key_words, counts, out_off, out, out_keys, out_cap,
-                           nullptr, nullptr);
+                           nullptr, nullptr, 0u);
     } else if (qb.shaped) {
         if (!out_keys || key_words != 1 || !im.fshape) return hipErrorInvalidValue;
         hipLaunchKernelGGL((tm_copy_out<false, true>), g, blk, 0, st, im, off, n, qb.twords, qb.words, qb.meta,
                            qb.path, qb.stage, nullptr, K, 1u, counts, out_off, out, out_keys, out_cap,
-                           qb.spill_chunks >= QRANGES ? qb.spill : nullptr, qb.spill_head);
+                           qb.spill_chunks >= QRANGES ? qb.spill : nullptr, qb.spill_head, 0u);
     } else {
-        hipLaunchKernelGGL((tm_copy_out<false, false>), g, blk, 0, st, im, off, n, qb.twords, qb.words, qb.meta,
+        hipLaunchKernelGGL((tm_copy_out<false, false>), g, blk, 0, st, im, off, nq, qb.twords, qb.words, qb.meta,
                            qb.path, qb.stage, nullptr, K, 1u, counts, out_off, out, nullptr, out_cap,
-                           qb.spill_chunks >= QRANGES ? qb.spill : nullptr, qb.spill_head);
+                           qb.spill_chunks >= QRANGES ? qb.spill : nullptr, qb.spill_head, split ? 1u : 0u);
     }
     return hipGetLastError();
 }
@@ -1962,23 +2049,31 @@ hipError_t launch_queue(bool stats_mode, bool xcdq, const ImageView& im, const u
         mark(5);
         mark(6);
         if (out_cap) {
-            err = launch_copy(im, bytes, off, n, qb, K, key_words, counts, out_off, out, out_keys, out_cap, st);
+            QueueBufs qc = qb;
+            qc.root_split = false;
+            err = launch_copy(im, bytes, off, n, qc, K, key_words, counts, out_off, out, out_keys, out_cap, st);
             if (err != hipSuccess) return err;
         }
         mark(7);
         return hipGetLastError();
     }
+    // option "root_split": 2n queue items (chunk rows only), their counts and
+    // offsets in qb.icounts / qb.ioff, folded into the topics' after the copy
+    // (a batch walked otherwise ignores it)
+    const bool split = qb.root_split && ch == CH_ROWS;
+    if (split && (!qb.icounts || !qb.ioff || n > (1u << 30))) return hipErrorInvalidValue;
+    uint32_t* const wcounts = split ? qb.icounts : counts;
     // spill chunks: unkeyed walks in arrival order (presorted rows re-walk)
     uint32_t* const spill = (!keys && !by_pos && qb.spill_chunks >= QRANGES) ? qb.spill : nullptr;
-    const uint32_t wg = ch == CH_ROWS ? resident_grid(tm_walk_queue<false, true, false, CH_ROWS>, div_up(n, 64),
+    const uint32_t wg = ch == CH_ROWS ? resident_grid(tm_walk_queue<false, true, false, CH_ROWS>, div_up(n << split, 64),
                                                       walk_blocks_per_cu)
-                                      : resident_grid(tm_walk_queue<false, false, false>, div_up(n, 64),
+                                      : resident_grid(tm_walk_queue<false, false, false>, div_up(n << split, 64),
                                                       walk_blocks_per_cu);
 #define TM_Q(S, X, Y, C)                                                                                           \
     hipLaunchKernelGGL((tm_walk_queue<S, X, Y, C>), dim3(wg), blk, 0, st, im, off, n, qb.twords, qb.words,       \
-                       qb.meta, qb.path, qb.stage, qb.kstage, K, key_words, counts, qb.ws, stats,                \
+                       qb.meta, qb.path, qb.stage, qb.kstage, K, key_words, wcounts, qb.ws, stats,               \
                        hist ? stats + HIST_OFF : nullptr, qb.perm, qb.twords_s, qb.meta_s, spill, qb.spill_head,   \
-                       qb.spill_chunks)
+                       qb.spill_chunks, split ? 1u : 0u)
     if (ch == CH_ROWS) {
         if (xcdq) TM_Q(false, true, false, CH_ROWS); else TM_Q(false, false, false, CH_ROWS);
     } else if (keys) {
@@ -1991,12 +2086,27 @@ hipError_t launch_queue(bool stats_mode, bool xcdq, const ImageView& im, const u
 #undef TM_Q
     mark(3);
     mark(4);
+    if (split) {
+        err = launch_scan(qb.icounts, 2 * n, qb.ioff, total, qb.scan_tmp, st);
+        if (err != hipSuccess) return err;
+        mark(5);
+        mark(6);
+        if (out_cap) {
+            err = launch_copy(im, bytes, off, n, qb, K, key_words, nullptr, nullptr, out, out_keys, out_cap, st);
+            if (err != hipSuccess) return err;
+        }
+        hipLaunchKernelGGL(tm_fold_items, dim3(div_up(n + 1, BLOCK)), blk, 0, st, qb.icounts, qb.ioff, n, counts,
+                           out_off);
+        mark(7);
+        return hipGetLastError();
+    }
     err = launch_scan(counts, n, out_off, total, qb.scan_tmp, st);
     if (err != hipSuccess) return err;
     mark(5);
     mark(6);
     if (out_cap) {
         QueueBufs qc = qb;
+        qc.root_split = false;
         if (!by_pos) qc.perm = nullptr;   // stage rows by topic
         err = launch_copy(im, bytes, off, n, qc, K, key_words, counts, out_off, out, out_keys, out_cap, st);
         if (err != hipSuccess) return err;
