@@ -215,10 +215,13 @@ struct Slot {
     DevBuf twords, words, path, meta, scan, stage, kstage, ws, stats, perm, skeys, svals, scount, soff, sscan,
         twords_s, meta_s, spill, spill_head;
     DevBuf icounts, ioff;           // option "root_split": the 2n items' counts and offsets
+    DevBuf prow, pdesc, pcnt, tfirst, dmask;   // option "donate": the piece pool and the topics' piece lists
+    uint32_t pcap = 0;
     DevBuf sctl;                    // tm_match_small's placement / completion counters (left zeroed by it)
     uint32_t spill_chunks = 0;      // spill capacity of the slot's last batch (0: none)
     bool sorted = false;            // the slot's last batch walked in presort order (perm valid)
     bool split = false;             // ... walked as 2n root-split items (icounts / ioff valid)
+    bool donated = false;           // ... with option "donate" (the piece pool and lists valid)
     uint64_t* h_maxc = nullptr;     // pinned copy of the slot's ws after its last walk (largest match count,
                                     // spill chunks taken per XCD)
     hipEvent_t maxc_ev = nullptr, done = nullptr;
@@ -681,6 +684,10 @@ struct tm_engine {
     int spill_on = 1;                   // option "spill": ids past K to spill chunks (0: re-walk, as keyed)
     int chunk_rows = TM_CHUNK_ROWS;     // option "chunk_rows" (kernels.h QueueBufs)
     int root_split = 0;                 // option "root_split" (kernels.h QueueBufs)
+    int donate = 0;                     // option "donate" (kernels.h QueueBufs): the drain's donation walk
+    uint32_t don_min = 2;               // option "donate_min": levels a donated subtree has below its node
+    uint32_t donate_max = 0xFFFFFFFFu;  // option "donate_max": only batches of at most this many topics
+    uint32_t don_busy = 8;              // option "donate_busy": only while at most this many lanes still walk
     uint32_t wave_walk_max = 32768;     // option "wave_walk_max": batches of at most this many topics take the
                                         // wave-per-topic walk (tm_walk_wave: ~2 dependent loads per level);
                                         // faster up to 16K topics, slower from 64K (profiles/r03_d)
@@ -2253,8 +2260,13 @@ struct tm_engine {
     }
     // (presort 4: the tail order, then the word-hash key within each heat
     // class; 5: the word-hash key within each XCD range -- A/B orders)
+    // the piece pool of a donating walk (option "donate"): up to n/2 pieces
+    static uint32_t piece_cap(uint32_t n) {
+        const uint64_t c = std::max<uint64_t>((uint64_t)n / 2, 8192);
+        return (uint32_t)std::min<uint64_t>((c + 7) & ~7ull, 1u << 30);
+    }
     void ensure_slot(DevState& d, Slot& w, uint32_t n, uint64_t nbytes, uint32_t key_words, int presort,
-                     bool split) {
+                     bool split, bool don = false) {
         // split: rows, counts, spill heads and scan by item (2n); a second
         // path area for the copy-out's re-walks of items 2t
         const uint32_t nq = split ? 2 * n : n;
@@ -2268,6 +2280,15 @@ struct tm_engine {
         if (split) {
             w.icounts.ensure((size_t)nq * 4 + 8);
             w.ioff.ensure(((size_t)nq + 2) * 8);
+        }
+        if (don) {
+            const uint32_t pc = piece_cap(n);
+            w.prow.ensure(((size_t)pc * d.stage_k + 4) * 4);
+            w.pdesc.ensure((size_t)pc * 16);
+            w.pcnt.ensure((size_t)pc * 8);
+            w.tfirst.ensure((size_t)n * 4 + 4);
+            w.dmask.ensure(((size_t)(n >> 5) + 1) * 4);
+            w.pcap = pc;
         }
         if (key_words) w.kstage.ensure(((size_t)n * d.stage_k * key_words + 4) * 8);
         w.spill_chunks = 0;
@@ -2354,6 +2375,17 @@ struct tm_engine {
         }
         d.stage_k = d.keyed_k;
     }
+    void set_pieces(QueueBufs& qb, Slot& w) const {
+        qb.donate = true;
+        qb.don_min = don_min;
+        qb.don_busy = don_busy;
+        qb.prow = w.prow.as<uint32_t>();
+        qb.pdesc = w.pdesc.as<uint32_t>();
+        qb.pcnt = w.pcnt.as<uint32_t>();
+        qb.tfirst = w.tfirst.as<uint32_t>();
+        qb.dmask = w.dmask.as<uint32_t>();
+        qb.pcap = w.pcap;
+    }
     void record_maxc(Slot& w, hipStream_t st) {
         if (!w.h_maxc) HIPCHK(hipHostMalloc((void**)&w.h_maxc, QWS_BYTES, hipHostMallocDefault));
         if (!w.maxc_ev) HIPCHK(hipEventCreateWithFlags(&w.maxc_ev, hipEventDisableTiming));
@@ -2379,6 +2411,8 @@ struct tm_engine {
         // rows (unkeyed, lane walk -- a wave-walk batch has no perm -- no stats)
         const bool wave = n <= wave_walk_max && !kw && presort != 1;
         const bool split = root_split && !kw && !shaped && !stats_enabled && chunk_rows && !wave && n <= (1u << 30);
+        // option "donate": the same batches (root_split gives way)
+        const bool don = donate && n <= donate_max && !kw && !shaped && !stats_enabled && chunk_rows && !wave;
         const int si = d.next_slot;
         d.next_slot = (d.next_slot + 1) % nslots;
         Slot& w = d.slots[si];
@@ -2386,7 +2420,7 @@ struct tm_engine {
         // every slot sized for this batch now: a slot first used later would
         // allocate (hipMalloc of GBs of stage rows) in the middle of a stream
         // of batches
-        for (int k = 0; k < nslots; ++k) ensure_slot(d, d.slots[(si + k) % nslots], n, nbytes, kw, presort, split);
+        for (int k = 0; k < nslots; ++k) ensure_slot(d, d.slots[(si + k) % nslots], n, nbytes, kw, presort, split && !don, don);
         d.last_slot = si;
         ImageView im = view(d);
         unsigned long long* sp = w.stats.as<unsigned long long>();
@@ -2430,13 +2464,15 @@ struct tm_engine {
             qb.spill_head = w.spill_head.as<uint32_t>();
             qb.spill_chunks = w.spill_chunks;
         }
-        qb.root_split = split;
-        if (split) {
+        qb.root_split = split && !don;
+        if (qb.root_split) {
             qb.icounts = w.icounts.as<uint32_t>();
             qb.ioff = w.ioff.as<uint64_t>();
         }
+        if (don) set_pieces(qb, w);
         w.sorted = queue_rows_by_position(qb, stats_enabled);   // the copy-out moves rows by perm
-        w.split = split;
+        w.split = qb.root_split;
+        w.donated = don;
         HIPCHK(launch_queue(stats_enabled, xcdq != 0, im, bytes, off, n, qb, d.stage_k, counts, out_off, ids, keys,
                             cap, total, sp, st, timing_enabled ? marks : nullptr, walk_bpc, hist_enabled != 0,
                             keys ? key_words : 1u));
@@ -2505,6 +2541,7 @@ struct tm_engine {
             qb.icounts = w.icounts.as<uint32_t>();
             qb.ioff = w.ioff.as<uint64_t>();
         }
+        if (w.donated) set_pieces(qb, w);   // the piece lists of a donating walk
         if (w.spill_chunks && !w.keyed) {   // the spill chunks of the same walk
             qb.spill = w.spill.as<uint32_t>();
             qb.spill_head = w.spill_head.as<uint32_t>();
@@ -3861,6 +3898,25 @@ extern "C" int tm_debug_last_order(tm_engine* e) { return e ? e->last_order.load
 // out[4x..4x+3] = ms from the walk's first wave start to XCD x's first wave
 // start, to the first exhaustion of its home range, to its last wave's end,
 // and the chunks its waves stole (-1 where not recorded)
+// diagnostics: pieces donated by the last batch's walk on replica 0, per XCD
+// (option "donate"; 0 without)
+extern "C" int tm_debug_walk_pieces(tm_engine* e, uint64_t* out) {
+    if (!e || !out) return TM_EINVAL;
+    auto held = lock_batches(e);
+    return guarded(e, [&]() -> int {
+        if (e->devs.empty()) return TM_EINVAL;
+        DevState& d = *e->devs[0];
+        tm_engine::Guard g(d.device);
+        const DevBuf& ws = d.slots[d.last_slot].ws;
+        if (!ws.p) return TM_EINVAL;
+        HIPCHK(hipDeviceSynchronize());
+        std::vector<uint64_t> h(QWS_BYTES / 8);
+        HIPCHK(hipMemcpy(h.data(), ws.p, QWS_BYTES, hipMemcpyDeviceToHost));
+        for (int x = 0; x < 8; ++x) out[x] = h[QWS_PIECE + 16 * x];
+        return TM_OK;
+    });
+}
+
 extern "C" int tm_debug_walk_clocks(tm_engine* e, double* out) {
     if (!e || !out) return TM_EINVAL;
     auto held = lock_batches(e);
@@ -4211,6 +4267,26 @@ int tm_set_option(tm_engine* e, const char* name, int64_t value) {
         if (!std::strcmp(name, "chunk_rows")) {
             if (value < 0 || value > 1) return TM_EINVAL;
             e->chunk_rows = (int)value;
+            return TM_OK;
+        }
+        if (!std::strcmp(name, "donate")) {   // the drain's donation walk (kernels.h QueueBufs)
+            if (value < 0 || value > 1) return TM_EINVAL;
+            e->donate = (int)value;
+            return TM_OK;
+        }
+        if (!std::strcmp(name, "donate_min")) {
+            if (value < 0 || value > 15) return TM_EINVAL;
+            e->don_min = (uint32_t)value;
+            return TM_OK;
+        }
+        if (!std::strcmp(name, "donate_busy")) {
+            if (value < 1 || value > 64) return TM_EINVAL;
+            e->don_busy = (uint32_t)value;
+            return TM_OK;
+        }
+        if (!std::strcmp(name, "donate_max")) {
+            if (value < 0 || value > 0xFFFFFFFFll) return TM_EINVAL;
+            e->donate_max = (uint32_t)value;
             return TM_OK;
         }
         if (!std::strcmp(name, "root_split")) {   // each topic walked as two queue items (kernels.h QueueBufs)

@@ -990,23 +990,54 @@ constexpr uint32_t NO_TOPIC = 0xFFFFFFFFu;
 // walk itself, dropping tm_tokenize, measured 13.15-15.89 ms: the tokenizer's
 // registers cut the walk's occupancy.)
 constexpr uint32_t CW = 8;   // words per topic in the chunk's LDS rows
-constexpr int CH_NONE = 0, CH_ROWS = 1;
+constexpr int CH_NONE = 0, CH_ROWS = 1, CH_DON = 2;   // CH_DON: chunk rows + option "donate"
 struct ChunkRows {
     uint32_t w[QCHUNK][CW];
     uint32_t meta[QCHUNK];
     uint32_t topic[QCHUNK];   // the topic at each queue position (presorted batches: perm)
 };
-template <bool STATS, bool XCDQ, bool KEYS, int CH = CH_NONE>
-__global__ void __launch_bounds__(BLOCK) TM_WALK_ATTR
-tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const uint32_t* __restrict__ twords,
+// Option "donate" (CH_DON): the walk's drain.  Once a wave's queues are
+// dry, its lanes finish the topics they hold while the others idle (at 1M
+// C3 topics a third of the walk).  A lane still walking then hands its
+// shallowest pending '+' child (the path entry walk_pop would take last) to
+// an idle lane of its wave, which walks that subtree as a piece of the
+// topic: own stage row in the piece pool, count, spill chain.  The fold of
+// emqx_trie.erl:130-136 discovers the shallowest pending subtree after all
+// the rest of the donor's walk, and the list is the discovery order
+// reversed, so the piece's list goes right BEFORE the donor's remaining
+// list: each topic's pieces form a list (tfirst[t], pdesc next) ending in
+// the topic's own row (PIECE_SELF), kept in order by inserting each new
+// piece before its donor (a lane holds its own predecessor, prv).  Every
+// piece of a topic lives in one wave, so the list is only changed by one
+// wave, one insertion per piece per round.  tm_add_pieces adds the pieces'
+// counts to their topics; tm_copy_out concatenates the lists of topics in
+// dmask.  Subtrees with fewer than don_min levels below them stay.
+constexpr uint32_t PIECE_SELF = 0xFFFFFFFEu;   // the end of a topic's piece list: its own row
+constexpr uint32_t NO_PIECE = 0xFFFFFFFFu;
+struct DonBufs {
+    uint32_t* prow;     // pcap x K
+    uint4* pdesc;       // topic, next, node, level | levels << 8
+    uint2* pcnt;        // count, spill head
+    uint32_t* tfirst;   // n
+    uint32_t* dmask;    // null: no donation in this batch
+    uint32_t pcap, don_min;
+    uint32_t max_busy;   // donate only while at most this many lanes of the wave still walk
+};
+
+template <bool STATS, bool XCDQ, bool KEYS, int CH>
+__device__ __forceinline__ void
+walk_queue_body(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const uint32_t* __restrict__ twords,
               const uint32_t* __restrict__ words, const uint32_t* __restrict__ meta, uint32_t* __restrict__ gpath,
               uint32_t* __restrict__ stage, uint64_t* __restrict__ kstage, uint32_t K, uint32_t KW,
               uint32_t* __restrict__ counts,
               unsigned long long* __restrict__ ws, unsigned long long* __restrict__ stats,
               unsigned long long* __restrict__ hist, const uint32_t* __restrict__ perm,
               const uint32_t* __restrict__ twords_s, const uint32_t* __restrict__ meta_s,
-              uint32_t* __restrict__ spill, uint32_t* __restrict__ spill_head, uint32_t spill_chunks, uint32_t split) {
+              uint32_t* __restrict__ spill, uint32_t* __restrict__ spill_head, uint32_t spill_chunks, uint32_t split,
+              DonBufs don) {
     static_assert(CH == CH_NONE || (!STATS && !KEYS), "chunk rows: unkeyed walks in arrival order only");
+    constexpr bool DON = CH == CH_DON && TM_PEND_MASK;
+    if (DON) split = 0;
     // queue positions: n topics, or 2n items (option "root_split": chunk-row
     // walks only; position p is item p & 1 of topic p >> 1, stage row,
     // count and spill head by item 2 x topic + part)
@@ -1026,6 +1057,11 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
     const uint32_t home = XCDQ ? xcc_id() : 0u;
     uint32_t qr = 0;                   // ranges given up so far (uniform)
     uint32_t my = NO_TOPIC, myt = 0;   // the lane's queue position and its topic
+    // DON, once dry: the lane's piece (PIECE_SELF: its topic's own row) and
+    // its predecessor in the topic's list, in LDS past the exchange slots
+    // (the chunk rows are free then; no registers held across the walk)
+    uint32_t* const dstate = reinterpret_cast<uint32_t*>(&CR) + 512 + 2 * lane;
+    bool don_init = false, pool_full = false;   // (uniform)
     bool is_long = false, drained = false;
     Cursor cur;
     RowEmit<KEYS> em{nullptr, nullptr, K, 0, {}, 0ull, KW, (uint64_t)n * K};
@@ -1195,14 +1231,97 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
                 qnext = qend;
             }
         }
+        if (DON && exhausted) {
+            // the drain: pair the j-th idle lane with the j-th lane that has
+            // a pending '+' subtree deep enough (uniform block)
+            if (!don_init) {   // every lane's topic is its own row so far
+                dstate[0] = PIECE_SELF;
+                dstate[1] = NO_PIECE;
+                don_init = true;
+                wave_sync_lds();
+            }
+            const uint64_t idle = __ballot(my == NO_TOPIC);
+            const bool tail = 64u - (uint32_t)__popcll(idle) <= don.max_busy;   // the wave's last walkers
+            const uint32_t lim = cur.n > don.don_min ? cur.n - don.don_min : 0u;   // levels k < lim qualify
+            const uint32_t pm = (tail && my != NO_TOPIC && !is_long) ? cur.pend & ((1u << (lim < WREG ? lim : WREG)) - 1u) : 0u;
+            const uint64_t dm = __ballot(pm != 0);
+            if (tail && idle && dm && !pool_full) {
+                const uint32_t ni = (uint32_t)__popcll(idle), nd = (uint32_t)__popcll(dm);
+                uint32_t np = ni < nd ? ni : nd;
+                const uint32_t x = xcc_id(), capx = don.pcap / QRANGES;
+                uint32_t at = 0;
+                if (lane == 0) at = (uint32_t)atomicAdd(ws + QWS_PIECE + 16 * x, (unsigned long long)np);
+                at = __shfl(at, 0, 64);
+                np = at >= capx ? 0u : (np < capx - at ? np : capx - at);
+                pool_full = at + np >= capx;
+                if (np) {
+                    const uint32_t dr = __builtin_amdgcn_mbcnt_hi((uint32_t)(dm >> 32),
+                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)dm, 0u));
+                    const uint32_t ir = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
+                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
+                    // the exchange slots: the chunk's LDS rows (no topic is taken from them once dry)
+                    uint4* xs = reinterpret_cast<uint4*>(&CR);
+                    if (pm && dr < np) {
+                        const uint32_t k = (uint32_t)__builtin_ctz(pm);
+                        const uint32_t p = lp(k);
+                        cur.pend &= ~(1u << k);
+                        const uint32_t y = x * capx + at + dr;
+                        const uint32_t mypid = dstate[0], prv = dstate[1];
+                        don.pdesc[y] = make_uint4(myt, mypid, p, (k + 1) | (cur.n << 8));
+                        if (prv == NO_PIECE) don.tfirst[myt] = y;
+                        else reinterpret_cast<uint32_t*>(don.pdesc + prv)[1] = y;
+                        xs[2 * dr] = make_uint4(y, prv, myt, p);
+                        xs[2 * dr + 1] = make_uint4((k + 1) | (cur.n << 8), 0u, 0u, 0u);
+                        dstate[1] = y;
+                    }
+                    wave_sync_lds();
+                    if (my == NO_TOPIC && ir < np) {   // take piece ir
+                        const uint4 a = xs[2 * ir], b = xs[2 * ir + 1];
+                        dstate[0] = a.x;
+                        dstate[1] = a.y;
+                        myt = a.z;
+                        const uint32_t nl = b.x >> 8;
+                        const uint4* src = reinterpret_cast<const uint4*>(twords + (uint64_t)a.z * WREG);
+#pragma unroll
+                        for (uint32_t k = 0; k < WREG / 4; ++k) {
+                            if (4 * k < nl) {
+                                const uint4 q = src[k];
+                                rw.w[4 * k] = q.x;
+                                rw.w[4 * k + 1] = q.y;
+                                rw.w[4 * k + 2] = q.z;
+                                rw.w[4 * k + 3] = q.w;
+                            }
+                        }
+                        cur.v = a.w;
+                        cur.r = cur.r0 = b.x & 255u;
+                        cur.n = nl;
+                        cur.pend = 0;
+                        cur.key = 0;
+                        cur.pf_id = NODE_NONE;
+                        em.row = don.prow + (uint64_t)a.x * K;
+                        em.cnt = 0;
+                        em.sfail = false;
+                        is_long = false;
+                        my = 0;   // (any position: a piece reads no chunk row)
+                    }
+                    wave_sync_lds();
+                }
+            }
+        }
         if (__all(my == NO_TOPIC && drained)) break;
         if (my == NO_TOPIC) continue;
         const bool fin = is_long ? walk_step<STATS, KEYS>(im, cur, gp, mw, em, st)
                                  : walk_step<STATS, KEYS>(im, cur, lp, rw, em, st);
         if (fin) {
             em.flush();
-            counts[myt] = em.cnt;
-            if (!KEYS && spill && em.cnt > K) spill_head[myt] = em.sfail ? NO_SPILL : em.shead;
+            const uint32_t mypid = DON && don_init ? dstate[0] : PIECE_SELF;
+            if (DON && mypid != PIECE_SELF) {
+                don.pcnt[mypid] = make_uint2(em.cnt, em.cnt > K && spill && !em.sfail ? em.shead : NO_SPILL);
+            } else {
+                counts[myt] = em.cnt;
+                if (!KEYS && spill && em.cnt > K) spill_head[myt] = em.sfail ? NO_SPILL : em.shead;
+                if (DON && don_init && dstate[1] != NO_PIECE) atomicOr(don.dmask + (myt >> 5), 1u << (myt & 31u));
+            }
             match_sum += em.cnt;
             maxc = em.cnt > maxc ? em.cnt : maxc;
             my = NO_TOPIC;
@@ -1220,6 +1339,40 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
     if (lane == 0 && maxl) atomicMax(ws + QWS_MAXL, (unsigned long long)maxl);
     if (TM_WALK_CLOCKS && XCDQ && lane == 0) atomicMax(ws + QWS_CLOCK + 16 * home + 2, (unsigned long long)wall_clock64());
     wave_stats_add<STATS>(stats, lev_sum, match_sum, st);
+}
+
+template <bool STATS, bool XCDQ, bool KEYS, int CH = CH_NONE>
+__global__ void __launch_bounds__(BLOCK) TM_WALK_ATTR
+tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const uint32_t* __restrict__ twords,
+              const uint32_t* __restrict__ words, const uint32_t* __restrict__ meta, uint32_t* __restrict__ gpath,
+              uint32_t* __restrict__ stage, uint64_t* __restrict__ kstage, uint32_t K, uint32_t KW,
+              uint32_t* __restrict__ counts,
+              unsigned long long* __restrict__ ws, unsigned long long* __restrict__ stats,
+              unsigned long long* __restrict__ hist, const uint32_t* __restrict__ perm,
+              const uint32_t* __restrict__ twords_s, const uint32_t* __restrict__ meta_s,
+              uint32_t* __restrict__ spill, uint32_t* __restrict__ spill_head, uint32_t spill_chunks, uint32_t split,
+              DonBufs don) {
+    walk_queue_body<STATS, XCDQ, KEYS, CH>(im, off, n, twords, words, meta, gpath, stage, kstage, K, KW, counts, ws, stats, hist, perm, twords_s, meta_s,
+                                     spill, spill_head, spill_chunks, split, don);
+}
+// option "donate": its own kernel, held to the chunk-row walk's 6 waves per
+// SIMD (the drain's donation code would otherwise cost a wave: 84 VGPRs)
+#ifndef TM_DON_WAVES
+#define TM_DON_WAVES 6
+#endif
+template <bool XCDQ>
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(TM_DON_WAVES, 8)))
+tm_walk_queue_don(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const uint32_t* __restrict__ twords,
+              const uint32_t* __restrict__ words, const uint32_t* __restrict__ meta, uint32_t* __restrict__ gpath,
+              uint32_t* __restrict__ stage, uint64_t* __restrict__ kstage, uint32_t K, uint32_t KW,
+              uint32_t* __restrict__ counts,
+              unsigned long long* __restrict__ ws, unsigned long long* __restrict__ stats,
+              unsigned long long* __restrict__ hist, const uint32_t* __restrict__ perm,
+              const uint32_t* __restrict__ twords_s, const uint32_t* __restrict__ meta_s,
+              uint32_t* __restrict__ spill, uint32_t* __restrict__ spill_head, uint32_t spill_chunks, uint32_t split,
+              DonBufs don) {
+    walk_queue_body<false, XCDQ, false, CH_DON>(im, off, n, twords, words, meta, gpath, stage, kstage, K, KW, counts, ws, stats, hist, perm, twords_s, meta_s,
+                                     spill, spill_head, spill_chunks, split, don);
 }
 
 // ---------------------------------------------------------------------------
@@ -1529,29 +1682,37 @@ constexpr uint32_t COPY_U = TM_COPY_U;
 // is its filter's order key im.fshape[id] (image.h filter_shape), and a
 // topic with a literal '+' / '#' level (MOOD: its walk repeats subtrees, so
 // keys by filter would tie) is re-walked keyed here, all of its outputs.
-template <bool KEYS, bool SHAPED>
+template <bool KEYS, bool SHAPED, bool DONP = false>
 __global__ void __launch_bounds__(BLOCK)
 tm_copy_out(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const uint32_t* __restrict__ twords,
             const uint32_t* __restrict__ words, const uint32_t* __restrict__ meta, uint32_t* __restrict__ gpath,
             const uint32_t* __restrict__ stage, const uint64_t* __restrict__ kstage, uint32_t K, uint32_t KW,
             const uint32_t* __restrict__ counts, const uint64_t* __restrict__ out_off, uint32_t* __restrict__ out,
             uint64_t* __restrict__ kout, uint64_t out_cap, const uint32_t* __restrict__ spill,
-            const uint32_t* __restrict__ spill_head, uint32_t split) {
+            const uint32_t* __restrict__ spill_head, uint32_t split, DonBufs don) {
     // split (option "root_split", unkeyed): n counts 2x the topics' items;
     // item x is part x & 1 of topic x >> 1 (its rows, words and path area)
+    // don.dmask (option "donate", unkeyed): topics whose list is pieces, in
+    // the loop at the end
     const uint64_t kplane = (uint64_t)n * K;   // KEYS: key word j of stage slot x at kstage[j * kplane + x],
                                                // of output p at kout[j * out_cap + p]
     __shared__ uint32_t lds_inc[BLOCK];
     __shared__ uint64_t lds_scan[BLOCK / 64];
+    __shared__ uint32_t lds_don[DONP ? BLOCK / 32 : 1];
     const uint32_t t0 = blockIdx.x * BLOCK;
     const uint32_t tn = n - t0 < (uint32_t)BLOCK ? n - t0 : (uint32_t)BLOCK;
     const uint32_t c = threadIdx.x < tn ? counts[t0 + threadIdx.x] : 0u;
+    const bool donb = DONP && !KEYS && !SHAPED && don.dmask != nullptr;
+    if (DONP && donb && threadIdx.x < BLOCK / 32)   // (t0 is a multiple of 32)
+        lds_don[threadIdx.x] = t0 + 32 * threadIdx.x < n ? don.dmask[(t0 >> 5) + threadIdx.x] : 0u;
     uint64_t agg;
     const uint64_t ex = block_exclusive_scan(c, lds_scan, agg);
     lds_inc[threadIdx.x] = (uint32_t)(ex + c);
     __syncthreads();
     const uint64_t base = out_off[t0];
-    auto ood = [&](uint32_t lt) { return SHAPED && (meta[t0 + lt] & MOOD) != 0; };
+    auto pieces = [&](uint32_t lt) { return donb && ((lds_don[lt >> 5] >> (lt & 31u)) & 1u) != 0; };
+    // topics copied by the loops below: not out-of-domain (SHAPED) and not in pieces
+    auto ood = [&](uint32_t lt) { return (SHAPED && (meta[t0 + lt] & MOOD) != 0) || pieces(lt); };
     auto put = [&](uint64_t p, uint32_t id) {
         if (TM_COPY_NT) __builtin_nontemporal_store(id, out + p);
         else out[p] = id;
@@ -1687,7 +1848,7 @@ tm_copy_out(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const ui
         }
     }
     const bool tail = c > K && (KEYS || !spill || spill_head[t0 + threadIdx.x] == NO_SPILL);
-    if (threadIdx.x < tn && (tail || ood(threadIdx.x))) {
+    if (threadIdx.x < tn && !pieces(threadIdx.x) && (tail || ood(threadIdx.x))) {
         // fan-out beyond the stage row and no spill: walk again, write the
         // head; SHAPED: keyed, and every output of an out-of-domain topic
         const uint32_t x = t0 + threadIdx.x, t = x >> split;   // item, topic
@@ -1711,6 +1872,77 @@ tm_copy_out(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const ui
             walk<false, WK>(im, mt & MN, (mt & MDOLLAR) != 0, GlobalPath{gpath + b + 2ull * t}, mw, em, s2);
         }
     }
+    if (DONP && donb) {
+        // topics whose list is pieces (option "donate"), one wave per topic:
+        // the pieces in list order, then the topic's own row; a part past K
+        // ids without a spill chain re-walks the whole topic (lane 0, every
+        // output)
+        const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+        auto copy_part = [&](const uint32_t* row, uint32_t pc, uint32_t sh, uint64_t o) {
+            for (uint32_t j = (pc > K ? pc - K : 0u) + lane; j < pc; j += 64)
+                if (o + j < out_cap) put(o + j, row[K + j - pc]);
+            if (pc > K) {   // the head from the spill chain (reverse discovery order)
+                uint32_t cur = sh;
+                const uint32_t m = pc - K;
+                for (uint32_t o0 = 0; o0 < m; o0 += SPILL_CHUNK - 1) {
+                    for (uint32_t j = lane; j < SPILL_CHUNK - 1 && o0 + j < m; j += 64) {
+                        const uint64_t p = o + m - 1 - (o0 + j);
+                        if (p < out_cap) put(p, spill[(uint64_t)cur * SPILL_CHUNK + 1 + j]);
+                    }
+                    if (o0 + SPILL_CHUNK - 1 < m) cur = spill[(uint64_t)cur * SPILL_CHUNK];
+                }
+            }
+        };
+        for (uint32_t lt = w; lt < tn; lt += BLOCK / 64) {
+            if (!pieces(lt)) continue;
+            const uint32_t t = t0 + lt;
+            const uint32_t prev = lt ? lds_inc[lt - 1] : 0u;
+            const uint32_t ct = lds_inc[lt] - prev;
+            const uint64_t ob = base + prev;
+            uint32_t sum = 0;
+            bool rew = false;
+            for (uint32_t y = don.tfirst[t]; y != PIECE_SELF; y = don.pdesc[y].y) {
+                const uint2 pc = don.pcnt[y];
+                sum += pc.x;
+                rew |= pc.x > K && pc.y == NO_SPILL;
+            }
+            const uint32_t own = ct - sum;
+            rew |= own > K && (!spill || spill_head[t] == NO_SPILL);
+            if (rew) {
+                if (lane == 0) {
+                    const uint32_t mt = meta[t];
+                    const uint64_t b = off[t] - off[0];
+                    const MemWords mw{twords + (uint64_t)t * WREG, words + b + t};
+                    TailEmit<false> em{out, kout, ob, out_cap, 0u, ct, 0, KW, out_cap};
+                    WalkStats s2;
+                    walk<false, false>(im, mt & MN, (mt & MDOLLAR) != 0, GlobalPath{gpath + b + 2ull * t}, mw, em, s2);
+                }
+                continue;
+            }
+            uint64_t o = ob;
+            for (uint32_t y = don.tfirst[t];; y = don.pdesc[y].y) {
+                const bool self = y == PIECE_SELF;
+                uint2 pc = make_uint2(own, own > K ? spill_head[t] : NO_SPILL);
+                if (!self) pc = don.pcnt[y];
+                copy_part(self ? stage + (uint64_t)t * K : don.prow + (uint64_t)y * K, pc.x, pc.y, o);
+                o += pc.x;
+                if (self) break;
+            }
+        }
+    }
+}
+
+// option "donate": each donated piece's count onto its topic's (the pieces
+// of XCD x are pdesc[x * pcap / 8 + i], i < the XCD's counter)
+__global__ void __launch_bounds__(BLOCK)
+tm_add_pieces(const unsigned long long* __restrict__ ws, const uint4* __restrict__ pdesc,
+              const uint2* __restrict__ pcnt, uint32_t pcap, uint32_t* __restrict__ counts) {
+    const uint32_t p = blockIdx.x * BLOCK + threadIdx.x;
+    const uint32_t capx = pcap / QRANGES;
+    if (p >= pcap) return;
+    const uint32_t x = p / capx, i = p - x * capx;
+    const unsigned long long taken = ws[QWS_PIECE + 16 * x];
+    if (i < taken) atomicAdd(counts + pdesc[p].x, pcnt[p].x);
 }
 
 // tm_copy_out over a presorted walk (option "presort"): stage row p holds
@@ -1957,10 +2189,20 @@ hipError_t launch_small(const ImageView& im, const uint8_t* bytes, const uint64_
 // tm_copy_out alone, over the stage rows, counts and offsets a finished
 // launch_queue left in qb (same n, K, key_words): the ids into a larger
 // output after the first one overflowed, without walking again
+static DonBufs don_bufs(const QueueBufs& qb) {
+    if (!qb.donate) return DonBufs{nullptr, nullptr, nullptr, nullptr, nullptr, 0u, 0u, 0u};
+    return DonBufs{qb.prow, reinterpret_cast<uint4*>(qb.pdesc), reinterpret_cast<uint2*>(qb.pcnt), qb.tfirst, qb.dmask,
+                   qb.pcap, qb.don_min, qb.don_busy};
+}
+
 hipError_t launch_copy(const ImageView& im, const uint8_t* bytes, const uint64_t* off, uint32_t n, const QueueBufs& qb,
                        uint32_t K, uint32_t key_words, const uint32_t* counts, const uint64_t* out_off, uint32_t* out,
                        uint64_t* out_keys, uint64_t out_cap, hipStream_t st) {
     if (n == 0 || out_cap == 0) return hipSuccess;
+    // option "donate": the batch's piece lists (unkeyed, not presorted by position)
+    if (qb.donate && (qb.kstage || qb.shaped || qb.root_split || !qb.dmask || !qb.tfirst)) return hipErrorInvalidValue;
+    const DonBufs db = don_bufs(qb);
+    const DonBufs none{nullptr, nullptr, nullptr, nullptr, nullptr, 0u, 0u, 0u};
     // option "root_split": the 2n items' rows, counts and offsets (counts /
     // out_off here are the topics', folded from them)
     const bool split = qb.root_split && !qb.kstage && !qb.shaped;
@@ -1972,6 +2214,7 @@ hipError_t launch_copy(const ImageView& im, const uint8_t* bytes, const uint64_t
     const uint32_t nq = split ? 2 * n : n;
     dim3 blk(BLOCK), g(div_up(nq, BLOCK));
     if (qb.perm && !split) {   // a presorted walk: stage row p is topic perm[p]
+        if (qb.donate) return hipErrorInvalidValue;
         if (qb.kstage)
             hipLaunchKernelGGL(tm_copy_out_sorted<true>, g, blk, 0, st, im, off, n, qb.twords, qb.words, qb.meta,
                                qb.path, qb.stage, qb.kstage, K, key_words, counts, out_off, out, out_keys, out_cap,
@@ -1982,16 +2225,20 @@ hipError_t launch_copy(const ImageView& im, const uint8_t* bytes, const uint64_t
     } else if (qb.kstage) {
         hipLaunchKernelGGL((tm_copy_out<true, false>), g, blk, 0, st, im, off, n, qb.twords, qb.words, qb.meta,
                            qb.path, qb.stage, qb.kstage, K, key_words, counts, out_off, out, out_keys, out_cap,
-                           nullptr, nullptr, 0u);
+                           nullptr, nullptr, 0u, none);
     } else if (qb.shaped) {
         if (!out_keys || key_words != 1 || !im.fshape) return hipErrorInvalidValue;
         hipLaunchKernelGGL((tm_copy_out<false, true>), g, blk, 0, st, im, off, n, qb.twords, qb.words, qb.meta,
                            qb.path, qb.stage, nullptr, K, 1u, counts, out_off, out, out_keys, out_cap,
-                           qb.spill_chunks >= QRANGES ? qb.spill : nullptr, qb.spill_head, 0u);
+                           qb.spill_chunks >= QRANGES ? qb.spill : nullptr, qb.spill_head, 0u, none);
+    } else if (db.dmask) {
+        hipLaunchKernelGGL((tm_copy_out<false, false, true>), g, blk, 0, st, im, off, nq, qb.twords, qb.words, qb.meta,
+                           qb.path, qb.stage, nullptr, K, 1u, counts, out_off, out, nullptr, out_cap,
+                           qb.spill_chunks >= QRANGES ? qb.spill : nullptr, qb.spill_head, split ? 1u : 0u, db);
     } else {
         hipLaunchKernelGGL((tm_copy_out<false, false>), g, blk, 0, st, im, off, nq, qb.twords, qb.words, qb.meta,
                            qb.path, qb.stage, nullptr, K, 1u, counts, out_off, out, nullptr, out_cap,
-                           qb.spill_chunks >= QRANGES ? qb.spill : nullptr, qb.spill_head, split ? 1u : 0u);
+                           qb.spill_chunks >= QRANGES ? qb.spill : nullptr, qb.spill_head, split ? 1u : 0u, none);
     }
     return hipGetLastError();
 }
@@ -2051,6 +2298,7 @@ hipError_t launch_queue(bool stats_mode, bool xcdq, const ImageView& im, const u
         if (out_cap) {
             QueueBufs qc = qb;
             qc.root_split = false;
+            qc.donate = false;
             err = launch_copy(im, bytes, off, n, qc, K, key_words, counts, out_off, out, out_keys, out_cap, st);
             if (err != hipSuccess) return err;
         }
@@ -2060,12 +2308,24 @@ hipError_t launch_queue(bool stats_mode, bool xcdq, const ImageView& im, const u
     // option "root_split": 2n queue items (chunk rows only), their counts and
     // offsets in qb.icounts / qb.ioff, folded into the topics' after the copy
     // (a batch walked otherwise ignores it)
-    const bool split = qb.root_split && ch == CH_ROWS;
+    const bool split = qb.root_split && ch == CH_ROWS && !qb.donate;
     if (split && (!qb.icounts || !qb.ioff || n > (1u << 30))) return hipErrorInvalidValue;
+    // option "donate": chunk-row walks (a batch walked otherwise ignores it)
+    const bool donate = qb.donate && ch == CH_ROWS;
+    if (donate && (!qb.prow || !qb.pdesc || !qb.pcnt || !qb.tfirst || !qb.dmask || qb.pcap < QRANGES ||
+                   (qb.pcap % QRANGES) != 0))
+        return hipErrorInvalidValue;
+    const DonBufs db = donate ? don_bufs(qb) : DonBufs{nullptr, nullptr, nullptr, nullptr, nullptr, 0u, 0u, 0u};
+    if (donate) {
+        err = hipMemsetAsync(qb.dmask, 0, ((size_t)(n >> 5) + 1) * 4, st);
+        if (err != hipSuccess) return err;
+    }
     uint32_t* const wcounts = split ? qb.icounts : counts;
     // spill chunks: unkeyed walks in arrival order (presorted rows re-walk)
     uint32_t* const spill = (!keys && !by_pos && qb.spill_chunks >= QRANGES) ? qb.spill : nullptr;
-    const uint32_t wg = ch == CH_ROWS ? resident_grid(tm_walk_queue<false, true, false, CH_ROWS>, div_up(n << split, 64),
+    const uint32_t wg = donate         ? resident_grid(tm_walk_queue_don<true>, div_up(n, 64),
+                                                      walk_blocks_per_cu)
+                        : ch == CH_ROWS ? resident_grid(tm_walk_queue<false, true, false, CH_ROWS>, div_up(n << split, 64),
                                                       walk_blocks_per_cu)
                                       : resident_grid(tm_walk_queue<false, false, false>, div_up(n << split, 64),
                                                       walk_blocks_per_cu);
@@ -2073,8 +2333,17 @@ hipError_t launch_queue(bool stats_mode, bool xcdq, const ImageView& im, const u
     hipLaunchKernelGGL((tm_walk_queue<S, X, Y, C>), dim3(wg), blk, 0, st, im, off, n, qb.twords, qb.words,       \
                        qb.meta, qb.path, qb.stage, qb.kstage, K, key_words, wcounts, qb.ws, stats,               \
                        hist ? stats + HIST_OFF : nullptr, qb.perm, qb.twords_s, qb.meta_s, spill, qb.spill_head,   \
-                       qb.spill_chunks, split ? 1u : 0u)
-    if (ch == CH_ROWS) {
+                       qb.spill_chunks, split ? 1u : 0u, db)
+    if (donate) {
+        if (xcdq)
+            hipLaunchKernelGGL((tm_walk_queue_don<true>), dim3(wg), blk, 0, st, im, off, n, qb.twords, qb.words, qb.meta,
+                               qb.path, qb.stage, qb.kstage, K, key_words, wcounts, qb.ws, stats, nullptr, qb.perm,
+                               qb.twords_s, qb.meta_s, spill, qb.spill_head, qb.spill_chunks, 0u, db);
+        else
+            hipLaunchKernelGGL((tm_walk_queue_don<false>), dim3(wg), blk, 0, st, im, off, n, qb.twords, qb.words, qb.meta,
+                               qb.path, qb.stage, qb.kstage, K, key_words, wcounts, qb.ws, stats, nullptr, qb.perm,
+                               qb.twords_s, qb.meta_s, spill, qb.spill_head, qb.spill_chunks, 0u, db);
+    } else if (ch == CH_ROWS) {
         if (xcdq) TM_Q(false, true, false, CH_ROWS); else TM_Q(false, false, false, CH_ROWS);
     } else if (keys) {
         if (stats_mode) TM_Q(true, true, true, CH_NONE); else TM_Q(false, true, true, CH_NONE);
@@ -2084,6 +2353,10 @@ hipError_t launch_queue(bool stats_mode, bool xcdq, const ImageView& im, const u
         if (xcdq) TM_Q(false, true, false, CH_NONE); else TM_Q(false, false, false, CH_NONE);
     }
 #undef TM_Q
+    if (donate)
+        hipLaunchKernelGGL(tm_add_pieces, dim3(div_up(qb.pcap, BLOCK)), blk, 0, st, qb.ws,
+                           reinterpret_cast<const uint4*>(qb.pdesc), reinterpret_cast<const uint2*>(qb.pcnt), qb.pcap,
+                           counts);
     mark(3);
     mark(4);
     if (split) {
@@ -2107,6 +2380,7 @@ hipError_t launch_queue(bool stats_mode, bool xcdq, const ImageView& im, const u
     if (out_cap) {
         QueueBufs qc = qb;
         qc.root_split = false;
+        qc.donate = donate;
         if (!by_pos) qc.perm = nullptr;   // stage rows by topic
         err = launch_copy(im, bytes, off, n, qc, K, key_words, counts, out_off, out, out_keys, out_cap, st);
         if (err != hipSuccess) return err;
