@@ -4279,8 +4279,8 @@ int tm_set_option(tm_engine* e, const char* name, int64_t value) {
             e->don_min = (uint32_t)value;
             return TM_OK;
         }
-        if (!std::strcmp(name, "donate_busy")) {
-            if (value < 1 || value > 64) return TM_EINVAL;
+        if (!std::strcmp(name, "donate_busy")) {   // (0: the donating walk kernel, nothing donated)
+            if (value < 0 || value > 64) return TM_EINVAL;
             e->don_busy = (uint32_t)value;
             return TM_OK;
         }

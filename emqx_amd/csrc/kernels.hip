@@ -1261,27 +1261,25 @@ walk_queue_body(ImageView im, const uint64_t* __restrict__ off, uint32_t n, cons
                                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
                     // the exchange slots: the chunk's LDS rows (no topic is taken from them once dry)
                     uint4* xs = reinterpret_cast<uint4*>(&CR);
-                    if (pm && dr < np) {
+                    if (pm && dr < np) {   // the donor: its subtree to slot dr (the piece's records: its donee)
                         const uint32_t k = (uint32_t)__builtin_ctz(pm);
-                        const uint32_t p = lp(k);
+                        xs[dr] = make_uint4(myt, lp(k), (k + 1) | (cur.n << 8) | (lane << 16), 0u);
                         cur.pend &= ~(1u << k);
-                        const uint32_t y = x * capx + at + dr;
-                        const uint32_t mypid = dstate[0], prv = dstate[1];
-                        don.pdesc[y] = make_uint4(myt, mypid, p, (k + 1) | (cur.n << 8));
-                        if (prv == NO_PIECE) don.tfirst[myt] = y;
-                        else reinterpret_cast<uint32_t*>(don.pdesc + prv)[1] = y;
-                        xs[2 * dr] = make_uint4(y, prv, myt, p);
-                        xs[2 * dr + 1] = make_uint4((k + 1) | (cur.n << 8), 0u, 0u, 0u);
-                        dstate[1] = y;
                     }
                     wave_sync_lds();
-                    if (my == NO_TOPIC && ir < np) {   // take piece ir
-                        const uint4 a = xs[2 * ir], b = xs[2 * ir + 1];
-                        dstate[0] = a.x;
-                        dstate[1] = a.y;
-                        myt = a.z;
-                        const uint32_t nl = b.x >> 8;
-                        const uint4* src = reinterpret_cast<const uint4*>(twords + (uint64_t)a.z * WREG);
+                    if (my == NO_TOPIC && ir < np) {   // take piece y = ir: insert it before its donor's
+                        const uint4 a = xs[ir];
+                        uint32_t* const ds = reinterpret_cast<uint32_t*>(&CR) + 512 + 2 * (a.z >> 16);
+                        const uint32_t y = x * capx + at + ir, prv = ds[1];
+                        don.pdesc[y] = make_uint4(a.x, ds[0], a.y, a.z & 0xFFFFu);
+                        if (prv == NO_PIECE) don.tfirst[a.x] = y;
+                        else reinterpret_cast<uint32_t*>(don.pdesc + prv)[1] = y;
+                        ds[1] = y;
+                        dstate[0] = y;
+                        dstate[1] = prv;
+                        myt = a.x;
+                        const uint32_t nl = (a.z >> 8) & 255u;
+                        const uint4* src = reinterpret_cast<const uint4*>(twords + (uint64_t)a.x * WREG);
 #pragma unroll
                         for (uint32_t k = 0; k < WREG / 4; ++k) {
                             if (4 * k < nl) {
@@ -1292,13 +1290,13 @@ walk_queue_body(ImageView im, const uint64_t* __restrict__ off, uint32_t n, cons
                                 rw.w[4 * k + 3] = q.w;
                             }
                         }
-                        cur.v = a.w;
-                        cur.r = cur.r0 = b.x & 255u;
+                        cur.v = a.y;
+                        cur.r = cur.r0 = a.z & 255u;
                         cur.n = nl;
                         cur.pend = 0;
                         cur.key = 0;
                         cur.pf_id = NODE_NONE;
-                        em.row = don.prow + (uint64_t)a.x * K;
+                        em.row = don.prow + (uint64_t)y * K;
                         em.cnt = 0;
                         em.sfail = false;
                         is_long = false;
