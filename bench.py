@@ -91,6 +91,9 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=1_500_000, help="topics timed on the host (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=None)
     ap.add_argument("--check", type=int, default=20_000, help="topics of each batch checked bit-exactly vs O1")
+    ap.add_argument("--stream-kind", choices=["pool", "prio"], default="prio",
+                    help="lane streams: high priority (default: a hardware queue each) or torch's pool (normal "
+                         "priority: two of three lanes shared a queue, profiles/r05_u)")
     ap.add_argument("--streams", type=int, default=3,
                     help="streams the steps alternate over (batches overlap on the GPU; 1 = strictly serial)")
     ap.add_argument("--roof-steps", type=int, default=20,
@@ -407,7 +410,7 @@ def main():
     batches = make_batches(a, cfg, rank, world)
     log("rank %d: %d batches of %d topics generated in %.1fs" % (rank, len(batches), len(batches[0][1]) - 1,
                                                                  time.time() - t0))
-    reg = Region(eng, dev, batches, a.streams, stats=True, hist=a.hist)
+    reg = Region(eng, dev, batches, a.streams, stats=True, hist=a.hist, kind=a.stream_kind)
     stats, fanout = reg.stats, reg.fanout
     log("fan-out per topic: %s" % fanout)
     reg.warm(a.warmup)
@@ -576,9 +579,10 @@ class Region:
     distinct batches.  Outputs are sized by one untimed counting pass per
     batch (exact stats of batch 0 when `stats`)."""
 
-    def __init__(self, eng, dev, batches, streams, stats=False, hist=False):
+    def __init__(self, eng, dev, batches, streams, stats=False, hist=False, kind="pool"):
         self.eng, self.dev = eng, dev
-        self.st = torch.cuda.Stream(device=dev)   # explicit (handle 0 would select the engine's own stream)
+        self.kind = kind
+        self.st = self._stream()   # explicit (handle 0 would select the engine's own stream)
         self.dbat = []
         for tb, to in batches:
             n = len(to) - 1
@@ -613,13 +617,23 @@ class Region:
         nmax = max(x[2] for x in self.dbat)
         self.lanes = []
         for k in range(streams):
-            s_ = self.st if k == 0 else torch.cuda.Stream(device=dev)
+            s_ = self.st if k == 0 else self._stream()
             self.lanes.append((s_, torch.empty(nmax, dtype=torch.int32, device=dev),
                                torch.empty(nmax + 1, dtype=torch.int64, device=dev),
                                torch.empty(self.cap, dtype=torch.int32, device=dev),
                                torch.zeros(1, dtype=torch.int64, device=dev)))
         self.k = 0
         self.last = {}
+
+    def _stream(self):
+        """a lane's stream.  Each stream is fed to one hardware queue (4 per
+        process for normal priority, GPU_MAX_HW_QUEUES): two lanes on one
+        queue run in submission order, so a batch's tokenizer waits behind
+        another lane's copy-out; high-priority streams come from a queue set
+        of their own (tools/stream_queues.py, profiles/r05_t)"""
+        if self.kind == "prio":
+            return torch.cuda.Stream(device=self.dev, priority=-1)
+        return torch.cuda.Stream(device=self.dev)
 
     def step(self):
         j = self.k

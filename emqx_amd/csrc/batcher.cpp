@@ -697,8 +697,14 @@ int tm_batcher_open(tm_engine* e, const tm_batcher_config* cfg, tm_batcher** out
             return TM_ENOMEM;
         }
         L->device = devs[k % devs.size()];
+        // high priority: a queue set of its own, so the lanes do not share a
+        // hardware queue with each other or the engine's streams (two lanes
+        // on one queue run in submission order: a batch's tokenizer behind
+        // the other lane's copy-out; bench.py --stream-kind, profiles/r05_u)
+        int least = 0, greatest = 0;
         if (L->device >= 0 && (hipSetDevice(L->device) != hipSuccess ||
-                               hipStreamCreateWithFlags(&L->stream, hipStreamNonBlocking) != hipSuccess)) {
+                               hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess ||
+                               hipStreamCreateWithPriority(&L->stream, hipStreamNonBlocking, greatest) != hipSuccess)) {
             b->shutdown_lanes();
             delete b;
             return TM_EDEVICE;

@@ -286,6 +286,13 @@ __device__ __forceinline__ uint32_t presort_key(const uint32_t (&tw)[WREG], uint
 // so the lanes that finish last are the ones on light topics.  Key: the
 // range (3 bits) over 31 - the summed heat of the first eight levels / 4
 // (5 bits), one radix pass (presort.hip).
+// the walk's XCD range of queue position t: [n r / 8, n (r+1) / 8)
+__device__ __forceinline__ uint32_t range_of(uint32_t t, uint32_t n) {
+    uint32_t r = (uint32_t)(((uint64_t)t * 8) / n);
+    while (r > 0 && (uint64_t)n * r / 8 > t) --r;
+    while (r < 7 && (uint64_t)n * (r + 1) / 8 <= t) ++r;
+    return r;
+}
 __device__ __forceinline__ uint32_t tail_key(const ImageView& im, const uint32_t (&tw)[WREG], uint32_t lev,
                                              uint32_t t, uint32_t n) {
     uint32_t cost = 0;
@@ -294,11 +301,8 @@ __device__ __forceinline__ uint32_t tail_key(const ImageView& im, const uint32_t
         const uint32_t w = tw[l];
         if (l < lev && w < im.n_words) cost += im.word_heat[w];
     }
-    uint32_t r = (uint32_t)(((uint64_t)t * 8) / n);   // range r = [n r / 8, n (r+1) / 8)
-    while (r > 0 && (uint64_t)n * r / 8 > t) --r;
-    while (r < 7 && (uint64_t)n * (r + 1) / 8 <= t) ++r;
     const uint32_t c = cost >> 2 < 31 ? cost >> 2 : 31u;
-    return (r << 5) | (31u - c);
+    return (range_of(t, n) << 5) | (31u - c);
 }
 
 template <class B>
@@ -340,7 +344,7 @@ __device__ __forceinline__ uint32_t tokenize_one(const ImageView& im, const B& b
         }
         skeys[t] = mode == 2   ? tail_key(im, tw, lev, t, n)
                    : mode == 4 ? tail_key(im, tw, lev, t, n) << 8 | presort_key(tw, lev) >> 24
-                   : mode == 5 ? (tail_key(im, tw, lev, t, n) >> 5) << (bits - 3) | presort_key(tw, lev) >> (35 - bits)
+                   : mode == 5 ? range_of(t, n) << (bits - 3) | presort_key(tw, lev) >> (35 - bits)   // (no heat)
                                : presort_key(tw, lev);
         svals[t] = t;
     }
