@@ -103,21 +103,17 @@ __device__ __forceinline__ uint64_t load_chunk(const B& bytes, uint64_t p, uint3
 // Split in two so the tokenizer can issue a level's slot load (dict_begin),
 // scan and hash the next level while it is in flight, then resolve it
 // (dict_end: byte-verify, probe on).
-struct DictProbe {
-    uint64_t p, s;
-    uint32_t tag, len, atom;   // atom: WORD_PLUS / WORD_HASH, or 0 (a dictionary word)
-    uint4 d0;             // the home slot's first half: tag, word, bytes 0-7
+struct DictProbe {         // 8 VGPRs: the tokenizer holds TM_TOK_DEPTH + 1 of them
+    uint32_t rel, s;          // the word's offset in its topic; the home slot
+    uint32_t tag, len;
+    uint4 d0;                 // the home slot's first half: tag, word, bytes 0-7
 };
 template <class B>
-__device__ __forceinline__ DictProbe dict_begin(const ImageView& im, const B& bytes, uint64_t p, uint32_t len) {
+__device__ __forceinline__ DictProbe dict_begin(const ImageView& im, const B& bytes, uint64_t b, uint64_t p,
+                                                uint32_t len) {
     DictProbe q;
-    q.p = p;
+    q.rel = (uint32_t)(p - b);
     q.len = len;
-    q.atom = 0;
-    if (len == 1) {
-        const uint32_t c = bytes.byte(p);
-        q.atom = c == '+' ? WORD_PLUS : c == '#' ? WORD_HASH : 0u;
-    }
     uint64_t h = 0x243F6A8885A308D3ULL;
     for (uint32_t i = 0; i < len; i += 8) {
         uint32_t k = len - i < 8 ? len - i : 8;
@@ -125,7 +121,7 @@ __device__ __forceinline__ DictProbe dict_begin(const ImageView& im, const B& by
     }
     h = word_hash_final(h, len);
     q.tag = dict_tag(h, len);
-    q.s = h & im.dict_slot_mask;
+    q.s = (uint32_t)(h & im.dict_slot_mask);
     q.d0 = reinterpret_cast<const uint4*>(im.dict + q.s)[0];
     return q;
 }
@@ -133,10 +129,14 @@ __device__ __forceinline__ DictProbe dict_begin(const ImageView& im, const B& by
 // bytes); 9-16 bytes also read the second half (same 32 B), longer words the
 // zero-padded arena
 template <class B>
-__device__ __forceinline__ uint32_t dict_end(const ImageView& im, const B& bytes, DictProbe q) {
-    if (q.atom) return q.atom;
-    const uint64_t p = q.p;
+__device__ __forceinline__ uint32_t dict_end(const ImageView& im, const B& bytes, uint64_t b, DictProbe q) {
+    const uint64_t p = b + q.rel;
     const uint32_t len = q.len;
+    if (len == 1) {   // the atoms '+' / '#'
+        const uint32_t c = bytes.byte(p);
+        if (c == '+') return WORD_PLUS;
+        if (c == '#') return WORD_HASH;
+    }
     const uint32_t tag = q.tag;
     uint64_t s = q.s;
     uint4 d0 = q.d0;
@@ -211,10 +211,14 @@ __device__ __forceinline__ uint64_t next_slash(const B& bytes, uint64_t q, uint6
 // emqx_topic:words/1 of topic [b, e): word id of level k to tw[k] (k < WREG,
 // registers: AND-mask updates, no dynamic index) or lw[k] (k >= WREG);
 // returns the number of levels (N slashes -> N+1 levels, empty levels kept).
-// Software-pipelined by one level: level k+1 is scanned, hashed and its
-// dictionary slot requested before level k's slot is resolved.
+// Software-pipelined by TM_TOK_DEPTH levels: levels k+1 .. k+D are scanned,
+// hashed and their dictionary slots requested before level k's slot is
+// resolved.
 #ifndef TM_TOK_LEAN
 #define TM_TOK_LEAN 0   // A/B builds: tokenizer without LDS staging or pipelining (fewer registers, no LDS)
+#endif
+#ifndef TM_TOK_DEPTH
+#define TM_TOK_DEPTH 2
 #endif
 template <class B>
 __device__ __forceinline__ uint32_t tokenize_topic(const ImageView& im, const B& bytes, uint64_t b, uint64_t e,
@@ -226,7 +230,7 @@ __device__ __forceinline__ uint32_t tokenize_topic(const ImageView& im, const B&
         uint64_t s = b;
         for (;;) {
             const uint64_t q = next_slash(bytes, s, e, found);
-            const uint32_t w = dict_end(im, bytes, dict_begin(im, bytes, s, (uint32_t)(q - s)));
+            const uint32_t w = dict_end(im, bytes, b, dict_begin(im, bytes, b, s, (uint32_t)(q - s)));
             ood |= w == WORD_PLUS || w == WORD_HASH;
             if (lev < WREG) {
 #pragma unroll
@@ -239,17 +243,7 @@ __device__ __forceinline__ uint32_t tokenize_topic(const ImageView& im, const B&
             s = q + 1;
         }
     }
-    uint64_t q = next_slash(bytes, b, e, found);
-    DictProbe cur = dict_begin(im, bytes, b, (uint32_t)(q - b));
-    for (;;) {
-        const bool more = found;
-        DictProbe nxt;
-        if (more) {
-            const uint64_t s = q + 1;
-            q = next_slash(bytes, s, e, found);
-            nxt = dict_begin(im, bytes, s, (uint32_t)(q - s));
-        }
-        const uint32_t w = dict_end(im, bytes, cur);
+    auto put = [&](uint32_t w) {
         ood |= w == WORD_PLUS || w == WORD_HASH;
         if (lev < WREG) {
 #pragma unroll
@@ -258,6 +252,45 @@ __device__ __forceinline__ uint32_t tokenize_topic(const ImageView& im, const B&
             lw[lev] = w;
         }
         ++lev;
+    };
+    uint64_t q = next_slash(bytes, b, e, found);
+    DictProbe cur = dict_begin(im, bytes, b, b, (uint32_t)(q - b));
+    if (TM_TOK_DEPTH >= 2) {
+        // two levels ahead: c1 (level lev + 1, valid if v1) and the next
+        // (lev + 2) are in flight while level lev resolves
+        DictProbe c1;
+        bool v1 = false;
+        if (found) {
+            const uint64_t s = q + 1;
+            q = next_slash(bytes, s, e, found);
+            c1 = dict_begin(im, bytes, b, s, (uint32_t)(q - s));
+            v1 = true;
+        }
+        for (;;) {
+            DictProbe c2;
+            bool v2 = false;
+            if (v1 && found) {
+                const uint64_t s = q + 1;
+                q = next_slash(bytes, s, e, found);
+                c2 = dict_begin(im, bytes, b, s, (uint32_t)(q - s));
+                v2 = true;
+            }
+            put(dict_end(im, bytes, b, cur));
+            if (!v1) return lev;
+            cur = c1;
+            c1 = c2;
+            v1 = v2;
+        }
+    }
+    for (;;) {
+        const bool more = found;
+        DictProbe nxt;
+        if (more) {
+            const uint64_t s = q + 1;
+            q = next_slash(bytes, s, e, found);
+            nxt = dict_begin(im, bytes, b, s, (uint32_t)(q - s));
+        }
+        put(dict_end(im, bytes, b, cur));
         if (!more) return lev;
         cur = nxt;
     }
