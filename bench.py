@@ -60,7 +60,7 @@ def log(*a):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--steps", type=int, default=500)   # ~5 s timed at C3 8M: long enough for a busy sampler
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", type=int, default=3, help="SURVEY §8(d) config (3 = the metric's)")
     ap.add_argument("--filters", type=int, default=None, help="override filter count")

@@ -25,6 +25,7 @@
 // flight at once (one per lane: packing, upload, walk, read-back and
 // callbacks of neighbouring batches overlap, and every GPU of a multi-device
 // engine works), and no per-topic work runs on the single sealing thread.
+#include <cstdlib>
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
@@ -697,11 +698,19 @@ int tm_batcher_open(tm_engine* e, const tm_batcher_config* cfg, tm_batcher** out
             return TM_ENOMEM;
         }
         L->device = devs[k % devs.size()];
-        // (normal priority: high-priority lanes, as bench.py's, took the
-        // flood from 166-181M to 145M topics/s and the p99 at 1M
-        // publishes/s from 245 us to 6.2 ms, profiles/r05_v)
-        if (L->device >= 0 && (hipSetDevice(L->device) != hipSuccess ||
-                               hipStreamCreateWithFlags(&L->stream, hipStreamNonBlocking) != hipSuccess)) {
+        // normal priority (A/B: TM_BATCHER_PRIO=1 makes the lanes
+        // high-priority streams, as bench.py's, each on a hardware queue of
+        // its own; profiles/r05_y)
+        static const bool prio = [] {
+            const char* v = std::getenv("TM_BATCHER_PRIO");
+            return v && v[0] == '1';
+        }();
+        int least = 0, greatest = 0;
+        if (L->device >= 0 &&
+            (hipSetDevice(L->device) != hipSuccess ||
+             (prio ? (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess ||
+                      hipStreamCreateWithPriority(&L->stream, hipStreamNonBlocking, greatest) != hipSuccess)
+                   : hipStreamCreateWithFlags(&L->stream, hipStreamNonBlocking) != hipSuccess))) {
             b->shutdown_lanes();
             delete b;
             return TM_EDEVICE;
