@@ -717,6 +717,32 @@ int tm_batcher_open(tm_engine* e, const tm_batcher_config* cfg, tm_batcher** out
         }
         b->lanes.push_back(std::move(L));
     }
+    // the workspaces sized up front (the engine's for max_topics, each lane's
+    // for batches of up to 32768 topics at 64 B and 64 ids per topic): a
+    // buffer grown later frees and reallocates device or pinned memory, which
+    // waits for the whole device -- stalls of up to ~16 ms in a new batcher's
+    // first second (the latency tail of profiles/r05_z)
+    if (R > 0) {
+        const uint64_t pre = std::min<uint64_t>(b->cfg.max_topics ? b->cfg.max_topics : 65536, 32768);
+        const uint64_t offb = (pre + 1) * 8, nbytes = pre * 64, cntb = pre * 4 + 8, cap = pre * 64 + 1024;
+        bool ok = tm_reserve(e, (uint32_t)std::min<uint64_t>(b->cfg.max_topics ? b->cfg.max_topics : 65536, 1u << 30),
+                             (uint64_t)(b->cfg.max_topics ? b->cfg.max_topics : 65536) * 64) == TM_OK;
+        for (auto& L : b->lanes) {
+            if (!ok || L->device < 0) continue;
+            ok = hipSetDevice(L->device) == hipSuccess && L->h_io.ensure(offb + nbytes + 16) &&
+                 L->d_io.ensure(offb + nbytes + 16) && L->h_out.ensure(8 + offb + cntb + cap * 4) &&
+                 L->d_out.ensure(8 + offb + cntb + cap * 4) && L->h_bytes.ensure(nbytes + 16) &&
+                 L->h_off.ensure(offb) && L->d_bytes.ensure(nbytes + 16) && L->d_off.ensure(offb) &&
+                 L->d_counts.ensure(pre * 4 + 4) && L->d_outoff.ensure(offb) && L->d_total.ensure(64) &&
+                 L->h_counts.ensure(pre * 4 + 4) && L->h_outoff.ensure(offb) && L->h_total.ensure(64) &&
+                 L->d_src.ensure(cap * 4) && L->h_src.ensure(cap * 4 + 4);
+        }
+        if (!ok) {
+            b->shutdown_lanes();
+            delete b;
+            return TM_ENOMEM;
+        }
+    }
     try {
         for (Stripe& x : b->stripes) x.cur = b->spare();
         for (size_t k = 0; k < b->lanes.size(); ++k) {

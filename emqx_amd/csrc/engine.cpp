@@ -2375,6 +2375,22 @@ struct tm_engine {
         }
         d.stage_k = d.keyed_k;
     }
+    // tm_reserve: every slot sized for batches of up to n topics (nbytes of
+    // topic bytes), the spill area for n / 16 chunks
+    void reserve(DevState& d, uint32_t n, uint64_t nbytes) {
+        const uint64_t sp = std::min<uint64_t>(((uint64_t)n / 16 + 7) & ~7ull, SPILL_BUDGET / (SPILL_CHUNK * 4));
+        d.spill_chunks = std::max<uint64_t>(d.spill_chunks, sp);
+        const int presort = presort_of(n, d);
+        for (int k = 0; k < nslots; ++k) {
+            Slot& w = d.slots[k];
+            ensure_slot(d, w, n, nbytes, 0, presort, false, false);
+            if (!w.sctl.p) {
+                w.sctl.ensure(64);
+                HIPCHK(hipMemset(w.sctl.p, 0, 64));
+            }
+        }
+        HIPCHK(hipDeviceSynchronize());
+    }
     void set_pieces(QueueBufs& qb, Slot& w) const {
         qb.donate = true;
         qb.don_min = don_min;
@@ -4082,6 +4098,18 @@ extern "C" int tm_debug_check_routes(tm_engine* e) {
             if (k.label != r->label || r->ord->r != r) return fail("order entry of " + *r->key);
             if (prev && !(prev->label < r->label && *prev->key < *r->key)) return fail("label order at " + *r->key);
             prev = r;
+        }
+        return TM_OK;
+    });
+}
+
+int tm_reserve(tm_engine* e, uint32_t n_topics, uint64_t n_bytes) {
+    if (!e) return TM_EINVAL;
+    auto held = lock_batches(e);
+    return guarded(e, [&]() -> int {
+        for (auto& dp : e->devs) {
+            tm_engine::Guard g(dp->device);
+            e->reserve(*dp, n_topics, n_bytes);
         }
         return TM_OK;
     });

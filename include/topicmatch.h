@@ -709,8 +709,24 @@ int  tm_rewrite_match_batch_device(tm_rewrite* r, const uint8_t* d_topics, const
  *              id by its filter's shape (the shard engines set it), 0 = keyed
  *              walk (default)
  *   "route_gc" garbage dest entries before a route-pool compaction is considered
+ *   "root_split" 1 = walk each topic as two queue items (the root's '+'
+ *              subtree, the rest), 0 = one (default; slower at C3)
+ *   "donate"   1 = once the queues are dry, lanes still walking hand pending
+ *              '+' subtrees to idle lanes of their wave (ordered pieces of the
+ *              topic's list), 0 = off (default; no gain at C3)
+ *   "donate_busy" donate only while at most this many lanes of a wave walk
+ *              (0..64, default 8); "donate_min" levels below a donated node
+ *              (default 2); "donate_max" largest batch that donates
  * TM_EINVAL for unknown names / values. */
 int tm_set_option(tm_engine* e, const char* name, int64_t value);
+
+/* Pre-size every replica's match workspaces for batches of up to n_topics
+ * topics of n_bytes topic bytes (optional).  Workspaces otherwise grow on
+ * demand, and each growth frees and reallocates device memory, which waits
+ * for the whole device: a stall of milliseconds in the middle of a stream of
+ * batches.  tm_batcher_open reserves for its batches.  No reference
+ * counterpart (an allocation hint, like tm_set_option). */
+int tm_reserve(tm_engine* e, uint32_t n_topics, uint64_t n_bytes);
 
 /* Counters of the last batch (visits, reference edge reads, matches).  Costs
  * one extra device pass; enable with tm_set_stats(e, 1) before the batch. */

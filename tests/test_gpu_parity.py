@@ -576,3 +576,19 @@ def test_side_stream_call_waits_for_fills_on_the_current_stream(gpu_device):
         assert np.array_equal(oo.cpu().numpy().view(np.uint64), wo)
         assert np.array_equal(ids[: int(wo[-1])].cpu().numpy().view(np.uint32), wi)
     e.close()
+
+
+def test_reserve_then_batches_exact(gpu_device):
+    """tm_reserve sizes every slot up front; batches of every size up to and
+    past the reservation stay exact against O1"""
+    fb, fo = W.filters(1)
+    o1 = O1()
+    o1.insert_many(fb, fo)
+    e = Engine(device=gpu_device)
+    e.insert_many(fb, fo)
+    e.commit()
+    assert e.lib.tm_reserve(e.h, 20000, 20000 * 64) == 0
+    for n in (1, 100, 20000, 30000):
+        tb, to = W.topics(1, n=n, stream=n)
+        _by_id(o1, e, tb, to)
+    e.close()
