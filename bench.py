@@ -451,7 +451,7 @@ def main():
     if a.scaling == "strong" and a.weak_topics > 0:
         wbatches = [W.topics(a.config, n=a.weak_topics, stream=multi.topic_stream(rank) * 64 + b)
                     for b in range(a.batches)]
-        wreg = Region(eng, dev, wbatches, a.streams)
+        wreg = Region(eng, dev, wbatches, a.streams, kind=a.stream_kind)
         wreg.warm(a.warmup)
         wdt = wreg.timed(a.steps)
         wres = wreg.results()
