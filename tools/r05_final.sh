@@ -16,3 +16,8 @@ case ${PART:-1} in
   3) STEPS="tests" TAG=${TAG}_big T_TESTS=1100 TESTS="tests/test_gpu_fullsize.py tests/test_gpu_configs.py" \
        bash tools/gpu.sh ;;
 esac
+# PART=4: the per-rank slices of strong scaling (1M/2M/4M/8M, rocprofv3 stats)
+# and the driver's N = 2 launch rehearsed on one GPU
+if [ "${PART:-1}" = 4 ]; then
+  STEPS="slices rehearse" TAG=${TAG}_slices NPROC=2 bash tools/gpu.sh
+fi
