@@ -46,7 +46,8 @@ class TmBatcherConfig(ctypes.Structure):
 class TmBatcherStats(ctypes.Structure):
     _fields_ = [(k, ctypes.c_uint64) for k in ("batches", "topics", "results", "max_batch", "size_seals",
                                                "deadline_seals", "failed_batches", "wait_ns", "pack_ns",
-                                               "device_ns", "callback_ns", "launch_ns", "sync_ns")]
+                                               "device_ns", "callback_ns", "launch_ns", "sync_ns", "max_wait_ns",
+                                               "max_pack_ns", "max_device_ns", "max_callback_ns", "max_sync_ns")]
 
 
 class TmExchangeIn(ctypes.Structure):

@@ -568,12 +568,19 @@ struct tm_batcher {
             }
             std::lock_guard<std::mutex> lk(mu);
             auto ns = [](clk::duration d) { return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(d).count(); };
-            st.wait_ns += ns(t_start - L.sealed);
-            st.pack_ns += ns(t_packed - t_start);
-            st.device_ns += ns(t_dev - t_packed);
-            st.callback_ns += ns(t_cb - t_dev);
+            const uint64_t w_ns = ns(t_start - L.sealed), p_ns = ns(t_packed - t_start), d_ns = ns(t_dev - t_packed),
+                           c_ns = ns(t_cb - t_dev);
+            st.wait_ns += w_ns;
+            st.pack_ns += p_ns;
+            st.device_ns += d_ns;
+            st.callback_ns += c_ns;
             st.launch_ns += L.launch_ns;
             st.sync_ns += L.sync_ns;
+            st.max_wait_ns = std::max(st.max_wait_ns, w_ns);
+            st.max_pack_ns = std::max(st.max_pack_ns, p_ns);
+            st.max_device_ns = std::max(st.max_device_ns, d_ns);
+            st.max_callback_ns = std::max(st.max_callback_ns, c_ns);
+            st.max_sync_ns = std::max(st.max_sync_ns, L.sync_ns);
             st.batches++;
             st.topics += m;
             if (m > st.max_batch) st.max_batch = m;
@@ -805,6 +812,8 @@ int tm_batcher_get_stats(tm_batcher* b, tm_batcher_stats* out) {
     if (!b || !out) return TM_EINVAL;
     std::lock_guard<std::mutex> lk(b->mu);
     *out = b->st;
+    // the max_* fields cover the batches since the previous call
+    b->st.max_wait_ns = b->st.max_pack_ns = b->st.max_device_ns = b->st.max_callback_ns = b->st.max_sync_ns = 0;
     return TM_OK;
 }
 

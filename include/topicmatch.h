@@ -562,6 +562,9 @@ typedef struct tm_batcher_stats {
      * spent enqueueing the copies and kernels and waiting on the stream */
     uint64_t wait_ns, pack_ns, device_ns, callback_ns;
     uint64_t launch_ns, sync_ns;
+    /* the largest of each over single batches (ns) since the previous
+     * tm_batcher_get_stats: where a stall sat */
+    uint64_t max_wait_ns, max_pack_ns, max_device_ns, max_callback_ns, max_sync_ns;
 } tm_batcher_stats;
 /* ids: filter ids (match/1), route sources (match_routes/1) or To ids
  * (deliveries); dests: route dest ids, target ids (deliveries) or null; n:

@@ -71,7 +71,7 @@ def main():
         for dl in [int(x) for x in a.deadlines.split(",")]:
             total = max(100_000, int(rate * a.seconds))
             log("offered %.0fM publishes/s, deadline %d us, %d publishes ..." % (rate / 1e6, dl, total))
-            r = (ctypes.c_double * 16)()
+            r = (ctypes.c_double * 24)()
             rc = f(e.h, tb.ctypes.data, to.ctypes.data, len(to) - 1, a.producers, rate, total, dl, a.max_topics,
                    a.lanes, (4 if eager else 0) | (8 if csr else 0) | (eus << 16), a.cb_threads, r)
             print(json.dumps({"opts": a.opt, "eager": eager, "eager_us": eus, "csr": csr, "offered_per_s": rate, "deadline_us": dl, "max_topics": a.max_topics,
@@ -82,7 +82,9 @@ def main():
                               "max_producer_lag_us": r[9],
                               "per_batch_us": {"sealed_to_lane": r[10], "pack": r[11], "device": r[12],
                                                "callbacks": r[13], "device_launch": r[14],
-                                               "device_wait": r[15]}}), flush=True)
+                                               "device_wait": r[15]},
+                              "worst_batch_us": {"sealed_to_lane": r[16], "pack": r[17], "device": r[18],
+                                                 "callbacks": r[19], "device_wait": r[20]}}), flush=True)
     e.close()
 
 

@@ -232,5 +232,11 @@ extern "C" int tm_bench_batcher_open_loop(tm_engine* e, const uint8_t* tb, const
     out[13] = (st.callback_ns - st0.callback_ns) / nb / 1e3;
     out[14] = (st.launch_ns - st0.launch_ns) / nb / 1e3;
     out[15] = (st.sync_ns - st0.sync_ns) / nb / 1e3;
+    // the worst single batch of the run (us; since the stats read after the warm-up)
+    out[16] = st.max_wait_ns / 1e3;
+    out[17] = st.max_pack_ns / 1e3;
+    out[18] = st.max_device_ns / 1e3;
+    out[19] = st.max_callback_ns / 1e3;
+    out[20] = st.max_sync_ns / 1e3;
     return TM_OK;
 }
