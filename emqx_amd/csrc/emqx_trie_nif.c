@@ -144,14 +144,13 @@ static ERL_NIF_TERM nif_open(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]
     if (rc == TM_OK) {
         /* batches sealed at 64K topics, once a lane is free and the oldest
          * topic has waited 40 us (eager), or 200 us after their first topic;
-         * 2 batches in flight per GPU (with 4, a stall of 8-16 ms in most
-         * runs at 10M publishes/s; with 2, p99 298-334 us there and
-         * 218-281 us at 1M/s -- DESIGN 5.6), and the callbacks (term
-         * building + enif_send, the per-topic host cost) shared with 8
-         * threads */
+         * 4 batches in flight per GPU (steady state at 1M / 10M publishes/s:
+         * p50 150-155 / 173-183 us, p99 219-225 / 281-306 us),
+         * and the callbacks (term building + enif_send, the per-topic host
+         * cost) shared with 8 threads */
         tm_batcher_config bc;
         memset(&bc, 0, sizeof(bc));
-        bc.lanes_per_replica = 2;
+        bc.lanes_per_replica = 4;
         bc.callback_threads = 8;
         bc.flags = TM_BATCHER_EAGER;
         rc = tm_batcher_open(r->e, &bc, &r->filters_b);
