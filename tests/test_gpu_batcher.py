@@ -134,3 +134,29 @@ def test_routes_and_deliveries_batchers_concurrently(gpu_device):
         assert got_r[t] == ([int(x) for x in want_r[t][0]], [int(x) for x in want_r[t][1]]), t
         assert got_d[t] == ([int(x) for x in want_d[t][0]], [int(x) for x in want_d[t][1]]), t
     e.close()
+
+
+def test_batcher_stats_worst_batch_since_last_read(gpu_device):
+    """tm_batcher_stats.max_*: the worst single batch's phases since the
+    previous read (a device batch ran: its device time is there and bounds
+    the mean; the next read starts again from zero)"""
+    from emqx_amd.batcher import Batcher
+    fb, fo = W.filters(1)
+    e = Engine(device=gpu_device)
+    e.insert_many(fb, fo)
+    e.commit()
+    b = Batcher(e, max_topics=512, deadline_us=200)
+    tb, to = W.topics(1, n=2000)
+    done = []
+    for t in W.unpack(tb, to):
+        b.submit(bytes(t), lambda st, ids, d: done.append(st))
+    b.flush()
+    s = b.stats()
+    assert len(done) == 2000 and all(x == 0 for x in done)
+    assert s["batches"] >= 4
+    assert s["max_device_ns"] > 0 and s["max_device_ns"] * s["batches"] >= s["device_ns"]
+    assert s["max_sync_ns"] <= s["max_device_ns"]   # a batch's stream wait is inside its device path
+    s2 = b.stats()
+    assert s2["max_device_ns"] == 0 and s2["max_wait_ns"] == 0 and s2["batches"] == s["batches"]
+    b.close()
+    e.close()
