@@ -565,7 +565,9 @@ struct tm_engine {
                                       // eight words (presort.hip; 0 = arrival order, 1 the word-hash key,
                                       // 2 the tail order, 5 the word-hash key within each XCD range, 3 by
                                       // batch size: 5 from sort_min topics, else 2)
-    uint32_t sort_min = 3000000;      // option "sort_min": presort 3's smallest batch in range-local word-hash order
+    uint32_t sort_min = 1500000;      // option "sort_min": presort 3's smallest batch in range-local word-hash order
+                                      // (with the lanes' drains hidden: 2M 2.806-2.809 ms vs 2.861-2.868 in the
+                                      // tail order, 1M 1.525 vs 1.514-1.515; profiles/r05_orders)
     uint32_t light_tail = 60;         // option "light_tail": presort 6 walks the lightest ~light_tail per mille of
                                       // each XCD range last (the cost classes that cover it in the previous batch)
     std::atomic<int> last_order{-1};  // the walk order (presort mode) of the last device batch (tm_debug_last_order)

@@ -690,7 +690,7 @@ int  tm_rewrite_match_batch_device(tm_rewrite* r, const uint8_t* d_topics, const
  *              below (default); 0 = arrival order; 4 = the tail order, then
  *              the word-hash key within a heat class (A/B)
  *   "sort_min" presort 3's smallest batch walked in range-local word-hash order
- *              (default 3000000)
+ *              (default 1500000)
  *   "sort_bits" the key bits presort 1 and 5 sort, one radix pass per 8
  *              (8..32, default 24; presort 5: the XCD range over the
  *              word-hash key's top sort_bits - 3 bits)

@@ -108,7 +108,7 @@ def test_c3_8m_device_default_order_every_topic_equals_o3(gpu_device, c3_full, c
     e.match_batch_device(d_b, d_o, n, int(to[-1]), c, oo, None, 0, t, stream=st)
     st.synchronize()
     # the engine's defaults walk an 8M-topic batch in the range-local
-    # word-hash order (option presort 3 -> 5 from sort_min = 3M topics)
+    # word-hash order (option presort 3 -> 5 from sort_min = 1.5M topics)
     assert e.lib.tm_debug_last_order(e.h) == 5
     cap = int(t.item()) + 64
     ids = torch.full((cap,), -1, dtype=torch.int32, device=dev)
