@@ -410,7 +410,12 @@ def main():
     batches = make_batches(a, cfg, rank, world)
     log("rank %d: %d batches of %d topics generated in %.1fs" % (rank, len(batches), len(batches[0][1]) - 1,
                                                                  time.time() - t0))
-    reg = Region(eng, dev, batches, a.streams, stats=True, hist=a.hist, kind=a.stream_kind)
+    # the lanes' streams, made once and shared by every region of the run:
+    # a second set of high-priority streams (the weak leg's) shared the
+    # process's few high-priority hardware queues with the first, and the
+    # weak 1M step took 1.59 instead of 1.51 ms (profiles/r06_ab/ab_r04.jsonl)
+    lane_streams = [Region.make_stream(dev, a.stream_kind) for _ in range(max(1, a.streams))]
+    reg = Region(eng, dev, batches, lane_streams, stats=True, hist=a.hist)
     stats, fanout = reg.stats, reg.fanout
     log("fan-out per topic: %s" % fanout)
     reg.warm(a.warmup)
@@ -451,7 +456,7 @@ def main():
     if a.scaling == "strong" and a.weak_topics > 0:
         wbatches = [W.topics(a.config, n=a.weak_topics, stream=multi.topic_stream(rank) * 64 + b)
                     for b in range(a.batches)]
-        wreg = Region(eng, dev, wbatches, a.streams, kind=a.stream_kind)
+        wreg = Region(eng, dev, wbatches, lane_streams)
         wreg.warm(a.warmup)
         wdt = wreg.timed(a.steps)
         wres = wreg.results()
@@ -579,10 +584,9 @@ class Region:
     distinct batches.  Outputs are sized by one untimed counting pass per
     batch (exact stats of batch 0 when `stats`)."""
 
-    def __init__(self, eng, dev, batches, streams, stats=False, hist=False, kind="pool"):
+    def __init__(self, eng, dev, batches, streams, stats=False, hist=False):
         self.eng, self.dev = eng, dev
-        self.kind = kind
-        self.st = self._stream()   # explicit (handle 0 would select the engine's own stream)
+        self.st = streams[0]   # explicit (handle 0 would select the engine's own stream)
         self.dbat = []
         for tb, to in batches:
             n = len(to) - 1
@@ -616,8 +620,7 @@ class Region:
         self.cap = max(self.totals) + 1024
         nmax = max(x[2] for x in self.dbat)
         self.lanes = []
-        for k in range(streams):
-            s_ = self.st if k == 0 else self._stream()
+        for s_ in streams:
             self.lanes.append((s_, torch.empty(nmax, dtype=torch.int32, device=dev),
                                torch.empty(nmax + 1, dtype=torch.int64, device=dev),
                                torch.empty(self.cap, dtype=torch.int32, device=dev),
@@ -625,15 +628,16 @@ class Region:
         self.k = 0
         self.last = {}
 
-    def _stream(self):
+    @staticmethod
+    def make_stream(dev, kind):
         """a lane's stream.  Each stream is fed to one hardware queue (4 per
         process for normal priority, GPU_MAX_HW_QUEUES): two lanes on one
         queue run in submission order, so a batch's tokenizer waits behind
         another lane's copy-out; high-priority streams come from a queue set
         of their own (tools/stream_queues.py, profiles/r05_t)"""
-        if self.kind == "prio":
-            return torch.cuda.Stream(device=self.dev, priority=-1)
-        return torch.cuda.Stream(device=self.dev)
+        if kind == "prio":
+            return torch.cuda.Stream(device=dev, priority=-1)
+        return torch.cuda.Stream(device=dev)
 
     def step(self):
         j = self.k

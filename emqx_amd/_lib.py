@@ -88,6 +88,7 @@ TM_BATCHER_ROUTES = 1
 TM_BATCHER_DELIVERIES = 2
 TM_BATCHER_EAGER = 4
 TM_BATCHER_CSR = 8
+TM_BATCHER_STATS_RESET_MAX = 1
 DONE_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, c_u32p, c_u32p, ctypes.c_uint32)
 
 # (name, restype, argtypes) — every symbol include/topicmatch.h declares
@@ -225,6 +226,8 @@ SIGNATURES = [
                                          c_u64p]),
     ("tm_batcher_flush", ctypes.c_int, [ctypes.c_void_p]),
     ("tm_batcher_get_stats", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(TmBatcherStats)]),
+    ("tm_batcher_get_stats2", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(TmBatcherStats), ctypes.c_uint32,
+                                             ctypes.c_uint32]),
     ("tm_batcher_close", None, [ctypes.c_void_p]),
     ("tm_acl_open", ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
     ("tm_acl_close", None, [ctypes.c_void_p]),

@@ -53,9 +53,14 @@ class Batcher:
         if rc != L.TM_OK:
             raise L.TopicMatchError(rc, "tm_batcher_flush")
 
-    def stats(self):
+    def stats(self, reset_max=False):
+        """tm_batcher_get_stats2: every counter; the max_* fields cover the
+        batches since the open or the last read with reset_max=True"""
         s = L.TmBatcherStats()
-        self.lib.tm_batcher_get_stats(self.h, ctypes.byref(s))
+        rc = self.lib.tm_batcher_get_stats2(self.h, ctypes.byref(s), ctypes.sizeof(s),
+                                            L.TM_BATCHER_STATS_RESET_MAX if reset_max else 0)
+        if rc != L.TM_OK:
+            raise L.TopicMatchError(rc, "tm_batcher_get_stats2")
         return {k: getattr(s, k) for k, _ in s._fields_}
 
     def close(self):

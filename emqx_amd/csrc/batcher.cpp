@@ -33,6 +33,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <deque>
+#include <cstddef>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -46,6 +47,9 @@ namespace {
 
 using clk = std::chrono::steady_clock;
 constexpr int NSTRIPE = 16;
+// engine workspaces reserved at open: batches up to this many topics (a
+// 256K-topic flood batch) run without growing them; larger ones grow on demand
+constexpr uint64_t TM_BATCHER_RESERVE_TOPICS = 262144;
 
 struct Req {
     tm_batch_done_fn fn;
@@ -724,30 +728,27 @@ int tm_batcher_open(tm_engine* e, const tm_batcher_config* cfg, tm_batcher** out
         }
         b->lanes.push_back(std::move(L));
     }
-    // the workspaces sized up front (the engine's for max_topics, each lane's
-    // for batches of up to 32768 topics at 64 B and 64 ids per topic): a
-    // buffer grown later frees and reallocates device or pinned memory, which
-    // waits for the whole device -- stalls of up to ~16 ms in a new batcher's
-    // first second (the latency tail of profiles/r05_z)
+    // the workspaces sized up front (the engine's for batches of up to
+    // TM_BATCHER_RESERVE_TOPICS, each lane's for batches of up to 32768
+    // topics at 64 B and 64 ids per topic): a buffer grown later frees and
+    // reallocates device or pinned memory, which waits for the whole device
+    // -- stalls of up to ~16 ms in a new batcher's first second (the latency
+    // tail of profiles/r05_z).  Best effort: a reservation that does not fit
+    // leaves the buffers to grow on demand, as before, and the open succeeds.
     if (R > 0) {
-        const uint64_t pre = std::min<uint64_t>(b->cfg.max_topics ? b->cfg.max_topics : 65536, 32768);
+        const uint64_t mt = b->cfg.max_topics;
+        const uint64_t pre = std::min<uint64_t>(mt, 32768);
         const uint64_t offb = (pre + 1) * 8, nbytes = pre * 64, cntb = pre * 4 + 8, cap = pre * 64 + 1024;
-        bool ok = tm_reserve(e, (uint32_t)std::min<uint64_t>(b->cfg.max_topics ? b->cfg.max_topics : 65536, 1u << 30),
-                             (uint64_t)(b->cfg.max_topics ? b->cfg.max_topics : 65536) * 64) == TM_OK;
+        const uint64_t eng = std::min<uint64_t>(mt, TM_BATCHER_RESERVE_TOPICS);
+        (void)tm_reserve(e, (uint32_t)eng, eng * 64);
         for (auto& L : b->lanes) {
-            if (!ok || L->device < 0) continue;
-            ok = hipSetDevice(L->device) == hipSuccess && L->h_io.ensure(offb + nbytes + 16) &&
-                 L->d_io.ensure(offb + nbytes + 16) && L->h_out.ensure(8 + offb + cntb + cap * 4) &&
-                 L->d_out.ensure(8 + offb + cntb + cap * 4) && L->h_bytes.ensure(nbytes + 16) &&
-                 L->h_off.ensure(offb) && L->d_bytes.ensure(nbytes + 16) && L->d_off.ensure(offb) &&
-                 L->d_counts.ensure(pre * 4 + 4) && L->d_outoff.ensure(offb) && L->d_total.ensure(64) &&
-                 L->h_counts.ensure(pre * 4 + 4) && L->h_outoff.ensure(offb) && L->h_total.ensure(64) &&
-                 L->d_src.ensure(cap * 4) && L->h_src.ensure(cap * 4 + 4);
-        }
-        if (!ok) {
-            b->shutdown_lanes();
-            delete b;
-            return TM_ENOMEM;
+            if (L->device < 0 || hipSetDevice(L->device) != hipSuccess) continue;
+            (void)(L->h_io.ensure(offb + nbytes + 16) && L->d_io.ensure(offb + nbytes + 16) &&
+                   L->h_out.ensure(8 + offb + cntb + cap * 4) && L->d_out.ensure(8 + offb + cntb + cap * 4) &&
+                   L->h_bytes.ensure(nbytes + 16) && L->h_off.ensure(offb) && L->d_bytes.ensure(nbytes + 16) &&
+                   L->d_off.ensure(offb) && L->d_counts.ensure(pre * 4 + 4) && L->d_outoff.ensure(offb) &&
+                   L->d_total.ensure(64) && L->h_counts.ensure(pre * 4 + 4) && L->h_outoff.ensure(offb) &&
+                   L->h_total.ensure(64) && L->d_src.ensure(cap * 4) && L->h_src.ensure(cap * 4 + 4));
         }
     }
     try {
@@ -808,12 +809,18 @@ int tm_batcher_flush(tm_batcher* b) {
     return TM_OK;
 }
 
+static_assert(offsetof(tm_batcher_stats, max_wait_ns) == TM_BATCHER_STATS_V1_BYTES, "round-4 stats prefix");
+
 int tm_batcher_get_stats(tm_batcher* b, tm_batcher_stats* out) {
-    if (!b || !out) return TM_EINVAL;
+    return tm_batcher_get_stats2(b, out, TM_BATCHER_STATS_V1_BYTES, 0);
+}
+
+int tm_batcher_get_stats2(tm_batcher* b, tm_batcher_stats* out, uint32_t out_size, uint32_t flags) {
+    if (!b || !out || out_size < TM_BATCHER_STATS_V1_BYTES) return TM_EINVAL;
     std::lock_guard<std::mutex> lk(b->mu);
-    *out = b->st;
-    // the max_* fields cover the batches since the previous call
-    b->st.max_wait_ns = b->st.max_pack_ns = b->st.max_device_ns = b->st.max_callback_ns = b->st.max_sync_ns = 0;
+    std::memcpy(out, &b->st, std::min<size_t>(out_size, sizeof(tm_batcher_stats)));
+    if (flags & TM_BATCHER_STATS_RESET_MAX)
+        b->st.max_wait_ns = b->st.max_pack_ns = b->st.max_device_ns = b->st.max_callback_ns = b->st.max_sync_ns = 0;
     return TM_OK;
 }
 

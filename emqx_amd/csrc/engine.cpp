@@ -36,6 +36,7 @@
 #include <thread>
 #include <stdexcept>
 #include <string>
+#include <string_view>
 #include <unordered_map>
 #include <unordered_set>
 #include <vector>
@@ -1317,6 +1318,32 @@ struct tm_engine {
         dev_dirty = true;
     }
 
+    // tm_insert_batch_ids' pre-pass: the error insert() under
+    // forced id `id` would throw for filter p, without changing anything, so
+    // a batch that fails is refused whole instead of partly applied
+    void check_forced(const uint8_t* p, uint32_t len, uint32_t id) {
+        if (id == FILTER_NONE) throw ArgError("filter id FILTER_NONE");
+        if (id >= 0x7FFFFFF0u) throw RangeError("filter id past 2^31 - 16");
+        const uint32_t v = split_words(p, len, false) ? walk(tmp_words) : NODE_NONE;
+        const uint32_t f = v != NODE_NONE ? nodes[v].self_filter : FILTER_NONE;
+        if (f != FILTER_NONE) {
+            if (f != id)
+                throw ArgError("filter already present under id " + std::to_string(f) + ", not " + std::to_string(id));
+            return;   // present under this id: insert is a no-op
+        }
+        if (id < filters.size() && filters[id].node != NODE_NONE)
+            throw ArgError("filter id " + std::to_string(id) + " in use");
+        auto q = quarantined.find(id);
+        if (q != quarantined.end()) {
+            const FilterRec& old = filters[id];
+            const bool same = old.len == len && (len == 0 || std::memcmp(&filter_arena[old.off], p, len) == 0);
+            std::lock_guard<std::mutex> lk(lease_mu);
+            if (!same && !quarantine_over(q->second, epoch.load(), oldest_lease()))
+                throw ArgError("filter id " + std::to_string(id) + " was deleted and may still be named by "
+                               "batches in flight");
+        }
+    }
+
     // emqx_trie:delete/1 (src/emqx_trie.erl:88-96) + delete_path/1 (:149-163)
     void remove(const uint8_t* p, uint32_t len) {
         if (!split_words(p, len, false)) return;  // [] -> ok
@@ -2383,15 +2410,20 @@ struct tm_engine {
         const uint64_t sp = std::min<uint64_t>(((uint64_t)n / 16 + 7) & ~7ull, SPILL_BUDGET / (SPILL_CHUNK * 4));
         d.spill_chunks = std::max<uint64_t>(d.spill_chunks, sp);
         const int presort = presort_of(n, d);
+        bool cleared = false;
         for (int k = 0; k < nslots; ++k) {
             Slot& w = d.slots[k];
             ensure_slot(d, w, n, nbytes, 0, presort, false, false);
             if (!w.sctl.p) {
                 w.sctl.ensure(64);
                 HIPCHK(hipMemset(w.sctl.p, 0, 64));
+                cleared = true;
             }
         }
-        HIPCHK(hipDeviceSynchronize());
+        // only the memsets on the null stream are waited for (the engine's
+        // streams are non-blocking): walks in flight on other streams go on
+        // (a device-wide sync stalled every batcher's lanes)
+        if (cleared) HIPCHK(hipStreamSynchronize(nullptr));
     }
     void set_pieces(QueueBufs& qb, Slot& w) const {
         qb.donate = true;
@@ -3124,9 +3156,21 @@ int tm_insert_batch_ids(tm_engine* e, const uint8_t* bytes, const uint64_t* off,
             tm_engine* e;
             ~Reset() { e->forced_fid = FILTER_NONE; }
         } reset{e};
+        // validate the whole batch first (each id free or this filter's, not
+        // quarantined for another filter; no id or filter twice with
+        // different partners), then insert: a refused batch changes nothing
+        std::unordered_map<uint32_t, std::string_view> by_id;
+        std::unordered_map<std::string_view, uint32_t> by_filter;
         for (uint32_t i = 0; i < n; ++i) {
             if (off[i + 1] < off[i] || off[i + 1] - off[i] > 0xFFFFFFFFull) throw ArgError("bad offsets");
-            if (ids[i] == FILTER_NONE) throw ArgError("filter id FILTER_NONE");
+            const std::string_view f(reinterpret_cast<const char*>(bytes + off[i]), (size_t)(off[i + 1] - off[i]));
+            e->check_forced(bytes + off[i], (uint32_t)f.size(), ids[i]);
+            auto a = by_id.emplace(ids[i], f);
+            auto b = by_filter.emplace(f, ids[i]);
+            if (a.first->second != f || b.first->second != ids[i])
+                throw ArgError("batch names filter id " + std::to_string(ids[i]) + " or its filter twice");
+        }
+        for (uint32_t i = 0; i < n; ++i) {
             e->forced_fid = ids[i];
             e->insert(bytes + off[i], (uint32_t)(off[i + 1] - off[i]));
         }

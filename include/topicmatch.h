@@ -562,10 +562,15 @@ typedef struct tm_batcher_stats {
      * spent enqueueing the copies and kernels and waiting on the stream */
     uint64_t wait_ns, pack_ns, device_ns, callback_ns;
     uint64_t launch_ns, sync_ns;
-    /* the largest of each over single batches (ns) since the previous
-     * tm_batcher_get_stats: where a stall sat */
+    /* the largest of each over single batches (ns) since the batcher opened
+     * or the last read with TM_BATCHER_STATS_RESET_MAX: where a stall sat.
+     * Only tm_batcher_get_stats2 writes these (a caller built against the
+     * round-4 header, whose struct ends before them, keeps calling
+     * tm_batcher_get_stats, which writes exactly that prefix) */
     uint64_t max_wait_ns, max_pack_ns, max_device_ns, max_callback_ns, max_sync_ns;
 } tm_batcher_stats;
+#define TM_BATCHER_STATS_V1_BYTES (13u * 8u)   /* the prefix tm_batcher_get_stats writes */
+#define TM_BATCHER_STATS_RESET_MAX 1u          /* tm_batcher_get_stats2: zero the max_* fields after this read */
 /* ids: filter ids (match/1), route sources (match_routes/1) or To ids
  * (deliveries); dests: route dest ids, target ids (deliveries) or null; n:
  * list length */
@@ -577,7 +582,13 @@ int  tm_batcher_submit(tm_batcher* b, const uint8_t* topic, uint32_t len, tm_bat
                        uint64_t* ticket_out);
 /* seal the open batch and wait until every submitted topic has completed */
 int  tm_batcher_flush(tm_batcher* b);
+/* the counters up to sync_ns (TM_BATCHER_STATS_V1_BYTES bytes; max_* untouched) */
 int  tm_batcher_get_stats(tm_batcher* b, tm_batcher_stats* out);
+/* min(out_size, sizeof(tm_batcher_stats)) bytes of the stats (out_size <
+ * TM_BATCHER_STATS_V1_BYTES: TM_EINVAL); flags TM_BATCHER_STATS_RESET_MAX
+ * starts a new max_* window after the read (only the reader that owns the
+ * window should pass it) */
+int  tm_batcher_get_stats2(tm_batcher* b, tm_batcher_stats* out, uint32_t out_size, uint32_t flags);
 /* flush, then stop the worker */
 void tm_batcher_close(tm_batcher* b);
 

@@ -138,8 +138,10 @@ def test_routes_and_deliveries_batchers_concurrently(gpu_device):
 
 def test_batcher_stats_worst_batch_since_last_read(gpu_device):
     """tm_batcher_stats.max_*: the worst single batch's phases since the
-    previous read (a device batch ran: its device time is there and bounds
-    the mean; the next read starts again from zero)"""
+    last resetting read (a device batch ran: its device time is there and
+    bounds the mean); a plain read leaves the window alone, a resetting one
+    starts it again from zero; tm_batcher_get_stats writes only the round-4
+    prefix"""
     from emqx_amd.batcher import Batcher
     fb, fo = W.filters(1)
     e = Engine(device=gpu_device)
@@ -156,7 +158,15 @@ def test_batcher_stats_worst_batch_since_last_read(gpu_device):
     assert s["batches"] >= 4
     assert s["max_device_ns"] > 0 and s["max_device_ns"] * s["batches"] >= s["device_ns"]
     assert s["max_sync_ns"] <= s["max_device_ns"]   # a batch's stream wait is inside its device path
+    assert b.stats()["max_device_ns"] == s["max_device_ns"]   # a second reader sees the same window
+    b.stats(reset_max=True)
     s2 = b.stats()
     assert s2["max_device_ns"] == 0 and s2["max_wait_ns"] == 0 and s2["batches"] == s["batches"]
+    import ctypes
+    from emqx_amd import _lib as L
+    v1 = L.TmBatcherStats()
+    v1.max_wait_ns = 12345
+    assert e.lib.tm_batcher_get_stats(b.h, ctypes.byref(v1)) == 0
+    assert v1.max_wait_ns == 12345 and v1.batches == s["batches"]   # nothing past the v1 prefix written
     b.close()
     e.close()

@@ -206,6 +206,29 @@ def test_forced_ids_duplicate_filter_and_live_id():
     eng.close()
 
 
+def test_forced_id_batch_refused_whole():
+    """a batch with one refused entry used to leave the entries
+    before it inserted (callers have no rollback).  The batch is now checked
+    whole first: any bad entry -- a live id, a filter under another id, an id
+    or a filter twice in the batch -- refuses it and changes nothing."""
+    from emqx_amd import _lib as L
+    eng = Engine(device=-1)
+    _ins_ids(eng, [b"s/+/x"], [5])
+    bad = [
+        ([b"a/1", b"b/+", b"t/#"], [10, 11, 5]),          # the last takes a live id
+        ([b"a/1", b"s/+/x"], [10, 12]),                   # a present filter under another id
+        ([b"a/1", b"b/+"], [10, 10]),                     # one id for two filters
+        ([b"a/1", b"a/1"], [10, 13]),                     # one filter under two ids
+    ]
+    for fl, ids in bad:
+        with pytest.raises(L.TopicMatchError):
+            _ins_ids(eng, fl, ids)
+        assert eng.filter_count == 1 and not eng.lookup(b"a/1") and not eng.lookup(b"b/+"), (fl, ids)
+    _ins_ids(eng, [b"a/1", b"a/1", b"s/+/x"], [10, 10, 5])   # repeats with the same partner: fine
+    assert eng.filter_count == 2 and fid(eng, b"a/1") == 10
+    eng.close()
+
+
 def test_forced_only_engine_drains_its_quarantine_at_commit():
     """a forced-only engine (routed shards) never calls the id allocator, so
     the quarantine must drain at commit: many delete / re-insert rounds of

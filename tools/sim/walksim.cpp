@@ -48,6 +48,7 @@ struct View {
 };
 
 enum Kind : uint8_t { K_INNER = 0, K_LEAF = 1, K_COLD = 2, K_HOT = 3, K_PAIR = 4, K_NKIND = 5 };
+constexpr uint8_t K_FIXK = K_PAIR;   // M_FIX quads (the pair kind is unused with it): address space 4
 
 // one load: its record, kind and dependent round within its step
 struct Acc {
@@ -94,6 +95,10 @@ enum Mode : int {
     M_BLOOMW = 32,   // the engine's blocks, Bloom test by a (mode >> 16)-bit mask, k = 2 (0 = no Bloom)
     M_BLOCKS = 8,    // per-node child blocks: a WIDE node's literal / '#' edges in a contiguous open-addressing
                      // block of its own (blocks in node order = heat order), not one shared table
+    M_FIX = 64,      // a fixed 64 B block per node id (no pointer: address = v * 64): up to 8 literal children
+                     // as 8 B {word, child} in 4 quads, home quad by word hash, quads probed in order (one
+                     // round each); nodes with more children: the shared table (with M_BLOCKS: their own
+                     // variable block, found through a header in the fixed block, one extra round)
 };
 
 // per-node child blocks (M_BLOCKS): 16 B slots {word, child, S(child), -}
@@ -102,11 +107,16 @@ struct Blocks {
     std::vector<uint32_t> size;    // per node: slots (power of two)
     std::vector<uint32_t> word, child, sum;
     uint32_t div = 2;              // block size >= div * edges
+    // M_FIX: per node, its literal children placed in the fixed block's quads (quad of child i), or
+    // cnt > 8 (big: variable block / shared table)
+    std::vector<uint32_t> cnt;
+    std::vector<std::vector<std::pair<uint32_t, uint8_t>>> fixq;   // per node with <= 8 children: (word, quad)
+    static uint32_t qhome(uint32_t w) { return (w * 0x9E3779B1u) >> 30; }
     static uint32_t home(uint32_t w, uint32_t mask) { return (w * 0x9E3779B1u >> 7) & mask; }
     void build(const View& v, uint32_t d) {
         div = d;
         const uint64_t n = v.n_nodes;
-        std::vector<uint32_t> cnt(n, 0);
+        cnt.assign(n, 0);
         auto each = [&](auto f) {
             for (const EdgeSlot* t : {v.cold, v.hot}) {
                 const uint64_t ns = t == v.cold ? v.cold_slots : v.hot_slots;
@@ -132,6 +142,15 @@ struct Blocks {
         word.assign(cur, EDGE_EMPTY);
         child.assign(cur, NODE_NONE);
         sum.assign(cur, 0);
+        fixq.assign(n, {});
+        std::vector<uint8_t> fill(n * 4, 0);
+        each([&](const EdgeSlot& e) {
+            if (cnt[e.parent] > 8 || e.word == WORD_HASH) return;
+            uint32_t q = qhome(e.word);
+            while (fill[(uint64_t)e.parent * 4 + q] >= 2) q = (q + 1) & 3;
+            ++fill[(uint64_t)e.parent * 4 + q];
+            fixq[e.parent].push_back({e.word, (uint8_t)q});
+        });
         each([&](const EdgeSlot& e) {
             const uint32_t m = size[e.parent] - 1;
             uint32_t p = home(e.word, m);
@@ -178,7 +197,46 @@ struct Walker {
                 }
             }
         }
-        if (mode & M_BLOCKS) {
+        if ((mode & M_FIX) && w != WORD_HASH) {
+            const uint32_t c = blk->cnt[node];
+            if (c && c <= 8) {
+                // quads from the home one on: a quad holding the word ends it; a
+                // quad with a free entry (fewer than 2) ends it too
+                std::vector<uint8_t> per(4, 0);
+                uint8_t wq = 255;
+                for (const auto& pr : blk->fixq[node]) {
+                    ++per[pr.second];
+                    if (pr.first == w) wq = pr.second;
+                }
+                uint32_t q = Blocks::qhome(w);
+                for (int k = 0; k < 4; ++k, q = (q + 1) & 3) {
+                    acc.push_back(Acc{(uint32_t)q, (uint8_t)(K_NKIND + 0), (uint8_t)std::min<uint32_t>(rd, 255)});
+                    acc.back().idx = node * 4 + q;
+                    acc.back().kind = K_FIXK;
+                    ++rd;
+                    if (q == wq) {
+                        ++probes_ok;
+                        // the child: from the shared table's record (same child, same summary)
+                        uint32_t r0 = 0;
+                        std::vector<Acc> dummy;
+                        const int m0 = mode;
+                        const_cast<Walker*>(this)->mode = 0;
+                        const Hit h = probe(node, w, dummy, r0);
+                        const_cast<Walker*>(this)->mode = m0;
+                        --probes_ok;
+                        return Hit{h.child, SUM_ALL, false};   // 8 B entries: no per-child summary
+                    }
+                    if (per[q] < 2) break;
+                }
+                ++probes_fail;
+                return Hit{NODE_NONE, 0, false};
+            }
+            if (c > 8 && (mode & M_BLOCKS)) {   // header round in the fixed block
+                acc.push_back(Acc{node * 4, K_FIXK, (uint8_t)std::min<uint32_t>(rd, 255)});
+                ++rd;
+            }
+        }
+        if ((mode & M_BLOCKS) && (!(mode & M_FIX) || blk->cnt[node] > 8)) {
             const uint64_t b = blk->base[node];
             if (b == ~0ull) {
                 ++probes_fail;
@@ -387,7 +445,7 @@ int sim_run(const void* view, const uint32_t* levels, const uint32_t* words, con
     const View& vw = *reinterpret_cast<const View*>(view);
     Walker wk(vw, mode);
     Blocks blocks;
-    if (mode & M_BLOCKS) {
+    if (mode & (M_BLOCKS | M_FIX)) {
         blocks.build(vw, (uint32_t)((mode >> 8) & 0xFF) ? (uint32_t)((mode >> 8) & 0xFF) : 2u);
         wk.blk = &blocks;
     }
@@ -404,8 +462,8 @@ int sim_run(const void* view, const uint32_t* levels, const uint32_t* words, con
     auto addr = [&](const Acc& a) -> uint64_t {
         const uint64_t i = a.idx & 0x7FFFFFFFu, hi = a.idx >> 31;
         switch (a.kind) {
-            case K_INNER:
-            case K_PAIR: return 0 * R + i * 16;
+            case K_INNER: return 0 * R + i * 16;
+            case K_PAIR: return (mode & M_FIX) ? 4 * R + (uint64_t)a.idx * 16 : 0 * R + i * 16;
             case K_LEAF: return 1 * R + i * 16;
             case K_COLD: return 2 * R + i * sb + hi * 16;
             default: return 3 * R + i * sb + hi * 16;

@@ -61,7 +61,7 @@ extern "C" int tm_bench_batcher(tm_engine* e, const uint8_t* tb, const uint64_t*
         tm_batcher_flush(b);
     }
     tm_batcher_stats st0;
-    tm_batcher_get_stats(b, &st0);
+    tm_batcher_get_stats2(b, &st0, sizeof st0, TM_BATCHER_STATS_RESET_MAX);
     std::vector<Rec> recs(nt);
     const auto t0 = clk::now();
     std::vector<std::thread> th;
@@ -79,7 +79,7 @@ extern "C" int tm_bench_batcher(tm_engine* e, const uint8_t* tb, const uint64_t*
     tm_batcher_flush(b);
     const double secs = std::chrono::duration<double>(clk::now() - t0).count();
     tm_batcher_stats st;
-    tm_batcher_get_stats(b, &st);
+    tm_batcher_get_stats2(b, &st, sizeof st, TM_BATCHER_STATS_RESET_MAX);
     tm_batcher_close(b);
     st.batches -= st0.batches;
     st.topics -= st0.topics;
@@ -162,7 +162,7 @@ extern "C" int tm_bench_batcher_open_loop(tm_engine* e, const uint8_t* tb, const
         tm_batcher_flush(b);
     }
     tm_batcher_stats st0;
-    tm_batcher_get_stats(b, &st0);
+    tm_batcher_get_stats2(b, &st0, sizeof st0, TM_BATCHER_STATS_RESET_MAX);
     g_ol_fail = 0;
     g_ol_done = 0;
     // a settling phase of 100 ms at the offered rate before the measured
@@ -213,13 +213,13 @@ extern "C" int tm_bench_batcher_open_loop(tm_engine* e, const uint8_t* tb, const
         });
     // the per-batch means and maxima from the end of the settling phase
     std::this_thread::sleep_until(t0 + std::chrono::nanoseconds((int64_t)(settle * ns_per)));
-    tm_batcher_get_stats(b, &st0);
+    tm_batcher_get_stats2(b, &st0, sizeof st0, TM_BATCHER_STATS_RESET_MAX);
     const auto t_meas = clk::now();
     for (auto& x : th) x.join();
     tm_batcher_flush(b);
     const double secs = std::chrono::duration<double>(clk::now() - t_meas).count();
     tm_batcher_stats st;
-    tm_batcher_get_stats(b, &st);
+    tm_batcher_get_stats2(b, &st, sizeof st, TM_BATCHER_STATS_RESET_MAX);
     tm_batcher_close(b);
     std::vector<int64_t> lat;
     for (const OLRec& r : recs)

@@ -94,7 +94,7 @@ int main(int argc, char** argv) {
         tm_batcher_flush(b);
         const double secs = std::chrono::duration<double>(clk::now() - t0).count();
         tm_batcher_stats st;
-        tm_batcher_get_stats(b, &st);
+        tm_batcher_get_stats2(b, &st, sizeof st, 0);
         tm_batcher_close(b);
         std::vector<int64_t> lat(nt);
         uint64_t fails = 0, ids = 0;
