@@ -439,16 +439,13 @@ def main():
         adt = reg.timed(a.steps)
         akms = reg.kernel_times(a.roof_steps)
         axcd = reg.walk_clocks()
-        apieces = reg.walk_pieces()
         ares = reg.results()
         same = all(np.array_equal(x[0], y[0]) and np.array_equal(x[1], y[1]) and np.array_equal(x[2], y[2])
                    for x, y in zip(ares, results))
         ab.append({"opts": spec, "ms_per_step": adt / a.steps * 1e3, "kernel_ms": akms, "walk_xcd_ms": axcd,
-                   "walk_pieces": apieces,
                    "value": (a.topics if a.scaling == "strong" else n0 * world) * a.steps / adt,
                    "lists_equal_headline": bool(same)})
-        log("A/B %s: %.3f ms per step, kernels %s, pieces %s, lists equal: %s" % (spec, adt / a.steps * 1e3, akms,
-                                                                                apieces, same))
+        log("A/B %s: %.3f ms per step, kernels %s, lists equal: %s" % (spec, adt / a.steps * 1e3, akms, same))
     # the other scaling figure beside it (not `value`): weak scaling at
     # SURVEY §8(d)'s 1M topics per GPU when the headline is strong
     weak = None
@@ -692,16 +689,6 @@ class Region:
         return [{"start": round(out[4 * x], 4), "home_done": round(out[4 * x + 1], 4), "end": round(out[4 * x + 2], 4),
                  "stolen_chunks": int(out[4 * x + 3])} for x in range(8)]
 
-    def walk_pieces(self):
-        """pieces the last walk donated (option "donate"), summed over XCDs"""
-        out = (ctypes.c_uint64 * 8)()
-        f = getattr(self.eng.lib, "tm_debug_walk_pieces", None)
-        if f is None:
-            return None
-        f.restype = ctypes.c_int
-        if f(self.eng.h, out) != 0:
-            return None
-        return int(sum(out))
 
     def results(self):
         """every batch's full result (host arrays: counts, offsets, ids)"""

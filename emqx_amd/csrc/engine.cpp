@@ -215,14 +215,9 @@ constexpr int N_KERNEL_SLOTS = 4;   // tokenize, walk, scan, copy_out
 struct Slot {
     DevBuf twords, words, path, meta, scan, stage, kstage, ws, stats, perm, skeys, svals, scount, soff, sscan,
         twords_s, meta_s, spill, spill_head;
-    DevBuf icounts, ioff;           // option "root_split": the 2n items' counts and offsets
-    DevBuf prow, pdesc, pcnt, tfirst, dmask;   // option "donate": the piece pool and the topics' piece lists
-    uint32_t pcap = 0;
     DevBuf sctl;                    // tm_match_small's placement / completion counters (left zeroed by it)
     uint32_t spill_chunks = 0;      // spill capacity of the slot's last batch (0: none)
     bool sorted = false;            // the slot's last batch walked in presort order (perm valid)
-    bool split = false;             // ... walked as 2n root-split items (icounts / ioff valid)
-    bool donated = false;           // ... with option "donate" (the piece pool and lists valid)
     uint64_t* h_maxc = nullptr;     // pinned copy of the slot's ws after its last walk (largest match count,
                                     // spill chunks taken per XCD)
     hipEvent_t maxc_ev = nullptr, done = nullptr;
@@ -243,7 +238,7 @@ constexpr int MAX_SLOTS = 4;
 // written, and only the next write to it waits for them (by then they are
 // long done).
 struct Image {
-    DevBuf d_nodes, d_edges, d_hedges, d_dict, d_arena, d_woff, d_inner, d_leaf, d_bpool;
+    DevBuf d_nodes, d_edges, d_hedges, d_dict, d_arena, d_woff, d_inner, d_leaf;
     // route image (routes.hip) and aggre tables (aggre.hip), same epoch as the
     // trie: a batch's filter ids and the route lists it expands them with
     // always come from one commit
@@ -263,7 +258,7 @@ struct Image {
     RouteView rv{};
     AggreView av{};
     void release() {
-        for (DevBuf* b : {&d_nodes, &d_edges, &d_hedges, &d_dict, &d_arena, &d_woff, &d_inner, &d_leaf, &d_bpool, &d_rslots,
+        for (DevBuf* b : {&d_nodes, &d_edges, &d_hedges, &d_dict, &d_arena, &d_woff, &d_inner, &d_leaf, &d_rslots,
                           &d_rarena, &d_rdest, &d_fr_meta, &d_rank_src, &d_dt, &d_rank_tg, &d_fshape, &d_wheat})
             b->release();
         for (hipEvent_t ev : uses) (void)hipEventDestroy(ev);
@@ -483,22 +478,6 @@ struct tm_engine {
     Dirty prev_node_dirty, prev_cold_dirty, prev_hot_dirty, prev_dict_dirty;
     EdgeTable& tab(uint32_t parent) { return parent < hot_limit ? hot : cold; }
     const EdgeTable& tab(uint32_t parent) const { return parent < hot_limit ? hot : cold; }
-    // per-node child blocks (option "blocks", image.h BlockSlot): with
-    // blocks_live, a WIDE node's literal children live in its own block of
-    // bpool (lw = first slot, lc = log2 slots << 27 | 27-bit Bloom) and the
-    // edge tables keep only '#' edges.  A block holds at most 1/block_div of
-    // its slots; a full one moves to a block twice the size at the pool's end
-    // (the old one is garbage until compaction or relayout, which lays the
-    // blocks out in node order)
-    std::vector<BlockSlot> bpool;
-    Dirty bpool_dirty, prev_bpool_dirty;
-    size_t bpool_garbage = 0;
-    int blocks_want = 0;              // option "blocks" (off: C3 walk 8.83 vs 8.61 ms with the shared table,
-                                      // its 27-bit Bloom passes 17.6 absent words per topic vs 11.9: DESIGN 5.2c)
-    bool blocks_live = false;         // the representation the host mirror is in (switched by relayout)
-    uint32_t block_div = 4;           // option "block_load": blocks kept at load <= 1/block_div
-    size_t block_gc_min = 1u << 20;   // option "block_gc": garbage slots before a compaction is considered
-
     // ---- filter registry ----
     std::vector<uint8_t> filter_arena;
     std::vector<FilterRec> filters;
@@ -686,11 +665,6 @@ struct tm_engine {
                                         // (no re-walks); unkeyed walks keep K and spill (kernels.h)
     int spill_on = 1;                   // option "spill": ids past K to spill chunks (0: re-walk, as keyed)
     int chunk_rows = TM_CHUNK_ROWS;     // option "chunk_rows" (kernels.h QueueBufs)
-    int root_split = 0;                 // option "root_split" (kernels.h QueueBufs)
-    int donate = 0;                     // option "donate" (kernels.h QueueBufs): the drain's donation walk
-    uint32_t don_min = 2;               // option "donate_min": levels a donated subtree has below its node
-    uint32_t donate_max = 0xFFFFFFFFu;  // option "donate_max": only batches of at most this many topics
-    uint32_t don_busy = 8;              // option "donate_busy": only while at most this many lanes still walk
     uint32_t wave_walk_max = 32768;     // option "wave_walk_max": batches of at most this many topics take the
                                         // wave-per-topic walk (tm_walk_wave: ~2 dependent loads per level);
                                         // faster up to 16K topics, slower from 64K (profiles/r03_d)
@@ -716,8 +690,6 @@ struct tm_engine {
             }
         }
         dict.assign(1024, DictSlot{0, WORD_NONE, 0, 0, 0, 0});
-        if (const char* v = std::getenv("TM_BLOCKS")) blocks_want = std::atoi(v) && kernels_have_blocks() ? 1 : 0;
-        blocks_live = blocks_want != 0 && !SLOT_RECORD;
         nodes.reserve(1024);
         cold.slots.assign(1024, kEmptySlot);
         hot.slots.assign(1024, kEmptySlot);
@@ -847,14 +819,6 @@ struct tm_engine {
         const uint32_t p = aux[x].parent, w = aux[x].word;
         if (p == NODE_NONE || w == WORD_PLUS) return;
         if (w != WORD_HASH && !(nodes[p].plus & WIDE)) return;
-        if (w != WORD_HASH && blocks_live) {
-            const size_t s = blk_find(p, w);
-            if (s != SIZE_MAX && bpool[s].sum != child_sum(x)) {
-                bpool[s].sum = child_sum(x);
-                bpool_dirty.mark(s);
-            }
-            return;
-        }
         const size_t s = edge_find_slot(p, w);
         if (s == SIZE_MAX) return;
         EdgeSlot& e = tab(p).slots[s];
@@ -908,118 +872,6 @@ struct tm_engine {
     }
 
     // ------------------------------------------------------------------
-    // child blocks (blocks_live): a WIDE node's literal children
-    static BlockSlot empty_block_slot() { return BlockSlot{WORD_NONE, NODE_NONE, 0, 0}; }
-    static uint32_t blk_log2(const Node& x) { return x.lc >> BLOCK_LOG2_SHIFT; }
-    // the smallest block for c children: at least 2 x 4 slots' worth of room
-    uint32_t blk_log2_for(uint32_t c) const {
-        uint32_t k = 2;
-        while ((1ull << k) < (uint64_t)c * block_div) ++k;
-        return k;
-    }
-    // slots of a new block of 2^k slots at the pool's end (blocks of up to
-    // 8 slots aligned to their size: never across a 128 B line)
-    uint64_t blk_alloc(uint32_t k) {
-        const uint64_t sz = 1ull << k, al = sz < 8 ? sz : 8;
-        uint64_t base = (bpool.size() + al - 1) & ~(al - 1);
-        if (base + sz > 0xFFFFFFF0ull) throw RangeError("child block pool past 2^32 slots");
-        const size_t old = bpool.size();
-        bpool.resize(base + sz, empty_block_slot());
-        bpool_garbage += base - old;   // alignment padding
-        for (size_t i = old; i < bpool.size() && !bpool_dirty.all; ++i) bpool_dirty.mark(i);
-        return base;
-    }
-    size_t blk_find(uint32_t v, uint32_t w) const {
-        const Node& x = nodes[v];
-        const uint32_t k = blk_log2(x), m = (1u << k) - 1;
-        for (uint32_t p = block_home(w, k);; p = (p + 1) & m) {
-            const BlockSlot& e = bpool[(size_t)x.lw + p];
-            if (e.word == w) return (size_t)x.lw + p;
-            if (e.word == WORD_NONE) return SIZE_MAX;
-        }
-    }
-    // place (w, c) in v's block, which has room
-    void blk_put(uint32_t v, uint32_t w, uint32_t c) {
-        Node& x = nodes[v];
-        const uint32_t k = blk_log2(x), m = (1u << k) - 1;
-        uint32_t p = block_home(w, k);
-        while (bpool[(size_t)x.lw + p].word != WORD_NONE) p = (p + 1) & m;
-        bpool[(size_t)x.lw + p] = BlockSlot{w, c, child_sum(c), 0};
-        bpool_dirty.mark((size_t)x.lw + p);
-        x.lc |= block_bloom(w);
-    }
-    // v's block moved to one of 2^k slots (its children re-placed)
-    void blk_resize(uint32_t v, uint32_t k) {
-        std::vector<BlockSlot> keep;
-        const Node& x0 = nodes[v];
-        const uint64_t ob = x0.lw, on = 1ull << blk_log2(x0);
-        for (uint64_t i = 0; i < on; ++i)
-            if (bpool[ob + i].word != WORD_NONE) keep.push_back(bpool[ob + i]);
-        const uint64_t nb = blk_alloc(k);   // (may reallocate bpool: no references held across it)
-        for (uint64_t i = 0; i < on; ++i) {
-            bpool[ob + i] = empty_block_slot();
-            bpool_dirty.mark(ob + i);
-        }
-        bpool_garbage += on;
-        Node& x = nodes[v];
-        x.lw = (uint32_t)nb;
-        x.lc = k << BLOCK_LOG2_SHIFT;   // Bloom rebuilt from the children kept
-        for (const BlockSlot& e : keep) blk_put(v, e.word, e.child);
-    }
-    // backward-shift deletion within the block (no tombstones)
-    void blk_erase(uint32_t v, uint32_t w) {
-        const size_t at = blk_find(v, w);
-        if (at == SIZE_MAX) return;
-        const Node& x = nodes[v];
-        const uint64_t b = x.lw;
-        const uint32_t m = (1u << blk_log2(x)) - 1;
-        uint32_t i = (uint32_t)(at - b), j = i;
-        for (;;) {
-            j = (j + 1) & m;
-            if (bpool[b + j].word == WORD_NONE) break;
-            const uint32_t h = block_home(bpool[b + j].word, blk_log2(x));
-            const bool move = (i <= j) ? (h <= i || h > j) : (h <= i && h > j);
-            if (move) {
-                bpool[b + i] = bpool[b + j];
-                bpool_dirty.mark(b + i);
-                i = j;
-            }
-        }
-        bpool[b + i] = empty_block_slot();
-        bpool_dirty.mark(b + i);
-    }
-    void blk_free(uint32_t v) {
-        bpool_garbage += 1ull << blk_log2(nodes[v]);
-        const uint64_t b = nodes[v].lw, n = 1ull << blk_log2(nodes[v]);
-        for (uint64_t i = 0; i < n; ++i) {
-            bpool[b + i] = empty_block_slot();
-            bpool_dirty.mark(b + i);
-        }
-    }
-    // the pool rewritten without garbage, blocks in node order (positions
-    // inside a block unchanged); every slot re-uploaded
-    void blk_compact() {
-        std::vector<BlockSlot> np;
-        np.reserve(bpool.size() - bpool_garbage + 64);
-        for (size_t v = 0; v < nodes.size(); ++v) {
-            Node& x = nodes[v];
-            if (!(x.plus & WIDE) || (aux[v].parent == NODE_NONE && v != ROOT)) continue;
-            const uint64_t sz = 1ull << blk_log2(x), al = sz < 8 ? sz : 8;
-            const uint64_t base = (np.size() + al - 1) & ~(al - 1);
-            np.resize(base, empty_block_slot());
-            np.insert(np.end(), bpool.begin() + x.lw, bpool.begin() + x.lw + sz);
-            x.lw = (uint32_t)base;
-            node_dirty.mark(v);
-        }
-        bpool.swap(np);
-        bpool_garbage = 0;
-        bpool_dirty.all = true;
-    }
-    void maybe_compact_blocks() {
-        if (blocks_live && bpool_garbage > block_gc_min && bpool_garbage * 2 > bpool.size()) blk_compact();
-    }
-
-    // ------------------------------------------------------------------
     // nodes
     uint32_t new_node(uint32_t parent, uint32_t word) {
         uint32_t id;
@@ -1057,10 +909,6 @@ struct tm_engine {
         if (w == WORD_PLUS) return x.plus & NODE_MASK;
         if (w == WORD_HASH) return x.hash;
         if (!(x.plus & WIDE)) return x.lw == w ? x.lc : NODE_NONE;
-        if (blocks_live) {
-            const size_t s = blk_find(v, w);
-            return s == SIZE_MAX ? NODE_NONE : bpool[s].child;
-        }
         size_t s = edge_find_slot(v, w);
         return s == SIZE_MAX ? NODE_NONE : tab(v).slots[s].child;
     }
@@ -1075,26 +923,6 @@ struct tm_engine {
     }
     void lit_add(uint32_t v, uint32_t w, uint32_t c) {
         Node& x = nodes[v];
-        if (blocks_live) {   // (aux[v].lit_count: the children before this one)
-            if (!(x.plus & WIDE)) {
-                if (x.lw == WORD_NONE) {
-                    x.lw = w;
-                    x.lc = c;
-                    return;
-                }
-                const uint32_t w0 = x.lw, c0 = x.lc, k = blk_log2_for(2);
-                const uint64_t base = blk_alloc(k);
-                Node& y = nodes[v];
-                y.plus |= WIDE;
-                y.lw = (uint32_t)base;
-                y.lc = k << BLOCK_LOG2_SHIFT;
-                blk_put(v, w0, c0);
-            } else if ((uint64_t)(aux[v].lit_count + 1) * block_div > (1ull << blk_log2(x))) {
-                blk_resize(v, blk_log2_for(aux[v].lit_count + 1));
-            }
-            blk_put(v, w, c);
-            return;
-        }
         if (!(x.plus & WIDE)) {
             if (x.lw == WORD_NONE) {
                 x.lw = w;
@@ -1115,14 +943,12 @@ struct tm_engine {
     void lit_remove(uint32_t v, uint32_t w) {
         Node& x = nodes[v];
         if (x.plus & WIDE) {
-            if (blocks_live) blk_erase(v, w);
-            else edge_erase(v, w);
+            edge_erase(v, w);
         } else if (x.lw == w) {
             x.lw = WORD_NONE;
             x.lc = NODE_NONE;
         }
         if (--aux[v].lit_count == 0) {
-            if (blocks_live && (nodes[v].plus & WIDE)) blk_free(v);
             nodes[v].plus &= ~WIDE;
             nodes[v].lw = WORD_NONE;
             nodes[v].lc = NODE_NONE;
@@ -1813,22 +1639,10 @@ struct tm_engine {
     // discovery order) directly follows it, two 32 B records to a 64 B line;
     // topics with a common prefix walk a compact region.  Deleted ids are
     // dropped (compaction).  Filter ids are unchanged.
-    // f(parent, word, child) for every literal edge of a WIDE node (in its
-    // block, or in the edge tables)
+    // f(parent, word, child) for every literal edge of a WIDE node (in the
+    // edge tables)
     template <class F>
     void table_literals(F&& f) const {
-        if (blocks_live) {
-            for (size_t v = 0; v < nodes.size(); ++v) {
-                const Node& x = nodes[v];
-                if (!(x.plus & WIDE) || (aux[v].parent == NODE_NONE && v != ROOT)) continue;
-                const uint64_t n = 1ull << blk_log2(x);
-                for (uint64_t i = 0; i < n; ++i) {
-                    const BlockSlot& e = bpool[(size_t)x.lw + i];
-                    if (e.word != WORD_NONE) f((uint32_t)v, e.word, e.child);
-                }
-            }
-            return;
-        }
         for (const EdgeTable* t : {&cold, &hot})
             for (const EdgeSlot& e : t->slots)
                 if (e.parent != EDGE_EMPTY && e.word != WORD_HASH) f(e.parent, e.word, e.child);
@@ -1959,47 +1773,10 @@ struct tm_engine {
             std::vector<EdgeSlot>().swap(t->slots);
             t->used = 0;
         }
-        std::vector<BlockSlot>().swap(bpool);
-        bpool_garbage = 0;
-        blocks_live = blocks_want != 0 && !SLOT_RECORD;
-        if (!blocks_live)
-            for (const EdgeSlot& e : old)
-                if (e.word != WORD_HASH) bloom_add(nn[newid[e.parent]], e.word);
+        for (const EdgeSlot& e : old)
+            if (e.word != WORD_HASH) bloom_add(nn[newid[e.parent]], e.word);
         nodes.swap(nn);
         aux.swap(na);   // before the edges are placed: slot_for reads the children's new summaries
-        if (blocks_live) {
-            // one block per WIDE node, in node order; the literal edges leave `old`
-            std::vector<EdgeSlot> lit;
-            size_t k = 0;
-            for (const EdgeSlot& e : old) {
-                if (e.word == WORD_HASH) old[k++] = e;
-                else lit.push_back(e);
-            }
-            old.resize(k);
-            std::sort(lit.begin(), lit.end(), [&](const EdgeSlot& a, const EdgeSlot& b) {
-                return newid[a.parent] != newid[b.parent] ? newid[a.parent] < newid[b.parent]
-                                                          : newid[a.child] < newid[b.child];
-            });
-            size_t total = 0;
-            for (size_t i = 0; i < lit.size();) {
-                size_t j = i;
-                while (j < lit.size() && lit[j].parent == lit[i].parent) ++j;
-                total += (size_t)1 << blk_log2_for((uint32_t)(j - i));
-                i = j;
-            }
-            bpool.reserve(total + total / 8 + 64);
-            for (size_t i = 0; i < lit.size();) {
-                size_t j = i;
-                while (j < lit.size() && lit[j].parent == lit[i].parent) ++j;
-                const uint32_t p = newid[lit[i].parent], kk = blk_log2_for((uint32_t)(j - i));
-                const uint64_t base = blk_alloc(kk);
-                nodes[p].lw = (uint32_t)base;
-                nodes[p].lc = kk << BLOCK_LOG2_SHIFT;
-                for (size_t q = i; q < j; ++q) blk_put(p, lit[q].word, newid[lit[q].child]);
-                i = j;
-            }
-            bpool_dirty.all = true;
-        }
         hot_limit = new_hot_limit;
         size_t nhot = 0;
         for (const EdgeSlot& e : old) nhot += newid[e.parent] < hot_limit;
@@ -2065,7 +1842,6 @@ struct tm_engine {
         im.edges = g.d_edges.as<const EdgeSlot>();
         im.edge_slot_mask = cold.slots.size() - 1;
         im.hot_edges = g.d_hedges.as<const EdgeSlot>();
-        im.blocks = blocks_live ? g.d_bpool.as<const BlockSlot>() : nullptr;
         im.hot_slot_mask = hot.slots.size() - 1;
         im.hot_limit = hot_limit;
         im.dict = g.d_dict.as<const DictSlot>();
@@ -2144,7 +1920,6 @@ struct tm_engine {
     // were launched on, consistent and untouched.
     void commit() {
         if (dev_dirty || devs.empty() || !devs[0]->img[devs[0]->cur].written) maybe_relayout();
-        maybe_compact_blocks();
         if (targets_dirty && !devs.empty()) rank_targets();
         if (devs.empty()) {
             ++epoch;
@@ -2174,7 +1949,6 @@ struct tm_engine {
             upload_table(d, g, g.d_nodes, nodes, node_dirty, prev_node_dirty);
             upload_table(d, g, g.d_edges, cold.slots, cold.dirty, prev_cold_dirty);
             upload_table(d, g, g.d_hedges, hot.slots, hot.dirty, prev_hot_dirty);
-            if (blocks_live) upload_table(d, g, g.d_bpool, bpool, bpool_dirty, prev_bpool_dirty);
             upload_table(d, g, g.d_dict, dict, dict_dirty, prev_dict_dirty);
             upload_table(d, g, g.d_rslots, rt_slots, t_slots.cur, t_slots.prev);
             upload_table(d, g, g.d_rarena, rt_arena, t_rarena.cur, t_rarena.prev);
@@ -2227,7 +2001,6 @@ struct tm_engine {
         for (const Rot& r : {Rot{&node_dirty, &prev_node_dirty, nodes.size()},
                              Rot{&cold.dirty, &prev_cold_dirty, cold.slots.size()},
                              Rot{&hot.dirty, &prev_hot_dirty, hot.slots.size()},
-                             Rot{&bpool_dirty, &prev_bpool_dirty, bpool.size()},
                              Rot{&dict_dirty, &prev_dict_dirty, dict.size()}}) {
             *r.prev = *r.cur;
             r.cur->clear();
@@ -2289,41 +2062,19 @@ struct tm_engine {
     }
     // (presort 4: the tail order, then the word-hash key within each heat
     // class; 5: the word-hash key within each XCD range -- A/B orders)
-    // the piece pool of a donating walk (option "donate"): up to n/2 pieces
-    static uint32_t piece_cap(uint32_t n) {
-        const uint64_t c = std::max<uint64_t>((uint64_t)n / 2, 8192);
-        return (uint32_t)std::min<uint64_t>((c + 7) & ~7ull, 1u << 30);
-    }
-    void ensure_slot(DevState& d, Slot& w, uint32_t n, uint64_t nbytes, uint32_t key_words, int presort,
-                     bool split, bool don = false) {
-        // split: rows, counts, spill heads and scan by item (2n); a second
-        // path area for the copy-out's re-walks of items 2t
-        const uint32_t nq = split ? 2 * n : n;
+    void ensure_slot(DevState& d, Slot& w, uint32_t n, uint64_t nbytes, uint32_t key_words, int presort) {
         w.twords.ensure((size_t)(n + 1) * WREG * 4);
         w.words.ensure((nbytes + n + 1) * 4);
-        w.path.ensure((nbytes + 2ull * n + 2) * 4 * (split ? 2 : 1));
+        w.path.ensure((nbytes + 2ull * n + 2) * 4);
         w.stats.ensure(STATS_BYTES);
         w.meta.ensure((size_t)(n + 1) * 4);
-        w.scan.ensure(scan_tmp_elems(nq) * 8 + 8);
-        w.stage.ensure(((size_t)nq * d.stage_k + 4) * 4);
-        if (split) {
-            w.icounts.ensure((size_t)nq * 4 + 8);
-            w.ioff.ensure(((size_t)nq + 2) * 8);
-        }
-        if (don) {
-            const uint32_t pc = piece_cap(n);
-            w.prow.ensure(((size_t)pc * d.stage_k + 4) * 4);
-            w.pdesc.ensure((size_t)pc * 16);
-            w.pcnt.ensure((size_t)pc * 8);
-            w.tfirst.ensure((size_t)n * 4 + 4);
-            w.dmask.ensure(((size_t)(n >> 5) + 1) * 4);
-            w.pcap = pc;
-        }
+        w.scan.ensure(scan_tmp_elems(n) * 8 + 8);
+        w.stage.ensure(((size_t)n * d.stage_k + 4) * 4);
         if (key_words) w.kstage.ensure(((size_t)n * d.stage_k * key_words + 4) * 8);
         w.spill_chunks = 0;
         if (!key_words && spill_on && (!presort || chunk_rows) && d.spill_chunks >= 8) {
             w.spill.ensure((size_t)d.spill_chunks * SPILL_CHUNK * 4);
-            w.spill_head.ensure((size_t)nq * 4 + 4);
+            w.spill_head.ensure((size_t)n * 4 + 4);
             w.spill_chunks = (uint32_t)d.spill_chunks;
         }
         w.ws.ensure(QWS_BYTES);
@@ -2413,7 +2164,7 @@ struct tm_engine {
         bool cleared = false;
         for (int k = 0; k < nslots; ++k) {
             Slot& w = d.slots[k];
-            ensure_slot(d, w, n, nbytes, 0, presort, false, false);
+            ensure_slot(d, w, n, nbytes, 0, presort);
             if (!w.sctl.p) {
                 w.sctl.ensure(64);
                 HIPCHK(hipMemset(w.sctl.p, 0, 64));
@@ -2424,17 +2175,6 @@ struct tm_engine {
         // streams are non-blocking): walks in flight on other streams go on
         // (a device-wide sync stalled every batcher's lanes)
         if (cleared) HIPCHK(hipStreamSynchronize(nullptr));
-    }
-    void set_pieces(QueueBufs& qb, Slot& w) const {
-        qb.donate = true;
-        qb.don_min = don_min;
-        qb.don_busy = don_busy;
-        qb.prow = w.prow.as<uint32_t>();
-        qb.pdesc = w.pdesc.as<uint32_t>();
-        qb.pcnt = w.pcnt.as<uint32_t>();
-        qb.tfirst = w.tfirst.as<uint32_t>();
-        qb.dmask = w.dmask.as<uint32_t>();
-        qb.pcap = w.pcap;
     }
     void record_maxc(Slot& w, hipStream_t st) {
         if (!w.h_maxc) HIPCHK(hipHostMalloc((void**)&w.h_maxc, QWS_BYTES, hipHostMallocDefault));
@@ -2457,12 +2197,8 @@ struct tm_engine {
         adapt_stage_k(d, n, kw);
         const int presort = presort_of(n, d);
         last_order = presort;
-        // option "root_split": exactly the batches launch_queue walks in chunk
-        // rows (unkeyed, lane walk -- a wave-walk batch has no perm -- no stats)
+        // small batches walk one wave per topic (a wave-walk batch has no perm)
         const bool wave = n <= wave_walk_max && !kw && presort != 1;
-        const bool split = root_split && !kw && !shaped && !stats_enabled && chunk_rows && !wave && n <= (1u << 30);
-        // option "donate": the same batches (root_split gives way)
-        const bool don = donate && n <= donate_max && !kw && !shaped && !stats_enabled && chunk_rows && !wave;
         const int si = d.next_slot;
         d.next_slot = (d.next_slot + 1) % nslots;
         Slot& w = d.slots[si];
@@ -2470,7 +2206,7 @@ struct tm_engine {
         // every slot sized for this batch now: a slot first used later would
         // allocate (hipMalloc of GBs of stage rows) in the middle of a stream
         // of batches
-        for (int k = 0; k < nslots; ++k) ensure_slot(d, d.slots[(si + k) % nslots], n, nbytes, kw, presort, split && !don, don);
+        for (int k = 0; k < nslots; ++k) ensure_slot(d, d.slots[(si + k) % nslots], n, nbytes, kw, presort);
         d.last_slot = si;
         ImageView im = view(d);
         unsigned long long* sp = w.stats.as<unsigned long long>();
@@ -2514,15 +2250,7 @@ struct tm_engine {
             qb.spill_head = w.spill_head.as<uint32_t>();
             qb.spill_chunks = w.spill_chunks;
         }
-        qb.root_split = split && !don;
-        if (qb.root_split) {
-            qb.icounts = w.icounts.as<uint32_t>();
-            qb.ioff = w.ioff.as<uint64_t>();
-        }
-        if (don) set_pieces(qb, w);
         w.sorted = queue_rows_by_position(qb, stats_enabled);   // the copy-out moves rows by perm
-        w.split = qb.root_split;
-        w.donated = don;
         HIPCHK(launch_queue(stats_enabled, xcdq != 0, im, bytes, off, n, qb, d.stage_k, counts, out_off, ids, keys,
                             cap, total, sp, st, timing_enabled ? marks : nullptr, walk_bpc, hist_enabled != 0,
                             keys ? key_words : 1u));
@@ -2586,12 +2314,6 @@ struct tm_engine {
         qb.scan_tmp = w.scan.as<uint64_t>();
         qb.ws = w.ws.as<unsigned long long>();
         qb.perm = w.sorted ? w.perm.as<uint32_t>() : nullptr;   // the rows of a presorted walk
-        if (w.split) {   // the item rows, counts and offsets of a root-split walk
-            qb.root_split = true;
-            qb.icounts = w.icounts.as<uint32_t>();
-            qb.ioff = w.ioff.as<uint64_t>();
-        }
-        if (w.donated) set_pieces(qb, w);   // the piece lists of a donating walk
         if (w.spill_chunks && !w.keyed) {   // the spill chunks of the same walk
             qb.spill = w.spill.as<uint32_t>();
             qb.spill_head = w.spill_head.as<uint32_t>();
@@ -3255,7 +2977,7 @@ int tm_engine_device(tm_engine* e) { return e ? e->device : -1; }
 uint64_t tm_image_bytes(tm_engine* e) {
     if (!e) return 0;
     return e->nodes.size() * sizeof(Node) + (e->cold.slots.size() + e->hot.slots.size()) * sizeof(EdgeSlot) +
-           (e->blocks_live ? e->bpool.size() * sizeof(BlockSlot) : 0) + e->dict.size() * sizeof(DictSlot) +
+           e->dict.size() * sizeof(DictSlot) +
            e->word_arena.size() + e->word_off.size() * 4;
 }
 
@@ -3911,45 +3633,6 @@ int tm_match_small_device(tm_engine* e, const uint8_t* d_bytes, const uint64_t* 
     }, [&] { e->finish_batch(n); });
 }
 
-// diagnostics (not part of include/topicmatch.h): host-side consistency of
-// the child blocks (option "blocks"): every WIDE node's block holds exactly
-// its literal children (each found from its home slot, with its word, its
-// current summary and a Bloom bit pattern the node carries), no other node
-// owns a slot of it.  TM_OK, or TM_EINVAL naming the first defect.
-extern "C" int tm_debug_check_blocks(tm_engine* e) {
-    if (!e) return TM_EINVAL;
-    return guarded(e, [&]() -> int {
-        if (!e->blocks_live) return TM_OK;
-        std::vector<uint8_t> owned(e->bpool.size(), 0);
-        for (size_t v = 0; v < e->nodes.size(); ++v) {
-            const Node& x = e->nodes[v];
-            if (!(x.plus & WIDE) || (e->aux[v].parent == NODE_NONE && v != ROOT)) continue;
-            const uint64_t n = 1ull << (x.lc >> BLOCK_LOG2_SHIFT);
-            if ((uint64_t)x.lw + n > e->bpool.size()) throw ArgError("node " + std::to_string(v) + ": block past the pool");
-            uint32_t cnt = 0;
-            for (uint64_t i = 0; i < n; ++i) {
-                if (owned[x.lw + i]) throw ArgError("slot " + std::to_string(x.lw + i) + " in two blocks");
-                owned[x.lw + i] = 1;
-                const BlockSlot& b = e->bpool[x.lw + i];
-                if (b.word == WORD_NONE) continue;
-                ++cnt;
-                if (b.child >= e->nodes.size() || e->aux[b.child].parent != v || e->aux[b.child].word != b.word)
-                    throw ArgError("node " + std::to_string(v) + ": slot " + std::to_string(i) + " names a stranger");
-                if (e->blk_find((uint32_t)v, b.word) != x.lw + i)
-                    throw ArgError("node " + std::to_string(v) + ": word " + std::to_string(b.word) + " unreachable");
-                if (b.sum != e->child_sum(b.child)) throw ArgError("node " + std::to_string(v) + ": stale summary");
-                const uint32_t bb = block_bloom(b.word);
-                if ((x.lc & bb) != bb) throw ArgError("node " + std::to_string(v) + ": Bloom misses a child");
-            }
-            if (cnt != e->aux[v].lit_count)
-                throw ArgError("node " + std::to_string(v) + ": " + std::to_string(cnt) + " block children, lit_count " +
-                               std::to_string(e->aux[v].lit_count));
-            if ((uint64_t)cnt * e->block_div > n) throw ArgError("node " + std::to_string(v) + ": block over its load");
-        }
-        return TM_OK;
-    });
-}
-
 // diagnostics (not part of include/topicmatch.h): the walk order of the
 // last device batch (option "presort" resolved by batch size: 5 the
 // range-local word-hash order, 2 the tail order, 0 arrival order ...)
@@ -3960,25 +3643,6 @@ extern "C" int tm_debug_last_order(tm_engine* e) { return e ? e->last_order.load
 // out[4x..4x+3] = ms from the walk's first wave start to XCD x's first wave
 // start, to the first exhaustion of its home range, to its last wave's end,
 // and the chunks its waves stole (-1 where not recorded)
-// diagnostics: pieces donated by the last batch's walk on replica 0, per XCD
-// (option "donate"; 0 without)
-extern "C" int tm_debug_walk_pieces(tm_engine* e, uint64_t* out) {
-    if (!e || !out) return TM_EINVAL;
-    auto held = lock_batches(e);
-    return guarded(e, [&]() -> int {
-        if (e->devs.empty()) return TM_EINVAL;
-        DevState& d = *e->devs[0];
-        tm_engine::Guard g(d.device);
-        const DevBuf& ws = d.slots[d.last_slot].ws;
-        if (!ws.p) return TM_EINVAL;
-        HIPCHK(hipDeviceSynchronize());
-        std::vector<uint64_t> h(QWS_BYTES / 8);
-        HIPCHK(hipMemcpy(h.data(), ws.p, QWS_BYTES, hipMemcpyDeviceToHost));
-        for (int x = 0; x < 8; ++x) out[x] = h[QWS_PIECE + 16 * x];
-        return TM_OK;
-    });
-}
-
 extern "C" int tm_debug_walk_clocks(tm_engine* e, double* out) {
     if (!e || !out) return TM_EINVAL;
     auto held = lock_batches(e);
@@ -4036,10 +3700,6 @@ struct tm_debug_image_view {
     uint32_t hot_limit;
     uint32_t aux_stride;     // bytes per aux record
     const void* aux;         // per node: {parent u32, word u32, edge_count u32, lit_count u32, ...}
-    const void* blocks;      // BlockSlot[block_slots] (option "blocks"; WIDE nodes: lw = first slot, lc = log2 | Bloom)
-    uint64_t block_slots;
-    uint32_t blocks_live;
-    uint32_t pad;
 };
 extern "C" int tm_debug_image(tm_engine* e, tm_debug_image_view* out) {
     if (!e || !out) return TM_EINVAL;
@@ -4053,10 +3713,6 @@ extern "C" int tm_debug_image(tm_engine* e, tm_debug_image_view* out) {
         out->hot_limit = e->hot_limit;
         out->aux_stride = (uint32_t)sizeof(NodeAux);
         out->aux = e->aux.data();
-        out->blocks = e->bpool.data();
-        out->block_slots = e->bpool.size();
-        out->blocks_live = e->blocks_live ? 1u : 0u;
-        out->pad = 0;
         return TM_OK;
     });
 }
@@ -4183,38 +3839,9 @@ int tm_set_option(tm_engine* e, const char* name, int64_t value) {
             e->layout_mode = (int)value;
             return TM_OK;
         }
-        if (!std::strcmp(name, "blocks")) {   // 1: WIDE nodes' children in per-node blocks, 0: the shared table
-            if (value < 0 || value > 1 || (value && SLOT_RECORD)) return TM_EINVAL;
-            // a device engine needs walks that read blocks (a TM_BLOCKS_PATH build)
-            if (value && !e->devs.empty() && !kernels_have_blocks()) return TM_EINVAL;
-            e->blocks_want = (int)value;
-            if ((value != 0) != e->blocks_live) {
-                if (e->live_nodes <= 1 && e->bpool.empty() && e->cold.used == 0 && e->hot.used == 0) {
-                    e->blocks_live = value != 0;   // an empty trie: switch now
-                } else {
-                    e->force_relayout = true;      // the next commit converts
-                    e->dev_dirty = true;
-                }
-            }
-            return TM_OK;
-        }
         if (!std::strcmp(name, "light_tail")) {   // per mille of each range walked last by presort 6
             if (value < 0 || value > 500) return TM_EINVAL;
             e->light_tail = (uint32_t)value;
-            return TM_OK;
-        }
-        if (!std::strcmp(name, "block_gc")) {
-            if (value < 0) return TM_EINVAL;
-            e->block_gc_min = (size_t)value;
-            return TM_OK;
-        }
-        if (!std::strcmp(name, "block_load")) {   // blocks kept at load <= 1/value (the next relayout resizes)
-            if (value < 2 || value > 16) return TM_EINVAL;
-            if ((uint32_t)value != e->block_div) {
-                e->block_div = (uint32_t)value;
-                e->force_relayout = true;
-                e->dev_dirty = true;
-            }
             return TM_OK;
         }
         if (!std::strcmp(name, "relayout")) {   // 1: relayout at the next commit (layout A/Bs)
@@ -4341,31 +3968,6 @@ int tm_set_option(tm_engine* e, const char* name, int64_t value) {
         if (!std::strcmp(name, "chunk_rows")) {
             if (value < 0 || value > 1) return TM_EINVAL;
             e->chunk_rows = (int)value;
-            return TM_OK;
-        }
-        if (!std::strcmp(name, "donate")) {   // the drain's donation walk (kernels.h QueueBufs)
-            if (value < 0 || value > 1) return TM_EINVAL;
-            e->donate = (int)value;
-            return TM_OK;
-        }
-        if (!std::strcmp(name, "donate_min")) {
-            if (value < 0 || value > 15) return TM_EINVAL;
-            e->don_min = (uint32_t)value;
-            return TM_OK;
-        }
-        if (!std::strcmp(name, "donate_busy")) {   // (0: the donating walk kernel, nothing donated)
-            if (value < 0 || value > 64) return TM_EINVAL;
-            e->don_busy = (uint32_t)value;
-            return TM_OK;
-        }
-        if (!std::strcmp(name, "donate_max")) {
-            if (value < 0 || value > 0xFFFFFFFFll) return TM_EINVAL;
-            e->donate_max = (uint32_t)value;
-            return TM_OK;
-        }
-        if (!std::strcmp(name, "root_split")) {   // each topic walked as two queue items (kernels.h QueueBufs)
-            if (value < 0 || value > 1) return TM_EINVAL;
-            e->root_split = (int)value;
             return TM_OK;
         }
         if (!std::strcmp(name, "shape_keys")) {

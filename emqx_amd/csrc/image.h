@@ -100,24 +100,6 @@ struct alignas(SLOT_RECORD ? 32 : 16) EdgeSlot {
 };
 static_assert(sizeof(EdgeSlot) == (SLOT_RECORD ? 32 : 16), "edge slot is one or two 16 B halves");
 
-// Per-node child blocks (option "blocks"): a WIDE node's literal children
-// in an open-addressing block of its own in one pool, instead of the shared
-// edge table.  The node's inner half then holds lw = the block's first slot
-// and lc = log2(slots) << 27 | a 27-bit Bloom mask of the children's words.
-// A lookup probes from home slot block_home(w) within the block.  Blocks are
-// laid out in node order (hot nodes first under the heat order), so the
-// blocks of the nodes every topic visits share few lines: the shared table
-// scatters a node's children over a line each, blocks pack four to a line.
-struct alignas(16) BlockSlot {
-    uint32_t word;         // child's word, WORD_NONE when free
-    uint32_t child;        // child node id
-    uint32_t sum;          // S(child), its subtree summary
-    uint32_t pad;
-};
-static_assert(sizeof(BlockSlot) == 16, "block slot is one 16 B load");
-constexpr uint32_t BLOCK_LOG2_SHIFT = 27;
-constexpr uint32_t BLOCK_BLOOM_MASK = (1u << BLOCK_LOG2_SHIFT) - 1;
-
 // Dictionary slot: the tokenizer's first 16 B load decides a word of <= 8
 // bytes on its own (tag, id and the bytes), a word of 9-16 bytes with the
 // second half (same 32 B, an L2 hit), a longer one against the arena.
@@ -140,7 +122,6 @@ struct ImageView {
     const EdgeSlot* edges;
     uint64_t        edge_slot_mask;    // slots - 1 (power of two)
     const EdgeSlot* hot_edges;         // edges of parents with id < hot_limit
-    const BlockSlot* blocks;           // option "blocks": WIDE nodes' literal children (null: in edges[])
     uint64_t        hot_slot_mask;
     uint32_t        hot_limit;
     const DictSlot* dict;
@@ -278,14 +259,6 @@ TM_HD uint64_t word_bloom(uint32_t w) {
     }
     const uint32_t h = w * 0x9E3779B1u;
     return (1ull << (h >> 26)) | (1ull << ((h >> 20) & 63u));
-}
-
-// child blocks: the home slot of word w in a block of 2^k slots (the top k
-// bits of its Fibonacci hash), and its two Bloom bits among the node's 27
-TM_HD uint32_t block_home(uint32_t w, uint32_t k) { return k ? (w * 0x9E3779B1u) >> (32 - k) : 0u; }
-TM_HD uint32_t block_bloom(uint32_t w) {
-    const uint32_t h = w * 0x85EBCA77u;
-    return (1u << (((h & 0xFFFFu) * 27u) >> 16)) | (1u << (((h >> 16) * 27u) >> 16));
 }
 
 // home slot of key (parent, word): a 32-bit mix (three 32-bit multiplies)

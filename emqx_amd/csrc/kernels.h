@@ -14,7 +14,6 @@ constexpr size_t QWS_BYTES = 3328;   // queue heads: 8 ranges x 128 B, 8 spill c
 constexpr size_t QWS_MAXC = 120;     // u64 slot of ws: the batch's largest match count
 constexpr size_t QWS_MAXL = 121;     // u64 slot of ws: most levels of a topic in a keyed batch
 constexpr size_t QWS_SPILL = 128;    // u64 slots 128 + 16 x: spill chunks taken by XCD x's waves
-constexpr size_t QWS_PIECE = 129;    // u64 slots 129 + 16 x: pieces donated by XCD x's waves (option "donate")
 // u64 slots 256 + 16 x (per-lane queue walks with XCD ranges; diagnostics,
 // tm_debug_walk_clocks): wall clock of XCD x's first wave start (stored
 // inverted: max of ~t), of its home range's first exhaustion (inverted), of
@@ -53,33 +52,6 @@ struct QueueBufs {
                                  // tail_key: heavy topics first in each XCD range, one radix pass)
     uint32_t sort_passes = 4;    // mode 1: radix passes over the key's top 8 * sort_passes bits (1..4)
     uint32_t light_max = 31;     // mode 6: cost classes <= light_max are walked last in their XCD range
-    // option "root_split": every topic is two queue items, 2t = the root's
-    // '+' subtree and 2t + 1 = the rest (the root's '#' filter and literal
-    // subtree), each with its own stage row (K slots), count (icounts) and
-    // spill head; their concatenation in item order IS the topic's list in
-    // emqx_trie:match/1 order (the '+' subtree is discovered last, so it is
-    // output first).  The item CSR (ioff, over 2n) is scanned and copied as
-    // usual, then folded into the topics' counts and offsets.  Halves the
-    // longest work item, so the walk's drain (lanes finishing their last
-    // topic while the queue is dry) shortens.  Unkeyed chunk-row walks only;
-    // long topics (> WREG levels) stay one item (2t + 1; 2t empty).
-    bool root_split = false;
-    uint32_t* icounts = nullptr;   // 2n
-    uint64_t* ioff = nullptr;      // 2n + 1
-    // option "donate": once the queues are dry, a lane still walking hands
-    // its shallowest pending '+' subtree (at least don_min levels deep) to an
-    // idle lane of its wave -- a piece with its own stage row (prow), linked
-    // into the topic's ordered list of pieces (kernels.hip DonBufs).  Unkeyed
-    // chunk-row walks only.
-    bool donate = false;
-    uint32_t don_min = 2;
-    uint32_t don_busy = 8;       // ... while at most don_busy lanes of the wave still walk
-    uint32_t* prow = nullptr;    // pcap x K
-    uint32_t* pdesc = nullptr;   // pcap x 4: topic, next piece, node, level | levels << 8
-    uint32_t* pcnt = nullptr;    // pcap x 2: count, spill head
-    uint32_t* tfirst = nullptr;  // n: the first piece of a topic that donated
-    uint32_t* dmask = nullptr;   // n / 32 + 1: topics that donated
-    uint32_t pcap = 0;           // a multiple of QRANGES (8)
     // the radix passes of the batch's presort: the tokenizer writes the keys
     // and values where the first pass reads them, so the last ends in perm
     uint32_t presort_passes() const { return presort_mode == 2 ? 1u : presort_mode == 4 ? 2u : sort_passes; }
@@ -116,8 +88,6 @@ hipError_t launch_presort(const uint32_t* twords, const uint32_t* meta, uint32_t
 // chunk's rows through perm and writes stage rows, counts and spill heads by
 // topic, so the ordinary copy-out (and spill) applies.
 bool queue_rows_by_position(const QueueBufs& qb, bool stats_mode);
-// the walk kernels of this build read per-node child blocks (TM_BLOCKS_PATH)
-bool kernels_have_blocks();
 
 // tokenize -> NFA walk -> scan -> copy-out, all on st.  marks: 8 events,
 // [2i] before / [2i+1] after stage i, or null.  out_cap == 0: counts and

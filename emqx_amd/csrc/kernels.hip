@@ -455,10 +455,6 @@ struct Hit {
 #define TM_WALK_CLOCKS 0   // diagnostic builds: the queue walk's per-XCD phase clocks (QWS_CLOCK,
                            // tm_debug_walk_clocks); 4 VGPRs of the walk, so off in the product build
 #endif
-#ifndef TM_BLOCKS_PATH
-#define TM_BLOCKS_PATH 0   // A/B builds: the walks' child-block lookups (option "blocks": measured slower,
-                           // DESIGN 5.2c; 3 VGPRs of the walk), 0: the shared edge table only
-#endif
 // literal (or '#') edge (v, w) in the edge table: linear probing, one 16 B
 // key half per slot (load factor <= 1/4: ~1.2 loads per hit); on a hit the
 // slot's second half completes the child's record
@@ -496,18 +492,6 @@ __device__ __forceinline__ Hit lit_child(const ImageView& im, uint32_t v, uint32
     const Hit none{NODE_NONE, 0, 0, 0, 0, 0, false};
     if (w < WORD_MAX) {
         if (!(plus & WIDE)) return Hit{lw == w ? lc : NODE_NONE, SUM_ALL, 0, 0, 0, 0, false};
-        if (TM_BLOCKS_PATH && im.blocks) {   // option "blocks": the node's own block (lw = first slot, lc = log2 size | Bloom)
-            const uint32_t bb = block_bloom(w);
-            if ((lc & bb) != bb) return none;
-            const uint32_t k = lc >> BLOCK_LOG2_SHIFT, m = (1u << k) - 1u;
-            const BlockSlot* blk = im.blocks + lw;
-            for (uint32_t p = block_home(w, k);; p = (p + 1) & m) {
-                const uint4 e = reinterpret_cast<const uint4*>(blk + p)[0];
-                if (STATS) ++loads;
-                if (e.x == w) return Hit{e.y, e.z, 0, 0, 0, 0, false};   // e.z: S(child)
-                if (e.x == WORD_NONE) return none;
-            }
-        }
         const uint64_t b = word_bloom(w);
         const uint64_t mask = ((uint64_t)lc << 32) | lw;
         return (mask & b) == b ? probe_edge<STATS>(im, v, w, loads) : none;
@@ -573,9 +557,6 @@ constexpr int HIST_OFF = 8;   // hist = stats + HIST_OFF
 #ifndef TM_PEND_MASK
 #define TM_PEND_MASK 1   // A/B at C3: walk 9.78 vs 10.08-10.09 ms (profiles/r03_ab)
 #endif
-// Cursor::pend bit 31 (option "root_split", item 2t + 1): the root's '+'
-// child is not visited (item 2t walks that subtree)
-constexpr uint32_t ROOT_NOPLUS = 1u << 31;
 struct Cursor {
     uint32_t v, r, n, r0;   // node to visit next and its level; topic levels; start level
     uint32_t pend;          // TM_PEND_MASK: bit k = path(k) holds a '+' child still to visit (k < r)
@@ -789,8 +770,7 @@ __device__ __forceinline__ bool walk_step(const ImageView& im, Cursor& c, Path p
         }
         if (STATS) st.prunable += (g.child != NODE_NONE && !lit_ok ? 1u : 0u) +
                                   ((plus & NODE_MASK) != NODE_NONE && !plus_ok ? 1u : 0u);
-        const uint32_t pc = ((STATS || plus_ok) && !(r == 0 && (c.pend & ROOT_NOPLUS))) ? (plus & NODE_MASK)
-                                                                                          : NODE_NONE;
+        const uint32_t pc = (STATS || plus_ok) ? (plus & NODE_MASK) : NODE_NONE;
         if (STATS && st.hist) {   // how the next visit is reached: [48] inline literal, [49] table literal,
                                   // [50] '+' (here or by a later pop: counted at the pop)
             if (g.child != NODE_NONE) atomicAdd(st.hist + ((plus & WIDE) ? 49 : 48), 1ull);
@@ -835,42 +815,6 @@ __device__ __forceinline__ void walk(const ImageView& im, uint32_t n, bool dolla
     Cursor c;
     if (!walk_begin(im, c, n, dollar, W, st)) return;
     while (!walk_step<STATS, KEYS>(im, c, path, W, emit, st)) {
-    }
-}
-
-// option "root_split": the start of item `part` of a topic.  Part 0 walks
-// the root's '+' subtree (from level 1; nothing for '$' topics, whose walk
-// skips the root's '+' and '#', emqx_trie.erl:121-122); part 1 the rest,
-// the root's '+' child left out.  Discovery order: the root's '#' filter,
-// its literal subtree (part 1), then its '+' subtree (part 0), so the
-// reversed lists concatenate as part 0's then part 1's.
-template <class Words>
-__device__ __forceinline__ bool walk_begin_part(const ImageView& im, Cursor& c, uint32_t n, bool dollar,
-                                                const Words& W, WalkStats& st, uint32_t part) {
-    if (part) {
-        const bool go = walk_begin(im, c, n, dollar, W, st);
-        if (!dollar) c.pend |= ROOT_NOPLUS;
-        return go;
-    }
-    c.n = n;
-    c.key = 0;
-    c.pend = 0;
-    c.pf_id = NODE_NONE;
-    if (dollar) return false;
-    const uint4 q = load_half(im, ROOT, false);
-    const uint32_t pc = q.x & NODE_MASK;
-    if (pc == NODE_NONE || ((q.y & SUM_TAG) && !sum_useful(q.y & SUM_ALL, n - 1))) return false;
-    c.v = pc;
-    c.r = c.r0 = 1;
-    return true;
-}
-// a whole walk of one item (part < 2) or topic (part = 2), global path
-template <class Words, class Emit>
-__device__ __forceinline__ void walk_item(const ImageView& im, uint32_t n, bool dollar, GlobalPath path,
-                                          const Words& W, Emit& emit, WalkStats& st, uint32_t part) {
-    Cursor c;
-    if (part < 2 ? !walk_begin_part(im, c, n, dollar, W, st, part) : !walk_begin(im, c, n, dollar, W, st)) return;
-    while (!walk_step<false, false>(im, c, path, W, emit, st)) {
     }
 }
 
@@ -1027,40 +971,12 @@ constexpr uint32_t NO_TOPIC = 0xFFFFFFFFu;
 // walk itself, dropping tm_tokenize, measured 13.15-15.89 ms: the tokenizer's
 // registers cut the walk's occupancy.)
 constexpr uint32_t CW = 8;   // words per topic in the chunk's LDS rows
-constexpr int CH_NONE = 0, CH_ROWS = 1, CH_DON = 2;   // CH_DON: chunk rows + option "donate"
+constexpr int CH_NONE = 0, CH_ROWS = 1;
 struct ChunkRows {
     uint32_t w[QCHUNK][CW];
     uint32_t meta[QCHUNK];
     uint32_t topic[QCHUNK];   // the topic at each queue position (presorted batches: perm)
 };
-// Option "donate" (CH_DON): the walk's drain.  Once a wave's queues are
-// dry, its lanes finish the topics they hold while the others idle (at 1M
-// C3 topics a third of the walk).  A lane still walking then hands its
-// shallowest pending '+' child (the path entry walk_pop would take last) to
-// an idle lane of its wave, which walks that subtree as a piece of the
-// topic: own stage row in the piece pool, count, spill chain.  The fold of
-// emqx_trie.erl:130-136 discovers the shallowest pending subtree after all
-// the rest of the donor's walk, and the list is the discovery order
-// reversed, so the piece's list goes right BEFORE the donor's remaining
-// list: each topic's pieces form a list (tfirst[t], pdesc next) ending in
-// the topic's own row (PIECE_SELF), kept in order by inserting each new
-// piece before its donor (a lane holds its own predecessor, prv).  Every
-// piece of a topic lives in one wave, so the list is only changed by one
-// wave, one insertion per piece per round.  tm_add_pieces adds the pieces'
-// counts to their topics; tm_copy_out concatenates the lists of topics in
-// dmask.  Subtrees with fewer than don_min levels below them stay.
-constexpr uint32_t PIECE_SELF = 0xFFFFFFFEu;   // the end of a topic's piece list: its own row
-constexpr uint32_t NO_PIECE = 0xFFFFFFFFu;
-struct DonBufs {
-    uint32_t* prow;     // pcap x K
-    uint4* pdesc;       // topic, next, node, level | levels << 8
-    uint2* pcnt;        // count, spill head
-    uint32_t* tfirst;   // n
-    uint32_t* dmask;    // null: no donation in this batch
-    uint32_t pcap, don_min;
-    uint32_t max_busy;   // donate only while at most this many lanes of the wave still walk
-};
-
 template <bool STATS, bool XCDQ, bool KEYS, int CH>
 __device__ __forceinline__ void
 walk_queue_body(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const uint32_t* __restrict__ twords,
@@ -1070,16 +986,9 @@ walk_queue_body(ImageView im, const uint64_t* __restrict__ off, uint32_t n, cons
               unsigned long long* __restrict__ ws, unsigned long long* __restrict__ stats,
               unsigned long long* __restrict__ hist, const uint32_t* __restrict__ perm,
               const uint32_t* __restrict__ twords_s, const uint32_t* __restrict__ meta_s,
-              uint32_t* __restrict__ spill, uint32_t* __restrict__ spill_head, uint32_t spill_chunks, uint32_t split,
-              DonBufs don) {
+              uint32_t* __restrict__ spill, uint32_t* __restrict__ spill_head, uint32_t spill_chunks) {
     static_assert(CH == CH_NONE || (!STATS && !KEYS), "chunk rows: unkeyed walks in arrival order only");
-    constexpr bool DON = CH == CH_DON && TM_PEND_MASK;
-    if (DON) split = 0;
-    // queue positions: n topics, or 2n items (option "root_split": chunk-row
-    // walks only; position p is item p & 1 of topic p >> 1, stage row,
-    // count and spill head by item 2 x topic + part)
-    if (CH == CH_NONE) split = 0;
-    const uint32_t nq = n << split;
+    const uint32_t nq = n;
     __shared__ uint32_t lds_path[WREG * BLOCK];
     __shared__ ChunkRows lds_chunk[CH != CH_NONE ? BLOCK / 64 : 1];
     const uint32_t lane = threadIdx.x & 63;
@@ -1094,11 +1003,6 @@ walk_queue_body(ImageView im, const uint64_t* __restrict__ off, uint32_t n, cons
     const uint32_t home = XCDQ ? xcc_id() : 0u;
     uint32_t qr = 0;                   // ranges given up so far (uniform)
     uint32_t my = NO_TOPIC, myt = 0;   // the lane's queue position and its topic
-    // DON, once dry: the lane's piece (PIECE_SELF: its topic's own row) and
-    // its predecessor in the topic's list, in LDS past the exchange slots
-    // (the chunk rows are free then; no registers held across the walk)
-    uint32_t* const dstate = reinterpret_cast<uint32_t*>(&CR) + 512 + 2 * lane;
-    bool don_init = false, pool_full = false;   // (uniform)
     bool is_long = false, drained = false;
     Cursor cur;
     RowEmit<KEYS> em{nullptr, nullptr, K, 0, {}, 0ull, KW, (uint64_t)n * K};
@@ -1168,9 +1072,8 @@ walk_queue_body(ImageView im, const uint64_t* __restrict__ off, uint32_t n, cons
                 if (t < gend) {
                     // a presorted batch: queue position t walks topic perm[t], whose row
                     // is read here (the rows are not gathered into walk order)
-                    const uint32_t tq = t >> split;
-                    const uint32_t tt = perm ? stream_load(perm + tq) : tq;
-                    CR.topic[lane] = (tt << split) | (t & split);   // the item (= the topic without split)
+                    const uint32_t tt = perm ? stream_load(perm + t) : t;
+                    CR.topic[lane] = tt;
                     CR.meta[lane] = stream_load(meta + tt);
                     const uint4* src = reinterpret_cast<const uint4*>(twords + (uint64_t)tt * WREG);
                     const uint4 a0 = stream_load16(src), a1 = stream_load16(src + 1);   // quad 1 may be stale: unread
@@ -1191,11 +1094,11 @@ walk_queue_body(ImageView im, const uint64_t* __restrict__ off, uint32_t n, cons
                 if (rank < avail) i = qnext + rank;
                 else if (g + (rank - avail) < gend) i = g + (rank - avail);
                 if (i != NO_TOPIC) {
-                    // i: queue position = stage row; ti: the topic; item: the
-                    // stage row / count / spill head (CH: by topic or item, so a
+                    // i: queue position = stage row; item = ti: the topic, whose
+                    // stage row / count / spill head it is (CH: by topic, so a
                     // presorted batch needs no position-ordered copy-out)
                     const uint32_t item = CH != CH_NONE ? CR.topic[i - cbase] : perm ? perm[i] : i;
-                    const uint32_t ti = item >> split, part = item & split;
+                    const uint32_t ti = item;
                     const uint32_t* tws = CH == CH_NONE && perm ? twords_s : twords;
                     const uint32_t mt = CH != CH_NONE ? CR.meta[i - cbase] : perm ? meta_s[i] : meta[i];
                     const uint32_t nl = mt & MN;
@@ -1221,8 +1124,7 @@ walk_queue_body(ImageView im, const uint64_t* __restrict__ off, uint32_t n, cons
                         rw.w[5] = a1.y;
                         rw.w[6] = a1.z;
                         rw.w[7] = a1.w;
-                        go = split ? walk_begin_part(im, cur, nl, dollar, rw, st, part)
-                                   : walk_begin(im, cur, nl, dollar, rw, st);
+                        go = walk_begin(im, cur, nl, dollar, rw, st);
                     } else if (!is_long) {
 #pragma unroll
                         for (uint32_t k = 0; k < WREG / 4; ++k) {
@@ -1235,15 +1137,12 @@ walk_queue_body(ImageView im, const uint64_t* __restrict__ off, uint32_t n, cons
                                 rw.w[4 * k + 3] = x.w;
                             }
                         }
-                        go = split ? walk_begin_part(im, cur, nl, dollar, rw, st, part)
-                                   : walk_begin(im, cur, nl, dollar, rw, st);
+                        go = walk_begin(im, cur, nl, dollar, rw, st);
                     } else {
                         const uint64_t b = off[ti] - off[0];
                         mw = MemWords{tw, words + b + ti};
                         gp.base = gpath + b + 2ull * ti;
-                        // a long topic is one item (2t + 1: the whole walk; 2t empty):
-                        // its global path area is the topic's
-                        go = (split && !part) ? false : walk_begin(im, cur, nl, dollar, mw, st);
+                        go = walk_begin(im, cur, nl, dollar, mw, st);
                     }
                     if (go) {
                         my = i;
@@ -1268,95 +1167,14 @@ walk_queue_body(ImageView im, const uint64_t* __restrict__ off, uint32_t n, cons
                 qnext = qend;
             }
         }
-        if (DON && exhausted) {
-            // the drain: pair the j-th idle lane with the j-th lane that has
-            // a pending '+' subtree deep enough (uniform block)
-            if (!don_init) {   // every lane's topic is its own row so far
-                dstate[0] = PIECE_SELF;
-                dstate[1] = NO_PIECE;
-                don_init = true;
-                wave_sync_lds();
-            }
-            const uint64_t idle = __ballot(my == NO_TOPIC);
-            const bool tail = 64u - (uint32_t)__popcll(idle) <= don.max_busy;   // the wave's last walkers
-            const uint32_t lim = cur.n > don.don_min ? cur.n - don.don_min : 0u;   // levels k < lim qualify
-            const uint32_t pm = (tail && my != NO_TOPIC && !is_long) ? cur.pend & ((1u << (lim < WREG ? lim : WREG)) - 1u) : 0u;
-            const uint64_t dm = __ballot(pm != 0);
-            if (tail && idle && dm && !pool_full) {
-                const uint32_t ni = (uint32_t)__popcll(idle), nd = (uint32_t)__popcll(dm);
-                uint32_t np = ni < nd ? ni : nd;
-                const uint32_t x = xcc_id(), capx = don.pcap / QRANGES;
-                uint32_t at = 0;
-                if (lane == 0) at = (uint32_t)atomicAdd(ws + QWS_PIECE + 16 * x, (unsigned long long)np);
-                at = __shfl(at, 0, 64);
-                np = at >= capx ? 0u : (np < capx - at ? np : capx - at);
-                pool_full = at + np >= capx;
-                if (np) {
-                    const uint32_t dr = __builtin_amdgcn_mbcnt_hi((uint32_t)(dm >> 32),
-                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)dm, 0u));
-                    const uint32_t ir = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
-                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
-                    // the exchange slots: the chunk's LDS rows (no topic is taken from them once dry)
-                    uint4* xs = reinterpret_cast<uint4*>(&CR);
-                    if (pm && dr < np) {   // the donor: its subtree to slot dr (the piece's records: its donee)
-                        const uint32_t k = (uint32_t)__builtin_ctz(pm);
-                        xs[dr] = make_uint4(myt, lp(k), (k + 1) | (cur.n << 8) | (lane << 16), 0u);
-                        cur.pend &= ~(1u << k);
-                    }
-                    wave_sync_lds();
-                    if (my == NO_TOPIC && ir < np) {   // take piece y = ir: insert it before its donor's
-                        const uint4 a = xs[ir];
-                        uint32_t* const ds = reinterpret_cast<uint32_t*>(&CR) + 512 + 2 * (a.z >> 16);
-                        const uint32_t y = x * capx + at + ir, prv = ds[1];
-                        don.pdesc[y] = make_uint4(a.x, ds[0], a.y, a.z & 0xFFFFu);
-                        if (prv == NO_PIECE) don.tfirst[a.x] = y;
-                        else reinterpret_cast<uint32_t*>(don.pdesc + prv)[1] = y;
-                        ds[1] = y;
-                        dstate[0] = y;
-                        dstate[1] = prv;
-                        myt = a.x;
-                        const uint32_t nl = (a.z >> 8) & 255u;
-                        const uint4* src = reinterpret_cast<const uint4*>(twords + (uint64_t)a.x * WREG);
-#pragma unroll
-                        for (uint32_t k = 0; k < WREG / 4; ++k) {
-                            if (4 * k < nl) {
-                                const uint4 q = src[k];
-                                rw.w[4 * k] = q.x;
-                                rw.w[4 * k + 1] = q.y;
-                                rw.w[4 * k + 2] = q.z;
-                                rw.w[4 * k + 3] = q.w;
-                            }
-                        }
-                        cur.v = a.y;
-                        cur.r = cur.r0 = a.z & 255u;
-                        cur.n = nl;
-                        cur.pend = 0;
-                        cur.key = 0;
-                        cur.pf_id = NODE_NONE;
-                        em.row = don.prow + (uint64_t)y * K;
-                        em.cnt = 0;
-                        em.sfail = false;
-                        is_long = false;
-                        my = 0;   // (any position: a piece reads no chunk row)
-                    }
-                    wave_sync_lds();
-                }
-            }
-        }
         if (__all(my == NO_TOPIC && drained)) break;
         if (my == NO_TOPIC) continue;
         const bool fin = is_long ? walk_step<STATS, KEYS>(im, cur, gp, mw, em, st)
                                  : walk_step<STATS, KEYS>(im, cur, lp, rw, em, st);
         if (fin) {
             em.flush();
-            const uint32_t mypid = DON && don_init ? dstate[0] : PIECE_SELF;
-            if (DON && mypid != PIECE_SELF) {
-                don.pcnt[mypid] = make_uint2(em.cnt, em.cnt > K && spill && !em.sfail ? em.shead : NO_SPILL);
-            } else {
-                counts[myt] = em.cnt;
-                if (!KEYS && spill && em.cnt > K) spill_head[myt] = em.sfail ? NO_SPILL : em.shead;
-                if (DON && don_init && dstate[1] != NO_PIECE) atomicOr(don.dmask + (myt >> 5), 1u << (myt & 31u));
-            }
+            counts[myt] = em.cnt;
+            if (!KEYS && spill && em.cnt > K) spill_head[myt] = em.sfail ? NO_SPILL : em.shead;
             match_sum += em.cnt;
             maxc = em.cnt > maxc ? em.cnt : maxc;
             my = NO_TOPIC;
@@ -1385,31 +1203,10 @@ tm_walk_queue(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const 
               unsigned long long* __restrict__ ws, unsigned long long* __restrict__ stats,
               unsigned long long* __restrict__ hist, const uint32_t* __restrict__ perm,
               const uint32_t* __restrict__ twords_s, const uint32_t* __restrict__ meta_s,
-              uint32_t* __restrict__ spill, uint32_t* __restrict__ spill_head, uint32_t spill_chunks, uint32_t split,
-              DonBufs don) {
+              uint32_t* __restrict__ spill, uint32_t* __restrict__ spill_head, uint32_t spill_chunks) {
     walk_queue_body<STATS, XCDQ, KEYS, CH>(im, off, n, twords, words, meta, gpath, stage, kstage, K, KW, counts, ws, stats, hist, perm, twords_s, meta_s,
-                                     spill, spill_head, spill_chunks, split, don);
+                                     spill, spill_head, spill_chunks);
 }
-// option "donate": its own kernel, held to the chunk-row walk's 6 waves per
-// SIMD (the drain's donation code would otherwise cost a wave: 84 VGPRs)
-#ifndef TM_DON_WAVES
-#define TM_DON_WAVES 6
-#endif
-template <bool XCDQ>
-__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(TM_DON_WAVES, 8)))
-tm_walk_queue_don(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const uint32_t* __restrict__ twords,
-              const uint32_t* __restrict__ words, const uint32_t* __restrict__ meta, uint32_t* __restrict__ gpath,
-              uint32_t* __restrict__ stage, uint64_t* __restrict__ kstage, uint32_t K, uint32_t KW,
-              uint32_t* __restrict__ counts,
-              unsigned long long* __restrict__ ws, unsigned long long* __restrict__ stats,
-              unsigned long long* __restrict__ hist, const uint32_t* __restrict__ perm,
-              const uint32_t* __restrict__ twords_s, const uint32_t* __restrict__ meta_s,
-              uint32_t* __restrict__ spill, uint32_t* __restrict__ spill_head, uint32_t spill_chunks, uint32_t split,
-              DonBufs don) {
-    walk_queue_body<false, XCDQ, false, CH_DON>(im, off, n, twords, words, meta, gpath, stage, kstage, K, KW, counts, ws, stats, hist, perm, twords_s, meta_s,
-                                     spill, spill_head, spill_chunks, split, don);
-}
-
 // ---------------------------------------------------------------------------
 // tm_walk_wave: the low-latency walk (small batches: engine option
 // "wave_walk_max").  One wave per topic, level by level: at level r the
@@ -1717,37 +1514,28 @@ constexpr uint32_t COPY_U = TM_COPY_U;
 // is its filter's order key im.fshape[id] (image.h filter_shape), and a
 // topic with a literal '+' / '#' level (MOOD: its walk repeats subtrees, so
 // keys by filter would tie) is re-walked keyed here, all of its outputs.
-template <bool KEYS, bool SHAPED, bool DONP = false>
+template <bool KEYS, bool SHAPED>
 __global__ void __launch_bounds__(BLOCK)
 tm_copy_out(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const uint32_t* __restrict__ twords,
             const uint32_t* __restrict__ words, const uint32_t* __restrict__ meta, uint32_t* __restrict__ gpath,
             const uint32_t* __restrict__ stage, const uint64_t* __restrict__ kstage, uint32_t K, uint32_t KW,
             const uint32_t* __restrict__ counts, const uint64_t* __restrict__ out_off, uint32_t* __restrict__ out,
             uint64_t* __restrict__ kout, uint64_t out_cap, const uint32_t* __restrict__ spill,
-            const uint32_t* __restrict__ spill_head, uint32_t split, DonBufs don) {
-    // split (option "root_split", unkeyed): n counts 2x the topics' items;
-    // item x is part x & 1 of topic x >> 1 (its rows, words and path area)
-    // don.dmask (option "donate", unkeyed): topics whose list is pieces, in
-    // the loop at the end
+            const uint32_t* __restrict__ spill_head) {
     const uint64_t kplane = (uint64_t)n * K;   // KEYS: key word j of stage slot x at kstage[j * kplane + x],
                                                // of output p at kout[j * out_cap + p]
     __shared__ uint32_t lds_inc[BLOCK];
     __shared__ uint64_t lds_scan[BLOCK / 64];
-    __shared__ uint32_t lds_don[DONP ? BLOCK / 32 : 1];
     const uint32_t t0 = blockIdx.x * BLOCK;
     const uint32_t tn = n - t0 < (uint32_t)BLOCK ? n - t0 : (uint32_t)BLOCK;
     const uint32_t c = threadIdx.x < tn ? counts[t0 + threadIdx.x] : 0u;
-    const bool donb = DONP && !KEYS && !SHAPED && don.dmask != nullptr;
-    if (DONP && donb && threadIdx.x < BLOCK / 32)   // (t0 is a multiple of 32)
-        lds_don[threadIdx.x] = t0 + 32 * threadIdx.x < n ? don.dmask[(t0 >> 5) + threadIdx.x] : 0u;
     uint64_t agg;
     const uint64_t ex = block_exclusive_scan(c, lds_scan, agg);
     lds_inc[threadIdx.x] = (uint32_t)(ex + c);
     __syncthreads();
     const uint64_t base = out_off[t0];
-    auto pieces = [&](uint32_t lt) { return donb && ((lds_don[lt >> 5] >> (lt & 31u)) & 1u) != 0; };
-    // topics copied by the loops below: not out-of-domain (SHAPED) and not in pieces
-    auto ood = [&](uint32_t lt) { return (SHAPED && (meta[t0 + lt] & MOOD) != 0) || pieces(lt); };
+    // topics copied by the loops below: not out-of-domain (SHAPED)
+    auto ood = [&](uint32_t lt) { return SHAPED && (meta[t0 + lt] & MOOD) != 0; };
     auto put = [&](uint64_t p, uint32_t id) {
         if (TM_COPY_NT) __builtin_nontemporal_store(id, out + p);
         else out[p] = id;
@@ -1883,10 +1671,10 @@ tm_copy_out(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const ui
         }
     }
     const bool tail = c > K && (KEYS || !spill || spill_head[t0 + threadIdx.x] == NO_SPILL);
-    if (threadIdx.x < tn && !pieces(threadIdx.x) && (tail || ood(threadIdx.x))) {
+    if (threadIdx.x < tn && (tail || ood(threadIdx.x))) {
         // fan-out beyond the stage row and no spill: walk again, write the
         // head; SHAPED: keyed, and every output of an out-of-domain topic
-        const uint32_t x = t0 + threadIdx.x, t = x >> split;   // item, topic
+        const uint32_t t = t0 + threadIdx.x;
         const uint32_t mt = meta[t];
         const uint64_t b = off[t] - off[0];
         const MemWords mw{twords + (uint64_t)t * WREG, words + b + t};
@@ -1894,90 +1682,9 @@ tm_copy_out(ImageView im, const uint64_t* __restrict__ off, uint32_t n, const ui
         TailEmit<WK> em{out, kout, base + ex, out_cap, ood(threadIdx.x) ? 0u : K, c, 0, KW, out_cap};
         WalkStats s2;
         // the topic's global path area (the walk's, for long topics): no LDS
-        // path here, so the copy-out's blocks stay small (1.3 KB of LDS);
-        // split: item 2t re-walks in a second area past the first (the
-        // engine sizes the path buffer twice over), item 2t + 1 in the topic's
-        if (!WK && split) {
-            const uint32_t nt = n >> 1;
-            const uint64_t second = (x & 1u) ? 0 : (off[nt] - off[0]) + 2ull * nt + 2;
-            // a long topic is item 2t + 1 alone (its walk is the whole topic)
-            const uint32_t part = (mt & MLONG) ? 2u : (x & 1u);
-            walk_item(im, mt & MN, (mt & MDOLLAR) != 0, GlobalPath{gpath + second + b + 2ull * t}, mw, em, s2, part);
-        } else {
-            walk<false, WK>(im, mt & MN, (mt & MDOLLAR) != 0, GlobalPath{gpath + b + 2ull * t}, mw, em, s2);
-        }
+        // path here, so the copy-out's blocks stay small (1.3 KB of LDS)
+        walk<false, WK>(im, mt & MN, (mt & MDOLLAR) != 0, GlobalPath{gpath + b + 2ull * t}, mw, em, s2);
     }
-    if (DONP && donb) {
-        // topics whose list is pieces (option "donate"), one wave per topic:
-        // the pieces in list order, then the topic's own row; a part past K
-        // ids without a spill chain re-walks the whole topic (lane 0, every
-        // output)
-        const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-        auto copy_part = [&](const uint32_t* row, uint32_t pc, uint32_t sh, uint64_t o) {
-            for (uint32_t j = (pc > K ? pc - K : 0u) + lane; j < pc; j += 64)
-                if (o + j < out_cap) put(o + j, row[K + j - pc]);
-            if (pc > K) {   // the head from the spill chain (reverse discovery order)
-                uint32_t cur = sh;
-                const uint32_t m = pc - K;
-                for (uint32_t o0 = 0; o0 < m; o0 += SPILL_CHUNK - 1) {
-                    for (uint32_t j = lane; j < SPILL_CHUNK - 1 && o0 + j < m; j += 64) {
-                        const uint64_t p = o + m - 1 - (o0 + j);
-                        if (p < out_cap) put(p, spill[(uint64_t)cur * SPILL_CHUNK + 1 + j]);
-                    }
-                    if (o0 + SPILL_CHUNK - 1 < m) cur = spill[(uint64_t)cur * SPILL_CHUNK];
-                }
-            }
-        };
-        for (uint32_t lt = w; lt < tn; lt += BLOCK / 64) {
-            if (!pieces(lt)) continue;
-            const uint32_t t = t0 + lt;
-            const uint32_t prev = lt ? lds_inc[lt - 1] : 0u;
-            const uint32_t ct = lds_inc[lt] - prev;
-            const uint64_t ob = base + prev;
-            uint32_t sum = 0;
-            bool rew = false;
-            for (uint32_t y = don.tfirst[t]; y != PIECE_SELF; y = don.pdesc[y].y) {
-                const uint2 pc = don.pcnt[y];
-                sum += pc.x;
-                rew |= pc.x > K && pc.y == NO_SPILL;
-            }
-            const uint32_t own = ct - sum;
-            rew |= own > K && (!spill || spill_head[t] == NO_SPILL);
-            if (rew) {
-                if (lane == 0) {
-                    const uint32_t mt = meta[t];
-                    const uint64_t b = off[t] - off[0];
-                    const MemWords mw{twords + (uint64_t)t * WREG, words + b + t};
-                    TailEmit<false> em{out, kout, ob, out_cap, 0u, ct, 0, KW, out_cap};
-                    WalkStats s2;
-                    walk<false, false>(im, mt & MN, (mt & MDOLLAR) != 0, GlobalPath{gpath + b + 2ull * t}, mw, em, s2);
-                }
-                continue;
-            }
-            uint64_t o = ob;
-            for (uint32_t y = don.tfirst[t];; y = don.pdesc[y].y) {
-                const bool self = y == PIECE_SELF;
-                uint2 pc = make_uint2(own, own > K ? spill_head[t] : NO_SPILL);
-                if (!self) pc = don.pcnt[y];
-                copy_part(self ? stage + (uint64_t)t * K : don.prow + (uint64_t)y * K, pc.x, pc.y, o);
-                o += pc.x;
-                if (self) break;
-            }
-        }
-    }
-}
-
-// option "donate": each donated piece's count onto its topic's (the pieces
-// of XCD x are pdesc[x * pcap / 8 + i], i < the XCD's counter)
-__global__ void __launch_bounds__(BLOCK)
-tm_add_pieces(const unsigned long long* __restrict__ ws, const uint4* __restrict__ pdesc,
-              const uint2* __restrict__ pcnt, uint32_t pcap, uint32_t* __restrict__ counts) {
-    const uint32_t p = blockIdx.x * BLOCK + threadIdx.x;
-    const uint32_t capx = pcap / QRANGES;
-    if (p >= pcap) return;
-    const uint32_t x = p / capx, i = p - x * capx;
-    const unsigned long long taken = ws[QWS_PIECE + 16 * x];
-    if (i < taken) atomicAdd(counts + pdesc[p].x, pcnt[p].x);
 }
 
 // tm_copy_out over a presorted walk (option "presort"): stage row p holds
@@ -2029,21 +1736,6 @@ tm_copy_out_sorted(ImageView im, const uint64_t* __restrict__ off, uint32_t n, c
         WalkStats s2;
         walk<false, KEYS>(im, mt & MN, (mt & MDOLLAR) != 0, GlobalPath{gpath + b + 2ull * t}, mw, em, s2);
     }
-}
-
-// option "root_split": the item CSR (2n counts, 2n + 1 offsets) folded into
-// the topics' (items 2t and 2t + 1 are adjacent, so a topic's list starts at
-// its first item's offset)
-__global__ void __launch_bounds__(BLOCK)
-tm_fold_items(const uint32_t* __restrict__ icounts, const uint64_t* __restrict__ ioff, uint32_t n,
-              uint32_t* __restrict__ counts, uint64_t* __restrict__ out_off) {
-    const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
-    if (t < n) {
-        const uint2 c = reinterpret_cast<const uint2*>(icounts)[t];
-        counts[t] = c.x + c.y;
-        out_off[t] = ioff[2ull * t];
-    }
-    if (t == n) out_off[n] = ioff[2ull * n];
 }
 
 constexpr int SCAN_ITEMS = 8;
@@ -2131,7 +1823,6 @@ tm_split_nodes(const uint4* __restrict__ nodes, uint64_t n, uint4* __restrict__ 
     }
 }
 
-bool kernels_have_blocks() { return TM_BLOCKS_PATH != 0; }
 
 hipError_t launch_split_nodes(const void* nodes, uint64_t n, void* inner, void* leaf, hipStream_t st) {
     if (n == 0) return hipSuccess;
@@ -2224,32 +1915,12 @@ hipError_t launch_small(const ImageView& im, const uint8_t* bytes, const uint64_
 // tm_copy_out alone, over the stage rows, counts and offsets a finished
 // launch_queue left in qb (same n, K, key_words): the ids into a larger
 // output after the first one overflowed, without walking again
-static DonBufs don_bufs(const QueueBufs& qb) {
-    if (!qb.donate) return DonBufs{nullptr, nullptr, nullptr, nullptr, nullptr, 0u, 0u, 0u};
-    return DonBufs{qb.prow, reinterpret_cast<uint4*>(qb.pdesc), reinterpret_cast<uint2*>(qb.pcnt), qb.tfirst, qb.dmask,
-                   qb.pcap, qb.don_min, qb.don_busy};
-}
-
 hipError_t launch_copy(const ImageView& im, const uint8_t* bytes, const uint64_t* off, uint32_t n, const QueueBufs& qb,
                        uint32_t K, uint32_t key_words, const uint32_t* counts, const uint64_t* out_off, uint32_t* out,
                        uint64_t* out_keys, uint64_t out_cap, hipStream_t st) {
     if (n == 0 || out_cap == 0) return hipSuccess;
-    // option "donate": the batch's piece lists (unkeyed, not presorted by position)
-    if (qb.donate && (qb.kstage || qb.shaped || qb.root_split || !qb.dmask || !qb.tfirst)) return hipErrorInvalidValue;
-    const DonBufs db = don_bufs(qb);
-    const DonBufs none{nullptr, nullptr, nullptr, nullptr, nullptr, 0u, 0u, 0u};
-    // option "root_split": the 2n items' rows, counts and offsets (counts /
-    // out_off here are the topics', folded from them)
-    const bool split = qb.root_split && !qb.kstage && !qb.shaped;
-    if (qb.root_split && !split) return hipErrorInvalidValue;
-    if (split) {
-        counts = qb.icounts;
-        out_off = qb.ioff;
-    }
-    const uint32_t nq = split ? 2 * n : n;
-    dim3 blk(BLOCK), g(div_up(nq, BLOCK));
-    if (qb.perm && !split) {   // a presorted walk: stage row p is topic perm[p]
-        if (qb.donate) return hipErrorInvalidValue;
+    dim3 blk(BLOCK), g(div_up(n, BLOCK));
+    if (qb.perm) {   // a presorted walk: stage row p is topic perm[p]
         if (qb.kstage)
             hipLaunchKernelGGL(tm_copy_out_sorted<true>, g, blk, 0, st, im, off, n, qb.twords, qb.words, qb.meta,
                                qb.path, qb.stage, qb.kstage, K, key_words, counts, out_off, out, out_keys, out_cap,
@@ -2260,20 +1931,16 @@ hipError_t launch_copy(const ImageView& im, const uint8_t* bytes, const uint64_t
     } else if (qb.kstage) {
         hipLaunchKernelGGL((tm_copy_out<true, false>), g, blk, 0, st, im, off, n, qb.twords, qb.words, qb.meta,
                            qb.path, qb.stage, qb.kstage, K, key_words, counts, out_off, out, out_keys, out_cap,
-                           nullptr, nullptr, 0u, none);
+                           nullptr, nullptr);
     } else if (qb.shaped) {
         if (!out_keys || key_words != 1 || !im.fshape) return hipErrorInvalidValue;
         hipLaunchKernelGGL((tm_copy_out<false, true>), g, blk, 0, st, im, off, n, qb.twords, qb.words, qb.meta,
                            qb.path, qb.stage, nullptr, K, 1u, counts, out_off, out, out_keys, out_cap,
-                           qb.spill_chunks >= QRANGES ? qb.spill : nullptr, qb.spill_head, 0u, none);
-    } else if (db.dmask) {
-        hipLaunchKernelGGL((tm_copy_out<false, false, true>), g, blk, 0, st, im, off, nq, qb.twords, qb.words, qb.meta,
-                           qb.path, qb.stage, nullptr, K, 1u, counts, out_off, out, nullptr, out_cap,
-                           qb.spill_chunks >= QRANGES ? qb.spill : nullptr, qb.spill_head, split ? 1u : 0u, db);
+                           qb.spill_chunks >= QRANGES ? qb.spill : nullptr, qb.spill_head);
     } else {
-        hipLaunchKernelGGL((tm_copy_out<false, false>), g, blk, 0, st, im, off, nq, qb.twords, qb.words, qb.meta,
+        hipLaunchKernelGGL((tm_copy_out<false, false>), g, blk, 0, st, im, off, n, qb.twords, qb.words, qb.meta,
                            qb.path, qb.stage, nullptr, K, 1u, counts, out_off, out, nullptr, out_cap,
-                           qb.spill_chunks >= QRANGES ? qb.spill : nullptr, qb.spill_head, split ? 1u : 0u, none);
+                           qb.spill_chunks >= QRANGES ? qb.spill : nullptr, qb.spill_head);
     }
     return hipGetLastError();
 }
@@ -2331,54 +1998,24 @@ hipError_t launch_queue(bool stats_mode, bool xcdq, const ImageView& im, const u
         mark(5);
         mark(6);
         if (out_cap) {
-            QueueBufs qc = qb;
-            qc.root_split = false;
-            qc.donate = false;
-            err = launch_copy(im, bytes, off, n, qc, K, key_words, counts, out_off, out, out_keys, out_cap, st);
+            err = launch_copy(im, bytes, off, n, qb, K, key_words, counts, out_off, out, out_keys, out_cap, st);
             if (err != hipSuccess) return err;
         }
         mark(7);
         return hipGetLastError();
     }
-    // option "root_split": 2n queue items (chunk rows only), their counts and
-    // offsets in qb.icounts / qb.ioff, folded into the topics' after the copy
-    // (a batch walked otherwise ignores it)
-    const bool split = qb.root_split && ch == CH_ROWS && !qb.donate;
-    if (split && (!qb.icounts || !qb.ioff || n > (1u << 30))) return hipErrorInvalidValue;
-    // option "donate": chunk-row walks (a batch walked otherwise ignores it)
-    const bool donate = qb.donate && ch == CH_ROWS;
-    if (donate && (!qb.prow || !qb.pdesc || !qb.pcnt || !qb.tfirst || !qb.dmask || qb.pcap < QRANGES ||
-                   (qb.pcap % QRANGES) != 0))
-        return hipErrorInvalidValue;
-    const DonBufs db = donate ? don_bufs(qb) : DonBufs{nullptr, nullptr, nullptr, nullptr, nullptr, 0u, 0u, 0u};
-    if (donate) {
-        err = hipMemsetAsync(qb.dmask, 0, ((size_t)(n >> 5) + 1) * 4, st);
-        if (err != hipSuccess) return err;
-    }
-    uint32_t* const wcounts = split ? qb.icounts : counts;
     // spill chunks: unkeyed walks in arrival order (presorted rows re-walk)
     uint32_t* const spill = (!keys && !by_pos && qb.spill_chunks >= QRANGES) ? qb.spill : nullptr;
-    const uint32_t wg = donate         ? resident_grid(tm_walk_queue_don<true>, div_up(n, 64),
+    const uint32_t wg = ch == CH_ROWS ? resident_grid(tm_walk_queue<false, true, false, CH_ROWS>, div_up(n, 64),
                                                       walk_blocks_per_cu)
-                        : ch == CH_ROWS ? resident_grid(tm_walk_queue<false, true, false, CH_ROWS>, div_up(n << split, 64),
-                                                      walk_blocks_per_cu)
-                                      : resident_grid(tm_walk_queue<false, false, false>, div_up(n << split, 64),
+                                      : resident_grid(tm_walk_queue<false, false, false>, div_up(n, 64),
                                                       walk_blocks_per_cu);
 #define TM_Q(S, X, Y, C)                                                                                           \
     hipLaunchKernelGGL((tm_walk_queue<S, X, Y, C>), dim3(wg), blk, 0, st, im, off, n, qb.twords, qb.words,       \
-                       qb.meta, qb.path, qb.stage, qb.kstage, K, key_words, wcounts, qb.ws, stats,               \
+                       qb.meta, qb.path, qb.stage, qb.kstage, K, key_words, counts, qb.ws, stats,                \
                        hist ? stats + HIST_OFF : nullptr, qb.perm, qb.twords_s, qb.meta_s, spill, qb.spill_head,   \
-                       qb.spill_chunks, split ? 1u : 0u, db)
-    if (donate) {
-        if (xcdq)
-            hipLaunchKernelGGL((tm_walk_queue_don<true>), dim3(wg), blk, 0, st, im, off, n, qb.twords, qb.words, qb.meta,
-                               qb.path, qb.stage, qb.kstage, K, key_words, wcounts, qb.ws, stats, nullptr, qb.perm,
-                               qb.twords_s, qb.meta_s, spill, qb.spill_head, qb.spill_chunks, 0u, db);
-        else
-            hipLaunchKernelGGL((tm_walk_queue_don<false>), dim3(wg), blk, 0, st, im, off, n, qb.twords, qb.words, qb.meta,
-                               qb.path, qb.stage, qb.kstage, K, key_words, wcounts, qb.ws, stats, nullptr, qb.perm,
-                               qb.twords_s, qb.meta_s, spill, qb.spill_head, qb.spill_chunks, 0u, db);
-    } else if (ch == CH_ROWS) {
+                       qb.spill_chunks)
+    if (ch == CH_ROWS) {
         if (xcdq) TM_Q(false, true, false, CH_ROWS); else TM_Q(false, false, false, CH_ROWS);
     } else if (keys) {
         if (stats_mode) TM_Q(true, true, true, CH_NONE); else TM_Q(false, true, true, CH_NONE);
@@ -2388,34 +2025,14 @@ hipError_t launch_queue(bool stats_mode, bool xcdq, const ImageView& im, const u
         if (xcdq) TM_Q(false, true, false, CH_NONE); else TM_Q(false, false, false, CH_NONE);
     }
 #undef TM_Q
-    if (donate)
-        hipLaunchKernelGGL(tm_add_pieces, dim3(div_up(qb.pcap, BLOCK)), blk, 0, st, qb.ws,
-                           reinterpret_cast<const uint4*>(qb.pdesc), reinterpret_cast<const uint2*>(qb.pcnt), qb.pcap,
-                           counts);
     mark(3);
     mark(4);
-    if (split) {
-        err = launch_scan(qb.icounts, 2 * n, qb.ioff, total, qb.scan_tmp, st);
-        if (err != hipSuccess) return err;
-        mark(5);
-        mark(6);
-        if (out_cap) {
-            err = launch_copy(im, bytes, off, n, qb, K, key_words, nullptr, nullptr, out, out_keys, out_cap, st);
-            if (err != hipSuccess) return err;
-        }
-        hipLaunchKernelGGL(tm_fold_items, dim3(div_up(n + 1, BLOCK)), blk, 0, st, qb.icounts, qb.ioff, n, counts,
-                           out_off);
-        mark(7);
-        return hipGetLastError();
-    }
     err = launch_scan(counts, n, out_off, total, qb.scan_tmp, st);
     if (err != hipSuccess) return err;
     mark(5);
     mark(6);
     if (out_cap) {
         QueueBufs qc = qb;
-        qc.root_split = false;
-        qc.donate = donate;
         if (!by_pos) qc.perm = nullptr;   // stage rows by topic
         err = launch_copy(im, bytes, off, n, qc, K, key_words, counts, out_off, out, out_keys, out_cap, st);
         if (err != hipSuccess) return err;

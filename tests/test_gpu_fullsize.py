@@ -133,25 +133,3 @@ def test_c3_8m_host_pipelined_every_topic_equals_o3(c3_full, capsys):
     _say(capsys, t0, "host pipelined path: all %d topics equal O3" % n)
 
 
-def test_c3_1m_slice_donating_walk_equals_o3(c3_full, capsys):
-    """option "donate" (the drain's donation of pending '+' subtrees to idle
-    lanes) on a 1M-topic slice of the same batch -- the per-rank size of the
-    8-GPU strong-scaling run -- every topic's list against O3, and pieces
-    were donated"""
-    import ctypes
-    t0 = time.time()
-    e, tb, to, want = c3_full
-    wc, wo, wi = want
-    n = 1_000_000
-    sb = np.ascontiguousarray(tb[:int(to[n])])
-    so = np.ascontiguousarray(to[:n + 1])
-    e.set_option("donate", 1)
-    try:
-        got = e.match_batch(sb, so)
-        pieces = (ctypes.c_uint64 * 8)()
-        assert e.lib.tm_debug_walk_pieces(e.h, pieces) == 0
-    finally:
-        e.set_option("donate", 0)
-    _assert_equal(got, (wc[:n], wo[:n + 1], wi[:int(wo[n])]))
-    assert sum(pieces) > 0
-    _say(capsys, t0, "1M slice, donating walk: all %d topics equal O3 (%d pieces)" % (n, sum(pieces)))

@@ -132,8 +132,8 @@ def test_c2_full_vs_o1(gpu_device):
     e.close()
 
 
-@pytest.mark.parametrize("chunk_rows,root_split,donate", [(0, 0, 0), (1, 0, 0), (1, 1, 0), (1, 0, 1)])
-def test_c5_sample_vs_o1(gpu_device, chunk_rows, root_split, donate):
+@pytest.mark.parametrize("chunk_rows", [0, 1])
+def test_c5_sample_vs_o1(gpu_device, chunk_rows):
     fb, fo = W.filters(5, n=200_000)
     raw = W.unpack(fb, fo)
     inner = [T.parse(f)[0] for f in raw]     # the trie sees the inner filter (emqx_topic.erl:189-197)
@@ -143,8 +143,6 @@ def test_c5_sample_vs_o1(gpu_device, chunk_rows, root_split, donate):
     e = Engine(device=gpu_device, filters_hint=len(io) - 1)
     if chunk_rows:   # the per-lane walk with chunk rows; 16-level topics read their global row
         e.set_option("wave_walk_max", 0)
-    e.set_option("root_split", root_split)
-    e.set_option("donate", donate)
     e.insert_many(ib, io)
     tb, to = W.topics(5, n=5000)
     counts = _by_id(o1, e, tb, to)
@@ -267,19 +265,6 @@ VARIANTS = {"queue": {}, "queue_xcd": {}, "queue_xcd@nosplit@dfs": {"split": 0, 
             # the range-local word-hash order with the lightest topics of each range last (three radix passes)
             "queue_xcd@order6": {"presort": 6}, "queue_xcd@order6@bits16@tail300": {"presort": 6, "sort_bits": 16,
                                                                                     "light_tail": 300},
-            # each topic as two queue items (the root's '+' subtree / the rest)
-            "queue_xcd@rootsplit": {"root_split": 1}, "queue@rootsplit@stagek8@nospill": {"root_split": 1,
-                                                                                          "stage_k": 8, "spill": 0},
-            "queue_xcd@rootsplit@order6": {"root_split": 1, "presort": 6},
-            "queue_xcd@rootsplit@tail@nosummaries": {"root_split": 1, "presort": 2, "summaries": 0},
-            "queue_xcd@rootsplit@norows": {"root_split": 1, "chunk_rows": 0},
-            # the drain's donation of pending '+' subtrees to idle lanes (pieces)
-            "queue_xcd@donate": {"donate": 1}, "queue@donate": {"donate": 1},
-            "queue_xcd@donate@min0@stagek8": {"donate": 1, "donate_min": 0, "stage_k": 8},
-            "queue_xcd@donate@min0@nospill": {"donate": 1, "donate_min": 0, "spill": 0},
-            "queue_xcd@donate@tail@nosummaries": {"donate": 1, "presort": 2, "summaries": 0},
-            "queue_xcd@donate@order6@min1": {"donate": 1, "presort": 6, "donate_min": 1},
-            "queue_xcd@donate@rootsplit": {"donate": 1, "root_split": 1},
 }
 
 
@@ -494,8 +479,7 @@ def test_pipelined_host_batch_equals_one_shot_and_o1(gpu_device):
     o1.close()
 
 
-@pytest.mark.parametrize("root_split,donate", [(0, 0), (1, 0), (0, 1)])
-def test_pipelined_host_owned_output_grows_exact(gpu_device, root_split, donate):
+def test_pipelined_host_owned_output_grows_exact(gpu_device):
     """the pipelined path sizes an owned output from its first
     chunk's fan-out (x 1.15 over the batch) and grows it when a later chunk
     outruns that.  Here the first 1M-topic chunk matches few filters (words no
@@ -517,8 +501,6 @@ def test_pipelined_host_owned_output_grows_exact(gpu_device, root_split, donate)
     assert rest > 1.5 * first * 1.15, (first, rest)   # a later chunk outruns the first one's estimate
     e = Engine(device=gpu_device)
     e.insert_many(fb, fo)
-    e.set_option("root_split", root_split)   # the re-copy of a root-split walk's item rows
-    e.set_option("donate", donate)           # ... of a donating walk's piece lists
     e.set_option("host_pipeline", 1)
     c1, o1_, i1 = e.match_batch(tb, to)                  # pipelined, owned: grows
     assert np.array_equal(c1, wc) and np.array_equal(o1_, wo) and np.array_equal(i1, wi)

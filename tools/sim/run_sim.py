@@ -26,15 +26,13 @@ from emqx_amd import Engine  # noqa: E402
 from emqx_amd import workload as W  # noqa: E402
 
 KINDS = ["inner", "leaf", "cold", "hot", "pair"]
-MODES = {"cur": 0, "slotrec": 1, "pair": 2, "spec": 4, "blocks": 8, "bloom64": 16, "fix": 64}
+MODES = {"cur": 0, "slotrec": 1, "pair": 2, "spec": 4, "blocks": 8, "fix": 64}
 
 
 class View(ctypes.Structure):
     _fields_ = [("nodes", ctypes.c_void_p), ("n_nodes", ctypes.c_uint64), ("cold", ctypes.c_void_p),
                 ("cold_slots", ctypes.c_uint64), ("hot", ctypes.c_void_p), ("hot_slots", ctypes.c_uint64),
-                ("hot_limit", ctypes.c_uint32), ("aux_stride", ctypes.c_uint32), ("aux", ctypes.c_void_p),
-                ("blocks", ctypes.c_void_p), ("block_slots", ctypes.c_uint64), ("blocks_live", ctypes.c_uint32),
-                ("pad", ctypes.c_uint32)]
+                ("hot_limit", ctypes.c_uint32), ("aux_stride", ctypes.c_uint32), ("aux", ctypes.c_void_p)]
 
 
 class SimOut(ctypes.Structure):
@@ -173,8 +171,6 @@ def main():
                 occ = int(part[3:])
             elif part.startswith("div"):   # per-node block load: size >= div x edges
                 mode |= int(part[3:]) << 8
-            elif part.startswith("bloomw"):   # the engine's blocks under a W-bit mask (0: none)
-                mode |= 32 | int(part[6:]) << 16
             else:
                 mode |= MODES[part]
         lanes = 32 * 4 * occ * 64

@@ -41,10 +41,6 @@ struct View {
     uint32_t hot_limit;
     uint32_t aux_stride;
     const uint8_t* aux;
-    const BlockSlot* blocks;   // the engine's own child blocks (blocks_live)
-    uint64_t block_slots;
-    uint32_t blocks_live;
-    uint32_t pad;
 };
 
 enum Kind : uint8_t { K_INNER = 0, K_LEAF = 1, K_COLD = 2, K_HOT = 3, K_PAIR = 4, K_NKIND = 5 };
@@ -91,8 +87,6 @@ enum Mode : int {
     M_SLOTREC = 1,   // TM_SLOT_RECORD: 32 B slots carry the child's record, the walk goes on in the same step
     M_PAIR = 2,      // a node's '+' child at id + 1, both halves loaded in one round; an immediate '+' step is free
     M_SPECPROBE = 4, // the parent's reference says "WIDE": the home slot is loaded with the node (no Bloom)
-    M_BLOOM64 = 16,  // the engine's blocks, Bloom test by a 64-bit mask of the block's words (word_bloom)
-    M_BLOOMW = 32,   // the engine's blocks, Bloom test by a (mode >> 16)-bit mask, k = 2 (0 = no Bloom)
     M_BLOCKS = 8,    // per-node child blocks: a WIDE node's literal / '#' edges in a contiguous open-addressing
                      // block of its own (blocks in node order = heat order), not one shared table
     M_FIX = 64,      // a fixed 64 B block per node id (no pointer: address = v * 64): up to 8 literal children
@@ -180,23 +174,6 @@ struct Walker {
     // probe_edge<false> (kernels.hip): linear probing from the home slot,
     // one dependent round per slot (from round rd0 on)
     Hit probe(uint32_t node, uint32_t w, std::vector<Acc>& acc, uint32_t& rd) const {
-        if (v.blocks_live && w != WORD_HASH) {   // the engine's blocks (lw = first slot, lc = log2 | Bloom)
-            const Node& x = v.nodes[node];
-            const uint32_t k = x.lc >> BLOCK_LOG2_SHIFT, m = (1u << k) - 1;
-            for (uint32_t p = block_home(w, k);; p = (p + 1) & m) {
-                const BlockSlot& e = v.blocks[(uint64_t)x.lw + p];
-                acc.push_back(Acc{x.lw + p, K_COLD, (uint8_t)std::min<uint32_t>(rd, 255)});
-                ++rd;
-                if (e.word == w) {
-                    ++probes_ok;
-                    return Hit{e.child, e.sum, false};
-                }
-                if (e.word == WORD_NONE) {
-                    ++probes_fail;
-                    return Hit{NODE_NONE, 0, false};
-                }
-            }
-        }
         if ((mode & M_FIX) && w != WORD_HASH) {
             const uint32_t c = blk->cnt[node];
             if (c && c <= 8) {
@@ -298,28 +275,9 @@ struct Walker {
                 if (h.child != NODE_NONE) ++wide_hist[32 + bk];
                 return h;
             }
-            if (v.blocks_live && (mode & (M_BLOOM64 | M_BLOOMW))) {   // emulated masks of the block's words
-                const uint32_t k = lc >> BLOCK_LOG2_SHIFT;
-                const uint32_t bits = (mode & M_BLOOM64) ? 64u : (uint32_t)(mode >> 16);
-                auto bl = [&](uint32_t x) -> uint64_t {
-                    if (bits == 64) return word_bloom(x);
-                    const uint32_t h = x * 0x85EBCA77u;
-                    return (1ull << (((h & 0xFFFFu) * bits) >> 16)) | (1ull << (((h >> 16) * bits) >> 16));
-                };
-                if (bits) {
-                    uint64_t m = 0;
-                    for (uint64_t i = 0; i < (1ull << k); ++i)
-                        if (v.blocks[(uint64_t)lw + i].word != WORD_NONE) m |= bl(v.blocks[(uint64_t)lw + i].word);
-                    if ((m & bl(w)) != bl(w)) return Hit{NODE_NONE, 0, false};
-                }
-            } else if (v.blocks_live) {
-                const uint32_t bb = block_bloom(w);
-                if ((lc & bb) != bb) return Hit{NODE_NONE, 0, false};
-            } else {
-                const uint64_t b = word_bloom(w);
-                const uint64_t mask = ((uint64_t)lc << 32) | lw;
-                if ((mask & b) != b) return Hit{NODE_NONE, 0, false};
-            }
+            const uint64_t b = word_bloom(w);
+            const uint64_t mask = ((uint64_t)lc << 32) | lw;
+            if ((mask & b) != b) return Hit{NODE_NONE, 0, false};
             ++wide_hist[16 + bk];
             const Hit h = probe(node, w, acc, rd);
             if (h.child != NODE_NONE) ++wide_hist[32 + bk];
