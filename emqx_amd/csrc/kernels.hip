@@ -67,6 +67,11 @@ __device__ __forceinline__ void stream_store16(void* p, uint4 v) {
     else *reinterpret_cast<uint4*>(p) = v;
 }
 
+__device__ __forceinline__ void wave_sync_lds() {
+    __threadfence_block();
+    __builtin_amdgcn_wave_barrier();
+}
+
 // ---------------------------------------------------------------------------
 // byte access: aligned 8-byte words (an aligned word holding a valid byte
 // never crosses a page), little-endian extraction.  Topic bytes are read
@@ -338,18 +343,13 @@ __device__ __forceinline__ uint32_t tail_key(const ImageView& im, const uint32_t
     return (range_of(t, n) << 5) | (31u - c);
 }
 
-template <class B>
-__device__ __forceinline__ uint32_t tokenize_one(const ImageView& im, const B& bytes,
-                                             const uint64_t* __restrict__ off, uint32_t t, uint32_t n,
-                                             uint32_t* __restrict__ twords, uint32_t* __restrict__ words,
-                                             uint32_t* __restrict__ meta, uint32_t* __restrict__ skeys,
-                                             uint32_t* __restrict__ svals, uint32_t key_mode) {
-    const uint64_t b = off[t], e = off[t + 1];
-    uint32_t tw[WREG];
-#pragma unroll
-    for (uint32_t k = 0; k < WREG; ++k) tw[k] = WORD_NONE;
-    bool ood;
-    const uint32_t lev = tokenize_topic(im, bytes, b, e, tw, words + (b - off[0]) + t, ood);
+// a tokenized topic's row (levels < WREG), meta and presort key; returns
+// the topic's cost class (presort 6) or 32
+__device__ __forceinline__ uint32_t tok_store(const ImageView& im, uint32_t t, uint32_t n, uint32_t lev,
+                                              const uint32_t (&tw)[WREG], bool ood, uint32_t dollar,
+                                              uint32_t* __restrict__ twords, uint32_t* __restrict__ meta,
+                                              uint32_t* __restrict__ skeys, uint32_t* __restrict__ svals,
+                                              uint32_t key_mode) {
     // the row as whole 16 B stores (per-level 4 B stores from 64 lanes to
     // 64 rows were partial-line writes: read-modify-write traffic), only the
     // quads the walk reads (4k < levels: 32 B for an 8-level topic)
@@ -357,7 +357,6 @@ __device__ __forceinline__ uint32_t tokenize_one(const ImageView& im, const B& b
 #pragma unroll
     for (uint32_t k = 0; k < WREG / 4; ++k)
         if (4 * k < lev || k == 0) stream_store16(row + k, make_uint4(tw[4 * k], tw[4 * k + 1], tw[4 * k + 2], tw[4 * k + 3]));
-    const uint32_t dollar = (e > b && bytes.byte(b) == '$') ? 1u : 0u;
     stream_store(meta + t, lev | (dollar << 31) | (lev > WREG ? MLONG : 0u) | (ood ? MOOD : 0u));
     if (skeys) {   // option "presort": the walk-order key (presort.hip)
         // 2: the tail order (8 bits); 4: the tail order, then the word-hash
@@ -384,6 +383,62 @@ __device__ __forceinline__ uint32_t tokenize_one(const ImageView& im, const B& b
     return 32u;   // (presort 6: the topic's cost class)
 }
 
+template <class B>
+__device__ __forceinline__ uint32_t tokenize_one(const ImageView& im, const B& bytes,
+                                             const uint64_t* __restrict__ off, uint32_t t, uint32_t n,
+                                             uint32_t* __restrict__ twords, uint32_t* __restrict__ words,
+                                             uint32_t* __restrict__ meta, uint32_t* __restrict__ skeys,
+                                             uint32_t* __restrict__ svals, uint32_t key_mode) {
+    const uint64_t b = off[t], e = off[t + 1];
+    uint32_t tw[WREG];
+#pragma unroll
+    for (uint32_t k = 0; k < WREG; ++k) tw[k] = WORD_NONE;
+    bool ood;
+    const uint32_t lev = tokenize_topic(im, bytes, b, e, tw, words + (b - off[0]) + t, ood);
+    const uint32_t dollar = (e > b && bytes.byte(b) == '$') ? 1u : 0u;
+    return tok_store(im, t, n, lev, tw, ood, dollar, twords, meta, skeys, svals, key_mode);
+}
+
+// The wave-cooperative tokenizer.  The per-lane scan
+// above walks each topic level by level on one lane (a '/' scan, the hash,
+// the dictionary probe, then the next level): ~300 VALU instructions and one
+// dependent round trip per level, with 64 lanes doing it in lockstep.  Here
+// a wave's 64 topics are split into their levels first, and the lanes then
+// take the levels, not the topics:
+//   1. each lane counts the '/' of its topic in the LDS window (an exact
+//      zero-byte test per 8 bytes, popcount), a wave prefix sum gives every
+//      topic its first level's index in the wave's level list, and the lane
+//      writes its levels' {start, length} there;
+//   2. lane j takes levels j, j + 64, ...: hashes the level's bytes and
+//      issues its dictionary slot load, TOK_BATCH levels at a time with all
+//      their loads in flight, then resolves them (byte-verified, dict_end)
+//      and writes the word id over the level's entry;
+//   3. each lane reads its topic's word ids back (consecutive entries) and
+//      stores the row, meta and presort key as before (tok_store).
+// emqx_topic:words/1 semantics are unchanged: N slashes make N + 1 levels,
+// empty levels are kept, '+' / '#' levels are the atoms.
+// levels per wave's list: one u32 each (the level's {start, length}, then
+// its word id); 1000 keeps a 4-wave block at 32.5 KB of LDS, 5 blocks per CU
+// (5 waves per SIMD, as the VGPRs allow); a wave with more: the per-lane path
+constexpr uint32_t TOK_LMAX = 1000;
+#ifndef TM_TOK_BATCH
+#define TM_TOK_BATCH 3   // dictionary probes in flight per lane (4: 97 VGPRs, 4 waves per SIMD)
+#endif
+// exact per-byte '/' test of an 8-byte word: 0x80 in each byte that is '/'
+__device__ __forceinline__ uint64_t slash_bytes(uint64_t x) {
+    constexpr uint64_t M = 0x7F7F7F7F7F7F7F7FULL;
+    x ^= 0x2F2F2F2F2F2F2F2FULL;   // '/' -> 0x00
+    return ~(((x & M) + M) | x | M);
+}
+// the bytes of window word q (window offset 8q) inside [b, e)
+__device__ __forceinline__ uint64_t range_bytes(uint32_t q, uint32_t b, uint32_t e) {
+    const uint32_t lo = 8 * q, hi = lo + 8;
+    uint64_t m = ~0ull;
+    if (b > lo) m &= ~0ull << (8 * (b - lo));
+    if (e < hi) m &= e > lo ? ~0ull >> (8 * (hi - e)) : 0ull;
+    return m;
+}
+
 __global__ void __launch_bounds__(BLOCK)
 tm_tokenize(ImageView im, const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint32_t n,
             uint32_t* __restrict__ twords, uint32_t* __restrict__ words, uint32_t* __restrict__ meta,
@@ -395,6 +450,7 @@ tm_tokenize(ImageView im, const uint8_t* __restrict__ bytes, const uint64_t* __r
         return;
     }
     __shared__ uint64_t win[BLOCK / 64][TOK_WIN_WORDS];
+    __shared__ uint32_t tok_lev[BLOCK / 64][TOK_LMAX];   // the wave's levels: start | length << 16, then the id
     __shared__ uint32_t chist[32];   // presort 6: the block's cost-class histogram (QWS_CHIST)
     const bool hist = skeys && (key_mode & 255u) == 6u;
     if (hist && threadIdx.x < 32) chist[threadIdx.x] = 0;
@@ -416,7 +472,79 @@ tm_tokenize(ImageView im, const uint8_t* __restrict__ bytes, const uint64_t* __r
     }
     __syncthreads();
     uint32_t c = 32u;
-    if (t < n) {
+    // 1. levels of the lane's topic: count, wave prefix sum, descriptors
+    uint32_t b = 0, e = 0, nl = 0;
+    if (lds && t < n) {
+        b = (uint32_t)(off[t] - wbase);
+        e = (uint32_t)(off[t + 1] - wbase);
+        for (uint32_t q = b >> 3; 8 * q < e; ++q)
+            nl += (uint32_t)__popcll(slash_bytes(win[wv][q]) & range_bytes(q, b, e));
+        nl += 1;
+    }
+    uint32_t first = nl;   // inclusive, then exclusive prefix over the wave
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)first, o, 64);
+        if ((int)lane >= o) first += y;
+    }
+    const uint32_t L = (uint32_t)__shfl((int)first, 63, 64);
+    first -= nl;
+    if (lds && L <= TOK_LMAX) {   // (uniform per wave)
+        uint32_t* lv = tok_lev[wv];
+        if (t < n) {
+            uint32_t k = first, s0 = b;
+            for (uint32_t q = b >> 3; 8 * q < e; ++q) {
+                uint64_t z = slash_bytes(win[wv][q]) & range_bytes(q, b, e);
+                while (z) {
+                    const uint32_t p = 8 * q + ((uint32_t)__builtin_ctzll(z) >> 3);
+                    z &= z - 1;
+                    lv[k++] = s0 | (p - s0) << 16;
+                    s0 = p + 1;
+                }
+            }
+            lv[k] = s0 | (e - s0) << 16;
+        }
+        wave_sync_lds();
+        // 2. lanes over levels: TM_TOK_BATCH dictionary loads in flight per lane
+        const LdsBytes lb{win[wv], wbase};
+        for (uint32_t i0 = 0; i0 < L; i0 += 64 * TM_TOK_BATCH) {
+            DictProbe q[TM_TOK_BATCH];
+#pragma unroll
+            for (uint32_t j = 0; j < TM_TOK_BATCH; ++j) {
+                const uint32_t i = i0 + 64 * j + lane;
+                if (i < L) {
+                    const uint32_t d = lv[i];
+                    q[j] = dict_begin(im, lb, wbase, wbase + (d & 0xFFFFu), d >> 16);
+                }
+            }
+#pragma unroll
+            for (uint32_t j = 0; j < TM_TOK_BATCH; ++j) {
+                const uint32_t i = i0 + 64 * j + lane;
+                if (i < L) lv[i] = dict_end(im, lb, wbase, q[j]);   // (only this lane reads entry i)
+            }
+        }
+        wave_sync_lds();
+        // 3. the lane's topic: its word ids, row, meta and key
+        if (t < n) {
+            uint32_t tw[WREG];
+            bool ood = false;
+#pragma unroll
+            for (uint32_t k = 0; k < WREG; ++k) {
+                const uint32_t w = k < nl ? lv[first + k] : WORD_NONE;
+                ood |= w == WORD_PLUS || w == WORD_HASH;
+                tw[k] = w;
+            }
+            if (nl > WREG) {   // levels >= WREG of a long topic: global, beside its bytes
+                uint32_t* lw = words + (off[t] - off[0]) + t;
+                for (uint32_t k = WREG; k < nl; ++k) {
+                    const uint32_t w = lv[first + k];
+                    ood |= w == WORD_PLUS || w == WORD_HASH;
+                    lw[k] = w;
+                }
+            }
+            const uint32_t dollar = (e > b && lb.byte(wbase + b) == '$') ? 1u : 0u;
+            c = tok_store(im, t, n, nl, tw, ood, dollar, twords, meta, skeys, svals, key_mode);
+        }
+    } else if (t < n) {
         if (lds)
             c = tokenize_one(im, LdsBytes{win[wv], wbase}, off, t, n, twords, words, meta, skeys, svals, key_mode);
         else
@@ -431,11 +559,6 @@ tm_tokenize(ImageView im, const uint8_t* __restrict__ bytes, const uint64_t* __r
 }
 
 
-
-__device__ __forceinline__ void wave_sync_lds() {
-    __threadfence_block();
-    __builtin_amdgcn_wave_barrier();
-}
 
 // ---------------------------------------------------------------------------
 // The child found by a probe, with its record when the edge table delivered
