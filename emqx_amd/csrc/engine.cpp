@@ -665,6 +665,7 @@ struct tm_engine {
                                         // (no re-walks); unkeyed walks keep K and spill (kernels.h)
     int spill_on = 1;                   // option "spill": ids past K to spill chunks (0: re-walk, as keyed)
     int chunk_rows = TM_CHUNK_ROWS;     // option "chunk_rows" (kernels.h QueueBufs)
+    int tok_wave = 1;                   // option "tok_wave" (kernels.h QueueBufs)
     uint32_t wave_walk_max = 32768;     // option "wave_walk_max": batches of at most this many topics take the
                                         // wave-per-topic walk (tm_walk_wave: ~2 dependent loads per level);
                                         // faster up to 16K topics, slower from 64K (profiles/r03_d)
@@ -2230,6 +2231,7 @@ struct tm_engine {
         // the tail order (presort 2) leaves small batches to the wave walk
         qb.wave_walk = wave;   // (the range-keyed orders: 2, 4, 5, 6)
         qb.chunk_rows = chunk_rows;
+        qb.tok_wave = tok_wave != 0;
         qb.scan_tmp = w.scan.as<uint64_t>();
         qb.ws = w.ws.as<unsigned long long>();
         qb.perm = presort && !shaped && !(qb.wave_walk && presort >= 2) ? w.perm.as<uint32_t>() : nullptr;
@@ -3968,6 +3970,11 @@ int tm_set_option(tm_engine* e, const char* name, int64_t value) {
         if (!std::strcmp(name, "chunk_rows")) {
             if (value < 0 || value > 1) return TM_EINVAL;
             e->chunk_rows = (int)value;
+            return TM_OK;
+        }
+        if (!std::strcmp(name, "tok_wave")) {   // 1: wave-cooperative tokenizer, 0: one lane per topic
+            if (value < 0 || value > 1) return TM_EINVAL;
+            e->tok_wave = (int)value;
             return TM_OK;
         }
         if (!std::strcmp(name, "shape_keys")) {

@@ -45,6 +45,7 @@ struct QueueBufs {
     bool wave_walk = false;   // small batch: tm_walk_wave, one wave per topic level by level (option "wave_walk_max")
     int chunk_rows = 1;       // option "chunk_rows": 1 a taken chunk's rows staged in LDS, 0 each topic's row
                               // read from HBM when a lane takes it
+    bool tok_wave = true;     // option "tok_wave": the wave-cooperative tokenizer (0: one lane per topic)
     uint64_t* scan_tmp;   // scan_tmp_elems(n)
     unsigned long long* ws;   // QWS_BYTES of queue heads
     uint32_t* perm;       // option "presort": queue position -> topic (n), or null (arrival order)

@@ -421,6 +421,7 @@ __device__ __forceinline__ uint32_t tokenize_one(const ImageView& im, const B& b
 // its word id); 1000 keeps a 4-wave block at 32.5 KB of LDS, 5 blocks per CU
 // (5 waves per SIMD, as the VGPRs allow); a wave with more: the per-lane path
 constexpr uint32_t TOK_LMAX = 1000;
+constexpr uint32_t TOK_WAVE = 1u << 24;   // key_mode bit: the wave path (option "tok_wave"; 0: per lane)
 #ifndef TM_TOK_BATCH
 #define TM_TOK_BATCH 3   // dictionary probes in flight per lane (4: 97 VGPRs, 4 waves per SIMD)
 #endif
@@ -488,7 +489,7 @@ tm_tokenize(ImageView im, const uint8_t* __restrict__ bytes, const uint64_t* __r
     }
     const uint32_t L = (uint32_t)__shfl((int)first, 63, 64);
     first -= nl;
-    if (lds && L <= TOK_LMAX) {   // (uniform per wave)
+    if (lds && L <= TOK_LMAX && (key_mode & TOK_WAVE)) {   // (uniform per wave)
         uint32_t* lv = tok_lev[wv];
         if (t < n) {
             uint32_t k = first, s0 = b;
@@ -2099,7 +2100,8 @@ hipError_t launch_queue(bool stats_mode, bool xcdq, const ImageView& im, const u
     hipLaunchKernelGGL(tm_tokenize, g, blk, 0, st, im, bytes, off, n, qb.twords, qb.words, qb.meta,
                        qb.perm ? qb.sort_keys + (odd ? n : 0u) : nullptr,
                        qb.perm ? (odd ? qb.sort_vals : qb.perm) : nullptr,
-                       qb.presort_mode | (8u * qb.presort_passes()) << 8 | (qb.light_max & 255u) << 16,
+                       qb.presort_mode | (8u * qb.presort_passes()) << 8 | (qb.light_max & 255u) << 16 |
+                           (qb.tok_wave ? TOK_WAVE : 0u),
                        qb.ws + QWS_CHIST);
     if (qb.perm) {   // option "presort": perm (and the rows in walk order unless chunk rows read them by perm)
         err = launch_presort(qb.twords, qb.meta, n, qb, st, by_pos);
