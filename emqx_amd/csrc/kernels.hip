@@ -191,6 +191,16 @@ __device__ __forceinline__ uint64_t block_exclusive_scan(uint64_t x, uint64_t* l
     return wpre + inc - x;
 }
 
+// exact per-byte '/' test of an 8-byte word: 0x80 in each byte that is '/'.
+// (The borrow form (x - 0x01..) & ~x & 0x80.. also flags a byte 0x01 above
+// a zero byte, i.e. a '.' right after a '/': a scan resumed after that '/'
+// split "a/.b" at the '.'; tests/test_gpu_tokenize.py)
+__device__ __forceinline__ uint64_t slash_bytes(uint64_t x) {
+    constexpr uint64_t M = 0x7F7F7F7F7F7F7F7FULL;
+    x ^= 0x2F2F2F2F2F2F2F2FULL;   // '/' -> 0x00
+    return ~(((x & M) + M) | x | M);
+}
+
 // the next '/' of topic bytes [q, e) eight bytes at a time (e when none)
 template <class B>
 __device__ __forceinline__ uint64_t next_slash(const B& bytes, uint64_t q, uint64_t e, bool& found) {
@@ -200,8 +210,7 @@ __device__ __forceinline__ uint64_t next_slash(const B& bytes, uint64_t q, uint6
         uint32_t start = (uint32_t)(q & 7);
         uint64_t rem = e - (q & ~7ull);
         uint32_t stop = rem < 8 ? (uint32_t)rem : 8;
-        uint64_t x = word8 ^ 0x2F2F2F2F2F2F2F2FULL;  // '/' -> 0x00
-        uint64_t z = (x - 0x0101010101010101ULL) & ~x & 0x8080808080808080ULL;
+        uint64_t z = slash_bytes(word8);
         z &= (~0ull) << (8 * start);
         if (stop < 8) z &= (~0ull) >> (64 - 8 * stop);
         if (z) {
@@ -425,12 +434,6 @@ constexpr uint32_t TOK_WAVE = 1u << 24;   // key_mode bit: the wave path (option
 #ifndef TM_TOK_BATCH
 #define TM_TOK_BATCH 3   // dictionary probes in flight per lane (4: 97 VGPRs, 4 waves per SIMD)
 #endif
-// exact per-byte '/' test of an 8-byte word: 0x80 in each byte that is '/'
-__device__ __forceinline__ uint64_t slash_bytes(uint64_t x) {
-    constexpr uint64_t M = 0x7F7F7F7F7F7F7F7FULL;
-    x ^= 0x2F2F2F2F2F2F2F2FULL;   // '/' -> 0x00
-    return ~(((x & M) + M) | x | M);
-}
 // the bytes of window word q (window offset 8q) inside [b, e)
 __device__ __forceinline__ uint64_t range_bytes(uint32_t q, uint32_t b, uint32_t e) {
     const uint32_t lo = 8 * q, hi = lo + 8;

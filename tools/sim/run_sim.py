@@ -26,7 +26,7 @@ from emqx_amd import Engine  # noqa: E402
 from emqx_amd import workload as W  # noqa: E402
 
 KINDS = ["inner", "leaf", "cold", "hot", "pair"]
-MODES = {"cur": 0, "slotrec": 1, "pair": 2, "spec": 4, "blocks": 8, "fix": 64}
+MODES = {"cur": 0, "slotrec": 1, "pair": 2, "spec": 4, "blocks": 8, "fix": 64, "nofp": 128}
 
 
 class View(ctypes.Structure):

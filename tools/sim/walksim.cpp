@@ -89,6 +89,7 @@ enum Mode : int {
     M_SPECPROBE = 4, // the parent's reference says "WIDE": the home slot is loaded with the node (no Bloom)
     M_BLOCKS = 8,    // per-node child blocks: a WIDE node's literal / '#' edges in a contiguous open-addressing
                      // block of its own (blocks in node order = heat order), not one shared table
+    M_NOFP = 128,    // upper bound of a perfect per-node filter: a Bloom pass for an absent word costs no probe
     M_FIX = 64,      // a fixed 64 B block per node id (no pointer: address = v * 64): up to 8 literal children
                      // as 8 B {word, child} in 4 quads, home quad by word hash, quads probed in order (one
                      // round each); nodes with more children: the shared table (with M_BLOCKS: their own
@@ -279,6 +280,21 @@ struct Walker {
             const uint64_t mask = ((uint64_t)lc << 32) | lw;
             if ((mask & b) != b) return Hit{NODE_NONE, 0, false};
             ++wide_hist[16 + bk];
+            if (mode & M_NOFP) {   // the probe's outcome without its loads: an absent word stops here
+                std::vector<Acc> dummy;
+                uint32_t r0 = 0;
+                const int m0 = mode;
+                const_cast<Walker*>(this)->mode = m0 & M_BLOCKS;
+                const uint64_t ok0 = probes_ok, f0 = probes_fail;
+                const Hit h0 = probe(node, w, dummy, r0);
+                const_cast<Walker*>(this)->mode = m0;
+                probes_ok = ok0;
+                probes_fail = f0;
+                if (h0.child == NODE_NONE) {
+                    ++probes_fail;
+                    return Hit{NODE_NONE, 0, false};
+                }
+            }
             const Hit h = probe(node, w, acc, rd);
             if (h.child != NODE_NONE) ++wide_hist[32 + bk];
             return h;
