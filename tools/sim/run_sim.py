@@ -26,7 +26,7 @@ from emqx_amd import Engine  # noqa: E402
 from emqx_amd import workload as W  # noqa: E402
 
 KINDS = ["inner", "leaf", "cold", "hot", "pair"]
-MODES = {"cur": 0, "slotrec": 1, "pair": 2, "spec": 4, "blocks": 8, "fix": 64, "nofp": 128}
+MODES = {"cur": 0, "slotrec": 1, "pair": 2, "spec": 4, "blocks": 8, "fix": 64, "nofp": 128, "gf": 256, "gfptr": 512}
 
 
 class View(ctypes.Structure):
@@ -169,6 +169,10 @@ def main():
         for part in name.split("+"):
             if part.startswith("occ"):
                 occ = int(part[3:])
+            elif part.startswith("gfmin"):   # gf: least literal children of a filtered node
+                mode |= int(part[5:]) << 16
+            elif part.startswith("gfbits"):   # gf: log2 words of the global filter (0: sized to ~8 % density)
+                mode |= int(part[6:]) << 24
             elif part.startswith("div"):   # per-node block load: size >= div x edges
                 mode |= int(part[3:]) << 8
             else:

@@ -89,7 +89,14 @@ enum Mode : int {
     M_SPECPROBE = 4, // the parent's reference says "WIDE": the home slot is loaded with the node (no Bloom)
     M_BLOCKS = 8,    // per-node child blocks: a WIDE node's literal / '#' edges in a contiguous open-addressing
                      // block of its own (blocks in node order = heat order), not one shared table
-    M_NOFP = 128,    // upper bound of a perfect per-node filter: a Bloom pass for an absent word costs no probe
+    M_NOFP = 128,
+    M_GFPTR = 512,   // with M_GF: the regions packed in node order (heat order) at 16 bits per child and found
+                     // through a pointer in the node (its useless Bloom bits): the filter load is a round of
+                     // its own after the node's half
+    M_GF = 256,      // a per-node filter for nodes with >= GF_MIN literal children: a region of a global bit
+                     // array at a hash of the node id, sized by a 2-bit class the reference to the node
+                     // carries, so the filter word is loaded beside the node's half (same round); an
+                     // absent word that passes the in-node Bloom but not the region costs no probe    // upper bound of a perfect per-node filter: a Bloom pass for an absent word costs no probe
     M_FIX = 64,      // a fixed 64 B block per node id (no pointer: address = v * 64): up to 8 literal children
                      // as 8 B {word, child} in 4 quads, home quad by word hash, quads probed in order (one
                      // round each); nodes with more children: the shared table (with M_BLOCKS: their own
@@ -157,8 +164,78 @@ struct Blocks {
     }
 };
 
+// M_GF: the global filter (built from the shared edge tables)
+struct GFilt {
+    uint32_t gbits = 0;                       // 2^gbits u32 words
+    std::vector<uint32_t> words;
+    std::vector<uint8_t> cls;                 // per node: 0 (none), 1..3
+    uint32_t min_children = 16;
+    static uint32_t region_words(uint32_t c) { return c == 1 ? 16u : c == 2 ? 128u : 1024u; }
+    static uint32_t cls_of(uint32_t children, uint32_t mn) {
+        return children < mn ? 0u : children <= 32 ? 1u : children <= 256 ? 2u : 3u;
+    }
+    bool packed = false;
+    std::vector<uint64_t> pbase;   // packed: per node its region's first word
+    std::vector<uint32_t> pwords;  // packed: per node its region's words (power of two)
+    uint32_t rwords(uint32_t v) const { return packed ? pwords[v] : region_words(cls[v]); }
+    uint64_t base(uint32_t v) const {
+        if (packed) return pbase[v];
+        const uint32_t R = region_words(cls[v]);
+        return (uint64_t)(fmix32(v * 0x9E3779B1u + 0x7F4A7C15u) & ((1u << gbits) - 1u)) & ~(uint64_t)(R - 1);
+    }
+    static uint32_t wpos(uint32_t w, uint32_t R) { return (w * 0x85EBCA77u >> 8) & (R - 1); }
+    static uint32_t wbits(uint32_t w) {
+        const uint32_t h = w * 0xC2B2AE35u;
+        return (1u << (h >> 27)) | (1u << ((h >> 22) & 31u));
+    }
+    void build(const View& v, uint32_t mn, uint32_t gb, bool pk) {
+        min_children = mn;
+        packed = pk;
+        const uint64_t n = v.n_nodes;
+        std::vector<uint32_t> cnt(n, 0);
+        for (const EdgeSlot* t : {v.cold, v.hot}) {
+            const uint64_t ns = t == v.cold ? v.cold_slots : v.hot_slots;
+            for (uint64_t s = 0; s < ns; ++s)
+                if (t[s].parent != EDGE_EMPTY && t[s].word != WORD_HASH) ++cnt[t[s].parent];
+        }
+        cls.assign(n, 0);
+        uint64_t eb = 0;
+        for (uint64_t x = 0; x < n; ++x) {
+            cls[x] = (uint8_t)cls_of(cnt[x], mn);
+            if (cls[x]) eb += cnt[x];
+        }
+        gbits = gb ? gb : 16;
+        while (!gb && (1ull << gbits) * 32 < eb * 2 * 24) ++gbits;   // ~8 % of the bits set
+        if (packed) {   // 16 bits per child, a power of two of u32 words, regions in node order
+            pbase.assign(n, 0);
+            pwords.assign(n, 0);
+            uint64_t cur = 0;
+            for (uint64_t x = 0; x < n; ++x) {
+                if (!cls[x]) continue;
+                uint32_t R = 1;
+                while (R * 32 < cnt[x] * 16) R <<= 1;
+                pwords[x] = R;
+                pbase[x] = cur;
+                cur += R;
+            }
+            gbits = 1;
+            while ((1ull << gbits) < cur) ++gbits;
+        }
+        words.assign(1ull << gbits, 0);
+        for (const EdgeSlot* t : {v.cold, v.hot}) {
+            const uint64_t ns = t == v.cold ? v.cold_slots : v.hot_slots;
+            for (uint64_t s = 0; s < ns; ++s) {
+                const EdgeSlot& e = t[s];
+                if (e.parent == EDGE_EMPTY || e.word == WORD_HASH || !cls[e.parent]) continue;
+                words[base(e.parent) + wpos(e.word, rwords(e.parent))] |= wbits(e.word);
+            }
+        }
+    }
+};
+
 struct Walker {
     const View& v;
+    const GFilt* gf = nullptr;
     int mode = 0;
     const Blocks* blk = nullptr;
     mutable uint64_t probes_ok = 0, probes_fail = 0, table_visits = 0, plus_now = 0, plus_pop = 0, lit_inline = 0;
@@ -279,6 +356,20 @@ struct Walker {
             const uint64_t b = word_bloom(w);
             const uint64_t mask = ((uint64_t)lc << 32) | lw;
             if ((mask & b) != b) return Hit{NODE_NONE, 0, false};
+            if (gf && gf->cls[node] && w < WORD_MAX) {   // the filter word came with the node's half (round 0)
+                const uint64_t i = gf->base(node) + GFilt::wpos(w, gf->rwords(node));
+                if (gf->packed) {   // after the node's half: a round of its own
+                    acc.push_back(Acc{(uint32_t)i, K_PAIR, (uint8_t)std::min<uint32_t>(rd, 255)});
+                    ++rd;
+                } else {
+                    acc.push_back(Acc{(uint32_t)i, K_PAIR, 0});
+                }
+                const uint32_t bb = GFilt::wbits(w);
+                if ((gf->words[i] & bb) != bb) {
+                    ++probes_fail;
+                    return Hit{NODE_NONE, 0, false};
+                }
+            }
             ++wide_hist[16 + bk];
             if (mode & M_NOFP) {   // the probe's outcome without its loads: an absent word stops here
                 std::vector<Acc> dummy;
@@ -419,6 +510,12 @@ int sim_run(const void* view, const uint32_t* levels, const uint32_t* words, con
     const View& vw = *reinterpret_cast<const View*>(view);
     Walker wk(vw, mode);
     Blocks blocks;
+    GFilt gfilt;
+    if (mode & M_GF) {
+        gfilt.build(vw, (uint32_t)((mode >> 16) & 0xFF) ? (uint32_t)((mode >> 16) & 0xFF) : 16u,
+                    (uint32_t)((mode >> 24) & 0x3F), (mode & M_GFPTR) != 0);
+        wk.gf = &gfilt;
+    }
     if (mode & (M_BLOCKS | M_FIX)) {
         blocks.build(vw, (uint32_t)((mode >> 8) & 0xFF) ? (uint32_t)((mode >> 8) & 0xFF) : 2u);
         wk.blk = &blocks;
@@ -437,7 +534,8 @@ int sim_run(const void* view, const uint32_t* levels, const uint32_t* words, con
         const uint64_t i = a.idx & 0x7FFFFFFFu, hi = a.idx >> 31;
         switch (a.kind) {
             case K_INNER: return 0 * R + i * 16;
-            case K_PAIR: return (mode & M_FIX) ? 4 * R + (uint64_t)a.idx * 16 : 0 * R + i * 16;
+            case K_PAIR: return (mode & M_FIX)  ? 4 * R + (uint64_t)a.idx * 16
+                                : (mode & M_GF) ? 5 * R + (uint64_t)a.idx * 4 : 0 * R + i * 16;
             case K_LEAF: return 1 * R + i * 16;
             case K_COLD: return 2 * R + i * sb + hi * 16;
             default: return 3 * R + i * sb + hi * 16;
