@@ -456,9 +456,18 @@ class RoutedSet:
         self.comms = Comm.init_all(self.devices)
 
     def insert_many(self, buf, off, gid_base=0):
-        for e in self.engines:
+        """every shard takes its part of the filter list; the shards build
+        in parallel threads (the C-ABI calls release the GIL, each engine has
+        its own locks), so S shards of C4's 100M filters build in about one
+        shard's time"""
+        from concurrent.futures import ThreadPoolExecutor
+
+        def build(e):
             e.insert_many(buf, off, gid_base)
             e.commit()
+        with ThreadPoolExecutor(max_workers=min(self.S, 8)) as ex:
+            for f in [ex.submit(build, e) for e in self.engines]:
+                f.result()
 
     def match_batches(self, batches):
         """batches: S host batches (tb, to); returns S (counts, offsets, gids)"""
