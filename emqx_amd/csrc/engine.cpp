@@ -245,7 +245,6 @@ struct Image {
     DevBuf d_rslots, d_rarena, d_rdest, d_fr_meta, d_rank_src, d_dt, d_rank_tg;
     DevBuf d_fshape;   // option "shape_keys": filter id -> order key
     DevBuf d_wheat;    // word id -> heat (option "presort" 2: the tail order's cost estimate)
-    DevBuf d_gf;       // option "gfilter": the big nodes' filter array (image.h gf_word)
     size_t arena_uploaded = 0, woff_uploaded = 0;
     uint64_t heat_uploaded = ~0ull;   // word_heat version in d_wheat
     uint32_t heat_words = 0;          // words in d_wheat (the host table may have grown since)
@@ -260,8 +259,7 @@ struct Image {
     AggreView av{};
     void release() {
         for (DevBuf* b : {&d_nodes, &d_edges, &d_hedges, &d_dict, &d_arena, &d_woff, &d_inner, &d_leaf, &d_rslots,
-                          &d_rarena, &d_rdest, &d_fr_meta, &d_rank_src, &d_dt, &d_rank_tg, &d_fshape, &d_wheat,
-                          &d_gf})
+                          &d_rarena, &d_rdest, &d_fr_meta, &d_rank_src, &d_dt, &d_rank_tg, &d_fshape, &d_wheat})
             b->release();
         for (hipEvent_t ev : uses) (void)hipEventDestroy(ev);
         uses.clear();
@@ -805,7 +803,7 @@ struct tm_engine {
         e.parent = parent;
         e.word = word;
         e.child = child;
-        e.plus = SLOT_RECORD ? c.plus : child_sum(child) | node_cls(child) << SLOT_CLS_SHIFT;
+        e.plus = SLOT_RECORD ? c.plus : child_sum(child);
 #if TM_SLOT_RECORD
         e.hash_filter = c.hash_filter;
         e.lw = c.lw;
@@ -817,29 +815,6 @@ struct tm_engine {
     // the summary a child's edge slot carries (image.h EdgeSlot): its own
     // S(c), so the walk drops a table child whose subtree cannot match
     uint32_t child_sum(uint32_t x) const { return summaries ? aux[x].sum : SUM_ALL; }
-
-    // ---- per-node filters of the big WIDE nodes (option "gfilter", image.h
-    // gf_word): classes are assigned by relayout from the children counts
-    // and stay until the next one (a node created since has class 0, a node
-    // that shrank keeps its region); a literal child added to a classed node
-    // sets its bits, a removed one leaves them (a superset: false positives
-    // only).  The class rides in the references to the node: its parent's
-    // '+' field and its edge slot.
-    int gfilter = 0;                  // option "gfilter" (1: on; changing it relayouts; C3 walk 8.55 vs 8.46 ms off)
-    std::vector<uint8_t> ncls;        // per node: 0 or 1..3
-    std::vector<uint32_t> gfa;        // the filter array (a power of two of u32, >= 1024; empty: off)
-    Dirty gf_dirty, prev_gf_dirty;
-    uint32_t node_cls(uint32_t x) const { return x < ncls.size() ? ncls[x] : 0u; }
-    void gf_add(uint32_t v, uint32_t w) {
-        const uint32_t c = node_cls(v);
-        if (!c || gfa.empty() || w >= WORD_MAX) return;
-        const uint64_t i = gf_word(v, c, w, gfa.size() - 1);
-        const uint32_t b = gf_bits(w);
-        if ((gfa[i] & b) != b) {
-            gfa[i] |= b;
-            gf_dirty.mark(i);
-        }
-    }
     void refresh_slot_sum(uint32_t x) {
         if (SLOT_RECORD) return;   // such slots carry the child's record instead
         const uint32_t p = aux[x].parent, w = aux[x].word;
@@ -848,7 +823,7 @@ struct tm_engine {
         const size_t s = edge_find_slot(p, w);
         if (s == SIZE_MAX) return;
         EdgeSlot& e = tab(p).slots[s];
-        const uint32_t v = child_sum(x) | node_cls(x) << SLOT_CLS_SHIFT;
+        const uint32_t v = child_sum(x);
         if (e.plus != v) {
             e.plus = v;
             tab(p).dirty.mark(s);
@@ -912,7 +887,6 @@ struct tm_engine {
         }
         nodes[id] = empty_node();
         aux[id] = NodeAux{parent, word, 0, 0, (uint16_t)SUM_NONE, (uint16_t)SUM_NONE};
-        if (id < ncls.size()) ncls[id] = 0;   // (a reused id: no filter until the next relayout)
         if (word < WORD_MAX) heat_bump(word, +1);
         node_dirty.mark(id);
         ++live_nodes;
@@ -963,11 +937,9 @@ struct tm_engine {
             y.lw = 0;
             y.lc = 0;
             bloom_add(y, w0);
-            gf_add(v, w0);
         }
         edge_insert(v, w, c);
         bloom_add(nodes[v], w);
-        gf_add(v, w);
     }
     void lit_remove(uint32_t v, uint32_t w) {
         Node& x = nodes[v];
@@ -1806,34 +1778,6 @@ struct tm_engine {
             if (e.word != WORD_HASH) bloom_add(nn[newid[e.parent]], e.word);
         nodes.swap(nn);
         aux.swap(na);   // before the edges are placed: slot_for reads the children's new summaries
-        // per-node filters (option "gfilter", image.h): classes from the
-        // children counts, before the edges are placed (slot_for puts each
-        // child's class in its slot), the regions filled from the literal
-        // edges, and every '+' field given its child's class
-        ncls.assign(nodes.size(), 0);
-        std::vector<uint32_t>().swap(gfa);
-        if (gfilter && !SLOT_RECORD) {
-            uint64_t eb = 0;
-            for (size_t v = 0; v < nodes.size(); ++v)
-                if (nodes[v].plus & WIDE) {
-                    ncls[v] = (uint8_t)gf_class_of(aux[v].lit_count);
-                    if (ncls[v]) eb += aux[v].lit_count;
-                }
-            if (eb) {
-                uint64_t words = 1024;
-                while (words * 32 < eb * 48) words <<= 1;   // 2 bits per child in 48: ~4 % of the bits set
-                gfa.assign(words, 0);
-                for (const EdgeSlot& e : old)
-                    if (e.word != WORD_HASH) gf_add(newid[e.parent], e.word);
-                for (Node& x : nodes) {
-                    const uint32_t pc = x.plus & NODE_MASK;
-                    if (pc != NODE_NONE) x.plus |= (uint32_t)ncls[pc] << CLS_SHIFT;
-                }
-            } else {
-                std::fill(ncls.begin(), ncls.end(), 0);
-            }
-        }
-        gf_dirty.all = true;
         hot_limit = new_hot_limit;
         size_t nhot = 0;
         for (const EdgeSlot& e : old) nhot += newid[e.parent] < hot_limit;
@@ -1908,9 +1852,6 @@ struct tm_engine {
         im.fshape = shape_keys ? g.d_fshape.as<const uint64_t>() : nullptr;
         im.word_heat = g.d_wheat.as<const uint8_t>();
         im.n_words = g.heat_words;
-        im.root_cls = gfa.empty() ? 0u : node_cls(ROOT);
-        im.gfilt = gfa.empty() ? nullptr : g.d_gf.as<const uint32_t>();
-        im.gf_mask = gfa.empty() ? 0 : gfa.size() - 1;
         return im;
     }
 
@@ -2010,7 +1951,6 @@ struct tm_engine {
             upload_table(d, g, g.d_edges, cold.slots, cold.dirty, prev_cold_dirty);
             upload_table(d, g, g.d_hedges, hot.slots, hot.dirty, prev_hot_dirty);
             upload_table(d, g, g.d_dict, dict, dict_dirty, prev_dict_dirty);
-            upload_table(d, g, g.d_gf, gfa, gf_dirty, prev_gf_dirty);
             upload_table(d, g, g.d_rslots, rt_slots, t_slots.cur, t_slots.prev);
             upload_table(d, g, g.d_rarena, rt_arena, t_rarena.cur, t_rarena.prev);
             upload_table(d, g, g.d_rdest, rt_dest, t_rdest.cur, t_rdest.prev);
@@ -2062,8 +2002,7 @@ struct tm_engine {
         for (const Rot& r : {Rot{&node_dirty, &prev_node_dirty, nodes.size()},
                              Rot{&cold.dirty, &prev_cold_dirty, cold.slots.size()},
                              Rot{&hot.dirty, &prev_hot_dirty, hot.slots.size()},
-                             Rot{&dict_dirty, &prev_dict_dirty, dict.size()},
-                             Rot{&gf_dirty, &prev_gf_dirty, gfa.size()}}) {
+                             Rot{&dict_dirty, &prev_dict_dirty, dict.size()}}) {
             *r.prev = *r.cur;
             r.cur->clear();
             r.cur->limit = std::max<size_t>(4096, r.elems / 16);
@@ -3040,7 +2979,7 @@ int tm_engine_device(tm_engine* e) { return e ? e->device : -1; }
 uint64_t tm_image_bytes(tm_engine* e) {
     if (!e) return 0;
     return e->nodes.size() * sizeof(Node) + (e->cold.slots.size() + e->hot.slots.size()) * sizeof(EdgeSlot) +
-           e->dict.size() * sizeof(DictSlot) + e->gfa.size() * 4 +
+           e->dict.size() * sizeof(DictSlot) +
            e->word_arena.size() + e->word_off.size() * 4;
 }
 
@@ -3701,40 +3640,6 @@ int tm_match_small_device(tm_engine* e, const uint8_t* d_bytes, const uint64_t* 
 // range-local word-hash order, 2 the tail order, 0 arrival order ...)
 extern "C" int tm_debug_last_order(tm_engine* e) { return e ? e->last_order.load() : TM_EINVAL; }
 
-// diagnostics (not part of include/topicmatch.h): host-side consistency of
-// the per-node filters (option "gfilter", image.h gf_word): every literal
-// child of a classed WIDE node has its bits in the node's region (no false
-// negative), every edge slot carries its child's class, every '+' field its
-// '+' child's class.  TM_OK, or TM_EINVAL naming the first defect (stderr).
-extern "C" int tm_debug_check_filters(tm_engine* e) {
-    if (!e) return TM_EINVAL;
-    return guarded(e, [&]() -> int {
-        auto fail = [](const std::string& m) {
-            std::fprintf(stderr, "tm_debug_check_filters: %s\n", m.c_str());
-            return TM_EINVAL;
-        };
-        for (const auto* t : {&e->cold, &e->hot})
-            for (const EdgeSlot& s : t->slots) {
-                if (s.parent == EDGE_EMPTY) continue;
-                if (((s.plus >> SLOT_CLS_SHIFT) & 3u) != e->node_cls(s.child))
-                    return fail("slot of child " + std::to_string(s.child) + ": class bits");
-                if (s.word == WORD_HASH || !e->node_cls(s.parent)) continue;
-                if (e->gfa.empty()) return fail("class without a filter array");
-                const uint32_t b = gf_bits(s.word);
-                if ((e->gfa[gf_word(s.parent, e->node_cls(s.parent), s.word, e->gfa.size() - 1)] & b) != b)
-                    return fail("node " + std::to_string(s.parent) + ": word " + std::to_string(s.word) +
-                                " missing from its filter");
-            }
-        for (size_t v = 0; v < e->nodes.size(); ++v) {
-            const uint32_t pc = e->nodes[v].plus & NODE_MASK;
-            if (pc == NODE_NONE) continue;
-            if (((e->nodes[v].plus & CLS_MASK) >> CLS_SHIFT) != e->node_cls(pc))
-                return fail("node " + std::to_string(v) + ": '+' child class bits");
-        }
-        return TM_OK;
-    });
-}
-
 // diagnostics (not part of include/topicmatch.h): the phases of the last
 // per-lane queue walk on replica 0, per XCD x (kernels.h QWS_CLOCK):
 // out[4x..4x+3] = ms from the walk's first wave start to XCD x's first wave
@@ -3939,15 +3844,6 @@ int tm_set_option(tm_engine* e, const char* name, int64_t value) {
         if (!std::strcmp(name, "light_tail")) {   // per mille of each range walked last by presort 6
             if (value < 0 || value > 500) return TM_EINVAL;
             e->light_tail = (uint32_t)value;
-            return TM_OK;
-        }
-        if (!std::strcmp(name, "gfilter")) {   // per-node filters of the big WIDE nodes (image.h gf_word)
-            if (value < 0 || value > 1) return TM_EINVAL;
-            if ((int)value != e->gfilter) {
-                e->gfilter = (int)value;
-                e->force_relayout = true;   // classes and regions are laid out by relayout
-                e->dev_dirty = true;
-            }
             return TM_OK;
         }
         if (!std::strcmp(name, "relayout")) {   // 1: relayout at the next commit (layout A/Bs)

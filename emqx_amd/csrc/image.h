@@ -131,9 +131,6 @@ struct ImageView {
     const uint64_t* fshape;            // filter id -> order key (filter_shape), or null (option "shape_keys" off)
     const uint8_t*  word_heat;         // word id -> floor(log2(1 + nodes it labels)) (presort mode 2)
     uint32_t        n_words;
-    uint32_t        root_cls;          // option "gfilter": the root's filter class (0: none)
-    const uint32_t* gfilt;             // option "gfilter": the global filter array (null: off)
-    uint64_t        gf_mask;           // its words - 1
 };
 
 
@@ -262,42 +259,6 @@ TM_HD uint64_t word_bloom(uint32_t w) {
     }
     const uint32_t h = w * 0x9E3779B1u;
     return (1ull << (h >> 26)) | (1ull << ((h >> 20) & 63u));
-}
-
-// Per-node filters of the big WIDE nodes (option "gfilter").  A WIDE node's
-// 64-bit Bloom passes nearly every word once it has more than ~32 children,
-// and each such pass for a word that is not a child is an edge-table probe
-// of a random line: 11.9 per C3 topic, the largest class of the walk's L2
-// misses (tools/sim: without them 18.0 instead of 32.3 fabric reads per
-// topic).  A node with >= GF_MIN literal children at relayout gets a class
-// (1: <= 32 children, 2: <= 256, 3: more) and a region of a global bit
-// array at a hash of its id, 16 bits per child of the class's bound; a
-// child word sets 2 bits of one u32 of the region.  The class rides in every
-// reference the walk follows to the node -- bits 29-30 of the parent's '+'
-// field, bits 16-17 of the edge slot's summary word, bits 29-30 of an
-// unkeyed walk's path entry -- so the walk loads the filter word beside the
-// node's own half (no extra dependent round), and an absent word that the
-// Bloom lets through costs no probe.  Regions of different nodes may
-// overlap: a shared bit is a false positive, never a miss (bits are only
-// set between relayouts, which rebuild them exactly).
-constexpr uint32_t GF_MIN = 16;
-constexpr uint32_t CLS_SHIFT = 29;              // class in node references (plus field, path entries)
-constexpr uint32_t CLS_MASK = 3u << CLS_SHIFT;
-constexpr uint32_t SLOT_CLS_SHIFT = 16;         // class in EdgeSlot::plus (above the 15-bit summary)
-TM_HD uint32_t gf_class_of(uint32_t children) {
-    return children < GF_MIN ? 0u : children <= 32 ? 1u : children <= 256 ? 2u : 3u;
-}
-TM_HD uint32_t gf_region_words(uint32_t cls) { return cls == 1 ? 16u : cls == 2 ? 128u : 1024u; }
-// the u32 of the global array (gmask + 1 words, a power of two >= 1024)
-// holding word w's bits in node v's region
-TM_HD uint64_t gf_word(uint32_t v, uint32_t cls, uint32_t w, uint64_t gmask) {
-    const uint32_t R = gf_region_words(cls);
-    const uint64_t base = ((uint64_t)fmix32(v * 0x9E3779B1u + 0x7F4A7C15u) & gmask) & ~(uint64_t)(R - 1);
-    return base + ((w * 0x85EBCA77u >> 8) & (R - 1));
-}
-TM_HD uint32_t gf_bits(uint32_t w) {
-    const uint32_t h = w * 0xC2B2AE35u;
-    return (1u << (h >> 27)) | (1u << ((h >> 22) & 31u));
 }
 
 // home slot of key (parent, word): a 32-bit mix (three 32-bit multiplies)

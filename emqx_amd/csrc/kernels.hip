@@ -613,17 +613,15 @@ __device__ __forceinline__ Hit probe_edge(const ImageView& im, uint32_t v, uint3
 // WORD_PLUS / WORD_HASH reproduce the reference for the out-of-domain topic
 // levels "+" / "#": the fold over [W, '+'] at emqx_trie.erl:131-136 follows
 // the '+' / '#' edge.
-// fok: the node's filter (option "gfilter") admits w (true without one).
-// A table child's filter class comes back in bits 16-17 of Hit::plus.
 template <bool STATS>
 __device__ __forceinline__ Hit lit_child(const ImageView& im, uint32_t v, uint32_t plus, uint32_t lw, uint32_t lc,
-                                         uint32_t w, uint64_t& loads, bool fok = true) {
+                                         uint32_t w, uint64_t& loads) {
     const Hit none{NODE_NONE, 0, 0, 0, 0, 0, false};
     if (w < WORD_MAX) {
         if (!(plus & WIDE)) return Hit{lw == w ? lc : NODE_NONE, SUM_ALL, 0, 0, 0, 0, false};
         const uint64_t b = word_bloom(w);
         const uint64_t mask = ((uint64_t)lc << 32) | lw;
-        return (mask & b) == b && fok ? probe_edge<STATS>(im, v, w, loads) : none;
+        return (mask & b) == b ? probe_edge<STATS>(im, v, w, loads) : none;
     }
     if (w == WORD_PLUS) return Hit{plus & NODE_MASK, SUM_ALL, 0, 0, 0, 0, false};
     if (w == WORD_HASH) return probe_edge<STATS>(im, v, WORD_HASH, loads);
@@ -790,16 +788,15 @@ __device__ __forceinline__ bool walk_begin(const ImageView& im, Cursor& c, uint3
     c.pend = 0;
     c.pf_id = NODE_NONE;
     if (!dollar) {
-        c.v = ROOT | im.root_cls << CLS_SHIFT;
+        c.v = ROOT;
         c.r = c.r0 = 0;
         return true;
     }
     c.key = rank_sym(0, 1);
     const uint4 q = load_half(im, ROOT, false);
-    const Hit g = lit_child<false>(im, ROOT, q.x, q.z, q.w, W(0), st.probe_loads);
-    c.v = g.child | ((g.plus >> SLOT_CLS_SHIFT) & 3u) << CLS_SHIFT;
+    c.v = lit_child<false>(im, ROOT, q.x, q.z, q.w, W(0), st.probe_loads).child;
     c.r = c.r0 = 1;
-    return g.child != NODE_NONE;
+    return c.v != NODE_NONE;
 }
 
 // one step; true when the topic's walk is complete.  A step loads ONE node
@@ -827,8 +824,8 @@ __device__ __forceinline__ bool walk_pop(Cursor& c, Path path, uint32_t r, uint6
     }
     for (uint32_t k = r; k > c.r0;) {   // scan the path down
         --k;
-        const uint32_t p = KEYS ? path(k) & NODE_MASK : path(k);   // (unkeyed: with the node's filter class)
-        if ((p & NODE_MASK) != NODE_NONE) {
+        const uint32_t p = KEYS ? path(k) & NODE_MASK : path(k);
+        if (p != NODE_NONE) {
             if (STATS && st.hist) atomicAdd(st.hist + 50, 1ull);
             path(k) = KEYS ? (NODE_NONE | SYM_PLUS) : NODE_NONE;
             c.v = p;
@@ -843,16 +840,9 @@ __device__ __forceinline__ bool walk_pop(Cursor& c, Path path, uint32_t r, uint6
 template <bool STATS, bool KEYS, class Path, class Words, class Emit>
 __device__ __forceinline__ bool walk_step(const ImageView& im, Cursor& c, Path path, const Words& W, Emit& emit,
                                           WalkStats& st) {
-    uint32_t v = c.v & NODE_MASK, r = c.r;
+    uint32_t v = c.v, r = c.r;
     uint64_t key = KEYS ? c.key : 0ull;
     bool leaf = r == c.n;
-    // the topic word of this level, and (option "gfilter") the node's filter
-    // word for it, loaded beside the node's half: the reference that led
-    // here carried the node's filter class
-    uint32_t w = leaf ? WORD_NONE : W(r);
-    const uint32_t vcls = (c.v >> CLS_SHIFT) & 3u;
-    uint32_t fw = ~0u;
-    if (!STATS && vcls && w < WORD_MAX && im.gfilt) fw = im.gfilt[gf_word(v, vcls, w, im.gf_mask)];
     uint4 h;
     if (TM_PF1 && !STATS) {
         const uint32_t sib = r > c.r0 ? (KEYS ? path(r - 1) & NODE_MASK : path(r - 1)) : NODE_NONE;
@@ -885,15 +875,15 @@ __device__ __forceinline__ bool walk_step(const ImageView& im, Cursor& c, Path p
         // with k = n - r - 1 levels left below it is never loaded.  The
         // stats walk (STATS) prunes nothing, so its E and visits are the
         // reference's, and counts what the summaries would skip.
+        const uint32_t w = W(r);
         bool lit_ok = true, plus_ok = true;
         if (hf & SUM_TAG) {
             const uint32_t k = c.n - r - 1;
             plus_ok = sum_useful(hf & SUM_ALL, k);
             lit_ok = w < WORD_MAX ? sum_useful((hf >> 15) & SUM_ALL, k) : w == WORD_PLUS ? plus_ok : true;
         }
-        const uint32_t fb = gf_bits(w);
         Hit g = (!STATS && !lit_ok) ? Hit{NODE_NONE, 0, 0, 0, 0, 0, false}
-                                    : lit_child<STATS>(im, v, plus, lw, lc, w, st.probe_loads, (fw & fb) == fb);
+                                    : lit_child<STATS>(im, v, plus, lw, lc, w, st.probe_loads);
         // a table child's own summary (its edge slot's fourth word): the
         // union summary above admitted the literal children as a whole
         const bool child_ok = SLOT_RECORD || g.child == NODE_NONE || sum_useful(g.plus & SUM_ALL, c.n - r - 1);
@@ -908,22 +898,19 @@ __device__ __forceinline__ bool walk_step(const ImageView& im, Cursor& c, Path p
         if (STATS) st.prunable += (g.child != NODE_NONE && !lit_ok ? 1u : 0u) +
                                   ((plus & NODE_MASK) != NODE_NONE && !plus_ok ? 1u : 0u);
         const uint32_t pc = (STATS || plus_ok) ? (plus & NODE_MASK) : NODE_NONE;
-        // the '+' child with its filter class (unkeyed path entries and the
-        // cursor; a keyed path entry's bits 29-30 hold the branch symbol)
-        const uint32_t pcc = pc | (pc != NODE_NONE ? (plus & CLS_MASK) : 0u);
         if (STATS && st.hist) {   // how the next visit is reached: [48] inline literal, [49] table literal,
                                   // [50] '+' (here or by a later pop: counted at the pop)
             if (g.child != NODE_NONE) atomicAdd(st.hist + ((plus & WIDE) ? 49 : 48), 1ull);
             else if ((plus & NODE_MASK) != NODE_NONE) atomicAdd(st.hist + 50, 1ull);
         }
         if (g.child != NODE_NONE) {   // literal subtree first, '+' child pending at level r
-            path(r) = KEYS ? (pc | SYM_LIT) : pcc;
+            path(r) = KEYS ? (pc | SYM_LIT) : pc;
             if (Path::kMask) c.pend = pc != NODE_NONE ? (c.pend | (1u << r)) : (c.pend & ~(1u << r));
             v = g.child;
             if (KEYS) key |= rank_sym(r, 1);
             ++r;
             if (!g.have) {
-                c.v = v | ((g.plus >> SLOT_CLS_SHIFT) & 3u) << CLS_SHIFT;
+                c.v = v;
                 c.r = r;
                 if (KEYS) c.key = key;
                 return false;
@@ -934,14 +921,12 @@ __device__ __forceinline__ bool walk_step(const ImageView& im, Cursor& c, Path p
             lc = g.lc;
             sf = g.sf;
             leaf = r == c.n;
-            w = leaf ? WORD_NONE : W(r);
-            fw = ~0u;
             continue;
         }
         if (pc != NODE_NONE) {        // no literal child: straight into the '+' subtree
             path(r) = KEYS ? (NODE_NONE | SYM_PLUS) : NODE_NONE;
             if (Path::kMask) c.pend &= ~(1u << r);
-            c.v = pcc;
+            c.v = pc;
             c.r = r + 1;
             if (KEYS) c.key = key | rank_sym(r, 2);
             return false;

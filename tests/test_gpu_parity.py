@@ -263,9 +263,6 @@ VARIANTS = {"queue": {}, "queue_xcd": {}, "queue_xcd@nosplit@dfs": {"split": 0, 
             # range-keyed orders with a word-hash part (two radix passes)
             "queue_xcd@order4": {"presort": 4}, "queue_xcd@order5@stagek8": {"presort": 5, "stage_k": 8},
             # the range-local word-hash order with the lightest topics of each range last (three radix passes)
-            # the walk with the big nodes' filters (option "gfilter", off by default)
-            "queue_xcd@gfilter": {"gfilter": 1}, "queue@gfilter@order5": {"gfilter": 1, "presort": 5},
-            "queue_xcd@gfilter@tail@nosummaries": {"gfilter": 1, "presort": 2, "summaries": 0},
             # the per-lane tokenizer (the wave-cooperative one is the default)
             "queue_xcd@toklane": {"tok_wave": 0}, "queue_xcd@toklane@order5": {"tok_wave": 0, "presort": 5},
             "queue_xcd@order6": {"presort": 6}, "queue_xcd@order6@bits16@tail300": {"presort": 6, "sort_bits": 16,
