@@ -10,6 +10,7 @@ import os
 import socket
 import sys
 
+import pytest
 import torch.multiprocessing as mp
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -65,8 +66,11 @@ def _worker(rank, world, port, depth, q):
     dist.destroy_process_group()
 
 
-def test_two_rank_routed_lists_equal_full_trie():
-    world, port = 2, _free_port()
+@pytest.mark.parametrize("world", [2, 8])
+def test_routed_lists_equal_full_trie(world):
+    """world 2 and 8 (the routed mode's placement and topic routing over the
+    driver's 8-rank launch shape, on the CPU)"""
+    port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     procs = [ctx.Process(target=_worker, args=(r, world, port, 2, q)) for r in range(world)]
@@ -78,4 +82,4 @@ def test_two_rank_routed_lists_equal_full_trie():
         assert p.exitcode == 0
     assert all(ok for _, ok, _, _ in res)
     assert sum(o for _, _, o, _ in res) == sum(n for _, _, _, n in res)   # every topic walked once
-    assert all(0 < o for _, _, o, _ in res)                               # both ranks own topics
+    assert all(0 < o for _, _, o, _ in res)                               # every rank owns topics
