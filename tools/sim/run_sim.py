@@ -131,7 +131,12 @@ def main():
     for kv in a.opt:
         k, x = kv.split("=")
         eng.set_option(k, int(x))
-    eng.insert_many(fb, fo)
+    step = 5_000_000   # in chunks, with progress (a silent multi-minute build reads as a hang)
+    n = len(fo) - 1
+    for i in range(0, n, step):
+        j = min(n, i + step)
+        eng.insert_many(fb, fo[i:j + 1])
+        print("# inserted %d / %d filters (%.0fs)" % (j, n, time.time() - t0), file=sys.stderr, flush=True)
     eng.commit()
     print("# built %d filters, %d nodes in %.1fs" % (eng.filter_count, eng.node_count, time.time() - t0),
           file=sys.stderr, flush=True)
