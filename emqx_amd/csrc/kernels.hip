@@ -432,7 +432,8 @@ __device__ __forceinline__ uint32_t tokenize_one(const ImageView& im, const B& b
 constexpr uint32_t TOK_LMAX = 1000;
 constexpr uint32_t TOK_WAVE = 1u << 24;   // key_mode bit: the wave path (option "tok_wave"; 0: per lane)
 #ifndef TM_TOK_BATCH
-#define TM_TOK_BATCH 3   // dictionary probes in flight per lane (4: 97 VGPRs, 4 waves per SIMD)
+#define TM_TOK_BATCH 3   // dictionary probes in flight per lane (4 held to 96 VGPRs, or at 97 and 4 waves:
+                         // the same or slower, profiles/r06_h_ab, r06_i_ab)
 #endif
 // the bytes of window word q (window offset 8q) inside [b, e)
 __device__ __forceinline__ uint64_t range_bytes(uint32_t q, uint32_t b, uint32_t e) {
@@ -1633,7 +1634,8 @@ constexpr uint32_t COPY_WAVE_MIN = TM_COPY_WAVE_MIN;
 #define TM_COPY_NT 0   // A/B builds: the unkeyed copy-out's stage reads and output stores non-temporal
 #endif
 #ifndef TM_COPY_U
-#define TM_COPY_U 4   // unkeyed copy-out: topics per wave with their row loads in flight together (1: one at a time)
+#define TM_COPY_U 8   // unkeyed copy-out: topics per wave with their row loads in flight together (1: one at a time;
+                      // 8 vs 4: 0.803-0.809 vs 0.827-0.843 ms at C3 8M, profiles/r06_h_ab, r06_i_ab)
 #endif
 constexpr uint32_t COPY_U = TM_COPY_U;
 

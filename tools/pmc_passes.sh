@@ -22,6 +22,10 @@ pass() {
     sq)    run sq SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_BUSY_CYCLES ;;
     tcp)   run tcp TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCP_TCC_WRITE_REQ_sum TCP_TOTAL_READ_sum ;;
     ta)    run ta TA_TA_BUSY_sum TA_BUFFER_READ_WAVEFRONTS_sum ;;
+    # LDS behaviour of the tokenizer and the walk: bank conflicts, unaligned
+    # 64/128-bit replays, LDS issue stalls (MI355X_MICROARCH.md LDS section)
+    lds)   run lds SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_LDS_UNALIGNED_STALL SQ_INSTS_LDS SQ_WAIT_INST_LDS \
+              SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_WAIT_ANY ;;
     tlb)   run tlb TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_UTCL1_REQUEST_sum TCP_TCC_READ_REQ_sum ;;
     # the L2 and translation groups in one pass (3 TCC + 4 TCP slots): for
     # workloads whose build dominates a pass (C4: 100M filters)
