@@ -3852,9 +3852,8 @@ int tm_set_option(tm_engine* e, const char* name, int64_t value) {
             e->dev_dirty = true;
             return TM_OK;
         }
-        if (!std::strcmp(name, "presort")) {   // 0 arrival order, 1 word-hash key, 2 the tail order, 3 auto,
-                                                // 7 word-hash key with work-balanced XCD ranges (kernels.h)
-            if (value < 0 || value > 7) return TM_EINVAL;
+        if (!std::strcmp(name, "presort")) {   // 0 arrival order, 1 word-hash key, 2 the tail order, 3 auto
+            if (value < 0 || value > 6) return TM_EINVAL;
             e->presort = (int)value;
             return TM_OK;
         }

@@ -13,7 +13,6 @@ constexpr size_t QWS_BYTES = 3328;   // queue heads: 8 ranges x 128 B, 8 spill c
                                      // the batch's cost histogram
 constexpr size_t QWS_MAXC = 120;     // u64 slot of ws: the batch's largest match count
 constexpr size_t QWS_MAXL = 121;     // u64 slot of ws: most levels of a topic in a keyed batch
-constexpr size_t QWS_BND = 122;      // u64 slots 122-126 as u32 [0..8]: presort 7's XCD range bounds (8 = n when set)
 constexpr size_t QWS_SPILL = 128;    // u64 slots 128 + 16 x: spill chunks taken by XCD x's waves
 // u64 slots 256 + 16 x (per-lane queue walks with XCD ranges; diagnostics,
 // tm_debug_walk_clocks): wall clock of XCD x's first wave start (stored
@@ -51,9 +50,7 @@ struct QueueBufs {
     unsigned long long* ws;   // QWS_BYTES of queue heads
     uint32_t* perm;       // option "presort": queue position -> topic (n), or null (arrival order)
     uint32_t presort_mode = 1;   // 1: key of the first eight words; 2: the tail order (kernels.hip
-                                 // tail_key: heavy topics first in each XCD range, one radix pass);
-                                 // 7: the key of 1 over the whole batch, XCD ranges cut at equal
-                                 // predicted work (presort.hip tm_presort_bounds)
+                                 // tail_key: heavy topics first in each XCD range, one radix pass)
     uint32_t sort_passes = 4;    // mode 1: radix passes over the key's top 8 * sort_passes bits (1..4)
     uint32_t light_max = 31;     // mode 6: cost classes <= light_max are walked last in their XCD range
     // the radix passes of the batch's presort: the tokenizer writes the keys

@@ -376,15 +376,6 @@ __device__ __forceinline__ uint32_t tok_store(const ImageView& im, uint32_t t, u
         // top bits - 3; 6 the range's 3 bits, a light-tail bit, then the
         // word-hash key's top bits - 4)
         const uint32_t mode = key_mode & 255u, bits = (key_mode >> 8) & 255u;
-        if (mode == 7) {   // the global word-hash key's top 24 bits, the topic's predicted cost in the low 8
-            uint32_t cost = 0;
-#pragma unroll
-            for (uint32_t l = 0; l < 8; ++l)
-                if (l < lev && tw[l] < im.n_words) cost += im.word_heat[tw[l]];
-            skeys[t] = (presort_key(tw, lev) & ~0xFFu) | (cost < 255u ? cost : 255u);
-            svals[t] = t;
-            return 32u;
-        }
         if (mode == 6) {
             const uint32_t tk = tail_key(im, tw, lev, t, n), c = 31u - (tk & 31u);
             const uint32_t light = c <= ((key_mode >> 16) & 255u) ? 1u : 0u;
@@ -1171,12 +1162,8 @@ walk_queue_body(ImageView im, const uint64_t* __restrict__ off, uint32_t n, cons
                 if (XCDQ) {
                     while (qr < QRANGES) {
                         const uint32_t r = (home + qr) & (QRANGES - 1);
-                        // presort 7: the ranges' bounds at equal predicted work
-                        // (ws QWS_BND, written after the sort; 0: equal counts)
-                        const uint32_t* bnd = reinterpret_cast<const uint32_t*>(ws + QWS_BND);
-                        const bool bv = bnd[QRANGES] == nq;
-                        const uint32_t rb = bv ? bnd[r] : (uint32_t)((uint64_t)nq * r / QRANGES);
-                        const uint32_t re = bv ? bnd[r + 1] : (uint32_t)((uint64_t)nq * (r + 1) / QRANGES);
+                        const uint32_t rb = (uint32_t)((uint64_t)nq * r / QRANGES);
+                        const uint32_t re = (uint32_t)((uint64_t)nq * (r + 1) / QRANGES);
                         uint32_t x = 0;
                         if (lane == leader)
                             x = (uint32_t)__hip_atomic_fetch_add(ws + 16 * r, (unsigned long long)QCHUNK,

@@ -217,51 +217,6 @@ tm_presort_gather(const uint32_t* __restrict__ perm, const uint32_t* __restrict_
     meta_s[p] = mt;
 }
 
-// presort 7: the sorted keys carry each topic's predicted cost (kernels.hip
-// tok_store: the summed heat of its first eight words) in their low byte.
-// The walk's 8 XCD ranges are cut where the running cost crosses k/8 of the
-// total (at 4096-topic tile precision), so every XCD gets a contiguous slice
-// of the key space -- its L2 holds that slice's nodes, not a copy of every
-// prefix's -- and about the same work.
-__global__ void __launch_bounds__(PS_BLOCK)
-tm_presort_cost_tiles(const uint32_t* __restrict__ keys, uint32_t n, uint32_t* __restrict__ tsum) {
-    __shared__ uint32_t part[PS_WAVES];
-    const uint32_t base = blockIdx.x * PS_TILE;
-    uint32_t c = 0;
-    for (uint32_t r = 0; r < PS_ROUNDS; ++r) {
-        const uint32_t i = base + r * PS_BLOCK + threadIdx.x;
-        if (i < n) c += keys[i] & 255u;
-    }
-    for (int o = 32; o > 0; o >>= 1) c += (uint32_t)__shfl_xor((int)c, o, 64);
-    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = c;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t t = 0;
-        for (uint32_t w = 0; w < PS_WAVES; ++w) t += part[w];
-        tsum[blockIdx.x] = t;
-    }
-}
-constexpr uint32_t PS_BND_TILES = 8192;   // tiles the one-block bound search holds in LDS (32M topics)
-__global__ void __launch_bounds__(PS_BLOCK)
-tm_presort_bounds(const uint32_t* __restrict__ tsum, uint32_t tiles, uint32_t n, uint32_t* __restrict__ bnd) {
-    __shared__ uint32_t ts[PS_BND_TILES];
-    for (uint32_t i = threadIdx.x; i < tiles; i += PS_BLOCK) ts[i] = tsum[i];
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint64_t total = 0;
-        for (uint32_t i = 0; i < tiles; ++i) total += ts[i];
-        uint64_t run = 0;
-        uint32_t q = 1, i = 0;
-        bnd[0] = 0;
-        for (; i < tiles && q < 8; ++i) {
-            while (q < 8 && run * 8 >= total * q) bnd[q++] = i * PS_TILE;
-            run += ts[i];
-        }
-        while (q < 8) bnd[q++] = i * PS_TILE < n ? i * PS_TILE : n;
-        bnd[8] = n;   // marks the bounds valid for this n
-    }
-}
-
 hipError_t launch_presort(const uint32_t* twords, const uint32_t* meta, uint32_t n, const QueueBufs& qb,
                           hipStream_t st, bool gather) {
     if (n == 0) return hipSuccess;
@@ -282,7 +237,7 @@ hipError_t launch_presort(const uint32_t* twords, const uint32_t* meta, uint32_t
     }
     // the lowest key bit sorted: the range-keyed orders (2, 4, 5) sort their
     // whole 8 / 16-bit key, the word-hash key (1) its top 8 x passes bits
-    const uint32_t low = qb.presort_mode >= 2 && qb.presort_mode != 7 ? 0u : 32u - 8u * passes;
+    const uint32_t low = qb.presort_mode >= 2 ? 0u : 32u - 8u * passes;
     for (uint32_t pass = 0; pass < passes; ++pass) {
         const uint32_t shift = low + 8 * pass;
         hipLaunchKernelGGL(tm_presort_count, dim3(tiles), dim3(PS_BLOCK), 0, st, ka, n, shift, qb.sort_counts);
@@ -300,11 +255,6 @@ hipError_t launch_presort(const uint32_t* twords, const uint32_t* meta, uint32_t
         t = va;
         va = vb;
         vb = t;
-    }
-    if (qb.presort_mode == 7 && tiles <= PS_BND_TILES) {   // the XCD ranges' bounds (the keys ended in A)
-        hipLaunchKernelGGL(tm_presort_cost_tiles, dim3(tiles), dim3(PS_BLOCK), 0, st, ka, n, qb.sort_counts);
-        hipLaunchKernelGGL(tm_presort_bounds, dim3(1), dim3(PS_BLOCK), 0, st, qb.sort_counts, tiles, n,
-                           reinterpret_cast<uint32_t*>(qb.ws + QWS_BND));
     }
     if (gather)   // rows into walk order (a walk with chunk rows reads them through perm instead)
         hipLaunchKernelGGL(tm_presort_gather, dim3((n + PS_BLOCK - 1) / PS_BLOCK), dim3(PS_BLOCK), 0, st, qb.perm,

@@ -265,9 +265,6 @@ VARIANTS = {"queue": {}, "queue_xcd": {}, "queue_xcd@nosplit@dfs": {"split": 0, 
             # the range-local word-hash order with the lightest topics of each range last (three radix passes)
             # the per-lane tokenizer (the wave-cooperative one is the default)
             "queue_xcd@toklane": {"tok_wave": 0}, "queue_xcd@toklane@order5": {"tok_wave": 0, "presort": 5},
-            # the word-hash order over the whole batch, XCD ranges cut at equal predicted work
-            "queue_xcd@order7": {"presort": 7}, "queue_xcd@order7@norows@stagek8": {"presort": 7, "chunk_rows": 0,
-                                                                                     "stage_k": 8},
             "queue_xcd@order6": {"presort": 6}, "queue_xcd@order6@bits16@tail300": {"presort": 6, "sort_bits": 16,
                                                                                     "light_tail": 300},
 }
