@@ -1,8 +1,12 @@
 """emqx_amd — MI355X-native topic-routing engine for EMQ X's publish path.
 
 The hot path (emqx_trie:match/1 with emqx_topic:words/1) runs as HIP kernels
-for gfx950 in libtopicmatch.so; this package is the host-side mirror of the
-reference's Erlang API (emqx_topic, emqx_trie, emqx_router) over its C-ABI.
+for gfx950 in libtopicmatch.so; this package is the host side over its C-ABI:
+`Engine` (emqx_trie's insert / delete / match / lookup, batched, and the
+route tables), the reference's Erlang modules mirrored where they add logic
+(emqx_topic, emqx_router, emqx_access, emqx_mod_rewrite), the micro-batcher,
+the multi-GPU modes and the delta feed.  The Erlang side is erlang/ over the
+NIF.
 """
 from . import _lib
 from .engine import Engine, pack
