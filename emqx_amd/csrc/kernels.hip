@@ -334,8 +334,9 @@ __device__ __forceinline__ uint32_t presort_key(const uint32_t (&tw)[WREG], uint
 // range (3 bits) over 31 - the summed heat of the first eight levels / 4
 // (5 bits), one radix pass (presort.hip).
 // the walk's XCD range of queue position t: [n r / 8, n (r+1) / 8)
+// (an f32 estimate, then exact: no 64-bit division)
 __device__ __forceinline__ uint32_t range_of(uint32_t t, uint32_t n) {
-    uint32_t r = (uint32_t)(((uint64_t)t * 8) / n);
+    uint32_t r = (uint32_t)__builtin_fminf(8.0f * (float)t * __builtin_amdgcn_rcpf((float)n), 7.0f);
     while (r > 0 && (uint64_t)n * r / 8 > t) --r;
     while (r < 7 && (uint64_t)n * (r + 1) / 8 <= t) ++r;
     return r;
@@ -435,13 +436,67 @@ constexpr uint32_t TOK_WAVE = 1u << 24;   // key_mode bit: the wave path (option
 #define TM_TOK_BATCH 3   // dictionary probes in flight per lane (4 held to 96 VGPRs, or at 97 and 4 waves:
                          // the same or slower, profiles/r06_h_ab, r06_i_ab)
 #endif
-// the bytes of window word q (window offset 8q) inside [b, e)
-__device__ __forceinline__ uint64_t range_bytes(uint32_t q, uint32_t b, uint32_t e) {
-    const uint32_t lo = 8 * q, hi = lo + 8;
-    uint64_t m = ~0ull;
-    if (b > lo) m &= ~0ull << (8 * (b - lo));
-    if (e < hi) m &= e > lo ? ~0ull >> (8 * (hi - e)) : 0ull;
-    return m;
+// bytes [o, o + k) of a wave's LDS window, k in 1..8, zero padded (32-bit
+// offsets: the window is at most 4 KiB)
+__device__ __forceinline__ uint64_t win_chunk(const uint64_t* w, uint32_t o, uint32_t k) {
+    const uint32_t q = o >> 3, sh = (o & 7u) * 8u;
+    uint64_t v = w[q] >> sh;
+    if (sh != 0 && (o & 7u) + k > 8) v |= w[q + 1] << (64 - sh);
+    return k < 8 ? v & (~0ull >> (64 - 8 * k)) : v;
+}
+// The wave path's dictionary probe: dict_begin / dict_end over the LDS
+// window, with the word's first 16 bytes kept from the hash pass for the
+// byte compare (dict_end re-assembles them from the bytes)
+struct WaveProbe {
+    uint32_t s, tag, len, off;   // home slot, tag, word length, window offset
+    uint64_t h0, h1;             // bytes 0-7, 8-15, zero padded
+    uint4 d0;                    // the home slot's first half
+};
+__device__ __forceinline__ WaveProbe wave_dict_begin(const ImageView& im, const uint64_t* w, uint32_t o,
+                                                     uint32_t len) {
+    WaveProbe q;
+    q.off = o;
+    q.len = len;
+    uint64_t h = 0x243F6A8885A308D3ULL;   // (dict_begin's hash, chunk by chunk)
+    q.h0 = len ? win_chunk(w, o, len < 8 ? len : 8u) : 0ull;
+    q.h1 = len > 8 ? win_chunk(w, o + 8, len < 16 ? len - 8 : 8u) : 0ull;
+    if (len) h = word_hash_step(h, q.h0);
+    if (len > 8) h = word_hash_step(h, q.h1);
+    for (uint32_t i = 16; i < len; i += 8) h = word_hash_step(h, win_chunk(w, o + i, len - i < 8 ? len - i : 8u));
+    h = word_hash_final(h, len);
+    q.tag = dict_tag(h, len);
+    q.s = (uint32_t)(h & im.dict_slot_mask);
+    q.d0 = reinterpret_cast<const uint4*>(im.dict + q.s)[0];
+    return q;
+}
+__device__ __forceinline__ uint32_t wave_dict_end(const ImageView& im, const uint64_t* w, const WaveProbe& q) {
+    const uint32_t len = q.len;
+    if (len == 1) {   // the atoms '+' / '#'
+        const uint32_t c = (uint32_t)q.h0;
+        if (c == '+') return WORD_PLUS;
+        if (c == '#') return WORD_HASH;
+    }
+    uint64_t s = q.s;
+    uint4 d0 = q.d0;
+    for (;;) {
+        const uint32_t word = d0.y;
+        if (word == WORD_NONE) return WORD_NONE;
+        if (d0.x == q.tag) {
+            bool eq = len == 0 || q.h0 == (((uint64_t)d0.w << 32) | d0.z);
+            if (eq && len > 8) {
+                const uint4 d1 = reinterpret_cast<const uint4*>(im.dict + s)[1];   // head1, exact len
+                eq = d1.z == len && q.h1 == (((uint64_t)d1.y << 32) | d1.x);
+                if (eq && len > 16) {
+                    const uint64_t* a = reinterpret_cast<const uint64_t*>(im.word_arena + im.word_off[word]);
+                    for (uint32_t i = 16; i < len && eq; i += 8)
+                        eq = win_chunk(w, q.off + i, len - i < 8 ? len - i : 8u) == a[i >> 3];
+                }
+            }
+            if (eq) return word;
+        }
+        s = (s + 1) & im.dict_slot_mask;
+        d0 = reinterpret_cast<const uint4*>(im.dict + s)[0];
+    }
 }
 
 __global__ void __launch_bounds__(BLOCK)
@@ -479,11 +534,17 @@ tm_tokenize(ImageView im, const uint8_t* __restrict__ bytes, const uint64_t* __r
     uint32_t c = 32u;
     // 1. levels of the lane's topic: count, wave prefix sum, descriptors
     uint32_t b = 0, e = 0, nl = 0;
+    uint64_t mlo = ~0ull, mhi = ~0ull;   // the topic's bytes in its first / last window word
+    auto tmask = [&](uint32_t q) -> uint64_t {   // the topic's bytes of window word q: two selects
+        return (q == b >> 3 ? mlo : ~0ull) & (q == (e - 1) >> 3 ? mhi : ~0ull);
+    };
     if (lds && t < n) {
         b = (uint32_t)(off[t] - wbase);
         e = (uint32_t)(off[t + 1] - wbase);
+        mlo = ~0ull << (8 * (b & 7u));
+        mhi = (e & 7u) ? ~0ull >> (64 - 8 * (e & 7u)) : ~0ull;
         for (uint32_t q = b >> 3; 8 * q < e; ++q)
-            nl += (uint32_t)__popcll(slash_bytes(win[wv][q]) & range_bytes(q, b, e));
+            nl += (uint32_t)__popcll(slash_bytes(win[wv][q]) & tmask(q));
         nl += 1;
     }
     uint32_t first = nl;   // inclusive, then exclusive prefix over the wave
@@ -498,7 +559,7 @@ tm_tokenize(ImageView im, const uint8_t* __restrict__ bytes, const uint64_t* __r
         if (t < n) {
             uint32_t k = first, s0 = b;
             for (uint32_t q = b >> 3; 8 * q < e; ++q) {
-                uint64_t z = slash_bytes(win[wv][q]) & range_bytes(q, b, e);
+                uint64_t z = slash_bytes(win[wv][q]) & tmask(q);
                 while (z) {
                     const uint32_t p = 8 * q + ((uint32_t)__builtin_ctzll(z) >> 3);
                     z &= z - 1;
@@ -512,19 +573,19 @@ tm_tokenize(ImageView im, const uint8_t* __restrict__ bytes, const uint64_t* __r
         // 2. lanes over levels: TM_TOK_BATCH dictionary loads in flight per lane
         const LdsBytes lb{win[wv], wbase};
         for (uint32_t i0 = 0; i0 < L; i0 += 64 * TM_TOK_BATCH) {
-            DictProbe q[TM_TOK_BATCH];
+            WaveProbe q[TM_TOK_BATCH];
 #pragma unroll
             for (uint32_t j = 0; j < TM_TOK_BATCH; ++j) {
                 const uint32_t i = i0 + 64 * j + lane;
                 if (i < L) {
                     const uint32_t d = lv[i];
-                    q[j] = dict_begin(im, lb, wbase, wbase + (d & 0xFFFFu), d >> 16);
+                    q[j] = wave_dict_begin(im, win[wv], d & 0xFFFFu, d >> 16);
                 }
             }
 #pragma unroll
             for (uint32_t j = 0; j < TM_TOK_BATCH; ++j) {
                 const uint32_t i = i0 + 64 * j + lane;
-                if (i < L) lv[i] = dict_end(im, lb, wbase, q[j]);   // (only this lane reads entry i)
+                if (i < L) lv[i] = wave_dict_end(im, win[wv], q[j]);   // (only this lane reads entry i)
             }
         }
         wave_sync_lds();
